@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""Headline benchmark: img/s of Byzantine-resilient ResNet-50 training with f=2
+Multi-Krum on 1..8 MI355X (BASELINE.json), plus the GAR overhead vs ``average``.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is
+launched by ``torch.distributed.run`` with one rank per GPU (RCCL). W untimed warmup
+steps, then EXACTLY K timed steps bracketed by barrier + synchronize, max over
+ranks; rank 0 prints one JSON line.
+
+Workload (fixed per GPU => weak scaling): each GPU hosts ``--workers-per-gpu``
+logical workers (default 8, so f = 2 Multi-Krum's n >= 2f + 3 = 7 holds on one GPU),
+each computing a full forward/backward of ResNet-50 (torchvision architecture,
+10 classes, random init) on its own synthetic CIFAR-10-shape micro-batch of
+``--batch`` images (default 250: the reference Garfield_CC ResNet-50 config,
+``PT/applications/Garfield_CC/run_exp.sh``), bf16 autocast. Every step: per-worker
+gradients -> bf16 rows -> RCCL all-gather into the [n, d] buffer (overlapped with
+the next worker's backward) -> HIP Multi-Krum (MFMA Gram, on-device selection) ->
+fused combine + SGD(momentum 0.9, wd 5e-4) on fp32 master weights.
+img/s = n_logical x batch / step time (whole job).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from garfield_amd.models import build_model, num_parameters  # noqa: E402
+from garfield_amd.parallel.comm import init_distributed, shutdown  # noqa: E402
+from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synthetic_batches  # noqa: E402
+
+BASELINE_VALUE = None  # BASELINE.json "published": {} -> no reference number to divide by
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--model", default="resnet50")
+    p.add_argument("--dataset", default="cifar10", choices=["cifar10", "imagenet"])
+    p.add_argument("--batch", type=int, default=250, help="micro-batch per logical worker")
+    p.add_argument("--workers-per-gpu", type=int, default=8)
+    p.add_argument("--gar", default="krum")
+    p.add_argument("--f", type=int, default=2)
+    p.add_argument("--exchange-dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--channels-last", action="store_true")
+    p.add_argument("--overhead", action="store_true",
+                   help="also time the same job with the 'average' GAR and report the Krum overhead")
+    p.add_argument("--cudnn-benchmark", action="store_true")
+    return p.parse_args()
+
+
+def timed_steps(eng, batches, steps, warmup, ctx):
+    for _ in range(warmup):
+        eng.step(batches)
+    if ctx.device.type == "cuda":
+        torch.cuda.synchronize()
+    ctx.barrier()
+    if ctx.device.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = eng.step(batches)
+    if ctx.device.type == "cuda":
+        torch.cuda.synchronize()
+    ctx.barrier()
+    if ctx.device.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if ctx.is_distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=ctx.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, float(loss)
+
+
+def main():
+    a = parse()
+    ctx = init_distributed()
+    if a.cudnn_benchmark:
+        torch.backends.cudnn.benchmark = True
+    world = ctx.world_size
+    if world != a.gpus and ctx.rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; reporting WORLD_SIZE", file=sys.stderr)
+    shape = (3, 32, 32) if a.dataset == "cifar10" else (3, 224, 224)
+    num_classes = 10 if a.dataset == "cifar10" else 1000
+    torch.manual_seed(1234)
+    model = build_model(a.model, num_classes=num_classes)
+    d = num_parameters(model)
+    xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
+    cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=0.2, momentum=0.9,
+                       weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last)
+    eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
+    batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
+                                seed=1000 + ctx.rank, channels_last=a.channels_last)
+    elapsed, loss = timed_steps(eng, batches, a.steps, a.warmup, ctx)
+    n = eng.n
+    imgs = n * a.batch * a.steps
+    value = imgs / elapsed
+    ms = 1000.0 * elapsed / a.steps
+    extra = {}
+    if a.overhead:
+        cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=0.2, momentum=0.9,
+                               weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last)
+        torch.manual_seed(1234)
+        eng_avg = RobustDataParallel(build_model(a.model, num_classes=num_classes), F.cross_entropy, ctx, cfg_avg)
+        e_avg, _ = timed_steps(eng_avg, batches, a.steps, a.warmup, ctx)
+        ms_avg = 1000.0 * e_avg / a.steps
+        extra = {"avg_ms_per_step": round(ms_avg, 3),
+                 "gar_overhead_pct_vs_average": round(100.0 * (ms - ms_avg) / ms_avg, 3)}
+    if ctx.rank == 0:
+        out = {
+            "metric": "img/sec ResNet-50 f=2 Multi-Krum",
+            "value": round(value, 2),
+            "unit": "img/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16",
+            "data": "synthetic (random CIFAR-10-shape images, random-init weights)",
+            "config": {
+                "model": f"{a.model} (torchvision architecture, {num_classes} classes, {d} params)",
+                "global_batch": n * a.batch,
+                "seq_len": None,
+                "image_shape": list(shape),
+                "parallelism": f"dp{world} (robust DP, {a.workers_per_gpu} logical workers/GPU, n={n})",
+                "gar": a.gar,
+                "f": a.f,
+                "batch_per_worker": a.batch,
+                "exchange_dtype": a.exchange_dtype,
+                "optimizer": "SGD lr=0.2 momentum=0.9 wd=5e-4 (fused into the GAR combine kernel)",
+            },
+            "final_loss": round(loss, 4),
+            **extra,
+        }
+        print(json.dumps(out), flush=True)
+    shutdown(ctx)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,380 @@
+// Python bindings of the Garfield-MI355X native layer (module garfield_amd._C).
+//
+// Reference counterpart: the per-rule pybind modules py_krum/py_bulyan/py_median/
+// py_brute (e.g. py_krum/rule.cpp:43-62) plus the dtype/device dispatcher
+// include/aggregator.hpp:76-135. Here one module exposes the building blocks
+// (Gram, selection, combine, coordinate-wise, fused SGD) on both devices; the
+// Python layer (garfield_amd/ops/gar.py) composes them into rules.
+#include <torch/extension.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "gar_common.hpp"
+#include "gar_cpu.hpp"
+#include "gar_gpu.hpp"
+#include "mailbox.hpp"
+#include "threadpool.hpp"
+
+namespace py = pybind11;
+using garfield::RowTable;
+
+namespace {
+
+int dtype_code(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return garfield::kF32;
+    case at::kBFloat16: return garfield::kBF16;
+    case at::kHalf: return garfield::kF16;
+    case at::kDouble: return garfield::kF64;
+    default: TORCH_CHECK(false, "garfield: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+// A validated set of n gradient rows of length d on one device.
+struct RowSet {
+  RowTable table{};
+  int n = 0;
+  int64_t d = 0;
+  int dt = 0;
+  at::Device device{at::kCPU};
+  at::ScalarType st = at::kFloat;
+};
+
+void check_row(const at::Tensor& t, const RowSet& rs, bool gpu) {
+  TORCH_CHECK(t.device() == rs.device, "garfield: all gradients must be on the same device");
+  TORCH_CHECK(t.scalar_type() == rs.st, "garfield: all gradients must have the same dtype");
+  if (gpu)
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+                "garfield: gradient rows must be 16-byte aligned on the GPU path");
+}
+
+RowSet rows_from_list(const std::vector<at::Tensor>& rows, bool gpu) {
+  TORCH_CHECK(!rows.empty(), "garfield: expected a non-empty list of gradients");
+  TORCH_CHECK(static_cast<int>(rows.size()) <= garfield::kMaxRows, "garfield: at most ", garfield::kMaxRows,
+              " gradients per call, got ", rows.size());
+  RowSet rs;
+  rs.n = static_cast<int>(rows.size());
+  rs.device = rows[0].device();
+  rs.st = rows[0].scalar_type();
+  rs.dt = dtype_code(rows[0]);
+  rs.d = rows[0].numel();
+  for (int i = 0; i < rs.n; ++i) {
+    const auto& t = rows[i];
+    TORCH_CHECK(t.is_contiguous(), "garfield: gradient ", i, " is not contiguous");
+    TORCH_CHECK(t.numel() == rs.d, "garfield: gradient ", i, " has ", t.numel(), " elements, expected ", rs.d);
+    check_row(t, rs, gpu);
+    rs.table.p[i] = t.data_ptr();
+  }
+  return rs;
+}
+
+RowSet rows_from_2d(const at::Tensor& G, bool gpu) {
+  TORCH_CHECK(G.dim() == 2, "garfield: expected a 2-D [n, d] gradient buffer");
+  TORCH_CHECK(G.size(0) >= 1 && G.size(0) <= garfield::kMaxRows, "garfield: 1 <= n <= ", garfield::kMaxRows);
+  TORCH_CHECK(G.stride(1) == 1, "garfield: gradient rows must be contiguous");
+  RowSet rs;
+  rs.n = static_cast<int>(G.size(0));
+  rs.d = G.size(1);
+  rs.device = G.device();
+  rs.st = G.scalar_type();
+  rs.dt = dtype_code(G);
+  const int64_t esz = G.element_size();
+  const char* base = static_cast<const char*>(G.data_ptr());
+  for (int i = 0; i < rs.n; ++i) rs.table.p[i] = base + static_cast<int64_t>(i) * G.stride(0) * esz;
+  if (gpu)
+    for (int i = 0; i < rs.n; ++i)
+      TORCH_CHECK(reinterpret_cast<uintptr_t>(rs.table.p[i]) % 16 == 0,
+                  "garfield: gradient rows must be 16-byte aligned on the GPU path (pad the row stride)");
+  return rs;
+}
+
+template <class T>
+garfield::cpu::Rows<T> cpu_rows(const RowSet& rs) {
+  TORCH_CHECK(rs.device.is_cpu(), "garfield: CPU path called with device tensors");
+  garfield::cpu::Rows<T> r;
+  r.n = static_cast<size_t>(rs.n);
+  r.d = static_cast<size_t>(rs.d);
+  for (int i = 0; i < rs.n; ++i) r.p.push_back(static_cast<const T*>(rs.table.p[i]));
+  return r;
+}
+
+void check_gpu(const RowSet& rs) {
+  TORCH_CHECK(rs.device.is_cuda(), "garfield: GPU path called with host tensors");
+  TORCH_CHECK(rs.dt != garfield::kF64, "garfield: fp64 is not supported by the MFMA kernels");
+}
+
+hipStream_t stream_of(const at::Device& dev) { return c10::hip::getCurrentHIPStream(dev.index()).stream(); }
+
+float* fptr(const at::Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous(), "garfield: expected a contiguous fp32 tensor");
+  return t.data_ptr<float>();
+}
+
+// ------------------------------------------------------------------ GPU ----
+
+void g_gram(const RowSet& rs, const at::Tensor& slabs, const at::Tensor& gram) {
+  check_gpu(rs);
+  c10::hip::HIPGuard guard(rs.device.index());
+  const int grid = garfield::gpu::gram_grid(rs.d, rs.dt, rs.n);
+  TORCH_CHECK(slabs.numel() >= grid * garfield::gpu::gram_slab_floats(rs.n), "garfield: gram slab workspace too small");
+  const int np = garfield::gpu::gram_padded(rs.n);
+  TORCH_CHECK(gram.numel() >= np * np, "garfield: gram output too small");
+  garfield::gpu::gram(rs.table, rs.n, rs.d, rs.dt, fptr(slabs), grid, fptr(gram), stream_of(rs.device));
+}
+
+void g_combine(const RowSet& rs, const at::Tensor& weights, const at::Tensor& out) {
+  check_gpu(rs);
+  c10::hip::HIPGuard guard(rs.device.index());
+  TORCH_CHECK(out.is_contiguous() && out.numel() == rs.d, "garfield: combine output shape mismatch");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "garfield: output must be 16-byte aligned");
+  garfield::gpu::combine(rs.table, rs.n, rs.d, rs.dt, fptr(weights), out.data_ptr(), dtype_code(out),
+                         stream_of(rs.device));
+}
+
+void g_combine_sgd(const RowSet& rs, const at::Tensor& weights, const at::Tensor& param, const at::Tensor& mom,
+                   const c10::optional<at::Tensor>& grad_out, double lr, double momentum, double dampening,
+                   double weight_decay, bool nesterov, bool first_step) {
+  check_gpu(rs);
+  c10::hip::HIPGuard guard(rs.device.index());
+  TORCH_CHECK(param.numel() == rs.d && mom.numel() == rs.d, "garfield: parameter/momentum size mismatch");
+  float* g = nullptr;
+  if (grad_out.has_value() && grad_out->defined()) {
+    TORCH_CHECK(grad_out->numel() == rs.d, "garfield: grad_out size mismatch");
+    g = fptr(*grad_out);
+  }
+  garfield::gpu::SgdArgs a{static_cast<float>(lr), static_cast<float>(momentum), static_cast<float>(dampening),
+                           static_cast<float>(weight_decay), nesterov ? 1 : 0, first_step ? 1 : 0};
+  garfield::gpu::combine_sgd(rs.table, rs.n, rs.d, rs.dt, fptr(weights), fptr(param), fptr(mom), g, a,
+                             stream_of(rs.device));
+}
+
+void g_coordwise(const RowSet& rs, int mode, int f, int beta, const c10::optional<at::Tensor>& W, int t,
+                 uint64_t seed, double p, const at::Tensor& out) {
+  check_gpu(rs);
+  c10::hip::HIPGuard guard(rs.device.index());
+  TORCH_CHECK(out.is_contiguous() && out.numel() == rs.d, "garfield: coordwise output shape mismatch");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "garfield: output must be 16-byte aligned");
+  const float* w = nullptr;
+  if (mode == garfield::kBulyanTail) {
+    TORCH_CHECK(W.has_value() && W->numel() >= t * rs.n, "garfield: Bulyan tail needs W[t, n]");
+    TORCH_CHECK(t >= 1 && t <= garfield::kMaxRows, "garfield: invalid t");
+    w = fptr(*W);
+  }
+  garfield::gpu::coordwise(rs.table, rs.n, rs.d, rs.dt, mode, f, beta, w, t, seed,
+                           garfield::bernoulli_threshold(p), out.data_ptr(), dtype_code(out), stream_of(rs.device));
+}
+
+void g_sqdist(const RowSet& rs, const at::Tensor& center, const at::Tensor& slabs) {
+  check_gpu(rs);
+  c10::hip::HIPGuard guard(rs.device.index());
+  TORCH_CHECK(center.numel() == rs.d, "garfield: centre size mismatch");
+  const int grid = garfield::gpu::sqdist_grid(rs.d);
+  TORCH_CHECK(slabs.numel() >= static_cast<int64_t>(grid) * rs.n, "garfield: sqdist workspace too small");
+  garfield::gpu::sqdist_partial(rs.table, rs.n, rs.d, rs.dt, fptr(center), fptr(slabs), grid, stream_of(rs.device));
+}
+
+// ------------------------------------------------------------------ CPU ----
+
+template <class F>
+auto cpu_dispatch(const RowSet& rs, F&& f) {
+  if (rs.dt == garfield::kF64) return f(cpu_rows<double>(rs), double{});
+  TORCH_CHECK(rs.dt == garfield::kF32, "garfield: CPU path supports fp32/fp64 (convert bf16/fp16 first)");
+  return f(cpu_rows<float>(rs), float{});
+}
+
+at::Tensor dist_tensor(const std::vector<double>& D, int64_t n) {
+  auto t = at::empty({n, n}, at::TensorOptions().dtype(at::kDouble));
+  std::copy(D.begin(), D.end(), t.data_ptr<double>());
+  return t;
+}
+
+at::Tensor weights_tensor(const std::vector<float>& w, std::vector<int64_t> shape) {
+  auto t = at::empty(shape, at::TensorOptions().dtype(at::kFloat));
+  std::copy(w.begin(), w.end(), t.data_ptr<float>());
+  return t;
+}
+
+std::vector<double> dist_from(const at::Tensor& D) {
+  auto c = D.to(at::kDouble).contiguous().cpu();
+  return std::vector<double>(c.data_ptr<double>(), c.data_ptr<double>() + c.numel());
+}
+
+std::vector<float> floats_from(const at::Tensor& W) {
+  auto c = W.to(at::kFloat).contiguous().cpu();
+  return std::vector<float>(c.data_ptr<float>(), c.data_ptr<float>() + c.numel());
+}
+
+at::Tensor c_pairwise(const RowSet& rs) {
+  return cpu_dispatch(rs, [&](auto r, auto) { return dist_tensor(garfield::cpu::pairwise_sqdist(r), rs.n); });
+}
+
+at::Tensor c_combine(const RowSet& rs, const at::Tensor& weights) {
+  auto w = floats_from(weights);
+  TORCH_CHECK(static_cast<int>(w.size()) == rs.n, "garfield: weights size mismatch");
+  auto out = at::empty({rs.d}, at::TensorOptions().dtype(rs.st));
+  cpu_dispatch(rs, [&](auto r, auto z) {
+    using T = decltype(z);
+    garfield::cpu::combine<T>(r, w, out.data_ptr<T>());
+    return 0;
+  });
+  return out;
+}
+
+at::Tensor c_coordwise(const RowSet& rs, int mode, int f, int beta, const c10::optional<at::Tensor>& W, int t,
+                       uint64_t seed, double p) {
+  std::vector<float> w;
+  if (mode == garfield::kBulyanTail) {
+    TORCH_CHECK(W.has_value(), "garfield: Bulyan tail needs W");
+    w = floats_from(*W);
+    TORCH_CHECK(static_cast<int64_t>(w.size()) >= static_cast<int64_t>(t) * rs.n, "garfield: W too small");
+  }
+  auto out = at::empty({rs.d}, at::TensorOptions().dtype(rs.st));
+  cpu_dispatch(rs, [&](auto r, auto z) {
+    using T = decltype(z);
+    garfield::cpu::coordwise<T>(r, mode, static_cast<size_t>(f), static_cast<size_t>(beta), w,
+                                static_cast<size_t>(t), seed, garfield::bernoulli_threshold(p), out.data_ptr<T>());
+    return 0;
+  });
+  return out;
+}
+
+at::Tensor c_sqdist(const RowSet& rs, const at::Tensor& center) {
+  auto c = center.to(rs.st).contiguous();
+  TORCH_CHECK(c.numel() == rs.d, "garfield: centre size mismatch");
+  return cpu_dispatch(rs, [&](auto r, auto z) {
+    using T = decltype(z);
+    auto v = garfield::cpu::sqdist_to<T>(r, c.data_ptr<T>());
+    auto t = at::empty({rs.n}, at::TensorOptions().dtype(at::kDouble));
+    std::copy(v.begin(), v.end(), t.data_ptr<double>());
+    return t;
+  });
+}
+
+// Register a function under `name` for both a 2-D buffer and a list of rows.
+template <class Fn2d, class FnList>
+void def_rows(py::module& m, const char* name, Fn2d&& f2d, FnList&& flist, const char* doc) {
+  m.def(name, std::forward<Fn2d>(f2d), doc);
+  m.def(name, std::forward<FnList>(flist), doc);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "Garfield-MI355X native robust-aggregation kernels (gfx950 HIP + C++ thread pool)";
+  m.attr("MAX_ROWS") = garfield::kMaxRows;
+  m.attr("MODE_MEDIAN") = static_cast<int>(garfield::kMedian);
+  m.attr("MODE_TRIMMED_MEAN") = static_cast<int>(garfield::kTrimmedMean);
+  m.attr("MODE_AVERAGED_MEDIAN") = static_cast<int>(garfield::kAveragedMedian);
+  m.attr("MODE_AVERAGE_NAN") = static_cast<int>(garfield::kAverageNan);
+  m.attr("MODE_CONDENSE") = static_cast<int>(garfield::kCondense);
+  m.attr("MODE_BULYAN_TAIL") = static_cast<int>(garfield::kBulyanTail);
+
+  // sizing helpers
+  m.def("gram_padded", &garfield::gpu::gram_padded);
+  m.def("gram_grid", [](int64_t d, const at::Tensor& like, int n) { return garfield::gpu::gram_grid(d, dtype_code(like), n); });
+  m.def("gram_slab_floats", &garfield::gpu::gram_slab_floats);
+  m.def("sqdist_grid", &garfield::gpu::sqdist_grid);
+
+  // GPU building blocks (asynchronous on the current stream)
+  def_rows(m, "gpu_gram",
+           [](const at::Tensor& G, const at::Tensor& s, const at::Tensor& g) { g_gram(rows_from_2d(G, true), s, g); },
+           [](const std::vector<at::Tensor>& L, const at::Tensor& s, const at::Tensor& g) { g_gram(rows_from_list(L, true), s, g); },
+           "Split-K MFMA Gram matrix G·Gᵀ (fp32 [np, np])");
+  m.def("gpu_krum_select", [](const at::Tensor& gram, int n, int f, int mm, const at::Tensor& w, const at::Tensor& order,
+                              const at::Tensor& scores) {
+    c10::hip::HIPGuard guard(gram.device().index());
+    TORCH_CHECK(order.scalar_type() == at::kInt, "order must be int32");
+    const int np = garfield::gpu::gram_padded(n);
+    garfield::gpu::krum_select(fptr(gram), np, n, f, mm, fptr(w), order.data_ptr<int>(), fptr(scores), stream_of(gram.device()));
+  });
+  m.def("gpu_bulyan_select", [](const at::Tensor& gram, int n, int f, int mm, int t, const at::Tensor& W) {
+    c10::hip::HIPGuard guard(gram.device().index());
+    TORCH_CHECK(W.numel() >= static_cast<int64_t>(t) * n, "W too small");
+    garfield::gpu::bulyan_select(fptr(gram), garfield::gpu::gram_padded(n), n, f, mm, t, fptr(W), stream_of(gram.device()));
+  });
+  m.def("gpu_brute_select", [](const at::Tensor& gram, int n, int f, const at::Tensor& best, const at::Tensor& w) {
+    c10::hip::HIPGuard guard(gram.device().index());
+    TORCH_CHECK(n <= 64, "brute: n must be <= 64");
+    TORCH_CHECK(best.scalar_type() == at::kLong && best.numel() >= 1, "best must be an int64 tensor");
+    garfield::gpu::brute_select(fptr(gram), garfield::gpu::gram_padded(n), n, f,
+                                reinterpret_cast<unsigned long long*>(best.data_ptr<int64_t>()), fptr(w), stream_of(gram.device()));
+  });
+  m.def("gpu_aksel_select", [](const at::Tensor& slabs, int n, int c, const at::Tensor& w, const at::Tensor& dists) {
+    c10::hip::HIPGuard guard(slabs.device().index());
+    const int grid = static_cast<int>(slabs.numel() / n);
+    garfield::gpu::aksel_select(fptr(slabs), grid, n, c, fptr(w), fptr(dists), stream_of(slabs.device()));
+  });
+  def_rows(m, "gpu_combine",
+           [](const at::Tensor& G, const at::Tensor& w, const at::Tensor& o) { g_combine(rows_from_2d(G, true), w, o); },
+           [](const std::vector<at::Tensor>& L, const at::Tensor& w, const at::Tensor& o) { g_combine(rows_from_list(L, true), w, o); },
+           "out = Σ_j w_j g_j");
+  def_rows(m, "gpu_combine_sgd",
+           [](const at::Tensor& G, const at::Tensor& w, const at::Tensor& p, const at::Tensor& b,
+              const c10::optional<at::Tensor>& go, double lr, double mo, double da, double wd, bool ne, bool first) {
+             g_combine_sgd(rows_from_2d(G, true), w, p, b, go, lr, mo, da, wd, ne, first);
+           },
+           [](const std::vector<at::Tensor>& L, const at::Tensor& w, const at::Tensor& p, const at::Tensor& b,
+              const c10::optional<at::Tensor>& go, double lr, double mo, double da, double wd, bool ne, bool first) {
+             g_combine_sgd(rows_from_list(L, true), w, p, b, go, lr, mo, da, wd, ne, first);
+           },
+           "Fused robust combine + SGD(momentum, dampening, weight decay, nesterov) on fp32 master weights");
+  def_rows(m, "gpu_coordwise",
+           [](const at::Tensor& G, int mode, int f, int beta, const c10::optional<at::Tensor>& W, int t, uint64_t seed,
+              double p, const at::Tensor& o) { g_coordwise(rows_from_2d(G, true), mode, f, beta, W, t, seed, p, o); },
+           [](const std::vector<at::Tensor>& L, int mode, int f, int beta, const c10::optional<at::Tensor>& W, int t,
+              uint64_t seed, double p, const at::Tensor& o) { g_coordwise(rows_from_list(L, true), mode, f, beta, W, t, seed, p, o); },
+           "Coordinate-wise rule (median / trimmed mean / averaged median / average-nan / condense / Bulyan tail)");
+  def_rows(m, "gpu_sqdist",
+           [](const at::Tensor& G, const at::Tensor& c, const at::Tensor& s) { g_sqdist(rows_from_2d(G, true), c, s); },
+           [](const std::vector<at::Tensor>& L, const at::Tensor& c, const at::Tensor& s) { g_sqdist(rows_from_list(L, true), c, s); },
+           "Partial squared distances of every row to a centre (split-K slabs [grid, n])");
+
+  // CPU building blocks (thread pool)
+  def_rows(m, "cpu_pairwise",
+           [](const at::Tensor& G) { return c_pairwise(rows_from_2d(G, false)); },
+           [](const std::vector<at::Tensor>& L) { return c_pairwise(rows_from_list(L, false)); },
+           "Pairwise squared distances (fp64 [n, n], +inf diagonal / non-finite)");
+  def_rows(m, "cpu_combine",
+           [](const at::Tensor& G, const at::Tensor& w) { return c_combine(rows_from_2d(G, false), w); },
+           [](const std::vector<at::Tensor>& L, const at::Tensor& w) { return c_combine(rows_from_list(L, false), w); },
+           "out = Σ_j w_j g_j");
+  def_rows(m, "cpu_coordwise",
+           [](const at::Tensor& G, int mode, int f, int beta, const c10::optional<at::Tensor>& W, int t, uint64_t seed, double p) {
+             return c_coordwise(rows_from_2d(G, false), mode, f, beta, W, t, seed, p);
+           },
+           [](const std::vector<at::Tensor>& L, int mode, int f, int beta, const c10::optional<at::Tensor>& W, int t,
+              uint64_t seed, double p) { return c_coordwise(rows_from_list(L, false), mode, f, beta, W, t, seed, p); },
+           "Coordinate-wise rule on the CPU");
+  def_rows(m, "cpu_sqdist",
+           [](const at::Tensor& G, const at::Tensor& c) { return c_sqdist(rows_from_2d(G, false), c); },
+           [](const std::vector<at::Tensor>& L, const at::Tensor& c) { return c_sqdist(rows_from_list(L, false), c); },
+           "Squared distance of every row to a centre (fp64 [n])");
+  m.def("cpu_krum_weights", [](const at::Tensor& D, int f, int mm) {
+    const int64_t n = D.size(0);
+    std::vector<double> scores;
+    auto w = garfield::cpu::krum_weights(dist_from(D), n, f, mm, &scores);
+    auto s = at::empty({n}, at::TensorOptions().dtype(at::kDouble));
+    std::copy(scores.begin(), scores.end(), s.data_ptr<double>());
+    return py::make_tuple(weights_tensor(w, {n}), s);
+  });
+  m.def("cpu_bulyan_weights", [](const at::Tensor& D, int f, int mm, int t) {
+    const int64_t n = D.size(0);
+    return weights_tensor(garfield::cpu::bulyan_weights(dist_from(D), n, f, mm, t), {t, n});
+  });
+  m.def("cpu_brute_weights", [](const at::Tensor& D, int f) {
+    const int64_t n = D.size(0);
+    return weights_tensor(garfield::cpu::brute_weights(dist_from(D), n, f), {n});
+  });
+  m.def("cpu_aksel_weights", [](const at::Tensor& dists, int c) {
+    const int64_t n = dists.numel();
+    return weights_tensor(garfield::cpu::aksel_weights(dist_from(dists), n, c), {n});
+  });
+  m.def("cpu_num_threads", [] { return garfield::cpu::pool().size(); });
+
+  garfield::mailbox::bind(m);
+}

@@ -1,0 +1,66 @@
+// Host-side launchers of the CDNA4 (gfx950) robust-aggregation kernels.
+//
+// Every launcher is asynchronous on the given stream, allocates nothing and
+// never synchronises, so a caller may capture it into a hipGraph
+// (contrast: the reference's cudaMalloc + cudaMemcpy + cudaStreamSynchronize
+// inside every call, pytorch_impl/libs/native/py_krum/krum.cu:77-154).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "gar_common.hpp"
+
+namespace garfield {
+namespace gpu {
+
+// ---- Gram matrix (pairwise distances as G·Gᵀ on MFMA) ----------------------
+int gram_nb(int n);                          // 16-row blocks: 1, 2, 4 or 8
+int gram_padded(int n);                      // 16 * gram_nb(n)
+int gram_grid(int64_t d, int dt, int n);     // split-K workgroups
+int64_t gram_slab_floats(int n);             // floats per split-K slab
+// slabs: [grid][slab_floats] workspace; gram: [np][np] fp32 output
+void gram(const RowTable& rows, int n, int64_t d, int dt, float* slabs, int grid,
+          float* gram, hipStream_t stream);
+
+// ---- Selection (one workgroup, on device, no host round-trip) --------------
+// weights[n] (fp32), order[n] (gradient ids by increasing score), scores[n]
+void krum_select(const float* gram, int np, int n, int f, int m, float* weights,
+                 int* order, float* scores, hipStream_t stream);
+// W[t][n]: row k = uniform weights of the (m-k) best-scoring gradients at step k
+void bulyan_select(const float* gram, int np, int n, int f, int m, int t, float* W,
+                   hipStream_t stream);
+// best: one uint64 (initialised here), weights[n]
+void brute_select(const float* gram, int np, int n, int f, unsigned long long* best,
+                  float* weights, hipStream_t stream);
+
+// ---- Weighted combine  out = Σ_j w_j g_j  (optionally fused SGD update) -----
+void combine(const RowTable& rows, int n, int64_t d, int dt, const float* weights,
+             void* out, int out_dt, hipStream_t stream);
+
+struct SgdArgs {
+  float lr;
+  float momentum;
+  float dampening;
+  float weight_decay;
+  int nesterov;
+  int first_step;  // momentum buffer initialised to the gradient (torch.optim.SGD)
+};
+void combine_sgd(const RowTable& rows, int n, int64_t d, int dt, const float* weights,
+                 float* param, float* momentum_buf, float* grad_out, SgdArgs args,
+                 hipStream_t stream);
+
+// ---- Coordinate-wise rules (median, trimmed mean, MeaMed, ...) -------------
+// W/t are only read for kBulyanTail; seed/threshold only for kCondense.
+void coordwise(const RowTable& rows, int n, int64_t d, int dt, int mode, int f, int beta,
+               const float* W, int t, uint64_t seed, uint64_t threshold, void* out,
+               int out_dt, hipStream_t stream);
+int coordwise_max_rows();
+
+// ---- Aksel: squared distances of every gradient to a centre vector ---------
+int sqdist_grid(int64_t d);
+void sqdist_partial(const RowTable& rows, int n, int64_t d, int dt, const float* center,
+                    float* slabs, int grid, hipStream_t stream);
+void aksel_select(const float* slabs, int grid, int n, int c, float* weights, float* dists,
+                  hipStream_t stream);
+
+}  // namespace gpu
+}  // namespace garfield

@@ -1,0 +1,275 @@
+"""Byzantine-resilient data-parallel training engine (collective form).
+
+The reference trains with a parameter server that pulls every worker's gradient
+over RPC, aggregates with a GAR and pushes the model back
+(``applications/Aggregathor/trainer.py:231-243``, ``garfieldpp/server.py``), or,
+in Garfield_CC, gathers every parameter tensor to rank 0 and broadcasts it back
+(``applications/Garfield_CC/trainer.py:55-207``).
+
+MI355X design:
+
+1. every rank hosts ``workers_per_rank`` *logical workers* (f = 2 Multi-Krum needs
+   n >= 7 gradients even on one GPU); each runs fwd/bwd on its own micro-batch
+   (bf16 autocast) with ``p.grad`` aliased into one flat fp32 buffer;
+2. the flat gradient is cast into this rank's row of slot j of the exchange
+   buffer ``X[k, world, ld]`` and slot j is all-gathered (RCCL, async) while the
+   next logical worker computes — only the last slot's transfer is exposed;
+3. every rank runs the SAME deterministic HIP GAR on ``X`` viewed as ``[n, d]``
+   (replicated-server semantics: no model broadcast needed);
+4. the fused combine + SGD(momentum, weight decay) kernel updates the flat fp32
+   master weights in one pass; replicas stay bit-identical.
+
+Byzantine workers are simulated per global slot (``byzantine={slot: attack}``).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from garfield_amd import _native
+from garfield_amd.ops import gar
+from garfield_amd.parallel.comm import DistContext, all_gather_rows
+from garfield_amd.runtime.attacks import NEEDS_ESTIMATES, apply_attack
+from garfield_amd.utils.flat import FlatParams
+
+WEIGHTED_RULES = {"average", "krum", "brute", "aksel"}
+COORD_RULES = {"median", "trimmed-mean", "averaged-median", "average-nan", "condense", "bulyan"}
+
+
+@dataclass
+class EngineConfig:
+    gar: str = "krum"
+    f: int = 2
+    m: int | None = None
+    gar_kwargs: dict = field(default_factory=dict)
+    workers_per_rank: int = 8
+    lr: float = 0.1
+    momentum: float = 0.9
+    dampening: float = 0.0
+    weight_decay: float = 5e-4
+    nesterov: bool = False
+    exchange_dtype: torch.dtype = torch.bfloat16
+    autocast_dtype: torch.dtype | None = torch.bfloat16
+    byzantine: dict = field(default_factory=dict)   # global slot -> attack name
+    channels_last: bool = False
+    seed: int = 1234
+
+
+class RobustDataParallel:
+    """Robust DP over one process per device (see module docstring)."""
+
+    def __init__(self, model: nn.Module, loss_fn, ctx: DistContext, cfg: EngineConfig):
+        self.ctx = ctx
+        self.cfg = cfg
+        self.device = ctx.device
+        self.model = model.to(self.device)
+        if cfg.channels_last and self.device.type == "cuda":
+            self.model = self.model.to(memory_format=torch.channels_last)
+        self.loss_fn = loss_fn
+        self.flat = FlatParams(self.model, device=self.device)
+        if ctx.is_distributed:
+            dist.broadcast(self.flat.data, src=0)
+        self.d, self.ld = self.flat.d, self.flat.ld
+        self.mom = torch.zeros(self.ld, dtype=torch.float32, device=self.device)
+        self.k = cfg.workers_per_rank
+        self.world = ctx.world_size
+        self.rank = ctx.rank
+        self.n = self.k * self.world
+        if self.n > gar.MAX_ROWS and self.device.type == "cuda":
+            raise ValueError(f"at most {gar.MAX_ROWS} logical workers per job on the GPU path, got {self.n}")
+        self.X = torch.zeros((self.k, self.world, self.ld), dtype=cfg.exchange_dtype, device=self.device)
+        self.G = self.X.view(self.n, self.ld)[:, : self.d]          # [n, d] GAR input (slot-major)
+        # local slot order: honest workers first so colluders see their estimates
+        self.local_slots = sorted(range(self.k), key=lambda j: (self.slot(j) in cfg.byzantine, j))
+        self.step_count = 0
+        self.last_weights = None
+        self._C = _native.require_for(self.device) if self.device.type == "cuda" else None
+        self._one = torch.ones(1, dtype=torch.float32, device=self.device)
+        self._gagg = torch.zeros(self.ld, dtype=torch.float32, device=self.device) \
+            if cfg.gar in COORD_RULES else None
+        self._gen = torch.Generator(device=self.device)
+        self._gen.manual_seed(cfg.seed + 7919 * self.rank)
+        self._check_gar()
+
+    # ------------------------------------------------------------------ #
+
+    def slot(self, j: int) -> int:
+        """Global slot id (row of the [n, d] GAR input) of local worker j."""
+        return j * self.world + self.rank
+
+    def _check_gar(self) -> None:
+        from garfield_amd import aggregators
+
+        rule = aggregators.get(self.cfg.gar)
+        kw = dict(self.cfg.gar_kwargs)
+        if self.cfg.m is not None:
+            kw["m"] = self.cfg.m
+        msg = rule.check(gradients=[torch.zeros(1)] * self.n, f=self.cfg.f, **kw)
+        if msg is not None:
+            raise ValueError(f"GAR {self.cfg.gar!r} with n={self.n}: {msg}")
+
+    # ------------------------------------------------------------------ #
+
+    def compute_local(self, batches) -> list:
+        """Forward/backward of every local logical worker; returns the loss tensors.
+
+        Starts the all-gather of each slot as soon as its row is ready."""
+        self.model.train()
+        works, losses = [], []
+        for j in self.local_slots:
+            x, y = batches[j]
+            self.flat.grad.zero_()
+            if self.cfg.autocast_dtype is not None and self.device.type == "cuda":
+                with torch.autocast("cuda", dtype=self.cfg.autocast_dtype):
+                    loss = self.loss_fn(self.model(x), y)
+            else:
+                loss = self.loss_fn(self.model(x), y)
+            loss.backward()
+            losses.append(loss.detach())
+            row = self.X[j, self.rank]
+            s = self.slot(j)
+            attack = self.cfg.byzantine.get(s)
+            if attack is None:
+                row[: self.d].copy_(self.flat.grad[: self.d])
+            else:
+                est = None
+                if attack in NEEDS_ESTIMATES:
+                    honest = [self.X[i, self.rank, : self.d] for i in self.local_slots
+                              if self.slot(i) not in self.cfg.byzantine and i != j]
+                    est = torch.stack([self.flat.grad[: self.d]] + [h.float() for h in honest])
+                row[: self.d].copy_(apply_attack(attack, self.flat.grad[: self.d], est, self._gen))
+            if self.world > 1:
+                works.append(all_gather_rows(self.X[j], self.rank, async_op=True))
+        for w in works:
+            w.wait()
+        return losses
+
+    def aggregate_and_update(self) -> None:
+        """Run the GAR on the gathered [n, d] gradients and apply the SGD update."""
+        cfg = self.cfg
+        first = self.step_count == 0
+        rule = cfg.gar
+        kw = dict(cfg.gar_kwargs)
+        if self.device.type == "cuda":
+            C = self._C
+            param, mom = self.flat.data[: self.d], self.mom[: self.d]
+            if rule in WEIGHTED_RULES:
+                w = self._weights(rule, kw)
+                self.last_weights = w
+                C.gpu_combine_sgd(self.G, w, param, mom, None, cfg.lr, cfg.momentum, cfg.dampening,
+                                  cfg.weight_decay, cfg.nesterov, first)
+            else:
+                g = self._gagg[: self.d]
+                self._coordinate(rule, kw, g)
+                C.gpu_combine_sgd(self._gagg.view(1, self.ld)[:, : self.d], self._one, param, mom, None, cfg.lr,
+                                  cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
+        else:
+            gkw = dict(kw)
+            if rule not in ("average", "median", "average-nan"):
+                gkw["f"] = cfg.f
+            if cfg.m is not None and rule in ("krum", "bulyan"):
+                gkw["m"] = cfg.m
+            if rule == "condense":
+                gkw.setdefault("seed", cfg.seed + self.step_count)
+            g = gar.aggregate(rule, self.G.float(), **gkw).float()
+            self._sgd_cpu(g, first)
+        self.step_count += 1
+
+    def _weights(self, rule: str, kw: dict) -> torch.Tensor:
+        f = self.cfg.f
+        if rule == "average":
+            w = getattr(self, "_avg_w", None)
+            if w is None:
+                w = torch.full((self.n,), 1.0 / self.n, dtype=torch.float32, device=self.device)
+                self._avg_w = w
+            return w
+        if rule == "krum":
+            return gar.krum_weights(self.G, f, self.cfg.m)
+        if rule == "brute":
+            return gar.brute_weights(self.G, f)
+        return gar.aksel_weights(self.G, f, kw.get("mode", "mid"))
+
+    def _coordinate(self, rule: str, kw: dict, out: torch.Tensor) -> None:
+        C, f = self._C, self.cfg.f
+        modes = gar._MODE
+        if rule == "bulyan":
+            t = self.n - 2 * f - 2
+            W = gar.bulyan_weights(self.G, f, self.cfg.m)
+            C.gpu_coordwise(self.G, modes["bulyan-tail"], f, t - 2 * f, W.reshape(-1), t, 0, 1.0, out)
+        elif rule == "median":
+            C.gpu_coordwise(self.G, modes["median"], 0, 0, None, 0, 0, 1.0, out)
+        elif rule == "trimmed-mean":
+            C.gpu_coordwise(self.G, modes["trimmed-mean"], f, 0, None, 0, 0, 1.0, out)
+        elif rule == "averaged-median":
+            beta = kw.get("beta") or self.n - f
+            C.gpu_coordwise(self.G, modes["averaged-median"], f, beta, None, 0, 0, 1.0, out)
+        elif rule == "average-nan":
+            C.gpu_coordwise(self.G, modes["average-nan"], 0, 0, None, 0, 0, 1.0, out)
+        elif rule == "condense":
+            C.gpu_coordwise(self.G, modes["condense"], f, 0, None, 0, self.cfg.seed + self.step_count,
+                            float(kw.get("p", 0.9)), out)
+        else:
+            raise ValueError(rule)
+
+    def _sgd_cpu(self, g: torch.Tensor, first: bool) -> None:
+        cfg = self.cfg
+        p, buf = self.flat.data[: self.d], self.mom[: self.d]
+        with torch.no_grad():
+            if cfg.weight_decay:
+                g = g + cfg.weight_decay * p
+            if cfg.momentum:
+                if first:
+                    buf.copy_(g)
+                else:
+                    buf.mul_(cfg.momentum).add_(g, alpha=1 - cfg.dampening)
+                g = g + cfg.momentum * buf if cfg.nesterov else buf
+            p.add_(g, alpha=-cfg.lr)
+
+    def step(self, batches) -> torch.Tensor:
+        """One synchronous robust training step; returns the mean local loss (device tensor)."""
+        losses = self.compute_local(batches)
+        self.aggregate_and_update()
+        return torch.stack(losses).float().mean()
+
+    # ------------------------------------------------------------------ #
+
+    def flat_model(self) -> torch.Tensor:
+        """Reference-layout flat parameter vector (a view; clone to keep)."""
+        return self.flat.vector()
+
+    def replica_checksum(self) -> float:
+        return float(self.flat.vector().double().sum())
+
+    @torch.no_grad()
+    def evaluate(self, batches, binary: bool = False) -> float:
+        self.model.eval()
+        correct = total = 0
+        for x, y in batches:
+            out = self.model(x.to(self.device))
+            pred = out.round() if binary else out.argmax(1)
+            correct += int((pred.view_as(y) == y.to(self.device)).sum())
+            total += y.numel()
+        self.model.train()
+        return 100.0 * correct / max(total, 1)
+
+
+def synthetic_batches(k: int, batch: int, shape, num_classes: int, device, seed: int = 0, channels_last=False):
+    """k fixed synthetic (input, label) micro-batches resident on ``device``."""
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    out = []
+    for _ in range(k):
+        x = torch.randn((batch, *shape), generator=g).to(device)
+        if channels_last and x.dim() == 4:
+            x = x.contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, num_classes, (batch,), generator=g).to(device)
+        out.append((x, y))
+    return out
+
+
+def gar_overhead(step_ms: float, avg_step_ms: float) -> float:
+    return 100.0 * (step_ms - avg_step_ms) / avg_step_ms if avg_step_ms > 0 else math.nan

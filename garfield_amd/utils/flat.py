@@ -1,0 +1,109 @@
+"""Flat-parameter layout: the reference's interchange and checkpoint format.
+
+The reference moves models and gradients as the concatenation of
+``p.view(-1)`` over ``model.parameters()`` in registration order
+(``garfieldpp/server.py:196-200,289-297``, ``worker.py:93-94``; buffers such as
+BatchNorm statistics excluded), and ``tools/pytorch.py:27-92`` provides
+``flatten`` / ``relink`` / ``grads_of``.
+
+``FlatParams`` goes one step further for the MI355X engine: every parameter's
+``.data`` (and optionally ``.grad``) is re-pointed to a view of ONE contiguous fp32
+buffer, so the fused GAR + SGD kernel updates the whole model in a single pass
+and the flat vector needs no gather/scatter. The buffer length is padded to a
+multiple of 64 elements (16-byte aligned rows for every dtype).
+"""
+from __future__ import annotations
+
+from typing import Iterable
+
+import torch
+import torch.nn as nn
+
+PAD = 64
+
+
+def padded(d: int, pad: int = PAD) -> int:
+    return ((d + pad - 1) // pad) * pad
+
+
+def flatten(tensors: Iterable[torch.Tensor]) -> torch.Tensor:
+    """Concatenate the (flattened) tensors into one new 1-D tensor."""
+    return torch.cat([t.reshape(-1) for t in tensors])
+
+
+def relink(tensors: Iterable[torch.Tensor], common: torch.Tensor) -> torch.Tensor:
+    """Make every tensor's storage a view of ``common`` (reference tools/pytorch.py:46-70)."""
+    pos = 0
+    for t in tensors:
+        n = t.numel()
+        t.data = common[pos:pos + n].view_as(t)
+        pos += n
+    return common
+
+
+def grads_of(tensors: Iterable[torch.Tensor]):
+    """Yield each tensor's gradient (zeros if it has none)."""
+    for t in tensors:
+        g = t.grad
+        yield torch.zeros_like(t) if g is None else g
+
+
+def flat_parameters(model: nn.Module) -> torch.Tensor:
+    """Reference-layout flat copy of the model parameters (``Server.get_model``)."""
+    return flatten(p.detach() for p in model.parameters())
+
+
+def flat_gradients(model: nn.Module) -> torch.Tensor:
+    """Reference-layout flat copy of the model gradients (``Worker.compute_gradients``)."""
+    return flatten(grads_of(model.parameters()))
+
+
+def write_flat_parameters(model: nn.Module, flat: torch.Tensor) -> None:
+    """Copy a reference-layout flat vector into the parameters (``Server.write_model``)."""
+    pos = 0
+    with torch.no_grad():
+        for p in model.parameters():
+            n = p.numel()
+            p.copy_(flat[pos:pos + n].view_as(p))
+            pos += n
+
+
+class FlatParams:
+    """All parameters of ``model`` as views of one padded fp32 buffer (+ grad buffer)."""
+
+    def __init__(self, model: nn.Module, device=None, dtype=torch.float32, with_grad: bool = True):
+        self.model = model
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.shapes = [p.shape for p in self.params]
+        self.numels = [p.numel() for p in self.params]
+        self.d = sum(self.numels)
+        self.ld = padded(self.d)
+        device = device or self.params[0].device
+        self.data = torch.zeros(self.ld, dtype=dtype, device=device)
+        pos = 0
+        with torch.no_grad():
+            for p, n in zip(self.params, self.numels):
+                self.data[pos:pos + n].copy_(p.detach().reshape(-1))
+                pos += n
+        relink(self.params, self.data)
+        self.grad = None
+        if with_grad:
+            self.grad = torch.zeros(self.ld, dtype=dtype, device=device)
+            self.attach_grads(self.grad)
+
+    def views(self, flat: torch.Tensor):
+        pos = 0
+        for shape, n in zip(self.shapes, self.numels):
+            yield flat[pos:pos + n].view(shape)
+            pos += n
+
+    def attach_grads(self, flat: torch.Tensor) -> None:
+        """Point every ``p.grad`` at its slice of ``flat`` (backward accumulates in place)."""
+        for p, v in zip(self.params, self.views(flat)):
+            p.grad = v
+
+    def vector(self) -> torch.Tensor:
+        return self.data[: self.d]
+
+    def grad_vector(self) -> torch.Tensor:
+        return self.grad[: self.d]

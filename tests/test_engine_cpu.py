@@ -1,0 +1,61 @@
+"""Robust DP engine on CPU: single process and 2-rank gloo (multi-process) runs."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+from garfield_amd.models import build_model
+from garfield_amd.parallel.comm import DistContext
+from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synthetic_batches
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("rule,f", [("krum", 2), ("median", 1), ("bulyan", 1), ("trimmed-mean", 2),
+                                    ("average", 1), ("brute", 2), ("aksel", 2)])
+def test_single_process_rules(rule, f):
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model("mlp"), F.nll_loss, DistContext(),
+                             EngineConfig(gar=rule, f=f, workers_per_rank=8,
+                                          byzantine={} if rule == "average" else {1: "reverse"}))
+    b = synthetic_batches(8, 16, (1, 28, 28), 10, "cpu")
+    l0 = float(eng.step(b))
+    for _ in range(5):
+        l1 = float(eng.step(b))
+    assert torch.isfinite(eng.flat_model()).all()
+    assert l1 < l0 + 1e-3
+
+
+def _worker(rank, world, port, outdir, rule):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from garfield_amd.parallel.comm import init_distributed, shutdown
+
+    ctx = init_distributed(backend="gloo", device="cpu")
+    torch.manual_seed(rank)  # different init per rank: the engine must broadcast rank 0's
+    eng = RobustDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                             EngineConfig(gar=rule, f=1, workers_per_rank=4, byzantine={3: "reverse"}))
+    b = synthetic_batches(4, 8, (1, 28, 28), 10, "cpu", seed=rank)
+    for _ in range(3):
+        eng.step(b)
+    torch.save({"flat": eng.flat_model().clone(), "w": eng.last_weights}, os.path.join(outdir, f"r{rank}.pt"))
+    shutdown(ctx)
+
+
+@pytest.mark.parametrize("rule", ["krum", "median"])
+def test_two_rank_gloo_replicas_identical(rule):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, free_port(), d, rule), nprocs=2, join=True)
+        r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
+        assert torch.equal(r0["flat"], r1["flat"])
