@@ -257,17 +257,27 @@ class RobustDataParallel:
         return 100.0 * correct / max(total, 1)
 
 
-def synthetic_batches(k: int, batch: int, shape, num_classes: int, device, seed: int = 0, channels_last=False):
-    """k fixed synthetic (input, label) micro-batches resident on ``device``."""
+def synthetic_batches(k: int, batch: int, shape, num_classes: int, device, seed: int = 0, channels_last=False,
+                      learnable: bool = True):
+    """k fixed synthetic (input, label) micro-batches resident on ``device``.
+
+    With ``learnable`` the labels are a fixed function of the input (argmax of a
+    fixed random projection, shared by all workers), so training makes progress."""
     g = torch.Generator(device="cpu")
     g.manual_seed(seed)
+    proj = torch.randn(int(torch.tensor(shape).prod()), num_classes,
+                       generator=torch.Generator().manual_seed(424242))
     out = []
     for _ in range(k):
-        x = torch.randn((batch, *shape), generator=g).to(device)
+        x = torch.randn((batch, *shape), generator=g)
+        if learnable:
+            y = (x.flatten(1) @ proj).argmax(1)
+        else:
+            y = torch.randint(0, num_classes, (batch,), generator=g)
+        x = x.to(device)
         if channels_last and x.dim() == 4:
             x = x.contiguous(memory_format=torch.channels_last)
-        y = torch.randint(0, num_classes, (batch,), generator=g).to(device)
-        out.append((x, y))
+        out.append((x, y.to(device)))
     return out
 
 

@@ -145,7 +145,7 @@ def test_list_input_and_unaligned_views(cuda):
 @pytest.mark.parametrize("nesterov", [False, True])
 def test_fused_combine_sgd_matches_torch_sgd(cuda, native, nesterov):
     n, d = 8, 10007
-    X = torch.randn(n, d, device=cuda)
+    X = torch.randn(n, 10016, device=cuda)[:, :d]   # padded row stride (16-byte aligned rows)
     w = torch.zeros(n, device=cuda)
     w[[1, 3, 4]] = 1 / 3
     p0 = torch.randn(d, device=cuda)
