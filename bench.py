@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--overhead", action="store_true",
                    help="also time the same job with the 'average' GAR and report the Krum overhead")
     p.add_argument("--cudnn-benchmark", action="store_true")
+    p.add_argument("--lr", type=float, default=0.2)
     return p.parse_args()
 
 
@@ -96,7 +97,7 @@ def main():
     model = build_model(a.model, num_classes=num_classes)
     d = num_parameters(model)
     xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
-    cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=0.2, momentum=0.9,
+    cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                        weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last)
     eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
     batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
@@ -108,7 +109,7 @@ def main():
     ms = 1000.0 * elapsed / a.steps
     extra = {}
     if a.overhead:
-        cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=0.2, momentum=0.9,
+        cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                                weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last)
         torch.manual_seed(1234)
         eng_avg = RobustDataParallel(build_model(a.model, num_classes=num_classes), F.cross_entropy, ctx, cfg_avg)
@@ -140,7 +141,7 @@ def main():
                 "f": a.f,
                 "batch_per_worker": a.batch,
                 "exchange_dtype": a.exchange_dtype,
-                "optimizer": "SGD lr=0.2 momentum=0.9 wd=5e-4 (fused into the GAR combine kernel)",
+                "optimizer": f"SGD lr={a.lr} momentum=0.9 wd=5e-4 (fused into the GAR combine kernel)",
             },
             "final_loss": round(loss, 4),
             **extra,

@@ -334,6 +334,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            [](const std::vector<at::Tensor>& L, const at::Tensor& c, const at::Tensor& s) { g_sqdist(rows_from_list(L, true), c, s); },
            "Partial squared distances of every row to a centre (split-K slabs [grid, n])");
 
+  m.def("gpu_flatten_cast", [](const std::vector<at::Tensor>& srcs, const at::Tensor& dst) {
+    TORCH_CHECK(!srcs.empty(), "flatten_cast: empty tensor list");
+    TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "flatten_cast: dst must be a contiguous device tensor");
+    c10::hip::HIPGuard guard(dst.device().index());
+    std::vector<const float*> ptrs;
+    std::vector<int64_t> numels, offs;
+    int64_t pos = 0;
+    for (const auto& t : srcs) {
+      TORCH_CHECK(t.scalar_type() == at::kFloat && t.device() == dst.device(), "flatten_cast: fp32 sources on dst's device");
+      TORCH_CHECK(t.is_non_overlapping_and_dense(), "flatten_cast: sources must be dense");
+      ptrs.push_back(t.data_ptr<float>());
+      numels.push_back(t.numel());
+      offs.push_back(pos);
+      pos += t.numel();
+    }
+    TORCH_CHECK(pos <= dst.numel(), "flatten_cast: destination too small (", dst.numel(), " < ", pos, ")");
+    return garfield::gpu::flatten_cast(ptrs.data(), numels.data(), offs.data(), static_cast<int>(ptrs.size()),
+                                       dst.data_ptr(), dtype_code(dst), stream_of(dst.device()));
+  }, "Copy a list of dense fp32 tensors (memory order) back to back into dst, casting to dst's dtype");
+
   // CPU building blocks (thread pool)
   def_rows(m, "cpu_pairwise",
            [](const at::Tensor& G) { return c_pairwise(rows_from_2d(G, false)); },

@@ -28,7 +28,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 HIPCC = str(ROCM / "bin" / "hipcc")
 
 HIP_SOURCES = [
-    "gar_gram.hip", "gar_combine.hip", "gar_coord.hip",
+    "gar_gram.hip", "gar_combine.hip", "gar_coord.hip", "gar_flatten.hip",
     "gar_coord_m0.hip", "gar_coord_m1.hip", "gar_coord_m2.hip",
     "gar_coord_m3.hip", "gar_coord_m4.hip", "gar_coord_m5.hip",
 ]

@@ -1,0 +1,87 @@
+// Multi-tensor flatten + cast: scatter-free copy of a model's per-parameter
+// gradients (fp32, each its own allocation) into one row of the gradient
+// exchange buffer (bf16 / fp16 / fp32), in ONE launch.
+//
+// Reference counterpart: `torch.cat([p.grad.view(-1) ...]).to("cpu")` in
+// garfieldpp/worker.py:93-94 (one concat kernel + a D2H copy per worker per step).
+// Here the row stays on the device, the cast is fused, and no intermediate fp32
+// flat vector is materialised.
+#include "gar_device.hpp"
+
+namespace garfield {
+namespace gpu {
+using namespace dev;
+namespace {
+
+constexpr int kChunk = 4096;  // elements per workgroup (256 threads x 16)
+
+struct FlatTable {
+  const float* src[kMaxFlatTensors];
+  int64_t numel[kMaxFlatTensors];
+  int64_t dst_off[kMaxFlatTensors];
+  int32_t chunk_start[kMaxFlatTensors + 1];  // prefix sum of chunks per tensor
+  int count;
+};
+
+template <int ODT>
+__device__ __forceinline__ void store8(void* dst, int64_t x, const float (&v)[8]) {
+  store_vec<8>(dst, ODT, x, v);
+}
+
+template <int ODT>
+__global__ __launch_bounds__(256) void k_flatten_cast(FlatTable t, void* __restrict__ dst) {
+  const int b = blockIdx.x;
+  // which tensor does this chunk belong to (uniform linear scan over <= 96 entries)
+  int ti = 0;
+  while (ti + 1 < t.count && t.chunk_start[ti + 1] <= b) ++ti;
+  const int64_t c0 = static_cast<int64_t>(b - t.chunk_start[ti]) * kChunk;
+  const int64_t numel = t.numel[ti];
+  const int64_t off = t.dst_off[ti];
+  const float* __restrict__ src = t.src[ti];
+  int64_t c1 = c0 + kChunk;
+  if (c1 > numel) c1 = numel;
+  const bool vec = ((off & 7) == 0) && ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+  if (vec) {
+    const int64_t v_end = c0 + ((c1 - c0) / 8) * 8;
+    for (int64_t x = c0 + threadIdx.x * 8; x < v_end; x += 256 * 8) {
+      const float4 a = *reinterpret_cast<const float4*>(src + x);
+      const float4 c = *reinterpret_cast<const float4*>(src + x + 4);
+      const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      store8<ODT>(dst, off + x, v);
+    }
+    for (int64_t x = v_end + threadIdx.x; x < c1; x += 256) store_one(dst, ODT, off + x, src[x]);
+  } else {
+    for (int64_t x = c0 + threadIdx.x; x < c1; x += 256) store_one(dst, ODT, off + x, src[x]);
+  }
+}
+
+}  // namespace
+
+int flatten_cast(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int count, void* dst,
+                 int out_dt, hipStream_t stream) {
+  int launched = 0;
+  for (int base = 0; base < count; base += kMaxFlatTensors) {
+    FlatTable t{};
+    int c = count - base;
+    if (c > kMaxFlatTensors) c = kMaxFlatTensors;
+    t.count = c;
+    int32_t chunks = 0;
+    for (int i = 0; i < c; ++i) {
+      t.src[i] = srcs[base + i];
+      t.numel[i] = numels[base + i];
+      t.dst_off[i] = offsets[base + i];
+      t.chunk_start[i] = chunks;
+      chunks += static_cast<int32_t>((numels[base + i] + kChunk - 1) / kChunk);
+    }
+    t.chunk_start[c] = chunks;
+    if (chunks == 0) continue;
+    if (out_dt == kBF16) hipLaunchKernelGGL(k_flatten_cast<kBF16>, dim3(chunks), dim3(256), 0, stream, t, dst);
+    else if (out_dt == kF16) hipLaunchKernelGGL(k_flatten_cast<kF16>, dim3(chunks), dim3(256), 0, stream, t, dst);
+    else hipLaunchKernelGGL(k_flatten_cast<kF32>, dim3(chunks), dim3(256), 0, stream, t, dst);
+    ++launched;
+  }
+  return launched;
+}
+
+}  // namespace gpu
+}  // namespace garfield

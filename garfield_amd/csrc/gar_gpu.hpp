@@ -62,5 +62,10 @@ void sqdist_partial(const RowTable& rows, int n, int64_t d, int dt, const float*
 void aksel_select(const float* slabs, int grid, int n, int c, float* weights, float* dists,
                   hipStream_t stream);
 
+// ---- Multi-tensor flatten + cast (per-parameter grads -> exchange row) -----
+constexpr int kMaxFlatTensors = 96;  // tensors per launch (kernarg budget); more => several launches
+int flatten_cast(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int count, void* dst,
+                 int out_dt, hipStream_t stream);
+
 }  // namespace gpu
 }  // namespace garfield

@@ -23,6 +23,7 @@ Byzantine workers are simulated per global slot (``byzantine={slot: attack}``).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from dataclasses import dataclass, field
 
@@ -70,7 +71,7 @@ class RobustDataParallel:
         if cfg.channels_last and self.device.type == "cuda":
             self.model = self.model.to(memory_format=torch.channels_last)
         self.loss_fn = loss_fn
-        self.flat = FlatParams(self.model, device=self.device)
+        self.flat = FlatParams(self.model, device=self.device, with_grad=False)
         if ctx.is_distributed:
             dist.broadcast(self.flat.data, src=0)
         self.d, self.ld = self.flat.d, self.flat.ld
@@ -117,36 +118,54 @@ class RobustDataParallel:
     def compute_local(self, batches) -> list:
         """Forward/backward of every local logical worker; returns the loss tensors.
 
-        Starts the all-gather of each slot as soon as its row is ready."""
+        Autograd's per-parameter gradients are "stolen" (``p.grad = None`` before each
+        backward, so no accumulate kernel runs) and one multi-tensor HIP kernel
+        flattens + casts them into this worker's exchange row. One autocast region
+        spans all local workers so the bf16 weight casts are cached across them.
+        The all-gather of each slot starts as soon as its row is ready."""
         self.model.train()
         works, losses = [], []
-        for j in self.local_slots:
-            x, y = batches[j]
-            self.flat.grad.zero_()
-            if self.cfg.autocast_dtype is not None and self.device.type == "cuda":
-                with torch.autocast("cuda", dtype=self.cfg.autocast_dtype):
-                    loss = self.loss_fn(self.model(x), y)
-            else:
+        cuda = self.device.type == "cuda"
+        amp = (torch.autocast("cuda", dtype=self.cfg.autocast_dtype)
+               if (self.cfg.autocast_dtype is not None and cuda) else contextlib.nullcontext())
+        params = self.flat.params
+        with amp:
+            for j in self.local_slots:
+                x, y = batches[j]
+                for p in params:
+                    p.grad = None
                 loss = self.loss_fn(self.model(x), y)
-            loss.backward()
-            losses.append(loss.detach())
-            row = self.X[j, self.rank]
-            s = self.slot(j)
-            attack = self.cfg.byzantine.get(s)
-            if attack is None:
-                row[: self.d].copy_(self.flat.grad[: self.d])
-            else:
-                est = None
-                if attack in NEEDS_ESTIMATES:
-                    honest = [self.X[i, self.rank, : self.d] for i in self.local_slots
-                              if self.slot(i) not in self.cfg.byzantine and i != j]
-                    est = torch.stack([self.flat.grad[: self.d]] + [h.float() for h in honest])
-                row[: self.d].copy_(apply_attack(attack, self.flat.grad[: self.d], est, self._gen))
-            if self.world > 1:
-                works.append(all_gather_rows(self.X[j], self.rank, async_op=True))
+                loss.backward()
+                losses.append(loss.detach())
+                row = self.X[j, self.rank, : self.d]
+                attack = self.cfg.byzantine.get(self.slot(j))
+                if attack is None:
+                    self._write_row(row)
+                else:
+                    g = self.flat.grads_flat(torch.empty(self.d, dtype=torch.float32, device=self.device))
+                    est = None
+                    if attack in NEEDS_ESTIMATES:
+                        honest = [self.X[i, self.rank, : self.d] for i in self.local_slots
+                                  if self.slot(i) not in self.cfg.byzantine and i != j]
+                        est = torch.stack([g] + [h.float() for h in honest])
+                    row.copy_(apply_attack(attack, g, est, self._gen))
+                if self.world > 1:
+                    works.append(all_gather_rows(self.X[j], self.rank, async_op=True))
+        for p in params:
+            p.grad = None
         for w in works:
             w.wait()
         return losses
+
+    def _write_row(self, row: torch.Tensor) -> None:
+        if self.device.type == "cuda":
+            grads = []
+            for p in self.flat.params:
+                g = p.grad
+                grads.append(g if g is not None else torch.zeros_like(p))
+            self._C.gpu_flatten_cast(grads, row)
+        else:
+            self.flat.grads_flat(row)
 
     def aggregate_and_update(self) -> None:
         """Run the GAR on the gathered [n, d] gradients and apply the SGD update."""

@@ -68,34 +68,64 @@ def write_flat_parameters(model: nn.Module, flat: torch.Tensor) -> None:
             pos += n
 
 
+def is_dense(t: torch.Tensor) -> bool:
+    """True when t's elements tile its storage span exactly (any dimension order)."""
+    expected = 1
+    for i in sorted(range(t.dim()), key=lambda i: t.stride(i)):
+        if t.size(i) == 1:
+            continue
+        if t.stride(i) != expected:
+            return False
+        expected *= t.size(i)
+    return True
+
+
+def memory_order_flat(t: torch.Tensor) -> torch.Tensor:
+    """1-D view/copy of a dense tensor in MEMORY order (== logical order when contiguous)."""
+    if t.is_contiguous():
+        return t.reshape(-1)
+    perm = sorted(range(t.dim()), key=lambda i: -t.stride(i))
+    return t.permute(perm).reshape(-1)
+
+
 class FlatParams:
-    """All parameters of ``model`` as views of one padded fp32 buffer (+ grad buffer)."""
+    """All parameters of ``model`` as views of one padded fp32 buffer (+ optional grad buffer).
+
+    Views keep each parameter's strides (``as_strided`` over the flat storage), so
+    a ``channels_last`` model stays ``channels_last``; the flat buffer is then in
+    memory order. ``reference_vector()`` always returns the reference layout
+    (logical ``p.view(-1)`` order) for checkpoints and the RPC API."""
 
     def __init__(self, model: nn.Module, device=None, dtype=torch.float32, with_grad: bool = True):
         self.model = model
         self.params = [p for p in model.parameters() if p.requires_grad]
-        self.shapes = [p.shape for p in self.params]
         self.numels = [p.numel() for p in self.params]
         self.d = sum(self.numels)
         self.ld = padded(self.d)
         device = device or self.params[0].device
         self.data = torch.zeros(self.ld, dtype=dtype, device=device)
+        self.offsets = []
         pos = 0
+        for p, n in zip(self.params, self.numels):
+            if not is_dense(p):
+                raise ValueError("FlatParams needs dense parameters")
+            self.offsets.append(pos)
+            pos += n
+        self.sizes = [tuple(p.size()) for p in self.params]
+        self.strides = [tuple(p.stride()) for p in self.params]
         with torch.no_grad():
-            for p, n in zip(self.params, self.numels):
-                self.data[pos:pos + n].copy_(p.detach().reshape(-1))
-                pos += n
-        relink(self.params, self.data)
+            for p, v in zip(self.params, self.views(self.data)):
+                v.copy_(p.detach())
+        for p, v in zip(self.params, self.views(self.data)):
+            p.data = v
         self.grad = None
         if with_grad:
             self.grad = torch.zeros(self.ld, dtype=dtype, device=device)
             self.attach_grads(self.grad)
 
     def views(self, flat: torch.Tensor):
-        pos = 0
-        for shape, n in zip(self.shapes, self.numels):
-            yield flat[pos:pos + n].view(shape)
-            pos += n
+        for size, stride, off in zip(self.sizes, self.strides, self.offsets):
+            yield torch.as_strided(flat, size, stride, off)
 
     def attach_grads(self, flat: torch.Tensor) -> None:
         """Point every ``p.grad`` at its slice of ``flat`` (backward accumulates in place)."""
@@ -107,3 +137,26 @@ class FlatParams:
 
     def grad_vector(self) -> torch.Tensor:
         return self.grad[: self.d]
+
+    def reference_vector(self) -> torch.Tensor:
+        """Reference interchange layout: cat of p.view(-1) (logical order)."""
+        return flatten(p.detach() for p in self.params)
+
+    def load_reference_vector(self, flat: torch.Tensor) -> None:
+        with torch.no_grad():
+            pos = 0
+            for p, n in zip(self.params, self.numels):
+                p.copy_(flat[pos:pos + n].view(p.shape))
+                pos += n
+
+    def grads_flat(self, out: torch.Tensor) -> torch.Tensor:
+        """Write the current per-parameter gradients (memory order) into ``out[:d]``."""
+        pos = 0
+        for p, n in zip(self.params, self.numels):
+            g = p.grad
+            if g is None:
+                out[pos:pos + n].zero_()
+            else:
+                out[pos:pos + n].copy_(memory_order_flat(g))
+            pos += n
+        return out

@@ -68,3 +68,19 @@ def test_engine_matches_reference_sgd_on_average(cuda):
         opt.step()
     flat2 = torch.cat([p.detach().reshape(-1) for p in m2.parameters()])
     assert torch.allclose(eng.flat_model(), flat2, atol=2e-4, rtol=1e-3)
+
+
+def test_engine_channels_last_matches_nchw(cuda):
+    """channels_last changes only the memory order of the flat buffer, not the training math."""
+    outs = []
+    for cl in (False, True):
+        torch.manual_seed(0)
+        cfg = EngineConfig(gar="average", f=1, workers_per_rank=5, exchange_dtype=torch.float32,
+                           autocast_dtype=None, channels_last=cl)
+        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+        b = synthetic_batches(5, 4, (3, 32, 32), 10, cuda, channels_last=cl)
+        for _ in range(2):
+            eng.step(b)
+        outs.append(eng.flat.reference_vector())
+    err = (outs[0] - outs[1]).abs().max().item()
+    assert err < 1e-3, err

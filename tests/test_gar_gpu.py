@@ -175,3 +175,19 @@ def test_deterministic_replicas(cuda):
     b = gar.krum(X.clone(), 3)
     assert torch.equal(a, b)
     assert torch.equal(gar.bulyan(X, 3), gar.bulyan(X.clone(), 3))
+
+
+@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32, torch.float16])
+def test_flatten_cast_matches_cat(cuda, native, odt):
+    torch.manual_seed(0)
+    shapes = [(64, 3, 7, 7), (10,), (3,), (512, 256, 3, 3), (1,), (130, 7)] * 20  # > 96 tensors: 2 launches
+    ts = [torch.randn(s, device=cuda) for s in shapes]
+    ts[0] = ts[0].contiguous(memory_format=torch.channels_last)
+    total = sum(t.numel() for t in ts)
+    dst = torch.zeros(total + 5, device=cuda, dtype=odt)
+    native.gpu_flatten_cast(ts, dst)
+    from garfield_amd.utils.flat import memory_order_flat
+    ref_ = torch.cat([memory_order_flat(t) for t in ts]).to(odt)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:total], ref_)
+    assert torch.equal(dst[total:], torch.zeros(5, device=cuda, dtype=odt))
