@@ -1,0 +1,81 @@
+"""LEARN: decentralised Byzantine-resilient learning (every node is worker + server).
+
+Reference: ``pytorch_impl/applications/LEARN/trainer.py:208-258``. Node ``node:i``
+hosts a ``Worker`` and a ``Server``; each iteration it pulls ``n - f`` gradients,
+aggregates them (GAR, f), optionally runs the ``ceil(log2(i+1))``-round average
+agreement on aggregated gradients (``--non_iid``), updates, then pulls ``n - f``
+models, aggregates and writes them. The reference's ``sleep(20)`` start barrier is
+replaced by the blocking peer-registration handshake of ``Server.get_rrefs``.
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import sys
+import time
+
+from garfield_amd import aggregators
+from garfield_amd.apps.common import StepTimer, add_common, init_rpc, print_setup, seed_all
+from garfield_amd.runtime.byz_worker import ByzWorker
+from garfield_amd.runtime.server import Server
+from garfield_amd.runtime.worker import Worker
+from garfield_amd.utils.logging import info
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(description="LEARN (Garfield-MI355X)", formatter_class=argparse.RawTextHelpFormatter)
+    add_common(p, ps=False)
+    p.add_argument("--num_nodes", type=int, default=3)
+    p.add_argument("--f", type=int, default=0, help="Number of declared Byzantine nodes.")
+    p.add_argument("--non_iid", type=int, default=0, help="1: run the log2(t) average-agreement rounds.")
+    p.set_defaults(port=29700)
+    return p.parse_args(argv)
+
+
+def avg_agree(ps, gar, aggr_grad, rounds: int, num_wait: int, f: int):
+    """Average agreement: ``rounds`` rounds of exchanging + aggregating aggregated gradients."""
+    for _ in range(rounds):
+        ps.latest_aggr_grad = aggr_grad
+        aggr_grad = gar(gradients=ps.get_aggr_grads(num_wait), f=f)
+    return aggr_grad
+
+
+def main(argv=None, results: dict | None = None):
+    a = parse(argv)
+    n, f = a.num_nodes, a.f
+    if a.rank == 0:
+        print_setup(a.rank, nodes=n, f=f, gar=a.gar, dataset=a.dataset, model=a.model, batch=a.batch,
+                    optimizer=a.optimizer, opt_args=a.opt_args, non_iid=a.non_iid)
+    seed_all(1234)
+    init_rpc(f"node:{a.rank}", a.rank, n, a.master, a.port, a.rpc_timeout)
+    gar = aggregators.get(a.gar)
+    if a.attack and a.rank < f:
+        ByzWorker(a.rank, n, n, a.batch, a.model, a.dataset, a.loss, a.attack, f, a.train_size, device=a.device)
+    else:
+        Worker(a.rank, n, n, a.batch, a.model, a.dataset, a.loss, a.train_size, device=a.device)
+    ps = Server(a.rank, n, n, n, f, f, "node:", "node:", a.batch, a.model, a.dataset, a.optimizer, a.train_size,
+                device=a.device, rpc_timeout=a.rpc_timeout, **a.opt_args)
+    start = time.time()
+    acc = None
+    for i in range(a.num_iter):
+        with StepTimer(a.bench) as t:
+            aggr = gar(gradients=ps.get_gradients(i, n - f), f=f)
+            if a.non_iid:
+                aggr = avg_agree(ps, gar, aggr, math.ceil(math.log2(i + 1)), n - f, f)
+            ps.latest_aggr_grad = aggr
+            ps.update_model(aggr)
+            ps.write_model(gar(gradients=ps.get_models(n - f), f=f))
+        if a.bench:
+            info(f"Training step {i} takes {t.seconds:.4f} s, consumed bandwidth {t.gbit:.4f} Gbits")
+        if (a.acc_freq and i % a.acc_freq == 0) or i == a.num_iter - 1:
+            acc = ps.compute_binary_accuracy() if a.dataset == "pima" else ps.compute_accuracy()
+            info(f"Node {a.rank} iteration: {i} Accuracy: {acc:.2f} Time: {time.time() - start:.2f}")
+    if results is not None:
+        results["accuracy"] = acc
+    import torch.distributed.rpc as rpc
+
+    rpc.shutdown()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

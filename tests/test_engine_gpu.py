@@ -82,5 +82,7 @@ def test_engine_channels_last_matches_nchw(cuda):
         for _ in range(2):
             eng.step(b)
         outs.append(eng.flat.reference_vector())
-    err = (outs[0] - outs[1]).abs().max().item()
-    assert err < 1e-3, err
+    # NCHW and NHWC convolutions use different MIOpen algorithms (accumulation order,
+    # Winograd): compare the whole parameter vector in relative norm
+    rel = ((outs[0] - outs[1]).norm() / outs[0].norm()).item()
+    assert rel < 1e-3, rel
