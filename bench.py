@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--overhead", action="store_true",
                    help="also time the same job with the 'average' GAR and report the Krum overhead")
     p.add_argument("--cudnn-benchmark", action="store_true")
+    p.add_argument("--no-graph", action="store_true", help="disable per-worker HIP graph capture (eager launches)")
     p.add_argument("--lr", type=float, default=0.01,
                    help="0.01: the reference lr (0.2) diverges from random init on the synthetic data")
     return p.parse_args()
@@ -99,7 +100,8 @@ def main():
     d = num_parameters(model)
     xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
     cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
-                       weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last)
+                       weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
+                       cuda_graph=not a.no_graph)
     eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
     batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
                                 seed=1000 + ctx.rank, channels_last=a.channels_last)
@@ -111,7 +113,8 @@ def main():
     extra = {}
     if a.overhead:
         cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
-                               weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last)
+                               weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
+                               cuda_graph=not a.no_graph)
         torch.manual_seed(1234)
         eng_avg = RobustDataParallel(build_model(a.model, num_classes=num_classes), F.cross_entropy, ctx, cfg_avg)
         e_avg, _ = timed_steps(eng_avg, batches, a.steps, a.warmup, ctx)
@@ -142,6 +145,7 @@ def main():
                 "f": a.f,
                 "batch_per_worker": a.batch,
                 "exchange_dtype": a.exchange_dtype,
+                "hip_graphs": bool(getattr(eng, "_graph", None)),
                 "optimizer": f"SGD lr={a.lr} momentum=0.9 wd=5e-4 (fused into the GAR combine kernel)",
             },
             "final_loss": round(loss, 4),

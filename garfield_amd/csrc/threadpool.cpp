@@ -43,7 +43,8 @@ void ThreadPool::run_chunks(size_t nchunks, const std::function<void(size_t)>& f
     return;
   }
   std::atomic<size_t> next{0};
-  std::atomic<size_t> done{0};
+  size_t done = 0;  // guarded by wmx: the waiter may only return (and destroy these locals)
+                    // once the last task has left its critical section
   std::mutex emx;
   std::exception_ptr err;
   std::mutex wmx;
@@ -60,10 +61,8 @@ void ThreadPool::run_chunks(size_t nchunks, const std::function<void(size_t)>& f
         if (!err) err = std::current_exception();
       }
     }
-    if (done.fetch_add(1) + 1 == ntasks) {
-      std::lock_guard<std::mutex> g(wmx);
-      wcv.notify_all();
-    }
+    std::lock_guard<std::mutex> g(wmx);
+    if (++done == ntasks) wcv.notify_all();
   };
   {
     std::lock_guard<std::mutex> g(mutex_);
@@ -72,7 +71,7 @@ void ThreadPool::run_chunks(size_t nchunks, const std::function<void(size_t)>& f
   cv_.notify_all();
   {
     std::unique_lock<std::mutex> lk(wmx);
-    wcv.wait(lk, [&] { return done.load() == ntasks; });
+    wcv.wait(lk, [&] { return done == ntasks; });
   }
   if (err) std::rethrow_exception(err);
 }

@@ -86,3 +86,22 @@ def test_engine_channels_last_matches_nchw(cuda):
     # Winograd): compare the whole parameter vector in relative norm
     rel = ((outs[0] - outs[1]).norm() / outs[0].norm()).item()
     assert rel < 1e-3, rel
+
+
+@pytest.mark.parametrize("rule", ["krum", "median"])
+def test_engine_cuda_graph_matches_eager(cuda, rule):
+    """Per-worker HIP-graph replay == eager steps (same math, fewer launches)."""
+    outs, losses = [], []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        cfg = EngineConfig(gar=rule, f=1, workers_per_rank=5, cuda_graph=graph, byzantine={4: "reverse"})
+        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+        b = synthetic_batches(5, 8, (3, 32, 32), 10, cuda)
+        ls = [float(eng.step(b)) for _ in range(4)]
+        if graph:
+            assert eng._graph is not None and not eng._graph_failed
+        outs.append(eng.flat.reference_vector().clone())
+        losses.append(ls)
+    rel = ((outs[0] - outs[1]).norm() / outs[0].norm()).item()
+    assert rel < 1e-2, rel
+    assert abs(losses[0][-1] - losses[1][-1]) < 0.1 * abs(losses[0][-1]) + 1e-3
