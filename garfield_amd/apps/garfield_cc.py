@@ -1,0 +1,134 @@
+"""Garfield_CC: Byzantine-resilient training over collectives (one process per GPU).
+
+Reference: ``pytorch_impl/applications/Garfield_CC/trainer.py`` (flags ``--master
+--rank --dataset --batch --num_ps --num_workers --fw --fps --model --loss --lr
+--momentum --wd --epochs --aggregator --mar --backend --bench --log``; per-parameter
+``dist.gather``/``broadcast`` on gloo because "NCCL does not support gather").
+
+Here every gradient exchange is ONE flat all-gather per logical-worker slot over
+RCCL (``--backend nccl``, default on GPU) or gloo, and:
+
+* ``--num_ps 0`` (or 1 with ``--fps 0``): replicated-server robust DP — every rank is
+  a worker (``--workers_per_rank`` logical workers) and runs the GAR redundantly
+  (``parallel.engine.RobustDataParallel``);
+* ``--num_ps P >= 2``: Byzantine-server mode — ranks < P are server replicas, the
+  others workers; servers aggregate worker gradients with ``--aggregator`` and every
+  rank aggregates the servers' models with ``--mar`` (``parallel.byzps``).
+
+Launch: ``torchrun --nproc-per-node 8 -m garfield_amd.apps.garfield_cc ...`` (reads
+RANK / WORLD_SIZE / LOCAL_RANK), or one process per node with ``--rank/--master``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+from garfield_amd.apps.common import str2bool
+from garfield_amd.data.datasets import CLASSES, DatasetManager
+from garfield_amd.models import build_model
+from garfield_amd.parallel.byzps import ByzantinePSDataParallel, ByzPSConfig
+from garfield_amd.parallel.comm import init_distributed, shutdown
+from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel
+from garfield_amd.utils.logging import info, set_rank_prefix
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(description="Garfield_CC (Garfield-MI355X, collectives)")
+    p.add_argument("--master", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
+    p.add_argument("--port", type=int, default=int(os.environ.get("MASTER_PORT", 29500)))
+    p.add_argument("--rank", type=int, default=None)
+    p.add_argument("--dataset", default="cifar10")
+    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--num_ps", type=int, default=0)
+    p.add_argument("--num_workers", type=int, default=None, help="worker ranks (default: world - num_ps)")
+    p.add_argument("--workers_per_rank", type=int, default=1, help="logical workers hosted by each worker rank")
+    p.add_argument("--fw", type=int, default=0)
+    p.add_argument("--fps", type=int, default=0)
+    p.add_argument("--model", default="resnet18")
+    p.add_argument("--loss", default="cross-entropy")
+    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--momentum", type=float, default=0.9)
+    p.add_argument("--wd", type=float, default=5e-4)
+    p.add_argument("--epochs", type=int, default=1)
+    p.add_argument("--num_iter", type=int, default=0, help="stop after this many iterations (0: epochs)")
+    p.add_argument("--aggregator", default="average")
+    p.add_argument("--mar", default="median")
+    p.add_argument("--attack", default="", help="attack of the fw Byzantine worker slots")
+    p.add_argument("--ps_attack", default="", help="attack of the fps Byzantine servers")
+    p.add_argument("--backend", default=None, help="nccl (RCCL) or gloo")
+    p.add_argument("--exchange_dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--cuda_graph", type=str2bool, default=True)
+    p.add_argument("--bench", type=str2bool, default=False)
+    p.add_argument("--log", type=str2bool, default=False)
+    p.add_argument("--acc_freq", type=int, default=0)
+    return p.parse_args(argv)
+
+
+def main(argv=None, results: dict | None = None):
+    a = parse(argv)
+    if a.rank is not None:
+        world = a.num_ps + (a.num_workers or 1)
+        os.environ.update(RANK=str(a.rank), WORLD_SIZE=str(world), MASTER_ADDR=a.master, MASTER_PORT=str(a.port))
+        os.environ.setdefault("LOCAL_RANK", str(a.rank % max(torch.cuda.device_count(), 1)))
+    ctx = init_distributed(backend=a.backend)
+    set_rank_prefix(f"[rank {ctx.rank}] " if ctx.world_size > 1 else "")
+    torch.manual_seed(1234)
+    ncls = CLASSES.get(a.dataset, 10)
+    loss_fn = F.nll_loss if a.loss == "nll" else (F.binary_cross_entropy if a.loss == "binary-cross-entropy"
+                                                    else F.cross_entropy)
+    model = build_model(a.model, num_classes=ncls)
+    xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
+    k = a.workers_per_rank
+    byz_mode = a.num_ps >= 2 or (a.num_ps == 1 and a.fps > 0)
+    worker_ranks = list(range(a.num_ps, ctx.world_size)) if byz_mode else list(range(ctx.world_size))
+    # Byzantine logical workers: the first fw global worker slots (slot = j * world + rank)
+    slots = sorted(j * ctx.world_size + r for j in range(k) for r in worker_ranks)
+    byz = {s: a.attack for s in slots[: a.fw]} if a.attack else {}
+    common = dict(gar=a.aggregator, f=max(a.fw, 1) if a.aggregator not in ("average", "median", "average-nan")
+                  else max(a.fw, 0), workers_per_rank=k, lr=a.lr, momentum=a.momentum, weight_decay=a.wd,
+                  exchange_dtype=xdt, byzantine=byz, cuda_graph=a.cuda_graph)
+    if byz_mode:
+        eng = ByzantinePSDataParallel(model, loss_fn, ctx,
+                                      ByzPSConfig(num_ps=a.num_ps, fps=a.fps, mar=a.mar, ps_attack=a.ps_attack,
+                                                  **common))
+    else:
+        eng = RobustDataParallel(model, loss_fn, ctx, EngineConfig(**common))
+    # data: logical worker j of rank r trains on partition (its worker index)
+    nwork = len(worker_ranks) * k
+    my_index = worker_ranks.index(ctx.rank) if ctx.rank in worker_ranks else 0
+    loaders = []
+    for j in range(k):
+        mgr = DatasetManager(a.dataset, a.batch, nwork, nwork, j * len(worker_ranks) + my_index, device=ctx.device)
+        loaders.append(mgr.get_train_set())
+    test = DatasetManager(a.dataset, a.batch, 1, 1, 0, device=ctx.device).get_test_set()
+    iters = a.num_iter or a.epochs * min(len(ld) for ld in loaders)
+    t0 = time.time()
+    loss = None
+    for i in range(iters):
+        batches = [ld[i] for ld in loaders]
+        ts = time.perf_counter()
+        loss = eng.step(batches)
+        if a.bench:
+            if ctx.device.type == "cuda":
+                torch.cuda.synchronize()
+            info(f"iteration {i}: {1000 * (time.perf_counter() - ts):.2f} ms")
+        if a.log:
+            info(f"iteration {i} loss {float(loss):.4f}")
+        if a.acc_freq and (i % a.acc_freq == 0 or i == iters - 1) and ctx.rank == 0:
+            info(f"iteration {i} accuracy {eng.evaluate(test, binary=ncls == 1):.2f} time {time.time() - t0:.1f}s")
+    acc = eng.evaluate(test, binary=ncls == 1)
+    if ctx.rank == 0:
+        info(f"final accuracy {acc:.2f} after {iters} iterations ({time.time() - t0:.1f}s)")
+    if results is not None:
+        results.update(accuracy=acc, checksum=eng.replica_checksum(), loss=float(loss) if loss is not None else None)
+    shutdown(ctx)
+    return acc
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -17,6 +17,7 @@ Here (no torchvision, no network):
 """
 from __future__ import annotations
 
+import functools
 import gzip
 import os
 import pathlib
@@ -145,6 +146,7 @@ class PimaDiabetesDataset(TensorDataset):
             super().__init__(s.x, s.y, name="pima", synthetic=True)
 
 
+@functools.lru_cache(maxsize=8)
 def fetch(name: str, train: bool = True, train_size: int | None = None) -> TensorDataset:
     if name not in datasets_list:
         raise ValueError(f"Existing datasets are: {datasets_list}")

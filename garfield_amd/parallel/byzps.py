@@ -1,0 +1,152 @@
+"""Byzantine-server mode (ByzSGD / GuanYu) over collectives.
+
+Reference: ``applications/Garfield_CC/trainer.py:90-196`` (per parameter tensor:
+every worker broadcasts its gradient to every PS replica inside a
+``workers ∪ {ps}`` group, PS replicas ``all_gather`` their aggregated gradients and
+apply ``--mar``, then every PS broadcasts to every worker, which applies ``--mar``
+again) and the RPC ``ByzSGD`` trainer (``get_models`` + model GAR).
+
+Collective form here, per step, on flat vectors (never per tensor):
+
+1. worker ranks (``rank >= num_ps``) compute their logical workers' gradients into
+   the exchange buffer ``X[k, world, ld]``; server ranks contribute zero rows;
+2. ``X`` is all-gathered (RCCL full mesh) slot by slot, overlapped with compute;
+3. every server replica runs the GAR (f = fw) on the worker rows only (a row
+   table over the worker slots — no stacking copy) and applies its SGD update;
+   simulated Byzantine servers (``ps_attack``, ranks < fps) then corrupt their model;
+4. every rank all-gathers the servers' models (``M[world, ld]``) and writes the
+   model aggregation rule (``mar``, f = fps) over the ``num_ps`` server rows into its
+   own parameters (HIP coordinate-wise kernel writing straight into the flat fp32
+   parameter buffer). Honest replicas therefore stay identical.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+
+from garfield_amd.ops import gar
+from garfield_amd.parallel.comm import DistContext, all_gather_rows
+from garfield_amd.parallel.engine import COORD_RULES, WEIGHTED_RULES, EngineConfig, RobustDataParallel
+from garfield_amd.runtime.attacks import SERVER_ATTACKS
+
+
+@dataclass
+class ByzPSConfig(EngineConfig):
+    num_ps: int = 3
+    fps: int = 1
+    mar: str = "trimmed-mean"
+    ps_attack: str = ""        # attack of the simulated Byzantine servers (ranks < fps)
+
+
+class ByzantinePSDataParallel(RobustDataParallel):
+    def __init__(self, model: nn.Module, loss_fn, ctx: DistContext, cfg: ByzPSConfig):
+        if not (0 < cfg.num_ps < ctx.world_size):
+            raise ValueError(f"need 0 < num_ps < world_size, got num_ps={cfg.num_ps} world={ctx.world_size}")
+        self.num_ps = cfg.num_ps
+        super().__init__(model, loss_fn, ctx, cfg)
+        self.is_ps = ctx.rank < cfg.num_ps
+        self.worker_ranks = list(range(cfg.num_ps, ctx.world_size))
+        self.n_w = self.k * len(self.worker_ranks)
+        self.M = torch.zeros((self.world, self.ld), dtype=torch.float32, device=self.device)
+        self._ps_gen = torch.Generator(device=self.device)
+        self._ps_gen.manual_seed(cfg.seed + 31 * ctx.rank)
+
+    def _check_gar(self) -> None:
+        from garfield_amd import aggregators
+
+        cfg = self.cfg
+        n_w = cfg.workers_per_rank * (self.ctx.world_size - cfg.num_ps)
+        msg = aggregators.get(cfg.gar).check(gradients=[torch.zeros(1)] * n_w, f=cfg.f, **cfg.gar_kwargs)
+        if msg is not None:
+            raise ValueError(f"GAR {cfg.gar!r} with {n_w} worker gradients: {msg}")
+        msg = aggregators.get(cfg.mar).check(gradients=[torch.zeros(1)] * cfg.num_ps, f=cfg.fps)
+        if msg is not None:
+            raise ValueError(f"MAR {cfg.mar!r} with {cfg.num_ps} servers: {msg}")
+
+    def graph_capturable(self) -> bool:
+        return False  # servers and workers run different bodies; keep it eager
+
+    def _worker_rows(self) -> list:
+        return [self.X[j, r, : self.d] for j in range(self.k) for r in self.worker_ranks]
+
+    def step(self, batches) -> torch.Tensor:
+        cfg = self.cfg
+        # 1-2: gradients (workers) + exchange (everyone)
+        if self.is_ps:
+            works = [all_gather_rows(self.X[j], self.rank, async_op=True) for j in range(self.k)] \
+                if self.world > 1 else []
+            for w in works:
+                w.wait()
+            loss = torch.zeros((), device=self.device)
+        else:
+            losses = self.compute_local(batches)
+            loss = torch.stack(losses).float().mean()
+        # 3: servers aggregate + update
+        if self.is_ps:
+            self._server_update()
+            if cfg.ps_attack and self.rank < cfg.fps:
+                v = self.flat.data[: self.d]
+                v.copy_(SERVER_ATTACKS[cfg.ps_attack](v, generator=self._ps_gen))
+        # 4: model exchange + model aggregation on every rank
+        self.M[self.rank].copy_(self.flat.data)
+        if self.world > 1:
+            all_gather_rows(self.M, self.rank)
+        models = [self.M[p, : self.d] for p in range(self.num_ps)]
+        self._write_mar(models)
+        self.step_count += 1
+        return loss
+
+    def _server_update(self) -> None:
+        cfg = self.cfg
+        rows = self._worker_rows()
+        first = self.step_count == 0
+        param, mom = self.flat.data[: self.d], self.mom[: self.d]
+        if self.device.type == "cuda":
+            C = self._C
+            if cfg.gar in WEIGHTED_RULES:
+                kw = {}
+                if cfg.gar == "krum":
+                    w = gar.krum_weights(rows, cfg.f, cfg.m)
+                elif cfg.gar == "brute":
+                    w = gar.brute_weights(rows, cfg.f)
+                elif cfg.gar == "aksel":
+                    w = gar.aksel_weights(rows, cfg.f, cfg.gar_kwargs.get("mode", "mid"))
+                else:
+                    w = torch.full((len(rows),), 1.0 / len(rows), device=self.device)
+                del kw
+                self.last_weights = w
+                C.gpu_combine_sgd(rows, w, param, mom, None, cfg.lr, cfg.momentum, cfg.dampening,
+                                  cfg.weight_decay, cfg.nesterov, first)
+                return
+            g = gar.aggregate(cfg.gar, rows, **self._gar_kwargs()).float()
+            C.gpu_combine_sgd([g], self._one, param, mom, None, cfg.lr, cfg.momentum, cfg.dampening,
+                              cfg.weight_decay, cfg.nesterov, first)
+        else:
+            g = gar.aggregate(cfg.gar, rows, **self._gar_kwargs()).float()
+            self._sgd_cpu(g, first)
+
+    def _gar_kwargs(self) -> dict:
+        cfg = self.cfg
+        kw = dict(cfg.gar_kwargs)
+        if cfg.gar not in ("average", "median", "average-nan"):
+            kw["f"] = cfg.f
+        if cfg.m is not None and cfg.gar in ("krum", "bulyan"):
+            kw["m"] = cfg.m
+        if cfg.gar == "condense":
+            kw.setdefault("seed", cfg.seed + self.step_count)
+        return kw
+
+    def _write_mar(self, models: list) -> None:
+        cfg = self.cfg
+        out = self.flat.data[: self.d]
+        kw = {} if cfg.mar in ("average", "median", "average-nan") else {"f": cfg.fps}
+        if self.device.type == "cuda" and cfg.mar in COORD_RULES and cfg.mar not in ("bulyan", "condense"):
+            modes = gar._MODE
+            beta = len(models) - cfg.fps
+            self._C.gpu_coordwise(models, modes[cfg.mar], cfg.fps, beta, None, 0, 0, 1.0, out)
+        else:
+            agg = gar.aggregate(cfg.mar, models, **kw)
+            with torch.no_grad():
+                out.copy_(agg)

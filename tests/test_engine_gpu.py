@@ -90,18 +90,22 @@ def test_engine_channels_last_matches_nchw(cuda):
 
 @pytest.mark.parametrize("rule", ["krum", "median"])
 def test_engine_cuda_graph_matches_eager(cuda, rule):
-    """Per-worker HIP-graph replay == eager steps (same math, fewer launches)."""
-    outs, losses = [], []
-    for graph in (False, True):
+    """Per-worker HIP-graph replay == eager steps (same math, fewer launches).
+
+    MIOpen's split-K weight-gradient kernels are not bitwise deterministic, so the
+    graph run is compared against the eager run-to-run noise floor."""
+    outs = []
+    for graph in (False, False, True):
         torch.manual_seed(0)
-        cfg = EngineConfig(gar=rule, f=1, workers_per_rank=5, cuda_graph=graph, byzantine={4: "reverse"})
+        cfg = EngineConfig(gar=rule, f=1, workers_per_rank=5, cuda_graph=graph, byzantine={4: "reverse"}, lr=1e-3)
         eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
         b = synthetic_batches(5, 8, (3, 32, 32), 10, cuda)
-        ls = [float(eng.step(b)) for _ in range(4)]
+        init = eng.flat.reference_vector().clone()
+        for _ in range(3):
+            eng.step(b)
         if graph:
             assert eng._graph is not None and not eng._graph_failed
-        outs.append(eng.flat.reference_vector().clone())
-        losses.append(ls)
-    rel = ((outs[0] - outs[1]).norm() / outs[0].norm()).item()
-    assert rel < 1e-2, rel
-    assert abs(losses[0][-1] - losses[1][-1]) < 0.1 * abs(losses[0][-1]) + 1e-3
+        outs.append(eng.flat.reference_vector().clone() - init)   # the accumulated update
+    noise = ((outs[0] - outs[1]).norm() / outs[0].norm()).item()
+    rel = ((outs[0] - outs[2]).norm() / outs[0].norm()).item()
+    assert rel < max(10 * noise, 1e-3), (rel, noise)
