@@ -17,11 +17,12 @@ class ByzServer(Server):
                  model, dataset, optimizer, attack, *args, train_size=None, **kwargs):
         if attack not in SERVER_ATTACKS:
             raise ValueError(f"The requested attack is not implemented; available attacks are: {list(SERVER_ATTACKS)}")
-        super().__init__(rank, world_size, num_workers, num_ps, byz_wrk, byz_ps, wrk_base_name, ps_base_name, batch,
-                         model, dataset, optimizer, train_size, *args, **kwargs)
+        # set before the base constructor announces this server to its peers
         self.attack_name = attack
         self.gen = torch.Generator()
         self.gen.manual_seed(20011 + rank)
+        super().__init__(rank, world_size, num_workers, num_ps, byz_wrk, byz_ps, wrk_base_name, ps_base_name, batch,
+                         model, dataset, optimizer, train_size, *args, **kwargs)
 
     def _attack(self, t: torch.Tensor) -> torch.Tensor:
         return SERVER_ATTACKS[self.attack_name](t, generator=self.gen)
