@@ -1,0 +1,10 @@
+"""Reference import name ``tools`` -> garfield_amd.utils (Context, UserException,
+info/warning/error/fatal/trace, pairwise, parse_keyval, TimedContext, flatten, relink,
+grads_of, import_directory, cluster_parse)."""
+from garfield_amd.utils.flat import flatten, grads_of, relink  # noqa: F401
+from garfield_amd.utils.logging import (  # noqa: F401
+    Context, UserException, context, error, fatal, info, trace, warning,
+)
+from garfield_amd.utils.misc import (  # noqa: F401
+    TimedContext, cluster_parse, import_directory, pairwise, parse_keyval,
+)

@@ -30,6 +30,30 @@ _REGISTRY = {
     "resnet50": ("resnet", "imagenet_resnet", {"depth": 50}),
     "resnet101": ("resnet", "imagenet_resnet", {"depth": 101}),
     "resnet152": ("resnet", "imagenet_resnet", {"depth": 152}),
+    "preactresnet18": ("zoo", "PreActResNet18", {}),
+    "googlenet": ("zoo", "GoogLeNet", {}),
+    "densenet121": ("zoo", "DenseNet121", {}),
+    "resnext29": ("zoo", "ResNeXt29_2x64d", {}),
+    "resnext29_4x64d": ("zoo", "ResNeXt29_4x64d", {}),
+    "resnext29_32x4d": ("zoo", "ResNeXt29_32x4d", {}),
+    "mobilenet": ("zoo", "MobileNet", {}),
+    "mobilenetv2": ("zoo", "MobileNetV2", {}),
+    "dpn26": ("zoo", "DPN26", {}),
+    "dpn92": ("zoo", "DPN92", {}),
+    "shufflenetg2": ("zoo", "ShuffleNetG2", {}),
+    "shufflenetg3": ("zoo", "ShuffleNetG3", {}),
+    "shufflenetv2": ("zoo", "ShuffleNetV2", {}),
+    "senet18": ("zoo", "SENet18", {}),
+    "efficientnetb0": ("zoo", "EfficientNetB0", {}),
+    "regnetx200": ("zoo", "RegNetX_200MF", {}),
+    "regnetx400": ("zoo", "RegNetX_400MF", {}),
+    "pnasneta": ("zoo", "PNASNetA", {}),
+    "pnasnetb": ("zoo", "PNASNetB", {}),
+    "vgg11_cifar": ("zoo", "VGG", {"vgg_name": "VGG11"}),
+    "vgg16_cifar": ("zoo", "VGG", {"vgg_name": "VGG16"}),
+    "vgg19_cifar": ("zoo", "VGG", {"vgg_name": "VGG19"}),
+    "vgg16": ("zoo", "ImageNetVGG", {"vgg_name": "VGG16"}),
+    "vgg19": ("zoo", "ImageNetVGG", {"vgg_name": "VGG19"}),
 }
 
 

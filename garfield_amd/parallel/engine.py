@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -36,6 +37,14 @@ from garfield_amd.ops import gar
 from garfield_amd.parallel.comm import DistContext, all_gather_rows
 from garfield_amd.runtime.attacks import NEEDS_ESTIMATES, apply_attack
 from garfield_amd.utils.flat import FlatParams
+
+# MIOpen's CK grouped-conv backward-weight solver is not HIP-graph-replay safe on
+# ROCm 7 / gfx950: from the second replay of a captured backward it leaves whole
+# bf16 weight gradients non-finite (diagnosed with scripts/debug_graph.py: fp32 and
+# BatchNorm-free nets are unaffected, disabling only this solver fixes VGG/ResNet).
+# It must be disabled before MIOpen picks solvers for the process, i.e. before
+# the first convolution; users may override the variable explicitly.
+os.environ.setdefault("MIOPEN_DEBUG_GROUP_CONV_IMPLICIT_GEMM_HIP_WRW_XDLOPS", "0")
 
 WEIGHTED_RULES = {"average", "krum", "brute", "aksel"}
 COORD_RULES = {"median", "trimmed-mean", "averaged-median", "average-nan", "condense", "bulyan"}
@@ -334,16 +343,26 @@ class RobustDataParallel:
         torch.cuda.synchronize()
         graphs = [None] * self.k
         pool = None
+        shared = os.environ.get("GARFIELD_GRAPH_SHARED_POOL", "1") == "1"
+        warm = int(os.environ.get("GARFIELD_GRAPH_WARMUP", "1"))
         try:
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
+            # warm-up ON THE CAPTURE STREAM (lazy per-stream library state: BLAS / MIOpen
+            # workspaces, algorithm caches) before any capture
+            with torch.cuda.stream(s):
+                for _ in range(warm):
+                    for j in self.local_slots:
+                        x, y = self._static[j]
+                        self._worker_body(j, x, y, self._static_loss[j])
+            s.synchronize()
             for j in self.local_slots:
                 g = torch.cuda.CUDAGraph()
                 mode = "thread_local" if self.world > 1 else "global"  # RCCL watchdog thread
                 with torch.cuda.graph(g, stream=s, pool=pool, capture_error_mode=mode):
                     x, y = self._static[j]
                     self._worker_body(j, x, y, self._static_loss[j])
-                if pool is None:
+                if pool is None and shared:
                     pool = g.pool()
                 graphs[j] = g
             torch.cuda.current_stream(self.device).wait_stream(s)

@@ -1,0 +1,77 @@
+"""Checkpoint / resume.
+
+The reference never saves a PyTorch checkpoint (no ``torch.save``);
+its de facto interchange format is the flat fp32 vector of ``model.parameters()``
+in registration order (``server.py:196-200,289-297``). A checkpoint here holds:
+
+* ``flat``: that reference-layout parameter vector (what ``Server.write_model`` /
+  ``get_model`` exchange), so a checkpoint can seed any node of any app;
+* ``buffers``: the model's named buffers (BatchNorm statistics);
+* ``momentum``: the engine's flat momentum buffer (memory order), when present;
+* ``step`` and free-form ``meta``.
+
+Files are written atomically (temp file + rename) with ``torch.save`` and read back
+with ``torch.load(weights_only=True)`` — plain tensors and primitives only.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+
+import torch
+import torch.nn as nn
+
+from garfield_amd.utils.flat import flatten, write_flat_parameters
+
+
+def model_state(model: nn.Module) -> dict:
+    return {"flat": flatten(p.detach() for p in model.parameters()).cpu(),
+            "buffers": {n: b.detach().cpu().clone() for n, b in model.named_buffers()}}
+
+
+def save(path: str, model: nn.Module, step: int = 0, momentum: torch.Tensor | None = None,
+         meta: dict | None = None) -> str:
+    state = model_state(model)
+    state["step"] = int(step)
+    if momentum is not None:
+        state["momentum"] = momentum.detach().cpu()
+    state["meta"] = dict(meta or {})
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(dir=d, prefix=".ckpt-")
+    os.close(fd)
+    torch.save(state, tmp)
+    os.replace(tmp, path)
+    return path
+
+
+def load(path: str, model: nn.Module | None = None, map_location="cpu") -> dict:
+    state = torch.load(path, map_location=map_location, weights_only=True)
+    if model is not None:
+        restore(model, state)
+    return state
+
+
+def restore(model: nn.Module, state: dict) -> None:
+    dev = next(model.parameters()).device
+    write_flat_parameters(model, state["flat"].to(dev))
+    saved = state.get("buffers", {})
+    with torch.no_grad():
+        for n, b in model.named_buffers():
+            s = saved.get(n)
+            if s is not None and b.shape == s.shape:
+                b.copy_(s.to(b.device))
+
+
+def save_engine(path: str, engine, meta: dict | None = None) -> str:
+    """Checkpoint of a ``RobustDataParallel`` engine (parameters, buffers, momentum, step)."""
+    return save(path, engine.model, engine.step_count, engine.mom[: engine.d], meta)
+
+
+def load_engine(path: str, engine) -> dict:
+    state = load(path, engine.model)
+    if "momentum" in state:
+        engine.mom[: engine.d].copy_(state["momentum"].to(engine.mom.device))
+    engine.step_count = int(state.get("step", 0))
+    engine._graph = None  # re-capture against the restored state
+    return state
