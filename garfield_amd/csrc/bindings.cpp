@@ -121,7 +121,8 @@ void g_gram(const RowSet& rs, const at::Tensor& slabs, const at::Tensor& gram) {
   check_gpu(rs);
   c10::hip::HIPGuard guard(rs.device.index());
   const int grid = garfield::gpu::gram_grid(rs.d, rs.dt, rs.n);
-  TORCH_CHECK(slabs.numel() >= grid * garfield::gpu::gram_slab_floats(rs.n), "garfield: gram slab workspace too small");
+  TORCH_CHECK(slabs.numel() >= (grid + garfield::gpu::kGramReduceGroups) * garfield::gpu::gram_slab_floats(rs.n),
+              "garfield: gram slab workspace too small");
   const int np = garfield::gpu::gram_padded(rs.n);
   TORCH_CHECK(gram.numel() >= np * np, "garfield: gram output too small");
   garfield::gpu::gram(rs.table, rs.n, rs.d, rs.dt, fptr(slabs), grid, fptr(gram), stream_of(rs.device));
@@ -278,6 +279,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gram_padded", &garfield::gpu::gram_padded);
   m.def("gram_grid", [](int64_t d, const at::Tensor& like, int n) { return garfield::gpu::gram_grid(d, dtype_code(like), n); });
   m.def("gram_slab_floats", &garfield::gpu::gram_slab_floats);
+  m.attr("GRAM_REDUCE_GROUPS") = garfield::gpu::kGramReduceGroups;
   m.def("sqdist_grid", &garfield::gpu::sqdist_grid);
 
   // GPU building blocks (asynchronous on the current stream)

@@ -13,10 +13,34 @@ using namespace dev;
 // a fully unrolled bitonic network per coordinate (constant register indices
 // only: no scratch). Rows >= n are padded with +inf.
 
-template <int DT, int NP, int VEC, int MODE>
-__device__ __forceinline__ void coord_body(const RowTable& rows, int n, int f, int beta, const float* sW,
-                                           int t, uint64_t seed, uint64_t thr, int64_t x, float (&res)[VEC],
-                                           bool vector_path) {
+// Row loaders: `load(i, g)` fills g[VEC] with row i's values at the current coordinate(s).
+template <int DT, int VEC>
+struct DirectLoader {  // straight from HBM: VEC consecutive coordinates per lane (8/16-byte loads)
+  const RowTable& rows;
+  int64_t x;
+  bool vector_path;
+  __device__ __forceinline__ void operator()(int i, float (&g)[VEC]) const {
+    if (vector_path) load_vec<DT, VEC>(rows.p[i], x, g);
+    else g[0] = load_one<DT>(rows.p[i], x);
+  }
+};
+
+template <int DT>
+struct LdsLoader {  // from an LDS tile [row][TILE coords] staged with 16-byte loads
+  const void* tile;
+  int pitch;  // elements per tile row
+  int col;
+  __device__ __forceinline__ void operator()(int i, float (&g)[1]) const {
+    if constexpr (DT == kF32) g[0] = static_cast<const float*>(tile)[i * pitch + col];
+    else g[0] = cvt16<DT>(static_cast<const uint16_t*>(tile)[i * pitch + col]);
+  }
+};
+
+// W is read with wave-uniform indices straight from global memory: scalar loads
+// (s_load) into SGPRs, shared by the 64 lanes — not one LDS read per lane and FMA.
+template <int DT, int NP, int VEC, int MODE, class Loader>
+__device__ __forceinline__ void coord_body(const Loader& load, int n, int f, int beta, const float* __restrict__ W,
+                                           int t, uint64_t seed, uint64_t thr, int64_t x, float (&res)[VEC]) {
   float v[NP][VEC];
   float first[VEC];
   if constexpr (MODE == kBulyanTail) {
@@ -26,14 +50,15 @@ __device__ __forceinline__ void coord_body(const RowTable& rows, int n, int f, i
       for (int c = 0; c < VEC; ++c) v[k][c] = 0.f;
     for (int j = 0; j < n; ++j) {
       float g[VEC];
-      if (vector_path) load_vec<DT, VEC>(rows.p[j], x, g);
-      else { g[0] = load_one<DT>(rows.p[j], x); }
+      load(j, g);
 #pragma unroll
       for (int k = 0; k < NP; ++k) {
         if (k < t) {
-          const float w = sW[k * n + j];
+          const float w = W[k * n + j];  // uniform index: scalar load
+          if (w != 0.f) {                // uniform branch: W rows are sparse (m - k non-zeros)
 #pragma unroll
-          for (int c = 0; c < VEC; ++c) v[k][c] += w * g[c];
+            for (int c = 0; c < VEC; ++c) v[k][c] += w * g[c];
+          }
         }
       }
     }
@@ -45,8 +70,7 @@ __device__ __forceinline__ void coord_body(const RowTable& rows, int n, int f, i
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       if (i < n) {
-        if (vector_path) load_vec<DT, VEC>(rows.p[i], x, v[i]);
-        else v[i][0] = load_one<DT>(rows.p[i], x);
+        load(i, v[i]);
       } else {
 #pragma unroll
         for (int c = 0; c < VEC; ++c) v[i][c] = kInf;
@@ -128,22 +152,55 @@ template <int DT, int NP, int VEC, int MODE>
 __global__ __launch_bounds__(256) void k_coordwise(RowTable rows, int n, int64_t d, int f, int beta,
                                                    const float* __restrict__ W, int t, uint64_t seed,
                                                    uint64_t thr, void* out, int out_dt) {
-  __shared__ float sW[(MODE == kBulyanTail) ? (NP * kMaxRows) : 1];
-  if constexpr (MODE == kBulyanTail) {
-    for (int e = threadIdx.x; e < t * n; e += blockDim.x) sW[e] = W[e];
-    __syncthreads();
-  }
   const int64_t dv = (d / VEC) * VEC;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x * VEC;
   for (int64_t x = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * VEC; x < dv; x += stride) {
     float res[VEC];
-    coord_body<DT, NP, VEC, MODE>(rows, n, f, beta, sW, t, seed, thr, x, res, true);
+    coord_body<DT, NP, VEC, MODE>(DirectLoader<DT, VEC>{rows, x, true}, n, f, beta, W, t, seed, thr, x, res);
     store_vec<VEC>(out, out_dt, x, res);
   }
   if (blockIdx.x == 0) {
     for (int64_t x = dv + threadIdx.x; x < d; x += blockDim.x) {
       float res[1];
-      coord_body<DT, NP, 1, MODE>(rows, n, f, beta, sW, t, seed, thr, x, res, false);
+      coord_body<DT, NP, 1, MODE>(DirectLoader<DT, 1>{rows, x, false}, n, f, beta, W, t, seed, thr, x, res);
+      store_one(out, out_dt, x, res[0]);
+    }
+  }
+}
+
+// Large n (NP >= 32): one lane per coordinate would issue n 2-byte loads; instead
+// a workgroup stages a [n x 256-coordinate] tile through LDS with 16-byte loads
+// (each row segment is 512 B / 1 KB contiguous), then every lane reads its
+// column (conflict-free: consecutive lanes, consecutive elements).
+constexpr int kCoordTile = 256;
+
+template <int DT, int NP, int MODE>
+__global__ __launch_bounds__(256) void k_coordwise_lds(RowTable rows, int n, int64_t d, int f, int beta,
+                                                       const float* __restrict__ W, int t, uint64_t seed,
+                                                       uint64_t thr, void* out, int out_dt) {
+  constexpr int ESZ = (DT == kF32) ? 4 : 2;
+  constexpr int CPR = kCoordTile * ESZ / 16;  // 16-byte chunks per tile row
+  __shared__ __align__(16) unsigned char tile[NP * kCoordTile * ESZ];
+  const int64_t ntiles = d / kCoordTile;
+  const int nrows = (MODE == kBulyanTail) ? n : (n < NP ? n : NP);
+  for (int64_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
+    const int64_t x0 = tb * kCoordTile;
+    for (int c = threadIdx.x; c < nrows * CPR; c += blockDim.x) {
+      const int i = c / CPR, k = c % CPR;
+      const uint4 val = *reinterpret_cast<const uint4*>(static_cast<const char*>(rows.p[i]) + x0 * ESZ + k * 16);
+      *reinterpret_cast<uint4*>(tile + (i * kCoordTile) * ESZ + k * 16) = val;
+    }
+    __syncthreads();
+    const int col = threadIdx.x;
+    float res[1];
+    coord_body<DT, NP, 1, MODE>(LdsLoader<DT>{tile, kCoordTile, col}, n, f, beta, W, t, seed, thr, x0 + col, res);
+    store_one(out, out_dt, x0 + col, res[0]);
+    __syncthreads();
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t x = ntiles * kCoordTile + threadIdx.x; x < d; x += blockDim.x) {
+      float res[1];
+      coord_body<DT, NP, 1, MODE>(DirectLoader<DT, 1>{rows, x, false}, n, f, beta, W, t, seed, thr, x, res);
       store_one(out, out_dt, x, res[0]);
     }
   }
@@ -152,6 +209,18 @@ __global__ __launch_bounds__(256) void k_coordwise(RowTable rows, int n, int64_t
 template <int DT, int NP, int VEC, int MODE>
 void launch_coord(const RowTable& rows, int n, int64_t d, int f, int beta, const float* W, int t, uint64_t seed,
                   uint64_t thr, void* out, int out_dt, hipStream_t s) {
+  constexpr int ESZ = (DT == kF32) ? 4 : 2;
+  // LDS-staged path: NP >= 32, tile <= 64 KB, and (Bulyan tail) all n rows fit the NP-row tile
+  if constexpr (NP >= 32 && NP * kCoordTile * ESZ <= 65536) {
+    if (MODE != kBulyanTail || n <= NP) {
+      int64_t g = d / kCoordTile;
+      if (g < 1) g = 1;
+      if (g > 2048) g = 2048;
+      hipLaunchKernelGGL((k_coordwise_lds<DT, NP, MODE>), dim3(static_cast<unsigned>(g)), dim3(256), 0, s, rows, n,
+                         d, f, beta, W, t, seed, thr, out, out_dt);
+      return;
+    }
+  }
   int64_t g = (d / VEC + 255) / 256;
   if (g < 1) g = 1;
   if (g > 4096) g = 4096;

@@ -17,7 +17,8 @@ int gram_nb(int n);                          // 16-row blocks: 1, 2, 4 or 8
 int gram_padded(int n);                      // 16 * gram_nb(n)
 int gram_grid(int64_t d, int dt, int n);     // split-K workgroups
 int64_t gram_slab_floats(int n);             // floats per split-K slab
-// slabs: [grid][slab_floats] workspace; gram: [np][np] fp32 output
+constexpr int kGramReduceGroups = 16;        // stage-1 partials of the slab reduction
+// slabs: [grid + kGramReduceGroups][slab_floats] workspace; gram: [np][np] fp32 output
 void gram(const RowTable& rows, int n, int64_t d, int dt, float* slabs, int grid,
           float* gram, hipStream_t stream);
 

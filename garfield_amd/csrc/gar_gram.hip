@@ -142,6 +142,24 @@ __global__ __launch_bounds__(256) void k_gram_partial(RowTable rows, int n, int6
   for (int e = threadIdx.x; e < NPAIR * 256; e += 256) slab[e] = red[e];
 }
 
+// Stage 1 of the slab reduction: block (bx, r) sums, for 64 entries, the slabs
+// g = r, r + R, r + 2R, ... (split over its 4 waves in a fixed order) into part[r].
+// Spreads the ~1024-slab reduction over ceil(E/64) x R workgroups instead of a
+// handful of latency-bound ones.
+__global__ __launch_bounds__(256) void k_gram_reduce_stage1(const float* __restrict__ slabs, int nslab, int E,
+                                                            int R, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  const int r = blockIdx.y;
+  __shared__ float acc[4][64];
+  float s = 0.f;
+  if (e < E)
+    for (int g = r + R * wave; g < nslab; g += 4 * R) s += slabs[static_cast<int64_t>(g) * E + e];
+  acc[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && e < E) part[static_cast<int64_t>(r) * E + e] = ((acc[0][lane] + acc[1][lane]) + acc[2][lane]) + acc[3][lane];
+}
+
 // Fixed-order reduction of the split-K slabs into the symmetric np x np Gram.
 __global__ __launch_bounds__(256) void k_gram_reduce(const float* __restrict__ slabs, int nslab,
                                                      int nb, float* __restrict__ gram) {
@@ -425,7 +443,16 @@ void gram(const RowTable& rows, int n, int64_t d, int dt, float* slabs, int grid
   by_dtype<GramPartial>(dt, rows, n, d, grid, slabs, stream);
   const int nb = gram_nb(n);
   const int E = nb * (nb + 1) / 2 * 256;
-  hipLaunchKernelGGL(k_gram_reduce, dim3((E + 63) / 64), dim3(256), 0, stream, slabs, grid, nb, gram_out);
+  if (grid > 2 * kGramReduceGroups) {
+    // two-stage deterministic reduction: grid slabs -> kGramReduceGroups partials -> gram
+    float* part = slabs + static_cast<int64_t>(grid) * E;
+    hipLaunchKernelGGL(k_gram_reduce_stage1, dim3((E + 63) / 64, kGramReduceGroups), dim3(256), 0, stream, slabs,
+                       grid, E, kGramReduceGroups, part);
+    hipLaunchKernelGGL(k_gram_reduce, dim3((E + 63) / 64), dim3(256), 0, stream, part, kGramReduceGroups, nb,
+                       gram_out);
+  } else {
+    hipLaunchKernelGGL(k_gram_reduce, dim3((E + 63) / 64), dim3(256), 0, stream, slabs, grid, nb, gram_out);
+  }
 }
 
 // ---------------------------------------------------------------------------

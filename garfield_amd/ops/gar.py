@@ -192,7 +192,7 @@ def gram(gradients) -> torch.Tensor:
 
 def _gram_into(C, rows: Rows, ws: Workspace) -> torch.Tensor:
     grid = C.gram_grid(rows.d, _dtype_probe(rows), rows.n)
-    slabs = ws.get("slabs", grid * C.gram_slab_floats(rows.n))
+    slabs = ws.get("slabs", (grid + C.GRAM_REDUCE_GROUPS) * C.gram_slab_floats(rows.n))
     np_ = C.gram_padded(rows.n)
     g = ws.get("gram", np_ * np_)
     C.gpu_gram(rows.obj, slabs, g)
