@@ -39,10 +39,8 @@ struct LdsLoader {  // from an LDS tile [row][TILE coords] staged with 16-byte l
 // W is read with wave-uniform indices straight from global memory: scalar loads
 // (s_load) into SGPRs, shared by the 64 lanes — not one LDS read per lane and FMA.
 template <int DT, int NP, int VEC, int MODE, class Loader>
-__device__ __forceinline__ void coord_body(const Loader& load, int n, int f, int beta, const float* __restrict__ W,
-                                           int t, uint64_t seed, uint64_t thr, int64_t x, float (&res)[VEC]) {
-  float v[NP][VEC];
-  float first[VEC];
+__device__ __forceinline__ void coord_gather(const Loader& load, int n, const float* __restrict__ W, int t,
+                                             float (&v)[NP][VEC]) {
   if constexpr (MODE == kBulyanTail) {
 #pragma unroll
     for (int k = 0; k < NP; ++k)
@@ -77,7 +75,12 @@ __device__ __forceinline__ void coord_body(const Loader& load, int n, int f, int
       }
     }
   }
+}
 
+template <int NP, int VEC, int MODE>
+__device__ __forceinline__ void coord_reduce(float (&v)[NP][VEC], int n, int f, int beta, int t,
+                                             uint64_t seed, uint64_t thr, int64_t x, float (&res)[VEC]) {
+  float first[VEC];
   if constexpr (MODE == kAverageNan) {
 #pragma unroll
     for (int c = 0; c < VEC; ++c) {
@@ -148,6 +151,14 @@ __device__ __forceinline__ void coord_body(const Loader& load, int n, int f, int
   }
 }
 
+template <int DT, int NP, int VEC, int MODE, class Loader>
+__device__ __forceinline__ void coord_body(const Loader& load, int n, int f, int beta, const float* __restrict__ W,
+                                           int t, uint64_t seed, uint64_t thr, int64_t x, float (&res)[VEC]) {
+  float v[NP][VEC];
+  coord_gather<DT, NP, VEC, MODE>(load, n, W, t, v);
+  coord_reduce<NP, VEC, MODE>(v, n, f, beta, t, seed, thr, x, res);
+}
+
 template <int DT, int NP, int VEC, int MODE>
 __global__ __launch_bounds__(256) void k_coordwise(RowTable rows, int n, int64_t d, int f, int beta,
                                                    const float* __restrict__ W, int t, uint64_t seed,
@@ -181,6 +192,24 @@ __global__ __launch_bounds__(256) void k_coordwise_lds(RowTable rows, int n, int
   constexpr int ESZ = (DT == kF32) ? 4 : 2;
   constexpr int CPR = kCoordTile * ESZ / 16;  // 16-byte chunks per tile row
   __shared__ __align__(16) unsigned char tile[NP * kCoordTile * ESZ];
+  // Bulyan tail: W [t][n] compacted once per workgroup into per-row index lists
+  // (uniform trip counts, one LDS read per selected gradient) + the row scale.
+  __shared__ uint8_t sel[(MODE == kBulyanTail) ? NP * NP : 1];
+  __shared__ int selcnt[(MODE == kBulyanTail) ? NP : 1];
+  __shared__ float selscale[(MODE == kBulyanTail) ? NP : 1];
+  if constexpr (MODE == kBulyanTail) {
+    for (int k = threadIdx.x; k < t; k += blockDim.x) {
+      int c = 0;
+      float sc = 0.f;
+      for (int j = 0; j < n; ++j) {
+        const float w = W[k * n + j];
+        if (w != 0.f) { sel[k * NP + c] = static_cast<uint8_t>(j); ++c; sc = w; }
+      }
+      selcnt[k] = c;
+      selscale[k] = sc;  // uniform weights 1/(m-k) per row
+    }
+    __syncthreads();
+  }
   const int64_t ntiles = d / kCoordTile;
   const int nrows = (MODE == kBulyanTail) ? n : (n < NP ? n : NP);
   for (int64_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
@@ -193,7 +222,29 @@ __global__ __launch_bounds__(256) void k_coordwise_lds(RowTable rows, int n, int
     __syncthreads();
     const int col = threadIdx.x;
     float res[1];
-    coord_body<DT, NP, 1, MODE>(LdsLoader<DT>{tile, kCoordTile, col}, n, f, beta, W, t, seed, thr, x0 + col, res);
+    if constexpr (MODE == kBulyanTail) {
+      const LdsLoader<DT> load{tile, kCoordTile, col};
+      float v[NP][1];
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        float acc = 0.f;
+        if (k < t) {
+          const int cnt = selcnt[k];
+          for (int c = 0; c < cnt; ++c) {
+            float g[1];
+            load(sel[k * NP + c], g);
+            acc += g[0];
+          }
+          acc = sanitize_inf(acc * selscale[k]);
+        } else {
+          acc = kInf;
+        }
+        v[k][0] = acc;
+      }
+      coord_reduce<NP, 1, MODE>(v, n, f, beta, t, seed, thr, x0 + col, res);
+    } else {
+      coord_body<DT, NP, 1, MODE>(LdsLoader<DT>{tile, kCoordTile, col}, n, f, beta, W, t, seed, thr, x0 + col, res);
+    }
     store_one(out, out_dt, x0 + col, res[0]);
     __syncthreads();
   }

@@ -55,7 +55,7 @@ def test_krum_selection_and_output(cuda, n, f, dtype):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("n,f", [(7, 1), (11, 2), (15, 3), (23, 5), (31, 7)])
+@pytest.mark.parametrize("n,f", [(7, 1), (11, 2), (15, 3), (23, 5), (31, 7), (40, 1), (64, 3)])
 def test_bulyan(cuda, n, f, dtype):
     X = separated(n, 1500, dtype, cuda, seed=100 + n)
     W = gar.bulyan_weights(X, f).cpu()
