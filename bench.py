@@ -56,6 +56,7 @@ def parse():
                    help="also time the same job with the 'average' GAR and report the Krum overhead")
     p.add_argument("--cudnn-benchmark", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="disable per-worker HIP graph capture (eager launches)")
+    p.add_argument("--phases", action="store_true", help="report per-phase device time (compute / exchange / GAR)")
     p.add_argument("--lr", type=float, default=0.01,
                    help="0.01: the reference lr (0.2) diverges from random init on the synthetic data")
     return p.parse_args()
@@ -101,7 +102,7 @@ def main():
     xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
     cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                        weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
-                       cuda_graph=not a.no_graph)
+                       cuda_graph=not a.no_graph, profile_phases=a.phases)
     eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
     batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
                                 seed=1000 + ctx.rank, channels_last=a.channels_last)
@@ -111,6 +112,11 @@ def main():
     value = imgs / elapsed
     ms = 1000.0 * elapsed / a.steps
     extra = {}
+    if a.phases:
+        eng.timer.reset()
+        for _ in range(3):
+            eng.step(batches)
+        extra["phase_ms"] = {k: round(v, 3) for k, v in eng.phase_times().items()}
     if a.overhead:
         cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                                weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,

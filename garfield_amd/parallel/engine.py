@@ -37,6 +37,7 @@ from garfield_amd.ops import gar
 from garfield_amd.parallel.comm import DistContext, all_gather_rows
 from garfield_amd.runtime.attacks import NEEDS_ESTIMATES, apply_attack
 from garfield_amd.utils.flat import FlatParams
+from garfield_amd.utils.profiling import PhaseTimer
 
 # MIOpen's CK grouped-conv backward-weight solver is not HIP-graph-replay safe on
 # ROCm 7 / gfx950: from the second replay of a captured backward it leaves whole
@@ -69,6 +70,7 @@ class EngineConfig:
     seed: int = 1234
     cuda_graph: bool = False          # capture the whole step in a HIP graph after one eager step
     drop_bn_counters: bool = True     # BatchNorm num_batches_tracked += 1 is a launch per BN per worker
+    profile_phases: bool = False      # HIP-event timers: compute / exchange / gar_update (see phase_times())
 
 
 class RobustDataParallel:
@@ -110,6 +112,7 @@ class RobustDataParallel:
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(cfg.seed + 7919 * self.rank)
         self._check_gar()
+        self.timer = PhaseTimer(self.device, cfg.profile_phases)
         self._graph = None
         self._graph_failed = False
         self._static = None
@@ -268,9 +271,15 @@ class RobustDataParallel:
             p.add_(g, alpha=-cfg.lr)
 
     def _eager_step(self, batches) -> torch.Tensor:
-        losses = self.compute_local(batches)
-        self.aggregate_and_update()
+        with self.timer.phase("compute+exchange"):
+            losses = self.compute_local(batches)
+        with self.timer.phase("gar_update"):
+            self.aggregate_and_update()
         return torch.stack(losses).float().mean()
+
+    def phase_times(self) -> dict:
+        """Mean ms per step of each phase (needs ``profile_phases=True``)."""
+        return self.timer.summary()
 
     def graph_capturable(self) -> bool:
         random_attacks = {"random", "drop"} & set(self.cfg.byzantine.values())
@@ -295,18 +304,21 @@ class RobustDataParallel:
             if self._graph is None:
                 return self._eager_step(batches)
         works = []
-        for j in self.local_slots:
-            sx, sy = self._static[j]
-            x, y = batches[j]
-            if x.data_ptr() != sx.data_ptr():
-                sx.copy_(x, non_blocking=True)
-                sy.copy_(y, non_blocking=True)
-            self._graph[j].replay()
-            if self.world > 1:
-                works.append(all_gather_rows(self.X[j], self.rank, async_op=True))
-        for w in works:
-            w.wait()
-        self.aggregate_and_update()
+        with self.timer.phase("compute"):
+            for j in self.local_slots:
+                sx, sy = self._static[j]
+                x, y = batches[j]
+                if x.data_ptr() != sx.data_ptr():
+                    sx.copy_(x, non_blocking=True)
+                    sy.copy_(y, non_blocking=True)
+                self._graph[j].replay()
+                if self.world > 1:
+                    works.append(all_gather_rows(self.X[j], self.rank, async_op=True))
+        with self.timer.phase("exchange_wait"):
+            for w in works:
+                w.wait()
+        with self.timer.phase("gar_update"):
+            self.aggregate_and_update()
         return self._static_loss.mean()
 
     def _worker_body(self, j: int, x, y, loss_out: torch.Tensor) -> None:

@@ -118,34 +118,79 @@ class Server:
         with self.lock:
             return self.flat.reference_vector().to("cpu")
 
-    def _pack(self, grads: list) -> list:
-        """Copy received flat gradients into one aligned [n, ld] device buffer; return row views."""
+    def _pack(self, grads: list, blocking: bool = False) -> list:
+        """Copy received flat gradients into one aligned [n, ld] device buffer; return row views.
+
+        ``blocking``: the sources are mailbox slots that RPC threads may rewrite as soon
+        as this returns, so the host waits for the DMA."""
         n = len(grads)
         d = grads[0].numel()
         ld = padded(d)
         if self._gbuf is None or self._gbuf.shape[0] < n or self._gbuf.shape[1] != ld:
             self._gbuf = torch.zeros((max(n, self.num_workers), ld), dtype=torch.float32, device=self.device)
         for i, g in enumerate(grads):
-            self._gbuf[i, :d].copy_(g, non_blocking=True)
+            self._gbuf[i, :d].copy_(g, non_blocking=not blocking)
         return [self._gbuf[i, :d] for i in range(n)]
+
+    def _mailbox(self, d: int):
+        """Pinned C++ inbox with one slot per worker (created on first use)."""
+        mb = getattr(self, "_mb", None)
+        if mb is None or mb.slot_bytes < 4 * d:
+            from garfield_amd import _native
+
+            C = _native.native()
+            mb = C.Mailbox(self.num_workers, 4 * d, self.device.type == "cuda")
+            self._mb = mb
+        return mb
 
     def get_gradients(self, iter_num, num_wait_wrk=-1):
         """Ask every worker for a gradient on the current model; return the first
-        ``num_wait_wrk`` (default n - f) received, on the server's device."""
+        ``num_wait_wrk`` (default n - f) received, on the server's device.
+
+        Replies land in the native pinned ``Mailbox`` (RPC threads copy into slot i
+        without the GIL, tagged with the iteration); the server blocks in C++ until
+        ``num_wait_wrk`` slots carry this iteration's tag, then DMAs exactly those
+        slots into the aligned device buffer. Late replies of older iterations can
+        never be mistaken for current ones (tag mismatch)."""
         if num_wait_wrk < 0:
             num_wait_wrk = self.num_workers - self.byz_wrk
         self.model.train()
         self.optimizer.zero_grad(set_to_none=False)
         payload = self._payload()
-        q = _Quorum(self.num_workers)
+        d = self.flat.d
+        try:
+            mb = self._mailbox(d)
+        except RuntimeError:
+            mb = None  # native extension unavailable (CPU-only fallback)
+        if mb is None:
+            q = _Quorum(self.num_workers)
+            for i, (rref, typ) in enumerate(zip(self.workers_rref, self.workers_types)):
+                _remote_method_async(typ.compute_gradients, rref, iter_num, payload).then(q.callback(i, lambda r: r[1]))
+            grads = q.wait(num_wait_wrk, self.rpc_timeout)
+            self.build_graph(iter_num)
+            return self._pack(grads)
+        errors = []
+
+        def make_cb(slot):
+            def cb(fut):
+                try:
+                    mb.write(slot, iter_num, fut.wait()[1])
+                except Exception as e:  # surface remote failures
+                    errors.append(e)
+                    mb.publish(slot, -2)
+            return cb
+
         for i, (rref, typ) in enumerate(zip(self.workers_rref, self.workers_types)):
-            fut = _remote_method_async(typ.compute_gradients, rref, iter_num, payload)
-            fut.then(q.callback(i, lambda r: r[1]))
-        build = threading.Thread(target=self.build_graph, args=(iter_num,))
-        build.start()
-        grads = q.wait(num_wait_wrk, self.rpc_timeout)
-        build.join()
-        return self._pack(grads)
+            _remote_method_async(typ.compute_gradients, rref, iter_num, payload).then(make_cb(i))
+        self.build_graph(iter_num)   # overlaps the workers' computation
+        timeout = -1.0 if self.rpc_timeout is None else float(self.rpc_timeout)
+        slots = mb.wait(iter_num, num_wait_wrk, timeout)
+        if len(slots) < num_wait_wrk:
+            if errors:
+                raise errors[0]
+            raise TimeoutError(f"only {len(slots)} of {num_wait_wrk} gradients arrived for iteration {iter_num}")
+        slots = slots[:num_wait_wrk]
+        return self._pack([mb.tensor(i, d, torch.float32) for i in slots], blocking=True)
 
     def get_models(self, num_wait_ps=-1):
         if num_wait_ps < 0:
