@@ -127,6 +127,20 @@ def build(verbose: bool = False, force: bool = False) -> Path:
     return out
 
 
+def build_selftest(sanitizer: str = "thread", out_dir: Path | None = None) -> Path:
+    """Host-only native self-test (thread pool, CPU GARs, mailbox) built with
+    ``-fsanitize=<sanitizer>`` (thread | address | undefined). GPU sanitizers are not
+    used: the sanitizer flags only ever reach host code (no HIP in this binary)."""
+    out_dir = out_dir or BUILD
+    out_dir.mkdir(parents=True, exist_ok=True)
+    exe = out_dir / f"selftest_{sanitizer}"
+    srcs = [CSRC / "selftest.cpp", CSRC / "threadpool.cpp", CSRC / "gar_cpu.cpp", CSRC / "mailbox.cpp"]
+    cmd = ["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer",
+           "-DGARFIELD_NO_TORCH", "-DGARFIELD_NO_HIP", f"-I{CSRC}", *map(str, srcs), "-o", str(exe), "-pthread"]
+    _run(cmd, False)
+    return exe
+
+
 if __name__ == "__main__":
     p = build(verbose="-v" in sys.argv, force="--force" in sys.argv)
     print(p)

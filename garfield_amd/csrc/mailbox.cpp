@@ -1,7 +1,11 @@
 #include "mailbox.hpp"
 
+#ifndef GARFIELD_NO_HIP
 #include <hip/hip_runtime.h>
+#endif
+#ifndef GARFIELD_NO_TORCH
 #include <torch/extension.h>
+#endif
 
 #include <algorithm>
 #include <chrono>
@@ -18,6 +22,7 @@ Mailbox::Mailbox(size_t nslots, size_t slot_bytes, bool pinned)
       tags_(nslots, -1), stamp_(nslots, 0) {
   if (nslots == 0) throw std::invalid_argument("mailbox: nslots must be > 0");
   const size_t total = stride_ * nslots_ + 256;
+#ifndef GARFIELD_NO_HIP
   if (pinned_) {
     if (hipHostMalloc(&base_, total, hipHostMallocDefault) != hipSuccess) {
       (void)hipGetLastError();
@@ -25,6 +30,9 @@ Mailbox::Mailbox(size_t nslots, size_t slot_bytes, bool pinned)
       pinned_ = false;  // no device / no driver: fall back to pageable memory
     }
   }
+#else
+  pinned_ = false;
+#endif
   if (!base_) {
     base_ = std::aligned_alloc(256, ((total + 255) / 256) * 256);
     if (!base_) throw std::bad_alloc();
@@ -32,8 +40,13 @@ Mailbox::Mailbox(size_t nslots, size_t slot_bytes, bool pinned)
 }
 
 Mailbox::~Mailbox() {
-  if (pinned_) (void)hipHostFree(base_);
-  else std::free(base_);
+#ifndef GARFIELD_NO_HIP
+  if (pinned_) {
+    (void)hipHostFree(base_);
+    return;
+  }
+#endif
+  std::free(base_);
 }
 
 void Mailbox::write(size_t i, int64_t tag, const void* src, size_t bytes) {
@@ -95,6 +108,7 @@ void Mailbox::clear() {
   std::fill(tags_.begin(), tags_.end(), -1);
 }
 
+#ifndef GARFIELD_NO_TORCH
 void bind(pybind11::module_& m) {
   namespace py = pybind11;
   py::class_<Mailbox, std::shared_ptr<Mailbox>>(m, "Mailbox",
@@ -135,6 +149,8 @@ void bind(pybind11::module_& m) {
            py::arg("slot"), py::arg("numel"), py::arg("dtype"),
            "Zero-copy host view of slot i (valid while the mailbox lives)");
 }
+
+#endif  // GARFIELD_NO_TORCH
 
 }  // namespace mailbox
 }  // namespace garfield
