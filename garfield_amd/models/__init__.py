@@ -30,6 +30,9 @@ _REGISTRY = {
     "resnet50": ("resnet", "imagenet_resnet", {"depth": 50}),
     "resnet101": ("resnet", "imagenet_resnet", {"depth": 101}),
     "resnet152": ("resnet", "imagenet_resnet", {"depth": 152}),
+    "resnet200": ("resnet", "imagenet_resnet", {"depth": 200}),
+    "inception_v3": ("inception", "InceptionV3", {}),
+    "inception": ("inception", "InceptionV3", {}),
     "preactresnet18": ("zoo", "PreActResNet18", {}),
     "googlenet": ("zoo", "GoogLeNet", {}),
     "densenet121": ("zoo", "DenseNet121", {}),

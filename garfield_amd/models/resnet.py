@@ -99,7 +99,8 @@ class ResNet(nn.Module):
 
 
 _CFG = {18: (BasicBlock, [2, 2, 2, 2]), 34: (BasicBlock, [3, 4, 6, 3]), 50: (Bottleneck, [3, 4, 6, 3]),
-        101: (Bottleneck, [3, 4, 23, 3]), 152: (Bottleneck, [3, 8, 36, 3])}
+        101: (Bottleneck, [3, 4, 23, 3]), 152: (Bottleneck, [3, 8, 36, 3]),
+        200: (Bottleneck, [3, 24, 36, 3])}
 
 
 def imagenet_resnet(depth: int, num_classes: int = 1000) -> ResNet:
