@@ -56,6 +56,10 @@ def parse():
                    help="also time the same job with the 'average' GAR and report the Krum overhead")
     p.add_argument("--cudnn-benchmark", action="store_true")
     p.add_argument("--no-graph", action="store_true", help="disable per-worker HIP graph capture (eager launches)")
+    p.add_argument("--no-lp-weights", action="store_true",
+                   help="autocast casts every conv/linear weight per worker instead of bf16 working weights")
+    p.add_argument("--ref-impl", action="store_true",
+                   help="also time the reference's algorithms run as-is (BASELINE.md (a)) and report the speedup")
     p.add_argument("--phases", action="store_true", help="report per-phase device time (compute / exchange / GAR)")
     p.add_argument("--lr", type=float, default=0.01,
                    help="0.01: the reference lr (0.2) diverges from random init on the synthetic data")
@@ -69,6 +73,8 @@ def timed_steps(eng, batches, steps, warmup, ctx):
         torch.cuda.synchronize()
     ctx.barrier()
     if ctx.device.type == "cuda":
+        if os.environ.get("GARFIELD_TRACE_MARK"):
+            torch.cuda._sleep(1000)  # marker kernel: scripts/trace_summary.py keeps what follows
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -102,7 +108,7 @@ def main():
     xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
     cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                        weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
-                       cuda_graph=not a.no_graph, profile_phases=a.phases)
+                       cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=not a.no_lp_weights)
     eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
     batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
                                 seed=1000 + ctx.rank, channels_last=a.channels_last)
@@ -120,13 +126,24 @@ def main():
     if a.overhead:
         cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                                weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
-                               cuda_graph=not a.no_graph)
+                               cuda_graph=not a.no_graph, lp_weights=not a.no_lp_weights)
         torch.manual_seed(1234)
         eng_avg = RobustDataParallel(build_model(a.model, num_classes=num_classes), F.cross_entropy, ctx, cfg_avg)
         e_avg, _ = timed_steps(eng_avg, batches, a.steps, a.warmup, ctx)
         ms_avg = 1000.0 * e_avg / a.steps
-        extra = {"avg_ms_per_step": round(ms_avg, 3),
-                 "gar_overhead_pct_vs_average": round(100.0 * (ms - ms_avg) / ms_avg, 3)}
+        extra.update({"avg_ms_per_step": round(ms_avg, 3),
+                      "gar_overhead_pct_vs_average": round(100.0 * (ms - ms_avg) / ms_avg, 3)})
+    if a.ref_impl and ctx.world_size == 1:
+        from garfield_amd.parallel.refimpl import ReferenceStyleDP
+
+        torch.manual_seed(1234)
+        ref = ReferenceStyleDP(build_model(a.model, num_classes=num_classes), F.cross_entropy, ctx.device,
+                               a.workers_per_gpu, a.f, a.lr, gar=a.gar if a.gar in ("krum", "average") else "krum")
+        e_ref, _ = timed_steps(ref, batches, a.steps, a.warmup, ctx)
+        ms_ref = 1000.0 * e_ref / a.steps
+        extra["ref_impl_ms_per_step"] = round(ms_ref, 3)
+        extra["ref_impl_img_per_s"] = round(n * a.batch / (ms_ref / 1000.0), 2)
+        extra["speedup_vs_ref_impl"] = round(ms_ref / ms, 3)
     if ctx.rank == 0:
         out = {
             "metric": "img/sec ResNet-50 f=2 Multi-Krum",
@@ -152,6 +169,7 @@ def main():
                 "batch_per_worker": a.batch,
                 "exchange_dtype": a.exchange_dtype,
                 "hip_graphs": bool(getattr(eng, "_graph", None)),
+                "lp_weights": eng._shadow is not None,
                 "optimizer": f"SGD lr={a.lr} momentum=0.9 wd=5e-4 (fused into the GAR combine kernel)",
             },
             "final_loss": round(loss, 4),

@@ -138,8 +138,8 @@ void g_combine(const RowSet& rs, const at::Tensor& weights, const at::Tensor& ou
 }
 
 void g_combine_sgd(const RowSet& rs, const at::Tensor& weights, const at::Tensor& param, const at::Tensor& mom,
-                   const c10::optional<at::Tensor>& grad_out, double lr, double momentum, double dampening,
-                   double weight_decay, bool nesterov, bool first_step) {
+                   const c10::optional<at::Tensor>& grad_out, const c10::optional<at::Tensor>& shadow, double lr,
+                   double momentum, double dampening, double weight_decay, bool nesterov, bool first_step) {
   check_gpu(rs);
   c10::hip::HIPGuard guard(rs.device.index());
   TORCH_CHECK(param.numel() == rs.d && mom.numel() == rs.d, "garfield: parameter/momentum size mismatch");
@@ -148,9 +148,21 @@ void g_combine_sgd(const RowSet& rs, const at::Tensor& weights, const at::Tensor
     TORCH_CHECK(grad_out->numel() == rs.d, "garfield: grad_out size mismatch");
     g = fptr(*grad_out);
   }
+  void* sh = nullptr;
+  int sh_dt = garfield::kBF16;
+  if (shadow.has_value() && shadow->defined()) {
+    TORCH_CHECK(shadow->is_cuda() && shadow->device() == param.device() && shadow->is_contiguous(),
+                "garfield: shadow must be a contiguous tensor on the parameters' device");
+    TORCH_CHECK(shadow->numel() >= rs.d, "garfield: shadow too small");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(shadow->data_ptr()) % 16 == 0, "garfield: shadow must be 16-byte aligned");
+    sh_dt = dtype_code(*shadow);
+    TORCH_CHECK(sh_dt == garfield::kBF16 || sh_dt == garfield::kF16 || sh_dt == garfield::kF32,
+                "garfield: shadow dtype must be bf16, fp16 or fp32");
+    sh = shadow->data_ptr();
+  }
   garfield::gpu::SgdArgs a{static_cast<float>(lr), static_cast<float>(momentum), static_cast<float>(dampening),
                            static_cast<float>(weight_decay), nesterov ? 1 : 0, first_step ? 1 : 0};
-  garfield::gpu::combine_sgd(rs.table, rs.n, rs.d, rs.dt, fptr(weights), fptr(param), fptr(mom), g, a,
+  garfield::gpu::combine_sgd(rs.table, rs.n, rs.d, rs.dt, fptr(weights), fptr(param), fptr(mom), g, sh, sh_dt, a,
                              stream_of(rs.device));
 }
 
@@ -317,14 +329,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "out = Σ_j w_j g_j");
   def_rows(m, "gpu_combine_sgd",
            [](const at::Tensor& G, const at::Tensor& w, const at::Tensor& p, const at::Tensor& b,
-              const c10::optional<at::Tensor>& go, double lr, double mo, double da, double wd, bool ne, bool first) {
-             g_combine_sgd(rows_from_2d(G, true), w, p, b, go, lr, mo, da, wd, ne, first);
+              const c10::optional<at::Tensor>& go, const c10::optional<at::Tensor>& sh, double lr, double mo, double da,
+              double wd, bool ne, bool first) {
+             g_combine_sgd(rows_from_2d(G, true), w, p, b, go, sh, lr, mo, da, wd, ne, first);
            },
            [](const std::vector<at::Tensor>& L, const at::Tensor& w, const at::Tensor& p, const at::Tensor& b,
-              const c10::optional<at::Tensor>& go, double lr, double mo, double da, double wd, bool ne, bool first) {
-             g_combine_sgd(rows_from_list(L, true), w, p, b, go, lr, mo, da, wd, ne, first);
+              const c10::optional<at::Tensor>& go, const c10::optional<at::Tensor>& sh, double lr, double mo, double da,
+              double wd, bool ne, bool first) {
+             g_combine_sgd(rows_from_list(L, true), w, p, b, go, sh, lr, mo, da, wd, ne, first);
            },
-           "Fused robust combine + SGD(momentum, dampening, weight decay, nesterov) on fp32 master weights");
+           "Fused robust combine + SGD(momentum, dampening, weight decay, nesterov) on fp32 master weights; "
+           "args (G, w, param, mom, grad_out|None, shadow|None, lr, momentum, dampening, weight_decay, nesterov, "
+           "first_step); shadow receives a bf16/fp16 copy of the updated parameters");
   def_rows(m, "gpu_coordwise",
            [](const at::Tensor& G, int mode, int f, int beta, const c10::optional<at::Tensor>& W, int t, uint64_t seed,
               double p, const at::Tensor& o) { g_coordwise(rows_from_2d(G, true), mode, f, beta, W, t, seed, p, o); },
@@ -340,21 +356,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     TORCH_CHECK(!srcs.empty(), "flatten_cast: empty tensor list");
     TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "flatten_cast: dst must be a contiguous device tensor");
     c10::hip::HIPGuard guard(dst.device().index());
-    std::vector<const float*> ptrs;
+    std::vector<const void*> ptrs;
+    std::vector<int> dts;
     std::vector<int64_t> numels, offs;
     int64_t pos = 0;
     for (const auto& t : srcs) {
-      TORCH_CHECK(t.scalar_type() == at::kFloat && t.device() == dst.device(), "flatten_cast: fp32 sources on dst's device");
+      const auto st = t.scalar_type();
+      TORCH_CHECK((st == at::kFloat || st == at::kBFloat16 || st == at::kHalf) && t.device() == dst.device(),
+                  "flatten_cast: fp32/bf16/fp16 sources on dst's device");
       TORCH_CHECK(t.is_non_overlapping_and_dense(), "flatten_cast: sources must be dense");
-      ptrs.push_back(t.data_ptr<float>());
+      ptrs.push_back(t.data_ptr());
+      dts.push_back(dtype_code(t));
       numels.push_back(t.numel());
       offs.push_back(pos);
       pos += t.numel();
     }
     TORCH_CHECK(pos <= dst.numel(), "flatten_cast: destination too small (", dst.numel(), " < ", pos, ")");
-    return garfield::gpu::flatten_cast(ptrs.data(), numels.data(), offs.data(), static_cast<int>(ptrs.size()),
-                                       dst.data_ptr(), dtype_code(dst), stream_of(dst.device()));
-  }, "Copy a list of dense fp32 tensors (memory order) back to back into dst, casting to dst's dtype");
+    return garfield::gpu::flatten_cast(ptrs.data(), dts.data(), numels.data(), offs.data(),
+                                       static_cast<int>(ptrs.size()), dst.data_ptr(), dtype_code(dst),
+                                       stream_of(dst.device()));
+  }, "Copy a list of dense fp32/bf16/fp16 tensors (memory order) back to back into dst, casting to dst's dtype");
 
   // CPU building blocks (thread pool)
   def_rows(m, "cpu_pairwise",

@@ -90,7 +90,7 @@ template <int DT>
 __global__ __launch_bounds__(256) void k_combine_sgd(RowTable rows, int n, int64_t d,
                                                      const float* __restrict__ weights, float* __restrict__ param,
                                                      float* __restrict__ mom, float* __restrict__ grad_out,
-                                                     SgdArgs args) {
+                                                     void* __restrict__ shadow, int shadow_dt, SgdArgs args) {
   __shared__ int sel[kMaxRows];
   __shared__ float wsel[kMaxRows];
   const int cnt = compact_selection(weights, n, sel, wsel);
@@ -111,6 +111,7 @@ __global__ __launch_bounds__(256) void k_combine_sgd(RowTable rows, int n, int64
     for (int c = 0; c < 8; ++c) sgd_apply(acc[c], pv[c], bv[c], args);
     *reinterpret_cast<float4*>(param + x) = make_float4(pv[0], pv[1], pv[2], pv[3]);
     *reinterpret_cast<float4*>(param + x + 4) = make_float4(pv[4], pv[5], pv[6], pv[7]);
+    if (shadow) store_vec<8>(shadow, shadow_dt, x, pv);
     if (args.momentum != 0.f) {
       *reinterpret_cast<float4*>(mom + x) = make_float4(bv[0], bv[1], bv[2], bv[3]);
       *reinterpret_cast<float4*>(mom + x + 4) = make_float4(bv[4], bv[5], bv[6], bv[7]);
@@ -124,6 +125,7 @@ __global__ __launch_bounds__(256) void k_combine_sgd(RowTable rows, int n, int64
       float b = (args.momentum != 0.f && !args.first_step) ? mom[x] : 0.f;
       sgd_apply(g, p, b, args);
       param[x] = p;
+      if (shadow) store_one(shadow, shadow_dt, x, p);
       if (args.momentum != 0.f) mom[x] = b;
     }
   }
@@ -213,8 +215,9 @@ template <int DT> struct Combine {
 };
 template <int DT> struct CombineSgd {
   static void run(const RowTable& rows, int n, int64_t d, const float* w, float* param, float* mom,
-                  float* gout, SgdArgs a, hipStream_t s) {
-    hipLaunchKernelGGL(k_combine_sgd<DT>, dim3(combine_grid(d)), dim3(256), 0, s, rows, n, d, w, param, mom, gout, a);
+                  float* gout, void* shadow, int shadow_dt, SgdArgs a, hipStream_t s) {
+    hipLaunchKernelGGL(k_combine_sgd<DT>, dim3(combine_grid(d)), dim3(256), 0, s, rows, n, d, w, param, mom, gout,
+                       shadow, shadow_dt, a);
   }
 };
 }  // namespace
@@ -225,8 +228,9 @@ void combine(const RowTable& rows, int n, int64_t d, int dt, const float* weight
 }
 
 void combine_sgd(const RowTable& rows, int n, int64_t d, int dt, const float* weights, float* param,
-                 float* momentum_buf, float* grad_out, SgdArgs args, hipStream_t stream) {
-  by_dtype<CombineSgd>(dt, rows, n, d, weights, param, momentum_buf, grad_out, args, stream);
+                 float* momentum_buf, float* grad_out, void* shadow, int shadow_dt, SgdArgs args,
+                 hipStream_t stream) {
+  by_dtype<CombineSgd>(dt, rows, n, d, weights, param, momentum_buf, grad_out, shadow, shadow_dt, args, stream);
 }
 
 // ---------------------------------------------------------------------------

@@ -1,6 +1,6 @@
 // Multi-tensor flatten + cast: scatter-free copy of a model's per-parameter
-// gradients (fp32, each its own allocation) into one row of the gradient
-// exchange buffer (bf16 / fp16 / fp32), in ONE launch.
+// gradients (fp32 / bf16 / fp16 per tensor, each its own allocation) into one row
+// of the gradient exchange buffer (bf16 / fp16 / fp32), in ONE launch.
 //
 // Reference counterpart: `torch.cat([p.grad.view(-1) ...]).to("cpu")` in
 // garfieldpp/worker.py:93-94 (one concat kernel + a D2H copy per worker per step).
@@ -16,16 +16,35 @@ namespace {
 constexpr int kChunk = 4096;  // elements per workgroup (256 threads x 16)
 
 struct FlatTable {
-  const float* src[kMaxFlatTensors];
+  const void* src[kMaxFlatTensors];
   int64_t numel[kMaxFlatTensors];
   int64_t dst_off[kMaxFlatTensors];
   int32_t chunk_start[kMaxFlatTensors + 1];  // prefix sum of chunks per tensor
+  int8_t src_dt[kMaxFlatTensors];            // kF32 / kBF16 / kF16 per source tensor
   int count;
 };
 
 template <int ODT>
 __device__ __forceinline__ void store8(void* dst, int64_t x, const float (&v)[8]) {
   store_vec<8>(dst, ODT, x, v);
+}
+
+template <int SDT, int ODT>
+__device__ __forceinline__ void copy_chunk(const void* __restrict__ src, void* __restrict__ dst, int64_t off,
+                                           int64_t c0, int64_t c1) {
+  // 8-element vectors: 2×16 B (fp32) or 16 B (16-bit) loads, both need a 16 B aligned source
+  const bool vec = ((off & 7) == 0) && ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
+  if (vec) {
+    const int64_t v_end = c0 + ((c1 - c0) / 8) * 8;
+    for (int64_t x = c0 + threadIdx.x * 8; x < v_end; x += 256 * 8) {
+      float v[8];
+      load_vec<SDT, 8>(src, x, v);
+      store8<ODT>(dst, off + x, v);
+    }
+    for (int64_t x = v_end + threadIdx.x; x < c1; x += 256) store_one(dst, ODT, off + x, load_one<SDT>(src, x));
+  } else {
+    for (int64_t x = c0 + threadIdx.x; x < c1; x += 256) store_one(dst, ODT, off + x, load_one<SDT>(src, x));
+  }
 }
 
 template <int ODT>
@@ -37,28 +56,19 @@ __global__ __launch_bounds__(256) void k_flatten_cast(FlatTable t, void* __restr
   const int64_t c0 = static_cast<int64_t>(b - t.chunk_start[ti]) * kChunk;
   const int64_t numel = t.numel[ti];
   const int64_t off = t.dst_off[ti];
-  const float* __restrict__ src = t.src[ti];
   int64_t c1 = c0 + kChunk;
   if (c1 > numel) c1 = numel;
-  const bool vec = ((off & 7) == 0) && ((reinterpret_cast<uintptr_t>(src) & 15) == 0);
-  if (vec) {
-    const int64_t v_end = c0 + ((c1 - c0) / 8) * 8;
-    for (int64_t x = c0 + threadIdx.x * 8; x < v_end; x += 256 * 8) {
-      const float4 a = *reinterpret_cast<const float4*>(src + x);
-      const float4 c = *reinterpret_cast<const float4*>(src + x + 4);
-      const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-      store8<ODT>(dst, off + x, v);
-    }
-    for (int64_t x = v_end + threadIdx.x; x < c1; x += 256) store_one(dst, ODT, off + x, src[x]);
-  } else {
-    for (int64_t x = c0 + threadIdx.x; x < c1; x += 256) store_one(dst, ODT, off + x, src[x]);
+  switch (t.src_dt[ti]) {
+    case kBF16: copy_chunk<kBF16, ODT>(t.src[ti], dst, off, c0, c1); break;
+    case kF16: copy_chunk<kF16, ODT>(t.src[ti], dst, off, c0, c1); break;
+    default: copy_chunk<kF32, ODT>(t.src[ti], dst, off, c0, c1); break;
   }
 }
 
 }  // namespace
 
-int flatten_cast(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int count, void* dst,
-                 int out_dt, hipStream_t stream) {
+int flatten_cast(const void* const* srcs, const int* src_dts, const int64_t* numels, const int64_t* offsets,
+                 int count, void* dst, int out_dt, hipStream_t stream) {
   int launched = 0;
   for (int base = 0; base < count; base += kMaxFlatTensors) {
     FlatTable t{};
@@ -68,6 +78,7 @@ int flatten_cast(const float* const* srcs, const int64_t* numels, const int64_t*
     int32_t chunks = 0;
     for (int i = 0; i < c; ++i) {
       t.src[i] = srcs[base + i];
+      t.src_dt[i] = static_cast<int8_t>(src_dts[base + i]);
       t.numel[i] = numels[base + i];
       t.dst_off[i] = offsets[base + i];
       t.chunk_start[i] = chunks;

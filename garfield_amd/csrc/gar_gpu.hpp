@@ -45,9 +45,11 @@ struct SgdArgs {
   int nesterov;
   int first_step;  // momentum buffer initialised to the gradient (torch.optim.SGD)
 };
+// shadow (optional): low-precision copy of the updated parameters (bf16/f16
+// working weights of the forward/backward), written in the same pass.
 void combine_sgd(const RowTable& rows, int n, int64_t d, int dt, const float* weights,
-                 float* param, float* momentum_buf, float* grad_out, SgdArgs args,
-                 hipStream_t stream);
+                 float* param, float* momentum_buf, float* grad_out, void* shadow, int shadow_dt,
+                 SgdArgs args, hipStream_t stream);
 
 // ---- Coordinate-wise rules (median, trimmed mean, MeaMed, ...) -------------
 // W/t are only read for kBulyanTail; seed/threshold only for kCondense.
@@ -65,8 +67,8 @@ void aksel_select(const float* slabs, int grid, int n, int c, float* weights, fl
 
 // ---- Multi-tensor flatten + cast (per-parameter grads -> exchange row) -----
 constexpr int kMaxFlatTensors = 96;  // tensors per launch (kernarg budget); more => several launches
-int flatten_cast(const float* const* srcs, const int64_t* numels, const int64_t* offsets, int count, void* dst,
-                 int out_dt, hipStream_t stream);
+int flatten_cast(const void* const* srcs, const int* src_dts, const int64_t* numels, const int64_t* offsets,
+                 int count, void* dst, int out_dt, hipStream_t stream);
 
 }  // namespace gpu
 }  // namespace garfield

@@ -95,6 +95,7 @@ class ByzantinePSDataParallel(RobustDataParallel):
             all_gather_rows(self.M, self.rank)
         models = [self.M[p, : self.d] for p in range(self.num_ps)]
         self._write_mar(models)
+        self.sync_shadow()   # master weights were rewritten by the model aggregation
         self.step_count += 1
         return loss
 
@@ -117,11 +118,11 @@ class ByzantinePSDataParallel(RobustDataParallel):
                     w = torch.full((len(rows),), 1.0 / len(rows), device=self.device)
                 del kw
                 self.last_weights = w
-                C.gpu_combine_sgd(rows, w, param, mom, None, cfg.lr, cfg.momentum, cfg.dampening,
+                C.gpu_combine_sgd(rows, w, param, mom, None, None, cfg.lr, cfg.momentum, cfg.dampening,
                                   cfg.weight_decay, cfg.nesterov, first)
                 return
             g = gar.aggregate(cfg.gar, rows, **self._gar_kwargs()).float()
-            C.gpu_combine_sgd([g], self._one, param, mom, None, cfg.lr, cfg.momentum, cfg.dampening,
+            C.gpu_combine_sgd([g], self._one, param, mom, None, None, cfg.lr, cfg.momentum, cfg.dampening,
                               cfg.weight_decay, cfg.nesterov, first)
         else:
             g = gar.aggregate(cfg.gar, rows, **self._gar_kwargs()).float()

@@ -48,6 +48,7 @@ from garfield_amd.utils.profiling import PhaseTimer
 os.environ.setdefault("MIOPEN_DEBUG_GROUP_CONV_IMPLICIT_GEMM_HIP_WRW_XDLOPS", "0")
 
 WEIGHTED_RULES = {"average", "krum", "brute", "aksel"}
+_LP_MODULES = (nn.modules.conv._ConvNd, nn.Linear)
 COORD_RULES = {"median", "trimmed-mean", "averaged-median", "average-nan", "condense", "bulyan"}
 
 
@@ -71,6 +72,7 @@ class EngineConfig:
     cuda_graph: bool = False          # capture the whole step in a HIP graph after one eager step
     drop_bn_counters: bool = True     # BatchNorm num_batches_tracked += 1 is a launch per BN per worker
     profile_phases: bool = False      # HIP-event timers: compute / exchange / gar_update (see phase_times())
+    lp_weights: bool = True           # bf16/fp16 working copies of conv/linear weights, refreshed by the update kernel
 
 
 class RobustDataParallel:
@@ -92,6 +94,9 @@ class RobustDataParallel:
         if ctx.is_distributed:
             dist.broadcast(self.flat.data, src=0)
         self.d, self.ld = self.flat.d, self.flat.ld
+        self.work_params = list(self.flat.params)   # what forward/backward sees (see _install_shadow)
+        self._shadow = None
+        self._install_shadow()
         self.mom = torch.zeros(self.ld, dtype=torch.float32, device=self.device)
         self.k = cfg.workers_per_rank
         self.world = ctx.world_size
@@ -119,6 +124,49 @@ class RobustDataParallel:
         self._static_loss = None
 
     # ------------------------------------------------------------------ #
+
+    def _install_shadow(self) -> None:
+        """Low-precision working weights for the matmul-shaped layers.
+
+        Under autocast every conv/linear weight is cast fp32 → bf16 on each forward
+        and the bf16 weight gradient cast back to fp32 on each backward: two
+        elementwise kernels per layer per logical worker (~900 launches and ~4.7 ms
+        per ResNet-50 step on MI355X, see profiles/). Instead, those layers get
+        bf16 parameters that are views of one flat ``shadow`` buffer laid out like the
+        fp32 master buffer. The fused GAR update kernel writes the shadow in the same
+        pass that updates the master weights, so the forward reads bf16 directly and
+        the backward produces bf16 gradients that the flatten kernel copies into the
+        exchange row as they are. The numbers are the same as with autocast: the cast
+        is the same round-to-nearest-even, and autocast's weight gradient is the bf16
+        gradient of that cast. BatchNorm and other parameters stay fp32 views of the
+        master buffer."""
+        lp = self.cfg.autocast_dtype
+        if not (self.cfg.lp_weights and self.device.type == "cuda" and lp in (torch.bfloat16, torch.float16)):
+            return
+        index = {id(p): i for i, p in enumerate(self.flat.params)}
+        self._shadow = torch.zeros(self.ld, dtype=lp, device=self.device)
+        views = list(self.flat.views(self._shadow))
+        replaced = {}
+        for mod in self.model.modules():
+            if not isinstance(mod, _LP_MODULES):
+                continue
+            for name in ("weight", "bias"):
+                p = mod._parameters.get(name)
+                if p is None or id(p) not in index:
+                    continue
+                i = index[id(p)]
+                if id(p) not in replaced:
+                    replaced[id(p)] = nn.Parameter(views[i], requires_grad=True)
+                    self.work_params[i] = replaced[id(p)]
+                mod._parameters[name] = replaced[id(p)]
+        self.sync_shadow()
+
+    def sync_shadow(self) -> None:
+        """Refresh the low-precision working weights from the fp32 master weights
+        (only needed after the master buffer is written outside the update kernel)."""
+        if self._shadow is not None:
+            with torch.no_grad():
+                self._shadow.copy_(self.flat.data)
 
     def slot(self, j: int) -> int:
         """Global slot id (row of the [n, d] GAR input) of local worker j."""
@@ -150,7 +198,7 @@ class RobustDataParallel:
         cuda = self.device.type == "cuda"
         amp = (torch.autocast("cuda", dtype=self.cfg.autocast_dtype)
                if (self.cfg.autocast_dtype is not None and cuda) else contextlib.nullcontext())
-        params = self.flat.params
+        params = self.work_params
         with amp:
             for j in self.local_slots:
                 x, y = batches[j]
@@ -164,7 +212,7 @@ class RobustDataParallel:
                 if attack is None:
                     self._write_row(row)
                 else:
-                    g = self.flat.grads_flat(torch.empty(self.d, dtype=torch.float32, device=self.device))
+                    g = self._grad_vector()
                     est = None
                     if attack in NEEDS_ESTIMATES:
                         honest = [self.X[i, self.rank, : self.d] for i in self.local_slots
@@ -182,12 +230,18 @@ class RobustDataParallel:
     def _write_row(self, row: torch.Tensor) -> None:
         if self.device.type == "cuda":
             grads = []
-            for p in self.flat.params:
+            for p in self.work_params:
                 g = p.grad
                 grads.append(g if g is not None else torch.zeros_like(p))
-            self._C.gpu_flatten_cast(grads, row)
+            self._C.gpu_flatten_cast(grads, row)   # fp32 and bf16 sources, one launch
         else:
             self.flat.grads_flat(row)
+
+    def _grad_vector(self) -> torch.Tensor:
+        """Current local gradient as one fp32 vector (memory order)."""
+        out = torch.empty(self.d, dtype=torch.float32, device=self.device)
+        self._write_row(out)
+        return out
 
     def aggregate_and_update(self) -> None:
         """Run the GAR on the gathered [n, d] gradients and apply the SGD update."""
@@ -201,13 +255,13 @@ class RobustDataParallel:
             if rule in WEIGHTED_RULES:
                 w = self._weights(rule, kw)
                 self.last_weights = w
-                C.gpu_combine_sgd(self.G, w, param, mom, None, cfg.lr, cfg.momentum, cfg.dampening,
+                C.gpu_combine_sgd(self.G, w, param, mom, None, self._shadow, cfg.lr, cfg.momentum, cfg.dampening,
                                   cfg.weight_decay, cfg.nesterov, first)
             else:
                 g = self._gagg[: self.d]
                 self._coordinate(rule, kw, g)
-                C.gpu_combine_sgd(self._gagg.view(1, self.ld)[:, : self.d], self._one, param, mom, None, cfg.lr,
-                                  cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
+                C.gpu_combine_sgd(self._gagg.view(1, self.ld)[:, : self.d], self._one, param, mom, None, self._shadow,
+                                  cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
         else:
             gkw = dict(kw)
             if rule not in ("average", "median", "average-nan"):
@@ -325,7 +379,7 @@ class RobustDataParallel:
         """fwd + bwd of local worker j, gradient flattened (and attacked) into its row."""
         amp = (torch.autocast("cuda", dtype=self.cfg.autocast_dtype, cache_enabled=False)
                if self.cfg.autocast_dtype is not None else contextlib.nullcontext())
-        for p in self.flat.params:
+        for p in self.work_params:
             p.grad = None
         with amp:
             loss = self.loss_fn(self.model(x), y)
@@ -336,14 +390,14 @@ class RobustDataParallel:
         if attack is None:
             self._write_row(row)
         else:
-            g = self.flat.grads_flat(torch.empty(self.d, dtype=torch.float32, device=self.device))
+            g = self._grad_vector()
             est = None
             if attack in NEEDS_ESTIMATES:
                 honest = [self.X[i, self.rank, : self.d] for i in self.local_slots
                           if self.slot(i) not in self.cfg.byzantine and i != j]
                 est = torch.stack([g] + [h.float() for h in honest])
             row.copy_(apply_attack(attack, g, est, None))
-        for p in self.flat.params:
+        for p in self.work_params:
             p.grad = None
 
     def _capture(self, batches) -> None:
@@ -398,8 +452,11 @@ class RobustDataParallel:
     def evaluate(self, batches, binary: bool = False) -> float:
         self.model.eval()
         correct = total = 0
+        amp = (torch.autocast("cuda", dtype=self.cfg.autocast_dtype)
+               if (self.cfg.autocast_dtype is not None and self.device.type == "cuda") else contextlib.nullcontext())
         for x, y in batches:
-            out = self.model(x.to(self.device))
+            with amp:
+                out = self.model(x.to(self.device)).float()
             pred = out.round() if binary else out.argmax(1)
             correct += int((pred.view_as(y) == y.to(self.device)).sum())
             total += y.numel()

@@ -24,14 +24,17 @@ import torch.nn as nn
 from garfield_amd.utils.flat import flatten, write_flat_parameters
 
 
-def model_state(model: nn.Module) -> dict:
-    return {"flat": flatten(p.detach() for p in model.parameters()).cpu(),
+def model_state(model: nn.Module, flat: torch.Tensor | None = None) -> dict:
+    """``flat`` overrides the parameter vector (an engine's fp32 master weights when the
+    module itself holds low-precision working copies)."""
+    vec = flat if flat is not None else flatten(p.detach() for p in model.parameters())
+    return {"flat": vec.detach().float().cpu(),
             "buffers": {n: b.detach().cpu().clone() for n, b in model.named_buffers()}}
 
 
 def save(path: str, model: nn.Module, step: int = 0, momentum: torch.Tensor | None = None,
-         meta: dict | None = None) -> str:
-    state = model_state(model)
+         meta: dict | None = None, flat: torch.Tensor | None = None) -> str:
+    state = model_state(model, flat)
     state["step"] = int(step)
     if momentum is not None:
         state["momentum"] = momentum.detach().cpu()
@@ -64,12 +67,23 @@ def restore(model: nn.Module, state: dict) -> None:
 
 
 def save_engine(path: str, engine, meta: dict | None = None) -> str:
-    """Checkpoint of a ``RobustDataParallel`` engine (parameters, buffers, momentum, step)."""
-    return save(path, engine.model, engine.step_count, engine.mom[: engine.d], meta)
+    """Checkpoint of a ``RobustDataParallel`` engine (fp32 master parameters in the
+    reference layout, buffers, momentum, step)."""
+    return save(path, engine.model, engine.step_count, engine.mom[: engine.d], meta,
+                flat=engine.flat.reference_vector())
 
 
 def load_engine(path: str, engine) -> dict:
-    state = load(path, engine.model)
+    state = load(path)
+    engine.flat.load_reference_vector(state["flat"].to(engine.flat.data.device))
+    saved = state.get("buffers", {})
+    with torch.no_grad():
+        for n, b in engine.model.named_buffers():
+            s = saved.get(n)
+            if s is not None and b.shape == s.shape:
+                b.copy_(s.to(b.device))
+    if hasattr(engine, "sync_shadow"):
+        engine.sync_shadow()
     if "momentum" in state:
         engine.mom[: engine.d].copy_(state["momentum"].to(engine.mom.device))
     engine.step_count = int(state.get("step", 0))

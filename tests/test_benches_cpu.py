@@ -1,0 +1,57 @@
+"""Benchmark apps run end to end on CPU: collective bandwidth (gloo, 2 ranks), RPC
+all-to-all pulls (3 local nodes) and the GAR micro-benchmark on host tensors."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env():
+    return dict(os.environ, PYTHONPATH=str(REPO), CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+                GARFIELD_NUM_THREADS="2")
+
+
+def _rows(out):
+    return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+
+
+def test_comm_bench_two_ranks():
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+                        "127.0.0.1", "--master-port", str(_port()), "-m", "garfield_amd.apps.comm_bench",
+                        "--sizes", "4096", "65536", "--iters", "2", "--warmup", "1", "--dtype", "fp32"],
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = _rows(r.stdout)
+    assert {x["op"] for x in rows} == {"all_gather", "broadcast", "all_reduce", "all_to_all"}
+    ag = [x for x in rows if x["op"] == "all_gather"][0]
+    assert ag["world"] == 2 and ag["bytes"] == 2 * 4096 * 4 and ag["busbw_GBps"] > 0
+
+
+def test_rpc_bench_spawn():
+    r = subprocess.run([sys.executable, "-m", "garfield_amd.apps.rpc_bench", "--spawn", "--n", "3", "--d", "5000",
+                        "--num_iter", "2", "--port", str(_port())], capture_output=True, text=True, timeout=300,
+                       env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = _rows(r.stdout)
+    assert len(rows) == 6 and all(x["d"] == 5000 and x["n"] == 3 for x in rows)
+
+
+def test_gar_bench_cpu():
+    r = subprocess.run([sys.executable, "-m", "garfield_amd.apps.gar_bench", "--device", "cpu", "--n", "8",
+                        "--d", "10000", "--iters", "1", "--rules", "krum", "median"],
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = _rows(r.stdout)
+    assert {x["rule"] for x in rows} == {"krum", "median"}

@@ -153,11 +153,24 @@ def test_fused_combine_sgd_matches_torch_sgd(cuda, native, nesterov):
     ref_p = torch.nn.Parameter(p0.clone())
     opt = torch.optim.SGD([ref_p], lr=0.1, momentum=0.9, weight_decay=5e-4, nesterov=nesterov)
     for step in range(3):
-        native.gpu_combine_sgd(X, w, param, mom, None, 0.1, 0.9, 0.0, 5e-4, nesterov, step == 0)
+        native.gpu_combine_sgd(X, w, param, mom, None, None, 0.1, 0.9, 0.0, 5e-4, nesterov, step == 0)
         ref_p.grad = (w[:, None] * X).sum(0)
         opt.step()
     torch.cuda.synchronize()
     assert torch.allclose(param, ref_p.detach(), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("sdt", [torch.bfloat16, torch.float16])
+def test_combine_sgd_writes_shadow(cuda, native, sdt):
+    n, d = 8, 10007
+    X = torch.randn(n, 10016, device=cuda, dtype=torch.bfloat16)[:, :d]   # 16-byte aligned rows
+    w = torch.full((n,), 1 / n, device=cuda)
+    param, mom = torch.randn(d, device=cuda), torch.zeros(d, device=cuda)
+    shadow = torch.zeros(d + 9, device=cuda, dtype=sdt)
+    native.gpu_combine_sgd(X, w, param, mom, None, shadow, 0.1, 0.9, 0.0, 5e-4, False, True)
+    torch.cuda.synchronize()
+    assert torch.equal(shadow[:d], param.to(sdt))
+    assert torch.equal(shadow[d:], torch.zeros(9, device=cuda, dtype=sdt))
 
 
 def test_large_n_fallback_matches_oracle(cuda):
@@ -191,3 +204,17 @@ def test_flatten_cast_matches_cat(cuda, native, odt):
     torch.cuda.synchronize()
     assert torch.equal(dst[:total], ref_)
     assert torch.equal(dst[total:], torch.zeros(5, device=cuda, dtype=odt))
+
+
+@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
+def test_flatten_cast_mixed_source_dtypes(cuda, native, odt):
+    torch.manual_seed(1)
+    shapes = [(64, 3, 7, 7), (10,), (3,), (256, 64, 3, 3), (1,), (130, 7), (7,)]
+    dts = [torch.bfloat16, torch.float32, torch.float16, torch.bfloat16, torch.float32, torch.bfloat16, torch.bfloat16]
+    ts = [torch.randn(s, device=cuda).to(dt) for s, dt in zip(shapes, dts)]
+    total = sum(t.numel() for t in ts)
+    dst = torch.zeros(total, device=cuda, dtype=odt)
+    native.gpu_flatten_cast(ts, dst)
+    ref_ = torch.cat([t.reshape(-1).float() for t in ts]).to(odt)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, ref_)
