@@ -12,10 +12,12 @@ logical workers (default 8, so f = 2 Multi-Krum's n >= 2f + 3 = 7 holds on one G
 each computing a full forward/backward of ResNet-50 (torchvision architecture,
 10 classes, random init) on its own synthetic CIFAR-10-shape micro-batch of
 ``--batch`` images (default 250: the reference Garfield_CC ResNet-50 config,
-``PT/applications/Garfield_CC/run_exp.sh``), bf16 autocast. Every step: per-worker
-gradients -> bf16 rows -> RCCL all-gather into the [n, d] buffer (overlapped with
-the next worker's backward) -> HIP Multi-Krum (MFMA Gram, on-device selection) ->
-fused combine + SGD(momentum 0.9, wd 5e-4) on fp32 master weights.
+``PT/applications/Garfield_CC/run_exp.sh``), bf16 autocast. Every step: the GPU's
+logical workers run as ONE grouped NHWC forward/backward (per-worker BatchNorm
+statistics and per-worker weight gradients, HIP BN/ReLU/residual kernels, one HIP
+graph) -> per-worker bf16 gradient rows -> RCCL all-gather into the [n, d]
+buffer -> HIP Multi-Krum (MFMA Gram, on-device selection) -> fused combine +
+SGD(momentum 0.9, wd 5e-4) on fp32 master weights.
 img/s = n_logical x batch / step time (whole job).
 """
 from __future__ import annotations
@@ -58,6 +60,9 @@ def parse():
     p.add_argument("--no-graph", action="store_true", help="disable per-worker HIP graph capture (eager launches)")
     p.add_argument("--no-lp-weights", action="store_true",
                    help="autocast casts every conv/linear weight per worker instead of bf16 working weights")
+    p.add_argument("--no-worker-batching", action="store_true",
+                   help="run the logical workers one after the other (per-worker graphs) instead of as one grouped "
+                        "NHWC batch with per-worker BatchNorm statistics and gradients")
     p.add_argument("--ref-impl", action="store_true",
                    help="also time the reference's algorithms run as-is (BASELINE.md (a)) and report the speedup")
     p.add_argument("--phases", action="store_true", help="report per-phase device time (compute / exchange / GAR)")
@@ -108,7 +113,8 @@ def main():
     xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
     cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                        weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
-                       cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=not a.no_lp_weights)
+                       cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=not a.no_lp_weights,
+                       worker_batching=False if a.no_worker_batching else None)
     eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
     batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
                                 seed=1000 + ctx.rank, channels_last=a.channels_last)
@@ -126,7 +132,8 @@ def main():
     if a.overhead:
         cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                                weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
-                               cuda_graph=not a.no_graph, lp_weights=not a.no_lp_weights)
+                               cuda_graph=not a.no_graph, lp_weights=not a.no_lp_weights,
+                               worker_batching=False if a.no_worker_batching else None)
         torch.manual_seed(1234)
         eng_avg = RobustDataParallel(build_model(a.model, num_classes=num_classes), F.cross_entropy, ctx, cfg_avg)
         e_avg, _ = timed_steps(eng_avg, batches, a.steps, a.warmup, ctx)
@@ -168,7 +175,8 @@ def main():
                 "f": a.f,
                 "batch_per_worker": a.batch,
                 "exchange_dtype": a.exchange_dtype,
-                "hip_graphs": bool(getattr(eng, "_graph", None)),
+                "hip_graphs": bool(getattr(eng, "_graph", None) or getattr(eng, "_ggraph", None)),
+                "worker_batching": eng._gexec is not None,
                 "lp_weights": eng._shadow is not None,
                 "optimizer": f"SGD lr={a.lr} momentum=0.9 wd=5e-4 (fused into the GAR combine kernel)",
             },

@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "bn_gpu.hpp"
 #include "gar_common.hpp"
 #include "gar_cpu.hpp"
 #include "gar_gpu.hpp"
@@ -268,6 +269,208 @@ at::Tensor c_sqdist(const RowSet& rs, const at::Tensor& center) {
   });
 }
 
+// ------------------------------------------------- worker-grouped layers ----
+// Every shape, dtype, device and alignment the kernels assume is checked here,
+// on the host, before anything is launched.
+
+void check_bf16_rows(const at::Tensor& t, const at::Device& dev, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.device() == dev && t.scalar_type() == at::kBFloat16,
+              "garfield: ", what, " must be a bf16 tensor on ", dev);
+  TORCH_CHECK(t.dim() == 2 && t.is_contiguous(), "garfield: ", what, " must be a contiguous [rows, C] matrix");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "garfield: ", what, " must be 16-byte aligned");
+}
+
+const uint16_t* u16(const at::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* u16_mut(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+float* opt_vec(const c10::optional<at::Tensor>& t, int64_t numel, const at::Device& dev, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->device() == dev && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == numel,
+              "garfield: ", what, " must be a contiguous fp32 tensor of ", numel, " elements on ", dev);
+  return t->data_ptr<float>();
+}
+
+float* ws_vec(const at::Tensor& t, int64_t numel, const at::Device& dev, const char* what) {
+  TORCH_CHECK(t.device() == dev && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() >= numel,
+              "garfield: ", what, " must be a contiguous fp32 tensor of >= ", numel, " elements on ", dev);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "garfield: ", what, " must be 16-byte aligned");
+  return t.data_ptr<float>();
+}
+
+int64_t bn_groups(const at::Tensor& x, int64_t groups) {
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(groups >= 1 && R > 0 && R % groups == 0, "garfield bn: ", R, " rows do not split into ", groups,
+              " equal worker groups");
+  TORCH_CHECK(C > 0 && C % 8 == 0, "garfield bn: the channel count must be a positive multiple of 8, got ", C);
+  return R / groups;
+}
+
+void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int64_t groups,
+                  const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta, double eps,
+                  double momentum, const c10::optional<at::Tensor>& run_mean,
+                  const c10::optional<at::Tensor>& run_var, const at::Tensor& part, const at::Tensor& mean,
+                  const at::Tensor& istd, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& y,
+                  bool relu) {
+  const auto dev = x.device();
+  check_bf16_rows(x, dev, "x");
+  check_bf16_rows(y, dev, "y");
+  TORCH_CHECK(y.sizes() == x.sizes(), "garfield bn: y must have x's shape");
+  const int64_t rg = bn_groups(x, groups);
+  const int64_t C = x.size(1);
+  const uint16_t* r = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_bf16_rows(*res, dev, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "garfield bn: the residual must have x's shape");
+    r = u16(*res);
+  }
+  const int G = static_cast<int>(groups);
+  float* pw = ws_vec(part, garfield::gpu::bn_part_floats(rg, G, static_cast<int>(C)), dev, "part");
+  float* m = ws_vec(mean, groups * C, dev, "mean");
+  float* is = ws_vec(istd, groups * C, dev, "istd");
+  float* sc = ws_vec(scale, groups * C, dev, "scale");
+  float* sh = ws_vec(shift, groups * C, dev, "shift");
+  const float* g = opt_vec(gamma, C, dev, "gamma");
+  const float* b = opt_vec(beta, C, dev, "beta");
+  float* rm = opt_vec(run_mean, C, dev, "running_mean");
+  float* rv = opt_vec(run_var, C, dev, "running_var");
+  TORCH_CHECK((rm == nullptr) == (rv == nullptr), "garfield bn: pass both running statistics or neither");
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::bn_forward(u16(x), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
+                            static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, u16_mut(y), relu,
+                            stream_of(dev));
+}
+
+void g_bn_backward(const at::Tensor& x, const at::Tensor& dy, const c10::optional<at::Tensor>& y, int64_t groups,
+                   const c10::optional<at::Tensor>& gamma, const at::Tensor& mean, const at::Tensor& istd,
+                   const at::Tensor& part, const at::Tensor& coef, const at::Tensor& dx,
+                   const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& grow, int64_t row_stride,
+                   int64_t off_gamma, int64_t off_beta) {
+  const auto dev = x.device();
+  check_bf16_rows(x, dev, "x");
+  check_bf16_rows(dy, dev, "dy");
+  check_bf16_rows(dx, dev, "dx");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes(), "garfield bn: dy/dx must have x's shape");
+  const int64_t rg = bn_groups(x, groups);
+  const int64_t C = x.size(1);
+  const uint16_t* yp = nullptr;
+  if (y.has_value() && y->defined()) {
+    check_bf16_rows(*y, dev, "y");
+    TORCH_CHECK(y->sizes() == x.sizes(), "garfield bn: y must have x's shape");
+    yp = u16(*y);
+  }
+  uint16_t* dr = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    check_bf16_rows(*dres, dev, "dres");
+    TORCH_CHECK(dres->sizes() == x.sizes(), "garfield bn: dres must have x's shape");
+    dr = u16_mut(*dres);
+  }
+  const int G = static_cast<int>(groups);
+  float* pw = ws_vec(part, garfield::gpu::bn_part_floats(rg, G, static_cast<int>(C)), dev, "part");
+  float* cw = ws_vec(coef, 3 * groups * C, dev, "coef");
+  const float* m = ws_vec(mean, groups * C, dev, "mean");
+  const float* is = ws_vec(istd, groups * C, dev, "istd");
+  const float* g = opt_vec(gamma, C, dev, "gamma");
+  void* gp = nullptr;
+  int gdt = garfield::kF32;
+  if (grow.has_value() && grow->defined()) {
+    TORCH_CHECK(grow->device() == dev && grow->is_contiguous(), "garfield bn: grow must be contiguous on ", dev);
+    gdt = dtype_code(*grow);
+    TORCH_CHECK(gdt != garfield::kF64, "garfield bn: grow must be fp32, bf16 or fp16");
+    TORCH_CHECK(row_stride >= 0 && off_gamma >= -1 && off_beta >= -1, "garfield bn: invalid grow offsets");
+    for (int64_t off : {off_gamma, off_beta})
+      if (off >= 0)
+        TORCH_CHECK((groups - 1) * row_stride + off + C <= grow->numel(), "garfield bn: grow offset ", off,
+                    " + ", groups, " rows of stride ", row_stride, " is out of bounds (", grow->numel(), ")");
+    gp = grow->data_ptr();
+  }
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::bn_backward(u16(x), u16(dy), yp, rg, G, static_cast<int>(C), g, m, is, pw, cw, u16_mut(dx), dr,
+                             gp, gdt, row_stride, off_gamma, off_beta, stream_of(dev));
+}
+
+garfield::gpu::Im2col conv_geometry(const at::Tensor& x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
+                                    int64_t pw, int64_t dh, int64_t dw) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4,
+              "garfield im2col: x must be a 4-D bf16 device tensor");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "garfield im2col: x must be channels_last");
+  TORCH_CHECK(kh >= 1 && kw >= 1 && sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0 && dh >= 1 && dw >= 1,
+              "garfield im2col: invalid kernel geometry");
+  garfield::gpu::Im2col g{};
+  g.N = static_cast<int>(x.size(0));
+  g.C = static_cast<int>(x.size(1));
+  g.H = static_cast<int>(x.size(2));
+  g.W = static_cast<int>(x.size(3));
+  g.KH = static_cast<int>(kh); g.KW = static_cast<int>(kw);
+  g.sh = static_cast<int>(sh); g.sw = static_cast<int>(sw);
+  g.ph = static_cast<int>(ph); g.pw = static_cast<int>(pw);
+  g.dh = static_cast<int>(dh); g.dw = static_cast<int>(dw);
+  g.Ho = static_cast<int>((x.size(2) + 2 * ph - dh * (kh - 1) - 1) / sh + 1);
+  g.Wo = static_cast<int>((x.size(3) + 2 * pw - dw * (kw - 1) - 1) / sw + 1);
+  TORCH_CHECK(g.Ho >= 1 && g.Wo >= 1, "garfield im2col: empty output");
+  TORCH_CHECK(x.numel() <= INT32_MAX && static_cast<int64_t>(g.N) * g.Ho * g.Wo <= INT32_MAX,
+              "garfield im2col: problem too large for 32-bit pixel indexing");
+  TORCH_CHECK(kh * kw * g.C <= INT32_MAX / 256, "garfield im2col: kernel too large");
+  return g;
+}
+
+void check_col(const at::Tensor& col, const at::Tensor& x, garfield::gpu::Im2col& g) {
+  const int64_t rows = static_cast<int64_t>(g.N) * g.Ho * g.Wo;
+  const int64_t K = static_cast<int64_t>(g.KH) * g.KW * g.C;
+  TORCH_CHECK(col.device() == x.device() && col.scalar_type() == at::kBFloat16 && col.is_contiguous() &&
+                  col.dim() == 2 && col.size(0) == rows && col.size(1) >= K && col.size(1) <= INT32_MAX / 256,
+              "garfield im2col: col must be a contiguous bf16 [", rows, ", >= ", K, "] tensor on x's device");
+  g.ldc = static_cast<int>(col.size(1));
+  if (g.C % 8 == 0)
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(col.data_ptr()) % 16 == 0,
+                "garfield im2col: x and col must be 16-byte aligned");
+}
+
+void g_im2col(const at::Tensor& x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+              int64_t dh, int64_t dw, const at::Tensor& col) {
+  auto g = conv_geometry(x, kh, kw, sh, sw, ph, pw, dh, dw);
+  check_col(col, x, g);
+  c10::hip::HIPGuard guard(x.device().index());
+  garfield::gpu::im2col_nhwc(u16(x), g, u16_mut(col), stream_of(x.device()));
+}
+
+// dx: the (channels_last, bf16) input-shaped output; dcol: [N*Ho*Wo, ldc] bf16
+void g_col2im(const at::Tensor& dcol, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
+              int64_t dh, int64_t dw, const at::Tensor& dx) {
+  auto g = conv_geometry(dx, kh, kw, sh, sw, ph, pw, dh, dw);
+  check_col(dcol, dx, g);
+  c10::hip::HIPGuard guard(dx.device().index());
+  garfield::gpu::col2im_nhwc(u16(dcol), g, u16_mut(dx), stream_of(dx.device()));
+}
+
+int g_flatten_cast_at(const std::vector<at::Tensor>& srcs, const std::vector<int64_t>& offsets,
+                      const at::Tensor& dst) {
+  TORCH_CHECK(srcs.size() == offsets.size(), "flatten_cast_at: one offset per source tensor");
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "flatten_cast_at: dst must be a contiguous device tensor");
+  const int odt = dtype_code(dst);
+  TORCH_CHECK(odt != garfield::kF64, "flatten_cast_at: dst must be fp32, bf16 or fp16");
+  if (srcs.empty()) return 0;
+  c10::hip::HIPGuard guard(dst.device().index());
+  std::vector<const void*> ptrs;
+  std::vector<int> dts;
+  std::vector<int64_t> numels, offs;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const auto& t = srcs[i];
+    const auto st = t.scalar_type();
+    TORCH_CHECK((st == at::kFloat || st == at::kBFloat16 || st == at::kHalf) && t.device() == dst.device(),
+                "flatten_cast_at: fp32/bf16/fp16 sources on dst's device");
+    TORCH_CHECK(t.is_non_overlapping_and_dense(), "flatten_cast_at: sources must be dense");
+    TORCH_CHECK(offsets[i] >= 0 && offsets[i] + t.numel() <= dst.numel(), "flatten_cast_at: source ", i,
+                " at offset ", offsets[i], " overruns dst (", dst.numel(), " elements)");
+    ptrs.push_back(t.data_ptr());
+    dts.push_back(dtype_code(t));
+    numels.push_back(t.numel());
+    offs.push_back(offsets[i]);
+  }
+  return garfield::gpu::flatten_cast(ptrs.data(), dts.data(), numels.data(), offs.data(),
+                                     static_cast<int>(ptrs.size()), dst.data_ptr(), odt, stream_of(dst.device()));
+}
+
 // Register a function under `name` for both a 2-D buffer and a list of rows.
 template <class Fn2d, class FnList>
 void def_rows(py::module& m, const char* name, Fn2d&& f2d, FnList&& flist, const char* doc) {
@@ -376,6 +579,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                        static_cast<int>(ptrs.size()), dst.data_ptr(), dtype_code(dst),
                                        stream_of(dst.device()));
   }, "Copy a list of dense fp32/bf16/fp16 tensors (memory order) back to back into dst, casting to dst's dtype");
+
+  m.def("gpu_flatten_cast_at", &g_flatten_cast_at,
+        "Copy dense fp32/bf16/fp16 tensors (memory order) into dst at explicit element offsets, casting to dst's dtype");
+
+  // worker-grouped NHWC layers (bn_nhwc.hip, im2col_nhwc.hip)
+  m.def("bn_part_floats", [](int64_t rg, int groups, int C) { return garfield::gpu::bn_part_floats(rg, groups, C); });
+  m.def("gpu_bn_forward", &g_bn_forward,
+        "Per-worker BatchNorm(+residual)(+ReLU) forward on [k*Rg, C] bf16 rows; args (x, res|None, groups, gamma, "
+        "beta, eps, momentum, running_mean|None, running_var|None, part, mean, istd, scale, shift, y, relu)");
+  m.def("gpu_bn_backward", &g_bn_backward,
+        "Per-worker BatchNorm backward; writes dγ/dβ of worker g to grow[g*row_stride + off_(gamma|beta) + c]; "
+        "args (x, dy, y|None, groups, gamma, mean, istd, part, coef, dx, dres|None, grow|None, row_stride, "
+        "off_gamma, off_beta)");
+  m.def("gpu_im2col", &g_im2col, "NHWC im2col of a channels_last bf16 tensor into col [N*Ho*Wo, ldc >= KH*KW*C] "
+        "(pad columns zeroed); args (x, kh, kw, sh, sw, ph, pw, dh, dw, col)");
+  m.def("gpu_col2im", &g_col2im, "Adjoint of gpu_im2col (gather, deterministic): dx = col2im(dcol); args "
+        "(dcol, kh, kw, sh, sw, ph, pw, dh, dw, dx)");
 
   // CPU building blocks (thread pool)
   def_rows(m, "cpu_pairwise",

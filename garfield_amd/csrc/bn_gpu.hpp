@@ -1,0 +1,46 @@
+// Host-side launchers of the worker-grouped NHWC kernels: BatchNorm(+residual)
+// (+ReLU) (bn_nhwc.hip) and the im2col gather of the per-worker weight-gradient
+// GEMMs. Asynchronous on the given stream, no allocation, no synchronisation:
+// HIP-graph capturable.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace garfield {
+namespace gpu {
+
+constexpr int kBnMaxChunks = 64;  // row chunks per (group, channel block) in the partial-sum pass
+
+// Floats of the partial-sum workspace for `groups` groups of `rg` rows and C channels.
+int64_t bn_part_floats(int64_t rg, int groups, int C);
+
+// x, res, y: [groups * rg, C] bf16 (NHWC rows). gamma/beta/run_*: [C] fp32 (nullable).
+// mean, istd, scale, shift: [groups, C] fp32 outputs (saved for the backward).
+void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
+                const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
+                float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, hipStream_t stream);
+
+// y (nullable) = forward output, used for the ReLU mask. dres (nullable) receives dz.
+// grow (nullable): exchange buffer; group g's dγ[c] goes to grow[g*row_stride + off_gamma + c]
+// (dβ likewise at off_beta; a negative offset skips it), cast to grow_dt.
+// coef: [groups, 3, C] fp32 workspace.
+void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, int64_t rg, int groups, int C,
+                 const float* gamma, const float* mean, const float* istd, float* part, float* coef, uint16_t* dx,
+                 uint16_t* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
+                 hipStream_t stream);
+
+// NHWC im2col (bf16): col[(n*Ho + ho)*Wo + wo][(i*KW + j)*C + c] = x[n][ho*sh - ph + i*dh][wo*sw - pw + j*dw][c]
+// (0 outside the image). col: [N*Ho*Wo, ldc] with ldc >= KH*KW*C; columns past KH*KW*C are zeroed
+// (GEMM-friendly padding of the 3-channel stem).
+struct Im2col {
+  int N, H, W, C, KH, KW, sh, sw, ph, pw, dh, dw, Ho, Wo;
+  int ldc;
+};
+void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t stream);
+
+// The adjoint gather: dx[n][hi][wi][c] = Σ_{taps (i, j) hitting (hi, wi)} dcol[(n*Ho + ho)*Wo + wo][(i*KW + j)*C + c]
+// (fp32 accumulation, every element written once: no atomics, deterministic).
+void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, hipStream_t stream);
+
+}  // namespace gpu
+}  // namespace garfield

@@ -1,0 +1,405 @@
+// Worker-grouped BatchNorm (+ residual add) (+ ReLU) for NHWC activations, gfx950.
+//
+// The engine runs its k logical workers as ONE batched forward/backward
+// (garfield_amd/parallel/grouped.py): the activations of all workers are one
+// [R, C] NHWC matrix with R = k * Rg rows (Rg = B*H*W rows per worker), and
+// BatchNorm must still use per-WORKER batch statistics, exactly as if each
+// worker ran alone. The reference runs one worker per process
+// (pytorch_impl/libs/garfieldpp/worker.py:77-96) and its nets use
+// nn.BatchNorm2d + F.relu (+ residual add): three to four kernels per layer per
+// worker (MIOpenBatchNormFwdTrainSpatial, relu, add; and their backward).
+// Here one layer costs three launches FOR ALL k WORKERS, forward and backward:
+//
+//   forward : partial (sum, sum of squares) per (worker, channel, row chunk)
+//             -> finalize (mean, 1/std, scale/shift, running-stat update that
+//                replays the k sequential worker updates)
+//             -> apply  y = relu(x*scale + shift [+ residual])      (bf16x8 I/O)
+//   backward: partial (Σdz, Σdz·(x-μ)) with dz = dy·[y > 0]
+//             -> finalize (dγ, dβ per worker, written STRAIGHT into each
+//                worker's row of the gradient exchange buffer; apply coefficients)
+//             -> apply  dx = γ/σ·(dz - dβ/M - x̂·dγ/M)   [+ dres = dz]
+//
+// Launch boundaries order the stages (no inter-workgroup hand-off inside a
+// launch); every reduction runs in a fixed order, so results are deterministic.
+#include "bn_gpu.hpp"
+#include "gar_device.hpp"
+
+namespace garfield {
+namespace gpu {
+using namespace dev;
+namespace {
+
+constexpr int kThreads = 256;
+
+struct Geo {
+  int64_t rg;      // rows per group (worker)
+  int groups;
+  int C;
+  int cb;          // channels per workgroup in the partial kernels (multiple of 8)
+  int tch;         // threads across channels = cb / 8
+  int rp;          // row lanes = 256 / tch
+  int chunks;      // row chunks per group
+  int64_t rows_per_chunk;
+};
+
+Geo geometry(int64_t rg, int groups, int C) {
+  Geo g{};
+  g.rg = rg;
+  g.groups = groups;
+  g.C = C;
+  g.cb = C < 512 ? C : 512;
+  g.tch = g.cb / 8;
+  g.rp = kThreads / g.tch;
+  if (g.rp < 1) g.rp = 1;
+  // enough row chunks to give the partial kernel ~1024 workgroups, each at least 4 row passes
+  const int ncb = (C + g.cb - 1) / g.cb;
+  const int64_t wg = static_cast<int64_t>(groups) * ncb;
+  int64_t want = (1024 + wg - 1) / wg;
+  int64_t maxc = (rg + 4 * g.rp - 1) / (4 * g.rp);
+  int64_t c = want < maxc ? want : maxc;
+  if (c < 1) c = 1;
+  if (c > kBnMaxChunks) c = kBnMaxChunks;
+  g.rows_per_chunk = (rg + c - 1) / c;
+  g.chunks = static_cast<int>((rg + g.rows_per_chunk - 1) / g.rows_per_chunk);
+  return g;
+}
+
+__device__ __forceinline__ void load8(const uint16_t* p, int64_t off, float (&v)[8]) {
+  load_vec<kBF16, 8>(p, off, v);
+}
+
+__device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// Partial per-(group, channel) sums over one row chunk.
+//   forward : s = Σ (x - shift), q = Σ (x - shift)^2  with shift = x[first row of the group]
+//             (shifted sums: no catastrophic cancellation when |mean| >> std)
+//   backward: s = Σ dz, q = Σ dz (x - mean)
+template <bool BWD, bool RELU>
+__global__ __launch_bounds__(kThreads) void k_partial(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                     const uint16_t* __restrict__ y, const float* __restrict__ mean,
+                                                     Geo geo, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float red[2][kThreads * 8];
+  const int C = geo.C;
+  const int tc = threadIdx.x % geo.tch;
+  const int tr = threadIdx.x / geo.tch;
+  const int chunk = blockIdx.x;
+  const int cbk = blockIdx.y;
+  const int g = blockIdx.z;
+  const int c0 = cbk * geo.cb + tc * 8;
+  const bool lane_ok = tr < geo.rp;
+  const bool active = lane_ok && (c0 < C);
+  const int64_t base = static_cast<int64_t>(g) * geo.rg;
+  const int64_t r0 = static_cast<int64_t>(chunk) * geo.rows_per_chunk;
+  int64_t r1 = r0 + geo.rows_per_chunk;
+  if (r1 > geo.rg) r1 = geo.rg;
+  float s[8], q[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; sh[i] = 0.f; }
+  if (active) {
+    if constexpr (BWD) load8f(mean + static_cast<int64_t>(g) * C + c0, sh);
+    else load8(x, base * C + c0, sh);
+    int64_t r = r0 + tr;
+    // two rows in flight per lane
+    for (; r + geo.rp < r1; r += 2 * geo.rp) {
+      const int64_t o0 = (base + r) * C + c0, o1 = o0 + static_cast<int64_t>(geo.rp) * C;
+      float a0[8], a1[8];
+      load8(x, o0, a0);
+      load8(x, o1, a1);
+      if constexpr (BWD) {
+        float d0[8], d1[8];
+        load8(dy, o0, d0);
+        load8(dy, o1, d1);
+        if constexpr (RELU) {
+          float y0[8], y1[8];
+          load8(y, o0, y0);
+          load8(y, o1, y1);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { d0[i] = y0[i] > 0.f ? d0[i] : 0.f; d1[i] = y1[i] > 0.f ? d1[i] : 0.f; }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s[i] += d0[i] + d1[i];
+          q[i] += d0[i] * (a0[i] - sh[i]) + d1[i] * (a1[i] - sh[i]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float e0 = a0[i] - sh[i], e1 = a1[i] - sh[i];
+          s[i] += e0 + e1;
+          q[i] += e0 * e0 + e1 * e1;
+        }
+      }
+    }
+    for (; r < r1; r += geo.rp) {
+      const int64_t o0 = (base + r) * C + c0;
+      float a0[8];
+      load8(x, o0, a0);
+      if constexpr (BWD) {
+        float d0[8];
+        load8(dy, o0, d0);
+        if constexpr (RELU) {
+          float y0[8];
+          load8(y, o0, y0);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) d0[i] = y0[i] > 0.f ? d0[i] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { s[i] += d0[i]; q[i] += d0[i] * (a0[i] - sh[i]); }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { const float e = a0[i] - sh[i]; s[i] += e; q[i] += e * e; }
+      }
+    }
+  }
+  // reduce the row lanes through LDS: red[.][lane_row * cb + channel]
+  if (lane_ok) {
+    float* p0 = &red[0][tr * geo.cb + tc * 8];
+    float* p1 = &red[1][tr * geo.cb + tc * 8];
+    *reinterpret_cast<float4*>(p0) = make_float4(s[0], s[1], s[2], s[3]);
+    *reinterpret_cast<float4*>(p0 + 4) = make_float4(s[4], s[5], s[6], s[7]);
+    *reinterpret_cast<float4*>(p1) = make_float4(q[0], q[1], q[2], q[3]);
+    *reinterpret_cast<float4*>(p1 + 4) = make_float4(q[4], q[5], q[6], q[7]);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < geo.cb; c += kThreads) {
+    const int cc = cbk * geo.cb + c;
+    if (cc >= C) continue;
+    float a = 0.f, b = 0.f;
+    for (int t = 0; t < geo.rp; ++t) { a += red[0][t * geo.cb + c]; b += red[1][t * geo.cb + c]; }
+    const int64_t o = (static_cast<int64_t>(g) * geo.chunks + chunk) * 2 * C;
+    part[o + cc] = a;
+    part[o + C + cc] = b;
+  }
+}
+
+// Forward finalize: one thread per channel, groups in order (replays the k
+// sequential running-stat updates of k independent workers).
+__global__ __launch_bounds__(kThreads) void k_fwd_finalize(const float* __restrict__ part, const uint16_t* __restrict__ x,
+                                                          Geo geo, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps, float momentum,
+                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                          float* __restrict__ mean, float* __restrict__ istd,
+                                                          float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  const int C = geo.C;
+  if (c >= C) return;
+  const float M = static_cast<float>(geo.rg);
+  const float gm = gamma ? gamma[c] : 1.f;
+  const float bt = beta ? beta[c] : 0.f;
+  float rm = run_mean ? run_mean[c] : 0.f;
+  float rv = run_var ? run_var[c] : 0.f;
+  for (int g = 0; g < geo.groups; ++g) {
+    float S = 0.f, Q = 0.f;
+    for (int ch = 0; ch < geo.chunks; ++ch) {
+      const int64_t o = (static_cast<int64_t>(g) * geo.chunks + ch) * 2 * C;
+      S += part[o + c];
+      Q += part[o + C + c];
+    }
+    const float sh = bf16_to_f(x[static_cast<int64_t>(g) * geo.rg * C + c]);
+    const float m1 = S / M;
+    float var = Q / M - m1 * m1;
+    var = var > 0.f ? var : 0.f;
+    const float mu = sh + m1;
+    const float is = rsqrtf(var + eps);
+    const int64_t gc = static_cast<int64_t>(g) * C + c;
+    mean[gc] = mu;
+    istd[gc] = is;
+    const float sc = gm * is;
+    scale[gc] = sc;
+    shift[gc] = bt - mu * sc;
+    if (run_mean) {
+      const float unb = geo.rg > 1 ? var * M / (M - 1.f) : var;
+      rm = (1.f - momentum) * rm + momentum * mu;
+      rv = (1.f - momentum) * rv + momentum * unb;
+    }
+  }
+  if (run_mean) { run_mean[c] = rm; run_var[c] = rv; }
+}
+
+// Elementwise passes over [R, C]: each workgroup owns kApplyIters x rp rows.
+constexpr int kApplyIters = 4;
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(kThreads) void k_fwd_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       int64_t rg, int64_t R, int C, int tch, int rp,
+                                                       uint16_t* __restrict__ y) {
+  const int tr = threadIdx.x / tch;
+  if (tr >= rp) return;
+  const int nv = C / 8;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * rp * kApplyIters;
+#pragma unroll
+  for (int it = 0; it < kApplyIters; ++it) {
+    const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
+    if (row >= R) break;
+    const int g = static_cast<int>(row / rg);
+    for (int v = threadIdx.x % tch; v < nv; v += tch) {
+      const int c = v * 8;
+      const int64_t off = row * C + c;
+      float a[8], sc[8], sf[8];
+      load8(x, off, a);
+      load8f(scale + static_cast<int64_t>(g) * C + c, sc);
+      load8f(shift + static_cast<int64_t>(g) * C + c, sf);
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = a[i] * sc[i] + sf[i];
+      if constexpr (RES) {
+        float r[8];
+        load8(res, off, r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] += r[i];
+      }
+      if constexpr (RELU) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = o[i] > 0.f ? o[i] : 0.f;
+      }
+      store_vec<8>(y, kBF16, off, o);
+    }
+  }
+}
+
+// Backward finalize: per (group, channel) dγ, dβ -> exchange rows; apply coefficients.
+__global__ __launch_bounds__(kThreads) void k_bwd_finalize(const float* __restrict__ part, Geo geo,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ istd,
+                                                          float* __restrict__ coef, void* grow, int grow_dt,
+                                                          int64_t row_stride, int64_t off_gamma, int64_t off_beta) {
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  const int C = geo.C;
+  if (c >= C) return;
+  const float M = static_cast<float>(geo.rg);
+  const float gm = gamma ? gamma[c] : 1.f;
+  for (int g = 0; g < geo.groups; ++g) {
+    float A = 0.f, B = 0.f;
+    for (int ch = 0; ch < geo.chunks; ++ch) {
+      const int64_t o = (static_cast<int64_t>(g) * geo.chunks + ch) * 2 * C;
+      A += part[o + c];
+      B += part[o + C + c];
+    }
+    const int64_t gc = static_cast<int64_t>(g) * C + c;
+    const float is = istd[gc];
+    const float dgamma = B * is;
+    const float dbeta = A;
+    if (grow) {
+      if (off_gamma >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_gamma + c, dgamma);
+      if (off_beta >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_beta + c, dbeta);
+    }
+    const int64_t o3 = static_cast<int64_t>(g) * 3 * C;
+    coef[o3 + c] = gm * is;                  // a
+    coef[o3 + C + c] = dbeta / M;            // b
+    coef[o3 + 2 * C + c] = dgamma / M * is;  // c  (x̂·dγ/M = (x-μ)·c)
+  }
+}
+
+template <bool RELU, bool RES_OUT>
+__global__ __launch_bounds__(kThreads) void k_bwd_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                       const uint16_t* __restrict__ y, const float* __restrict__ mean,
+                                                       const float* __restrict__ coef, int64_t rg, int64_t R, int C,
+                                                       int tch, int rp, uint16_t* __restrict__ dx,
+                                                       uint16_t* __restrict__ dres) {
+  const int tr = threadIdx.x / tch;
+  if (tr >= rp) return;
+  const int nv = C / 8;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * rp * kApplyIters;
+#pragma unroll
+  for (int it = 0; it < kApplyIters; ++it) {
+    const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
+    if (row >= R) break;
+    const int g = static_cast<int>(row / rg);
+    const float* cg = coef + static_cast<int64_t>(g) * 3 * C;
+    for (int v = threadIdx.x % tch; v < nv; v += tch) {
+      const int c = v * 8;
+      const int64_t off = row * C + c;
+      float a[8], d[8], mu[8], ca[8], cb[8], cc[8];
+      load8(x, off, a);
+      load8(dy, off, d);
+      if constexpr (RELU) {
+        float yy[8];
+        load8(y, off, yy);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = yy[i] > 0.f ? d[i] : 0.f;
+      }
+      load8f(mean + static_cast<int64_t>(g) * C + c, mu);
+      load8f(cg + c, ca);
+      load8f(cg + C + c, cb);
+      load8f(cg + 2 * C + c, cc);
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = ca[i] * (d[i] - cb[i] - (a[i] - mu[i]) * cc[i]);
+      store_vec<8>(dx, kBF16, off, o);
+      if constexpr (RES_OUT) store_vec<8>(dres, kBF16, off, d);
+    }
+  }
+}
+
+void apply_geometry(int C, int* tch, int* rp) {
+  int t = C / 8;
+  if (t > kThreads) t = kThreads;
+  *tch = t;
+  *rp = kThreads / t;
+}
+
+dim3 apply_grid(int64_t R, int rp) {
+  const int64_t rows_per_wg = static_cast<int64_t>(rp) * kApplyIters;
+  return dim3(static_cast<unsigned>((R + rows_per_wg - 1) / rows_per_wg));
+}
+
+}  // namespace
+
+int64_t bn_part_floats(int64_t rg, int groups, int C) {
+  const Geo g = geometry(rg, groups, C);
+  return static_cast<int64_t>(groups) * g.chunks * 2 * C;
+}
+
+void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
+                const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
+                float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, hipStream_t stream) {
+  const Geo g = geometry(rg, groups, C);
+  const int ncb = (C + g.cb - 1) / g.cb;
+  hipLaunchKernelGGL((k_partial<false, false>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
+                     nullptr, nullptr, g, part);
+  hipLaunchKernelGGL(k_fwd_finalize, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, part, x, g,
+                     gamma, beta, eps, momentum, run_mean, run_var, mean, istd, scale, shift);
+  int tch, rp;
+  apply_geometry(C, &tch, &rp);
+  const int64_t R = rg * groups;
+  const dim3 grid = apply_grid(R, rp);
+  if (res) {
+    if (relu) hipLaunchKernelGGL((k_fwd_apply<true, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y);
+    else hipLaunchKernelGGL((k_fwd_apply<true, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y);
+  } else {
+    if (relu) hipLaunchKernelGGL((k_fwd_apply<false, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y);
+    else hipLaunchKernelGGL((k_fwd_apply<false, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y);
+  }
+}
+
+void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, int64_t rg, int groups, int C,
+                 const float* gamma, const float* mean, const float* istd, float* part, float* coef, uint16_t* dx,
+                 uint16_t* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
+                 hipStream_t stream) {
+  const Geo g = geometry(rg, groups, C);
+  const int ncb = (C + g.cb - 1) / g.cb;
+  const bool relu = y != nullptr;
+  if (relu) hipLaunchKernelGGL((k_partial<true, true>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, dy, y, mean, g, part);
+  else hipLaunchKernelGGL((k_partial<true, false>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, dy, y, mean, g, part);
+  hipLaunchKernelGGL(k_bwd_finalize, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, part, g, gamma,
+                     istd, coef, grow, grow_dt, row_stride, off_gamma, off_beta);
+  int tch, rp;
+  apply_geometry(C, &tch, &rp);
+  const int64_t R = rg * groups;
+  const dim3 grid = apply_grid(R, rp);
+  if (relu) {
+    if (dres) hipLaunchKernelGGL((k_bwd_apply<true, true>), grid, dim3(kThreads), 0, stream, x, dy, y, mean, coef, rg, R, C, tch, rp, dx, dres);
+    else hipLaunchKernelGGL((k_bwd_apply<true, false>), grid, dim3(kThreads), 0, stream, x, dy, y, mean, coef, rg, R, C, tch, rp, dx, dres);
+  } else {
+    if (dres) hipLaunchKernelGGL((k_bwd_apply<false, true>), grid, dim3(kThreads), 0, stream, x, dy, y, mean, coef, rg, R, C, tch, rp, dx, dres);
+    else hipLaunchKernelGGL((k_bwd_apply<false, false>), grid, dim3(kThreads), 0, stream, x, dy, y, mean, coef, rg, R, C, tch, rp, dx, dres);
+  }
+}
+
+}  // namespace gpu
+}  // namespace garfield

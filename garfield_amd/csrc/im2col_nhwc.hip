@@ -1,0 +1,161 @@
+// NHWC im2col / col2im (bf16) for the worker-grouped convolutions
+// (garfield_amd/ops/grouped.py). With the k logical workers batched, every
+// k x k convolution of the grouped step is three GEMMs on hipBLASLt around these
+// two gathers, no MIOpen call (MIOpen's NHWC solvers are not HIP-graph replay
+// safe on ROCm 7 / gfx950: weight gradients go non-finite from a replay on):
+//
+//   forward : col = im2col(x);  y = col · Wᵀ              (W: [Cout, KH*KW*Cin], the
+//                                                         channels_last weight's memory order)
+//   dgrad   : dcol = dy · W;    dx = col2im(dcol)
+//   wgrad   : dW_g = dy_gᵀ · col_g for every worker g     (ONE strided-batched GEMM; col's
+//                                                         (kh, kw, ci) column order IS the
+//                                                         weight's memory order, so each dW_g
+//                                                         lands in the exchange row as it is)
+//
+// col2im is written as a gather (each input pixel sums the taps that read it),
+// so it needs no atomics and is deterministic.
+#include "bn_gpu.hpp"
+#include "gar_device.hpp"
+
+namespace garfield {
+namespace gpu {
+using namespace dev;
+namespace {
+
+constexpr int kThreads = 256;
+
+// Vector path (C % 8 == 0): one thread per 16-byte channel vector of one
+// (output pixel, kernel tap); a workgroup covers whole col rows, so every index
+// is 32-bit except the final element offsets.
+__global__ __launch_bounds__(kThreads) void k_im2col_vec(const uint16_t* __restrict__ x, Im2col g,
+                                                        uint16_t* __restrict__ col, int rows_per_wg) {
+  const int cv = g.C / 8;
+  const int K = g.KH * g.KW * cv;  // vectors per col row
+  const int rows = g.N * g.Ho * g.Wo;
+  for (int t = threadIdx.x; t < rows_per_wg * K; t += kThreads) {
+    const int m = blockIdx.x * rows_per_wg + t / K;
+    if (m >= rows) break;
+    const int r = t % K;
+    const int kp = r / cv, v = r % cv;
+    const int i = kp / g.KW, j = kp % g.KW;
+    const int wo = m % g.Wo;
+    const int ho = (m / g.Wo) % g.Ho;
+    const int n = m / (g.Wo * g.Ho);
+    const int hi = ho * g.sh - g.ph + i * g.dh;
+    const int wi = wo * g.sw - g.pw + j * g.dw;
+    uint4 val = make_uint4(0u, 0u, 0u, 0u);
+    if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+      val = *reinterpret_cast<const uint4*>(x + ((static_cast<int64_t>(n) * g.H + hi) * g.W + wi) * g.C + v * 8);
+    *reinterpret_cast<uint4*>(col + static_cast<int64_t>(m) * g.ldc + static_cast<int64_t>(r) * 8) = val;
+  }
+}
+
+// Scalar path (any C, e.g. the 3-channel stem); also zero-fills the pad columns.
+__global__ __launch_bounds__(kThreads) void k_im2col_scalar(const uint16_t* __restrict__ x, Im2col g,
+                                                           uint16_t* __restrict__ col, int rows_per_wg) {
+  const int K = g.KH * g.KW * g.C;
+  const int L = g.ldc;
+  const int rows = g.N * g.Ho * g.Wo;
+  for (int t = threadIdx.x; t < rows_per_wg * L; t += kThreads) {
+    const int m = blockIdx.x * rows_per_wg + t / L;
+    if (m >= rows) break;
+    const int r = t % L;
+    uint16_t val = 0;
+    if (r < K) {
+      const int kp = r / g.C, c = r % g.C;
+      const int i = kp / g.KW, j = kp % g.KW;
+      const int wo = m % g.Wo;
+      const int ho = (m / g.Wo) % g.Ho;
+      const int n = m / (g.Wo * g.Ho);
+      const int hi = ho * g.sh - g.ph + i * g.dh;
+      const int wi = wo * g.sw - g.pw + j * g.dw;
+      if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+        val = x[((static_cast<int64_t>(n) * g.H + hi) * g.W + wi) * g.C + c];
+    }
+    col[static_cast<int64_t>(m) * L + r] = val;
+  }
+}
+
+// (hi, wi) -> output pixel of tap (i, j), or -1.
+__device__ __forceinline__ int tap_row(const Im2col& g, int n, int hi, int wi, int i, int j) {
+  const int a = hi + g.ph - i * g.dh;
+  const int b = wi + g.pw - j * g.dw;
+  if (a < 0 || b < 0 || a % g.sh || b % g.sw) return -1;
+  const int ho = a / g.sh, wo = b / g.sw;
+  if (ho >= g.Ho || wo >= g.Wo) return -1;
+  return (n * g.Ho + ho) * g.Wo + wo;
+}
+
+// col2im vector path: one thread per 8-channel vector of one input pixel.
+__global__ __launch_bounds__(kThreads) void k_col2im_vec(const uint16_t* __restrict__ dcol, Im2col g,
+                                                        uint16_t* __restrict__ dx) {
+  const int cv = g.C / 8;
+  const int64_t total = static_cast<int64_t>(g.N) * g.H * g.W * cv;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * kThreads) {
+    const int v = static_cast<int>(t % cv);
+    const int pix = static_cast<int>(t / cv);
+    const int wi = pix % g.W;
+    const int hi = (pix / g.W) % g.H;
+    const int n = pix / (g.W * g.H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < g.KH; ++i) {
+      for (int j = 0; j < g.KW; ++j) {
+        const int m = tap_row(g, n, hi, wi, i, j);
+        if (m < 0) continue;
+        float a[8];
+        load_vec<kBF16, 8>(dcol, static_cast<int64_t>(m) * g.ldc + (i * g.KW + j) * g.C + v * 8, a);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += a[e];
+      }
+    }
+    store_vec<8>(dx, kBF16, static_cast<int64_t>(pix) * g.C + v * 8, acc);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_col2im_scalar(const uint16_t* __restrict__ dcol, Im2col g,
+                                                           uint16_t* __restrict__ dx) {
+  const int64_t total = static_cast<int64_t>(g.N) * g.H * g.W * g.C;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * kThreads) {
+    const int c = static_cast<int>(t % g.C);
+    const int pix = static_cast<int>(t / g.C);
+    const int wi = pix % g.W;
+    const int hi = (pix / g.W) % g.H;
+    const int n = pix / (g.W * g.H);
+    float acc = 0.f;
+    for (int i = 0; i < g.KH; ++i)
+      for (int j = 0; j < g.KW; ++j) {
+        const int m = tap_row(g, n, hi, wi, i, j);
+        if (m >= 0) acc += bf16_to_f(dcol[static_cast<int64_t>(m) * g.ldc + (i * g.KW + j) * g.C + c]);
+      }
+    dx[t] = f_to_bf16(acc);
+  }
+}
+
+}  // namespace
+
+void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t stream) {
+  const int rows = g.N * g.Ho * g.Wo;
+  if (rows <= 0) return;
+  const bool vec = g.C % 8 == 0 && g.ldc == g.KH * g.KW * g.C;
+  const int K = vec ? g.KH * g.KW * (g.C / 8) : g.ldc;
+  int rpw = kThreads * 4 / K;  // ~4 items per thread
+  if (rpw < 1) rpw = 1;
+  const dim3 grid((rows + rpw - 1) / rpw);
+  if (vec) hipLaunchKernelGGL(k_im2col_vec, grid, dim3(kThreads), 0, stream, x, g, col, rpw);
+  else hipLaunchKernelGGL(k_im2col_scalar, grid, dim3(kThreads), 0, stream, x, g, col, rpw);
+}
+
+void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, hipStream_t stream) {
+  const bool vec = g.C % 8 == 0 && g.ldc % 8 == 0;
+  const int64_t items = static_cast<int64_t>(g.N) * g.H * g.W * (vec ? g.C / 8 : g.C);
+  if (items <= 0) return;
+  int64_t blocks = (items + kThreads - 1) / kThreads;
+  if (blocks > 65536) blocks = 65536;  // grid-stride beyond
+  if (vec) hipLaunchKernelGGL(k_col2im_vec, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0, stream, dcol, g, dx);
+  else hipLaunchKernelGGL(k_col2im_scalar, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0, stream, dcol, g, dx);
+}
+
+}  // namespace gpu
+}  // namespace garfield

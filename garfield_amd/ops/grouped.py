@@ -1,0 +1,468 @@
+"""Worker-grouped layers: the k logical workers of a rank as ONE batched pass.
+
+The reference computes each worker's gradient in its own process, one batch at a
+time (``pytorch_impl/libs/garfieldpp/worker.py:77-96``). Its robust rules need
+every worker's gradient *separately*, so a naive port runs k small forward/
+backward passes per GPU: ResNet-50 on CIFAR-shape batches of 250 is ~960 small
+kernels per worker, and on MI355X the step becomes kernel-boundary bound (1.5-2 µs
+per dependent launch, tiny grids on 256 CUs).
+
+Here the k workers' micro-batches are concatenated into one NHWC batch. Only two
+things couple samples, and both are kept per worker:
+
+* **BatchNorm statistics**: ``grouped_bn`` normalises each worker's rows with
+  that worker's own mean/variance (hand-written HIP kernels ``bn_nhwc.hip``, with
+  the ReLU and the residual add fused) and replays the k sequential running-stat
+  updates;
+* **parameter gradients**: the weight gradient of every layer is produced per
+  worker (one strided-batched GEMM per layer: directly for 1x1 convolutions and
+  the classifier, over an NHWC im2col gather (``im2col_nhwc.hip``) otherwise) and
+  lands in that worker's row of the exchange buffer through a ``GradSink``;
+  BatchNorm's dγ/dβ are written there directly by the finalize kernel.
+
+Activation gradients (dgrad) and forward convolutions run once on the whole
+batch (k-times larger GEMMs). The custom autograd functions take the real
+parameters as inputs (so the graph reaches them) but return ``None`` for them:
+nothing is accumulated into ``.grad``.
+
+CPU tensors take plain PyTorch implementations of the same math (used by the CPU
+test suite); on the GPU the native extension is mandatory.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from garfield_amd import _native
+from garfield_amd.utils.flat import is_dense
+
+# k x k convolutions of the grouped step on the GPU: "gemm" (HIP im2col/col2im +
+# hipBLASLt GEMMs, per-worker weight gradients in one batched GEMM) or "miopen"
+# (ATen/MIOpen convolutions, one weight-gradient call per worker). MIOpen's NHWC
+# solvers are not HIP-graph replay safe on ROCm 7 / gfx950 (non-finite weight
+# gradients from a replay on), so "miopen" is only for eager A/B runs.
+CONV_MODE = os.environ.get("GARFIELD_GROUPED_CONV", "gemm")
+
+
+def rows2d(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last tensor -> its [N*H*W, C] row view (no copy)."""
+    if t.dim() == 2:
+        return t
+    if not t.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("grouped layers need channels_last activations")
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def from_rows(t2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    """[N*H*W, C] rows -> [N, C, H, W] channels_last view."""
+    return t2.view(n, h, w, t2.shape[1]).permute(0, 3, 1, 2)
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    return t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t.contiguous()
+
+
+# --------------------------------------------------------------------------- #
+# Gradient sink: per-worker parameter gradients -> exchange-buffer rows
+
+
+class GradSink:
+    """Routes per-worker parameter gradients into the exchange buffer.
+
+    ``flat`` is the whole exchange buffer (1-D); worker g's row starts at
+    ``base + g * row_stride``; parameter p occupies ``[offset(p), offset(p) + numel)``
+    of a row, in the parameter's MEMORY order (the flat-parameter layout).
+    Dense per-worker gradient tensors are queued with ``put`` and written by one
+    multi-tensor cast kernel in ``flush``."""
+
+    def __init__(self, flat: torch.Tensor, row_stride: int, base: int, offsets: dict, groups: int):
+        self.flat = flat
+        self.row_stride = int(row_stride)
+        self.base = int(base)
+        self.offsets = offsets        # id(param) -> element offset inside a row
+        self.groups = int(groups)
+        self._srcs: list = []
+        self._offs: list = []
+
+    def offset(self, p: torch.Tensor) -> int:
+        return self.offsets[id(p)]
+
+    def row_offset(self, g: int, p: torch.Tensor) -> int:
+        return self.base + g * self.row_stride + self.offsets[id(p)]
+
+    def put(self, p: torch.Tensor, g: int, grad: torch.Tensor) -> None:
+        if grad.numel() != p.numel():
+            raise ValueError(f"gradient of {grad.numel()} elements for a parameter of {p.numel()}")
+        self._srcs.append(grad)
+        self._offs.append(self.row_offset(g, p))
+
+    def put_groups(self, p: torch.Tensor, grads) -> None:
+        """``grads``: [groups, ...] tensor or a list of per-group tensors."""
+        for g in range(self.groups):
+            self.put(p, g, grads[g])
+
+    def flush(self) -> None:
+        if not self._srcs:
+            return
+        if self.flat.is_cuda:
+            srcs = [s if is_dense(s) else s.contiguous() for s in self._srcs]
+            _native.native().gpu_flatten_cast_at(srcs, self._offs, self.flat)
+        else:
+            with torch.no_grad():
+                for s, o in zip(self._srcs, self._offs):
+                    v = _memory_order(s)
+                    self.flat[o:o + v.numel()].copy_(v)
+        self._srcs.clear()
+        self._offs.clear()
+
+
+def _memory_order(t: torch.Tensor) -> torch.Tensor:
+    if t.is_contiguous():
+        return t.reshape(-1)
+    perm = sorted(range(t.dim()), key=lambda i: -t.stride(i))
+    return t.permute(perm).reshape(-1)
+
+
+# --------------------------------------------------------------------------- #
+# Grouped BatchNorm (+ residual) (+ ReLU)
+
+
+class BNState:
+    """Per-layer buffers of a grouped BatchNorm (allocated once, reused: capture-safe)."""
+
+    def __init__(self, bn: torch.nn.BatchNorm2d, relu: bool, sink: GradSink | None, groups: int):
+        if bn.momentum is None:
+            raise ValueError("grouped BatchNorm needs a momentum (cumulative averaging is not supported)")
+        self.bn = bn
+        self.relu = relu
+        self.sink = sink
+        self.groups = groups
+        self.C = bn.num_features
+        self.mean = self.istd = self.scale = self.shift = None
+
+    def ensure(self, device, dtype=torch.float32) -> None:
+        if self.mean is None or self.mean.device != device or self.mean.dtype != dtype:
+            shape = (self.groups, self.C)
+            self.mean = torch.empty(shape, dtype=dtype, device=device)
+            self.istd = torch.empty_like(self.mean)
+            self.scale = torch.empty_like(self.mean)
+            self.shift = torch.empty_like(self.mean)
+
+
+class Workspace:
+    """Shared scratch (BatchNorm partial sums / backward coefficients)."""
+
+    def __init__(self):
+        self.t = {}
+
+    def get(self, name: str, numel: int, device) -> torch.Tensor:
+        t = self.t.get(name)
+        if t is None or t.numel() < numel or t.device != device:
+            t = torch.empty(max(int(numel), 1), dtype=torch.float32, device=device)
+            self.t[name] = t
+        return t
+
+
+def _acc(t: torch.Tensor) -> torch.Tensor:
+    """Accumulation dtype of the CPU reference path: fp64 stays fp64, the rest fp32."""
+    return t if t.dtype == torch.float64 else t.float()
+
+
+def _affine(bn, like):
+    gamma = bn.weight.detach().to(like.dtype) if bn.weight is not None else torch.ones_like(like)
+    beta = bn.bias.detach().to(like.dtype) if bn.bias is not None else torch.zeros_like(like)
+    return gamma, beta
+
+
+def _bn_fwd_ref(x2, r2, st: BNState):
+    """fp32 PyTorch reference of the grouped forward (CPU path)."""
+    bn, G = st.bn, st.groups
+    xg = _acc(x2).view(G, -1, st.C)
+    M = xg.shape[1]
+    mean = xg.mean(1)
+    var = xg.var(1, unbiased=False)
+    istd = torch.rsqrt(var + bn.eps)
+    gamma, beta = _affine(bn, mean[0])
+    scale = istd * gamma
+    shift = beta - mean * scale
+    y = xg * scale[:, None] + shift[:, None]
+    if r2 is not None:
+        y = y + _acc(r2).view(G, -1, st.C)
+    if st.relu:
+        y = y.clamp_min(0)
+    st.mean.copy_(mean)
+    st.istd.copy_(istd)
+    st.scale.copy_(scale)
+    st.shift.copy_(shift)
+    if bn.track_running_stats and bn.running_mean is not None:
+        m = bn.momentum
+        unb = var * M / max(M - 1, 1)
+        with torch.no_grad():
+            for g in range(G):
+                bn.running_mean.mul_(1 - m).add_(mean[g], alpha=m)
+                bn.running_var.mul_(1 - m).add_(unb[g], alpha=m)
+    return y.view(-1, st.C).to(x2.dtype)
+
+
+def _bn_bwd_ref(x2, dy2, y2, st: BNState, need_res: bool):
+    bn, G = st.bn, st.groups
+    xg = _acc(x2).view(G, -1, st.C)
+    dz = _acc(dy2).view(G, -1, st.C)
+    if st.relu:
+        dz = torch.where(y2.view(G, -1, st.C) > 0, dz, torch.zeros_like(dz))
+    M = xg.shape[1]
+    mean, istd = st.mean.to(xg.dtype), st.istd.to(xg.dtype)
+    xm = xg - mean[:, None]
+    A = dz.sum(1)
+    B = (dz * xm).sum(1)
+    dgamma = B * istd
+    dbeta = A
+    gamma, _ = _affine(bn, A[0])
+    dx = (gamma * istd)[:, None] * (dz - (A / M)[:, None] - xm * (istd * dgamma / M)[:, None])
+    if st.sink is not None:
+        with torch.no_grad():
+            for g in range(G):
+                if bn.weight is not None:
+                    o = st.sink.row_offset(g, bn.weight)
+                    st.sink.flat[o:o + st.C].copy_(dgamma[g])
+                if bn.bias is not None:
+                    o = st.sink.row_offset(g, bn.bias)
+                    st.sink.flat[o:o + st.C].copy_(dbeta[g])
+    dres = dz.reshape(-1, st.C).to(x2.dtype) if need_res else None
+    return dx.reshape(-1, st.C).to(x2.dtype), dres
+
+
+class _GroupedBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, st: BNState, ws: Workspace):
+        n, C, h, w = x.shape
+        x2 = rows2d(x)
+        r2 = rows2d(res) if res is not None else None
+        st.ensure(x.device, torch.float64 if x.dtype == torch.float64 else torch.float32)
+        if x.is_cuda:
+            if x.dtype != torch.bfloat16:
+                raise TypeError("grouped BatchNorm on the GPU takes bf16 activations")
+            y = torch.empty_like(x, memory_format=torch.channels_last)
+            bn = st.bn
+            rg = x2.shape[0] // st.groups
+            C_ = _native.native()
+            part = ws.get("bn_part", C_.bn_part_floats(rg, st.groups, C), x.device)
+            track = bn.track_running_stats and bn.running_mean is not None
+            C_.gpu_bn_forward(x2, r2, st.groups, bn.weight, bn.bias, float(bn.eps), float(bn.momentum),
+                              bn.running_mean if track else None, bn.running_var if track else None,
+                              part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu)
+        else:
+            y = from_rows(_bn_fwd_ref(x2, r2, st), n, h, w)
+        ctx.st, ctx.ws, ctx.has_res = st, ws, res is not None
+        ctx.save_for_backward(x, y if st.relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        st, ws = ctx.st, ctx.ws
+        n, C, h, w = x.shape
+        dy = _cl(dy)
+        x2, dy2 = rows2d(x), rows2d(dy)
+        y2 = rows2d(y) if y is not None else None
+        if x.is_cuda:
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+            rg = x2.shape[0] // st.groups
+            C_ = _native.native()
+            part = ws.get("bn_part", C_.bn_part_floats(rg, st.groups, C), x.device)
+            coef = ws.get("bn_coef", 3 * st.groups * C, x.device)
+            sink, bn = st.sink, st.bn
+            grow, stride, og, ob = None, 0, -1, -1
+            if sink is not None:
+                grow, stride = sink.flat, sink.row_stride
+                og = sink.base + sink.offset(bn.weight) if bn.weight is not None else -1
+                ob = sink.base + sink.offset(bn.bias) if bn.bias is not None else -1
+            C_.gpu_bn_backward(x2, dy2, y2, st.groups, bn.weight, st.mean, st.istd, part, coef, rows2d(dx),
+                               rows2d(dres) if dres is not None else None, grow, stride, og, ob)
+        else:
+            dx2, dr2 = _bn_bwd_ref(x2, dy2, y2, st, ctx.has_res)
+            dx = from_rows(dx2, n, h, w)
+            dres = from_rows(dr2, n, h, w) if dr2 is not None else None
+        return dx, None, None, dres, None, None
+
+
+def grouped_bn(x, st: BNState, ws: Workspace, res=None):
+    """y = [relu](BN_per_worker(x) [+ res]); x/res channels_last."""
+    return _GroupedBN.apply(_cl(x), st.bn.weight, st.bn.bias, _cl(res) if res is not None else None, st, ws)
+
+
+# --------------------------------------------------------------------------- #
+# Grouped convolution (per-worker weight gradients)
+
+
+class ConvSpec:
+    def __init__(self, conv: torch.nn.Conv2d, sink: GradSink | None, groups: int):
+        if conv.groups != 1 or conv.bias is not None:
+            raise ValueError("grouped convolution supports groups=1 convolutions without bias")
+        self.conv = conv
+        self.sink = sink
+        self.groups = groups
+        self.kernel = tuple(conv.kernel_size)
+        self.stride = tuple(conv.stride)
+        self.padding = tuple(conv.padding)
+        self.dilation = tuple(conv.dilation)
+        self.gemm = (self.kernel == (1, 1) and self.stride == (1, 1) and self.padding == (0, 0)
+                     and self.dilation == (1, 1))
+
+
+def _conv_bwd(dy, x, w, spec: ConvSpec, mask):
+    return torch.ops.aten.convolution_backward(dy, x, w, None, list(spec.stride), list(spec.padding),
+                                               list(spec.dilation), False, [0, 0], 1, mask)
+
+
+def _out_hw(spec: ConvSpec, h: int, w: int):
+    (kh, kw), (sh, sw), (ph, pw), (dh, dw) = spec.kernel, spec.stride, spec.padding, spec.dilation
+    return (h + 2 * ph - dh * (kh - 1) - 1) // sh + 1, (w + 2 * pw - dw * (kw - 1) - 1) // sw + 1
+
+
+def _geom(spec: ConvSpec):
+    return (*spec.kernel, *spec.stride, *spec.padding, *spec.dilation)
+
+
+def _im2col(x: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    """[N*Ho*Wo, Kp] bf16 col (Kp = KH*KW*C rounded up to 8, pad columns zero)."""
+    n, c, h, w = x.shape
+    ho, wo = _out_hw(spec, h, w)
+    K = spec.kernel[0] * spec.kernel[1] * c
+    col = torch.empty((n * ho * wo, (K + 7) // 8 * 8), dtype=x.dtype, device=x.device)
+    _native.native().gpu_im2col(x, *_geom(spec), col)
+    return col
+
+
+def _wmat(w: torch.Tensor, kp: int) -> torch.Tensor:
+    """channels_last weight [Cout, Cin, KH, KW] -> [Cout, Kp] in (kh, kw, ci) column order."""
+    w2 = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+    return F.pad(w2, (0, kp - w2.shape[1])) if kp != w2.shape[1] else w2
+
+
+def _channels_last_weight(w: torch.Tensor) -> bool:
+    return w.dim() == 4 and w.is_contiguous(memory_format=torch.channels_last)
+
+
+def _match_layout(g: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+    """A dense copy/view of gradient g with the same memory order as parameter p."""
+    if p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last) and not p.is_contiguous():
+        return g.contiguous(memory_format=torch.channels_last)
+    return g.contiguous()
+
+
+class _GroupedConv(torch.autograd.Function):
+    """Convolution over the grouped batch with per-worker weight gradients.
+
+    GPU, k x k kernels (``CONV_MODE == "gemm"``): im2col -> hipBLASLt GEMMs ->
+    col2im (im2col_nhwc.hip); the forward's col is kept for the weight gradient.
+    1x1 stride-1 kernels are plain GEMMs on the NHWC rows. CPU (and
+    ``CONV_MODE == "miopen"``): ATen convolutions, per-worker weight gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w, spec: ConvSpec):
+        ctx.spec = spec
+        ctx.xshape = tuple(x.shape)
+        n, _, h, wd = x.shape
+        if spec.gemm:
+            ctx.mode = "rows"
+            ctx.save_for_backward(x, w)
+            return from_rows(torch.mm(rows2d(x), w.reshape(w.shape[0], -1).t()), n, h, wd)
+        if x.is_cuda and CONV_MODE == "gemm" and _channels_last_weight(w):
+            ctx.mode = "col"
+            col = _im2col(x, spec)
+            ho, wo = _out_hw(spec, h, wd)
+            y = from_rows(torch.mm(col, _wmat(w, col.shape[1]).t()), n, ho, wo)
+            ctx.save_for_backward(col, w)
+            return y
+        ctx.mode = "aten"
+        ctx.save_for_backward(x, w)
+        return _cl(F.conv2d(x, w, None, spec.stride, spec.padding, spec.dilation))
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, w = ctx.saved_tensors
+        spec, mode = ctx.spec, ctx.mode
+        dy = _cl(dy)
+        G = spec.groups
+        cout = dy.shape[1]
+        dy2 = rows2d(dy)
+        n, cin, h, wd = ctx.xshape
+        dx = None
+        if mode == "rows":                       # a = x
+            if ctx.needs_input_grad[0]:
+                dx = from_rows(torch.mm(dy2, w.reshape(cout, -1)), n, h, wd)
+            if spec.sink is not None:
+                dW = torch.bmm(dy2.view(G, -1, cout).transpose(1, 2), rows2d(a).view(G, -1, cin))
+                spec.sink.put_groups(spec.conv.weight, dW)
+        elif mode == "col":                      # a = col [N*Ho*Wo, Kp]
+            kp = a.shape[1]
+            if ctx.needs_input_grad[0]:
+                dcol = torch.mm(dy2, _wmat(w, kp))
+                dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device).contiguous(
+                    memory_format=torch.channels_last)
+                _native.native().gpu_col2im(dcol, *_geom(spec), dx)
+            if spec.sink is not None:
+                # dW_g[co, (i, j, ci)] = Σ_rows dy_g[row, co] · col_g[row, (i, j, ci)]: the
+                # weight's channels_last memory order, one batched GEMM for all workers
+                dW = torch.bmm(dy2.view(G, -1, cout).transpose(1, 2), a.view(G, -1, kp))
+                K = w.numel() // cout
+                if kp != K:
+                    dW = dW[:, :, :K].contiguous()
+                spec.sink.put_groups(spec.conv.weight, dW)
+        else:                                    # a = x
+            if ctx.needs_input_grad[0]:
+                dx = _cl(_conv_bwd(dy, a, w, spec, [True, False, False])[0])
+            if spec.sink is not None:
+                B = a.shape[0] // G
+                for g in range(G):
+                    sl = slice(g * B, (g + 1) * B)
+                    dw = _conv_bwd(dy[sl], a[sl], w, spec, [False, True, False])[1]
+                    spec.sink.put(spec.conv.weight, g, _match_layout(dw, w))
+        return dx, None, None
+
+
+def grouped_conv(x, spec: ConvSpec):
+    return _GroupedConv.apply(_cl(x), spec.conv.weight, spec)
+
+
+# --------------------------------------------------------------------------- #
+# Grouped linear (classifier)
+
+
+class LinearSpec:
+    def __init__(self, lin: torch.nn.Linear, sink: GradSink | None, groups: int):
+        self.lin = lin
+        self.sink = sink
+        self.groups = groups
+
+
+class _GroupedLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, spec: LinearSpec):
+        ctx.spec = spec
+        ctx.save_for_backward(x, w)
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        spec = ctx.spec
+        G = spec.groups
+        dy = dy.contiguous()
+        dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
+        if spec.sink is not None:
+            out, fin = dy.shape[1], x.shape[1]
+            dy3 = dy.view(G, -1, out)
+            dW = torch.bmm(dy3.transpose(1, 2), x.contiguous().view(G, -1, fin))
+            spec.sink.put_groups(spec.lin.weight, dW)
+            if spec.lin.bias is not None:
+                spec.sink.put_groups(spec.lin.bias, _acc(dy3).sum(1))
+        return dx, None, None, None
+
+
+def grouped_linear(x, spec: LinearSpec):
+    return _GroupedLinear.apply(x, spec.lin.weight, spec.lin.bias, spec)

@@ -41,6 +41,8 @@ class ByzPSConfig(EngineConfig):
 
 
 class ByzantinePSDataParallel(RobustDataParallel):
+    _supports_grouping = False   # server ranks contribute no gradients: per-worker path only
+
     def __init__(self, model: nn.Module, loss_fn, ctx: DistContext, cfg: ByzPSConfig):
         if not (0 < cfg.num_ps < ctx.world_size):
             raise ValueError(f"need 0 < num_ps < world_size, got num_ps={cfg.num_ps} world={ctx.world_size}")

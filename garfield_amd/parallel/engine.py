@@ -73,17 +73,24 @@ class EngineConfig:
     drop_bn_counters: bool = True     # BatchNorm num_batches_tracked += 1 is a launch per BN per worker
     profile_phases: bool = False      # HIP-event timers: compute / exchange / gar_update (see phase_times())
     lp_weights: bool = True           # bf16/fp16 working copies of conv/linear weights, refreshed by the update kernel
+    # run the k local workers as ONE grouped NHWC batch (per-worker BN statistics and
+    # per-worker weight gradients; parallel/grouped.py) when the model supports it.
+    # None: on for GPU runs, off on CPU.
+    worker_batching: bool | None = None
 
 
 class RobustDataParallel:
     """Robust DP over one process per device (see module docstring)."""
+
+    _supports_grouping = True   # subclasses with their own step() opt out
 
     def __init__(self, model: nn.Module, loss_fn, ctx: DistContext, cfg: EngineConfig):
         self.ctx = ctx
         self.cfg = cfg
         self.device = ctx.device
         self.model = model.to(self.device)
-        if cfg.channels_last and self.device.type == "cuda":
+        self._grouping = self._want_grouping(self.model)
+        if (cfg.channels_last and self.device.type == "cuda") or self._grouping:
             self.model = self.model.to(memory_format=torch.channels_last)
         self.loss_fn = loss_fn
         if cfg.drop_bn_counters:
@@ -122,8 +129,37 @@ class RobustDataParallel:
         self._graph_failed = False
         self._static = None
         self._static_loss = None
+        self._gexec = None
+        if self._grouping:
+            self._init_grouped(loss_fn)
 
     # ------------------------------------------------------------------ #
+
+    def _want_grouping(self, model: nn.Module) -> bool:
+        from garfield_amd.parallel import grouped
+
+        wb = self.cfg.worker_batching
+        if wb is None:
+            wb = self.device.type == "cuda"
+        if not (wb and self._supports_grouping and grouped.supports(model)):
+            return False
+        if self.device.type == "cuda":
+            # bf16 activations with bf16 working weights (the grouped kernels' contract)
+            return self.cfg.lp_weights and self.cfg.autocast_dtype == torch.bfloat16
+        return True
+
+    def _init_grouped(self, loss_fn) -> None:
+        from garfield_amd.ops.grouped import GradSink
+        from garfield_amd.parallel.grouped import GroupedResNet
+
+        offsets = {id(p): off for p, off in zip(self.work_params, self.flat.offsets)}
+        sink = GradSink(self.X.view(-1), self.world * self.ld, self.rank * self.ld, offsets, self.k)
+        self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn)
+        self._gx = self._gy = None
+        self._gsrc = None
+        self._gsrc_refs = None
+        self._gloss = torch.zeros(self.k, dtype=torch.float32, device=self.device)
+        self._ggraph = None
 
     def _install_shadow(self) -> None:
         """Low-precision working weights for the matmul-shaped layers.
@@ -350,7 +386,12 @@ class RobustDataParallel:
         ResNet-50 worker become one graph launch. The RCCL all-gathers (overlapped
         with the next worker's graph) and the GAR + update stay eager (a handful
         of launches), so no collective is ever captured. New input tensors are
-        copied into the static buffers."""
+        copied into the static buffers.
+
+        With worker batching (``_grouped_step``) the k local workers are one
+        batched forward/backward instead, captured as ONE graph."""
+        if self._gexec is not None and self._groupable(batches):
+            return self._grouped_step(batches)
         if not self.graph_capturable() or self.step_count == 0:
             return self._eager_step(batches)
         if self._graph is None:
@@ -374,6 +415,104 @@ class RobustDataParallel:
         with self.timer.phase("gar_update"):
             self.aggregate_and_update()
         return self._static_loss.mean()
+
+    # ------------------------------------------------------------------ #
+    # Worker batching: the k local workers as one grouped batch
+
+    def _groupable(self, batches) -> bool:
+        if len(batches) != self.k:
+            return False
+        x0, y0 = batches[0]
+        return x0.dim() == 4 and all(x.shape == x0.shape and y.shape == y0.shape for x, y in batches)
+
+    def _stage_grouped(self, batches) -> None:
+        """Concatenate the k micro-batches into the static grouped input buffers
+        (skipped when the caller passes the very same, unmodified tensors again)."""
+        x0, y0 = batches[0]
+        B = x0.shape[0]
+        shape = (self.k * B, *x0.shape[1:])
+        if self._gx is None or tuple(self._gx.shape) != shape:
+            dt = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+            self._gx = torch.empty(shape, dtype=dt, device=self.device).contiguous(memory_format=torch.channels_last)
+            self._gy = torch.empty((self.k * B, *y0.shape[1:]), dtype=y0.dtype, device=self.device)
+            self._ggraph = None
+            self._gsrc = None
+        key = tuple((id(x), x._version, id(y), y._version) for x, y in batches)
+        if key != self._gsrc:
+            with torch.no_grad():
+                for j, (x, y) in enumerate(batches):
+                    self._gx[j * B:(j + 1) * B].copy_(x)
+                    self._gy[j * B:(j + 1) * B].copy_(y)
+            self._gsrc = key
+            self._gsrc_refs = [t for xy in batches for t in xy]  # keep ids valid while cached
+
+    def _grouped_step(self, batches) -> torch.Tensor:
+        cuda = self.device.type == "cuda"
+        self._stage_grouped(batches)
+        works = []
+        with self.timer.phase("compute"):
+            if (cuda and self.cfg.cuda_graph and not self._graph_failed and self.step_count >= 1
+                    and self._ggraph is None):
+                self._capture_grouped()
+            if self._ggraph is not None:
+                self._ggraph.replay()
+            else:
+                self._gexec.run(self._gx, self._gy, self._gloss)
+            self._attack_local_rows()
+            if self.world > 1:
+                works = [all_gather_rows(self.X[j], self.rank, async_op=True) for j in range(self.k)]
+        with self.timer.phase("exchange_wait"):
+            for w in works:
+                w.wait()
+        with self.timer.phase("gar_update"):
+            self.aggregate_and_update()
+        return self._gloss.mean()
+
+    def _attack_local_rows(self) -> None:
+        """Overwrite the simulated Byzantine workers' rows (after the honest rows exist)."""
+        cfg = self.cfg
+        for j in self.local_slots:
+            attack = cfg.byzantine.get(self.slot(j))
+            if attack is None:
+                continue
+            row = self.X[j, self.rank, : self.d]
+            g = row.float()
+            est = None
+            if attack in NEEDS_ESTIMATES:
+                honest = [self.X[i, self.rank, : self.d] for i in self.local_slots
+                          if self.slot(i) not in cfg.byzantine and i != j]
+                est = torch.stack([g] + [h.float() for h in honest])
+            row.copy_(apply_attack(attack, g, est, self._gen))
+
+    def _capture_grouped(self) -> None:
+        """Capture the grouped forward/backward (+ gradient scatter) as one HIP graph."""
+        from garfield_amd.utils.logging import warning
+
+        bns = [m for m in self.model.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)
+               and m.running_mean is not None]
+        saved = [(m.running_mean.clone(), m.running_var.clone()) for m in bns]
+        torch.cuda.synchronize()
+        try:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):  # warm-up on the capture stream (per-stream library state)
+                self._gexec.run(self._gx, self._gy, self._gloss)
+            s.synchronize()
+            g = torch.cuda.CUDAGraph()
+            mode = "thread_local" if self.world > 1 else "global"
+            with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
+                self._gexec.run(self._gx, self._gy, self._gloss)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._ggraph = g
+        except Exception as e:  # capture unsupported: stay eager
+            warning(f"HIP graph capture of the grouped step failed, running eagerly: {e!r}")
+            self._graph_failed = True
+            self._ggraph = None
+        torch.cuda.synchronize()
+        with torch.no_grad():  # the warm-up pass must not count as an extra step of the running statistics
+            for m, (rm, rv) in zip(bns, saved):
+                m.running_mean.copy_(rm)
+                m.running_var.copy_(rv)
 
     def _worker_body(self, j: int, x, y, loss_out: torch.Tensor) -> None:
         """fwd + bwd of local worker j, gradient flattened (and attacked) into its row."""

@@ -1,0 +1,121 @@
+"""Grouped execution of a rank's k logical workers (ResNet family).
+
+The engine's per-worker loop (``engine.RobustDataParallel.compute_local``) runs k
+independent forward/backward passes per step; for ResNet-50 on CIFAR-shape
+micro-batches that is ~7.5k small kernels per step on one MI355X, and the step is
+bound by kernel boundaries, not by the matrix cores. ``GroupedResNet`` runs the
+same k workers as ONE NHWC batch with per-worker BatchNorm statistics and
+per-worker parameter gradients (``garfield_amd.ops.grouped``), which is the same
+math as k separate workers (tests/test_grouped_cpu.py checks it against k
+sequential standard forward/backward passes, running statistics included).
+
+Reference counterpart: one ``Worker.compute_gradients`` per worker process
+(``pytorch_impl/libs/garfieldpp/worker.py:77-96``) on the reference's ResNet
+models (``models/resnet.py``; torchvision ``resnet50`` for ``resnet50``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
+from garfield_amd.ops.grouped import (BNState, ConvSpec, GradSink, LinearSpec, Workspace, grouped_bn, grouped_conv,
+                                      grouped_linear)
+
+
+def supports(model: nn.Module) -> bool:
+    """True for the zoo's ResNets with layers the grouped kernels handle."""
+    if not isinstance(model, ResNet):
+        return False
+    for m in model.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            if m.num_features % 8 or m.momentum is None or not m.affine:
+                return False
+        elif isinstance(m, nn.Conv2d):
+            if m.groups != 1 or m.bias is not None:
+                return False
+    for layer in (model.layer1, model.layer2, model.layer3, model.layer4):
+        for blk in layer:
+            if not isinstance(blk, (BasicBlock, Bottleneck)):
+                return False
+    return isinstance(model.maxpool, (nn.MaxPool2d, nn.Identity))
+
+
+class GroupedResNet:
+    """Forward + backward of ``groups`` workers' micro-batches in one pass.
+
+    ``run(x, y)`` takes the concatenated inputs (worker g = rows [g*B, (g+1)*B),
+    channels_last) and labels, writes every worker's parameter gradient into its
+    exchange row through ``sink`` and returns the per-worker mean losses."""
+
+    def __init__(self, model: ResNet, groups: int, sink: GradSink, loss_fn=F.cross_entropy):
+        if not supports(model):
+            raise ValueError("GroupedResNet supports the zoo's ResNet models only")
+        self.model = model
+        self.groups = int(groups)
+        self.sink = sink
+        self.loss_fn = loss_fn
+        self.ws = Workspace()
+        self.conv = {m: ConvSpec(m, sink, self.groups) for m in model.modules() if isinstance(m, nn.Conv2d)}
+        self.fc = LinearSpec(model.fc, sink, self.groups)
+        self.bn: dict = {}
+
+    # ------------------------------------------------------------------ #
+
+    def _bn(self, x, bn: nn.BatchNorm2d, relu: bool, res=None):
+        st = self.bn.get(bn)
+        if st is None:
+            st = self.bn[bn] = BNState(bn, relu, self.sink, self.groups)
+        return grouped_bn(x, st, self.ws, res)
+
+    def _conv(self, x, conv: nn.Conv2d):
+        return grouped_conv(x, self.conv[conv])
+
+    def _block(self, blk, x):
+        out = self._bn(self._conv(x, blk.conv1), blk.bn1, True)
+        if isinstance(blk, Bottleneck):
+            out = self._bn(self._conv(out, blk.conv2), blk.bn2, True)
+            last_conv, last_bn = blk.conv3, blk.bn3
+        else:
+            last_conv, last_bn = blk.conv2, blk.bn2
+        if blk.downsample is None:
+            sc = x
+        else:
+            sc = self._bn(self._conv(x, blk.downsample[0]), blk.downsample[1], False)
+        return self._bn(self._conv(out, last_conv), last_bn, True, sc)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        m = self.model
+        x = self._bn(self._conv(x, m.conv1), m.bn1, True)
+        if isinstance(m.maxpool, nn.MaxPool2d):
+            mp = m.maxpool
+            x = F.max_pool2d(x, mp.kernel_size, mp.stride, mp.padding, mp.dilation, mp.ceil_mode)
+            x = x.contiguous(memory_format=torch.channels_last)
+        for layer in (m.layer1, m.layer2, m.layer3, m.layer4):
+            for blk in layer:
+                x = self._block(blk, x)
+        n, c, h, w = x.shape
+        pooled = x.reshape(n, c) if h * w == 1 else x.mean((2, 3))
+        return grouped_linear(pooled, self.fc)
+
+    def losses(self, logits: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        G = self.groups
+        if logits.dtype != torch.float64:
+            logits = logits.float()
+        if self.loss_fn is F.cross_entropy:
+            return F.cross_entropy(logits, y, reduction="none").view(G, -1).mean(1)
+        lg = logits.view(G, -1, logits.shape[-1])
+        yg = y.view(G, -1, *y.shape[1:])
+        return torch.stack([self.loss_fn(lg[g], yg[g]) for g in range(G)])
+
+    def run(self, x: torch.Tensor, y: torch.Tensor, loss_out: torch.Tensor | None = None) -> torch.Tensor:
+        if x.shape[0] % self.groups:
+            raise ValueError(f"batch of {x.shape[0]} rows is not divisible into {self.groups} workers")
+        per = self.losses(self.forward(x), y)
+        per.sum().backward()
+        self.sink.flush()
+        per = per.detach()
+        if loss_out is not None:
+            loss_out.copy_(per)
+        return per

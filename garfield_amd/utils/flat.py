@@ -124,8 +124,11 @@ class FlatParams:
             self.attach_grads(self.grad)
 
     def views(self, flat: torch.Tensor):
+        """Per-parameter views (parameter strides) of a flat buffer laid out like ``data``;
+        ``flat`` may itself be a view (e.g. one row of a 2-D buffer)."""
+        base = flat.storage_offset()
         for size, stride, off in zip(self.sizes, self.strides, self.offsets):
-            yield torch.as_strided(flat, size, stride, off)
+            yield torch.as_strided(flat, size, stride, base + off)
 
     def attach_grads(self, flat: torch.Tensor) -> None:
         """Point every ``p.grad`` at its slice of ``flat`` (backward accumulates in place)."""

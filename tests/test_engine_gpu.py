@@ -97,7 +97,8 @@ def test_engine_cuda_graph_matches_eager(cuda, rule):
     outs = []
     for graph in (False, False, True):
         torch.manual_seed(0)
-        cfg = EngineConfig(gar=rule, f=1, workers_per_rank=5, cuda_graph=graph, byzantine={4: "reverse"}, lr=1e-3)
+        cfg = EngineConfig(gar=rule, f=1, workers_per_rank=5, cuda_graph=graph, byzantine={4: "reverse"}, lr=1e-3,
+                           worker_batching=False)
         eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
         b = synthetic_batches(5, 8, (3, 32, 32), 10, cuda)
         init = eng.flat.reference_vector().clone()
