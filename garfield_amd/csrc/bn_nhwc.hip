@@ -11,9 +11,10 @@
 // Here one layer costs three launches FOR ALL k WORKERS, forward and backward:
 //
 //   forward : partial (sum, sum of squares) per (worker, channel, row chunk)
-//             -> finalize (mean, 1/std, scale/shift, running-stat update that
-//                replays the k sequential worker updates)
-//             -> apply  y = relu(x*scale + shift [+ residual])      (bf16x8 I/O)
+//             -> finalize (mean, 1/std, scale/shift per worker and channel)
+//             -> apply  y = relu(x*scale + shift [+ residual])      (bf16x8 I/O);
+//                its first workgroup also replays the k sequential running-stat
+//                updates of k independent workers
 //   backward: partial (Σdz, Σdz·(x-μ)) with dz = dy·[y > 0]
 //             -> finalize (dγ, dβ per worker, written STRAIGHT into each
 //                worker's row of the gradient exchange buffer; apply coefficients)
@@ -176,58 +177,109 @@ __global__ __launch_bounds__(kThreads) void k_partial(const uint16_t* __restrict
   }
 }
 
-// Forward finalize: one thread per channel, groups in order (replays the k
-// sequential running-stat updates of k independent workers).
-__global__ __launch_bounds__(kThreads) void k_fwd_finalize(const float* __restrict__ part, const uint16_t* __restrict__ x,
-                                                          Geo geo, const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float eps, float momentum,
-                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                          float* __restrict__ mean, float* __restrict__ istd,
-                                                          float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * kThreads + threadIdx.x;
+// Finalize workgroups: 64 channels x 4 chunk lanes for ONE group (blockIdx.y),
+// every chunk load issued before it is consumed (the chunk sums are a
+// latency-bound gather otherwise), lanes reduced through LDS in a fixed order.
+constexpr int kFinCh = 64;
+constexpr int kFinLanes = kThreads / kFinCh;  // 4
+
+__device__ __forceinline__ void chunk_sums(const float* __restrict__ part, const Geo& geo, int g, int c, float* sred,
+                                           float* qred, float& S, float& Q) {
+  const int tc = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
   const int C = geo.C;
-  if (c >= C) return;
-  const float M = static_cast<float>(geo.rg);
-  const float gm = gamma ? gamma[c] : 1.f;
-  const float bt = beta ? beta[c] : 0.f;
-  float rm = run_mean ? run_mean[c] : 0.f;
-  float rv = run_var ? run_var[c] : 0.f;
-  for (int g = 0; g < geo.groups; ++g) {
-    float S = 0.f, Q = 0.f;
-    for (int ch = 0; ch < geo.chunks; ++ch) {
-      const int64_t o = (static_cast<int64_t>(g) * geo.chunks + ch) * 2 * C;
-      S += part[o + c];
-      Q += part[o + C + c];
-    }
-    const float sh = bf16_to_f(x[static_cast<int64_t>(g) * geo.rg * C + c]);
-    const float m1 = S / M;
-    float var = Q / M - m1 * m1;
-    var = var > 0.f ? var : 0.f;
-    const float mu = sh + m1;
-    const float is = rsqrtf(var + eps);
-    const int64_t gc = static_cast<int64_t>(g) * C + c;
-    mean[gc] = mu;
-    istd[gc] = is;
-    const float sc = gm * is;
-    scale[gc] = sc;
-    shift[gc] = bt - mu * sc;
-    if (run_mean) {
-      const float unb = geo.rg > 1 ? var * M / (M - 1.f) : var;
-      rm = (1.f - momentum) * rm + momentum * mu;
-      rv = (1.f - momentum) * rv + momentum * unb;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    for (int ch0 = lane; ch0 < geo.chunks; ch0 += kFinLanes * 8) {
+      float a[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int ch = ch0 + kFinLanes * u;
+        const int64_t o = (static_cast<int64_t>(g) * geo.chunks + ch) * 2 * C;
+        a[u] = ch < geo.chunks ? part[o + c] : 0.f;
+        b[u] = ch < geo.chunks ? part[o + C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { s += a[u]; q += b[u]; }
     }
   }
-  if (run_mean) { run_mean[c] = rm; run_var[c] = rv; }
+  sred[lane * kFinCh + tc] = s;
+  qred[lane * kFinCh + tc] = q;
+  __syncthreads();
+  S = 0.f;
+  Q = 0.f;
+#pragma unroll
+  for (int l = 0; l < kFinLanes; ++l) { S += sred[l * kFinCh + tc]; Q += qred[l * kFinCh + tc]; }
+}
+
+// Forward finalize of one (group, 64-channel block): mean, 1/std, scale, shift.
+__global__ __launch_bounds__(kThreads) void k_fwd_finalize(const float* __restrict__ part, const uint16_t* __restrict__ x,
+                                                          Geo geo, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          float* __restrict__ mean, float* __restrict__ istd,
+                                                          float* __restrict__ scale, float* __restrict__ shift) {
+  __shared__ float sred[kThreads], qred[kThreads];
+  const int C = geo.C;
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  float S, Q;
+  chunk_sums(part, geo, g, c, sred, qred, S, Q);
+  if (threadIdx.x >= kFinCh || c >= C) return;
+  const float M = static_cast<float>(geo.rg);
+  const float sh = bf16_to_f(x[static_cast<int64_t>(g) * geo.rg * C + c]);
+  const float m1 = S / M;
+  float var = Q / M - m1 * m1;
+  var = var > 0.f ? var : 0.f;
+  const float mu = sh + m1;
+  const float is = rsqrtf(var + eps);
+  const int64_t gc = static_cast<int64_t>(g) * C + c;
+  mean[gc] = mu;
+  istd[gc] = is;
+  const float sc = (gamma ? gamma[c] : 1.f) * is;
+  scale[gc] = sc;
+  shift[gc] = (beta ? beta[c] : 0.f) - mu * sc;
+}
+
+// Running statistics: the k sequential updates of k independent workers, in
+// worker order (run by the first workgroup of the apply pass).
+__device__ __forceinline__ void running_update(const float* __restrict__ mean, const float* __restrict__ istd,
+                                               int groups, int C, int64_t rg, float eps, float momentum,
+                                               float* __restrict__ run_mean, float* __restrict__ run_var) {
+  const float M = static_cast<float>(rg);
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    float rm = run_mean[c], rv = run_var[c];
+    for (int g = 0; g < groups; ++g) {
+      const float is = istd[static_cast<int64_t>(g) * C + c];
+      float var = 1.f / (is * is) - eps;
+      var = var > 0.f ? var : 0.f;
+      const float unb = rg > 1 ? var * M / (M - 1.f) : var;
+      rm = (1.f - momentum) * rm + momentum * mean[static_cast<int64_t>(g) * C + c];
+      rv = (1.f - momentum) * rv + momentum * unb;
+    }
+    run_mean[c] = rm;
+    run_var[c] = rv;
+  }
 }
 
 // Elementwise passes over [R, C]: each workgroup owns kApplyIters x rp rows.
 constexpr int kApplyIters = 4;
 
+struct RunStats {
+  const float* mean;
+  const float* istd;
+  float* run_mean;
+  float* run_var;
+  float eps;
+  float momentum;
+  int groups;
+};
+
 template <bool RES, bool RELU>
 __global__ __launch_bounds__(kThreads) void k_fwd_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        int64_t rg, int64_t R, int C, int tch, int rp,
-                                                       uint16_t* __restrict__ y) {
+                                                       uint16_t* __restrict__ y, RunStats rs) {
+  if (blockIdx.x == 0 && rs.run_mean)
+    running_update(rs.mean, rs.istd, rs.groups, C, rg, rs.eps, rs.momentum, rs.run_mean, rs.run_var);
   const int tr = threadIdx.x / tch;
   if (tr >= rp) return;
   const int nv = C / 8;
@@ -262,37 +314,33 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const uint16_t* __restri
   }
 }
 
-// Backward finalize: per (group, channel) dγ, dβ -> exchange rows; apply coefficients.
+// Backward finalize of one (group, 64-channel block): dγ, dβ -> exchange rows;
+// apply coefficients.
 __global__ __launch_bounds__(kThreads) void k_bwd_finalize(const float* __restrict__ part, Geo geo,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ istd,
                                                           float* __restrict__ coef, void* grow, int grow_dt,
                                                           int64_t row_stride, int64_t off_gamma, int64_t off_beta) {
-  const int c = blockIdx.x * kThreads + threadIdx.x;
+  __shared__ float sred[kThreads], qred[kThreads];
   const int C = geo.C;
-  if (c >= C) return;
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  float A, B;
+  chunk_sums(part, geo, g, c, sred, qred, A, B);
+  if (threadIdx.x >= kFinCh || c >= C) return;
   const float M = static_cast<float>(geo.rg);
-  const float gm = gamma ? gamma[c] : 1.f;
-  for (int g = 0; g < geo.groups; ++g) {
-    float A = 0.f, B = 0.f;
-    for (int ch = 0; ch < geo.chunks; ++ch) {
-      const int64_t o = (static_cast<int64_t>(g) * geo.chunks + ch) * 2 * C;
-      A += part[o + c];
-      B += part[o + C + c];
-    }
-    const int64_t gc = static_cast<int64_t>(g) * C + c;
-    const float is = istd[gc];
-    const float dgamma = B * is;
-    const float dbeta = A;
-    if (grow) {
-      if (off_gamma >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_gamma + c, dgamma);
-      if (off_beta >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_beta + c, dbeta);
-    }
-    const int64_t o3 = static_cast<int64_t>(g) * 3 * C;
-    coef[o3 + c] = gm * is;                  // a
-    coef[o3 + C + c] = dbeta / M;            // b
-    coef[o3 + 2 * C + c] = dgamma / M * is;  // c  (x̂·dγ/M = (x-μ)·c)
+  const int64_t gc = static_cast<int64_t>(g) * C + c;
+  const float is = istd[gc];
+  const float dgamma = B * is;
+  const float dbeta = A;
+  if (grow) {
+    if (off_gamma >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_gamma + c, dgamma);
+    if (off_beta >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_beta + c, dbeta);
   }
+  const int64_t o3 = static_cast<int64_t>(g) * 3 * C;
+  coef[o3 + c] = (gamma ? gamma[c] : 1.f) * is;  // a
+  coef[o3 + C + c] = dbeta / M;                 // b
+  coef[o3 + 2 * C + c] = dgamma / M * is;       // c  (x̂·dγ/M = (x-μ)·c)
 }
 
 template <bool RELU, bool RES_OUT>
@@ -362,18 +410,20 @@ void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, 
   const int ncb = (C + g.cb - 1) / g.cb;
   hipLaunchKernelGGL((k_partial<false, false>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
                      nullptr, nullptr, g, part);
-  hipLaunchKernelGGL(k_fwd_finalize, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, part, x, g,
-                     gamma, beta, eps, momentum, run_mean, run_var, mean, istd, scale, shift);
+  const dim3 fgrid((C + kFinCh - 1) / kFinCh, groups);
+  hipLaunchKernelGGL(k_fwd_finalize, fgrid, dim3(kThreads), 0, stream, part, x, g, gamma, beta, eps, mean, istd,
+                     scale, shift);
+  const RunStats rs{mean, istd, run_mean, run_var, eps, momentum, groups};
   int tch, rp;
   apply_geometry(C, &tch, &rp);
   const int64_t R = rg * groups;
   const dim3 grid = apply_grid(R, rp);
   if (res) {
-    if (relu) hipLaunchKernelGGL((k_fwd_apply<true, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y);
-    else hipLaunchKernelGGL((k_fwd_apply<true, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y);
+    if (relu) hipLaunchKernelGGL((k_fwd_apply<true, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, rs);
+    else hipLaunchKernelGGL((k_fwd_apply<true, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, rs);
   } else {
-    if (relu) hipLaunchKernelGGL((k_fwd_apply<false, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y);
-    else hipLaunchKernelGGL((k_fwd_apply<false, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y);
+    if (relu) hipLaunchKernelGGL((k_fwd_apply<false, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, rs);
+    else hipLaunchKernelGGL((k_fwd_apply<false, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, rs);
   }
 }
 
@@ -386,8 +436,8 @@ void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, int64
   const bool relu = y != nullptr;
   if (relu) hipLaunchKernelGGL((k_partial<true, true>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, dy, y, mean, g, part);
   else hipLaunchKernelGGL((k_partial<true, false>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, dy, y, mean, g, part);
-  hipLaunchKernelGGL(k_bwd_finalize, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, part, g, gamma,
-                     istd, coef, grow, grow_dt, row_stride, off_gamma, off_beta);
+  hipLaunchKernelGGL(k_bwd_finalize, dim3((C + kFinCh - 1) / kFinCh, groups), dim3(kThreads), 0, stream, part, g,
+                     gamma, istd, coef, grow, grow_dt, row_stride, off_gamma, off_beta);
   int tch, rp;
   apply_geometry(C, &tch, &rp);
   const int64_t R = rg * groups;

@@ -402,8 +402,7 @@ class _GroupedConv(torch.autograd.Function):
             kp = a.shape[1]
             if ctx.needs_input_grad[0]:
                 dcol = torch.mm(dy2, _wmat(w, kp))
-                dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device).contiguous(
-                    memory_format=torch.channels_last)
+                dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
                 _native.native().gpu_col2im(dcol, *_geom(spec), dx)
             if spec.sink is not None:
                 # dW_g[co, (i, j, ci)] = Σ_rows dy_g[row, co] · col_g[row, (i, j, ci)]: the

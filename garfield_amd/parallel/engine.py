@@ -433,7 +433,7 @@ class RobustDataParallel:
         shape = (self.k * B, *x0.shape[1:])
         if self._gx is None or tuple(self._gx.shape) != shape:
             dt = torch.bfloat16 if self.device.type == "cuda" else torch.float32
-            self._gx = torch.empty(shape, dtype=dt, device=self.device).contiguous(memory_format=torch.channels_last)
+            self._gx = torch.empty(shape, dtype=dt, device=self.device, memory_format=torch.channels_last)
             self._gy = torch.empty((self.k * B, *y0.shape[1:]), dtype=y0.dtype, device=self.device)
             self._ggraph = None
             self._gsrc = None
