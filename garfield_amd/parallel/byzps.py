@@ -42,6 +42,7 @@ class ByzPSConfig(EngineConfig):
 
 class ByzantinePSDataParallel(RobustDataParallel):
     _supports_grouping = False   # server ranks contribute no gradients: per-worker path only
+    _supports_sharding = False   # servers aggregate the worker rows themselves (all-gather form)
 
     def __init__(self, model: nn.Module, loss_fn, ctx: DistContext, cfg: ByzPSConfig):
         if not (0 < cfg.num_ps < ctx.world_size):

@@ -77,12 +77,17 @@ class EngineConfig:
     # per-worker weight gradients; parallel/grouped.py) when the model supports it.
     # None: on for GPU runs, off on CPU.
     worker_batching: bool | None = None
+    # world > 1: aggregate sharded (all-to-all of coordinate shards, partial Gram
+    # all-reduce, sharded update, all-gather of the master; parallel/sharded.py)
+    # instead of all-gathering every gradient to every rank. None: on when world > 1.
+    shard_gar: bool | None = None
 
 
 class RobustDataParallel:
     """Robust DP over one process per device (see module docstring)."""
 
     _supports_grouping = True   # subclasses with their own step() opt out
+    _supports_sharding = True
 
     def __init__(self, model: nn.Module, loss_fn, ctx: DistContext, cfg: EngineConfig):
         self.ctx = ctx
@@ -97,22 +102,32 @@ class RobustDataParallel:
             for mod in self.model.modules():
                 if isinstance(mod, nn.modules.batchnorm._BatchNorm) and mod.momentum is not None:
                     mod.num_batches_tracked = None  # only read when momentum is None
-        self.flat = FlatParams(self.model, device=self.device, with_grad=False)
+        self._sharded = self._want_sharded()
+        from garfield_amd.parallel.sharded import shard_pad
+
+        pad = shard_pad(ctx.world_size) if self._sharded else 64
+        self.flat = FlatParams(self.model, device=self.device, with_grad=False, pad=pad)
         if ctx.is_distributed:
             dist.broadcast(self.flat.data, src=0)
         self.d, self.ld = self.flat.d, self.flat.ld
         self.work_params = list(self.flat.params)   # what forward/backward sees (see _install_shadow)
         self._shadow = None
         self._install_shadow()
-        self.mom = torch.zeros(self.ld, dtype=torch.float32, device=self.device)
         self.k = cfg.workers_per_rank
         self.world = ctx.world_size
         self.rank = ctx.rank
         self.n = self.k * self.world
         if self.n > gar.MAX_ROWS and self.device.type == "cuda":
             raise ValueError(f"at most {gar.MAX_ROWS} logical workers per job on the GPU path, got {self.n}")
-        self.X = torch.zeros((self.k, self.world, self.ld), dtype=cfg.exchange_dtype, device=self.device)
-        self.G = self.X.view(self.n, self.ld)[:, : self.d]          # [n, d] GAR input (slot-major)
+        # momentum: the whole vector, or this rank's shard when the aggregation is sharded
+        self.mom = torch.zeros(self.ld // self.world if self._sharded else self.ld, dtype=torch.float32,
+                               device=self.device)
+        # exchange buffer X[k, world, ld]: row (j, rank) is local worker j's gradient; the
+        # sharded form keeps the local rows only (X[k, 1, ld]) and all-to-alls shards of them
+        self.xr = 0 if self._sharded else self.rank
+        self.X = torch.zeros((self.k, 1 if self._sharded else self.world, self.ld), dtype=cfg.exchange_dtype,
+                             device=self.device)
+        self.G = None if self._sharded else self.X.view(self.n, self.ld)[:, : self.d]  # [n, d] GAR input
         # local slot order: honest workers first so colluders see their estimates
         self.local_slots = sorted(range(self.k), key=lambda j: (self.slot(j) in cfg.byzantine, j))
         self.step_count = 0
@@ -132,6 +147,11 @@ class RobustDataParallel:
         self._gexec = None
         if self._grouping:
             self._init_grouped(loss_fn)
+        self._shard = None
+        if self._sharded:
+            from garfield_amd.parallel.sharded import ShardedAggregator
+
+            self._shard = ShardedAggregator(self)
 
     # ------------------------------------------------------------------ #
 
@@ -148,12 +168,37 @@ class RobustDataParallel:
             return self.cfg.lp_weights and self.cfg.autocast_dtype == torch.bfloat16
         return True
 
+    def _want_sharded(self) -> bool:
+        from garfield_amd.parallel.sharded import SUPPORTED
+
+        sg = self.cfg.shard_gar
+        if sg is None:   # default: on for multi-rank jobs
+            sg = self.ctx.world_size > 1 and self.ctx.is_distributed
+        if not (sg and self._supports_sharding):
+            return False
+        if self.ctx.world_size > 1 and not self.ctx.is_distributed:
+            raise ValueError("sharded aggregation over several ranks needs an initialised process group")
+        if self.cfg.gar not in SUPPORTED:
+            raise ValueError(f"sharded aggregation does not support {self.cfg.gar!r} (shard_gar=False)")
+        return True
+
+    def _gather_slot(self, j: int):
+        """Start the all-gather of local worker j's slot (unsharded form only)."""
+        if self.world == 1 or self._sharded:
+            return None
+        return all_gather_rows(self.X[j], self.rank, async_op=True)
+
+    def momentum_vector(self) -> torch.Tensor:
+        """The full momentum buffer (all-gathered when the optimizer state is sharded)."""
+        return self._shard.momentum_vector() if self._shard is not None else self.mom
+
     def _init_grouped(self, loss_fn) -> None:
         from garfield_amd.ops.grouped import GradSink
         from garfield_amd.parallel.grouped import GroupedResNet
 
         offsets = {id(p): off for p, off in zip(self.work_params, self.flat.offsets)}
-        sink = GradSink(self.X.view(-1), self.world * self.ld, self.rank * self.ld, offsets, self.k)
+        nrow = self.X.shape[1]
+        sink = GradSink(self.X.view(-1), nrow * self.ld, self.xr * self.ld, offsets, self.k)
         self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn)
         self._gx = self._gy = None
         self._gsrc = None
@@ -243,7 +288,7 @@ class RobustDataParallel:
                 loss = self.loss_fn(self.model(x), y)
                 loss.backward()
                 losses.append(loss.detach())
-                row = self.X[j, self.rank, : self.d]
+                row = self.X[j, self.xr, : self.d]
                 attack = self.cfg.byzantine.get(self.slot(j))
                 if attack is None:
                     self._write_row(row)
@@ -251,12 +296,13 @@ class RobustDataParallel:
                     g = self._grad_vector()
                     est = None
                     if attack in NEEDS_ESTIMATES:
-                        honest = [self.X[i, self.rank, : self.d] for i in self.local_slots
+                        honest = [self.X[i, self.xr, : self.d] for i in self.local_slots
                                   if self.slot(i) not in self.cfg.byzantine and i != j]
                         est = torch.stack([g] + [h.float() for h in honest])
                     row.copy_(apply_attack(attack, g, est, self._gen))
-                if self.world > 1:
-                    works.append(all_gather_rows(self.X[j], self.rank, async_op=True))
+                w = self._gather_slot(j)
+                if w is not None:
+                    works.append(w)
         for p in params:
             p.grad = None
         for w in works:
@@ -283,6 +329,10 @@ class RobustDataParallel:
         """Run the GAR on the gathered [n, d] gradients and apply the SGD update."""
         cfg = self.cfg
         first = self.step_count == 0
+        if self._shard is not None:
+            self._shard.aggregate_and_update(first)
+            self.step_count += 1
+            return
         rule = cfg.gar
         kw = dict(cfg.gar_kwargs)
         if self.device.type == "cuda":
@@ -407,8 +457,9 @@ class RobustDataParallel:
                     sx.copy_(x, non_blocking=True)
                     sy.copy_(y, non_blocking=True)
                 self._graph[j].replay()
-                if self.world > 1:
-                    works.append(all_gather_rows(self.X[j], self.rank, async_op=True))
+                w = self._gather_slot(j)
+                if w is not None:
+                    works.append(w)
         with self.timer.phase("exchange_wait"):
             for w in works:
                 w.wait()
@@ -459,8 +510,7 @@ class RobustDataParallel:
             else:
                 self._gexec.run(self._gx, self._gy, self._gloss)
             self._attack_local_rows()
-            if self.world > 1:
-                works = [all_gather_rows(self.X[j], self.rank, async_op=True) for j in range(self.k)]
+            works = [w for w in (self._gather_slot(j) for j in range(self.k)) if w is not None]
         with self.timer.phase("exchange_wait"):
             for w in works:
                 w.wait()
@@ -475,11 +525,11 @@ class RobustDataParallel:
             attack = cfg.byzantine.get(self.slot(j))
             if attack is None:
                 continue
-            row = self.X[j, self.rank, : self.d]
+            row = self.X[j, self.xr, : self.d]
             g = row.float()
             est = None
             if attack in NEEDS_ESTIMATES:
-                honest = [self.X[i, self.rank, : self.d] for i in self.local_slots
+                honest = [self.X[i, self.xr, : self.d] for i in self.local_slots
                           if self.slot(i) not in cfg.byzantine and i != j]
                 est = torch.stack([g] + [h.float() for h in honest])
             row.copy_(apply_attack(attack, g, est, self._gen))
@@ -524,7 +574,7 @@ class RobustDataParallel:
             loss = self.loss_fn(self.model(x), y)
         loss.backward()
         loss_out.copy_(loss.detach().float())
-        row = self.X[j, self.rank, : self.d]
+        row = self.X[j, self.xr, : self.d]
         attack = self.cfg.byzantine.get(self.slot(j))
         if attack is None:
             self._write_row(row)
@@ -532,7 +582,7 @@ class RobustDataParallel:
             g = self._grad_vector()
             est = None
             if attack in NEEDS_ESTIMATES:
-                honest = [self.X[i, self.rank, : self.d] for i in self.local_slots
+                honest = [self.X[i, self.xr, : self.d] for i in self.local_slots
                           if self.slot(i) not in self.cfg.byzantine and i != j]
                 est = torch.stack([g] + [h.float() for h in honest])
             row.copy_(apply_attack(attack, g, est, None))

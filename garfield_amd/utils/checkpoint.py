@@ -69,7 +69,8 @@ def restore(model: nn.Module, state: dict) -> None:
 def save_engine(path: str, engine, meta: dict | None = None) -> str:
     """Checkpoint of a ``RobustDataParallel`` engine (fp32 master parameters in the
     reference layout, buffers, momentum, step)."""
-    return save(path, engine.model, engine.step_count, engine.mom[: engine.d], meta,
+    mom = engine.momentum_vector() if hasattr(engine, "momentum_vector") else engine.mom
+    return save(path, engine.model, engine.step_count, mom[: engine.d], meta,
                 flat=engine.flat.reference_vector())
 
 
@@ -85,7 +86,14 @@ def load_engine(path: str, engine) -> dict:
     if hasattr(engine, "sync_shadow"):
         engine.sync_shadow()
     if "momentum" in state:
-        engine.mom[: engine.d].copy_(state["momentum"].to(engine.mom.device))
+        m = state["momentum"].to(engine.mom.device)
+        shard = getattr(engine, "_shard", None)
+        if shard is not None:   # sharded optimizer state: this rank's slice
+            full = torch.zeros(shard.world * shard.S, dtype=m.dtype, device=m.device)
+            full[: m.numel()] = m
+            engine.mom.copy_(full[shard.sl])
+        else:
+            engine.mom[: engine.d].copy_(m)
     engine.step_count = int(state.get("step", 0))
     engine._graph = None  # re-capture against the restored state
     return state

@@ -96,12 +96,12 @@ class FlatParams:
     memory order. ``reference_vector()`` always returns the reference layout
     (logical ``p.view(-1)`` order) for checkpoints and the RPC API."""
 
-    def __init__(self, model: nn.Module, device=None, dtype=torch.float32, with_grad: bool = True):
+    def __init__(self, model: nn.Module, device=None, dtype=torch.float32, with_grad: bool = True, pad: int = PAD):
         self.model = model
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.numels = [p.numel() for p in self.params]
         self.d = sum(self.numels)
-        self.ld = padded(self.d)
+        self.ld = padded(self.d, pad)
         device = device or self.params[0].device
         self.data = torch.zeros(self.ld, dtype=dtype, device=device)
         self.offsets = []

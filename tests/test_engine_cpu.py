@@ -59,3 +59,55 @@ def test_two_rank_gloo_replicas_identical(rule):
         r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
         r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
         assert torch.equal(r0["flat"], r1["flat"])
+
+
+def _sharded_worker(rank, world, port, outdir, rule, shard):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from garfield_amd.parallel.comm import init_distributed, shutdown
+
+    ctx = init_distributed(backend="gloo", device="cpu")
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                             EngineConfig(gar=rule, f=1, workers_per_rank=4, byzantine={3: "reverse"},
+                                          shard_gar=shard, lr=0.05))
+    assert (eng._shard is not None) == shard
+    b = synthetic_batches(4, 8, (1, 28, 28), 10, "cpu", seed=rank)
+    for _ in range(3):
+        eng.step(b)
+    torch.save({"flat": eng.flat_model().clone(), "mom": eng.momentum_vector()[: eng.d].clone()},
+               os.path.join(outdir, f"{int(shard)}r{rank}.pt"))
+    shutdown(ctx)
+
+
+@pytest.mark.parametrize("rule", ["krum", "median", "bulyan", "aksel", "average", "trimmed-mean", "brute"])
+def test_two_rank_sharded_aggregation_matches_allgather(rule):
+    """all_to_all + sharded GAR + all-gather == all-gather + redundant GAR (and replicas agree)."""
+    with tempfile.TemporaryDirectory() as d:
+        for shard in (False, True):
+            mp.spawn(_sharded_worker, args=(2, free_port(), d, rule, shard), nprocs=2, join=True)
+        r = {k: torch.load(os.path.join(d, f"{k}.pt"), weights_only=True) for k in ("0r0", "0r1", "1r0", "1r1")}
+        assert torch.equal(r["1r0"]["flat"], r["1r1"]["flat"])           # sharded replicas identical
+        ref_flat = r["0r0"]["flat"]
+        rel = ((r["1r0"]["flat"] - ref_flat).norm() / ref_flat.norm()).item()
+        assert rel < 1e-5, rel
+        m0, m1 = r["0r0"]["mom"], r["1r0"]["mom"]
+        assert ((m1 - m0).norm() / m0.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("rule,f", [("krum", 2), ("median", 1), ("bulyan", 1), ("aksel", 2)])
+def test_single_rank_sharded_path_matches(rule, f):
+    """shard_gar=True on one rank runs the sharded code path with identity collectives."""
+    outs = []
+    for shard in (False, True):
+        torch.manual_seed(0)
+        eng = RobustDataParallel(build_model("mlp"), F.nll_loss, DistContext(),
+                                 EngineConfig(gar=rule, f=f, workers_per_rank=8, shard_gar=shard,
+                                              byzantine={1: "reverse"}))
+        assert (eng._shard is not None) == shard
+        b = synthetic_batches(8, 16, (1, 28, 28), 10, "cpu")
+        for _ in range(3):
+            eng.step(b)
+        outs.append(eng.flat_model().clone())
+    rel = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
+    assert rel < 1e-6, rel

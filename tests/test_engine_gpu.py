@@ -110,3 +110,28 @@ def test_engine_cuda_graph_matches_eager(cuda, rule):
     noise = ((outs[0] - outs[1]).norm() / outs[0].norm()).item()
     rel = ((outs[0] - outs[2]).norm() / outs[0].norm()).item()
     assert rel < max(10 * noise, 1e-3), (rel, noise)
+
+
+@pytest.mark.parametrize("rule,f", [("krum", 2), ("median", 1), ("bulyan", 1), ("aksel", 2), ("brute", 2),
+                                    ("average", 0), ("trimmed-mean", 2)])
+def test_sharded_gpu_path_single_rank_matches(cuda, rule, f):
+    """The sharded aggregation's GPU code (row-list GAR on the shard, Gram all-reduce,
+    fused update of the master shard, working-weight refresh) with identity
+    collectives on one rank == the redundant path."""
+    outs = []
+    for shard in (False, True):
+        torch.manual_seed(0)
+        cfg = EngineConfig(gar=rule, f=max(f, 1), workers_per_rank=8, shard_gar=shard,
+                           byzantine={} if rule == "average" else {3: "reverse"}, lr=0.01)
+        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+        assert (eng._shard is not None) == shard
+        b = synthetic_batches(8, 8, (3, 32, 32), 10, cuda)
+        for _ in range(3):
+            eng.step(b)
+        torch.cuda.synchronize()
+        outs.append((eng.flat.reference_vector().clone(), eng.last_weights))
+    (p0, w0), (p1, w1) = outs
+    rel = ((p1 - p0).norm() / p0.norm()).item()
+    assert rel < 1e-5, rel
+    if w0 is not None:
+        assert torch.equal(w0.cpu(), w1.cpu())
