@@ -76,6 +76,42 @@ __global__ __launch_bounds__(kThreads) void k_im2col_scalar(const uint16_t* __re
   }
 }
 
+// Chunked path (any C, ldc % 8 == 0, e.g. the 3-channel stem padded to 152
+// columns): one thread gathers 8 consecutive columns of one col row and writes
+// them with one 16-byte store.
+__global__ __launch_bounds__(kThreads) void k_im2col_chunk8(const uint16_t* __restrict__ x, Im2col g,
+                                                           uint16_t* __restrict__ col, int rows_per_wg) {
+  const int K = g.KH * g.KW * g.C;
+  const int L8 = g.ldc / 8;
+  const int rows = g.N * g.Ho * g.Wo;
+  for (int t = threadIdx.x; t < rows_per_wg * L8; t += kThreads) {
+    const int m = blockIdx.x * rows_per_wg + t / L8;
+    if (m >= rows) break;
+    const int r0 = (t % L8) * 8;
+    const int wo = m % g.Wo;
+    const int ho = (m / g.Wo) % g.Ho;
+    const int n = m / (g.Wo * g.Ho);
+    uint16_t v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int r = r0 + e;
+      uint16_t val = 0;
+      if (r < K) {
+        const int kp = r / g.C, c = r % g.C;
+        const int hi = ho * g.sh - g.ph + (kp / g.KW) * g.dh;
+        const int wi = wo * g.sw - g.pw + (kp % g.KW) * g.dw;
+        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+          val = x[((static_cast<int64_t>(n) * g.H + hi) * g.W + wi) * g.C + c];
+      }
+      v[e] = val;
+    }
+    uint4 w;
+    w.x = v[0] | (uint32_t(v[1]) << 16); w.y = v[2] | (uint32_t(v[3]) << 16);
+    w.z = v[4] | (uint32_t(v[5]) << 16); w.w = v[6] | (uint32_t(v[7]) << 16);
+    *reinterpret_cast<uint4*>(col + static_cast<int64_t>(m) * g.ldc + r0) = w;
+  }
+}
+
 // (hi, wi) -> output pixel of tap (i, j), or -1.
 __device__ __forceinline__ int tap_row(const Im2col& g, int n, int hi, int wi, int i, int j) {
   const int a = hi + g.ph - i * g.dh;
@@ -139,11 +175,13 @@ void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t 
   const int rows = g.N * g.Ho * g.Wo;
   if (rows <= 0) return;
   const bool vec = g.C % 8 == 0 && g.ldc == g.KH * g.KW * g.C;
-  const int K = vec ? g.KH * g.KW * (g.C / 8) : g.ldc;
+  const bool chunk8 = !vec && g.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(col) & 15) == 0;
+  const int K = vec ? g.KH * g.KW * (g.C / 8) : (chunk8 ? g.ldc / 8 : g.ldc);
   int rpw = kThreads * 4 / K;  // ~4 items per thread
   if (rpw < 1) rpw = 1;
   const dim3 grid((rows + rpw - 1) / rpw);
   if (vec) hipLaunchKernelGGL(k_im2col_vec, grid, dim3(kThreads), 0, stream, x, g, col, rpw);
+  else if (chunk8) hipLaunchKernelGGL(k_im2col_chunk8, grid, dim3(kThreads), 0, stream, x, g, col, rpw);
   else hipLaunchKernelGGL(k_im2col_scalar, grid, dim3(kThreads), 0, stream, x, g, col, rpw);
 }
 
