@@ -288,3 +288,16 @@ class DatasetManager:
     def get_test_set(self) -> DeviceLoader:
         ds = self.fetch_dataset(train=False)
         return DeviceLoader(ds, range(len(ds)), 100, self.device)
+
+
+def poison_batch(x: torch.Tensor, y: torch.Tensor, severity: int, generator: torch.Generator | None = None):
+    """Malformed-input (data poisoning) attack of the legacy ``mnistAttack`` experiment
+    (``tensorflow_impl/applications/Garfield_legacy/experiments/mnistAttack.py:34-80``):
+    severity 1 scales the inputs by -100; severity 2 scales them by -1e12 and
+    shuffles the labels against the inputs. Severity 0 returns the batch unchanged."""
+    if severity <= 0:
+        return x, y
+    if severity == 1:
+        return x * -100.0, y
+    perm = torch.randperm(y.shape[0], generator=generator, device="cpu").to(y.device)
+    return x * -1e12, y[perm]
