@@ -40,7 +40,9 @@ def avg_agree(ps, gar, aggr_grad, rounds: int, num_wait: int, f: int):
     return aggr_grad
 
 
-def main(argv=None, results: dict | None = None):
+def main(argv=None, results: dict | None = None, progress=None):
+    """Run one LEARN node; ``progress(done, total)`` is called after every iteration
+    (the web demo's progress queue, reference ``LEARN/demo.py:225-235``)."""
     a = parse(argv)
     n, f = a.num_nodes, a.f
     if a.rank == 0:
@@ -70,6 +72,8 @@ def main(argv=None, results: dict | None = None):
         if (a.acc_freq and i % a.acc_freq == 0) or i == a.num_iter - 1:
             acc = ps.compute_binary_accuracy() if a.dataset == "pima" else ps.compute_accuracy()
             info(f"Node {a.rank} iteration: {i} Accuracy: {acc:.2f} Time: {time.time() - start:.2f}")
+        if progress is not None:
+            progress(i + 1, a.num_iter)
     if results is not None:
         results["accuracy"] = acc
     import torch.distributed.rpc as rpc
