@@ -111,3 +111,34 @@ def test_single_rank_sharded_path_matches(rule, f):
         outs.append(eng.flat_model().clone())
     rel = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
     assert rel < 1e-6, rel
+
+
+def _grouped_sharded_worker(rank, world, port, outdir, shard):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from garfield_amd.parallel.comm import init_distributed, shutdown
+
+    ctx = init_distributed(backend="gloo", device="cpu")
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, ctx,
+                             EngineConfig(gar="krum", f=1, workers_per_rank=3, byzantine={1: "reverse"},
+                                          shard_gar=shard, worker_batching=True, autocast_dtype=None,
+                                          exchange_dtype=torch.float32, lr=0.01))
+    assert eng._gexec is not None and (eng._shard is not None) == shard
+    b = synthetic_batches(3, 4, (3, 32, 32), 10, "cpu", seed=rank)
+    for _ in range(2):
+        eng.step(b)
+    torch.save({"flat": eng.flat_model().clone()}, os.path.join(outdir, f"{int(shard)}r{rank}.pt"))
+    shutdown(ctx)
+
+
+def test_two_rank_grouped_workers_with_sharded_aggregation():
+    """The flagship multi-GPU configuration on CPU: worker batching + sharded aggregation."""
+    with tempfile.TemporaryDirectory() as d:
+        for shard in (False, True):
+            mp.spawn(_grouped_sharded_worker, args=(2, free_port(), d, shard), nprocs=2, join=True)
+        r = {k: torch.load(os.path.join(d, f"{k}.pt"), weights_only=True)["flat"]
+             for k in ("0r0", "0r1", "1r0", "1r1")}
+        assert torch.equal(r["1r0"], r["1r1"]) and torch.equal(r["0r0"], r["0r1"])
+        rel = ((r["1r0"] - r["0r0"]).norm() / r["0r0"].norm()).item()
+        assert rel < 1e-5, rel
