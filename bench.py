@@ -152,8 +152,10 @@ def main():
         extra["ref_impl_img_per_s"] = round(n * a.batch / (ms_ref / 1000.0), 2)
         extra["speedup_vs_ref_impl"] = round(ms_ref / ms, 3)
     if ctx.rank == 0:
+        default = (a.model, a.gar, a.f, a.dataset) == ("resnet50", "krum", 2, "cifar10")
+        gar_name = {"krum": "Multi-Krum"}.get(a.gar, a.gar)
         out = {
-            "metric": "img/sec ResNet-50 f=2 Multi-Krum",
+            "metric": "img/sec ResNet-50 f=2 Multi-Krum" if default else f"img/sec {a.model} f={a.f} {gar_name}",
             "value": round(value, 2),
             "unit": "img/s",
             "n_gpus": world,
@@ -164,7 +166,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16",
-            "data": "synthetic (random CIFAR-10-shape images, random-init weights)",
+            "data": f"synthetic (random {'CIFAR-10' if a.dataset == 'cifar10' else 'ImageNet'}-shape images, "
+                    "random-init weights)",
             "config": {
                 "model": f"{a.model} (torchvision architecture, {num_classes} classes, {d} params)",
                 "global_batch": n * a.batch,
