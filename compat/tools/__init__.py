@@ -6,5 +6,7 @@ from garfield_amd.utils.logging import (  # noqa: F401
     Context, UserException, context, error, fatal, info, trace, warning,
 )
 from garfield_amd.utils.misc import (  # noqa: F401
-    TimedContext, cluster_parse, import_directory, pairwise, parse_keyval,
+    ExpandPath, TimedContext, cluster_parse, device_from_tuple, import_directory, make_interface, pairwise,
+    parse_keyval, print_args,
 )
+from garfield_amd.utils.checkpoint import Checkpoints  # noqa: F401

@@ -41,7 +41,7 @@ def save(path: str, model: nn.Module, step: int = 0, momentum: torch.Tensor | No
     state["meta"] = dict(meta or {})
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
-    fd, tmp = tempfile.mkstemp(dir=d, prefix=".ckpt-")
+    fd, tmp = tempfile.mkstemp(dir=d, prefix="tmp-ckpt-", suffix=".part")
     os.close(fd)
     torch.save(state, tmp)
     os.replace(tmp, path)
@@ -97,3 +97,56 @@ def load_engine(path: str, engine) -> dict:
     engine.step_count = int(state.get("step", 0))
     engine._graph = None  # re-capture against the restored state
     return state
+
+
+class Checkpoints:
+    """Numbered checkpoints in one directory, keeping the newest ``max_to_keep``
+    (the role of the reference's TF1 ``Checkpoints`` Saver wrapper,
+    ``tensorflow_impl/rsrcs/tools/tf.py:78-173``, which the trainers never call).
+
+    ``save(target, step)`` accepts a ``RobustDataParallel``-like engine (master
+    weights, momentum, step) or a plain module; ``restore(target)`` loads the newest
+    (or the given step). Only rank 0 should save in a data-parallel job: replicas are
+    identical."""
+
+    PREFIX, SUFFIX = "ckpt-", ".pt"
+
+    def __init__(self, directory: str, max_to_keep: int = 5):
+        self.directory = directory
+        self.max_to_keep = max(int(max_to_keep), 1)
+        os.makedirs(directory, exist_ok=True)
+
+    def path(self, step: int) -> str:
+        return os.path.join(self.directory, f"{self.PREFIX}{int(step):010d}{self.SUFFIX}")
+
+    def steps(self) -> list[int]:
+        out = []
+        for name in os.listdir(self.directory):
+            if name.startswith(self.PREFIX) and name.endswith(self.SUFFIX):
+                try:
+                    out.append(int(name[len(self.PREFIX):-len(self.SUFFIX)]))
+                except ValueError:
+                    pass
+        return sorted(out)
+
+    def latest(self) -> int | None:
+        s = self.steps()
+        return s[-1] if s else None
+
+    def save(self, target, step: int | None = None, meta: dict | None = None) -> str:
+        if hasattr(target, "flat") and hasattr(target, "step_count"):
+            step = target.step_count if step is None else step
+            p = save_engine(self.path(step), target, meta)
+        else:
+            p = save(self.path(step or 0), target, step or 0, None, meta)
+        for old in self.steps()[:-self.max_to_keep]:
+            os.remove(self.path(old))
+        return p
+
+    def restore(self, target, step: int | None = None) -> dict:
+        step = self.latest() if step is None else step
+        if step is None:
+            raise FileNotFoundError(f"no checkpoint in {self.directory}")
+        if hasattr(target, "flat") and hasattr(target, "step_count"):
+            return load_engine(self.path(step), target)
+        return load(self.path(step), target)

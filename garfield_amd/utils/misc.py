@@ -118,3 +118,66 @@ def cluster_parse(spec: str | None = None, env_key: str = "OAR_FILE_NODES") -> l
             seen.add(h)
             out.append(h)
     return out
+
+
+def print_args(name: str, selected, list_keyval, head: str = "[ARGS] ") -> None:
+    """Print a selected instance and its ``key:value`` arguments
+    (reference ``tensorflow_impl/rsrcs/tools/misc.py:172-184``)."""
+    print(head + "Selected " + name + ": " + (selected if selected else "<none>"))
+    for key, val in parse_keyval(list_keyval).items():
+        print(head + "· " + key + ": " + str(val))
+
+
+class ExpandPath:
+    """Temporarily append paths to ``sys.path`` (reference ``misc.py:189-219``)."""
+
+    def __init__(self, *paths):
+        self._exp = [str(p) for p in paths]
+        self._old = None
+
+    def __enter__(self):
+        import sys
+
+        self._old = sys.path
+        sys.path = sys.path + self._exp
+        return self
+
+    def __exit__(self, *exc):
+        import sys
+
+        sys.path = self._old
+        return False
+
+
+def make_interface(_create, _destroy, **methods):
+    """Pointer-implementation class over a native handle (reference ``misc.py:224-283``):
+    ``_create(*args) -> handle``, ``_destroy(handle)``, each method ``f(handle, ...)``."""
+    nname = "_native"
+    if nname in methods:
+        raise ValueError(f"Method name {nname!r} is reserved")
+
+    class Interface:
+        def __init__(self, *args):
+            setattr(self, nname, _create(*args))
+
+        def __del__(self):
+            if nname in self.__dict__:
+                _destroy(self.__dict__[nname])
+
+        def __getattr__(self, name):
+            if nname not in self.__dict__:
+                raise AttributeError("Unable to access instance as its creation failed")
+            method = methods[name]
+            native = self.__dict__[nname]
+            return lambda *args: method(native, *args)
+
+        def __call__(self):
+            return self.__dict__[nname]
+
+    return Interface
+
+
+def device_from_tuple(job: str, task: int, dev_type: str = "cpu", dev_index: int = 0) -> str:
+    """Device name for a cluster (job, task) pair (reference ``rsrcs/tools/tf.py:63-73``);
+    here one process per device, so the (type, index) part is a torch device string."""
+    return f"/job:{job}/replica:0/task:{task}/device:{dev_type.upper()}:{dev_index}"

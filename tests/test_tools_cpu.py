@@ -1,0 +1,47 @@
+"""Reference ``tools`` helpers (PT libs/tools, TF rsrcs/tools) and the Checkpoints manager."""
+import sys
+
+import torch
+import torch.nn.functional as F
+
+from garfield_amd.models import build_model
+from garfield_amd.parallel.comm import DistContext
+from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synthetic_batches
+from garfield_amd.utils.checkpoint import Checkpoints
+from garfield_amd.utils.misc import ExpandPath, device_from_tuple, make_interface, print_args
+
+
+def test_checkpoints_keep_and_resume(tmp_path):
+    torch.manual_seed(0)
+    cfg = EngineConfig(gar="krum", f=1, workers_per_rank=5, lr=0.05)
+    eng = RobustDataParallel(build_model("mlp"), F.nll_loss, DistContext(), cfg)
+    b = synthetic_batches(5, 8, (1, 28, 28), 10, "cpu")
+    ck = Checkpoints(str(tmp_path / "ck"), max_to_keep=2)
+    for _ in range(3):
+        eng.step(b)
+        ck.save(eng)
+    assert ck.steps() == [2, 3]
+    ref = eng.flat_model().clone()
+    eng.step(b)
+    torch.manual_seed(0)
+    eng2 = RobustDataParallel(build_model("mlp"), F.nll_loss, DistContext(), cfg)
+    ck.restore(eng2)
+    assert eng2.step_count == 3 and torch.equal(eng2.flat_model(), ref)
+    eng2.step(b)
+    assert torch.allclose(eng2.flat_model(), eng.flat_model(), atol=1e-6)
+
+
+def test_misc_helpers(capsys, tmp_path):
+    print_args("rule", "krum", ["m:3"])
+    assert "Selected rule: krum" in capsys.readouterr().out
+    with ExpandPath(tmp_path):
+        assert str(tmp_path) in sys.path
+    assert str(tmp_path) not in sys.path
+    freed = []
+    Box = make_interface(lambda v: [v], lambda h: freed.append(h), get=lambda h: h[0], put=lambda h, v: h.__setitem__(0, v))
+    b = Box(3)
+    b.put(5)
+    assert b.get() == 5 and b() == [5]
+    del b
+    assert freed == [[5]]
+    assert device_from_tuple("ps", 1, "gpu", 0) == "/job:ps/replica:0/task:1/device:GPU:0"
