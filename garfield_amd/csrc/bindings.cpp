@@ -436,11 +436,11 @@ void g_im2col(const at::Tensor& x, int64_t kh, int64_t kw, int64_t sh, int64_t s
 
 // dx: the (channels_last, bf16) input-shaped output; dcol: [N*Ho*Wo, ldc] bf16
 void g_col2im(const at::Tensor& dcol, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph, int64_t pw,
-              int64_t dh, int64_t dw, const at::Tensor& dx) {
+              int64_t dh, int64_t dw, const at::Tensor& dx, bool accumulate) {
   auto g = conv_geometry(dx, kh, kw, sh, sw, ph, pw, dh, dw);
   check_col(dcol, dx, g);
   c10::hip::HIPGuard guard(dx.device().index());
-  garfield::gpu::col2im_nhwc(u16(dcol), g, u16_mut(dx), stream_of(dx.device()));
+  garfield::gpu::col2im_nhwc(u16(dcol), g, u16_mut(dx), accumulate, stream_of(dx.device()));
 }
 
 int g_flatten_cast_at(const std::vector<at::Tensor>& srcs, const std::vector<int64_t>& offsets,
@@ -595,7 +595,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_im2col", &g_im2col, "NHWC im2col of a channels_last bf16 tensor into col [N*Ho*Wo, ldc >= KH*KW*C] "
         "(pad columns zeroed); args (x, kh, kw, sh, sw, ph, pw, dh, dw, col)");
   m.def("gpu_col2im", &g_col2im, "Adjoint of gpu_im2col (gather, deterministic): dx = col2im(dcol); args "
-        "(dcol, kh, kw, sh, sw, ph, pw, dh, dw, dx)");
+        "(dcol, kh, kw, sh, sw, ph, pw, dh, dw, dx, accumulate=False); accumulate adds into dx",
+        py::arg("dcol"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("dh"), py::arg("dw"), py::arg("dx"), py::arg("accumulate") = false);
 
   // CPU building blocks (thread pool)
   def_rows(m, "cpu_pairwise",

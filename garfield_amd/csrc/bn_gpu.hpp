@@ -40,7 +40,8 @@ void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t 
 
 // The adjoint gather: dx[n][hi][wi][c] = Σ_{taps (i, j) hitting (hi, wi)} dcol[(n*Ho + ho)*Wo + wo][(i*KW + j)*C + c]
 // (fp32 accumulation, every element written once: no atomics, deterministic).
-void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, hipStream_t stream);
+// accumulate: dx += col2im(dcol) instead of dx = col2im(dcol).
+void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, bool accumulate, hipStream_t stream);
 
 }  // namespace gpu
 }  // namespace garfield

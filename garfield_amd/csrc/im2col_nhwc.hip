@@ -122,7 +122,10 @@ __device__ __forceinline__ int tap_row(const Im2col& g, int n, int hi, int wi, i
   return (n * g.Ho + ho) * g.Wo + wo;
 }
 
-// col2im vector path: one thread per 8-channel vector of one input pixel.
+// col2im vector path: one thread per 8-channel vector of one input pixel. ACC adds
+// into dx (the other branch's gradient of the same input, e.g. a residual block's
+// conv1 and downsample), instead of a separate elementwise add.
+template <bool ACC>
 __global__ __launch_bounds__(kThreads) void k_col2im_vec(const uint16_t* __restrict__ dcol, Im2col g,
                                                         uint16_t* __restrict__ dx) {
   const int cv = g.C / 8;
@@ -135,6 +138,7 @@ __global__ __launch_bounds__(kThreads) void k_col2im_vec(const uint16_t* __restr
     const int hi = (pix / g.W) % g.H;
     const int n = pix / (g.W * g.H);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ACC) load_vec<kBF16, 8>(dx, static_cast<int64_t>(pix) * g.C + v * 8, acc);
     for (int i = 0; i < g.KH; ++i) {
       for (int j = 0; j < g.KW; ++j) {
         const int m = tap_row(g, n, hi, wi, i, j);
@@ -149,6 +153,7 @@ __global__ __launch_bounds__(kThreads) void k_col2im_vec(const uint16_t* __restr
   }
 }
 
+template <bool ACC>
 __global__ __launch_bounds__(kThreads) void k_col2im_scalar(const uint16_t* __restrict__ dcol, Im2col g,
                                                            uint16_t* __restrict__ dx) {
   const int64_t total = static_cast<int64_t>(g.N) * g.H * g.W * g.C;
@@ -159,7 +164,7 @@ __global__ __launch_bounds__(kThreads) void k_col2im_scalar(const uint16_t* __re
     const int wi = pix % g.W;
     const int hi = (pix / g.W) % g.H;
     const int n = pix / (g.W * g.H);
-    float acc = 0.f;
+    float acc = ACC ? bf16_to_f(dx[t]) : 0.f;
     for (int i = 0; i < g.KH; ++i)
       for (int j = 0; j < g.KW; ++j) {
         const int m = tap_row(g, n, hi, wi, i, j);
@@ -185,14 +190,17 @@ void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t 
   else hipLaunchKernelGGL(k_im2col_scalar, grid, dim3(kThreads), 0, stream, x, g, col, rpw);
 }
 
-void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, hipStream_t stream) {
+void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, bool accumulate, hipStream_t stream) {
   const bool vec = g.C % 8 == 0 && g.ldc % 8 == 0;
   const int64_t items = static_cast<int64_t>(g.N) * g.H * g.W * (vec ? g.C / 8 : g.C);
   if (items <= 0) return;
   int64_t blocks = (items + kThreads - 1) / kThreads;
   if (blocks > 65536) blocks = 65536;  // grid-stride beyond
-  if (vec) hipLaunchKernelGGL(k_col2im_vec, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0, stream, dcol, g, dx);
-  else hipLaunchKernelGGL(k_col2im_scalar, dim3(static_cast<unsigned>(blocks)), dim3(kThreads), 0, stream, dcol, g, dx);
+  const dim3 grid(static_cast<unsigned>(blocks));
+  if (vec && accumulate) hipLaunchKernelGGL(k_col2im_vec<true>, grid, dim3(kThreads), 0, stream, dcol, g, dx);
+  else if (vec) hipLaunchKernelGGL(k_col2im_vec<false>, grid, dim3(kThreads), 0, stream, dcol, g, dx);
+  else if (accumulate) hipLaunchKernelGGL(k_col2im_scalar<true>, grid, dim3(kThreads), 0, stream, dcol, g, dx);
+  else hipLaunchKernelGGL(k_col2im_scalar<false>, grid, dim3(kThreads), 0, stream, dcol, g, dx);
 }
 
 }  // namespace gpu

@@ -98,6 +98,22 @@ class GradSink:
         self._srcs.append(grad)
         self._offs.append(self.row_offset(g, p))
 
+    def rows_view(self, p: torch.Tensor, shape: tuple, dtype: torch.dtype) -> torch.Tensor | None:
+        """[groups, *shape] view of parameter p's slots in every worker row (``shape``:
+        p's memory-order shape, last dim contiguous), for GEMMs / reductions that write
+        the per-worker gradients in place; None when the exchange dtype is not
+        ``dtype`` (the caller then queues a ``put``)."""
+        if self.flat.dtype != dtype:
+            return None
+        strides, acc = [], 1
+        for d in reversed(shape):
+            strides.append(acc)
+            acc *= int(d)
+        if acc != p.numel():
+            raise ValueError(f"rows_view of {acc} elements for a parameter of {p.numel()}")
+        return self.flat.as_strided((self.groups, *shape), (self.row_stride, *reversed(strides)),
+                                    self.base + self.offsets[id(p)])
+
     def put_groups(self, p: torch.Tensor, grads) -> None:
         """``grads``: [groups, ...] tensor or a list of per-group tensors."""
         for g in range(self.groups):
@@ -123,6 +139,32 @@ def _memory_order(t: torch.Tensor) -> torch.Tensor:
         return t.reshape(-1)
     perm = sorted(range(t.dim()), key=lambda i: -t.stride(i))
     return t.permute(perm).reshape(-1)
+
+
+class GradJoin:
+    """Sums the two gradient branches of one activation inside a backward kernel.
+
+    A residual block's input x is read by two branches (conv1 and the shortcut:
+    the identity, through the last BatchNorm's residual input, or the downsample
+    convolution). Autograd would produce both gradients and add them with a
+    separate elementwise kernel. Instead, the branch whose backward runs FIRST
+    parks its gradient here and returns None for x; the second one folds it into
+    its own output (``addmm_`` for a 1x1 GEMM dgrad, an accumulating col2im for a
+    k x k one) and returns the sum. A fresh join is made per forward."""
+
+    __slots__ = ("pending",)
+
+    def __init__(self):
+        self.pending = None
+
+    def take(self):
+        prev, self.pending = self.pending, None
+        return prev
+
+    def park(self, g: torch.Tensor) -> None:
+        if self.pending is not None:
+            raise RuntimeError("GradJoin: both branches parked a gradient")
+        self.pending = g
 
 
 # --------------------------------------------------------------------------- #
@@ -236,7 +278,7 @@ def _bn_bwd_ref(x2, dy2, y2, st: BNState, need_res: bool):
 
 class _GroupedBN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, st: BNState, ws: Workspace):
+    def forward(ctx, x, gamma, beta, res, st: BNState, ws: Workspace, join: GradJoin | None = None):
         n, C, h, w = x.shape
         x2 = rows2d(x)
         r2 = rows2d(res) if res is not None else None
@@ -255,7 +297,7 @@ class _GroupedBN(torch.autograd.Function):
                               part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu)
         else:
             y = from_rows(_bn_fwd_ref(x2, r2, st), n, h, w)
-        ctx.st, ctx.ws, ctx.has_res = st, ws, res is not None
+        ctx.st, ctx.ws, ctx.has_res, ctx.join = st, ws, res is not None, join
         ctx.save_for_backward(x, y if st.relu else None)
         return y
 
@@ -286,12 +328,17 @@ class _GroupedBN(torch.autograd.Function):
             dx2, dr2 = _bn_bwd_ref(x2, dy2, y2, st, ctx.has_res)
             dx = from_rows(dx2, n, h, w)
             dres = from_rows(dr2, n, h, w) if dr2 is not None else None
-        return dx, None, None, dres, None, None
+        if dres is not None and ctx.join is not None:
+            ctx.join.park(dres)
+            dres = None
+        return dx, None, None, dres, None, None, None
 
 
-def grouped_bn(x, st: BNState, ws: Workspace, res=None):
-    """y = [relu](BN_per_worker(x) [+ res]); x/res channels_last."""
-    return _GroupedBN.apply(_cl(x), st.bn.weight, st.bn.bias, _cl(res) if res is not None else None, st, ws)
+def grouped_bn(x, st: BNState, ws: Workspace, res=None, res_join: GradJoin | None = None):
+    """y = [relu](BN_per_worker(x) [+ res]); x/res channels_last. With ``res_join``
+    the residual's gradient is handed to the join instead of autograd."""
+    return _GroupedBN.apply(_cl(x), st.bn.weight, st.bn.bias, _cl(res) if res is not None else None, st, ws,
+                            res_join)
 
 
 # --------------------------------------------------------------------------- #
@@ -354,22 +401,28 @@ def _match_layout(g: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
     return g.contiguous()
 
 
-def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int) -> torch.Tensor:
+def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int, out: torch.Tensor | None = None) -> torch.Tensor:
     """Per-worker weight gradients ``dW_g = dy_gᵀ · a_g`` for all G workers: [G, Cout, K].
 
     One strided-batched GEMM; when each worker has many rows (the CIFAR stem and
     layer1: 16k-64k rows against 64 output channels) the row dimension is split S
     ways into a (G*S)-batch GEMM and the S partials are summed in fp32: the
     reduction is too long and the output too small for one GEMM to fill 256 CUs
-    (measured 1.6-3.7x faster on those layers, scripts/bench_wgrad_gemm.py)."""
+    (measured 1.6-3.7x faster on those layers, scripts/bench_wgrad_gemm.py).
+    ``out`` ([G, Cout, K], e.g. ``GradSink.rows_view``) receives the result in place:
+    the GEMM (or the fp32-accumulated split-K sum) writes the exchange rows directly."""
     cout, K = dy2.shape[1], a2.shape[1]
     M = dy2.shape[0] // G
     S = 1
     while S < 16 and M % (2 * S) == 0 and M // (2 * S) >= 4000:
         S *= 2
     if S == 1:
+        if out is not None:
+            return torch.bmm(dy2.view(G, M, cout).transpose(1, 2), a2.view(G, M, K), out=out)
         return torch.bmm(dy2.view(G, M, cout).transpose(1, 2), a2.view(G, M, K))
     part = torch.bmm(dy2.view(G * S, M // S, cout).transpose(1, 2), a2.view(G * S, M // S, K))
+    if out is not None:
+        return torch.sum(part.view(G, S, cout, K), 1, out=out)   # fp32 accumulation, one rounding
     return part.view(G, S, cout, K).float().sum(1)
 
 
@@ -382,8 +435,9 @@ class _GroupedConv(torch.autograd.Function):
     ``CONV_MODE == "miopen"``): ATen convolutions, per-worker weight gradients."""
 
     @staticmethod
-    def forward(ctx, x, w, spec: ConvSpec):
+    def forward(ctx, x, w, spec: ConvSpec, join: GradJoin | None = None):
         ctx.spec = spec
+        ctx.join = join
         ctx.xshape = tuple(x.shape)
         n, _, h, wd = x.shape
         if spec.gemm:
@@ -411,27 +465,47 @@ class _GroupedConv(torch.autograd.Function):
         dy2 = rows2d(dy)
         n, cin, h, wd = ctx.xshape
         dx = None
+        need_dx = ctx.needs_input_grad[0]
+        prev = ctx.join.take() if (need_dx and ctx.join is not None) else None
+        first = need_dx and ctx.join is not None and prev is None   # park dx for the other branch
         if mode == "rows":                       # a = x
-            if ctx.needs_input_grad[0]:
-                dx = from_rows(torch.mm(dy2, w.reshape(cout, -1)), n, h, wd)
+            if need_dx:
+                w2 = w.reshape(cout, -1)
+                if prev is not None:             # the other branch's gradient, folded into the GEMM
+                    p2 = rows2d(_cl(prev))
+                    dx = from_rows(p2.addmm_(dy2, w2), n, h, wd)
+                    prev = None
+                else:
+                    dx = from_rows(torch.mm(dy2, w2), n, h, wd)
             if spec.sink is not None:
-                spec.sink.put_groups(spec.conv.weight, _wgrad(dy2, rows2d(a), G))
+                K = w.numel() // cout
+                out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype)
+                dW = _wgrad(dy2, rows2d(a), G, out)
+                if out is None:
+                    spec.sink.put_groups(spec.conv.weight, dW)
         elif mode == "col":                      # a = col [N*Ho*Wo, Kp]
             kp = a.shape[1]
-            if ctx.needs_input_grad[0]:
+            if need_dx:
                 dcol = torch.mm(dy2, _wmat(w, kp))
-                dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
-                _native.native().gpu_col2im(dcol, *_geom(spec), dx)
+                if prev is not None:
+                    dx = _cl(prev)
+                    _native.native().gpu_col2im(dcol, *_geom(spec), dx, True)
+                    prev = None
+                else:
+                    dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+                    _native.native().gpu_col2im(dcol, *_geom(spec), dx)
             if spec.sink is not None:
                 # dW_g[co, (i, j, ci)] = Σ_rows dy_g[row, co] · col_g[row, (i, j, ci)]: the
                 # weight's channels_last memory order, one batched GEMM for all workers
-                dW = _wgrad(dy2, a, G)
                 K = w.numel() // cout
-                if kp != K:
-                    dW = dW[:, :, :K].contiguous()
-                spec.sink.put_groups(spec.conv.weight, dW)
+                out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if kp == K else None
+                dW = _wgrad(dy2, a, G, out)
+                if out is None:
+                    if kp != K:
+                        dW = dW[:, :, :K].contiguous()
+                    spec.sink.put_groups(spec.conv.weight, dW)
         else:                                    # a = x
-            if ctx.needs_input_grad[0]:
+            if need_dx:
                 dx = _cl(_conv_bwd(dy, a, w, spec, [True, False, False])[0])
             if spec.sink is not None:
                 B = a.shape[0] // G
@@ -439,11 +513,18 @@ class _GroupedConv(torch.autograd.Function):
                     sl = slice(g * B, (g + 1) * B)
                     dw = _conv_bwd(dy[sl], a[sl], w, spec, [False, True, False])[1]
                     spec.sink.put(spec.conv.weight, g, _match_layout(dw, w))
-        return dx, None, None
+        if prev is not None:                     # aten mode: not folded above
+            dx = dx + prev
+        if first:
+            ctx.join.park(dx)
+            dx = None
+        return dx, None, None, None
 
 
-def grouped_conv(x, spec: ConvSpec):
-    return _GroupedConv.apply(_cl(x), spec.conv.weight, spec)
+def grouped_conv(x, spec: ConvSpec, join: GradJoin | None = None):
+    """Convolution with per-worker weight gradients; ``join``: x's other gradient
+    branch (see ``GradJoin``)."""
+    return _GroupedConv.apply(_cl(x), spec.conv.weight, spec, join)
 
 
 # --------------------------------------------------------------------------- #
@@ -474,10 +555,18 @@ class _GroupedLinear(torch.autograd.Function):
         if spec.sink is not None:
             out, fin = dy.shape[1], x.shape[1]
             dy3 = dy.view(G, -1, out)
-            dW = torch.bmm(dy3.transpose(1, 2), x.contiguous().view(G, -1, fin))
-            spec.sink.put_groups(spec.lin.weight, dW)
+            x3 = x.contiguous().view(G, -1, fin)
+            wv = spec.sink.rows_view(spec.lin.weight, (out, fin), dy.dtype)
+            if wv is not None:
+                torch.bmm(dy3.transpose(1, 2), x3, out=wv)
+            else:
+                spec.sink.put_groups(spec.lin.weight, torch.bmm(dy3.transpose(1, 2), x3))
             if spec.lin.bias is not None:
-                spec.sink.put_groups(spec.lin.bias, _acc(dy3).sum(1))
+                bv = spec.sink.rows_view(spec.lin.bias, (out,), dy.dtype)
+                if bv is not None:       # reduced in fp32, written in the exchange dtype
+                    torch.sum(dy3, 1, out=bv)
+                else:
+                    spec.sink.put_groups(spec.lin.bias, _acc(dy3).sum(1))
         return dx, None, None, None
 
 

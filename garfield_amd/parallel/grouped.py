@@ -20,8 +20,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
-from garfield_amd.ops.grouped import (BNState, ConvSpec, GradSink, LinearSpec, Workspace, grouped_bn, grouped_conv,
-                                      grouped_linear)
+from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, grouped_bn,
+                                      grouped_conv, grouped_linear)
 
 
 def supports(model: nn.Module) -> bool:
@@ -60,29 +60,32 @@ class GroupedResNet:
         self.conv = {m: ConvSpec(m, sink, self.groups) for m in model.modules() if isinstance(m, nn.Conv2d)}
         self.fc = LinearSpec(model.fc, sink, self.groups)
         self.bn: dict = {}
+        self.join_residuals = True
 
     # ------------------------------------------------------------------ #
 
-    def _bn(self, x, bn: nn.BatchNorm2d, relu: bool, res=None):
+    def _bn(self, x, bn: nn.BatchNorm2d, relu: bool, res=None, res_join=None):
         st = self.bn.get(bn)
         if st is None:
             st = self.bn[bn] = BNState(bn, relu, self.sink, self.groups)
-        return grouped_bn(x, st, self.ws, res)
+        return grouped_bn(x, st, self.ws, res, res_join)
 
-    def _conv(self, x, conv: nn.Conv2d):
-        return grouped_conv(x, self.conv[conv])
+    def _conv(self, x, conv: nn.Conv2d, join=None):
+        return grouped_conv(x, self.conv[conv], join)
 
     def _block(self, blk, x):
-        out = self._bn(self._conv(x, blk.conv1), blk.bn1, True)
+        # x's two gradient branches (conv1 and the shortcut) are summed inside the
+        # second branch's backward kernel instead of by an autograd add
+        join = GradJoin() if self.join_residuals else None
+        out = self._bn(self._conv(x, blk.conv1, join), blk.bn1, True)
         if isinstance(blk, Bottleneck):
             out = self._bn(self._conv(out, blk.conv2), blk.bn2, True)
             last_conv, last_bn = blk.conv3, blk.bn3
         else:
             last_conv, last_bn = blk.conv2, blk.bn2
         if blk.downsample is None:
-            sc = x
-        else:
-            sc = self._bn(self._conv(x, blk.downsample[0]), blk.downsample[1], False)
+            return self._bn(self._conv(out, last_conv), last_bn, True, x, join)
+        sc = self._bn(self._conv(x, blk.downsample[0], join), blk.downsample[1], False)
         return self._bn(self._conv(out, last_conv), last_bn, True, sc)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

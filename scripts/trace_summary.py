@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--marker", default="spin")
+    ap.add_argument("--sequence", default="", help="also write the last step's dispatches (start offset, "
+                    "duration, kernel) to this file")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as fh:
@@ -46,6 +48,14 @@ def main():
     print(f"{'ms/step':>9} {'%':>6} {'calls/step':>10}  kernel")
     for name, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
         print(f"{t / 1e6 / k:9.3f} {100 * t / total:6.2f} {c / k:10.1f}  {name}")
+    if a.sequence:
+        last = rows[-(len(rows) // k):]
+        t0 = last[0][0]
+        with open(a.sequence, "w") as fh:
+            fh.write(f"{'start_us':>9} {'dur_us':>8}  kernel\n")
+            for s, e, name in last:
+                short = name.replace("(anonymous namespace)::", "").split("(")[0][:90]
+                fh.write(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  {short}\n")
 
 
 if __name__ == "__main__":
