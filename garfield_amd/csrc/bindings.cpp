@@ -443,6 +443,77 @@ void g_col2im(const at::Tensor& dcol, int64_t kh, int64_t kw, int64_t sh, int64_
   garfield::gpu::col2im_nhwc(u16(dcol), g, u16_mut(dx), accumulate, stream_of(dx.device()));
 }
 
+// Implicit-GEMM convolution: y = conv(x, w) (+ add); x/y/add channels_last bf16, w the
+// [Cout, KH, KW, C]-ordered weight (a channels_last 4-D weight or its [Cout, K] matrix).
+void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
+             int64_t pw, int64_t dh, int64_t dw, const at::Tensor& y, const c10::optional<at::Tensor>& add,
+             int64_t pm) {
+  auto g = conv_geometry(x, kh, kw, sh, sw, ph, pw, dh, dw);
+  TORCH_CHECK(g.C % 32 == 0, "gpu_iconv: input channels must be a multiple of 32 (got ", g.C, ")");
+  TORCH_CHECK(y.is_cuda() && y.device() == x.device() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 &&
+                  y.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "gpu_iconv: y must be a channels_last bf16 tensor on x's device");
+  const int64_t cout = y.size(1);
+  TORCH_CHECK(cout % 64 == 0, "gpu_iconv: output channels must be a multiple of 64 (got ", cout, ")");
+  TORCH_CHECK(y.size(0) == g.N && y.size(2) == g.Ho && y.size(3) == g.Wo, "gpu_iconv: y must be [", g.N, ", Cout, ",
+              g.Ho, ", ", g.Wo, "]");
+  const int64_t K = static_cast<int64_t>(g.KH) * g.KW * g.C;
+  TORCH_CHECK(w.device() == x.device() && w.scalar_type() == at::kBFloat16 && w.numel() == cout * K,
+              "gpu_iconv: w must be a bf16 weight of ", cout, " x ", K, " elements on x's device");
+  if (w.dim() == 4) {
+    TORCH_CHECK(w.size(0) == cout && w.size(1) == g.C && w.size(2) == g.KH && w.size(3) == g.KW &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_iconv: a 4-D weight must be channels_last [Cout, C, KH, KW]");
+  } else {
+    TORCH_CHECK(w.dim() == 2 && w.size(0) == cout && w.is_contiguous(), "gpu_iconv: a 2-D weight must be [Cout, K]");
+  }
+  const uint16_t* ap = nullptr;
+  if (add.has_value()) {
+    const auto& a = *add;
+    TORCH_CHECK(a.device() == x.device() && a.scalar_type() == at::kBFloat16 && a.sizes() == y.sizes() &&
+                    a.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_iconv: add must be a channels_last bf16 tensor shaped like y");
+    ap = u16(a);
+  }
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0 &&
+                  (ap == nullptr || reinterpret_cast<uintptr_t>(ap) % 8 == 0),
+              "gpu_iconv: x and w must be 16-byte aligned, y and add 8-byte aligned");
+  TORCH_CHECK(static_cast<int64_t>(g.N) * g.H * g.W * g.C < INT32_MAX && static_cast<int64_t>(g.N) * g.Ho * g.Wo < INT32_MAX,
+              "gpu_iconv: tensor too large");
+  c10::hip::HIPGuard guard(x.device().index());
+  garfield::gpu::iconv_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap, static_cast<int>(pm),
+                            stream_of(x.device()));
+}
+
+garfield::gpu::Im2col pool_geometry(const at::Tensor& x, const at::Tensor& y, const at::Tensor& idx, int64_t k,
+                                    int64_t s, int64_t p) {
+  auto g = conv_geometry(x, k, k, s, s, p, p, 1, 1);
+  TORCH_CHECK(g.C % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "garfield maxpool: channels must be a multiple of 8 and x 16-byte aligned");
+  TORCH_CHECK(y.device() == x.device() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == g.N &&
+                  y.size(1) == g.C && y.size(2) == g.Ho && y.size(3) == g.Wo &&
+                  y.is_contiguous(at::MemoryFormat::ChannelsLast) && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+              "garfield maxpool: y must be a channels_last bf16 [", g.N, ", ", g.C, ", ", g.Ho, ", ", g.Wo, "] tensor");
+  TORCH_CHECK(idx.device() == x.device() && idx.scalar_type() == at::kByte && idx.numel() == y.numel() &&
+                  idx.is_contiguous() && reinterpret_cast<uintptr_t>(idx.data_ptr()) % 8 == 0 && k * k <= 256,
+              "garfield maxpool: idx must be a contiguous uint8 tensor of y's element count");
+  return g;
+}
+
+void g_maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p, const at::Tensor& y, const at::Tensor& idx) {
+  auto g = pool_geometry(x, y, idx, k, s, p);
+  c10::hip::HIPGuard guard(x.device().index());
+  garfield::gpu::maxpool_fwd_nhwc(u16(x), g, u16_mut(y), static_cast<uint8_t*>(idx.data_ptr()), stream_of(x.device()));
+}
+
+void g_maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t k, int64_t s, int64_t p, const at::Tensor& dx) {
+  auto g = pool_geometry(dx, dy, idx, k, s, p);
+  c10::hip::HIPGuard guard(dx.device().index());
+  garfield::gpu::maxpool_bwd_nhwc(u16(dy), static_cast<const uint8_t*>(idx.data_ptr()), g, u16_mut(dx),
+                                  stream_of(dx.device()));
+}
+
 int g_flatten_cast_at(const std::vector<at::Tensor>& srcs, const std::vector<int64_t>& offsets,
                       const at::Tensor& dst) {
   TORCH_CHECK(srcs.size() == offsets.size(), "flatten_cast_at: one offset per source tensor");
@@ -598,6 +669,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "(dcol, kh, kw, sh, sw, ph, pw, dh, dw, dx, accumulate=False); accumulate adds into dx",
         py::arg("dcol"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("dh"), py::arg("dw"), py::arg("dx"), py::arg("accumulate") = false);
+
+  m.def("gpu_iconv", &g_iconv, "Implicit-GEMM NHWC convolution on MFMA: y = conv(x, w) (+ add); args (x, w, kh, kw, "
+        "sh, sw, ph, pw, dh, dw, y, add=None, pm=0); x/y/add channels_last bf16, C % 32 == 0, Cout % 64 == 0",
+        py::arg("x"), py::arg("w"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
+        py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("y"), py::arg("add") = py::none(), py::arg("pm") = 0);
+
+  m.def("gpu_maxpool_fwd", &g_maxpool_fwd, "NHWC bf16 max pooling (k x k, stride s, padding p) keeping the "
+        "argmax tap per element; args (x, k, s, p, y, idx)");
+  m.def("gpu_maxpool_bwd", &g_maxpool_bwd, "Max-pooling backward as a gather; args (dy, idx, k, s, p, dx)");
 
   // CPU building blocks (thread pool)
   def_rows(m, "cpu_pairwise",

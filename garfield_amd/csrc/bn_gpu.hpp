@@ -40,6 +40,14 @@ void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t 
 
 // The adjoint gather: dx[n][hi][wi][c] = Σ_{taps (i, j) hitting (hi, wi)} dcol[(n*Ho + ho)*Wo + wo][(i*KW + j)*C + c]
 // (fp32 accumulation, every element written once: no atomics, deterministic).
+// Implicit-GEMM convolution on MFMA (iconv_nhwc.hip): y[m, co] = Σ x-patch · w[co, (i, j, ci)]
+// (+ add[m, co]); C % 32 == 0, Cout % 64 == 0; pm = pixel fragments per wave (0: auto).
+void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
+                int pm, hipStream_t stream);
+// Max pooling over NHWC bf16 (C % 8 == 0); idx: the window tap of each output maximum
+// (one byte per output element), consumed by the gather backward.
+void maxpool_fwd_nhwc(const uint16_t* x, const Im2col& g, uint16_t* y, uint8_t* idx, hipStream_t stream);
+void maxpool_bwd_nhwc(const uint16_t* dy, const uint8_t* idx, const Im2col& g, uint16_t* dx, hipStream_t stream);
 // accumulate: dx += col2im(dcol) instead of dx = col2im(dcol).
 void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, bool accumulate, hipStream_t stream);
 

@@ -174,6 +174,82 @@ __global__ __launch_bounds__(kThreads) void k_col2im_scalar(const uint16_t* __re
   }
 }
 
+// Max pooling (NHWC, bf16, C % 8 == 0), forward keeping the window position of
+// every output element's maximum as one byte, backward as a gather over the
+// windows that cover an input pixel (no scatter, no atomics, no zero fill).
+// Ties and NaN follow ATen: the first maximum in (i, j) scan order wins, a NaN
+// always wins.
+__global__ __launch_bounds__(kThreads) void k_maxpool_fwd(const uint16_t* __restrict__ x, Im2col g,
+                                                         uint16_t* __restrict__ y, uint8_t* __restrict__ idx) {
+  const int cv = g.C / 8;
+  const int64_t total = static_cast<int64_t>(g.N) * g.Ho * g.Wo * cv;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * kThreads) {
+    const int v = static_cast<int>(t % cv);
+    const int m = static_cast<int>(t / cv);
+    const int wo = m % g.Wo;
+    const int ho = (m / g.Wo) % g.Ho;
+    const int n = m / (g.Wo * g.Ho);
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -__builtin_inff(); arg[e] = 0; }
+    for (int i = 0; i < g.KH; ++i) {
+      const int hi = ho * g.sh - g.ph + i * g.dh;
+      if (hi < 0 || hi >= g.H) continue;
+      for (int j = 0; j < g.KW; ++j) {
+        const int wi = wo * g.sw - g.pw + j * g.dw;
+        if (wi < 0 || wi >= g.W) continue;
+        float a[8];
+        load_vec<kBF16, 8>(x, ((static_cast<int64_t>(n) * g.H + hi) * g.W + wi) * g.C + v * 8, a);
+        const int tap = i * g.KW + j;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (a[e] > best[e] || (a[e] != a[e] && best[e] == best[e])) { best[e] = a[e]; arg[e] = tap; }
+      }
+    }
+    const int64_t o = static_cast<int64_t>(m) * g.C + v * 8;
+    store_vec<8>(y, kBF16, o, best);
+    uint2 packed;
+    packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (static_cast<uint32_t>(arg[3]) << 24);
+    packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (static_cast<uint32_t>(arg[7]) << 24);
+    *reinterpret_cast<uint2*>(idx + o) = packed;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_maxpool_bwd(const uint16_t* __restrict__ dy,
+                                                         const uint8_t* __restrict__ idx, Im2col g,
+                                                         uint16_t* __restrict__ dx) {
+  const int cv = g.C / 8;
+  const int64_t total = static_cast<int64_t>(g.N) * g.H * g.W * cv;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * kThreads) {
+    const int v = static_cast<int>(t % cv);
+    const int pix = static_cast<int>(t / cv);
+    const int wi = pix % g.W;
+    const int hi = (pix / g.W) % g.H;
+    const int n = pix / (g.W * g.H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < g.KH; ++i) {
+      for (int j = 0; j < g.KW; ++j) {
+        const int m = tap_row(g, n, hi, wi, i, j);
+        if (m < 0) continue;
+        const int64_t o = static_cast<int64_t>(m) * g.C + v * 8;
+        const uint2 p = *reinterpret_cast<const uint2*>(idx + o);
+        const int tap = i * g.KW + j;
+        float d[8];
+        load_vec<kBF16, 8>(dy, o, d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t word = e < 4 ? p.x : p.y;
+          if (static_cast<int>((word >> (8 * (e & 3))) & 0xffu) == tap) acc[e] += d[e];
+        }
+      }
+    }
+    store_vec<8>(dx, kBF16, static_cast<int64_t>(pix) * g.C + v * 8, acc);
+  }
+}
+
 }  // namespace
 
 void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t stream) {
@@ -201,6 +277,26 @@ void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, bool accum
   else if (vec) hipLaunchKernelGGL(k_col2im_vec<false>, grid, dim3(kThreads), 0, stream, dcol, g, dx);
   else if (accumulate) hipLaunchKernelGGL(k_col2im_scalar<true>, grid, dim3(kThreads), 0, stream, dcol, g, dx);
   else hipLaunchKernelGGL(k_col2im_scalar<false>, grid, dim3(kThreads), 0, stream, dcol, g, dx);
+}
+
+namespace {
+unsigned grid_for(int64_t items) {
+  int64_t blocks = (items + kThreads - 1) / kThreads;
+  if (blocks > 65536) blocks = 65536;  // grid-stride beyond
+  return static_cast<unsigned>(blocks < 1 ? 1 : blocks);
+}
+}  // namespace
+
+void maxpool_fwd_nhwc(const uint16_t* x, const Im2col& g, uint16_t* y, uint8_t* idx, hipStream_t stream) {
+  const int64_t items = static_cast<int64_t>(g.N) * g.Ho * g.Wo * (g.C / 8);
+  if (items <= 0) return;
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for(items)), dim3(kThreads), 0, stream, x, g, y, idx);
+}
+
+void maxpool_bwd_nhwc(const uint16_t* dy, const uint8_t* idx, const Im2col& g, uint16_t* dx, hipStream_t stream) {
+  const int64_t items = static_cast<int64_t>(g.N) * g.H * g.W * (g.C / 8);
+  if (items <= 0) return;
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(items)), dim3(kThreads), 0, stream, dy, idx, g, dx);
 }
 
 }  // namespace gpu

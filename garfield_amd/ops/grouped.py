@@ -30,6 +30,7 @@ test suite); on the GPU the native extension is mandatory.
 """
 from __future__ import annotations
 
+import math
 import os
 
 import torch
@@ -44,6 +45,10 @@ from garfield_amd.utils.flat import is_dense
 # solvers are not HIP-graph replay safe on ROCm 7 / gfx950 (non-finite weight
 # gradients from a replay on), so "miopen" is only for eager A/B runs.
 CONV_MODE = os.environ.get("GARFIELD_GROUPED_CONV", "gemm")
+# Implicit-GEMM MFMA convolutions (iconv_nhwc.hip) for the k x k layers whose
+# channel counts fit its tiles (C % 32, Cout % 64): forward, and the stride-1 data
+# gradient as a convolution with the flipped weight. "0" keeps im2col + GEMM.
+ICONV = os.environ.get("GARFIELD_ICONV", "1") != "0"
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -390,6 +395,39 @@ def _wmat(w: torch.Tensor, kp: int) -> torch.Tensor:
     return F.pad(w2, (0, kp - w2.shape[1])) if kp != w2.shape[1] else w2
 
 
+def _iconv_ok(x: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
+    """The MFMA kernel keeps one global-load round trip per 32-deep k-step in flight
+    per wave, so it wins where the reduction is short and the pixel count large
+    (CIFAR layer1: K = 576, 128k output pixels: 51 vs 79 µs forward, 52 vs 77 µs
+    data gradient) and loses to im2col + hipBLASLt on the deep, narrow layers
+    (layer2-4: K = 1152-4608 on 32k-2k pixels, measured 1.7-3.8x slower)."""
+    K = w.shape[1] * w.shape[2] * w.shape[3]
+    return (ICONV and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.shape[1] % 32 == 0 and w.shape[0] % 64 == 0 and K <= 640 and rows >= 32768)
+
+
+def _iconv(x: torch.Tensor, w: torch.Tensor, geom, out_hw, add: torch.Tensor | None = None) -> torch.Tensor:
+    """y = conv(x, w) (+ add, written in place of add when given) on the MFMA kernel."""
+    n = x.shape[0]
+    if add is not None:
+        y = add
+    else:
+        y = torch.empty((n, w.shape[0], *out_hw), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    _native.native().gpu_iconv(x, w, *geom, y, add)
+    return y
+
+
+def _dgrad_weight_shape(w: torch.Tensor) -> torch.Tensor:
+    """A meta tensor shaped like ``_dgrad_weight(w)`` (for the kernel-choice test)."""
+    return torch.empty((w.shape[1], w.shape[0], w.shape[2], w.shape[3]), dtype=w.dtype, device="meta")
+
+
+def _dgrad_weight(w: torch.Tensor) -> torch.Tensor:
+    """W'[ci, i', j', co] = W[co, KH-1-i', KW-1-j', ci] as a channels_last [Cin, Cout, KH, KW] tensor: the
+    data gradient of a stride-1 convolution is the convolution of dy with W'."""
+    return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+
+
 def _channels_last_weight(w: torch.Tensor) -> bool:
     return w.dim() == 4 and w.is_contiguous(memory_format=torch.channels_last)
 
@@ -444,6 +482,10 @@ class _GroupedConv(torch.autograd.Function):
             ctx.mode = "rows"
             ctx.save_for_backward(x, w)
             return from_rows(torch.mm(rows2d(x), w.reshape(w.shape[0], -1).t()), n, h, wd)
+        if CONV_MODE == "gemm" and _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
+            ctx.mode = "iconv"
+            ctx.save_for_backward(x, w)
+            return _iconv(x, w, _geom(spec), _out_hw(spec, h, wd))
         if x.is_cuda and CONV_MODE == "gemm" and _channels_last_weight(w):
             ctx.mode = "col"
             col = _im2col(x, spec)
@@ -482,6 +524,33 @@ class _GroupedConv(torch.autograd.Function):
                 out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype)
                 dW = _wgrad(dy2, rows2d(a), G, out)
                 if out is None:
+                    spec.sink.put_groups(spec.conv.weight, dW)
+        elif mode == "iconv":                    # a = x
+            (kh, kw), (sh, sw), (ph, pw), (dh, dw) = spec.kernel, spec.stride, spec.padding, spec.dilation
+            col = _im2col(a, spec)
+            kp = col.shape[1]
+            if need_dx:
+                if ((sh, sw, dh, dw) == (1, 1, 1, 1) and ph <= kh - 1 and pw <= kw - 1
+                        and _iconv_ok(dy, _dgrad_weight_shape(w), dy2.shape[0])):
+                    dx = _iconv(dy, _dgrad_weight(w), (kh, kw, 1, 1, kh - 1 - ph, kw - 1 - pw, 1, 1), (h, wd),
+                                _cl(prev) if prev is not None else None)
+                else:
+                    dcol = torch.mm(dy2, _wmat(w, kp))
+                    if prev is not None:
+                        dx = _cl(prev)
+                        _native.native().gpu_col2im(dcol, *_geom(spec), dx, True)
+                    else:
+                        dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device,
+                                         memory_format=torch.channels_last)
+                        _native.native().gpu_col2im(dcol, *_geom(spec), dx)
+                prev = None
+            if spec.sink is not None:
+                K = w.numel() // cout
+                out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if kp == K else None
+                dW = _wgrad(dy2, col, G, out)
+                if out is None:
+                    if kp != K:
+                        dW = dW[:, :, :K].contiguous()
                     spec.sink.put_groups(spec.conv.weight, dW)
         elif mode == "col":                      # a = col [N*Ho*Wo, Kp]
             kp = a.shape[1]
@@ -525,6 +594,55 @@ def grouped_conv(x, spec: ConvSpec, join: GradJoin | None = None):
     """Convolution with per-worker weight gradients; ``join``: x's other gradient
     branch (see ``GradJoin``)."""
     return _GroupedConv.apply(_cl(x), spec.conv.weight, spec, join)
+
+
+# --------------------------------------------------------------------------- #
+# Max pooling (the stem's 3x3/2): no per-worker state, only a faster kernel
+
+
+def _pool_args(mp: torch.nn.MaxPool2d):
+    def one(v):
+        if isinstance(v, (tuple, list)):
+            return v[0] if len(set(v)) == 1 else None
+        return v
+    return one(mp.kernel_size), one(mp.stride if mp.stride is not None else mp.kernel_size), one(mp.padding), \
+        one(mp.dilation)
+
+
+class _MaxPool(torch.autograd.Function):
+    """NHWC max pooling keeping a one-byte argmax per output element; the backward
+    is a gather over the covering windows (ATen's NHWC backward scatters into a
+    zero-filled gradient: 102 + 10 µs vs ~15 µs for the stem of the grouped
+    ResNet-50 step)."""
+
+    @staticmethod
+    def forward(ctx, x, k: int, s: int, p: int):
+        n, c, h, w = x.shape
+        ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+        y = torch.empty((n, c, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        idx = torch.empty((n * ho * wo * c,), dtype=torch.uint8, device=x.device)
+        _native.native().gpu_maxpool_fwd(x, k, s, p, y, idx)
+        ctx.geom = (k, s, p)
+        ctx.xshape = tuple(x.shape)
+        ctx.save_for_backward(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        k, s, p = ctx.geom
+        dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        _native.native().gpu_maxpool_bwd(_cl(dy), idx, k, s, p, dx)
+        return dx, None, None, None
+
+
+def grouped_maxpool(x: torch.Tensor, mp: torch.nn.MaxPool2d) -> torch.Tensor:
+    k, s, p, d = _pool_args(mp)
+    if (x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0 and d == 1 and not mp.ceil_mode
+            and None not in (k, s, p) and 2 * p <= k and k * k <= 256):
+        return _MaxPool.apply(_cl(x), int(k), int(s), int(p))
+    y = F.max_pool2d(x, mp.kernel_size, mp.stride, mp.padding, mp.dilation, mp.ceil_mode)
+    return y.contiguous(memory_format=torch.channels_last)
 
 
 # --------------------------------------------------------------------------- #

@@ -21,7 +21,7 @@ import torch.nn.functional as F
 
 from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
 from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, grouped_bn,
-                                      grouped_conv, grouped_linear)
+                                      grouped_conv, grouped_linear, grouped_maxpool)
 
 
 def supports(model: nn.Module) -> bool:
@@ -92,9 +92,7 @@ class GroupedResNet:
         m = self.model
         x = self._bn(self._conv(x, m.conv1), m.bn1, True)
         if isinstance(m.maxpool, nn.MaxPool2d):
-            mp = m.maxpool
-            x = F.max_pool2d(x, mp.kernel_size, mp.stride, mp.padding, mp.dilation, mp.ceil_mode)
-            x = x.contiguous(memory_format=torch.channels_last)
+            x = grouped_maxpool(x, m.maxpool)
         for layer in (m.layer1, m.layer2, m.layer3, m.layer4):
             for blk in layer:
                 x = self._block(blk, x)

@@ -108,6 +108,59 @@ def test_col2im_matches_fold(cuda, native, N, C, H, k, s, p):
     assert rel(dx.float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,C,Co,H,k,s,p,pm", [(4, 64, 64, 8, 3, 1, 1, 0), (3, 128, 128, 7, 3, 2, 1, 2),
+                                                (5, 64, 256, 8, 1, 2, 0, 1), (2, 256, 64, 5, 1, 1, 0, 4),
+                                                (7, 32, 128, 9, 3, 1, 1, 4), (2, 64, 64, 6, 3, 1, 0, 1),
+                                                (9, 512, 512, 2, 3, 1, 1, 0)])
+def test_iconv_matches_conv2d(cuda, native, N, C, Co, H, k, s, p, pm):
+    """Implicit-GEMM MFMA convolution vs an fp32 conv2d of the same bf16 operands (ragged pixel tiles,
+    strides, padding, the fused add)."""
+    x = torch.randn(N, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, k, k, device=cuda) / (C * k * k) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.float(), w.float(), None, s, p)
+    y = torch.empty(ref.shape, dtype=torch.bfloat16, device=cuda, memory_format=torch.channels_last)
+    native.gpu_iconv(x, w, k, k, s, s, p, p, 1, 1, y, None, pm)
+    assert rel(y.float(), ref) < 1e-2
+    add = torch.randn(ref.shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref2 = ref + add.float()
+    native.gpu_iconv(x, w, k, k, s, s, p, p, 1, 1, add, add, pm)   # in place: add += conv
+    assert rel(add.float(), ref2) < 1e-2
+
+
+def test_iconv_dgrad_matches_autograd(cuda, native):
+    """The stride-1 data gradient as a convolution with the flipped, transposed weight."""
+    from garfield_amd.ops.grouped import _dgrad_weight
+
+    x = torch.randn(4, 64, 8, 8, device=cuda, requires_grad=True)
+    w = (torch.randn(128, 64, 3, 3, device=cuda) / 24).to(torch.bfloat16).float()
+    dy = torch.randn(4, 128, 8, 8, device=cuda).to(torch.bfloat16).float()
+    F.conv2d(x, w, None, 1, 1).backward(dy)
+    dyb = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wb = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dx = torch.empty(4, 64, 8, 8, dtype=torch.bfloat16, device=cuda, memory_format=torch.channels_last)
+    native.gpu_iconv(dyb, _dgrad_weight(wb), 3, 3, 1, 1, 1, 1, 1, 1, dx)
+    assert rel(dx.float(), x.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,C,H,k,s,p", [(4, 64, 16, 3, 2, 1), (3, 8, 7, 2, 2, 0), (2, 16, 9, 3, 1, 1)])
+def test_maxpool_matches_aten(cuda, N, C, H, k, s, p):
+    from garfield_amd.ops.grouped import grouped_maxpool
+
+    mp = nn.MaxPool2d(k, s, p)
+    x = torch.randn(N, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x[0, 0, :2, :2] = 1.0                      # ties: the first maximum in scan order takes the gradient
+    xr = x.detach().clone().requires_grad_(True)
+    xa = x.detach().clone().requires_grad_(True)
+    y = grouped_maxpool(xr, mp)
+    ya = F.max_pool2d(xa, k, s, p)
+    assert torch.equal(y, ya)
+    dy = torch.randn_like(ya)
+    y.backward(dy)
+    ya.backward(dy)
+    assert torch.allclose(xr.grad.float(), xa.grad.float(), atol=1e-2, rtol=1e-2)
+
+
 def test_flatten_cast_at(cuda, native):
     dst = torch.zeros(1000, dtype=torch.bfloat16, device=cuda)
     a = torch.randn(37, device=cuda)
