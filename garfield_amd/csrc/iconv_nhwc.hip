@@ -138,6 +138,169 @@ __global__ __launch_bounds__(256) void k_iconv(const uint16_t* __restrict__ x, c
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-staged variant (C % 64 == 0): every 64-deep k-step (one tap, 64 input
+// channels) of the workgroup's W tile [64 co x 64 k] and X tile [64*PM pixels x
+// 64 k] is copied global -> LDS by global_load_lds (16 B per lane, no VGPR
+// round trip), NS stages deep, so a wave keeps NS-1 stages of loads in flight
+// instead of one (the register variant above is one load latency per k-step).
+// LDS images are [row][8 x 16-byte chunks] with the chunk index XOR-swizzled by
+// (row & 7) on the GLOBAL side (glds writes lane-linear): the fragment reads
+// (16 rows x one chunk) then hit 8 different bank groups.
+
+__device__ __attribute__((aligned(16))) uint4 g_iconv_zero[8];  // 128 zero bytes: source of padded taps
+
+using lds_ptr = __attribute__((address_space(3))) void*;
+
+template <int PM, int NS, bool ADD>
+__global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                   Im2col g, int Cout, uint16_t* y, const uint16_t* add) {
+  constexpr int BM = 64 * PM;          // pixels per workgroup
+  constexpr int XB = BM * 128;         // X tile bytes per stage
+  constexpr int WB = 64 * 128;         // W tile bytes per stage
+  constexpr int SB = XB + WB;
+  constexpr int XI = XB / 1024 / 4;    // X glds instructions per wave per stage
+  constexpr int WI = WB / 1024 / 4;    // W glds instructions per wave per stage (2)
+  __shared__ __attribute__((aligned(16))) char lds[NS * SB];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int M = g.N * g.Ho * g.Wo;
+  const int K = g.KH * g.KW * g.C;
+  const int m0 = blockIdx.x * BM;
+  const int co0 = blockIdx.y * 64;
+  const int lrow = lane >> 3, lchunk = lane & 7;
+
+  // this lane's sources: X rows (wave*XI + u)*8 + lrow, W rows (wave*WI + u)*8 + lrow
+  int xh[XI], xw[XI], xn[XI], xq[XI];
+  bool xv[XI];
+#pragma unroll
+  for (int u = 0; u < XI; ++u) {
+    const int px = (wave * XI + u) * 8 + lrow;
+    const int m = m0 + px;
+    xv[u] = m < M;
+    const int mm = xv[u] ? m : 0;
+    const int wo = mm % g.Wo;
+    const int t = mm / g.Wo;
+    xh[u] = (t % g.Ho) * g.sh - g.ph;
+    xw[u] = wo * g.sw - g.pw;
+    xn[u] = t / g.Ho;
+    xq[u] = lchunk ^ (px & 7);
+  }
+  const uint16_t* wsrc[WI];
+#pragma unroll
+  for (int u = 0; u < WI; ++u) {
+    const int co = (wave * WI + u) * 8 + lrow;
+    wsrc[u] = w + static_cast<int64_t>(co0 + co) * K + (lchunk ^ (co & 7)) * 8;
+  }
+  const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
+
+  const int csteps = g.C / 64;
+  const int steps = g.KH * g.KW * csteps;
+
+  auto issue = [&](int s, int slot) {
+    const int tap = s / csteps;
+    const int c0 = (s - tap * csteps) * 64;
+    const int i = tap / g.KW, j = tap - (tap / g.KW) * g.KW;
+    char* base = lds + slot * SB;
+#pragma unroll
+    for (int u = 0; u < WI; ++u)
+      __builtin_amdgcn_global_load_lds(wsrc[u] + tap * g.C + c0, (lds_ptr)(base + XB + (wave * WI + u) * 1024), 16, 0,
+                                       0);
+#pragma unroll
+    for (int u = 0; u < XI; ++u) {
+      const int hi = xh[u] + i * g.dh, wi = xw[u] + j * g.dw;
+      const bool ok = xv[u] && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+      // both addresses computed, then one select (a conditional address expression
+      // becomes a branch around each load)
+      const int hc = ok ? hi : 0, wc = ok ? wi : 0;
+      const uint64_t ax = reinterpret_cast<uint64_t>(
+          x + ((static_cast<int64_t>(xn[u]) * g.H + hc) * g.W + wc) * g.C + c0 + xq[u] * 8);
+      const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? ax : az),
+                                       (lds_ptr)(base + (wave * XI + u) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[PM][4];
+#pragma unroll
+  for (int r = 0; r < PM; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets inside a stage (row-major 128-B rows, swizzled chunks)
+  const int fr = lane & 15, fq = lane >> 4;   // row in fragment, 8-element k slice
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < steps) issue(s0, s0);
+
+  for (int s = 0; s < steps; ++s) {
+    // stage s has landed when at most (stages issued after it) x (glds per stage) are outstanding
+    const int ahead = (steps - 1 - s) < (NS - 2) ? (steps - 1 - s) : (NS - 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (WI + XI)) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WI + XI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
+    const char* base = lds + (s % NS) * SB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 a[4], b[PM];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int row = c * 16 + fr;
+        const int chunk = (ks * 4 + fq) ^ (row & 7);
+        a[c] = *reinterpret_cast<const bf16x8*>(base + XB + row * 128 + chunk * 16);
+      }
+#pragma unroll
+      for (int r = 0; r < PM; ++r) {
+        const int row = (wave * PM + r) * 16 + fr;
+        const int chunk = (ks * 4 + fq) ^ (row & 7);
+        b[r] = *reinterpret_cast<const bf16x8*>(base + row * 128 + chunk * 16);
+      }
+#pragma unroll
+      for (int r = 0; r < PM; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[r], acc[r][c], 0, 0, 0);
+    }
+    // every wave's fragment reads of this slot retire before the barrier that lets it be refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+#pragma unroll
+  for (int r = 0; r < PM; ++r) {
+    const int m = m0 + (wave * PM + r) * 16 + fr;
+    if (m >= M) continue;
+    const int64_t rowoff = static_cast<int64_t>(m) * Cout;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t off = rowoff + co0 + c * 16 + fq * 4;
+      float v[4] = {acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]};
+      if constexpr (ADD) {
+        const uint2 a = *reinterpret_cast<const uint2*>(add + off);
+        v[0] += bf16_to_f(static_cast<uint16_t>(a.x & 0xffffu));
+        v[1] += bf16_to_f(static_cast<uint16_t>(a.x >> 16));
+        v[2] += bf16_to_f(static_cast<uint16_t>(a.y & 0xffffu));
+        v[3] += bf16_to_f(static_cast<uint16_t>(a.y >> 16));
+      }
+      uint2 o;
+      o.x = static_cast<uint32_t>(f_to_bf16(v[0])) | (static_cast<uint32_t>(f_to_bf16(v[1])) << 16);
+      o.y = static_cast<uint32_t>(f_to_bf16(v[2])) | (static_cast<uint32_t>(f_to_bf16(v[3])) << 16);
+      *reinterpret_cast<uint2*>(y + off) = o;
+    }
+  }
+}
+
+template <int PM, int NS>
+void launch_lds(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
+                hipStream_t stream) {
+  const int M = g.N * g.Ho * g.Wo;
+  const dim3 grid((M + 64 * PM - 1) / (64 * PM), Cout / 64);
+  if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+  else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+}
+
 template <int PM>
 void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
             hipStream_t stream) {
@@ -153,11 +316,20 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
                 int pm, hipStream_t stream) {
   const int M = g.N * g.Ho * g.Wo;
   if (M <= 0) return;
-  if (pm <= 0) {  // measured (scripts/bench_iconv.py): the largest pixel tile that keeps ~256 workgroups
+  if (pm <= 0) {  // measured (scripts/bench_iconv.py): the largest pixel tile that keeps ~500 workgroups
     const int64_t ncb = Cout / 64;
     pm = 4;
-    while (pm > 1 && ((M + 64 * pm - 1) / (64 * pm)) * ncb < 250) pm /= 2;
+    while (pm > 1 && ((M + 64 * pm - 1) / (64 * pm)) * ncb < 500) pm /= 2;
+    if (g.C % 64 == 0) pm += 10;   // the LDS-staged kernel whenever its k-step fits
   }
+  // pm 11 / 12 / 14: the LDS-staged kernel with 1 / 2 / 4 pixel fragments per wave (C % 64 == 0)
+  if (pm > 10 && g.C % 64 == 0) {
+    if (pm == 11) launch_lds<1, 4>(x, w, g, Cout, y, add, stream);
+    else if (pm == 12) launch_lds<2, 3>(x, w, g, Cout, y, add, stream);
+    else launch_lds<4, 2>(x, w, g, Cout, y, add, stream);
+    return;
+  }
+  if (pm > 10) pm -= 10;
   if (pm >= 4) launch<4>(x, w, g, Cout, y, add, stream);
   else if (pm == 2) launch<2>(x, w, g, Cout, y, add, stream);
   else launch<1>(x, w, g, Cout, y, add, stream);

@@ -78,11 +78,17 @@ __global__ __launch_bounds__(kThreads) void k_im2col_scalar(const uint16_t* __re
 
 // Chunked path (any C, ldc % 8 == 0, e.g. the 3-channel stem padded to 152
 // columns): one thread gathers 8 consecutive columns of one col row and writes
-// them with one 16-byte store.
+// them with one 16-byte store. C_/KW_/L8_ != 0 fix the channel count, kernel
+// width and 16-byte chunks per row at compile time (the ResNet stem: 3, 7, 19),
+// turning the per-element divisions into multiplies; out-of-range taps load a
+// clamped in-bounds element and are zeroed by a select (no branch per load).
+template <int C_, int KW_, int L8_>
 __global__ __launch_bounds__(kThreads) void k_im2col_chunk8(const uint16_t* __restrict__ x, Im2col g,
                                                            uint16_t* __restrict__ col, int rows_per_wg) {
-  const int K = g.KH * g.KW * g.C;
-  const int L8 = g.ldc / 8;
+  const int C = C_ ? C_ : g.C;
+  const int KW = KW_ ? KW_ : g.KW;
+  const int L8 = L8_ ? L8_ : g.ldc / 8;
+  const int K = g.KH * KW * C;
   const int rows = g.N * g.Ho * g.Wo;
   for (int t = threadIdx.x; t < rows_per_wg * L8; t += kThreads) {
     const int m = blockIdx.x * rows_per_wg + t / L8;
@@ -91,23 +97,22 @@ __global__ __launch_bounds__(kThreads) void k_im2col_chunk8(const uint16_t* __re
     const int wo = m % g.Wo;
     const int ho = (m / g.Wo) % g.Ho;
     const int n = m / (g.Wo * g.Ho);
-    uint16_t v[8];
+    const int h0 = ho * g.sh - g.ph, w0 = wo * g.sw - g.pw;
+    const int64_t nbase = static_cast<int64_t>(n) * g.H;
+    uint32_t v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int r = r0 + e;
-      uint16_t val = 0;
-      if (r < K) {
-        const int kp = r / g.C, c = r % g.C;
-        const int hi = ho * g.sh - g.ph + (kp / g.KW) * g.dh;
-        const int wi = wo * g.sw - g.pw + (kp % g.KW) * g.dw;
-        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-          val = x[((static_cast<int64_t>(n) * g.H + hi) * g.W + wi) * g.C + c];
-      }
-      v[e] = val;
+      const int kp = r / C, c = r - (r / C) * C;
+      const int hi = h0 + (kp / KW) * g.dh;
+      const int wi = w0 + (kp - (kp / KW) * KW) * g.dw;
+      const bool ok = r < K && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+      const uint16_t val = x[((nbase + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * C + (ok ? c : 0)];
+      v[e] = ok ? val : 0u;
     }
     uint4 w;
-    w.x = v[0] | (uint32_t(v[1]) << 16); w.y = v[2] | (uint32_t(v[3]) << 16);
-    w.z = v[4] | (uint32_t(v[5]) << 16); w.w = v[6] | (uint32_t(v[7]) << 16);
+    w.x = v[0] | (v[1] << 16); w.y = v[2] | (v[3] << 16);
+    w.z = v[4] | (v[5] << 16); w.w = v[6] | (v[7] << 16);
     *reinterpret_cast<uint4*>(col + static_cast<int64_t>(m) * g.ldc + r0) = w;
   }
 }
@@ -262,7 +267,9 @@ void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t 
   if (rpw < 1) rpw = 1;
   const dim3 grid((rows + rpw - 1) / rpw);
   if (vec) hipLaunchKernelGGL(k_im2col_vec, grid, dim3(kThreads), 0, stream, x, g, col, rpw);
-  else if (chunk8) hipLaunchKernelGGL(k_im2col_chunk8, grid, dim3(kThreads), 0, stream, x, g, col, rpw);
+  else if (chunk8 && g.C == 3 && g.KW == 7 && g.ldc == 152)
+    hipLaunchKernelGGL((k_im2col_chunk8<3, 7, 19>), grid, dim3(kThreads), 0, stream, x, g, col, rpw);
+  else if (chunk8) hipLaunchKernelGGL((k_im2col_chunk8<0, 0, 0>), grid, dim3(kThreads), 0, stream, x, g, col, rpw);
   else hipLaunchKernelGGL(k_im2col_scalar, grid, dim3(kThreads), 0, stream, x, g, col, rpw);
 }
 

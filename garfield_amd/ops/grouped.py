@@ -396,14 +396,14 @@ def _wmat(w: torch.Tensor, kp: int) -> torch.Tensor:
 
 
 def _iconv_ok(x: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
-    """The MFMA kernel keeps one global-load round trip per 32-deep k-step in flight
-    per wave, so it wins where the reduction is short and the pixel count large
-    (CIFAR layer1: K = 576, 128k output pixels: 51 vs 79 µs forward, 52 vs 77 µs
-    data gradient) and loses to im2col + hipBLASLt on the deep, narrow layers
-    (layer2-4: K = 1152-4608 on 32k-2k pixels, measured 1.7-3.8x slower)."""
-    K = w.shape[1] * w.shape[2] * w.shape[3]
+    """Use the implicit-GEMM MFMA kernel (its LDS-staged form: C % 64, Cout % 64) when
+    it has enough workgroups to fill the chip. Measured on the step's 3x3 shapes
+    (scripts/bench_iconv.py, profiles/bench_iconv_r1.log): layer1 23.9 vs 73.8 µs for
+    im2col + hipBLASLt, layer2 24.4 vs 42.3, layer3 30.5 vs 41.2; layer4 (2000 output
+    pixels, 256 workgroups over a 4608-deep reduction) stays on im2col + GEMM, 48 vs 33."""
     return (ICONV and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and x.shape[1] % 32 == 0 and w.shape[0] % 64 == 0 and K <= 640 and rows >= 32768)
+            and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
+            and -(-rows // 64) * (w.shape[0] // 64) >= 400)
 
 
 def _iconv(x: torch.Tensor, w: torch.Tensor, geom, out_hw, add: torch.Tensor | None = None) -> torch.Tensor:

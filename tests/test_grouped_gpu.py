@@ -94,6 +94,19 @@ def test_im2col_matches_unfold(cuda, native, N, C, H, k, s, p):
     assert torch.equal(col.float(), ref)
 
 
+def test_im2col_stem_padded_columns(cuda, native):
+    """The ResNet stem (C = 3, 7x7/2, col padded to 152 columns): specialised chunked gather."""
+    N, C, H, k, s, p = 5, 3, 32, 7, 2, 3
+    x = torch.randn(N, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    Ho = (H + 2 * p - k) // s + 1
+    col = torch.full((N * Ho * Ho, 152), 7.0, dtype=torch.bfloat16, device=cuda)
+    native.gpu_im2col(x, k, k, s, s, p, p, 1, 1, col)
+    ref = F.unfold(x.float(), k, padding=p, stride=s)
+    ref = ref.view(N, C, k * k, -1).permute(0, 3, 2, 1).reshape(N * Ho * Ho, k * k * C)
+    assert torch.equal(col[:, :147].float(), ref)
+    assert torch.count_nonzero(col[:, 147:]) == 0
+
+
 @pytest.mark.parametrize("N,C,H,k,s,p", [(4, 64, 8, 3, 1, 1), (3, 128, 7, 3, 2, 1), (2, 3, 32, 7, 2, 3),
                                          (5, 16, 5, 1, 2, 0), (2, 8, 4, 3, 1, 0)])
 def test_col2im_matches_fold(cuda, native, N, C, H, k, s, p):
@@ -111,7 +124,11 @@ def test_col2im_matches_fold(cuda, native, N, C, H, k, s, p):
 @pytest.mark.parametrize("N,C,Co,H,k,s,p,pm", [(4, 64, 64, 8, 3, 1, 1, 0), (3, 128, 128, 7, 3, 2, 1, 2),
                                                 (5, 64, 256, 8, 1, 2, 0, 1), (2, 256, 64, 5, 1, 1, 0, 4),
                                                 (7, 32, 128, 9, 3, 1, 1, 4), (2, 64, 64, 6, 3, 1, 0, 1),
-                                                (9, 512, 512, 2, 3, 1, 1, 0)])
+                                                (9, 512, 512, 2, 3, 1, 1, 0),
+                                                # LDS-staged variant (pm 11 / 12 / 14)
+                                                (4, 64, 64, 8, 3, 1, 1, 11), (3, 128, 128, 7, 3, 2, 1, 12),
+                                                (5, 64, 256, 8, 1, 2, 0, 14), (9, 512, 512, 2, 3, 1, 1, 12),
+                                                (7, 64, 128, 9, 3, 1, 1, 14), (2, 192, 64, 6, 3, 1, 0, 11)])
 def test_iconv_matches_conv2d(cuda, native, N, C, Co, H, k, s, p, pm):
     """Implicit-GEMM MFMA convolution vs an fp32 conv2d of the same bf16 operands (ragged pixel tiles,
     strides, padding, the fused add)."""
