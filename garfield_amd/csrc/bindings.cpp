@@ -305,16 +305,29 @@ int64_t bn_groups(const at::Tensor& x, int64_t groups) {
   return R / groups;
 }
 
+// One bit per element of the [R, C] rows (C % 8 == 0 by check_bf16_rows): a uint8 tensor of R*C/8 bytes.
+void check_relu_mask(const at::Tensor& mask, const at::Tensor& x) {
+  TORCH_CHECK(mask.device() == x.device() && mask.scalar_type() == at::kByte && mask.is_contiguous() &&
+                  mask.numel() * 8 == x.numel(),
+              "garfield bn: the ReLU mask must be a contiguous uint8 tensor of numel(x) / 8 bytes on x's device");
+}
+
 void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int64_t groups,
                   const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta, double eps,
                   double momentum, const c10::optional<at::Tensor>& run_mean,
                   const c10::optional<at::Tensor>& run_var, const at::Tensor& part, const at::Tensor& mean,
                   const at::Tensor& istd, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& y,
-                  bool relu) {
+                  bool relu, const c10::optional<at::Tensor>& mask) {
   const auto dev = x.device();
   check_bf16_rows(x, dev, "x");
   check_bf16_rows(y, dev, "y");
   TORCH_CHECK(y.sizes() == x.sizes(), "garfield bn: y must have x's shape");
+  uint8_t* mp = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(relu, "garfield bn: a ReLU mask needs relu=True");
+    check_relu_mask(*mask, x);
+    mp = static_cast<uint8_t*>(mask->data_ptr());
+  }
   const int64_t rg = bn_groups(x, groups);
   const int64_t C = x.size(1);
   const uint16_t* r = nullptr;
@@ -336,7 +349,7 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
   TORCH_CHECK((rm == nullptr) == (rv == nullptr), "garfield bn: pass both running statistics or neither");
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::bn_forward(u16(x), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
-                            static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, u16_mut(y), relu,
+                            static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, u16_mut(y), relu, mp,
                             stream_of(dev));
 }
 
@@ -353,10 +366,16 @@ void g_bn_backward(const at::Tensor& x, const at::Tensor& dy, const c10::optiona
   const int64_t rg = bn_groups(x, groups);
   const int64_t C = x.size(1);
   const uint16_t* yp = nullptr;
+  const uint8_t* mp = nullptr;
   if (y.has_value() && y->defined()) {
-    check_bf16_rows(*y, dev, "y");
-    TORCH_CHECK(y->sizes() == x.sizes(), "garfield bn: y must have x's shape");
-    yp = u16(*y);
+    if (y->scalar_type() == at::kByte) {   // the forward's ReLU bit mask
+      check_relu_mask(*y, x);
+      mp = static_cast<const uint8_t*>(y->data_ptr());
+    } else {
+      check_bf16_rows(*y, dev, "y");
+      TORCH_CHECK(y->sizes() == x.sizes(), "garfield bn: y must have x's shape");
+      yp = u16(*y);
+    }
   }
   uint16_t* dr = nullptr;
   if (dres.has_value() && dres->defined()) {
@@ -384,7 +403,7 @@ void g_bn_backward(const at::Tensor& x, const at::Tensor& dy, const c10::optiona
     gp = grow->data_ptr();
   }
   c10::hip::HIPGuard guard(dev.index());
-  garfield::gpu::bn_backward(u16(x), u16(dy), yp, rg, G, static_cast<int>(C), g, m, is, pw, cw, u16_mut(dx), dr,
+  garfield::gpu::bn_backward(u16(x), u16(dy), yp, mp, rg, G, static_cast<int>(C), g, m, is, pw, cw, u16_mut(dx), dr,
                              gp, gdt, row_stride, off_gamma, off_beta, stream_of(dev));
 }
 
@@ -658,11 +677,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_part_floats", [](int64_t rg, int groups, int C) { return garfield::gpu::bn_part_floats(rg, groups, C); });
   m.def("gpu_bn_forward", &g_bn_forward,
         "Per-worker BatchNorm(+residual)(+ReLU) forward on [k*Rg, C] bf16 rows; args (x, res|None, groups, gamma, "
-        "beta, eps, momentum, running_mean|None, running_var|None, part, mean, istd, scale, shift, y, relu)");
+        "beta, eps, momentum, running_mean|None, running_var|None, part, mean, istd, scale, shift, y, relu, "
+        "mask=None); mask: uint8 [numel/8] ReLU bit mask written for the backward",
+        py::arg("x"), py::arg("res"), py::arg("groups"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
+        py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"), py::arg("part"), py::arg("mean"),
+        py::arg("istd"), py::arg("scale"), py::arg("shift"), py::arg("y"), py::arg("relu"),
+        py::arg("mask") = py::none());
   m.def("gpu_bn_backward", &g_bn_backward,
         "Per-worker BatchNorm backward; writes dγ/dβ of worker g to grow[g*row_stride + off_(gamma|beta) + c]; "
-        "args (x, dy, y|None, groups, gamma, mean, istd, part, coef, dx, dres|None, grow|None, row_stride, "
-        "off_gamma, off_beta)");
+        "args (x, dy, y|mask|None, groups, gamma, mean, istd, part, coef, dx, dres|None, grow|None, row_stride, "
+        "off_gamma, off_beta); the ReLU test reads y > 0 (bf16) or the forward's uint8 bit mask");
   m.def("gpu_im2col", &g_im2col, "NHWC im2col of a channels_last bf16 tensor into col [N*Ho*Wo, ldc >= KH*KW*C] "
         "(pad columns zeroed); args (x, kh, kw, sh, sw, ph, pw, dh, dw, col)");
   m.def("gpu_col2im", &g_col2im, "Adjoint of gpu_im2col (gather, deterministic): dx = col2im(dcol); args "

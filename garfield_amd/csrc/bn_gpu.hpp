@@ -18,13 +18,16 @@ int64_t bn_part_floats(int64_t rg, int groups, int C);
 // mean, istd, scale, shift: [groups, C] fp32 outputs (saved for the backward).
 void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
-                float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, hipStream_t stream);
+                float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
+                hipStream_t stream);
 
-// y (nullable) = forward output, used for the ReLU mask. dres (nullable) receives dz.
+// mask (nullable, relu only): bit (r*C + c) of the byte array = y[r, c] > 0, for the backward.
+// ReLU source of the backward: mask when given, else y (nullable) > 0. dres (nullable) receives dz.
 // grow (nullable): exchange buffer; group g's dγ[c] goes to grow[g*row_stride + off_gamma + c]
 // (dβ likewise at off_beta; a negative offset skips it), cast to grow_dt.
 // coef: [groups, 3, C] fp32 workspace.
-void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, int64_t rg, int groups, int C,
+void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const uint8_t* mask, int64_t rg, int groups,
+                 int C,
                  const float* gamma, const float* mean, const float* istd, float* part, float* coef, uint16_t* dx,
                  uint16_t* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
                  hipStream_t stream);

@@ -15,7 +15,8 @@
 //             -> apply  y = relu(x*scale + shift [+ residual])      (bf16x8 I/O);
 //                its first workgroup also replays the k sequential running-stat
 //                updates of k independent workers
-//   backward: partial (Σdz, Σdz·(x-μ)) with dz = dy·[y > 0]
+//   backward: partial (Σdz, Σdz·(x-μ)) with dz = dy·[y > 0] (the ReLU test reads a
+//             one-bit-per-element mask written by the forward apply, not y)
 //             -> finalize (dγ, dβ per worker, written STRAIGHT into each
 //                worker's row of the gradient exchange buffer; apply coefficients)
 //             -> apply  dx = γ/σ·(dz - dβ/M - x̂·dγ/M)   [+ dres = dz]
@@ -79,10 +80,13 @@ __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
 //   forward : s = Σ (x - shift), q = Σ (x - shift)^2  with shift = x[first row of the group]
 //             (shifted sums: no catastrophic cancellation when |mean| >> std)
 //   backward: s = Σ dz, q = Σ dz (x - mean)
-template <bool BWD, bool RELU>
+// RM: ReLU mask source of the backward: 0 none, 1 the bf16 output y (> 0), 2 the
+// forward's bit mask (one byte per 8 channels: 1/16 of y's bytes).
+template <bool BWD, int RM>
 __global__ __launch_bounds__(kThreads) void k_partial(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                                                     const uint16_t* __restrict__ y, const float* __restrict__ mean,
-                                                     Geo geo, float* __restrict__ part) {
+                                                     const uint16_t* __restrict__ y, const uint8_t* __restrict__ mask,
+                                                     const float* __restrict__ mean, Geo geo,
+                                                     float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float red[2][kThreads * 8];
   const int C = geo.C;
   const int tc = threadIdx.x % geo.tch;
@@ -114,12 +118,19 @@ __global__ __launch_bounds__(kThreads) void k_partial(const uint16_t* __restrict
         float d0[8], d1[8];
         load8(dy, o0, d0);
         load8(dy, o1, d1);
-        if constexpr (RELU) {
+        if constexpr (RM == 1) {
           float y0[8], y1[8];
           load8(y, o0, y0);
           load8(y, o1, y1);
 #pragma unroll
           for (int i = 0; i < 8; ++i) { d0[i] = y0[i] > 0.f ? d0[i] : 0.f; d1[i] = y1[i] > 0.f ? d1[i] : 0.f; }
+        } else if constexpr (RM == 2) {
+          const uint32_t m0 = mask[o0 >> 3], m1 = mask[o1 >> 3];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            d0[i] = (m0 >> i) & 1u ? d0[i] : 0.f;
+            d1[i] = (m1 >> i) & 1u ? d1[i] : 0.f;
+          }
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -142,11 +153,15 @@ __global__ __launch_bounds__(kThreads) void k_partial(const uint16_t* __restrict
       if constexpr (BWD) {
         float d0[8];
         load8(dy, o0, d0);
-        if constexpr (RELU) {
+        if constexpr (RM == 1) {
           float y0[8];
           load8(y, o0, y0);
 #pragma unroll
           for (int i = 0; i < 8; ++i) d0[i] = y0[i] > 0.f ? d0[i] : 0.f;
+        } else if constexpr (RM == 2) {
+          const uint32_t m0 = mask[o0 >> 3];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) d0[i] = (m0 >> i) & 1u ? d0[i] : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) { s[i] += d0[i]; q[i] += d0[i] * (a0[i] - sh[i]); }
@@ -277,7 +292,8 @@ template <bool RES, bool RELU>
 __global__ __launch_bounds__(kThreads) void k_fwd_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        int64_t rg, int64_t R, int C, int tch, int rp,
-                                                       uint16_t* __restrict__ y, RunStats rs) {
+                                                       uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                                                       RunStats rs) {
   if (blockIdx.x == 0 && rs.run_mean)
     running_update(rs.mean, rs.istd, rs.groups, C, rg, rs.eps, rs.momentum, rs.run_mean, rs.run_var);
   const int tr = threadIdx.x / tch;
@@ -308,6 +324,12 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const uint16_t* __restri
       if constexpr (RELU) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = o[i] > 0.f ? o[i] : 0.f;
+        if (mask) {  // bit i: the STORED (bf16) value is > 0, exactly what a y > 0 test reads back
+          uint32_t bits = 0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) bits |= (f_to_bf16(o[i]) != 0 ? 1u : 0u) << i;
+          mask[off >> 3] = static_cast<uint8_t>(bits);
+        }
       }
       store_vec<8>(y, kBF16, off, o);
     }
@@ -343,9 +365,10 @@ __global__ __launch_bounds__(kThreads) void k_bwd_finalize(const float* __restri
   coef[o3 + 2 * C + c] = dgamma / M * is;       // c  (x̂·dγ/M = (x-μ)·c)
 }
 
-template <bool RELU, bool RES_OUT>
+template <int RM, bool RES_OUT>
 __global__ __launch_bounds__(kThreads) void k_bwd_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                                                       const uint16_t* __restrict__ y, const float* __restrict__ mean,
+                                                       const uint16_t* __restrict__ y, const uint8_t* __restrict__ mask,
+                                                       const float* __restrict__ mean,
                                                        const float* __restrict__ coef, int64_t rg, int64_t R, int C,
                                                        int tch, int rp, uint16_t* __restrict__ dx,
                                                        uint16_t* __restrict__ dres) {
@@ -365,11 +388,15 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const uint16_t* __restri
       float a[8], d[8], mu[8], ca[8], cb[8], cc[8];
       load8(x, off, a);
       load8(dy, off, d);
-      if constexpr (RELU) {
+      if constexpr (RM == 1) {
         float yy[8];
         load8(y, off, yy);
 #pragma unroll
         for (int i = 0; i < 8; ++i) d[i] = yy[i] > 0.f ? d[i] : 0.f;
+      } else if constexpr (RM == 2) {
+        const uint32_t mb = mask[off >> 3];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = (mb >> i) & 1u ? d[i] : 0.f;
       }
       load8f(mean + static_cast<int64_t>(g) * C + c, mu);
       load8f(cg + c, ca);
@@ -405,11 +432,12 @@ int64_t bn_part_floats(int64_t rg, int groups, int C) {
 
 void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
-                float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, hipStream_t stream) {
+                float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
+                hipStream_t stream) {
   const Geo g = geometry(rg, groups, C);
   const int ncb = (C + g.cb - 1) / g.cb;
-  hipLaunchKernelGGL((k_partial<false, false>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
-                     nullptr, nullptr, g, part);
+  hipLaunchKernelGGL((k_partial<false, 0>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
+                     nullptr, nullptr, nullptr, g, part);
   const dim3 fgrid((C + kFinCh - 1) / kFinCh, groups);
   hipLaunchKernelGGL(k_fwd_finalize, fgrid, dim3(kThreads), 0, stream, part, x, g, gamma, beta, eps, mean, istd,
                      scale, shift);
@@ -419,36 +447,37 @@ void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, 
   const int64_t R = rg * groups;
   const dim3 grid = apply_grid(R, rp);
   if (res) {
-    if (relu) hipLaunchKernelGGL((k_fwd_apply<true, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, rs);
-    else hipLaunchKernelGGL((k_fwd_apply<true, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, rs);
+    if (relu) hipLaunchKernelGGL((k_fwd_apply<true, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, mask, rs);
+    else hipLaunchKernelGGL((k_fwd_apply<true, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, nullptr, rs);
   } else {
-    if (relu) hipLaunchKernelGGL((k_fwd_apply<false, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, rs);
-    else hipLaunchKernelGGL((k_fwd_apply<false, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, rs);
+    if (relu) hipLaunchKernelGGL((k_fwd_apply<false, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, mask, rs);
+    else hipLaunchKernelGGL((k_fwd_apply<false, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, nullptr, rs);
   }
 }
 
-void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, int64_t rg, int groups, int C,
-                 const float* gamma, const float* mean, const float* istd, float* part, float* coef, uint16_t* dx,
+void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const uint8_t* mask, int64_t rg, int groups,
+                 int C, const float* gamma, const float* mean, const float* istd, float* part, float* coef, uint16_t* dx,
                  uint16_t* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
                  hipStream_t stream) {
   const Geo g = geometry(rg, groups, C);
   const int ncb = (C + g.cb - 1) / g.cb;
-  const bool relu = y != nullptr;
-  if (relu) hipLaunchKernelGGL((k_partial<true, true>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, dy, y, mean, g, part);
-  else hipLaunchKernelGGL((k_partial<true, false>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, dy, y, mean, g, part);
+  const int rm = mask ? 2 : (y ? 1 : 0);
+  const dim3 pgrid(g.chunks, ncb, groups);
+  if (rm == 2) hipLaunchKernelGGL((k_partial<true, 2>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
+  else if (rm == 1) hipLaunchKernelGGL((k_partial<true, 1>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
+  else hipLaunchKernelGGL((k_partial<true, 0>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
   hipLaunchKernelGGL(k_bwd_finalize, dim3((C + kFinCh - 1) / kFinCh, groups), dim3(kThreads), 0, stream, part, g,
                      gamma, istd, coef, grow, grow_dt, row_stride, off_gamma, off_beta);
   int tch, rp;
   apply_geometry(C, &tch, &rp);
   const int64_t R = rg * groups;
   const dim3 grid = apply_grid(R, rp);
-  if (relu) {
-    if (dres) hipLaunchKernelGGL((k_bwd_apply<true, true>), grid, dim3(kThreads), 0, stream, x, dy, y, mean, coef, rg, R, C, tch, rp, dx, dres);
-    else hipLaunchKernelGGL((k_bwd_apply<true, false>), grid, dim3(kThreads), 0, stream, x, dy, y, mean, coef, rg, R, C, tch, rp, dx, dres);
-  } else {
-    if (dres) hipLaunchKernelGGL((k_bwd_apply<false, true>), grid, dim3(kThreads), 0, stream, x, dy, y, mean, coef, rg, R, C, tch, rp, dx, dres);
-    else hipLaunchKernelGGL((k_bwd_apply<false, false>), grid, dim3(kThreads), 0, stream, x, dy, y, mean, coef, rg, R, C, tch, rp, dx, dres);
-  }
+#define GARFIELD_BWD_APPLY(RMV, RESV) \
+  hipLaunchKernelGGL((k_bwd_apply<RMV, RESV>), grid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, coef, rg, R, C, tch, rp, dx, dres)
+  if (rm == 2) { if (dres) GARFIELD_BWD_APPLY(2, true); else GARFIELD_BWD_APPLY(2, false); }
+  else if (rm == 1) { if (dres) GARFIELD_BWD_APPLY(1, true); else GARFIELD_BWD_APPLY(1, false); }
+  else { if (dres) GARFIELD_BWD_APPLY(0, true); else GARFIELD_BWD_APPLY(0, false); }
+#undef GARFIELD_BWD_APPLY
 }
 
 }  // namespace gpu

@@ -297,23 +297,26 @@ class _GroupedBN(torch.autograd.Function):
             C_ = _native.native()
             part = ws.get("bn_part", C_.bn_part_floats(rg, st.groups, C), x.device)
             track = bn.track_running_stats and bn.running_mean is not None
+            # the backward's ReLU test reads one bit per element instead of y
+            relu_state = torch.empty((x2.numel() // 8,), dtype=torch.uint8, device=x.device) if st.relu else None
             C_.gpu_bn_forward(x2, r2, st.groups, bn.weight, bn.bias, float(bn.eps), float(bn.momentum),
                               bn.running_mean if track else None, bn.running_var if track else None,
-                              part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu)
+                              part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu, relu_state)
         else:
             y = from_rows(_bn_fwd_ref(x2, r2, st), n, h, w)
+            relu_state = y if st.relu else None
         ctx.st, ctx.ws, ctx.has_res, ctx.join = st, ws, res is not None, join
-        ctx.save_for_backward(x, y if st.relu else None)
+        ctx.save_for_backward(x, relu_state)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y = ctx.saved_tensors
+        x, y = ctx.saved_tensors                # y: the ReLU state (bit mask on the GPU, y on the CPU) or None
         st, ws = ctx.st, ctx.ws
         n, C, h, w = x.shape
         dy = _cl(dy)
         x2, dy2 = rows2d(x), rows2d(dy)
-        y2 = rows2d(y) if y is not None else None
+        y2 = (y if y.dim() == 1 else rows2d(y)) if y is not None else None
         if x.is_cuda:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
