@@ -505,6 +505,50 @@ void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, i
                             stream_of(x.device()));
 }
 
+// Per-worker implicit weight gradient. out: fp32 [splits, groups, Cout, K] (contiguous partial
+// slabs) or, with splits == 1, a bf16 [groups, Cout, K] view whose rows are contiguous (any group
+// stride: the exchange rows).
+void g_iwgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
+              int64_t pw, int64_t dh, int64_t dw, int64_t groups, const at::Tensor& out, int64_t splits) {
+  auto g = conv_geometry(x, kh, kw, sh, sw, ph, pw, dh, dw);
+  TORCH_CHECK(g.C % 64 == 0, "gpu_iwgrad: input channels must be a multiple of 64 (got ", g.C, ")");
+  TORCH_CHECK(dy.is_cuda() && dy.device() == x.device() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.size(0) == g.N && dy.size(2) == g.Ho &&
+                  dy.size(3) == g.Wo,
+              "gpu_iwgrad: dy must be a channels_last bf16 [", g.N, ", Cout, ", g.Ho, ", ", g.Wo, "] tensor");
+  const int64_t cout = dy.size(1);
+  TORCH_CHECK(cout % 64 == 0, "gpu_iwgrad: output channels must be a multiple of 64 (got ", cout, ")");
+  const int64_t M = static_cast<int64_t>(g.N) * g.Ho * g.Wo;
+  TORCH_CHECK(groups >= 1 && M % groups == 0, "gpu_iwgrad: ", M, " output pixels do not split into ", groups,
+              " workers");
+  TORCH_CHECK(M < INT32_MAX && static_cast<int64_t>(g.N) * g.H * g.W * g.C < INT32_MAX,
+              "gpu_iwgrad: tensor too large");
+  TORCH_CHECK(splits >= 1 && splits <= 64, "gpu_iwgrad: splits must be in [1, 64]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0,
+              "gpu_iwgrad: x and dy must be 16-byte aligned");
+  const int64_t K = static_cast<int64_t>(g.KH) * g.KW * g.C;
+  TORCH_CHECK(out.device() == x.device(), "gpu_iwgrad: out must be on x's device");
+  bool bf16 = false;
+  int64_t ss = 0, gs = 0;
+  if (out.scalar_type() == at::kFloat) {
+    TORCH_CHECK(out.is_contiguous() && out.dim() == 4 && out.size(0) == splits && out.size(1) == groups &&
+                    out.size(2) == cout && out.size(3) == K,
+                "gpu_iwgrad: an fp32 out must be contiguous [splits, groups, Cout, K]");
+    ss = groups * cout * K;
+    gs = cout * K;
+  } else {
+    TORCH_CHECK(out.scalar_type() == at::kBFloat16 && splits == 1 && out.dim() == 3 && out.size(0) == groups &&
+                    out.size(1) == cout && out.size(2) == K && out.stride(2) == 1 && out.stride(1) == K &&
+                    out.stride(0) >= cout * K,
+                "gpu_iwgrad: a bf16 out must be a [groups, Cout, K] view with contiguous rows (splits == 1)");
+    bf16 = true;
+    gs = out.stride(0);
+  }
+  c10::hip::HIPGuard guard(x.device().index());
+  garfield::gpu::iwgrad_nhwc(u16(x), u16(dy), g, static_cast<int>(cout), static_cast<int>(groups), M / groups,
+                             static_cast<int>(splits), out.data_ptr(), bf16, ss, gs, stream_of(x.device()));
+}
+
 garfield::gpu::Im2col pool_geometry(const at::Tensor& x, const at::Tensor& y, const at::Tensor& idx, int64_t k,
                                     int64_t s, int64_t p) {
   auto g = conv_geometry(x, k, k, s, s, p, p, 1, 1);
@@ -699,6 +743,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("w"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
         py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("y"), py::arg("add") = py::none(), py::arg("pm") = 0);
 
+  m.def("gpu_iwgrad", &g_iwgrad, "Per-worker implicit-GEMM weight gradient on MFMA: out[s, g] = Σ over pixel "
+        "split s of worker g of dyᵀ · patches(x); args (x, dy, kh, kw, sh, sw, ph, pw, dh, dw, groups, out, splits)");
   m.def("gpu_maxpool_fwd", &g_maxpool_fwd, "NHWC bf16 max pooling (k x k, stride s, padding p) keeping the "
         "argmax tap per element; args (x, k, s, p, y, idx)");
   m.def("gpu_maxpool_bwd", &g_maxpool_bwd, "Max-pooling backward as a gather; args (dy, idx, k, s, p, dx)");

@@ -51,6 +51,11 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
 // (one byte per output element), consumed by the gather backward.
 void maxpool_fwd_nhwc(const uint16_t* x, const Im2col& g, uint16_t* y, uint8_t* idx, hipStream_t stream);
 void maxpool_bwd_nhwc(const uint16_t* dy, const uint8_t* idx, const Im2col& g, uint16_t* dx, hipStream_t stream);
+// Per-worker implicit weight gradient (iconv_nhwc.hip): out[s][g][co][k] (fp32 partial slab s of
+// worker g, or bf16 when out_bf16, e.g. straight into the exchange rows) = Σ over the s-th of `splits`
+// pixel ranges of worker g of dy[m, co] · patch(x)[m, k]; C % 64 == 0, Cout % 64 == 0, x / dy 16-B aligned.
+void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
+                 int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream);
 // accumulate: dx += col2im(dcol) instead of dx = col2im(dcol).
 void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, bool accumulate, hipStream_t stream);
 

@@ -301,6 +301,143 @@ void launch_lds(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
 }
 
+// ---------------------------------------------------------------------------
+// Implicit weight gradient, per worker, on MFMA:
+//
+//   dW_g[co, (i, j, ci)] = Σ_{m in worker g} dy[m, co] · x[pixel(m, i, j), ci]
+//
+// (the reduction runs over output pixels m, so both operands need a transpose
+// from their natural [pixel][channel] rows: the tiles are staged with
+// global_load_lds as plain 128-byte rows and read with ds_read_b64_tr_b16, whose
+// 16-lane groups gather 4 rows x 16 columns and hand lane i column i). No im2col
+// matrix is written or read. Workgroup tile: 64 output channels x 64 k-columns
+// (one tap, 64 input channels) of one worker, 32 pixels per k-step, NS-deep glds
+// ring; the worker's pixels are split ``splits`` ways (fp32 partial slabs summed
+// afterwards) when the tile grid alone cannot fill the chip.
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+using lds_s16x4 = __attribute__((address_space(3))) s16x4*;
+
+template <int NS, bool OUT_BF16>
+__global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
+                                                int64_t split_stride, int64_t group_stride) {
+  constexpr int TB = 32 * 128;  // one 32-pixel x 64-channel tile
+  constexpr int SB = 2 * TB;    // dy tile + x tile per stage
+  __shared__ __attribute__((aligned(16))) char lds[NS * SB];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int K = g.KH * g.KW * g.C;
+  const int nkb = K / 64;
+  const int kb = blockIdx.x % nkb, cb = blockIdx.x / nkb;
+  const int gi = blockIdx.y, sp = blockIdx.z;
+  const int k0 = kb * 64, co0 = cb * 64;
+  const int tap = k0 / g.C, c0 = k0 - tap * g.C;
+  const int ti = tap / g.KW, tj = tap - ti * g.KW;
+  const int64_t mbeg = static_cast<int64_t>(gi) * rg + static_cast<int64_t>(sp) * per_split;
+  int64_t mend = mbeg + per_split;
+  if (mend > static_cast<int64_t>(gi + 1) * rg) mend = static_cast<int64_t>(gi + 1) * rg;
+  const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
+
+  const int lrow = wave * 8 + (lane >> 3), lchunk = lane & 7;   // this lane's glds row / 16-byte chunk
+  const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
+  const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
+
+  auto issue = [&](int s, int slot) {
+    const int m = static_cast<int>(mbeg) + s * 32 + lrow;   // < 2^31: checked by the host wrapper
+    const bool mv = m < static_cast<int>(mend);
+    const int mm = mv ? m : 0;
+    char* base = lds + slot * SB;
+    const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lchunk * 8);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? ady : az), (lds_ptr)(base + wave * 1024), 16,
+                                     0, 0);
+    const int wo = mm % g.Wo;
+    const int t = mm / g.Wo;
+    const int ho = t % g.Ho;
+    const int n = t / g.Ho;
+    const int hi = ho * g.sh - g.ph + ti * g.dh, wi = wo * g.sw - g.pw + tj * g.dw;
+    const bool ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+    const uint64_t ax = reinterpret_cast<uint64_t>(
+        x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 + lchunk * 8);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? ax : az),
+                                     (lds_ptr)(base + TB + wave * 1024), 16, 0, 0);
+  };
+
+  // wave tile: output-channel fragments {cf0, cf0+1} x k-column fragments {kf0, kf0+1}
+  const int cf0 = 2 * (wave >> 1), kf0 = 2 * (wave & 1);
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Transposed fragments: lane i of 16-lane group grp gets tile column 16f + i at rows
+  // 8*grp .. 8*grp+7 (two ds_read_b64_tr_b16: lane 4q+p addresses row 8*grp + 4h + q, columns
+  // 16f + 4p .. +3). The reads are inline asm with their own lgkmcnt wait: as a builtin, hipcc
+  // puts a vmcnt(0) in front of them (it cannot tell them from the in-flight LDS-DMA ring
+  // stages), which serialises the ring.
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)lds));
+  const uint32_t offA = (8 * grp + q) * 128 + (16 * cf0 + 4 * p) * 2;
+  const uint32_t offB = TB + (8 * grp + q) * 128 + (16 * kf0 + 4 * p) * 2;
+
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < steps) issue(s0, s0);
+  for (int s = 0; s < steps; ++s) {
+    const int ahead = (steps - 1 - s) < (NS - 2) ? (steps - 1 - s) : (NS - 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const uint32_t sb = lds0 + (s % NS) * SB;
+    s16x4 r[8];
+    asm volatile(
+        "ds_read_b64_tr_b16 %0, %8\n\t"
+        "ds_read_b64_tr_b16 %1, %8 offset:512\n\t"
+        "ds_read_b64_tr_b16 %2, %8 offset:32\n\t"
+        "ds_read_b64_tr_b16 %3, %8 offset:544\n\t"
+        "ds_read_b64_tr_b16 %4, %9\n\t"
+        "ds_read_b64_tr_b16 %5, %9 offset:512\n\t"
+        "ds_read_b64_tr_b16 %6, %9 offset:32\n\t"
+        "ds_read_b64_tr_b16 %7, %9 offset:544\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+        : "v"(sb + offA), "v"(sb + offB)
+        : "memory");
+    // every wave's reads of this slot are done (waited above) before the next barrier lets it be refilled
+    if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
+    bf16x8 a[2], b[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const short va[8] = {r[2 * u][0], r[2 * u][1], r[2 * u][2], r[2 * u][3],
+                           r[2 * u + 1][0], r[2 * u + 1][1], r[2 * u + 1][2], r[2 * u + 1][3]};
+      const short vb[8] = {r[4 + 2 * u][0], r[4 + 2 * u][1], r[4 + 2 * u][2], r[4 + 2 * u][3],
+                           r[5 + 2 * u][0], r[5 + 2 * u][1], r[5 + 2 * u][2], r[5 + 2 * u][3]};
+      a[u] = __builtin_bit_cast(bf16x8, va);   // dy tile: A[co][m]
+      b[u] = __builtin_bit_cast(bf16x8, vb);   // x tile:  B[m][k]
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[v], acc[u][v], 0, 0, 0);
+  }
+
+  // D[co = 4*grp + e][k = li] of each (u, v) fragment
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + (cf0 + u) * 16 + 4 * grp + e;
+        const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
+                          static_cast<int64_t>(co) * K + k0 + (kf0 + v) * 16 + li;
+        if constexpr (OUT_BF16) static_cast<uint16_t*>(out)[o] = f_to_bf16(acc[u][v][e]);
+        else static_cast<float*>(out)[o] = acc[u][v][e];
+      }
+}
+
 template <int PM>
 void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
             hipStream_t stream) {
@@ -333,6 +470,20 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   if (pm >= 4) launch<4>(x, w, g, Cout, y, add, stream);
   else if (pm == 2) launch<2>(x, w, g, Cout, y, add, stream);
   else launch<1>(x, w, g, Cout, y, add, stream);
+}
+
+void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
+                 int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream) {
+  const int K = g.KH * g.KW * g.C;
+  if (splits < 1) splits = 1;
+  const int64_t per_split = (rg + splits - 1) / splits;
+  const dim3 grid((K / 64) * (Cout / 64), groups, splits);
+  if (out_bf16)
+    hipLaunchKernelGGL((k_iwgrad<3, true>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                       split_stride, group_stride);
+  else
+    hipLaunchKernelGGL((k_iwgrad<3, false>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                       split_stride, group_stride);
 }
 
 }  // namespace gpu

@@ -145,6 +145,33 @@ def test_iconv_matches_conv2d(cuda, native, N, C, Co, H, k, s, p, pm):
     assert rel(add.float(), ref2) < 1e-2
 
 
+@pytest.mark.parametrize("G,B,C,Co,H,k,s,p,splits", [(4, 3, 64, 64, 8, 3, 1, 1, 1), (4, 3, 64, 64, 8, 3, 1, 1, 4),
+                                                     (2, 5, 128, 128, 7, 3, 2, 1, 2), (3, 2, 256, 128, 4, 1, 2, 0, 1),
+                                                     (2, 9, 64, 192, 3, 3, 1, 1, 3)])
+def test_iwgrad_matches_per_worker_conv_weight_grad(cuda, native, G, B, C, Co, H, k, s, p, splits):
+    """Implicit per-worker weight gradient vs fp32 conv2d_weight of each worker's slice
+    (ragged pixel splits, strides, padding, the fp32-slab and bf16 strided-view outputs)."""
+    x = torch.randn(G * B, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    Ho = (H + 2 * p - k) // s + 1
+    dy = torch.randn(G * B, Co, Ho, Ho, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    K = k * k * C
+    ref = []
+    for gi in range(G):
+        sl = slice(gi * B, (gi + 1) * B)
+        dw = torch.nn.grad.conv2d_weight(x[sl].float(), (Co, C, k, k), dy[sl].float(), s, p)
+        ref.append(dw.permute(0, 2, 3, 1).reshape(Co, K))    # channels_last (kh, kw, ci) order
+    ref = torch.stack(ref)
+    part = torch.empty(splits, G, Co, K, device=cuda)
+    native.gpu_iwgrad(x, dy, k, k, s, s, p, p, 1, 1, G, part, splits)
+    assert rel(part.sum(0), ref) < 1e-2
+    if splits == 1:
+        flat = torch.zeros(G * (Co * K + 100), dtype=torch.bfloat16, device=cuda)
+        view = flat.as_strided((G, Co, K), (Co * K + 100, K, 1), 40)
+        native.gpu_iwgrad(x, dy, k, k, s, s, p, p, 1, 1, G, view, 1)
+        assert rel(view.float(), ref) < 1e-2
+        assert torch.count_nonzero(flat[:40]) == 0
+
+
 def test_iconv_dgrad_matches_autograd(cuda, native):
     """The stride-1 data gradient as a convolution with the flipped, transposed weight."""
     from garfield_amd.ops.grouped import _dgrad_weight
