@@ -15,13 +15,19 @@ things couple samples, and both are kept per worker:
   the ReLU and the residual add fused) and replays the k sequential running-stat
   updates;
 * **parameter gradients**: the weight gradient of every layer is produced per
-  worker (one strided-batched GEMM per layer: directly for 1x1 convolutions and
-  the classifier, over an NHWC im2col gather (``im2col_nhwc.hip``) otherwise) and
-  lands in that worker's row of the exchange buffer through a ``GradSink``;
+  worker (the implicit-GEMM MFMA kernel ``iconv_nhwc.hip:k_iwgrad`` for the
+  k x k layers, one strided-batched GEMM for 1x1 convolutions and the classifier,
+  an NHWC im2col gather + batched GEMM for the rest, e.g. the 3-channel stem) and
+  lands in that worker's row of the exchange buffer (written in place through
+  ``GradSink.rows_view``, or queued for one multi-tensor cast kernel);
   BatchNorm's dγ/dβ are written there directly by the finalize kernel.
 
 Activation gradients (dgrad) and forward convolutions run once on the whole
-batch (k-times larger GEMMs). The custom autograd functions take the real
+batch: implicit-GEMM MFMA convolutions (``k_iconv_lds``, no im2col matrix) for the
+k x k layers with enough workgroups, hipBLASLt GEMMs on the NHWC rows for 1x1
+stride-1 layers, im2col + GEMM (+ col2im) otherwise. The two gradient branches of
+a residual block's input are summed inside the second branch's kernel
+(``GradJoin``). The custom autograd functions take the real
 parameters as inputs (so the graph reaches them) but return ``None`` for them:
 nothing is accumulated into ``.grad``.
 
@@ -46,7 +52,7 @@ from garfield_amd.utils.flat import is_dense
 # gradients from a replay on), so "miopen" is only for eager A/B runs.
 CONV_MODE = os.environ.get("GARFIELD_GROUPED_CONV", "gemm")
 # Implicit-GEMM MFMA convolutions (iconv_nhwc.hip) for the k x k layers whose
-# channel counts fit its tiles (C % 32, Cout % 64): forward, and the stride-1 data
+# channel counts fit its tiles (C % 64, Cout % 64): forward, and the stride-1 data
 # gradient as a convolution with the flipped weight. "0" keeps im2col + GEMM.
 ICONV = os.environ.get("GARFIELD_ICONV", "1") != "0"
 # Their per-worker weight gradients by the implicit MFMA kernel (no im2col matrix).
