@@ -466,7 +466,7 @@ void g_col2im(const at::Tensor& dcol, int64_t kh, int64_t kw, int64_t sh, int64_
 // [Cout, KH, KW, C]-ordered weight (a channels_last 4-D weight or its [Cout, K] matrix).
 void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
              int64_t pw, int64_t dh, int64_t dw, const at::Tensor& y, const c10::optional<at::Tensor>& add,
-             int64_t pm) {
+             int64_t pm, bool transpose_w) {
   auto g = conv_geometry(x, kh, kw, sh, sw, ph, pw, dh, dw);
   TORCH_CHECK(g.C % 32 == 0, "gpu_iconv: input channels must be a multiple of 32 (got ", g.C, ")");
   TORCH_CHECK(y.is_cuda() && y.device() == x.device() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 &&
@@ -479,7 +479,12 @@ void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, i
   const int64_t K = static_cast<int64_t>(g.KH) * g.KW * g.C;
   TORCH_CHECK(w.device() == x.device() && w.scalar_type() == at::kBFloat16 && w.numel() == cout * K,
               "gpu_iconv: w must be a bf16 weight of ", cout, " x ", K, " elements on x's device");
-  if (w.dim() == 4) {
+  if (transpose_w) {
+    TORCH_CHECK(g.C % 64 == 0, "gpu_iconv: transpose_w needs C % 64 == 0");
+    TORCH_CHECK(w.dim() == 4 && w.size(0) == g.C && w.size(1) == cout && w.size(2) == g.KH && w.size(3) == g.KW &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_iconv: with transpose_w, w must be the channels_last forward weight [C, Cout, KH, KW]");
+  } else if (w.dim() == 4) {
     TORCH_CHECK(w.size(0) == cout && w.size(1) == g.C && w.size(2) == g.KH && w.size(3) == g.KW &&
                     w.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "gpu_iconv: a 4-D weight must be channels_last [Cout, C, KH, KW]");
@@ -502,7 +507,7 @@ void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, i
               "gpu_iconv: tensor too large");
   c10::hip::HIPGuard guard(x.device().index());
   garfield::gpu::iconv_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap, static_cast<int>(pm),
-                            stream_of(x.device()));
+                            transpose_w, stream_of(x.device()));
 }
 
 // Per-worker implicit weight gradient. out: fp32 [splits, groups, Cout, K] (contiguous partial
@@ -739,9 +744,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dh"), py::arg("dw"), py::arg("dx"), py::arg("accumulate") = false);
 
   m.def("gpu_iconv", &g_iconv, "Implicit-GEMM NHWC convolution on MFMA: y = conv(x, w) (+ add); args (x, w, kh, kw, "
-        "sh, sw, ph, pw, dh, dw, y, add=None, pm=0); x/y/add channels_last bf16, C % 32 == 0, Cout % 64 == 0",
+        "sh, sw, ph, pw, dh, dw, y, add=None, pm=0, transpose_w=False); x/y/add channels_last bf16, C % 32 == 0, "
+        "Cout % 64 == 0; transpose_w: w is the forward weight [C, Cout, KH, KW] whose flipped transpose is applied "
+        "(the data gradient of that convolution)",
         py::arg("x"), py::arg("w"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
-        py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("y"), py::arg("add") = py::none(), py::arg("pm") = 0);
+        py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("y"), py::arg("add") = py::none(), py::arg("pm") = 0,
+        py::arg("transpose_w") = false);
 
   m.def("gpu_iwgrad", &g_iwgrad, "Per-worker implicit-GEMM weight gradient on MFMA: out[s, g] = Σ over pixel "
         "split s of worker g of dyᵀ · patches(x); args (x, dy, kh, kw, sh, sw, ph, pw, dh, dw, groups, out, splits)");

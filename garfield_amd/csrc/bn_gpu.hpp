@@ -45,8 +45,10 @@ void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t 
 // (fp32 accumulation, every element written once: no atomics, deterministic).
 // Implicit-GEMM convolution on MFMA (iconv_nhwc.hip): y[m, co] = Σ x-patch · w[co, (i, j, ci)]
 // (+ add[m, co]); C % 32 == 0, Cout % 64 == 0; pm = pixel fragments per wave (0: auto).
+// transpose_w (C % 64 == 0): w is the forward weight [C][KH][KW][Cout] of the convolution whose data
+// gradient this computes (flipped taps, swapped channel roles).
 void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
-                int pm, hipStream_t stream);
+                int pm, bool transpose_w, hipStream_t stream);
 // Max pooling over NHWC bf16 (C % 8 == 0); idx: the window tap of each output maximum
 // (one byte per output element), consumed by the gather backward.
 void maxpool_fwd_nhwc(const uint16_t* x, const Im2col& g, uint16_t* y, uint8_t* idx, hipStream_t stream);

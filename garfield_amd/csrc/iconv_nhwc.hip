@@ -151,8 +151,14 @@ __global__ __launch_bounds__(256) void k_iconv(const uint16_t* __restrict__ x, c
 __device__ __attribute__((aligned(16))) uint4 g_iconv_zero[8];  // 128 zero bytes: source of padded taps
 
 using lds_ptr = __attribute__((address_space(3))) void*;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
 
-template <int PM, int NS, bool ADD>
+// TW: w is the FORWARD weight of a stride-1 convolution and this launch computes its data
+// gradient (x = dy, C = the forward's output channels, Cout = its input channels, padding
+// KH-1-ph): A[o][(i', j', c)] = Wf[c][KH-1-i'][KW-1-j'][o]. The W tile is staged as plain
+// [c][o] rows and its fragments are read transposed (ds_read_b64_tr_b16), so no flipped /
+// transposed weight copy is made.
+template <int PM, int NS, bool ADD, bool TW>
 __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                    Im2col g, int Cout, uint16_t* y, const uint16_t* add) {
   constexpr int BM = 64 * PM;          // pixels per workgroup
@@ -188,10 +194,12 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
     xq[u] = lchunk ^ (px & 7);
   }
   const uint16_t* wsrc[WI];
+  const int KF = g.KH * g.KW * Cout;   // TW: row stride of the forward weight
 #pragma unroll
   for (int u = 0; u < WI; ++u) {
-    const int co = (wave * WI + u) * 8 + lrow;
-    wsrc[u] = w + static_cast<int64_t>(co0 + co) * K + (lchunk ^ (co & 7)) * 8;
+    const int row = (wave * WI + u) * 8 + lrow;
+    if constexpr (TW) wsrc[u] = w + static_cast<int64_t>(row) * KF + co0 + lchunk * 8;
+    else wsrc[u] = w + static_cast<int64_t>(co0 + row) * K + (lchunk ^ (row & 7)) * 8;
   }
   const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
 
@@ -203,10 +211,12 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
     const int c0 = (s - tap * csteps) * 64;
     const int i = tap / g.KW, j = tap - (tap / g.KW) * g.KW;
     char* base = lds + slot * SB;
+    int64_t woff;
+    if constexpr (TW) woff = static_cast<int64_t>(c0) * KF + ((g.KH - 1 - i) * g.KW + (g.KW - 1 - j)) * Cout;
+    else woff = tap * g.C + c0;
 #pragma unroll
     for (int u = 0; u < WI; ++u)
-      __builtin_amdgcn_global_load_lds(wsrc[u] + tap * g.C + c0, (lds_ptr)(base + XB + (wave * WI + u) * 1024), 16, 0,
-                                       0);
+      __builtin_amdgcn_global_load_lds(wsrc[u] + woff, (lds_ptr)(base + XB + (wave * WI + u) * 1024), 16, 0, 0);
 #pragma unroll
     for (int u = 0; u < XI; ++u) {
       const int hi = xh[u] + i * g.dh, wi = xw[u] + j * g.dw;
@@ -243,14 +253,50 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
     __builtin_amdgcn_s_barrier();
     if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
     const char* base = lds + (s % NS) * SB;
+    s16x4 tr[TW ? 16 : 1];
+    if constexpr (TW) {
+      // A fragments of both 32-deep halves: lane (group grp, 4q+p) reads W-tile row
+      // 32*ks + 8*grp + 4h + q, columns 16c + 4p .. +3 (inline asm: see k_iwgrad)
+      const uint32_t ab = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)base)) + XB +
+                          (8 * (lane >> 4) + ((lane & 15) >> 2)) * 128 + 8 * (lane & 3);
+      asm volatile(
+            "ds_read_b64_tr_b16 %0, %16 offset:0\n\t"
+            "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
+            "ds_read_b64_tr_b16 %2, %16 offset:32\n\t"
+            "ds_read_b64_tr_b16 %3, %16 offset:544\n\t"
+            "ds_read_b64_tr_b16 %4, %16 offset:64\n\t"
+            "ds_read_b64_tr_b16 %5, %16 offset:576\n\t"
+            "ds_read_b64_tr_b16 %6, %16 offset:96\n\t"
+            "ds_read_b64_tr_b16 %7, %16 offset:608\n\t"
+            "ds_read_b64_tr_b16 %8, %16 offset:4096\n\t"
+            "ds_read_b64_tr_b16 %9, %16 offset:4608\n\t"
+            "ds_read_b64_tr_b16 %10, %16 offset:4128\n\t"
+            "ds_read_b64_tr_b16 %11, %16 offset:4640\n\t"
+            "ds_read_b64_tr_b16 %12, %16 offset:4160\n\t"
+            "ds_read_b64_tr_b16 %13, %16 offset:4672\n\t"
+            "ds_read_b64_tr_b16 %14, %16 offset:4192\n\t"
+            "ds_read_b64_tr_b16 %15, %16 offset:4704\n\t"
+            "s_waitcnt lgkmcnt(0)"
+          : "=&v"(tr[0]), "=&v"(tr[1]), "=&v"(tr[2]), "=&v"(tr[3]), "=&v"(tr[4]), "=&v"(tr[5]), "=&v"(tr[6]),
+            "=&v"(tr[7]), "=&v"(tr[8]), "=&v"(tr[9]), "=&v"(tr[10]), "=&v"(tr[11]), "=&v"(tr[12]), "=&v"(tr[13]),
+            "=&v"(tr[14]), "=&v"(tr[15])
+          : "v"(ab)
+          : "memory");
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 a[4], b[PM];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int row = c * 16 + fr;
-        const int chunk = (ks * 4 + fq) ^ (row & 7);
-        a[c] = *reinterpret_cast<const bf16x8*>(base + XB + row * 128 + chunk * 16);
+        if constexpr (TW) {
+          const s16x4 lo = tr[ks * 8 + 2 * c], hi = tr[ks * 8 + 2 * c + 1];
+          const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          a[c] = __builtin_bit_cast(bf16x8, v);
+        } else {
+          const int row = c * 16 + fr;
+          const int chunk = (ks * 4 + fq) ^ (row & 7);
+          a[c] = *reinterpret_cast<const bf16x8*>(base + XB + row * 128 + chunk * 16);
+        }
       }
 #pragma unroll
       for (int r = 0; r < PM; ++r) {
@@ -294,11 +340,16 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
 
 template <int PM, int NS>
 void launch_lds(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
-                hipStream_t stream) {
+                bool tw, hipStream_t stream) {
   const int M = g.N * g.Ho * g.Wo;
   const dim3 grid((M + 64 * PM - 1) / (64 * PM), Cout / 64);
-  if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
-  else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+  if (tw) {
+    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, true>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, true>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+  } else {
+    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -315,8 +366,6 @@ void launch_lds(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
 // ring; the worker's pixels are split ``splits`` ways (fp32 partial slabs summed
 // afterwards) when the tile grid alone cannot fill the chip.
 
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-using lds_s16x4 = __attribute__((address_space(3))) s16x4*;
 
 template <int NS, bool OUT_BF16>
 __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
@@ -450,7 +499,7 @@ void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uin
 }  // namespace
 
 void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
-                int pm, hipStream_t stream) {
+                int pm, bool transpose_w, hipStream_t stream) {
   const int M = g.N * g.Ho * g.Wo;
   if (M <= 0) return;
   if (pm <= 0) {  // measured (scripts/bench_iconv.py): the largest pixel tile that keeps ~500 workgroups
@@ -461,12 +510,18 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   }
   // pm 11 / 12 / 14: the LDS-staged kernel with 1 / 2 / 4 pixel fragments per wave (C % 64 == 0)
   if (pm > 10 && g.C % 64 == 0) {
-    if (pm == 11) launch_lds<1, 4>(x, w, g, Cout, y, add, stream);
-    else if (pm == 12) launch_lds<2, 3>(x, w, g, Cout, y, add, stream);
-    else launch_lds<4, 2>(x, w, g, Cout, y, add, stream);
+    if (pm == 11) launch_lds<1, 4>(x, w, g, Cout, y, add, transpose_w, stream);
+    else if (pm == 12) launch_lds<2, 3>(x, w, g, Cout, y, add, transpose_w, stream);
+    else launch_lds<4, 2>(x, w, g, Cout, y, add, transpose_w, stream);
     return;
   }
   if (pm > 10) pm -= 10;
+  if (transpose_w) {  // only the LDS-staged kernel reads the weight transposed (the wrapper checks C % 64)
+    if (pm >= 4) launch_lds<4, 2>(x, w, g, Cout, y, add, true, stream);
+    else if (pm == 2) launch_lds<2, 3>(x, w, g, Cout, y, add, true, stream);
+    else launch_lds<1, 4>(x, w, g, Cout, y, add, true, stream);
+    return;
+  }
   if (pm >= 4) launch<4>(x, w, g, Cout, y, add, stream);
   else if (pm == 2) launch<2>(x, w, g, Cout, y, add, stream);
   else launch<1>(x, w, g, Cout, y, add, stream);

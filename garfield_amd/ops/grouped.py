@@ -419,14 +419,17 @@ def _iconv_ok(x: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
             and -(-rows // 64) * (w.shape[0] // 64) >= 400)
 
 
-def _iconv(x: torch.Tensor, w: torch.Tensor, geom, out_hw, add: torch.Tensor | None = None) -> torch.Tensor:
-    """y = conv(x, w) (+ add, written in place of add when given) on the MFMA kernel."""
+def _iconv(x: torch.Tensor, w: torch.Tensor, geom, out_hw, add: torch.Tensor | None = None,
+           transpose_w: bool = False) -> torch.Tensor:
+    """y = conv(x, w) (+ add, written in place of add when given) on the MFMA kernel;
+    ``transpose_w``: w is a forward weight and its flipped transpose is applied (dgrad)."""
     n = x.shape[0]
+    cout = w.shape[1] if transpose_w else w.shape[0]
     if add is not None:
         y = add
     else:
-        y = torch.empty((n, w.shape[0], *out_hw), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-    _native.native().gpu_iconv(x, w, *geom, y, add)
+        y = torch.empty((n, cout, *out_hw), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    _native.native().gpu_iconv(x, w, *geom, y, add, 0, transpose_w)
     return y
 
 
@@ -581,8 +584,8 @@ class _GroupedConv(torch.autograd.Function):
             if need_dx:
                 if ((sh, sw, dh, dw) == (1, 1, 1, 1) and ph <= kh - 1 and pw <= kw - 1
                         and _iconv_ok(dy, _dgrad_weight_shape(w), dy2.shape[0])):
-                    dx = _iconv(dy, _dgrad_weight(w), (kh, kw, 1, 1, kh - 1 - ph, kw - 1 - pw, 1, 1), (h, wd),
-                                _cl(prev) if prev is not None else None)
+                    dx = _iconv(dy, w, (kh, kw, 1, 1, kh - 1 - ph, kw - 1 - pw, 1, 1), (h, wd),
+                                _cl(prev) if prev is not None else None, transpose_w=True)
                 else:
                     dcol = torch.mm(dy2, _wmat(w, kp))
                     if prev is not None:

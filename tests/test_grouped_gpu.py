@@ -185,6 +185,14 @@ def test_iconv_dgrad_matches_autograd(cuda, native):
     dx = torch.empty(4, 64, 8, 8, dtype=torch.bfloat16, device=cuda, memory_format=torch.channels_last)
     native.gpu_iconv(dyb, _dgrad_weight(wb), 3, 3, 1, 1, 1, 1, 1, 1, dx)
     assert rel(dx.float(), x.grad) < 1e-2
+    for pm in (11, 12, 14):   # the forward weight read transposed in-kernel, no weight copy
+        dx2 = torch.empty_like(dx)
+        native.gpu_iconv(dyb, wb, 3, 3, 1, 1, 1, 1, 1, 1, dx2, None, pm, True)
+        assert rel(dx2.float(), x.grad) < 1e-2
+        add = torch.randn_like(dx)
+        ref = add.float() + x.grad
+        native.gpu_iconv(dyb, wb, 3, 3, 1, 1, 1, 1, 1, 1, add, add, pm, True)
+        assert rel(add.float(), ref) < 1e-2
 
 
 @pytest.mark.parametrize("N,C,H,k,s,p", [(4, 64, 16, 3, 2, 1), (3, 8, 7, 2, 2, 0), (2, 16, 9, 3, 1, 1)])
