@@ -317,7 +317,7 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
                   double momentum, const c10::optional<at::Tensor>& run_mean,
                   const c10::optional<at::Tensor>& run_var, const at::Tensor& part, const at::Tensor& mean,
                   const at::Tensor& istd, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& y,
-                  bool relu, const c10::optional<at::Tensor>& mask) {
+                  bool relu, const c10::optional<at::Tensor>& mask, bool defer_running) {
   const auto dev = x.device();
   check_bf16_rows(x, dev, "x");
   check_bf16_rows(y, dev, "y");
@@ -350,7 +350,40 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::bn_forward(u16(x), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
                             static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, u16_mut(y), relu, mp,
-                            stream_of(dev));
+                            defer_running, stream_of(dev));
+}
+
+void g_bn_running_update(const std::vector<py::tuple>& jobs) {
+  garfield::gpu::RunJobs rj{};
+  c10::Device dev = c10::Device(c10::kCPU);
+  size_t i = 0;
+  auto flush = [&]() {
+    if (rj.n == 0) return;
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::bn_running_update(rj, stream_of(dev));
+    rj.n = 0;
+  };
+  for (; i < jobs.size(); ++i) {
+    const auto& t = jobs[i];
+    TORCH_CHECK(t.size() == 7, "gpu_bn_running_update: each job is (mean, istd, running_mean, running_var, rg, eps, "
+                "momentum)");
+    auto mean = t[0].cast<at::Tensor>(), istd = t[1].cast<at::Tensor>();
+    auto rm = t[2].cast<at::Tensor>(), rv = t[3].cast<at::Tensor>();
+    const int64_t rg = t[4].cast<int64_t>();
+    if (i == 0) dev = mean.device();
+    TORCH_CHECK(mean.device() == dev && mean.is_cuda(), "gpu_bn_running_update: all jobs on one device");
+    const int64_t C = rm.numel();
+    TORCH_CHECK(C > 0 && mean.numel() % C == 0 && istd.numel() == mean.numel() && rv.numel() == C, "gpu_bn_running_update: shapes");
+    float* pm = ws_vec(mean, mean.numel(), dev, "mean");
+    float* pi = ws_vec(istd, istd.numel(), dev, "istd");
+    float* prm = ws_vec(rm, C, dev, "running_mean");
+    float* prv = ws_vec(rv, C, dev, "running_var");
+    rj.j[rj.n++] = garfield::gpu::RunJob{pm, pi, prm, prv, rg, static_cast<int>(C),
+                                         static_cast<int>(mean.numel() / C), static_cast<float>(t[5].cast<double>()),
+                                         static_cast<float>(t[6].cast<double>())};
+    if (rj.n == garfield::gpu::kRunJobs) flush();
+  }
+  flush();
 }
 
 void g_bn_backward(const at::Tensor& x, const at::Tensor& dy, const c10::optional<at::Tensor>& y, int64_t groups,
@@ -731,7 +764,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("res"), py::arg("groups"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
         py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"), py::arg("part"), py::arg("mean"),
         py::arg("istd"), py::arg("scale"), py::arg("shift"), py::arg("y"), py::arg("relu"),
-        py::arg("mask") = py::none());
+        py::arg("mask") = py::none(), py::arg("defer_running") = false);
+  m.def("bn_small", [](int64_t rg) { return garfield::gpu::bn_small(rg); },
+        "True when rg rows per worker take the single-kernel BatchNorm path (whose running statistics "
+        "can be deferred to gpu_bn_running_update)");
+  m.def("gpu_bn_running_update", &g_bn_running_update,
+        "Replay the per-worker running-statistics updates of several layers in one launch; args (jobs) with "
+        "jobs = [(mean, istd, running_mean, running_var, rows_per_worker, eps, momentum), ...]");
   m.def("gpu_bn_backward", &g_bn_backward,
         "Per-worker BatchNorm backward; writes dγ/dβ of worker g to grow[g*row_stride + off_(gamma|beta) + c]; "
         "args (x, dy, y|mask|None, groups, gamma, mean, istd, part, coef, dx, dres|None, grow|None, row_stride, "

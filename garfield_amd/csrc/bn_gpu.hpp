@@ -16,10 +16,33 @@ int64_t bn_part_floats(int64_t rg, int groups, int C);
 
 // x, res, y: [groups * rg, C] bf16 (NHWC rows). gamma/beta/run_*: [C] fp32 (nullable).
 // mean, istd, scale, shift: [groups, C] fp32 outputs (saved for the backward).
+// Running-statistics replay of one or more layers (the k sequential updates of k workers).
+struct RunJob {
+  const float* mean;
+  const float* istd;
+  float* run_mean;
+  float* run_var;
+  int64_t rg;
+  int C;
+  int groups;
+  float eps;
+  float momentum;
+};
+constexpr int kRunJobs = 48;
+struct RunJobs {
+  RunJob j[kRunJobs];
+  int n;
+};
+void bn_running_update(const RunJobs& jobs, hipStream_t stream);
+// True when a layer of rg rows per worker takes the single-kernel small-layer path.
+bool bn_small(int64_t rg);
+
+// defer_running (small-layer path only): skip the running-statistics replay; the caller
+// batches it with bn_running_update.
 void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
                 float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
-                hipStream_t stream);
+                bool defer_running, hipStream_t stream);
 
 // mask (nullable, relu only): bit (r*C + c) of the byte array = y[r, c] > 0, for the backward.
 // ReLU source of the backward: mask when given, else y (nullable) > 0. dres (nullable) receives dz.

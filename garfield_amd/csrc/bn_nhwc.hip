@@ -423,6 +423,225 @@ dim3 apply_grid(int64_t R, int rp) {
   return dim3(static_cast<unsigned>((R + rows_per_wg - 1) / rows_per_wg));
 }
 
+// ---------------------------------------------------------------------------
+// Small layers (<= kSmallRows rows per worker: CIFAR layer3/layer4, 250-1000 rows):
+// the three-launch pipeline above is launch-bound there (~5 µs per dependent kernel
+// for a few MB of data), so ONE workgroup per (worker, 64 channels) does the whole
+// layer: the statistics pass, the finalize (LDS), and the apply pass over the same
+// (L2-resident) rows. No inter-workgroup hand-off; the running statistics are
+// replayed by k_running (one tiny launch, or batched for many layers by the caller).
+constexpr int kSmallRows = 1024;
+constexpr int kSmallThreads = 1024;             // 16 waves per workgroup to hide the load latency
+constexpr int kSmallCh = 32;                    // channels per workgroup (4 vectors of 8)
+constexpr int kSmallVec = kSmallCh / 8;
+constexpr int kSmallLanes = kSmallThreads / kSmallVec;   // 256 row lanes
+constexpr int kSmallSplit = kSmallThreads / kSmallCh;    // first-stage reduction splits per channel
+
+// Sums red[k][lane][c] over the kSmallLanes lanes for both k; result in red[k][0][c].
+__device__ __forceinline__ void small_reduce(float (&red)[2][kSmallLanes][kSmallCh]) {
+  const int c = threadIdx.x % kSmallCh, part = threadIdx.x / kSmallCh;
+  constexpr int per = kSmallLanes / kSmallSplit;
+  float a = 0.f, b = 0.f;
+#pragma unroll 8
+  for (int t = 0; t < per; ++t) { a += red[0][part * per + t][c]; b += red[1][part * per + t][c]; }
+  __syncthreads();
+  red[0][part][c] = a;
+  red[1][part][c] = b;
+  __syncthreads();
+  if (threadIdx.x < kSmallCh) {
+    a = 0.f; b = 0.f;
+#pragma unroll
+    for (int t = 0; t < kSmallSplit; ++t) { a += red[0][t][c]; b += red[1][t][c]; }
+    red[0][0][c] = a;
+    red[1][0][c] = b;
+  }
+  __syncthreads();
+}
+
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* __restrict__ x,
+                                                          const uint16_t* __restrict__ res, int64_t rg, int C,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          float* __restrict__ mean, float* __restrict__ istd,
+                                                          float* __restrict__ scale, float* __restrict__ shift,
+                                                          uint16_t* __restrict__ y, uint8_t* __restrict__ mask) {
+  __shared__ float red[2][kSmallLanes][kSmallCh];
+  __shared__ float lsc[kSmallCh], lsh[kSmallCh];
+  const int tc = threadIdx.x % kSmallVec, tr = threadIdx.x / kSmallVec;
+  const int g = blockIdx.y;
+  const int c0 = blockIdx.x * kSmallCh + tc * 8;
+  const bool act = c0 < C;
+  const int64_t base = static_cast<int64_t>(g) * rg;
+  float s[8], q[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; sh[i] = 0.f; }
+  if (act) {
+    load8(x, base * C + c0, sh);   // shifted sums (see k_partial)
+    for (int64_t r = tr; r < rg; r += kSmallLanes) {
+      float a[8];
+      load8(x, (base + r) * C + c0, a);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { const float e = a[i] - sh[i]; s[i] += e; q[i] += e * e; }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[0][tr][tc * 8 + i] = s[i]; red[1][tr][tc * 8 + i] = q[i]; }
+  __syncthreads();
+  small_reduce(red);
+  if (threadIdx.x < kSmallCh) {
+    const int c = blockIdx.x * kSmallCh + threadIdx.x;
+    const float S = red[0][0][threadIdx.x], Q = red[1][0][threadIdx.x];
+    float sc = 0.f, sf = 0.f;
+    if (c < C) {
+      const float M = static_cast<float>(rg);
+      const float m1 = S / M;
+      float var = Q / M - m1 * m1;
+      var = var > 0.f ? var : 0.f;
+      const float mu = bf16_to_f(x[base * C + c]) + m1;
+      const float is = rsqrtf(var + eps);
+      const int64_t gc = static_cast<int64_t>(g) * C + c;
+      mean[gc] = mu;
+      istd[gc] = is;
+      sc = (gamma ? gamma[c] : 1.f) * is;
+      sf = (beta ? beta[c] : 0.f) - mu * sc;
+      scale[gc] = sc;
+      shift[gc] = sf;
+    }
+    lsc[threadIdx.x] = sc;
+    lsh[threadIdx.x] = sf;
+  }
+  __syncthreads();
+  if (!act) return;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sc[i] = lsc[tc * 8 + i]; sf[i] = lsh[tc * 8 + i]; }
+  for (int64_t r = tr; r < rg; r += kSmallLanes) {
+    const int64_t off = (base + r) * C + c0;
+    float a[8], o[8];
+    load8(x, off, a);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = a[i] * sc[i] + sf[i];
+    if constexpr (RES) {
+      float rr[8];
+      load8(res, off, rr);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] += rr[i];
+    }
+    if constexpr (RELU) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = o[i] > 0.f ? o[i] : 0.f;
+      if (mask) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) bits |= (f_to_bf16(o[i]) != 0 ? 1u : 0u) << i;
+        mask[off >> 3] = static_cast<uint8_t>(bits);
+      }
+    }
+    store_vec<8>(y, kBF16, off, o);
+  }
+}
+
+template <int RM, bool RES_OUT>
+__global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+    const uint8_t* __restrict__ mask, int64_t rg, int C, const float* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ istd, uint16_t* __restrict__ dx,
+    uint16_t* __restrict__ dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta) {
+  __shared__ float red[2][kSmallLanes][kSmallCh];
+  __shared__ float la[kSmallCh], lb[kSmallCh], lc[kSmallCh];
+  const int tc = threadIdx.x % kSmallVec, tr = threadIdx.x / kSmallVec;
+  const int g = blockIdx.y;
+  const int c0 = blockIdx.x * kSmallCh + tc * 8;
+  const bool act = c0 < C;
+  const int64_t base = static_cast<int64_t>(g) * rg;
+  auto dz_of = [&](int64_t off, float (&d)[8]) {
+    load8(dy, off, d);
+    if constexpr (RM == 1) {
+      float yy[8];
+      load8(y, off, yy);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = yy[i] > 0.f ? d[i] : 0.f;
+    } else if constexpr (RM == 2) {
+      const uint32_t mb = mask[off >> 3];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = (mb >> i) & 1u ? d[i] : 0.f;
+    }
+  };
+  float A[8], B[8], mu[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { A[i] = 0.f; B[i] = 0.f; mu[i] = 0.f; }
+  if (act) {
+    load8f(mean + static_cast<int64_t>(g) * C + c0, mu);
+    for (int64_t r = tr; r < rg; r += kSmallLanes) {
+      const int64_t off = (base + r) * C + c0;
+      float a[8], d[8];
+      load8(x, off, a);
+      dz_of(off, d);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { A[i] += d[i]; B[i] += d[i] * (a[i] - mu[i]); }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[0][tr][tc * 8 + i] = A[i]; red[1][tr][tc * 8 + i] = B[i]; }
+  __syncthreads();
+  small_reduce(red);
+  if (threadIdx.x < kSmallCh) {
+    const int c = blockIdx.x * kSmallCh + threadIdx.x;
+    const float SA = red[0][0][threadIdx.x], SB = red[1][0][threadIdx.x];
+    float ca = 0.f, cb = 0.f, cc = 0.f;
+    if (c < C) {
+      const float M = static_cast<float>(rg);
+      const float is = istd[static_cast<int64_t>(g) * C + c];
+      const float dgamma = SB * is, dbeta = SA;
+      if (grow) {
+        if (off_gamma >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_gamma + c, dgamma);
+        if (off_beta >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_beta + c, dbeta);
+      }
+      ca = (gamma ? gamma[c] : 1.f) * is;
+      cb = dbeta / M;
+      cc = dgamma / M * is;
+    }
+    la[threadIdx.x] = ca;
+    lb[threadIdx.x] = cb;
+    lc[threadIdx.x] = cc;
+  }
+  __syncthreads();
+  if (!act) return;
+  float ca[8], cb[8], cc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { ca[i] = la[tc * 8 + i]; cb[i] = lb[tc * 8 + i]; cc[i] = lc[tc * 8 + i]; }
+  for (int64_t r = tr; r < rg; r += kSmallLanes) {
+    const int64_t off = (base + r) * C + c0;
+    float a[8], d[8], o[8];
+    load8(x, off, a);
+    dz_of(off, d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = ca[i] * (d[i] - cb[i] - (a[i] - mu[i]) * cc[i]);
+    store_vec<8>(dx, kBF16, off, o);
+    if constexpr (RES_OUT) store_vec<8>(dres, kBF16, off, d);
+  }
+}
+
+// Running statistics of up to kRunJobs layers in one launch (blockIdx.y = layer).
+__global__ __launch_bounds__(kThreads) void k_running(RunJobs jobs) {
+  const RunJob& j = jobs.j[blockIdx.y];
+  const float M = static_cast<float>(j.rg);
+  for (int c = blockIdx.x * kThreads + threadIdx.x; c < j.C; c += gridDim.x * kThreads) {
+    float rm = j.run_mean[c], rv = j.run_var[c];
+    for (int g = 0; g < j.groups; ++g) {
+      const float is = j.istd[static_cast<int64_t>(g) * j.C + c];
+      float var = 1.f / (is * is) - j.eps;
+      var = var > 0.f ? var : 0.f;
+      const float unb = j.rg > 1 ? var * M / (M - 1.f) : var;
+      rm = (1.f - j.momentum) * rm + j.momentum * j.mean[static_cast<int64_t>(g) * j.C + c];
+      rv = (1.f - j.momentum) * rv + j.momentum * unb;
+    }
+    j.run_mean[c] = rm;
+    j.run_var[c] = rv;
+  }
+}
+
 }  // namespace
 
 int64_t bn_part_floats(int64_t rg, int groups, int C) {
@@ -433,7 +652,24 @@ int64_t bn_part_floats(int64_t rg, int groups, int C) {
 void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
                 float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
-                hipStream_t stream) {
+                bool defer_running, hipStream_t stream) {
+  if (rg <= kSmallRows) {
+    const dim3 sgrid((C + kSmallCh - 1) / kSmallCh, groups);
+    if (res) {
+      if (relu) hipLaunchKernelGGL((k_bn_fwd_small<true, true>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
+      else hipLaunchKernelGGL((k_bn_fwd_small<true, false>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+    } else {
+      if (relu) hipLaunchKernelGGL((k_bn_fwd_small<false, true>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
+      else hipLaunchKernelGGL((k_bn_fwd_small<false, false>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+    }
+    if (run_mean && !defer_running) {
+      RunJobs jobs{};
+      jobs.j[0] = RunJob{mean, istd, run_mean, run_var, rg, C, groups, eps, momentum};
+      jobs.n = 1;
+      bn_running_update(jobs, stream);
+    }
+    return;
+  }
   const Geo g = geometry(rg, groups, C);
   const int ncb = (C + g.cb - 1) / g.cb;
   hipLaunchKernelGGL((k_partial<false, 0>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
@@ -459,9 +695,20 @@ void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const
                  int C, const float* gamma, const float* mean, const float* istd, float* part, float* coef, uint16_t* dx,
                  uint16_t* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
                  hipStream_t stream) {
+  const int rm = mask ? 2 : (y ? 1 : 0);
+  if (rg <= kSmallRows) {
+    const dim3 sgrid((C + kSmallCh - 1) / kSmallCh, groups);
+#define GARFIELD_BWD_SMALL(RMV, RESV)                                                                           \
+  hipLaunchKernelGGL((k_bn_bwd_small<RMV, RESV>), sgrid, dim3(kSmallThreads), 0, stream, x, dy, y, mask, rg, C, gamma, \
+                     mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta)
+    if (rm == 2) { if (dres) GARFIELD_BWD_SMALL(2, true); else GARFIELD_BWD_SMALL(2, false); }
+    else if (rm == 1) { if (dres) GARFIELD_BWD_SMALL(1, true); else GARFIELD_BWD_SMALL(1, false); }
+    else { if (dres) GARFIELD_BWD_SMALL(0, true); else GARFIELD_BWD_SMALL(0, false); }
+#undef GARFIELD_BWD_SMALL
+    return;
+  }
   const Geo g = geometry(rg, groups, C);
   const int ncb = (C + g.cb - 1) / g.cb;
-  const int rm = mask ? 2 : (y ? 1 : 0);
   const dim3 pgrid(g.chunks, ncb, groups);
   if (rm == 2) hipLaunchKernelGGL((k_partial<true, 2>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
   else if (rm == 1) hipLaunchKernelGGL((k_partial<true, 1>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
@@ -479,6 +726,16 @@ void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const
   else { if (dres) GARFIELD_BWD_APPLY(0, true); else GARFIELD_BWD_APPLY(0, false); }
 #undef GARFIELD_BWD_APPLY
 }
+
+void bn_running_update(const RunJobs& jobs, hipStream_t stream) {
+  if (jobs.n <= 0) return;
+  int cmax = 0;
+  for (int i = 0; i < jobs.n; ++i) cmax = jobs.j[i].C > cmax ? jobs.j[i].C : cmax;
+  const dim3 grid((cmax + kThreads - 1) / kThreads, jobs.n);
+  hipLaunchKernelGGL(k_running, grid, dim3(kThreads), 0, stream, jobs);
+}
+
+bool bn_small(int64_t rg) { return rg <= kSmallRows; }
 
 }  // namespace gpu
 }  // namespace garfield

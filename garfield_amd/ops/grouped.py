@@ -209,10 +209,19 @@ class BNState:
 
 
 class Workspace:
-    """Shared scratch (BatchNorm partial sums / backward coefficients)."""
+    """Shared scratch (BatchNorm partial sums / backward coefficients), and the
+    running-statistics updates deferred by single-kernel (small) BatchNorm layers
+    when ``defer_running`` is set: ``flush_running`` replays them in one launch."""
 
     def __init__(self):
         self.t = {}
+        self.defer_running = False
+        self.running_jobs: list = []
+
+    def flush_running(self) -> None:
+        if self.running_jobs:
+            _native.native().gpu_bn_running_update(self.running_jobs)
+            self.running_jobs = []
 
     def get(self, name: str, numel: int, device) -> torch.Tensor:
         t = self.t.get(name)
@@ -309,9 +318,13 @@ class _GroupedBN(torch.autograd.Function):
             track = bn.track_running_stats and bn.running_mean is not None
             # the backward's ReLU test reads one bit per element instead of y
             relu_state = torch.empty((x2.numel() // 8,), dtype=torch.uint8, device=x.device) if st.relu else None
+            defer = bool(track and ws.defer_running and C_.bn_small(rg))
             C_.gpu_bn_forward(x2, r2, st.groups, bn.weight, bn.bias, float(bn.eps), float(bn.momentum),
                               bn.running_mean if track else None, bn.running_var if track else None,
-                              part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu, relu_state)
+                              part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu, relu_state, defer)
+            if defer:
+                ws.running_jobs.append((st.mean, st.istd, bn.running_mean, bn.running_var, rg, float(bn.eps),
+                                        float(bn.momentum)))
         else:
             y = from_rows(_bn_fwd_ref(x2, r2, st), n, h, w)
             relu_state = y if st.relu else None

@@ -90,12 +90,16 @@ class GroupedResNet:
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         m = self.model
+        # small layers' running statistics: one batched launch after the last BatchNorm
+        self.ws.defer_running = x.is_cuda
+        self.ws.running_jobs = []
         x = self._bn(self._conv(x, m.conv1), m.bn1, True)
         if isinstance(m.maxpool, nn.MaxPool2d):
             x = grouped_maxpool(x, m.maxpool)
         for layer in (m.layer1, m.layer2, m.layer3, m.layer4):
             for blk in layer:
                 x = self._block(blk, x)
+        self.ws.flush_running()
         n, c, h, w = x.shape
         pooled = x.reshape(n, c) if h * w == 1 else x.mean((2, 3))
         return grouped_linear(pooled, self.fc)

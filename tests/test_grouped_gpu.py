@@ -32,7 +32,8 @@ def _bn_ref_group(xg, gamma, beta, eps, rg, relu):
 @pytest.mark.parametrize("G,B,H,C,relu,res", [(8, 16, 4, 64, True, False), (3, 5, 3, 96, False, False),
                                               (4, 8, 2, 256, True, True), (2, 9, 1, 2048, True, True),
                                               (8, 2, 8, 520, True, False), (1, 64, 8, 128, False, True)])
-def test_bn_kernels_match_fp32_reference(cuda, G, B, H, C, relu, res):
+@pytest.mark.parametrize("defer", [False, True])
+def test_bn_kernels_match_fp32_reference(cuda, G, B, H, C, relu, res, defer):
     torch.manual_seed(C + G)
     N = G * B
     x = (torch.randn(N, C, H, H, device=cuda) * 2 + 0.5).to(torch.bfloat16)
@@ -51,7 +52,10 @@ def test_bn_kernels_match_fp32_reference(cuda, G, B, H, C, relu, res):
     st = BNState(bn, relu, sink, G)
     xin = x.clone().requires_grad_(True)
     rin = r.clone().requires_grad_(True) if res else None
-    y = grouped_bn(xin, st, Workspace(), rin)
+    ws = Workspace()
+    ws.defer_running = defer   # small layers queue their running-statistics update
+    y = grouped_bn(xin, st, ws, rin)
+    ws.flush_running()
     dy = torch.randn_like(x).contiguous(memory_format=torch.channels_last)
     y.backward(dy)
 
