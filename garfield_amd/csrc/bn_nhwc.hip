@@ -436,6 +436,7 @@ constexpr int kSmallCh = 32;                    // channels per workgroup (4 vec
 constexpr int kSmallVec = kSmallCh / 8;
 constexpr int kSmallLanes = kSmallThreads / kSmallVec;   // 256 row lanes
 constexpr int kSmallSplit = kSmallThreads / kSmallCh;    // first-stage reduction splits per channel
+static_assert(kSmallRows % kSmallLanes == 0, "small-layer rows must tile the row lanes");
 
 // Sums red[k][lane][c] over the kSmallLanes lanes for both k; result in red[k][0][c].
 __device__ __forceinline__ void small_reduce(float (&red)[2][kSmallLanes][kSmallCh]) {
@@ -458,6 +459,21 @@ __device__ __forceinline__ void small_reduce(float (&red)[2][kSmallLanes][kSmall
   __syncthreads();
 }
 
+constexpr int kSmallIt = kSmallRows / kSmallLanes;   // rows per thread, held in registers
+
+__device__ __forceinline__ uint4 ld_raw8(const uint16_t* p, int64_t off) {
+  return *reinterpret_cast<const uint4*>(p + off);
+}
+
+__device__ __forceinline__ void unpack8(const uint4 u, float (&v)[8]) {
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+
+// Each thread keeps its (<= kSmallIt) rows of 8 channels in registers as packed bf16,
+// so the apply pass does not re-read x (or dy) from memory.
 template <bool RES, bool RELU>
 __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* __restrict__ x,
                                                           const uint16_t* __restrict__ res, int64_t rg, int C,
@@ -474,15 +490,24 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* 
   const bool act = c0 < C;
   const int64_t base = static_cast<int64_t>(g) * rg;
   float s[8], q[8], sh[8];
+  uint4 xr[kSmallIt];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; sh[i] = 0.f; }
   if (act) {
     load8(x, base * C + c0, sh);   // shifted sums (see k_partial)
-    for (int64_t r = tr; r < rg; r += kSmallLanes) {
-      float a[8];
-      load8(x, (base + r) * C + c0, a);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { const float e = a[i] - sh[i]; s[i] += e; q[i] += e * e; }
+    for (int it = 0; it < kSmallIt; ++it) {
+      const int64_t r = tr + it * kSmallLanes;
+      if (r < rg) xr[it] = ld_raw8(x, (base + r) * C + c0);
+    }
+#pragma unroll
+    for (int it = 0; it < kSmallIt; ++it) {
+      if (tr + it * kSmallLanes < rg) {
+        float a[8];
+        unpack8(xr[it], a);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { const float e = a[i] - sh[i]; s[i] += e; q[i] += e * e; }
+      }
     }
   }
 #pragma unroll
@@ -516,10 +541,13 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* 
   float sc[8], sf[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { sc[i] = lsc[tc * 8 + i]; sf[i] = lsh[tc * 8 + i]; }
-  for (int64_t r = tr; r < rg; r += kSmallLanes) {
+#pragma unroll
+  for (int it = 0; it < kSmallIt; ++it) {
+    const int64_t r = tr + it * kSmallLanes;
+    if (r >= rg) break;
     const int64_t off = (base + r) * C + c0;
     float a[8], o[8];
-    load8(x, off, a);
+    unpack8(xr[it], a);
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = a[i] * sc[i] + sf[i];
     if constexpr (RES) {
@@ -555,31 +583,48 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
   const int c0 = blockIdx.x * kSmallCh + tc * 8;
   const bool act = c0 < C;
   const int64_t base = static_cast<int64_t>(g) * rg;
-  auto dz_of = [&](int64_t off, float (&d)[8]) {
-    load8(dy, off, d);
-    if constexpr (RM == 1) {
-      float yy[8];
-      load8(y, off, yy);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) d[i] = yy[i] > 0.f ? d[i] : 0.f;
-    } else if constexpr (RM == 2) {
-      const uint32_t mb = mask[off >> 3];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) d[i] = (mb >> i) & 1u ? d[i] : 0.f;
-    }
-  };
+  // dz = dy masked by the forward ReLU, kept packed (bf16) in registers with x
+  uint4 xr[kSmallIt], dr[kSmallIt];
   float A[8], B[8], mu[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { A[i] = 0.f; B[i] = 0.f; mu[i] = 0.f; }
   if (act) {
     load8f(mean + static_cast<int64_t>(g) * C + c0, mu);
-    for (int64_t r = tr; r < rg; r += kSmallLanes) {
-      const int64_t off = (base + r) * C + c0;
-      float a[8], d[8];
-      load8(x, off, a);
-      dz_of(off, d);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { A[i] += d[i]; B[i] += d[i] * (a[i] - mu[i]); }
+    for (int it = 0; it < kSmallIt; ++it) {
+      const int64_t r = tr + it * kSmallLanes;
+      if (r < rg) {
+        const int64_t off = (base + r) * C + c0;
+        xr[it] = ld_raw8(x, off);
+        uint4 d = ld_raw8(dy, off);
+        if constexpr (RM == 1) {
+          const uint4 yy = ld_raw8(y, off);
+          // bf16 > 0: sign bit clear and non-zero
+          auto keep = [](uint32_t dv, uint32_t yv) {
+            const uint32_t lo = ((yv & 0x8000u) == 0 && (yv & 0x7fffu) != 0) ? 0x0000ffffu : 0u;
+            const uint32_t hi = ((yv & 0x80000000u) == 0 && (yv & 0x7fff0000u) != 0) ? 0xffff0000u : 0u;
+            return dv & (lo | hi);
+          };
+          d.x = keep(d.x, yy.x); d.y = keep(d.y, yy.y); d.z = keep(d.z, yy.z); d.w = keep(d.w, yy.w);
+        } else if constexpr (RM == 2) {
+          const uint32_t mb = mask[off >> 3];
+          auto keep = [](uint32_t dv, uint32_t m2) {
+            return dv & (((m2 & 1u) ? 0x0000ffffu : 0u) | ((m2 & 2u) ? 0xffff0000u : 0u));
+          };
+          d.x = keep(d.x, mb); d.y = keep(d.y, mb >> 2); d.z = keep(d.z, mb >> 4); d.w = keep(d.w, mb >> 6);
+        }
+        dr[it] = d;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < kSmallIt; ++it) {
+      if (tr + it * kSmallLanes < rg) {
+        float a[8], d[8];
+        unpack8(xr[it], a);
+        unpack8(dr[it], d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { A[i] += d[i]; B[i] += d[i] * (a[i] - mu[i]); }
+      }
     }
   }
 #pragma unroll
@@ -611,15 +656,18 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
   float ca[8], cb[8], cc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { ca[i] = la[tc * 8 + i]; cb[i] = lb[tc * 8 + i]; cc[i] = lc[tc * 8 + i]; }
-  for (int64_t r = tr; r < rg; r += kSmallLanes) {
+#pragma unroll
+  for (int it = 0; it < kSmallIt; ++it) {
+    const int64_t r = tr + it * kSmallLanes;
+    if (r >= rg) break;
     const int64_t off = (base + r) * C + c0;
     float a[8], d[8], o[8];
-    load8(x, off, a);
-    dz_of(off, d);
+    unpack8(xr[it], a);
+    unpack8(dr[it], d);
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = ca[i] * (d[i] - cb[i] - (a[i] - mu[i]) * cc[i]);
     store_vec<8>(dx, kBF16, off, o);
-    if constexpr (RES_OUT) store_vec<8>(dres, kBF16, off, d);
+    if constexpr (RES_OUT) *reinterpret_cast<uint4*>(dres + off) = dr[it];
   }
 }
 
