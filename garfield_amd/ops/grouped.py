@@ -36,6 +36,7 @@ test suite); on the GPU the native extension is mandatory.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 
@@ -59,6 +60,9 @@ ICONV = os.environ.get("GARFIELD_ICONV", "1") != "0"
 IWGRAD = os.environ.get("GARFIELD_IWGRAD", "1") != "0"
 # ... and for the 1x1 stride-1 convolutions too (else a split-K batched hipBLASLt GEMM).
 IWGRAD_1X1 = os.environ.get("GARFIELD_IWGRAD_1X1", "0") != "0"   # measured a wash: 7.715 vs 7.739 ms/step
+# weight gradients on a side stream (see WgradStream): measured slower in the graphed step
+# (7.23 vs 7.07 ms: per-layer fork/join dependencies leave 8% of the window idle), so off
+WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0") != "0"
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -524,6 +528,48 @@ def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int, out: torch.Tensor | None
     return part.view(G, S, cout, K).float().sum(1)
 
 
+class WgradStream:
+    """Side stream for the per-worker weight gradients of the backward.
+
+    A layer's weight gradient and its data gradient are independent; the data
+    gradient feeds the next BatchNorm backward, a chain of short, latency-bound
+    kernels (few workgroups, one launch gap each) that leaves most CUs idle. The
+    weight-gradient GEMMs run on this stream, forked from the current stream at
+    each layer and joined once (``join``) before the exchange rows are read, so
+    they fill those gaps. Under HIP-graph capture the fork/join become parallel
+    graph branches. Operands are ``record_stream``-ed so the caching allocator
+    does not recycle them while the side stream still reads them."""
+
+    _streams: dict = {}
+    active: dict = {}
+
+    @classmethod
+    def fork(cls, *tensors: torch.Tensor):
+        dev = tensors[0].device
+        s = cls._streams.get(dev)
+        if s is None:
+            s = cls._streams[dev] = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        for t in tensors:
+            if t is not None:
+                t.record_stream(s)
+        cls.active[dev] = s
+        return torch.cuda.stream(s)
+
+    @classmethod
+    def join(cls, dev) -> None:
+        s = cls.active.pop(dev, None)
+        if s is not None:
+            torch.cuda.current_stream(dev).wait_stream(s)
+
+
+def _wgrad_ctx(*tensors):
+    """Side-stream context for a weight-gradient computation (a no-op on CPU or when disabled)."""
+    if WGRAD_STREAM and tensors[0].is_cuda:
+        return WgradStream.fork(*tensors)
+    return contextlib.nullcontext()
+
+
 class _GroupedConv(torch.autograd.Function):
     """Convolution over the grouped batch with per-worker weight gradients.
 
@@ -581,13 +627,14 @@ class _GroupedConv(torch.autograd.Function):
                     dx = from_rows(torch.mm(dy2, w2), n, h, wd)
             if spec.sink is not None:
                 K = w.numel() // cout
-                if IWGRAD_1X1 and _iwgrad_ok(a, dy):
-                    _iwgrad(a, dy, spec, G, K)
-                else:
-                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype)
-                    dW = _wgrad(dy2, rows2d(a), G, out)
-                    if out is None:
-                        spec.sink.put_groups(spec.conv.weight, dW)
+                with _wgrad_ctx(a, dy):
+                    if IWGRAD_1X1 and _iwgrad_ok(a, dy):
+                        _iwgrad(a, dy, spec, G, K)
+                    else:
+                        out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype)
+                        dW = _wgrad(dy2, rows2d(a), G, out)
+                        if out is None:
+                            spec.sink.put_groups(spec.conv.weight, dW)
         elif mode == "iconv":                    # a = x
             (kh, kw), (sh, sw), (ph, pw), (dh, dw) = spec.kernel, spec.stride, spec.padding, spec.dilation
             K = w.numel() // cout
@@ -610,14 +657,16 @@ class _GroupedConv(torch.autograd.Function):
                         _native.native().gpu_col2im(dcol, *_geom(spec), dx)
                 prev = None
             if use_iw:
-                _iwgrad(a, dy, spec, G, K)
+                with _wgrad_ctx(a, dy):
+                    _iwgrad(a, dy, spec, G, K)
             elif spec.sink is not None:
-                out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if kp == K else None
-                dW = _wgrad(dy2, col, G, out)
-                if out is None:
-                    if kp != K:
-                        dW = dW[:, :, :K].contiguous()
-                    spec.sink.put_groups(spec.conv.weight, dW)
+                with _wgrad_ctx(col, dy):
+                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if kp == K else None
+                    dW = _wgrad(dy2, col, G, out)
+                    if out is None:
+                        if kp != K:
+                            dW = dW[:, :, :K].contiguous()
+                        spec.sink.put_groups(spec.conv.weight, dW)
         elif mode == "col":                      # a = col [N*Ho*Wo, Kp]
             kp = a.shape[1]
             if need_dx:
@@ -633,12 +682,13 @@ class _GroupedConv(torch.autograd.Function):
                 # dW_g[co, (i, j, ci)] = Σ_rows dy_g[row, co] · col_g[row, (i, j, ci)]: the
                 # weight's channels_last memory order, one batched GEMM for all workers
                 K = w.numel() // cout
-                out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if kp == K else None
-                dW = _wgrad(dy2, a, G, out)
-                if out is None:
-                    if kp != K:
-                        dW = dW[:, :, :K].contiguous()
-                    spec.sink.put_groups(spec.conv.weight, dW)
+                with _wgrad_ctx(a, dy):
+                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if kp == K else None
+                    dW = _wgrad(dy2, a, G, out)
+                    if out is None:
+                        if kp != K:
+                            dW = dW[:, :, :K].contiguous()
+                        spec.sink.put_groups(spec.conv.weight, dW)
         else:                                    # a = x
             if need_dx:
                 dx = _cl(_conv_bwd(dy, a, w, spec, [True, False, False])[0])

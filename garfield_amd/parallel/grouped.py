@@ -21,7 +21,7 @@ import torch.nn.functional as F
 
 from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
 from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, grouped_bn,
-                                      grouped_conv, grouped_linear, grouped_maxpool)
+                                      WgradStream, grouped_conv, grouped_linear, grouped_maxpool)
 
 
 def supports(model: nn.Module) -> bool:
@@ -119,6 +119,8 @@ class GroupedResNet:
             raise ValueError(f"batch of {x.shape[0]} rows is not divisible into {self.groups} workers")
         per = self.losses(self.forward(x), y)
         per.sum().backward()
+        if x.is_cuda:
+            WgradStream.join(x.device)   # weight gradients computed on the side stream
         self.sink.flush()
         per = per.detach()
         if loss_out is not None:
