@@ -516,7 +516,9 @@ def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int, out: torch.Tensor | None
     cout, K = dy2.shape[1], a2.shape[1]
     M = dy2.shape[0] // G
     S = 1
-    while S < 16 and M % (2 * S) == 0 and M // (2 * S) >= 4000:
+    # layer2-size reductions (4000 rows) still gain from S=4: 21.6 vs 28.3 µs for 128>512
+    # (scripts/bench_wgrad_1x1.py, profiles/bench_wgrad_1x1_r1.log); 1000 rows lose
+    while S < 16 and M % (2 * S) == 0 and (M // (2 * S) >= 4000 or (S < 4 and M // (2 * S) >= 1000)):
         S *= 2
     if S == 1:
         if out is not None:
