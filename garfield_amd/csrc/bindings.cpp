@@ -17,6 +17,7 @@
 #include "gar_common.hpp"
 #include "gar_cpu.hpp"
 #include "gar_gpu.hpp"
+#include "loss_gpu.hpp"
 #include "mailbox.hpp"
 #include "threadpool.hpp"
 
@@ -351,6 +352,45 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
   garfield::gpu::bn_forward(u16(x), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
                             static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, u16_mut(y), relu, mp,
                             defer_running, stream_of(dev));
+}
+
+int xent_dtype(const at::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 2, "gpu_xent: ", what, " must be a contiguous 2-D GPU tensor");
+  if (t.scalar_type() == at::kFloat) return garfield::kF32;
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "gpu_xent: ", what, " must be fp32 or bf16");
+  return garfield::kBF16;
+}
+
+void g_xent_forward(const at::Tensor& logits, const at::Tensor& labels, int64_t groups, const at::Tensor& loss,
+                    const at::Tensor& dlogits) {
+  const int dt = xent_dtype(logits, "logits");
+  TORCH_CHECK(xent_dtype(dlogits, "dlogits") == dt && dlogits.sizes() == logits.sizes(), "gpu_xent: dlogits shape/dtype");
+  const int64_t N = logits.size(0), nc = logits.size(1);
+  TORCH_CHECK(groups > 0 && N % groups == 0, "gpu_xent: rows not divisible into groups");
+  TORCH_CHECK(nc >= 1 && nc <= garfield::gpu::kXentMaxClasses, "gpu_xent: 1..", garfield::gpu::kXentMaxClasses, " classes");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == N,
+              "gpu_xent: labels must be a contiguous int64 GPU tensor of N entries");
+  TORCH_CHECK(loss.is_cuda() && loss.scalar_type() == at::kFloat && loss.is_contiguous() && loss.numel() == groups,
+              "gpu_xent: loss must be a contiguous fp32 GPU tensor of `groups` entries");
+  const auto dev = logits.device();
+  TORCH_CHECK(labels.device() == dev && loss.device() == dev && dlogits.device() == dev, "gpu_xent: one device");
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::xent_forward(logits.data_ptr(), dt, labels.data_ptr<int64_t>(), N / groups, static_cast<int>(groups),
+                              static_cast<int>(nc), loss.data_ptr<float>(), dlogits.data_ptr(), stream_of(dev));
+}
+
+void g_xent_backward(const at::Tensor& dlogits, const at::Tensor& grad_loss, int64_t groups, const at::Tensor& dx) {
+  const int dt = xent_dtype(dlogits, "dlogits");
+  TORCH_CHECK(xent_dtype(dx, "dx") == dt && dx.sizes() == dlogits.sizes(), "gpu_xent: dx shape/dtype");
+  const int64_t N = dlogits.size(0), nc = dlogits.size(1);
+  TORCH_CHECK(groups > 0 && N % groups == 0, "gpu_xent: rows not divisible into groups");
+  TORCH_CHECK(grad_loss.is_cuda() && grad_loss.scalar_type() == at::kFloat && grad_loss.is_contiguous() &&
+                  grad_loss.numel() == groups, "gpu_xent: grad_loss must be a contiguous fp32 GPU tensor of `groups`");
+  const auto dev = dlogits.device();
+  TORCH_CHECK(grad_loss.device() == dev && dx.device() == dev, "gpu_xent: one device");
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::xent_backward(dlogits.data_ptr(), dt, grad_loss.data_ptr<float>(), N / groups,
+                               static_cast<int>(groups), static_cast<int>(nc), dx.data_ptr(), stream_of(dev));
 }
 
 void g_bn_running_update(const std::vector<py::tuple>& jobs) {
@@ -771,6 +811,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_bn_running_update", &g_bn_running_update,
         "Replay the per-worker running-statistics updates of several layers in one launch; args (jobs) with "
         "jobs = [(mean, istd, running_mean, running_var, rows_per_worker, eps, momentum), ...]");
+  m.def("gpu_xent_forward", &g_xent_forward,
+        "Per-worker mean cross-entropy of [groups*rows, nc] logits (nc <= 64) and d(loss_g)/d(logits); args "
+        "(logits, labels, groups, loss[groups] fp32, dlogits like logits)");
+  m.def("gpu_xent_backward", &g_xent_backward,
+        "dx = dlogits scaled row-wise by the upstream per-worker loss gradient; args (dlogits, grad_loss, groups, dx)");
   m.def("gpu_bn_backward", &g_bn_backward,
         "Per-worker BatchNorm backward; writes dγ/dβ of worker g to grow[g*row_stride + off_(gamma|beta) + c]; "
         "args (x, dy, y|mask|None, groups, gamma, mean, istd, part, coef, dx, dres|None, grow|None, row_stride, "

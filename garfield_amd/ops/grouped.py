@@ -63,6 +63,7 @@ IWGRAD_1X1 = os.environ.get("GARFIELD_IWGRAD_1X1", "0") != "0"   # measured a wa
 # weight gradients on a side stream (see WgradStream): measured slower in the graphed step
 # (7.23 vs 7.07 ms: per-layer fork/join dependencies leave 8% of the window idle), so off
 WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0") != "0"
+XENT = os.environ.get("GARFIELD_XENT", "1") != "0"   # fused per-worker cross-entropy kernel
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -808,3 +809,35 @@ class _GroupedLinear(torch.autograd.Function):
 
 def grouped_linear(x, spec: LinearSpec):
     return _GroupedLinear.apply(x, spec.lin.weight, spec.lin.bias, spec)
+
+
+class _GroupedXent(torch.autograd.Function):
+    """Per-worker mean cross-entropy on the fused HIP kernel (loss_xent.hip): the
+    forward writes each worker's loss and d(loss_g)/d(logits); the backward scales
+    that by the upstream per-worker gradient."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, groups: int):
+        loss = torch.empty(groups, dtype=torch.float32, device=logits.device)
+        dl = torch.empty_like(logits)
+        _native.native().gpu_xent_forward(logits, labels, groups, loss, dl)
+        ctx.save_for_backward(dl)
+        ctx.groups = groups
+        return loss
+
+    @staticmethod
+    def backward(ctx, go):
+        (dl,) = ctx.saved_tensors
+        dx = torch.empty_like(dl)
+        _native.native().gpu_xent_backward(dl, go.float().contiguous(), ctx.groups, dx)
+        return dx, None, None
+
+
+def grouped_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, groups: int) -> torch.Tensor:
+    """[groups] per-worker mean cross-entropy of ``logits`` [groups*rows, classes];
+    the fused kernel on GPU (bf16/fp32 logits, <= 64 classes, int64 labels), else ATen."""
+    if (XENT and logits.is_cuda and logits.dim() == 2 and logits.shape[1] <= 64
+            and logits.dtype in (torch.bfloat16, torch.float32) and labels.dtype == torch.int64):
+        return _GroupedXent.apply(logits.contiguous(), labels.contiguous(), groups)
+    lg = logits if logits.dtype == torch.float64 else logits.float()
+    return F.cross_entropy(lg, labels, reduction="none").view(groups, -1).mean(1)

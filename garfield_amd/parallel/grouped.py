@@ -21,7 +21,8 @@ import torch.nn.functional as F
 
 from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
 from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, grouped_bn,
-                                      WgradStream, grouped_conv, grouped_linear, grouped_maxpool)
+                                      WgradStream, grouped_conv, grouped_cross_entropy, grouped_linear,
+                                      grouped_maxpool)
 
 
 def supports(model: nn.Module) -> bool:
@@ -106,10 +107,10 @@ class GroupedResNet:
 
     def losses(self, logits: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         G = self.groups
+        if self.loss_fn is F.cross_entropy:
+            return grouped_cross_entropy(logits, y, G)
         if logits.dtype != torch.float64:
             logits = logits.float()
-        if self.loss_fn is F.cross_entropy:
-            return F.cross_entropy(logits, y, reduction="none").view(G, -1).mean(1)
         lg = logits.view(G, -1, logits.shape[-1])
         yg = y.view(G, -1, *y.shape[1:])
         return torch.stack([self.loss_fn(lg[g], yg[g]) for g in range(G)])

@@ -7,7 +7,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from garfield_amd.models import build_model
-from garfield_amd.ops.grouped import BNState, GradSink, Workspace, grouped_bn, rows2d
+from garfield_amd.ops.grouped import BNState, GradSink, Workspace, grouped_bn, grouped_cross_entropy, rows2d
 from garfield_amd.parallel.comm import DistContext
 from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synthetic_batches
 
@@ -285,3 +285,22 @@ def test_grouped_engine_graph_matches_eager_and_excludes_attacker(cuda):
         assert all(torch.isfinite(torch.tensor(losses)))
         outs.append(eng.flat.reference_vector().clone() - init)
     assert rel(outs[1], outs[0]) < 2e-2
+
+
+@pytest.mark.parametrize("G,B,nc,dt", [(8, 250, 10, torch.bfloat16), (3, 7, 64, torch.float32),
+                                      (1, 300, 2, torch.bfloat16)])
+def test_grouped_cross_entropy_matches_fp32_reference(cuda, native, G, B, nc, dt):
+    """loss_xent.hip: per-worker mean loss and its logits gradient vs fp32 ATen."""
+    torch.manual_seed(nc)
+    z = (torch.randn(G * B, nc, device=cuda) * 4).to(dt)
+    y = torch.randint(0, nc, (G * B,), device=cuda)
+    zi = z.clone().requires_grad_(True)
+    loss = grouped_cross_entropy(zi, y, G)
+    go = torch.rand(G, device=cuda) + 0.5
+    loss.backward(go)
+    zr = z.float().requires_grad_(True)
+    ref = F.cross_entropy(zr, y, reduction="none").view(G, B).mean(1)
+    ref.backward(go)
+    assert rel(loss, ref) < 1e-5
+    assert zi.grad.dtype == dt
+    assert rel(zi.grad, zr.grad) < (1e-2 if dt == torch.bfloat16 else 1e-5)
