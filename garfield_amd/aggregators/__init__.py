@@ -72,3 +72,6 @@ def get(name: str):
         return gars[name]
     except KeyError:
         raise UserException(f"Unknown aggregation rule {name!r}; available: {sorted(gars)}") from None
+
+# TF graph-mode class interface (``aggregators.instantiate(name, nbworkers, nbbyzwrks, args)``)
+from garfield_amd.aggregators.classreg import instantiate, itemize  # noqa: E402,F401
