@@ -10,3 +10,6 @@ from garfield_amd.utils.misc import (  # noqa: F401
     parse_keyval, print_args,
 )
 from garfield_amd.utils.checkpoint import Checkpoints  # noqa: F401
+from garfield_amd.utils.flat import flatten_weights, inflate, mapflat, reshape_weights  # noqa: F401,E402
+from garfield_amd.utils.profiling import trace_graph  # noqa: F401,E402
+from garfield_amd.aggregators.classreg import ClassRegister  # noqa: F401,E402

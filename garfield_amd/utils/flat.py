@@ -163,3 +163,72 @@ class FlatParams:
                 out[pos:pos + n].copy_(memory_order_flat(g))
             pos += n
         return out
+
+
+# --------------------------------------------------------------------------- #
+# TF-tree helpers, over torch tensors / numpy arrays
+
+def flatten_pairs(pairs, flatmap: dict | None = None):
+    """Flatten ``[(gradient, variable), ...]`` skipping ``None`` gradients (reference
+    ``Garfield_legacy/helper.py:65-88``). Without ``flatmap`` returns ``(flat, flatmap)``
+    with ``flatmap[variable] = position``; with it, places each gradient at its
+    recorded position and returns the flat tensor only. Variables are keyed by identity."""
+    if flatmap is None:
+        flatmap, res = {}, []
+        for g, v in pairs:
+            if g is None:
+                continue
+            flatmap[id(v)] = len(res)
+            res.append(g.reshape(-1))
+        return torch.cat(res), flatmap
+    res = [None] * len(flatmap)
+    for g, v in pairs:
+        if g is not None:
+            res[flatmap[id(v)]] = g.reshape(-1)
+    return torch.cat(res)
+
+
+def mapflat(flatmap: dict, variables: Iterable) -> list:
+    """Variables ordered by their position in the flat gradient (``helper.py:90-100``);
+    ``variables`` resolves the identity keys ``flatten_pairs`` records."""
+    by_id = {id(v): v for v in variables}
+    res = [None] * len(flatmap)
+    for key, pos in flatmap.items():
+        res[pos] = by_id[key]
+    return res
+
+
+def inflate(flat: torch.Tensor, ordered: Iterable) -> list:
+    """``[(view, variable), ...]``: slices of ``flat`` shaped like each variable, in order
+    (``helper.py:102-120``). The slices are views, no copy."""
+    res, pos = [], 0
+    for v in ordered:
+        n = v.numel()
+        res.append((flat[pos:pos + n].view(v.shape), v))
+        pos += n
+    return res
+
+
+def flatten_weights(tensors: Iterable):
+    """numpy concatenation of the raveled weights (reference ``TF/libs/tools.py:112-121``)."""
+    import numpy as np
+
+    return np.concatenate([np.asarray(t.detach().cpu() if isinstance(t, torch.Tensor) else t).reshape(-1)
+                           for t in tensors])
+
+
+def reshape_weights(model, flat) -> list:
+    """Split ``flat`` into numpy arrays shaped like ``model``'s trainable parameters
+    (reference ``TF/libs/tools.py:123-144``)."""
+    import numpy as np
+
+    flat = np.asarray(flat)
+    out, i = [], 0
+    params = model.parameters() if isinstance(model, nn.Module) else model
+    for p in params:
+        if isinstance(p, torch.Tensor) and not p.requires_grad:
+            continue
+        n = int(np.prod(p.shape))
+        out.append(np.array(flat[i:i + n]).reshape(tuple(p.shape)))
+        i += n
+    return out

@@ -106,3 +106,22 @@ def torch_profile(enabled: bool = True, sort_by: str = "self_cpu_time_total", ro
     with profile(activities=acts) as prof:
         yield prof
     print(prof.key_averages().table(sort_by=sort_by, row_limit=row_limit))
+
+
+def trace_graph(fn, what: str):
+    """Wrap ``fn`` so each call prints ``[TRACE] (begin) what`` / ``[TRACE] (end)   what``
+    around it and shows up as a named roctx range in ``rocprofv3 --marker-trace`` (reference
+    ``TF/rsrcs/tools/tf.py:41-58``, which wires two ``tf.Print`` ops around a graph node).
+    The end line is printed after the call returns on the host; GPU work it queued may
+    still be running (use ``PhaseTimer`` for device time)."""
+    import functools
+
+    @functools.wraps(fn)
+    def traced(*args, **kwargs):
+        print(f"[TRACE] (begin) {what}", flush=True)
+        with range_ctx(what):
+            out = fn(*args, **kwargs)
+        print(f"[TRACE] (end)   {what}", flush=True)
+        return out
+
+    return traced

@@ -45,3 +45,36 @@ def test_misc_helpers(capsys, tmp_path):
     del b
     assert freed == [[5]]
     assert device_from_tuple("ps", 1, "gpu", 0) == "/job:ps/replica:0/task:1/device:GPU:0"
+
+
+def test_tf_flatten_helpers_roundtrip():
+    import numpy as np
+    import torch.nn as nn
+
+    from garfield_amd.utils.flat import flatten_pairs, flatten_weights, inflate, mapflat, reshape_weights
+
+    m = nn.Sequential(nn.Linear(3, 4), nn.Linear(4, 2))
+    ps = list(m.parameters())
+    grads = [torch.randn_like(p) for p in ps]
+    pairs = list(zip(grads, ps)) + [(None, torch.zeros(1))]
+    flat, fmap = flatten_pairs(pairs)
+    assert flat.numel() == sum(p.numel() for p in ps)
+    assert torch.equal(flatten_pairs(list(reversed(pairs)), fmap), flat)   # positions follow the map
+    order = mapflat(fmap, ps)
+    assert order == ps
+    for (view, v), g in zip(inflate(flat, order), grads):
+        assert view.shape == v.shape and torch.equal(view, g)
+    w = flatten_weights(ps)
+    assert isinstance(w, np.ndarray) and w.size == flat.numel()
+    back = reshape_weights(m, w)
+    for a, p in zip(back, ps):
+        np.testing.assert_array_equal(a, p.detach().numpy())
+
+
+def test_trace_graph_prints_begin_end(capsys):
+    from garfield_amd.utils.profiling import trace_graph
+
+    f = trace_graph(lambda a, b: a + b, "add")
+    assert f(2, 3) == 5
+    out = capsys.readouterr().out
+    assert "[TRACE] (begin) add" in out and "[TRACE] (end)   add" in out
