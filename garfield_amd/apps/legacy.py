@@ -73,7 +73,16 @@ def parse_args(argv=None):
     ap.add_argument("--linger", type=float, default=60.0)
     ap.add_argument("--retry_delay", type=float, default=5.0)
     ap.add_argument("--summary", default=None)
-    return ap.parse_args(argv)
+    ap.add_argument("--experiment", default=None,
+                    help="experiments registry name (mnist, mnistAttack, cnnet, slim-<model>-<dataset>, "
+                         "byzPS.py:120); overrides --dataset / --model")
+    a = ap.parse_args(argv)
+    if a.experiment:
+        from garfield_amd.apps.experiments import instantiate
+
+        a.dataset = instantiate(a.experiment, [f"batch-size:{a.batch}"]).dataset
+        a.model = f"experiment:{a.experiment}"
+    return a
 
 
 def period(a) -> int:

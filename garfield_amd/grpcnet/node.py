@@ -38,6 +38,10 @@ TF_MODELS = {"CNN": "cnn", "Cifarnet": "cifarnet", "MobileNetV2": "mobilenetv2",
 
 def build_tf_model(name: str, dataset: str) -> torch.nn.Module:
     classes = NUM_CLASSES.get(dataset, 10)
+    if name.startswith("experiment:"):   # Garfield_legacy ``--experiment`` (apps/experiments.py)
+        from garfield_amd.apps.experiments import instantiate
+
+        return instantiate(name.split(":", 1)[1]).model()
     if name == "Small":   # Flatten → Dense(128, relu) → Dense(classes)
         sample = fetch(dataset, train=False).x[:1]
         return MLP(num_classes=classes, in_features=int(np.prod(sample.shape[1:])))

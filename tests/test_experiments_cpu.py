@@ -39,3 +39,13 @@ def test_cnnet_and_slim():
     _step(cn)
     sl = ex.instantiate("slim-cifarnet-cifar10", ["batch-size:4"])
     _step(sl)
+
+
+def test_legacy_experiment_flag():
+    from garfield_amd.apps.legacy import parse_args
+    from garfield_amd.grpcnet.node import build_tf_model
+
+    a = parse_args(["--experiment", "cnnet", "--batch", "8"])
+    assert a.dataset == "cifar10" and a.model == "experiment:cnnet"
+    m = build_tf_model(a.model, a.dataset)
+    assert m(torch.randn(2, 3, 32, 32)).shape == (2, 10)
