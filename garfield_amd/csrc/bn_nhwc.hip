@@ -23,6 +23,8 @@
 //
 // Launch boundaries order the stages (no inter-workgroup hand-off inside a
 // launch); every reduction runs in a fixed order, so results are deterministic.
+#include <cstdlib>
+
 #include "bn_gpu.hpp"
 #include "gar_device.hpp"
 
@@ -56,11 +58,21 @@ Geo geometry(int64_t rg, int groups, int C) {
   // enough row chunks to give the partial kernel ~1024 workgroups, each at least 4 row passes
   const int ncb = (C + g.cb - 1) / g.cb;
   const int64_t wg = static_cast<int64_t>(groups) * ncb;
-  int64_t want = (1024 + wg - 1) / wg;
+  static const int64_t target = [] {   // tuning knob: total partial-pass workgroups
+    const char* e = std::getenv("GARFIELD_BN_PARTIAL_WG");
+    const long v = e ? std::atol(e) : 0;
+    return static_cast<int64_t>(v > 0 ? v : 1024);
+  }();
+  int64_t want = (target + wg - 1) / wg;
   int64_t maxc = (rg + 4 * g.rp - 1) / (4 * g.rp);
   int64_t c = want < maxc ? want : maxc;
   if (c < 1) c = 1;
-  if (c > kBnMaxChunks) c = kBnMaxChunks;
+  static const int64_t max_chunks = [] {   // tuning knob: cap on row chunks
+    const char* e = std::getenv("GARFIELD_BN_MAX_CHUNKS");
+    const long v = e ? std::atol(e) : 0;
+    return static_cast<int64_t>(v > 0 ? v : kBnMaxChunks);
+  }();
+  if (c > max_chunks) c = max_chunks;
   g.rows_per_chunk = (rg + c - 1) / c;
   g.chunks = static_cast<int>((rg + g.rows_per_chunk - 1) / g.rows_per_chunk);
   return g;
