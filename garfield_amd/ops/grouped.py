@@ -460,9 +460,14 @@ def _iwgrad_splits(rows_per_worker: int, tiles: int) -> int:
     """Pixel splits of the implicit weight gradient: enough workgroups (~1024) to fill the
     chip, each split at least 256 pixels."""
     S = 1
-    while S < 16 and tiles * S < 1024 and rows_per_worker // (2 * S) >= 256:
+    while S < 16 and tiles * S < _IWGRAD_WG and rows_per_worker // (2 * S) >= _IWGRAD_MINPIX:
         S *= 2
     return S
+
+
+# tuning knobs (profiles/iwgrad_split_sweep_r1.log)
+_IWGRAD_WG = int(os.environ.get("GARFIELD_IWGRAD_WG", "1024"))
+_IWGRAD_MINPIX = int(os.environ.get("GARFIELD_IWGRAD_MINPIX", "256"))
 
 
 def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int) -> None:
