@@ -55,3 +55,22 @@ def test_gar_bench_cpu():
     assert r.returncode == 0, r.stderr[-3000:]
     rows = _rows(r.stdout)
     assert {x["rule"] for x in rows} == {"krum", "median"}
+
+
+def test_bench_py_contract_two_ranks():
+    """The driver's bench.py contract at world 2 (gloo): exactly one JSON line from rank 0
+    with the required keys, n_gpus = WORLD_SIZE, weak scaling (k workers per rank)."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(REPO / "bench.py"),
+                        "--gpus", "2", "--steps", "1", "--warmup", "1", "--model", "cifarnet", "--batch", "4",
+                        "--workers-per-gpu", "3", "--f", "1"],
+                       capture_output=True, text=True, timeout=600, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = _rows(r.stdout)
+    assert len(rows) == 1, r.stdout[-2000:]
+    row = rows[0]
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in row, key
+    assert row["n_gpus"] == 2 and row["steps"] == 1 and row["warmup"] == 1 and row["scaling"] == "weak"
+    assert row["config"]["global_batch"] == 2 * 3 * 4 and row["value"] > 0
