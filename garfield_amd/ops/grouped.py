@@ -434,7 +434,10 @@ def _iconv_ok(x: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
     pixels, 256 workgroups over a 4608-deep reduction) stays on im2col + GEMM, 48 vs 33."""
     return (ICONV and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
-            and -(-rows // 64) * (w.shape[0] // 64) >= 400)
+            and -(-rows // 64) * (w.shape[0] // 64) >= _ICONV_MINWG)
+
+
+_ICONV_MINWG = int(os.environ.get("GARFIELD_ICONV_MINWG", "400"))   # tuning knob (workgroups)
 
 
 def _iconv(x: torch.Tensor, w: torch.Tensor, geom, out_hw, add: torch.Tensor | None = None,
