@@ -218,3 +218,23 @@ def test_flatten_cast_mixed_source_dtypes(cuda, native, odt):
     ref_ = torch.cat([t.reshape(-1).float() for t in ts]).to(odt)
     torch.cuda.synchronize()
     assert torch.equal(dst, ref_)
+
+
+@pytest.mark.parametrize("name", ["krum-tf", "bulyan-py", "median", "averaged-median", "trimmed-mean"])
+def test_class_interface_on_device(cuda, name):
+    """TF graph-mode class interface (aggregators.instantiate) on bf16 device gradients:
+    runs the HIP rules and matches the fp64 oracle of the same rule."""
+    from garfield_amd import aggregators
+
+    n, f, d = 15, 3, 70001
+    torch.manual_seed(5)
+    g = torch.randn(n, d, dtype=torch.float64)
+    g[:f] *= -20.0
+    dev = [row.to(cuda, torch.bfloat16) for row in g]
+    out = aggregators.instantiate(name, n, f, None).aggregate(dev)
+    assert out.device.type == "cuda" and out.shape == (d,)
+    base = name.split("-")[0] if name in ("krum-tf", "bulyan-py") else name
+    kw = {"m": n - f - 2} if base == "krum" else {"beta": n - f} if base == "averaged-median" else {}
+    want = aggregators.gars[base](gradients=torch.stack([r.double().cpu() for r in dev]), f=f, **kw)
+    err = (out.double().cpu() - want).norm() / want.norm()
+    assert err < 1e-2, err
