@@ -19,6 +19,8 @@
 //             per lane) for median / trimmed-mean / averaged-median / Condense /
 //             average-nan, and the Bulyan tail fused with its W·G selection (no t x d
 //             intermediate).
+#include <cstdlib>
+
 #include "gar_device.hpp"
 
 namespace garfield {
@@ -413,7 +415,12 @@ int gram_grid(int64_t d, int dt, int n) {
   const int64_t steps = d / kspan;         // wave steps over the whole vector
   int64_t g = steps / 32;                  // >= 8 steps per wave
   if (g < 1) g = 1;
-  if (g > 1024) g = 1024;
+  static const int64_t cap = [] {   // tuning knob: split-K workgroup cap
+    const char* e = std::getenv("GARFIELD_GRAM_MAXGRID");
+    const long v = e ? std::atol(e) : 0;
+    return static_cast<int64_t>(v > 0 ? v : 1024);
+  }();
+  if (g > cap) g = cap;
   return static_cast<int>(g);
 }
 
