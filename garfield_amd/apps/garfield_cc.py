@@ -84,6 +84,14 @@ def main(argv=None, results: dict | None = None):
     model = build_model(a.model, num_classes=ncls)
     xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
     k = a.workers_per_rank
+    mar = a.mar
+    if mar in ("crash", "vanilla"):
+        # crash-tolerant / vanilla servers (reference trainer.py:97,137,520-523): no Byzantine server, the
+        # trusted PS 0 broadcasts its aggregate. Every server here computes the same deterministic
+        # aggregate from the same gradients, so averaging the identical server models is that broadcast.
+        if a.fps != 0:
+            raise SystemExit(f"--mar {mar} tolerates no Byzantine server: use --fps 0")
+        mar = "average"
     byz_mode = a.num_ps >= 2 or (a.num_ps == 1 and a.fps > 0)
     worker_ranks = list(range(a.num_ps, ctx.world_size)) if byz_mode else list(range(ctx.world_size))
     # Byzantine logical workers: the first fw global worker slots (slot = j * world + rank)
@@ -94,7 +102,7 @@ def main(argv=None, results: dict | None = None):
                   exchange_dtype=xdt, byzantine=byz, cuda_graph=a.cuda_graph)
     if byz_mode:
         eng = ByzantinePSDataParallel(model, loss_fn, ctx,
-                                      ByzPSConfig(num_ps=a.num_ps, fps=a.fps, mar=a.mar, ps_attack=a.ps_attack,
+                                      ByzPSConfig(num_ps=a.num_ps, fps=a.fps, mar=mar, ps_attack=a.ps_attack,
                                                   **common))
     else:
         eng = RobustDataParallel(model, loss_fn, ctx, EngineConfig(**common))

@@ -108,3 +108,17 @@ def test_garfield_cc_byzantine_servers():
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
     m = re.search(r"final accuracy ([0-9.]+)", out.stdout + out.stderr)
     assert m and float(m.group(1)) > 15.0
+
+
+def test_garfield_cc_crash_mar():
+    """--mar crash (reference Garfield_CC/trainer.py:97,137,520-523): 2 trusted servers + 2 workers,
+    median gradient aggregation, servers averaged (their aggregates are identical)."""
+    port = free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    base = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "4", "--master-addr", "127.0.0.1",
+            "--master-port", str(port), "-m", "garfield_amd.apps.garfield_cc", "--num_ps", "2",
+            "--aggregator", "median", "--model", "mlp", "--dataset", "mnist", "--num_iter", "10", "--lr", "0.05",
+            "--loss", "nll", "--workers_per_rank", "3", "--mar", "crash"]
+    out = subprocess.run(base, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+    assert re.search(r"final accuracy ([0-9.]+)", out.stdout + out.stderr)
