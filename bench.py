@@ -25,10 +25,39 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
+
+def _self_launch() -> int | None:
+    """``python bench.py --gpus N`` (N > 1) without a torchrun environment: start
+    ``torch.distributed.run`` with N ranks on this node as a CHILD process and
+    return its exit code. Runs before torch is imported, so nothing has touched
+    the GPU yet (and it is never an exec)."""
+    if "WORLD_SIZE" in os.environ:
+        return None
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument("--gpus", type=int, default=1)
+    known, _ = p.parse_known_args()
+    if known.gpus <= 1:
+        return None
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={known.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
+if __name__ == "__main__":
+    _rc = _self_launch()
+    if _rc is not None:
+        sys.exit(_rc)
+
+import torch  # noqa: E402
 import torch.distributed as dist
 import torch.nn.functional as F
 
@@ -103,8 +132,11 @@ def main():
     if a.cudnn_benchmark:
         torch.backends.cudnn.benchmark = True
     world = ctx.world_size
-    if world != a.gpus and ctx.rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; reporting WORLD_SIZE", file=sys.stderr)
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {world} ranks "
+                         f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')}); refusing to report a mislabelled number")
+    if world > 1:
+        assert ctx.is_distributed and dist.get_world_size() == a.gpus, "process group not initialised"
     shape = (3, 32, 32) if a.dataset == "cifar10" else (3, 224, 224)
     num_classes = 10 if a.dataset == "cifar10" else 1000
     torch.manual_seed(1234)
@@ -174,6 +206,8 @@ def main():
                 "seq_len": None,
                 "image_shape": list(shape),
                 "parallelism": f"dp{world} (robust DP, {a.workers_per_gpu} logical workers/GPU, n={n})",
+                "process_group": {"backend": ctx.backend,
+                                  "world_size": dist.get_world_size() if ctx.is_distributed else 1},
                 "gar": a.gar,
                 "f": a.f,
                 "batch_per_worker": a.batch,

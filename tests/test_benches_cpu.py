@@ -74,3 +74,27 @@ def test_bench_py_contract_two_ranks():
         assert key in row, key
     assert row["n_gpus"] == 2 and row["steps"] == 1 and row["warmup"] == 1 and row["scaling"] == "weak"
     assert row["config"]["global_batch"] == 2 * 3 * 4 and row["value"] > 0
+
+
+def test_bench_py_self_launches_ranks():
+    """``python bench.py --gpus 2`` with NO torchrun: bench.py starts torch.distributed.run
+    itself (child process) and the JSON reports the real process-group size."""
+    env = _env()
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+                        "--model", "cifarnet", "--batch", "4", "--workers-per-gpu", "3", "--f", "1"],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = _rows(r.stdout)
+    assert len(rows) == 1, r.stdout[-2000:]
+    assert rows[0]["n_gpus"] == 2 and rows[0]["config"]["global_batch"] == 2 * 3 * 4
+
+
+def test_bench_py_rejects_world_mismatch():
+    """A rank whose process group disagrees with --gpus must fail instead of printing a number."""
+    env = dict(_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--model", "cifarnet", "--batch", "2", "--workers-per-gpu", "3", "--f", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and not _rows(r.stdout)
