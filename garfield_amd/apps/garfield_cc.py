@@ -56,7 +56,7 @@ def parse(argv=None):
     p.add_argument("--wd", type=float, default=5e-4)
     p.add_argument("--epochs", type=int, default=1)
     p.add_argument("--num_iter", type=int, default=0, help="stop after this many iterations (0: epochs)")
-    p.add_argument("--aggregator", default="average")
+    p.add_argument("--aggregator", default="vanilla", help="GAR name; vanilla = average (reference default)")
     p.add_argument("--mar", default="median")
     p.add_argument("--attack", default="", help="attack of the fw Byzantine worker slots")
     p.add_argument("--ps_attack", default="", help="attack of the fps Byzantine servers")
@@ -97,8 +97,10 @@ def main(argv=None, results: dict | None = None):
     # Byzantine logical workers: the first fw global worker slots (slot = j * world + rank)
     slots = sorted(j * ctx.world_size + r for j in range(k) for r in worker_ranks)
     byz = {s: a.attack for s in slots[: a.fw]} if a.attack else {}
-    common = dict(gar=a.aggregator, f=max(a.fw, 1) if a.aggregator not in ("average", "median", "average-nan")
-                  else max(a.fw, 0), workers_per_rank=k, lr=a.lr, momentum=a.momentum, weight_decay=a.wd,
+    # --aggregator vanilla is the reference default: plain averaging (trainer.py:83-84,444-445)
+    gar_name = "average" if a.aggregator == "vanilla" else a.aggregator
+    # f = fw as in the reference (gar(gradients, f=fw)); a rule whose check needs f >= 1 fails loudly
+    common = dict(gar=gar_name, f=a.fw, workers_per_rank=k, lr=a.lr, momentum=a.momentum, weight_decay=a.wd,
                   exchange_dtype=xdt, byzantine=byz, cuda_graph=a.cuda_graph)
     if byz_mode:
         eng = ByzantinePSDataParallel(model, loss_fn, ctx,

@@ -83,6 +83,30 @@ class EngineConfig:
     shard_gar: bool | None = None
 
 
+class _SlotIssuer:
+    """Starts the per-slot all-gathers in slot order 0..k-1 on EVERY rank.
+
+    Collectives pair up by call order, not by tensor: the local compute order puts a
+    rank's Byzantine slots last (so colluders see the honest estimates) and differs
+    between ranks, so a slot's all-gather is deferred until every lower slot has
+    been issued."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.done = set()
+        self.next = 0
+
+    def ready(self, j: int) -> list:
+        self.done.add(j)
+        works = []
+        while self.next in self.done:
+            w = self.eng._gather_slot(self.next)
+            if w is not None:
+                works.append(w)
+            self.next += 1
+        return works
+
+
 class RobustDataParallel:
     """Robust DP over one process per device (see module docstring)."""
 
@@ -280,6 +304,7 @@ class RobustDataParallel:
         amp = (torch.autocast("cuda", dtype=self.cfg.autocast_dtype)
                if (self.cfg.autocast_dtype is not None and cuda) else contextlib.nullcontext())
         params = self.work_params
+        issue = _SlotIssuer(self)
         with amp:
             for j in self.local_slots:
                 x, y = batches[j]
@@ -300,9 +325,7 @@ class RobustDataParallel:
                                   if self.slot(i) not in self.cfg.byzantine and i != j]
                         est = torch.stack([g] + [h.float() for h in honest])
                     row.copy_(apply_attack(attack, g, est, self._gen))
-                w = self._gather_slot(j)
-                if w is not None:
-                    works.append(w)
+                works += issue.ready(j)
         for p in params:
             p.grad = None
         for w in works:
@@ -444,22 +467,23 @@ class RobustDataParallel:
             return self._grouped_step(batches)
         if not self.graph_capturable() or self.step_count == 0:
             return self._eager_step(batches)
+        if self._graph is not None and not self._static_fits(batches):
+            return self._eager_step(batches)   # e.g. a short last batch: the graphs keep their shapes
         if self._graph is None:
             self._capture(batches)
             if self._graph is None:
                 return self._eager_step(batches)
         works = []
+        issue = _SlotIssuer(self)
         with self.timer.phase("compute"):
             for j in self.local_slots:
                 sx, sy = self._static[j]
                 x, y = batches[j]
-                if x.data_ptr() != sx.data_ptr():
-                    sx.copy_(x, non_blocking=True)
-                    sy.copy_(y, non_blocking=True)
+                # engine-owned static inputs: the caller's tensors are only ever read
+                sx.copy_(x, non_blocking=True)
+                sy.copy_(y, non_blocking=True)
                 self._graph[j].replay()
-                w = self._gather_slot(j)
-                if w is not None:
-                    works.append(w)
+                works += issue.ready(j)
         with self.timer.phase("exchange_wait"):
             for w in works:
                 w.wait()
@@ -589,10 +613,17 @@ class RobustDataParallel:
         for p in self.work_params:
             p.grad = None
 
+    def _static_fits(self, batches) -> bool:
+        if len(batches) != len(self._static):
+            return False
+        return all(x.shape == sx.shape and y.shape == sy.shape and x.dtype == sx.dtype and y.dtype == sy.dtype
+                   for (x, y), (sx, sy) in zip(batches, self._static))
+
     def _capture(self, batches) -> None:
         from garfield_amd.utils.logging import warning
 
-        self._static = [(x, y) for x, y in batches]  # the caller's tensors become the static inputs
+        # engine-owned static inputs (never the caller's tensors: a loader's views must not be overwritten)
+        self._static = [(x.clone(memory_format=torch.preserve_format), y.clone()) for x, y in batches]
         self._static_loss = torch.zeros(self.k, dtype=torch.float32, device=self.device)
         self.model.train()
         torch.cuda.synchronize()

@@ -7,7 +7,9 @@ in registration order (``server.py:196-200,289-297``). A checkpoint here holds:
 * ``flat``: that reference-layout parameter vector (what ``Server.write_model`` /
   ``get_model`` exchange), so a checkpoint can seed any node of any app;
 * ``buffers``: the model's named buffers (BatchNorm statistics);
-* ``momentum``: the engine's flat momentum buffer (memory order), when present;
+* ``momentum``: the engine's momentum in the same reference layout as ``flat``
+  (so a channels_last / grouped GPU checkpoint resumes correctly on an NCHW
+  engine, and vice versa), when present;
 * ``step`` and free-form ``meta``.
 
 Files are written atomically (temp file + rename) with ``torch.save`` and read back
@@ -70,7 +72,7 @@ def save_engine(path: str, engine, meta: dict | None = None) -> str:
     """Checkpoint of a ``RobustDataParallel`` engine (fp32 master parameters in the
     reference layout, buffers, momentum, step)."""
     mom = engine.momentum_vector() if hasattr(engine, "momentum_vector") else engine.mom
-    return save(path, engine.model, engine.step_count, mom[: engine.d], meta,
+    return save(path, engine.model, engine.step_count, engine.flat.to_reference(mom), meta,
                 flat=engine.flat.reference_vector())
 
 
@@ -87,13 +89,15 @@ def load_engine(path: str, engine) -> dict:
         engine.sync_shadow()
     if "momentum" in state:
         m = state["momentum"].to(engine.mom.device)
+        full = torch.zeros(engine.flat.ld, dtype=engine.mom.dtype, device=engine.mom.device)
+        engine.flat.from_reference(m, full)        # reference layout -> this engine's memory order
         shard = getattr(engine, "_shard", None)
-        if shard is not None:   # sharded optimizer state: this rank's slice
-            full = torch.zeros(shard.world * shard.S, dtype=m.dtype, device=m.device)
-            full[: m.numel()] = m
+        if shard is not None and hasattr(shard, "load_momentum"):
+            shard.load_momentum(full)
+        elif shard is not None:   # sharded optimizer state: this rank's slice
             engine.mom.copy_(full[shard.sl])
         else:
-            engine.mom[: engine.d].copy_(m)
+            engine.mom.copy_(full[: engine.mom.numel()])
     engine.step_count = int(state.get("step", 0))
     engine._graph = None  # re-capture against the restored state
     return state

@@ -152,6 +152,20 @@ class FlatParams:
                 p.copy_(flat[pos:pos + n].view(p.shape))
                 pos += n
 
+    def to_reference(self, buf: torch.Tensor) -> torch.Tensor:
+        """A buffer laid out like ``data`` (memory order, e.g. the momentum) in the
+        reference layout (logical ``p.view(-1)`` order per parameter)."""
+        return flatten(v.detach() for v in self.views(buf))
+
+    def from_reference(self, flat: torch.Tensor, buf: torch.Tensor) -> torch.Tensor:
+        """Scatter a reference-layout vector into ``buf`` (laid out like ``data``)."""
+        with torch.no_grad():
+            pos = 0
+            for v, n in zip(self.views(buf), self.numels):
+                v.copy_(flat[pos:pos + n].view(v.shape))
+                pos += n
+        return buf
+
     def grads_flat(self, out: torch.Tensor) -> torch.Tensor:
         """Write the current per-parameter gradients (memory order) into ``out[:d]``."""
         pos = 0

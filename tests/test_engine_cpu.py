@@ -88,6 +88,7 @@ def test_two_rank_sharded_aggregation_matches_allgather(rule):
             mp.spawn(_sharded_worker, args=(2, free_port(), d, rule, shard), nprocs=2, join=True)
         r = {k: torch.load(os.path.join(d, f"{k}.pt"), weights_only=True) for k in ("0r0", "0r1", "1r0", "1r1")}
         assert torch.equal(r["1r0"]["flat"], r["1r1"]["flat"])           # sharded replicas identical
+        assert torch.equal(r["0r0"]["flat"], r["0r1"]["flat"])           # redundant replicas identical
         ref_flat = r["0r0"]["flat"]
         rel = ((r["1r0"]["flat"] - ref_flat).norm() / ref_flat.norm()).item()
         assert rel < 1e-5, rel

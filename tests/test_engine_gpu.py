@@ -135,3 +135,27 @@ def test_sharded_gpu_path_single_rank_matches(cuda, rule, f):
     assert rel < 1e-5, rel
     if w0 is not None:
         assert torch.equal(w0.cpu(), w1.cpu())
+
+
+@pytest.mark.gpu
+def test_cuda_graph_never_writes_loader_tensors(cuda):
+    """Per-worker HIP-graph path fed by DeviceLoaders with a short last batch: the
+    engine copies into its OWN static inputs (the loader's label/input views stay
+    untouched) and a batch of another shape runs eagerly instead of failing."""
+    from garfield_amd.data.datasets import DeviceLoader, TensorDataset
+
+    torch.manual_seed(0)
+    k = 3
+    ds = TensorDataset(torch.randn(10 * k, 3, 32, 32), torch.randint(0, 10, (10 * k,)))
+    loaders = [DeviceLoader(ds, range(10 * j, 10 * (j + 1)), 4, cuda) for j in range(k)]   # 4, 4, 2
+    y0 = [ld.y.clone() for ld in loaders]
+    x0 = [ld.x.clone() for ld in loaders]
+    cfg = EngineConfig(gar="median", f=1, workers_per_rank=k, cuda_graph=True, worker_batching=False, lr=1e-3)
+    eng = RobustDataParallel(build_model("cifarnet"), F.cross_entropy, DistContext(device=cuda), cfg)
+    for it in range(2 * len(loaders[0])):
+        loss = eng.step([ld[it] for ld in loaders])
+        assert torch.isfinite(loss).item()
+    torch.cuda.synchronize()
+    assert eng._graph is not None
+    for ld, y, x in zip(loaders, y0, x0):
+        assert torch.equal(ld.y, y) and torch.equal(ld.x, x)

@@ -78,3 +78,32 @@ def test_trace_graph_prints_begin_end(capsys):
     assert f(2, 3) == 5
     out = capsys.readouterr().out
     assert "[TRACE] (begin) add" in out and "[TRACE] (end)   add" in out
+
+
+def test_checkpoint_channels_last_to_nchw_roundtrip(tmp_path):
+    """Momentum is saved in the reference layout: a checkpoint of a grouped
+    (channels_last memory order) engine resumes an NCHW engine exactly."""
+    from garfield_amd.utils.checkpoint import load_engine, save_engine
+
+    kw = dict(gar="krum", f=1, workers_per_rank=5, lr=0.05, autocast_dtype=None, exchange_dtype=torch.float32)
+    torch.manual_seed(0)
+    a = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(),
+                           EngineConfig(worker_batching=True, **kw))
+    assert a._gexec is not None
+    conv = next(p for p in a.model.parameters() if p.dim() == 4)
+    assert conv.is_contiguous(memory_format=torch.channels_last) and not conv.is_contiguous()
+    b = synthetic_batches(5, 2, (3, 32, 32), 10, "cpu")
+    for _ in range(2):
+        a.step(b)
+    save_engine(str(tmp_path / "a.pt"), a)
+    torch.manual_seed(1)
+    c = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(),
+                           EngineConfig(worker_batching=False, **kw))
+    assert c._gexec is None
+    load_engine(str(tmp_path / "a.pt"), c)
+    assert torch.equal(c.flat.reference_vector(), a.flat.reference_vector())
+    assert torch.equal(c.flat.to_reference(c.mom), a.flat.to_reference(a.mom))
+    a.step(b)
+    c.step(b)
+    ra, rc = a.flat.reference_vector(), c.flat.reference_vector()
+    assert ((ra - rc).norm() / ra.norm()).item() < 1e-5
