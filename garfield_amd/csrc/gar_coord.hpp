@@ -1,6 +1,7 @@
 // Coordinate-wise rule kernels (register bitonic networks), instantiated per
 // mode in gar_coord_m*.hip so the 90 variants compile in parallel.
 #pragma once
+#include <cstdlib>
 #include "gar_device.hpp"
 
 namespace garfield {
@@ -179,6 +180,34 @@ __global__ __launch_bounds__(256) void k_coordwise(RowTable rows, int n, int64_t
   }
 }
 
+// knobs: GARFIELD_COORD16=0 disables the packed 16-bit-key kernels (A/B runs);
+// GARFIELD_COORD16_GRID caps their grid (grid-stride loop beyond it)
+inline bool coord16_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("GARFIELD_COORD16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+inline int64_t coord16_grid_cap() {
+  static const int64_t cap = [] {
+    const char* e = std::getenv("GARFIELD_COORD16_GRID");
+    const long v = e ? std::atol(e) : 0;
+    return static_cast<int64_t>(v > 0 ? v : 4096);
+  }();
+  return cap;
+}
+
+}  // namespace coord
+}  // namespace gpu
+}  // namespace garfield
+
+#include "gar_coord16.hpp"
+
+namespace garfield {
+namespace gpu {
+namespace coord {
+
 // Large n (NP >= 32): one lane per coordinate would issue n 2-byte loads; instead
 // a workgroup stages a [n x 256-coordinate] tile through LDS with 16-byte loads
 // (each row segment is 512 B / 1 KB contiguous), then every lane reads its
@@ -261,6 +290,12 @@ template <int DT, int NP, int VEC, int MODE>
 void launch_coord(const RowTable& rows, int n, int64_t d, int f, int beta, const float* W, int t, uint64_t seed,
                   uint64_t thr, void* out, int out_dt, hipStream_t s) {
   constexpr int ESZ = (DT == kF32) ? 4 : 2;
+  if constexpr (DT != kF32 && coord16_mode<MODE>()) {
+    if (coord16_enabled()) {
+      launch_coord16<DT, NP, MODE>(rows, n, d, f, beta, seed, thr, out, out_dt, s);
+      return;
+    }
+  }
   // LDS-staged path: NP >= 32, tile <= 64 KB, and (Bulyan tail) all n rows fit the NP-row tile
   if constexpr (NP >= 32 && NP * kCoordTile * ESZ <= 65536) {
     if (MODE != kBulyanTail || n <= NP) {

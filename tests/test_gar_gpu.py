@@ -238,3 +238,62 @@ def test_class_interface_on_device(cuda, name):
     want = aggregators.gars[base](gradients=torch.stack([r.double().cpu() for r in dev]), f=f, **kw)
     err = (out.double().cpu() - want).norm() / want.norm()
     assert err < 1e-2, err
+
+
+def _nonfinite_rows(n, d, dtype, seed):
+    """Random rows with NaN / +inf / -inf sprinkled over a few coordinates (and
+    whole rows of them in others), so the packed-key kernels' exact fallback runs."""
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, d, generator=g)
+    cols = torch.randperm(d, generator=g)[: max(d // 50, 3)]
+    for k, c in enumerate(cols.tolist()):
+        r = torch.randperm(n, generator=g)[: 1 + k % max(n // 3, 1)]
+        X[r, c] = (math.nan, math.inf, -math.inf)[k % 3]
+    return X.to(dtype)
+
+
+def _same(a, b, dtype):
+    a, b = a.double().cpu(), b.double().cpu()
+    fa, fb = torch.isfinite(a), torch.isfinite(b)
+    assert torch.equal(fa, fb)
+    assert torch.equal(torch.isnan(a), torch.isnan(b))
+    assert torch.equal(a[~fa & ~torch.isnan(a)], b[~fb & ~torch.isnan(b)])
+    if fa.any():
+        err = (a[fa] - b[fa]).abs().max().item()
+        assert err <= TOL[dtype] * max(b[fa].abs().max().item(), 1.0), err
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n", [5, 8, 13, 16, 32, 40, 64])
+def test_packed_key_rules_with_nonfinite(cuda, n, dtype):
+    """bf16/fp16 median, trimmed mean, averaged median and condense (packed 16-bit
+    key networks + exact rank fallback for NaN/inf coordinates and the tail) vs
+    the fp64 oracle; d is odd so the scalar tail runs too."""
+    X = _nonfinite_rows(n, 2 * 1024 + 7, dtype, seed=n)
+    Xc = X.to(cuda)
+    assert torch.equal(gar.median(Xc).double().cpu(), ref.median(X).to(dtype).double())
+    f = max((n - 1) // 4, 1)
+    _same(gar.trimmed_mean(Xc, f), ref.trimmed_mean(X, f), dtype)
+    beta = n - f
+    _same(gar.averaged_median(Xc, beta=beta), ref.averaged_median(X, beta), dtype)
+    out = gar.condense(Xc, p=0.7, seed=99)
+    assert torch.allclose(out.double().cpu(), ref.condense(X, 0.7, 99).to(dtype).double(), rtol=0, atol=0,
+                          equal_nan=True)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n", [8, 16, 32, 64])
+def test_packed_key_rules_ties_and_extremes(cuda, n, dtype):
+    """Heavy ties (values drawn from 5 levels), largest finite values and -0.0/+0.0:
+    the order-preserving key map and the max-finite padding must not change results."""
+    g = torch.Generator().manual_seed(n)
+    levels = torch.tensor([-0.0, 0.0, 1.5, -2.25, torch.finfo(dtype).max])
+    X = levels[torch.randint(0, 5, (n, 4096 + 3), generator=g)].to(dtype)
+    Xc = X.to(cuda)
+    assert torch.equal(gar.median(Xc).double().cpu(), ref.median(X).to(dtype).double())
+    # sums of dtype-max values overflow fp32 accumulators (not the fp64 oracle): use 1e4 there
+    X = torch.where(X.float().abs() > 1e4, torch.full_like(X, 1e4), X)
+    Xc = X.to(cuda)
+    f = max(n // 8, 1)
+    _same(gar.trimmed_mean(Xc, f), ref.trimmed_mean(X, f), dtype)
+    _same(gar.averaged_median(Xc, beta=n - f), ref.averaged_median(X, n - f), dtype)
