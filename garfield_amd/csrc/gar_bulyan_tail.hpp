@@ -1,0 +1,453 @@
+// Bulyan's coordinate-wise tail for n <= 64 gradients (every dtype).
+//
+// Input: the t x n selection matrix W of bulyan_select (row k = uniform weights
+// 1/(m-k) over the set S_k chosen at step k). Output per coordinate: the mean of
+// the beta values closest to the median of the t selection means
+// (reference: py_bulyan/bulyan.cu:227-243, 256-322).
+//
+// The previous form gathered every mean from scratch: sum_k |S_k| ~ t*m LDS reads
+// and FMAs per coordinate (1,764 at n = 64, f = 3). Consecutive sets differ by a
+// few gradients, so here the means are built INCREMENTALLY: each set S_k is a
+// 64-bit mask (kept in LDS, read as wave-uniform SGPRs), the running sum adds
+// S_k \ S_{k-1} and subtracts S_{k-1} \ S_k with scalar bit loops (about m + 2t
+// LDS reads). A coordinate whose running sum turns non-finite (inf - inf) is
+// recomputed exactly with direct per-set sums (divergent, rare).
+//
+// The t means are sorted with an odd-even merge network in registers; the beta
+// closest to the median form a window [a, a + beta) of the sorted values, whose
+// start a is found from the e = t - beta smallest and largest values (no second
+// sort by distance, unlike the generic closest_mean).
+#pragma once
+#include "gar_device.hpp"
+
+namespace garfield {
+namespace gpu {
+namespace coord {
+using namespace dev;
+
+// fp32 <-> order-preserving int32 key (NaN already mapped to +inf): integer
+// min/max need no NaN canonicalisation of their inputs, unlike fminf/fmaxf
+__device__ __forceinline__ int f32_key(float f) {
+  const int b = __float_as_int(f);
+  return b ^ ((b >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ float key_f32(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
+
+template <int NP>
+__device__ __forceinline__ void oem_sort_i32(int (&v)[NP]) {
+#pragma unroll
+  for (int p = 1; p < NP; p <<= 1) {
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+      for (int j = k % p; j + k < NP; j += 2 * k) {
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
+          if (i + j + k < NP && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            const int a = v[i + j], b = v[i + j + k];
+            v[i + j] = min(a, b);
+            v[i + j + k] = max(a, b);
+          }
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+constexpr int kTailTile = 256;
+constexpr int kTailMaxExcluded = 16;  // e = t - beta <= 16 (host checks; larger e: generic kernel)
+
+template <int DT, int NP, bool DIRECT>
+__global__ __launch_bounds__(256) void k_bulyan_tail(RowTable rows, int n, int64_t d, int beta,
+                                                     const float* __restrict__ W, int t, void* out, int out_dt) {
+  constexpr int ESZ = (DT == kF32) ? 4 : 2;
+  constexpr int CPR = kTailTile * ESZ / 16;  // 16-byte chunks per tile row
+  __shared__ __align__(16) unsigned char tile[64 * kTailTile * ESZ];
+  __shared__ uint64_t smask[NP];
+  __shared__ float sscale[NP];
+  for (int k = threadIdx.x; k < t && !DIRECT; k += blockDim.x) {
+    uint64_t m = 0;
+    float sc = 0.f;
+    for (int j = 0; j < n; ++j) {
+      const float w = W[k * n + j];
+      if (w != 0.f) { m |= 1ull << j; sc = w; }
+    }
+    smask[k] = m;
+    sscale[k] = sc;
+  }
+  __syncthreads();
+  const int e = t - beta;  // values left out of the window
+  const float inv_beta = 1.f / static_cast<float>(beta);
+  const int64_t ntiles = d / kTailTile;
+  auto at = [&](int j, int col) -> float {
+    if constexpr (DT == kF32) return reinterpret_cast<const float*>(tile)[j * kTailTile + col];
+    else return cvt16<DT>(reinterpret_cast<const uint16_t*>(tile)[j * kTailTile + col]);
+  };
+  for (int64_t tb = blockIdx.x; tb < ntiles + 1; tb += gridDim.x) {
+    const int64_t x0 = tb * kTailTile;
+    const int width = static_cast<int>(tb < ntiles ? kTailTile : d - x0);  // last tile: the d % 256 tail
+    if (width <= 0) break;
+    if (width == kTailTile) {
+      for (int c = threadIdx.x; c < n * CPR; c += blockDim.x) {
+        const int i = c / CPR, k = c % CPR;
+        *reinterpret_cast<uint4*>(tile + (i * kTailTile) * ESZ + k * 16) =
+            *reinterpret_cast<const uint4*>(static_cast<const char*>(rows.p[i]) + x0 * ESZ + k * 16);
+      }
+    } else {
+      for (int c = threadIdx.x; c < n * kTailTile; c += blockDim.x) {  // columns >= width repeat column 0
+        const int i = c / kTailTile, k = c % kTailTile;
+        const int64_t xs = k < width ? x0 + k : x0;
+        if constexpr (DT == kF32) reinterpret_cast<float*>(tile)[i * kTailTile + k] = load_one<DT>(rows.p[i], xs);
+        else reinterpret_cast<uint16_t*>(tile)[i * kTailTile + k] = static_cast<const uint16_t*>(rows.p[i])[xs];
+      }
+    }
+    __syncthreads();
+    const int col = threadIdx.x;
+    const int tt = opaque_uniform(t), ee = opaque_uniform(e), bb = opaque_uniform(beta);
+    float v[NP];
+    float r = 0.f;
+    uint64_t prev = 0;
+    bool exact = true;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      if constexpr (DIRECT) {  // averaged median: the rows themselves (NaN -> +inf)
+        v[k] = k < tt ? sanitize_inf(at(k, col)) : kInf;
+        continue;
+      }
+      if (k < tt) {  // uniform
+        // volatile LDS reads: the per-set mask and scale are tile-invariant, and hoisting
+        // all t of them out of the tile loop would pin 2t SGPRs + t VGPRs (spills)
+        const uint64_t cur = uniform64(*reinterpret_cast<volatile uint64_t*>(&smask[k]));
+        uint64_t add = cur & ~prev, rem = prev & ~cur;
+#pragma clang loop unroll(disable)
+        while (add) { r += at(__builtin_ctzll(add), col); add &= add - 1; }
+#pragma clang loop unroll(disable)
+        while (rem) { r -= at(__builtin_ctzll(rem), col); rem &= rem - 1; }
+        prev = cur;
+        exact = exact && isfinite(r);
+        v[k] = r * *reinterpret_cast<volatile float*>(&sscale[k]);
+      } else {
+        v[k] = kInf;
+      }
+    }
+    if (!DIRECT && !exact) {  // inf / NaN inputs: direct per-set sums (sanitised like the generic path)
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        if (k < tt) {
+          uint64_t m = uniform64(*reinterpret_cast<volatile uint64_t*>(&smask[k]));
+          float s = 0.f;
+#pragma clang loop unroll(disable)
+          while (m) { s += at(__builtin_ctzll(m), col); m &= m - 1; }
+          v[k] = sanitize_inf(s * *reinterpret_cast<volatile float*>(&sscale[k]));
+        }
+      }
+    }
+    int key[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) key[k] = f32_key(sanitize_inf(v[k]));
+    oem_sort_i32<NP>(key);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) v[k] = key_f32(key[k]);
+    const float med = pick_sel(v, tt / 2);
+    // window start a = #{s < e : v[s] is farther from med than v[s + beta]} (monotone in s);
+    // v[s + beta] for s < e comes from a barrel shift by the uniform beta (static indices only)
+    float u[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) u[i] = v[i];
+#pragma unroll
+    for (int b = NP / 2; b >= 1; b >>= 1) {
+      if (bb & b) {
+#pragma unroll
+        for (int i = 0; i + b < NP; ++i) u[i] = u[i + b];
+      }
+    }
+    int a = 0;
+#pragma unroll
+    for (int s = 0; s < kTailMaxExcluded; ++s) {
+      if (s < ee) a += !(sanitize_inf(med - v[s]) <= sanitize_inf(u[s] - med));
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) acc += (i >= a && i < a + bb) ? v[i] : 0.f;
+    if (col < width) store_one(out, out_dt, x0 + col, acc * inv_beta);
+    __syncthreads();
+  }
+}
+
+// W == nullptr: averaged median of the n rows themselves (t = n)
+template <int DT, int NP>
+void launch_bulyan_tail(const RowTable& rows, int n, int64_t d, int beta, const float* W, int t, void* out,
+                        int out_dt, hipStream_t s) {
+  int64_t g = d / kTailTile + 1;
+  if (g > 2048) g = 2048;
+  if (W == nullptr)
+    hipLaunchKernelGGL((k_bulyan_tail<DT, NP, true>), dim3(static_cast<unsigned>(g)), dim3(256), 0, s, rows, n, d,
+                       beta, W, n, out, out_dt);
+  else
+    hipLaunchKernelGGL((k_bulyan_tail<DT, NP, false>), dim3(static_cast<unsigned>(g)), dim3(256), 0, s, rows, n, d,
+                       beta, W, t, out, out_dt);
+}
+
+// ---------------------------------------------------------------------------
+// bf16 / fp16 gradients: the t selection means on MFMA.
+//
+// The means are a GEMM: C[t x coords] = S[t x n] . G[n x coords] with S the 0/1
+// selection matrix (exact in bf16/fp16; the 1/(m-k) scale is applied in fp32
+// afterwards). One wave owns 64 coordinates: it stages the [n x 64] gradient
+// tile in its own LDS region with 16-byte loads (no workgroup barrier), reads
+// the B fragments with ds_read_b64_tr_b16 (the hardware transpose: gradient rows
+// are contiguous along coordinates, the MFMA wants 8 consecutive rows per lane),
+// and runs MB x 2 x KS v_mfma_f32_32x32x16 with the S fragments held in
+// registers for the whole kernel. A v_permlane32_swap then leaves every lane
+// with all t means of ONE coordinate (lane = coordinate), which it sorts in
+// registers as above. Coordinates whose means are not all finite (an inf/NaN
+// input also turns 0 * inf into NaN inside the MFMA) are recomputed exactly with
+// direct per-set sums from the same LDS tile.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int kMfmaTailPitch = 144;  // bytes per LDS tile row: 64 coordinates x 2 B + 16 B (bank spread)
+
+template <int DT>
+__device__ __forceinline__ f32x16_t mfma32x32x16(s16x8_t a, s16x8_t b, f32x16_t c) {
+  if constexpr (DT == kBF16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                  0, 0, 0);
+}
+
+// key[idx] for a runtime idx: OR of masked terms (a select of one load and a
+// constant 0 per element is not folded back into one dynamically indexed load, and
+// needs no forced register copies)
+template <int N>
+__device__ __forceinline__ int pick_or(const int (&key)[N], int idx) {
+  int r = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r |= (i == idx) ? key[i] : 0;
+  return r;
+}
+
+// sorted means -> mean of the beta closest to the median (window [a, a + beta))
+template <int NP>
+__device__ __forceinline__ float window_mean(float (&v)[NP], int tt, int bb, float inv_beta) {
+  int key[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) key[k] = f32_key(sanitize_inf(v[k]));
+  oem_sort_i32<NP>(key);
+  const float med = key_f32(pick_or(key, tt / 2));
+  const int ee = tt - bb;
+  int a = 0;
+#pragma unroll
+  for (int s = 0; s < kTailMaxExcluded; ++s) {
+    if (s < ee)
+      a += !(sanitize_inf(med - key_f32(key[s])) <= sanitize_inf(key_f32(pick_or(key, s + bb)) - med));
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) acc += (i >= a && i < a + bb) ? key_f32(key[i]) : 0.f;
+  return acc * inv_beta;
+}
+
+template <int DT, int KR>
+__device__ __forceinline__ void stage_tile(unsigned char* tile, const void* const* sptr, int nn, int64_t x0, int lane) {
+#pragma unroll
+  for (int c0 = 0; c0 < KR * 8; c0 += 64) {
+    const int c = c0 + lane, row = c >> 3, ch = c & 7;
+    u32x4 val = {0u, 0u, 0u, 0u};
+    if (row < nn) val = *reinterpret_cast<const u32x4*>(static_cast<const char*>(sptr[row]) + x0 * 2 + ch * 16);
+    *reinterpret_cast<u32x4*>(tile + row * kMfmaTailPitch + ch * 16) = val;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // wave-local LDS hand-off
+}
+
+constexpr int kTailBadSlots = 32;  // per-wave list of 64-coordinate groups needing the exact path
+
+template <int DT, int MB, int KS>
+__global__ __launch_bounds__(256) void k_bulyan_tail_mfma(RowTable rows, int n, int64_t ngroups, int beta,
+                                                          const float* __restrict__ W, int t, void* out,
+                                                          int out_dt) {
+  constexpr int NP = 32 * MB;  // means per coordinate (padded)
+  constexpr int KR = 16 * KS;  // gradient rows (padded)
+  __shared__ __align__(16) unsigned char tiles[4][KR * kMfmaTailPitch];
+  __shared__ __align__(16) uint16_t sA[NP * KR];
+  __shared__ const void* sptr[KR];
+  __shared__ uint64_t smask[NP];
+  __shared__ float sscale[NP];
+  __shared__ int64_t sbad[4][kTailBadSlots];
+  __shared__ int sbadn[4];
+  const uint16_t one = DT == kBF16 ? 0x3F80 : 0x3C00;
+  for (int k = threadIdx.x; k < NP; k += blockDim.x) {
+    uint64_t m = 0;
+    float sc = 0.f;
+    for (int j = 0; j < KR; ++j) {
+      const float w = (k < t && j < n) ? W[k * n + j] : 0.f;
+      sA[k * KR + j] = w != 0.f ? one : 0;
+      if (w != 0.f) { m |= 1ull << j; sc = w; }
+    }
+    smask[k] = m;
+    sscale[k] = sc;
+  }
+  for (int j = threadIdx.x; j < KR; j += blockDim.x) sptr[j] = rows.p[j < n ? j : 0];
+  if (threadIdx.x < 4) sbadn[threadIdx.x] = 0;
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned char* tile = tiles[wave];
+  // ds_read_b64_tr_b16 addressing: group g = lane / 16 reads rows 8 (g >> 1) + q and
+  // columns 16 (g & 1) + 4 p .. + 3 (lane = 16 g + 4 q + p); lane i of the group gets column i
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int tr_off = (8 * (g >> 1) + q) * kMfmaTailPitch + (16 * (g & 1) + 4 * p) * 2;
+  const int a_off = (lane & 31) * KR + 8 * (lane >> 5);
+  const float inv_beta = 1.f / static_cast<float>(beta);
+  bool overflow = false;
+  for (int64_t gi = static_cast<int64_t>(blockIdx.x) * 4 + wave; gi < ngroups; gi += static_cast<int64_t>(gridDim.x) * 4) {
+    const int64_t x0 = gi * 64;
+    const int nn = opaque_uniform(n), tt = opaque_uniform(t), bb = opaque_uniform(beta);
+    stage_tile<DT, KR>(tile, sptr, nn, x0, lane);
+    f32x16_t acc[MB][2];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[mb][nb][i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      s16x8_t afrag[MB];  // S[32 mb + (l & 31)][16 ks + 8 (l >> 5) + 0..7], re-read (frees registers)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        afrag[mb] = *reinterpret_cast<const volatile s16x8_t*>(&sA[a_off + 32 * mb * KR + 16 * ks]);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+        const unsigned char* base = tile + ks * 16 * kMfmaTailPitch + nb * 64 + tr_off;
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * kMfmaTailPitch));
+        const s16x8_t bfrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) acc[mb][nb] = mfma32x32x16<DT>(afrag[mb], bfrag, acc[mb][nb]);
+      }
+    }
+    // lane = coordinate: swap the halves so each lane holds all NP means of x0 + lane
+    float v[NP];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[mb][0][i]),
+                                                         __float_as_uint(acc[mb][1][i]), false, false);
+        const int k0 = 32 * mb + (i & 3) + 8 * (i >> 2);
+        v[k0] = __uint_as_float(sw[0]);
+        v[k0 + 4] = __uint_as_float(sw[1]);
+      }
+    bool finite = true;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const float sc = *reinterpret_cast<volatile float*>(&sscale[k]);
+      v[k] = k < tt ? v[k] * sc : kInf;
+      finite = finite && (k >= tt || isfinite(v[k]));
+    }
+    if (__builtin_amdgcn_ballot_w64(!finite)) {  // exact pass later (out of this loop's registers)
+      const int slot = sbadn[wave];
+      if (slot < kTailBadSlots) {
+        if (lane == 0) sbad[wave][slot] = gi;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) sbadn[wave] = slot + 1;
+      } else {
+        overflow = true;
+      }
+    }
+    store_one(out, out_dt, x0 + lane, window_mean<NP>(v, tt, bb, inv_beta));
+  }
+  // exact pass: groups whose MFMA means were not all finite (inf/NaN inputs), recomputed
+  // with direct per-set sums from the LDS tile; after an overflow of the list, every group
+  // of this wave is re-examined
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int nbad = overflow ? 0 : sbadn[wave];
+  int64_t gi = overflow ? static_cast<int64_t>(blockIdx.x) * 4 + wave : 0;
+  for (int b = 0; overflow ? gi < ngroups : b < nbad; ++b) {
+    const int64_t gcur = overflow ? gi : sbad[wave][b];
+    if (overflow) gi += static_cast<int64_t>(gridDim.x) * 4;
+    const int64_t x0 = gcur * 64;
+    const int nn = opaque_uniform(n), tt = opaque_uniform(t), bb = opaque_uniform(beta);
+    stage_tile<DT, KR>(tile, sptr, nn, x0, lane);
+    const uint16_t* col = reinterpret_cast<const uint16_t*>(tile) + lane;
+    float v[NP];
+    bool finite = true;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      v[k] = kInf;
+      if (k < tt) {
+        uint64_t m = uniform64(*reinterpret_cast<volatile uint64_t*>(&smask[k]));
+        float s = 0.f;
+#pragma clang loop unroll(disable)
+        while (m) {
+          s += cvt16<DT>(col[__builtin_ctzll(m) * (kMfmaTailPitch / 2)]);
+          m &= m - 1;
+        }
+        v[k] = sanitize_inf(s * *reinterpret_cast<volatile float*>(&sscale[k]));
+        finite = finite && isfinite(v[k]);
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(!finite))  // only groups that really hold a non-finite mean
+      store_one(out, out_dt, x0 + lane, window_mean<NP>(v, tt, bb, inv_beta));
+  }
+}
+
+// t <= 64, n <= 64, bf16/fp16: MFMA means for the 64-coordinate groups, the
+// incremental kernel for the d % 64 tail
+template <int DT, int MB>
+void launch_tail_mfma_ks(int ks, const RowTable& rows, int n, int64_t groups, int beta, const float* W, int t,
+                         void* out, int out_dt, hipStream_t s) {
+  int64_t g = (groups + 3) / 4;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  const dim3 grid(static_cast<unsigned>(g)), block(256);
+  switch (ks) {
+    case 1: hipLaunchKernelGGL((k_bulyan_tail_mfma<DT, MB, 1>), grid, block, 0, s, rows, n, groups, beta, W, t, out, out_dt); break;
+    case 2: hipLaunchKernelGGL((k_bulyan_tail_mfma<DT, MB, 2>), grid, block, 0, s, rows, n, groups, beta, W, t, out, out_dt); break;
+    case 3: hipLaunchKernelGGL((k_bulyan_tail_mfma<DT, MB, 3>), grid, block, 0, s, rows, n, groups, beta, W, t, out, out_dt); break;
+    default: hipLaunchKernelGGL((k_bulyan_tail_mfma<DT, MB, 4>), grid, block, 0, s, rows, n, groups, beta, W, t, out, out_dt); break;
+  }
+}
+
+template <int DT>
+bool launch_bulyan_tail_mfma(const RowTable& rows, int n, int64_t d, int beta, const float* W, int t, void* out,
+                             int out_dt, hipStream_t s) {
+  if (DT == kF32 || n > 64 || t > 64 || t - beta > kTailMaxExcluded || W == nullptr) return false;
+  const int64_t groups = d / 64;
+  const int ks = (n + 15) / 16;
+  if (groups > 0) {
+    if (t <= 32) launch_tail_mfma_ks<DT, 1>(ks, rows, n, groups, beta, W, t, out, out_dt, s);
+    else launch_tail_mfma_ks<DT, 2>(ks, rows, n, groups, beta, W, t, out, out_dt, s);
+  }
+  const int64_t done = groups * 64;
+  if (done < d) {  // tail coordinates: shifted row table, generic incremental kernel
+    RowTable r2 = rows;
+    for (int i = 0; i < n; ++i) r2.p[i] = static_cast<const char*>(rows.p[i]) + done * 2;
+    void* o2 = static_cast<char*>(out) + done * (out_dt == kF32 ? 4 : 2);
+    const int np = t <= 8 ? 8 : (t <= 16 ? 16 : (t <= 32 ? 32 : 64));
+    switch (np) {
+      case 8: launch_bulyan_tail<DT, 8>(r2, n, d - done, beta, W, t, o2, out_dt, s); break;
+      case 16: launch_bulyan_tail<DT, 16>(r2, n, d - done, beta, W, t, o2, out_dt, s); break;
+      case 32: launch_bulyan_tail<DT, 32>(r2, n, d - done, beta, W, t, o2, out_dt, s); break;
+      default: launch_bulyan_tail<DT, 64>(r2, n, d - done, beta, W, t, o2, out_dt, s); break;
+    }
+  }
+  return true;
+}
+
+}  // namespace coord
+}  // namespace gpu
+}  // namespace garfield

@@ -189,6 +189,13 @@ inline bool coord16_enabled() {
   }();
   return on;
 }
+inline bool coord_mfma_tail_enabled() {  // GARFIELD_MFMA_TAIL=0: Bulyan tail without MFMA (A/B runs)
+  static const bool on = [] {
+    const char* e = std::getenv("GARFIELD_MFMA_TAIL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 inline int64_t coord16_grid_cap() {
   static const int64_t cap = [] {
     const char* e = std::getenv("GARFIELD_COORD16_GRID");
@@ -203,6 +210,7 @@ inline int64_t coord16_grid_cap() {
 }  // namespace garfield
 
 #include "gar_coord16.hpp"
+#include "gar_bulyan_tail.hpp"
 
 namespace garfield {
 namespace gpu {
@@ -293,6 +301,18 @@ void launch_coord(const RowTable& rows, int n, int64_t d, int f, int beta, const
   if constexpr (DT != kF32 && coord16_mode<MODE>()) {
     if (coord16_enabled()) {
       launch_coord16<DT, NP, MODE>(rows, n, d, f, beta, seed, thr, out, out_dt, s);
+      return;
+    }
+  }
+  if constexpr (MODE == kBulyanTail && DT != kF32) {
+    if (n <= 64 && coord16_enabled() && coord_mfma_tail_enabled() &&
+        launch_bulyan_tail_mfma<DT>(rows, n, d, beta, W, t, out, out_dt, s))
+      return;
+  }
+  if constexpr ((MODE == kBulyanTail || MODE == kAveragedMedian) && NP <= 64) {
+    const int tt = MODE == kBulyanTail ? t : n;
+    if (n <= 64 && tt - beta <= kTailMaxExcluded && coord16_enabled()) {
+      launch_bulyan_tail<DT, NP>(rows, n, d, beta, MODE == kBulyanTail ? W : nullptr, t, out, out_dt, s);
       return;
     }
   }

@@ -80,20 +80,13 @@ __device__ __forceinline__ float key_val(uint32_t keyword, int h) {
   else return f16_to_f(h ? (w >> 16) : (w & 0xffffu));
 }
 
-// v[idx][q] for a runtime idx as a v_cndmask chain. The empty asm makes each
-// operand opaque: otherwise instcombine folds the select-of-loads back into ONE
-// dynamically indexed load, which pins the whole register array in scratch.
+// v[idx][q] for a wave-uniform runtime idx (scalar branch tree, gar_device.hpp).
 template <int NP, int P>
 __device__ __forceinline__ uint32_t pick_word(const uint32_t (&v)[NP][P], int q, int idx) {
-  uint32_t r = v[0][q];
-  asm("" : "+v"(r));
+  uint32_t col[NP];
 #pragma unroll
-  for (int i = 1; i < NP; ++i) {
-    uint32_t t = v[i][q];
-    asm("" : "+v"(t));
-    r = (i == idx) ? t : r;
-  }
-  return r;
+  for (int i = 0; i < NP; ++i) col[i] = v[i][q];
+  return pick_uniform(col, idx);  // idx is wave-uniform at every call site
 }
 
 template <int DT, int NP, int P, int MODE>
@@ -281,7 +274,8 @@ __global__ __launch_bounds__(256) void k_coord16(RowTable rows, int n, int64_t d
     }
     float res[VEC];
     if (!bad) {
-      coord16_fast<DT, NP, P, MODE>(v, first, n, f, beta, seed, thr, x, res);
+      coord16_fast<DT, NP, P, MODE>(v, first, opaque_uniform(n), opaque_uniform(f), opaque_uniform(beta), seed, thr,
+                                    x, res);
     } else {  // a NaN / inf among this lane's coordinates: exact fp32 per-coordinate path
 #pragma unroll
       for (int c = 0; c < VEC; ++c) res[c] = coord16_rank<DT, MODE>(rows, n, f, beta, seed, thr, x + c);
@@ -297,7 +291,7 @@ __global__ __launch_bounds__(256) void k_coord16(RowTable rows, int n, int64_t d
 template <int NP> struct Coord16Words { static constexpr int P = NP <= 16 ? 4 : (NP == 32 ? 2 : 1); };
 
 template <int MODE> constexpr bool coord16_mode() {
-  return MODE == kMedian || MODE == kTrimmedMean || MODE == kAveragedMedian || MODE == kCondense;
+  return MODE == kMedian || MODE == kTrimmedMean || MODE == kCondense;  // averaged median: gar_bulyan_tail.hpp
 }
 
 template <int DT, int NP, int MODE>

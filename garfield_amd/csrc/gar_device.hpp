@@ -123,6 +123,52 @@ __device__ __forceinline__ float sanitize_inf(float v) {
   return (v == v) ? v : kInf;  // NaN -> +inf (total order for sorting)
 }
 
+// A wave-uniform int re-materialised inside a loop body (volatile asm: never
+// hoisted). Comparisons of unrolled static indices against a loop-invariant
+// uniform bound otherwise become NP hoisted 64-bit lane masks per bound, which
+// spill the SGPR file into VGPR lanes.
+__device__ __forceinline__ int opaque_uniform(int v) {
+  int r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(v));
+  return r;
+}
+
+// v[idx] of a register array for a WAVE-UNIFORM runtime idx: a binary tree of
+// scalar branches ending in one static register read (no select chain, no
+// dynamically indexed — scratch-backed — array).
+template <int LO, int HI, class T, int N>
+__device__ __forceinline__ T pick_uniform_rec(const T (&v)[N], int idx) {
+  if constexpr (HI - LO == 1) {
+    T r = v[LO];
+    asm volatile("" : "+v"(r));
+    return r;
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (idx < MID) return pick_uniform_rec<LO, MID, T, N>(v, idx);
+    return pick_uniform_rec<MID, HI, T, N>(v, idx);
+  }
+}
+template <class T, int N>
+__device__ __forceinline__ T pick_uniform(const T (&v)[N], int idx) {
+  return pick_uniform_rec<0, N, T, N>(v, idx);
+}
+
+// v[idx] for any runtime idx as a v_cndmask chain; the empty asm keeps each operand
+// opaque (otherwise instcombine re-forms ONE dynamically indexed load, which pins
+// the whole array in scratch). Pass an opaque_uniform() idx inside loops.
+template <class T, int N>
+__device__ __forceinline__ T pick_sel(const T (&v)[N], int idx) {
+  T r = v[0];
+  asm("" : "+v"(r));
+#pragma unroll
+  for (int i = 1; i < N; ++i) {
+    T t = v[i];
+    asm("" : "+v"(t));
+    r = (i == idx) ? t : r;
+  }
+  return r;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
