@@ -95,6 +95,9 @@ def parse():
     p.add_argument("--ref-impl", action="store_true",
                    help="also time the reference's algorithms run as-is (BASELINE.md (a)) and report the speedup")
     p.add_argument("--phases", action="store_true", help="report per-phase device time (compute / exchange / GAR)")
+    p.add_argument("--shard-gar", action="store_true",
+                   help="force the sharded, bucketed aggregation even on one GPU (with GARFIELD_LOOPBACK_EXCHANGE=1 "
+                        "the exchange is emulated by side-stream copies: overlap traces)")
     p.add_argument("--lr", type=float, default=0.01,
                    help="0.01: the reference lr (0.2) diverges from random init on the synthetic data")
     return p.parse_args()
@@ -146,7 +149,8 @@ def main():
     cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                        weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
                        cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=not a.no_lp_weights,
-                       worker_batching=False if a.no_worker_batching else None)
+                       worker_batching=False if a.no_worker_batching else None,
+                       shard_gar=True if a.shard_gar else None)
     eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
     batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
                                 seed=1000 + ctx.rank, channels_last=a.channels_last)

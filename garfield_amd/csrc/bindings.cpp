@@ -692,7 +692,55 @@ void def_rows(py::module& m, const char* name, Fn2d&& f2d, FnList&& flist, const
 
 }  // namespace
 
+// Stream-ordered signals for waiting on a point INSIDE a captured HIP graph
+// (hipEventRecordExternal is rejected during capture on ROCm 7, and torch refuses
+// Event(external=True) there). A 1-thread kernel captured in the graph stores 1 to an
+// 8-byte signal word (system-scope release, a vector store); another stream waits
+// with hipStreamWaitValue64 (a command-processor wait: no spinning kernel) and
+// re-arms the word with hipStreamWriteValue64.
+int64_t signal_alloc(int64_t count) {
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, static_cast<size_t>(8 * count), hipMallocSignalMemory) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  (void)hipMemset(p, 0, static_cast<size_t>(8 * count));
+  (void)hipDeviceSynchronize();
+  return reinterpret_cast<int64_t>(p);
+}
+void signal_free(int64_t p) { (void)hipFree(reinterpret_cast<void*>(p)); }
+bool signal_wait_supported(int64_t device) {
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, static_cast<int>(device)) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return v != 0;
+}
+void signal_set(int64_t p, int64_t value, int64_t stream) {
+  garfield::gpu::signal_set(reinterpret_cast<void*>(p), static_cast<uint64_t>(value),
+                            reinterpret_cast<hipStream_t>(stream));
+  TORCH_CHECK(hipGetLastError() == hipSuccess, "garfield: signal_set launch failed");
+}
+void stream_wait_value(int64_t stream, int64_t p, int64_t value) {
+  TORCH_CHECK(hipStreamWaitValue64(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<void*>(p),
+                                   static_cast<uint64_t>(value), hipStreamWaitValueGte,
+                                   0xFFFFFFFFFFFFFFFFull) == hipSuccess,
+              "garfield: hipStreamWaitValue64 failed");
+}
+void stream_write_value(int64_t stream, int64_t p, int64_t value) {
+  TORCH_CHECK(hipStreamWriteValue64(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<void*>(p),
+                                    static_cast<uint64_t>(value), 0) == hipSuccess,
+              "garfield: hipStreamWriteValue64 failed");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("signal_alloc", &signal_alloc, py::arg("count"));
+  m.def("signal_free", &signal_free);
+  m.def("signal_wait_supported", &signal_wait_supported, py::arg("device"));
+  m.def("signal_set", &signal_set, py::arg("ptr"), py::arg("value"), py::arg("stream"));
+  m.def("stream_wait_value", &stream_wait_value, py::arg("stream"), py::arg("ptr"), py::arg("value"));
+  m.def("stream_write_value", &stream_write_value, py::arg("stream"), py::arg("ptr"), py::arg("value"));
   m.doc() = "Garfield-MI355X native robust-aggregation kernels (gfx950 HIP + C++ thread pool)";
   m.attr("MAX_ROWS") = garfield::kMaxRows;
   m.attr("MODE_MEDIAN") = static_cast<int>(garfield::kMedian);

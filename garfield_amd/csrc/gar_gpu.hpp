@@ -70,5 +70,8 @@ constexpr int kMaxFlatTensors = 96;  // tensors per launch (kernarg budget); mor
 int flatten_cast(const void* const* srcs, const int* src_dts, const int64_t* numels, const int64_t* offsets,
                  int count, void* dst, int out_dt, hipStream_t stream);
 
+// ---- Stream signal: 1-thread kernel storing `value` (system-scope release) ----
+void signal_set(void* p, uint64_t value, hipStream_t stream);
+
 }  // namespace gpu
 }  // namespace garfield

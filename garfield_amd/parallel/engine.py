@@ -175,7 +175,8 @@ class RobustDataParallel:
         if self._sharded:
             from garfield_amd.parallel.sharded import ShardedAggregator
 
-            self._shard = ShardedAggregator(self)
+            bounds = self._gexec.bucket_offsets() if self._gexec is not None else ()
+            self._shard = ShardedAggregator(self, bounds)
 
     # ------------------------------------------------------------------ #
 
@@ -223,7 +224,10 @@ class RobustDataParallel:
         offsets = {id(p): off for p, off in zip(self.work_params, self.flat.offsets)}
         nrow = self.X.shape[1]
         sink = GradSink(self.X.view(-1), nrow * self.ld, self.xr * self.ld, offsets, self.k)
-        self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn)
+        # bucket marks (sharded multi-rank exchange): the backward records an event when
+        # it has written the gradients of layer4 + fc, then of layer3
+        marks = ("layer4", "layer3") if self._sharded else ()
+        self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn, marks=marks, offsets=offsets)
         self._gx = self._gy = None
         self._gsrc = None
         self._gsrc_refs = None
@@ -269,6 +273,9 @@ class RobustDataParallel:
     def sync_shadow(self) -> None:
         """Refresh the low-precision working weights from the fp32 master weights
         (only needed after the master buffer is written outside the update kernel)."""
+        shard = getattr(self, "_shard", None)
+        if shard is not None:
+            shard.master_stale = False   # the whole master was just written
         if self._shadow is not None:
             with torch.no_grad():
                 self._shadow.copy_(self.flat.data)
@@ -313,18 +320,11 @@ class RobustDataParallel:
                 loss = self.loss_fn(self.model(x), y)
                 loss.backward()
                 losses.append(loss.detach())
-                row = self.X[j, self.xr, : self.d]
-                attack = self.cfg.byzantine.get(self.slot(j))
-                if attack is None:
-                    self._write_row(row)
-                else:
-                    g = self._grad_vector()
-                    est = None
-                    if attack in NEEDS_ESTIMATES:
-                        honest = [self.X[i, self.xr, : self.d] for i in self.local_slots
-                                  if self.slot(i) not in self.cfg.byzantine and i != j]
-                        est = torch.stack([g] + [h.float() for h in honest])
-                    row.copy_(apply_attack(attack, g, est, self._gen))
+                # the honest gradient goes into the row; a Byzantine slot's row is then
+                # attacked from it (sharded: at exchange time, bucket by bucket)
+                self._write_row(self.X[j, self.xr, : self.d])
+                if self._shard is None:
+                    self._attack_rows(0, self.d, (j,))
                 works += issue.ready(j)
         for p in params:
             p.grad = None
@@ -353,7 +353,7 @@ class RobustDataParallel:
         cfg = self.cfg
         first = self.step_count == 0
         if self._shard is not None:
-            self._shard.aggregate_and_update(first)
+            self._shard.aggregate_and_update(first)   # starts the exchange unless already started
             self.step_count += 1
             return
         rule = cfg.gar
@@ -533,14 +533,41 @@ class RobustDataParallel:
                 self._ggraph.replay()
             else:
                 self._gexec.run(self._gx, self._gy, self._gloss)
-            self._attack_local_rows()
-            works = [w for w in (self._gather_slot(j) for j in range(self.k)) if w is not None]
+            if self._shard is not None:   # buckets leave as the backward finishes them
+                self._shard.start_exchange(self._gexec.mark_events())
+            else:
+                self._attack_local_rows()
+                works = [w for w in (self._gather_slot(j) for j in range(self.k)) if w is not None]
         with self.timer.phase("exchange_wait"):
             for w in works:
                 w.wait()
         with self.timer.phase("gar_update"):
             self.aggregate_and_update()
         return self._gloss.mean()
+
+    _DEFAULT_GEN = object()
+
+    def _attack_rows(self, lo: int, hi: int, slots=None, gen=_DEFAULT_GEN) -> None:
+        """Simulated Byzantine workers of this rank (``slots``: local worker ids, default
+        all), on coordinates [lo, hi) of their rows, which hold their honest gradient.
+        Every attack is coordinate-wise; colluders estimate from the honest rows' slices."""
+        cfg = self.cfg
+        hi = min(hi, self.d)
+        if lo >= hi or not cfg.byzantine:
+            return
+        gen = self._gen if gen is RobustDataParallel._DEFAULT_GEN else gen
+        for j in (self.local_slots if slots is None else slots):
+            attack = cfg.byzantine.get(self.slot(j))
+            if attack is None:
+                continue
+            row = self.X[j, self.xr, lo:hi]
+            g = row.float()
+            est = None
+            if attack in NEEDS_ESTIMATES:
+                honest = [self.X[i, self.xr, lo:hi] for i in self.local_slots
+                          if self.slot(i) not in cfg.byzantine and i != j]
+                est = torch.stack([g] + [h.float() for h in honest])
+            row.copy_(apply_attack(attack, g, est, gen))
 
     def _attack_local_rows(self) -> None:
         """Overwrite the simulated Byzantine workers' rows (after the honest rows exist)."""
@@ -582,6 +609,7 @@ class RobustDataParallel:
             warning(f"HIP graph capture of the grouped step failed, running eagerly: {e!r}")
             self._graph_failed = True
             self._ggraph = None
+        self._gexec.reset_marks(torch.cuda.current_stream(self.device))   # the warm-up pass set them
         torch.cuda.synchronize()
         with torch.no_grad():  # the warm-up pass must not count as an extra step of the running statistics
             for m, (rm, rv) in zip(bns, saved):
@@ -598,18 +626,9 @@ class RobustDataParallel:
             loss = self.loss_fn(self.model(x), y)
         loss.backward()
         loss_out.copy_(loss.detach().float())
-        row = self.X[j, self.xr, : self.d]
-        attack = self.cfg.byzantine.get(self.slot(j))
-        if attack is None:
-            self._write_row(row)
-        else:
-            g = self._grad_vector()
-            est = None
-            if attack in NEEDS_ESTIMATES:
-                honest = [self.X[i, self.xr, : self.d] for i in self.local_slots
-                          if self.slot(i) not in self.cfg.byzantine and i != j]
-                est = torch.stack([g] + [h.float() for h in honest])
-            row.copy_(apply_attack(attack, g, est, None))
+        self._write_row(self.X[j, self.xr, : self.d])
+        if self._shard is None:
+            self._attack_rows(0, self.d, (j,), gen=None)   # captured: deterministic attacks only
         for p in self.work_params:
             p.grad = None
 
@@ -661,11 +680,20 @@ class RobustDataParallel:
 
     # ------------------------------------------------------------------ #
 
+    def sync_master(self) -> None:
+        """Collective in sharded multi-rank runs: refresh the fp32 master weights outside
+        this rank's shards (the step all-gathers the bf16 working weights only)."""
+        if self._shard is not None:
+            self._shard.sync_master()
+
     def flat_model(self) -> torch.Tensor:
-        """Reference-layout flat parameter vector (a view; clone to keep)."""
+        """Reference-layout flat parameter vector (a view; clone to keep). Collective in
+        sharded multi-rank runs (see ``sync_master``)."""
+        self.sync_master()
         return self.flat.vector()
 
     def replica_checksum(self) -> float:
+        self.sync_master()
         return float(self.flat.vector().double().sum())
 
     @torch.no_grad()

@@ -50,7 +50,8 @@ class GroupedResNet:
     channels_last) and labels, writes every worker's parameter gradient into its
     exchange row through ``sink`` and returns the per-worker mean losses."""
 
-    def __init__(self, model: ResNet, groups: int, sink: GradSink, loss_fn=F.cross_entropy):
+    def __init__(self, model: ResNet, groups: int, sink: GradSink, loss_fn=F.cross_entropy, marks=(),
+                 offsets: dict | None = None):
         if not supports(model):
             raise ValueError("GroupedResNet supports the zoo's ResNet models only")
         self.model = model
@@ -62,6 +63,39 @@ class GroupedResNet:
         self.fc = LinearSpec(model.fc, sink, self.groups)
         self.bn: dict = {}
         self.join_residuals = True
+        # bucket marks: the backward records an event when it has produced every
+        # gradient of the named layer and the layers after it (the exchange of that
+        # bucket can start). External events: inside a captured HIP graph they become
+        # event-record nodes that each replay records.
+        self.marks = tuple(marks)
+        self._offsets = offsets or {}
+        self._events = None
+        if self.marks and next(model.parameters()).is_cuda:
+            dev = next(model.parameters()).device
+            sig = {name: GraphSignal(dev) for name in self.marks}
+            if all(x.available() for x in sig.values()):
+                self._events = sig
+
+    def bucket_offsets(self) -> list:
+        """Flat offset where each marked layer's parameters start (bucket boundaries)."""
+        out = []
+        for name in self.marks:
+            layer = getattr(self.model, name)
+            offs = [self._offsets[id(p)] for p in layer.parameters() if id(p) in self._offsets]
+            if offs:
+                out.append(min(offs))
+        return out
+
+    def mark_events(self):
+        """Signals in the order the backward records them (= the marks' order), or None."""
+        if self._events is None:
+            return None
+        return [self._events[name] for name in self.marks]
+
+    def reset_marks(self, stream) -> None:
+        if self._events is not None:
+            for sgn in self._events.values():
+                sgn.reset(stream)
 
     # ------------------------------------------------------------------ #
 
@@ -97,8 +131,10 @@ class GroupedResNet:
         x = self._bn(self._conv(x, m.conv1), m.bn1, True)
         if isinstance(m.maxpool, nn.MaxPool2d):
             x = grouped_maxpool(x, m.maxpool)
-        for layer in (m.layer1, m.layer2, m.layer3, m.layer4):
-            for blk in layer:
+        for name in ("layer1", "layer2", "layer3", "layer4"):
+            if self._events is not None and name in self._events:
+                x = _BucketMark.apply(x, self._events[name])
+            for blk in getattr(m, name):
                 x = self._block(blk, x)
         self.ws.flush_running()
         n, c, h, w = x.shape
@@ -127,3 +163,64 @@ class GroupedResNet:
         if loss_out is not None:
             loss_out.copy_(per)
         return per
+
+
+class GraphSignal:
+    """A point inside the step's HIP graph that another stream can wait for.
+
+    ``record(stream)`` launches a 1-thread kernel (captured into the graph like any
+    other) that stores 1 to an 8-byte signal word; ``wait_on(stream)`` enqueues a
+    command-processor wait for that word (``hipStreamWaitValue64``) and re-arms it
+    to 0 behind the wait, so every step's wait matches that step's record. (HIP
+    rejects external event-record nodes during capture, and torch refuses
+    ``Event(external=True)`` on ROCm.) ``available()`` is False when the device
+    cannot wait on a value: callers then wait for the whole stream instead."""
+
+    _supported: dict = {}
+
+    def __init__(self, device: torch.device):
+        from garfield_amd import _native
+
+        self._C = _native.native()
+        dev = device.index if device.index is not None else torch.cuda.current_device()
+        if dev not in GraphSignal._supported:
+            GraphSignal._supported[dev] = bool(self._C.signal_wait_supported(dev))
+        self.ptr = self._C.signal_alloc(1) if GraphSignal._supported[dev] else 0
+
+    def available(self) -> bool:
+        return self.ptr != 0
+
+    def record(self, stream) -> None:
+        if self.ptr:
+            self._C.signal_set(self.ptr, 1, stream.cuda_stream)
+
+    def wait_on(self, stream) -> None:
+        self._C.stream_wait_value(stream.cuda_stream, self.ptr, 1)
+        self._C.stream_write_value(stream.cuda_stream, self.ptr, 0)
+
+    def reset(self, stream) -> None:
+        """Re-arm after executions nobody waited for (warm-up / capture passes)."""
+        if self.ptr:
+            self._C.stream_write_value(stream.cuda_stream, self.ptr, 0)
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                self._C.signal_free(self.ptr)
+        except Exception:
+            pass
+
+
+class _BucketMark(torch.autograd.Function):
+    """Identity whose backward records ``event`` (a GraphSignal) on the current stream:
+    by then the backward has produced every gradient of the layers after this point."""
+
+    @staticmethod
+    def forward(ctx, x, event):
+        ctx.event = event
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        ctx.event.record(torch.cuda.current_stream(dy.device))
+        return dy, None

@@ -1,4 +1,4 @@
-"""Sharded robust aggregation: every rank aggregates 1/world of the coordinates.
+"""Sharded, bucketed robust aggregation: every rank aggregates 1/world of the coordinates.
 
 The redundant form of the engine (``engine.RobustDataParallel`` with
 ``shard_gar=False``) all-gathers every worker's full gradient to every rank, so
@@ -10,28 +10,40 @@ Every rule the engine runs is either coordinate-wise or decides from per-pair
 squared distances, and squared distances are additive over coordinate blocks:
 ``||g_i - g_j||^2 = sum_s ||g_i^(s) - g_j^(s)||^2``. So, per step:
 
-1. ``all_to_all_single``: rank r receives coordinate shard r of all n gradients
-   (``k * d * (world-1)/world`` values out and in per rank, ~8x less than the
-   all-gather at 8 GPUs);
-2. distance-based rules (Krum/Multi-Krum, Bulyan's selection, Brute): each rank
-   computes the partial Gram matrix of its shard (split-K MFMA kernel), the
-   ``[n, n]`` partials are all-gathered (a few KB) and summed in rank order, so
-   every rank sees the same matrix and makes the same selection; Aksel does the
-   same with its per-row distances to the coordinate-wise median;
-3. the combine / coordinate-wise kernel and the fused SGD update run on the
-   shard only (fp32 master shard, momentum shard: optimizer state is sharded);
-4. ``all_gather_into_tensor`` of the updated fp32 master shards; the bf16 working
-   weights are re-cast locally.
+1. the flat vector is cut into BUCKETS at layer boundaries, in the order the
+   backward finishes them (layer4 + fc first: 64% of ResNet-50's parameters);
+   each bucket is cut into ``world`` equal shards and rank r owns shard r of
+   every bucket;
+2. a bucket is exchanged as soon as the backward has written it: the grouped
+   executor records an event when its backward crosses the bucket boundary
+   (an external event node inside the HIP graph), a side stream waits on it,
+   applies the simulated attacks to that slice and issues one zero-copy
+   ``all_to_all_single`` per local worker row (row slice in, ``[world, S_b]``
+   out) -- so most of the exchange runs under the rest of the backward;
+3. distance-based rules (Krum/Multi-Krum, Bulyan's selection, Brute): each rank
+   adds the partial Gram matrices of its shards (split-K MFMA kernel, one per
+   bucket as it lands), the ``[n, n]`` partials are all-gathered (a few KB) and
+   summed in rank order, so every rank sees the same matrix and makes the same
+   selection; Aksel does the same with its per-row distances to the median;
+4. the combine / coordinate-wise kernel and the fused SGD update run bucket by
+   bucket on the owned shard (fp32 master shard, momentum shard: optimizer state
+   is sharded) and write the bf16 working weights of the shard in the same pass;
+5. the updated bf16 working weights are all-gathered per bucket (2 bytes per
+   parameter, not the 4-byte fp32 master); the few fp32 parameters the
+   forward reads directly (BatchNorm affine) travel in one small all-reduce.
+   The fp32 master outside the owned shards is refreshed lazily
+   (``sync_master``) for checkpoints and the reference-layout flat vector.
 
-Replicas stay bit-identical (they all receive the same all-gathered master).
+Replicas stay bit-identical (same gathered bytes everywhere).
 Reference: the PS pull/aggregate/push loop of ``garfieldpp/server.py:112-159`` and
-Garfield_CC's per-tensor gather/broadcast (``Garfield_CC/trainer.py:55-207``).
-Condense draws its per-coordinate coin with the shard-local coordinate index, so
-its mask differs from the unsharded run's (same Bernoulli(p) law).
+Garfield_CC's per-tensor gather/broadcast (``Garfield_CC/trainer.py:55-207,
+288-314``). Condense draws its per-coordinate coin with the shard-local coordinate
+index, so its mask differs from the unsharded run's (same Bernoulli(p) law).
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -50,39 +62,134 @@ def shard_pad(world: int, base: int = 64) -> int:
     return base * world
 
 
-class ShardedAggregator:
-    """All-to-all of the local gradient rows, sharded GAR, sharded SGD, all-gather."""
+def overlap_enabled() -> bool:
+    """GARFIELD_OVERLAP=0: exchange after the whole backward (A/B runs, debugging)."""
+    return os.environ.get("GARFIELD_OVERLAP", "1") != "0"
 
-    def __init__(self, engine):
+
+class _Bucket:
+    def __init__(self, lo: int, hi: int, world: int, rank: int, k: int, dev, dt):
+        self.lo, self.hi = lo, hi
+        self.S = (hi - lo) // world
+        self.own = slice(lo + rank * self.S, lo + (rank + 1) * self.S)
+        # recv[j, src] = shard `rank` of source rank src's local worker j
+        self.recv = torch.empty((k, world, self.S), dtype=dt, device=dev) if world > 1 else None
+        self.moff = 0          # offset of this bucket's shard in the momentum buffer
+        self.works: list = []
+        self.rows: list = []
+        self.gagg = None
+
+
+class ShardedAggregator:
+    """Bucketed all-to-all of the local gradient rows, sharded GAR, sharded SGD,
+    all-gather of the working weights (see the module docstring)."""
+
+    def __init__(self, engine, boundaries=()):
         e = engine
         self.e = e
         self.world, self.rank, self.k, self.n = e.world, e.rank, e.k, e.n
         if e.ld % self.world:
             raise ValueError("sharded aggregation needs the row length padded to a multiple of the world size")
-        self.S = e.ld // self.world
+        align = shard_pad(self.world)
+        cuts = sorted({min(e.ld, ((int(b) + align - 1) // align) * align) for b in boundaries} - {0, e.ld})
+        edges = [0, *cuts, e.ld]
         dev, dt = e.device, e.X.dtype
-        self.send = torch.empty((self.world, self.k, self.S), dtype=dt, device=dev)
-        self.recv = torch.empty((self.world, self.k, self.S), dtype=dt, device=dev)
-        # slot j * world + src  ->  recv[src, j]  (the unsharded engine's row order)
-        self.rows = [self.recv[s % self.world, s // self.world] for s in range(self.n)]
-        self.lo = self.rank * self.S
-        self.sl = slice(self.lo, self.lo + self.S)
-        self.gagg = torch.zeros(self.S, dtype=torch.float32, device=dev)
+        # ready order of the backward: highest coordinates (last layers) first
+        self.buckets = [_Bucket(edges[i], edges[i + 1], self.world, self.rank, self.k, dev, dt)
+                        for i in reversed(range(len(edges) - 1))]
+        off = 0
+        for b in sorted(self.buckets, key=lambda b: b.lo):
+            b.moff = off
+            off += b.S
+        self.S = off                                   # owned coordinates = ld / world
+        for b in self.buckets:
+            b.rows = self._rows_of(b)
         self._one = torch.ones(1, dtype=torch.float32, device=dev)
-        self._ws = None
         self._avg = torch.full((self.n,), 1.0 / self.n, dtype=torch.float32, device=dev)
+        self._ws = {}
+        self._started = False
+        self._gathers: list = []
+        self.master_stale = False
+        self._comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self._init_fp32_sync()
 
     # ------------------------------------------------------------------ #
+    # layout
 
-    def exchange(self) -> None:
-        """all_to_all: shard s of every local row goes to rank s."""
+    def _rows_of(self, b: _Bucket) -> list:
+        """Row (global slot j * world + src) -> its shard of bucket b, in slot order."""
         e = self.e
-        local = e.X.view(self.k, self.world, self.S)
-        if self.world == 1:   # single rank (tests): the shard is the whole row
-            self.recv.copy_(local.transpose(0, 1))
+        if self.world == 1:
+            return [e.X[j, 0, b.lo:b.hi] for j in range(self.k)]
+        return [b.recv[s // self.world, s % self.world] for s in range(self.n)]
+
+    def _init_fp32_sync(self) -> None:
+        """fp32 parameters the forward reads directly (not mirrored by the bf16 working
+        weights): their owned values travel in one all-reduce of a compact vector."""
+        e = self.e
+        self._np_idx = None
+        if e._shadow is None or self.world == 1:
             return
-        self.send.copy_(local.transpose(0, 1))
-        dist.all_to_all_single(self.recv.view(-1), self.send.view(-1))
+        lp = {id(p) for p in e.work_params if p.dtype != torch.float32}
+        idx = []
+        for p, wp, off, numel in zip(e.flat.params, e.work_params, e.flat.offsets, e.flat.numels):
+            if id(wp) not in lp:
+                idx.append(torch.arange(off, off + numel))
+        if not idx:
+            return
+        gidx = torch.cat(idx)
+        own = torch.zeros(e.ld, dtype=torch.bool)
+        for b in self.buckets:
+            own[b.own] = True
+        self._np_idx = gidx.to(e.device)
+        self._np_own_pos = torch.nonzero(own[gidx]).flatten().to(e.device)
+        self._np_own_idx = gidx[own[gidx]].to(e.device)
+        self._np_buf = torch.zeros(gidx.numel(), dtype=torch.float32, device=e.device)
+
+    # ------------------------------------------------------------------ #
+    # exchange
+
+    def start_exchange(self, events=None) -> None:
+        """Issue every bucket's all-to-all, in ready order. ``events[i]`` (optional)
+        marks the point of the backward where bucket i's rows are complete; the
+        side stream waits on it, so the exchange overlaps the rest of the backward."""
+        e = self.e
+        cuda = e.device.type == "cuda"
+        main = torch.cuda.current_stream(e.device) if cuda else None
+        for i, b in enumerate(self.buckets):
+            if cuda:
+                s = self._comm_stream
+                ev = events[i] if (events is not None and i < len(events) and overlap_enabled()) else None
+                if ev is not None:
+                    ev.wait_on(s)      # a point inside the step's graph (grouped.GraphSignal)
+                else:
+                    s.wait_stream(main)
+                ctx = torch.cuda.stream(s)
+            else:
+                ctx = _nullctx()
+            with ctx:
+                e._attack_rows(b.lo, b.hi)
+                b.works = []
+                if self.world > 1:
+                    for j in range(self.k):
+                        src = e.X[j, 0, b.lo:b.hi]
+                        b.works.append(dist.all_to_all_single(b.recv[j].view(-1), src, async_op=True))
+                elif cuda and loopback_enabled():   # world 1: emulate the transfer (traces / tests)
+                    if b.recv is None:
+                        b.recv = torch.empty((self.k, 1, b.S), dtype=e.X.dtype, device=e.device)
+                        b.rows = [b.recv[j, 0] for j in range(self.k)]
+                    b.recv.copy_(e.X[:, :, b.lo:b.hi])
+                if cuda:
+                    b.done = torch.cuda.Event()
+                    b.done.record(s)
+        self._started = True
+
+    def _wait(self, b: _Bucket) -> None:
+        for w in b.works:
+            w.wait()
+        b.works = []
+        if self.e.device.type == "cuda":
+            torch.cuda.current_stream(self.e.device).wait_event(b.done)
 
     def _sum_over_ranks(self, t: torch.Tensor) -> torch.Tensor:
         """Every rank's ``t`` summed in rank order (identical result on every rank)."""
@@ -103,105 +210,188 @@ class ShardedAggregator:
 
     def aggregate_and_update(self, first: bool) -> None:
         e, cfg = self.e, self.e.cfg
-        self.exchange()
+        if not self._started:
+            self.start_exchange()
         if e.device.type == "cuda":
             self._gpu(cfg, first)
         else:
             self._cpu(cfg, first)
-        self._gather_master()
+        self._started = False
+        self._gather_weights()
 
-    def _gather_master(self) -> None:
+    def _gather_weights(self) -> None:
+        """All-gather the updated parameters per bucket: the bf16 working weights (and
+        the compact fp32 parameters) when the forward reads those, else the fp32 master."""
         e = self.e
-        full = e.flat.data
-        if self.world > 1:
-            mine = full[self.sl]
+        if self.world == 1:
+            if e._shadow is not None and e.device.type != "cuda":
+                with torch.no_grad():
+                    e._shadow.copy_(e.flat.data)
+            return
+        lp = e._shadow is not None
+        buf = e._shadow if lp else e.flat.data
+        for b in sorted(self.buckets, key=lambda b: b.lo):   # the next forward reads low coordinates first
+            full, mine = buf[b.lo:b.hi], buf[b.own]
             if full.device.type == "cpu":
                 mine = mine.clone()  # gloo rejects an input aliasing the output
             dist.all_gather_into_tensor(full, mine)
-        if e._shadow is not None:
-            with torch.no_grad():
-                e._shadow.copy_(full)
+        if lp:
+            self.master_stale = True
+            if self._np_idx is not None:
+                nb = self._np_buf
+                nb.zero_()
+                nb[self._np_own_pos] = e.flat.data[self._np_own_idx]
+                dist.all_reduce(nb)
+                e.flat.data[self._np_idx] = nb
+
+    def sync_master(self) -> None:
+        """Collective: refresh the fp32 master outside this rank's shards (checkpoints,
+        the reference-layout flat vector). Every rank must call it."""
+        if not self.master_stale or self.world == 1:
+            self.master_stale = False
+            return
+        data = self.e.flat.data
+        for b in sorted(self.buckets, key=lambda b: b.lo):
+            mine = data[b.own]
+            if data.device.type == "cpu":
+                mine = mine.clone()
+            dist.all_gather_into_tensor(data[b.lo:b.hi], mine)
+        self.master_stale = False
 
     # ------------------------------------------------------------------ #
-    # GPU: the HIP building blocks on the shard
+    # GPU: the HIP building blocks, bucket by bucket
+
+    def _wsp(self, b: _Bucket):
+        ws = self._ws.get(b.lo)
+        if ws is None:
+            ws = self._ws[b.lo] = gar.Workspace(self.n, b.S, self.e.device)
+        return ws
+
+    def _param(self, b: _Bucket):
+        e = self.e
+        mom = e.mom[b.moff:b.moff + b.S]
+        shadow = e._shadow[b.own] if e._shadow is not None else None
+        return e.flat.data[b.own], mom, shadow
 
     def _gpu(self, cfg, first: bool) -> None:
         e, C = self.e, self.e._C
         rule, f, kw = cfg.gar, cfg.f, dict(cfg.gar_kwargs)
-        rows = gar.prepare(self.rows)
-        if self._ws is None:
-            self._ws = gar.Workspace(self.n, self.S, e.device)
-        ws = self._ws
-        param, mom = e.flat.data[self.sl], e.mom
-        args = (cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
-        if rule in ("average", "krum", "brute", "aksel"):
-            w = self._gpu_weights(C, rows, ws, rule, f, kw)
-            e.last_weights = w
-            C.gpu_combine_sgd(self.rows, w, param, mom, None, None, *args)
-            return
-        g = self.gagg
-        modes = gar._MODE
-        if rule == "bulyan":
-            m = cfg.m if cfg.m is not None else self.n - f - 2
-            t = self.n - 2 * f - 2
-            W = ws.get("bulyan_W", t * self.n)
-            C.gpu_bulyan_select(self._total_gram(C, rows, ws), self.n, f, m, t, W)
-            C.gpu_coordwise(self.rows, modes["bulyan-tail"], f, t - 2 * f, W, t, 0, 1.0, g)
-        elif rule == "median":
-            C.gpu_coordwise(self.rows, modes["median"], 0, 0, None, 0, 0, 1.0, g)
-        elif rule == "trimmed-mean":
-            C.gpu_coordwise(self.rows, modes["trimmed-mean"], f, 0, None, 0, 0, 1.0, g)
-        elif rule == "averaged-median":
-            C.gpu_coordwise(self.rows, modes["averaged-median"], f, kw.get("beta") or self.n - f, None, 0, 0, 1.0, g)
-        elif rule == "average-nan":
-            C.gpu_coordwise(self.rows, modes["average-nan"], 0, 0, None, 0, 0, 1.0, g)
-        elif rule == "condense":
-            C.gpu_coordwise(self.rows, modes["condense"], f, 0, None, 0, cfg.seed + e.step_count,
-                            float(kw.get("p", 0.9)), g)
-        else:
-            raise ValueError(f"sharded aggregation does not support {rule!r}")
-        C.gpu_combine_sgd([g], self._one, param, mom, None, None, *args)
-
-    def _total_gram(self, C, rows, ws) -> torch.Tensor:
-        g = gar._gram_into(C, rows, ws)
-        return self._sum_over_ranks(g)
-
-    def _gpu_weights(self, C, rows, ws, rule, f, kw) -> torch.Tensor:
         n = self.n
-        if rule == "average":
-            return self._avg
-        w = ws.get("weights", n)
+        args = (cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
+        modes = gar._MODE
+        if rule in DISTANCE_RULES or rule == "aksel":
+            total = None
+            slabs = []
+            for b in self.buckets:   # partial statistics as the buckets land
+                self._wait(b)
+                rows = gar.prepare(b.rows)
+                ws = self._wsp(b)
+                if rule == "aksel":
+                    med = ws.get("aksel_med", b.S)
+                    C.gpu_coordwise(b.rows, modes["median"], 0, 0, None, 0, 0, 1.0, med)
+                    grid = C.sqdist_grid(b.S)
+                    sl = ws.get("aksel_slabs", grid * n)
+                    C.gpu_sqdist(b.rows, med, sl)
+                    slabs.append(sl.view(grid, n))
+                else:
+                    g = gar._gram_into(C, rows, ws)
+                    total = g.clone() if total is None else total.add_(g)
+            if rule == "aksel":
+                c = (n + 1) // 2 if kw.get("mode", "mid") == "mid" else n - f
+                allslabs = self._concat_ranks(torch.cat(slabs))
+                w = self._ws_any().get("weights", n)
+                dists = self._ws_any().get("aksel_dists", n)
+                C.gpu_aksel_select(allslabs.contiguous().view(-1), n, c, w, dists)
+            else:
+                total = self._sum_over_ranks(total)
+                w = self._select(C, total, rule, f, cfg)
+            if rule != "bulyan":
+                e.last_weights = w
+                for b in self.buckets:
+                    p, mom, sh = self._param(b)
+                    C.gpu_combine_sgd(b.rows, w, p, mom, None, sh, *args)
+                return
+            t = n - 2 * f - 2
+            for b in self.buckets:
+                g = self._gagg(b)
+                C.gpu_coordwise(b.rows, modes["bulyan-tail"], f, t - 2 * f, w, t, 0, 1.0, g)
+                p, mom, sh = self._param(b)
+                C.gpu_combine_sgd([g], self._one, p, mom, None, sh, *args)
+            return
+        for b in self.buckets:
+            self._wait(b)
+            p, mom, sh = self._param(b)
+            if rule == "average":
+                e.last_weights = self._avg
+                C.gpu_combine_sgd(b.rows, self._avg, p, mom, None, sh, *args)
+                continue
+            g = self._gagg(b)
+            if rule == "median":
+                C.gpu_coordwise(b.rows, modes["median"], 0, 0, None, 0, 0, 1.0, g)
+            elif rule == "trimmed-mean":
+                C.gpu_coordwise(b.rows, modes["trimmed-mean"], f, 0, None, 0, 0, 1.0, g)
+            elif rule == "averaged-median":
+                C.gpu_coordwise(b.rows, modes["averaged-median"], f, kw.get("beta") or n - f, None, 0, 0, 1.0, g)
+            elif rule == "average-nan":
+                C.gpu_coordwise(b.rows, modes["average-nan"], 0, 0, None, 0, 0, 1.0, g)
+            elif rule == "condense":
+                C.gpu_coordwise(b.rows, modes["condense"], f, 0, None, 0, cfg.seed + e.step_count + 7919 * b.lo,
+                                float(kw.get("p", 0.9)), g)
+            else:
+                raise ValueError(f"sharded aggregation does not support {rule!r}")
+            C.gpu_combine_sgd([g], self._one, p, mom, None, sh, *args)
+
+    def _ws_any(self):
+        return self._wsp(self.buckets[0])
+
+    def _gagg(self, b: _Bucket) -> torch.Tensor:
+        if b.gagg is None:
+            b.gagg = torch.zeros(b.S, dtype=torch.float32, device=self.e.device)
+        return b.gagg
+
+    def _select(self, C, gram_total, rule, f, cfg) -> torch.Tensor:
+        n = self.n
+        ws = self._ws_any()
+        m = cfg.m if cfg.m is not None else n - f - 2
         if rule == "krum":
-            m = self.e.cfg.m if self.e.cfg.m is not None else n - f - 2
+            w = ws.get("weights", n)
             order = ws.get("order", n, torch.int32)
             scores = ws.get("scores", n)
-            C.gpu_krum_select(self._total_gram(C, rows, ws), n, f, m, w, order, scores)
-        elif rule == "brute":
+            C.gpu_krum_select(gram_total, n, f, m, w, order, scores)
+            return w
+        if rule == "brute":
             if n > 64:
                 raise ValueError("brute: n must be <= 64 on the GPU")
+            w = ws.get("weights", n)
             best = ws.get("brute_best", 1, torch.int64)
-            C.gpu_brute_select(self._total_gram(C, rows, ws), n, f, best, w)
-        else:  # aksel: distances to the coordinate-wise median, summed over shards
-            c = (n + 1) // 2 if kw.get("mode", "mid") == "mid" else n - f
-            med = ws.get("aksel_med", self.S)
-            C.gpu_coordwise(self.rows, gar._MODE["median"], 0, 0, None, 0, 0, 1.0, med)
-            grid = C.sqdist_grid(self.S)
-            slabs = ws.get("aksel_slabs", grid * n)
-            C.gpu_sqdist(self.rows, med, slabs)
-            allslabs = self._concat_ranks(slabs.view(grid, n))
-            dists = ws.get("aksel_dists", n)
-            C.gpu_aksel_select(allslabs.contiguous().view(-1), n, c, w, dists)
-        return w
+            C.gpu_brute_select(gram_total, n, f, best, w)
+            return w
+        t = n - 2 * f - 2   # bulyan
+        W = ws.get("bulyan_W", t * n)
+        C.gpu_bulyan_select(gram_total, n, f, m, t, W)
+        return W
 
     # ------------------------------------------------------------------ #
-    # CPU (gloo): the same decomposition with the C++ / oracle building blocks
+    # CPU (gloo): the owned shards concatenated, the C++ / oracle building blocks
 
     def _cpu(self, cfg, first: bool) -> None:
         e = self.e
+        for b in self.buckets:
+            self._wait(b)
+        order = sorted(self.buckets, key=lambda b: b.lo)
+        X = torch.cat([torch.stack([r.float() for r in b.rows]) for b in order], dim=1)   # [n, S] owned
+        g = self._cpu_rule(cfg, X)
+        pos = 0
+        for b in order:
+            self._sgd_cpu(b, g[pos:pos + b.S], first)
+            pos += b.S
+
+    def _cpu_rule(self, cfg, X: torch.Tensor) -> torch.Tensor:
+        e = self.e
         rule, f, kw = cfg.gar, cfg.f, dict(cfg.gar_kwargs)
-        X = torch.stack([r.float() for r in self.rows])            # [n, S] shard
         n = self.n
         if rule in DISTANCE_RULES or rule == "aksel":
+            C = _native.require_for(X.device)
             if rule == "aksel":
                 med = gar.aggregate("median", X)
                 part = ((X.double() - med.double()) ** 2).sum(1)
@@ -211,41 +401,35 @@ class ShardedAggregator:
                 order = sorted(range(n), key=lambda j: (float(dist_[j]), j))
                 w = torch.zeros(n, dtype=torch.float32)
                 w[order[:c]] = 1.0 / c
-                C = _native.require_for(X.device)
-                g = C.cpu_combine(X, w) if C is not None else (w[:, None] * X).sum(0)
+                e.last_weights = w
+                return C.cpu_combine(X, w) if C is not None else (w[:, None] * X).sum(0)
+            D = self._sum_over_ranks(gar.pairwise_distances(X))
+            m = cfg.m if cfg.m is not None else n - f - 2
+            if rule == "bulyan":
+                t = n - 2 * f - 2
+                e.last_weights = None
+                if C is not None:
+                    W = C.cpu_bulyan_weights(D, f, m, t)
+                    return C.cpu_coordwise(X, gar._MODE["bulyan-tail"], f, t - 2 * f, W.reshape(-1), t, 0, 1.0)
+                return gar._torch_closest_mean(ref.bulyan_weights(D, f, m).float() @ X, t - 2 * f)
+            if rule == "krum":
+                w = C.cpu_krum_weights(D, f, m)[0] if C is not None else ref.krum_weights(D, f, m).float()
             else:
-                D = self._sum_over_ranks(gar.pairwise_distances(X))
-                m = cfg.m if cfg.m is not None else n - f - 2
-                C = _native.require_for(X.device)
-                if rule == "bulyan":
-                    t = n - 2 * f - 2
-                    if C is not None:
-                        W = C.cpu_bulyan_weights(D, f, m, t)
-                        g = C.cpu_coordwise(X, gar._MODE["bulyan-tail"], f, t - 2 * f, W.reshape(-1), t, 0, 1.0)
-                    else:
-                        g = gar._torch_closest_mean(ref.bulyan_weights(D, f, m).float() @ X, t - 2 * f)
-                    w = None
-                else:
-                    if rule == "krum":
-                        w = C.cpu_krum_weights(D, f, m)[0] if C is not None else ref.krum_weights(D, f, m).float()
-                    else:
-                        w = C.cpu_brute_weights(D, f) if C is not None else ref.brute_weights(D, f).float()
-                    g = C.cpu_combine(X, w) if C is not None else (w[:, None] * X).sum(0)
-            e.last_weights = w if rule != "bulyan" else None
-        elif rule == "average":
-            g = gar.aggregate("average", X).float()
-        else:
-            gkw = dict(kw)
-            if rule not in ("median", "average-nan"):
-                gkw["f"] = f
-            if rule == "condense":
-                gkw.setdefault("seed", cfg.seed + e.step_count)
-            g = gar.aggregate(rule, X, **gkw).float()
-        self._sgd_cpu(g, first)
+                w = C.cpu_brute_weights(D, f) if C is not None else ref.brute_weights(D, f).float()
+            e.last_weights = w
+            return C.cpu_combine(X, w) if C is not None else (w[:, None] * X).sum(0)
+        if rule == "average":
+            return gar.aggregate("average", X).float()
+        gkw = dict(kw)
+        if rule not in ("median", "average-nan"):
+            gkw["f"] = f
+        if rule == "condense":
+            gkw.setdefault("seed", cfg.seed + e.step_count)
+        return gar.aggregate(rule, X, **gkw).float()
 
-    def _sgd_cpu(self, g: torch.Tensor, first: bool) -> None:
+    def _sgd_cpu(self, b: _Bucket, g: torch.Tensor, first: bool) -> None:
         cfg = self.e.cfg
-        p, buf = self.e.flat.data[self.sl], self.e.mom
+        p, buf, _ = self._param(b)
         with torch.no_grad():
             if cfg.weight_decay:
                 g = g + cfg.weight_decay * p
@@ -256,11 +440,40 @@ class ShardedAggregator:
                     buf.mul_(cfg.momentum).add_(g, alpha=1 - cfg.dampening)
                 g = g + cfg.momentum * buf if cfg.nesterov else buf
             p.add_(g, alpha=-cfg.lr)
+            sh = self.e._shadow
+            if sh is not None:
+                sh[b.own].copy_(p)
+
+    # ------------------------------------------------------------------ #
+    # optimizer state in the reference layout (checkpoints)
 
     def momentum_vector(self) -> torch.Tensor:
-        """The full (unsharded) momentum buffer, all-gathered (checkpoints)."""
-        if self.world == 1:
-            return self.e.mom
-        out = torch.empty(self.world * self.S, dtype=self.e.mom.dtype, device=self.e.mom.device)
-        dist.all_gather_into_tensor(out, self.e.mom.clone())
+        """The full (unsharded) momentum buffer, all-gathered (collective)."""
+        e = self.e
+        out = torch.zeros(e.ld, dtype=e.mom.dtype, device=e.mom.device)
+        for b in sorted(self.buckets, key=lambda b: b.lo):
+            mine = e.mom[b.moff:b.moff + b.S].clone()
+            if self.world == 1:
+                out[b.lo:b.hi] = mine
+            else:
+                dist.all_gather_into_tensor(out[b.lo:b.hi], mine)
         return out
+
+    def load_momentum(self, full: torch.Tensor) -> None:
+        e = self.e
+        for b in self.buckets:
+            e.mom[b.moff:b.moff + b.S].copy_(full[b.own])
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def loopback_enabled() -> bool:
+    """GARFIELD_LOOPBACK_EXCHANGE=1 at world 1: copy every bucket into a receive buffer
+    on the side stream, as the all-to-all would (rocprof traces of the overlap, tests)."""
+    return os.environ.get("GARFIELD_LOOPBACK_EXCHANGE", "0") == "1"

@@ -71,6 +71,8 @@ def restore(model: nn.Module, state: dict) -> None:
 def save_engine(path: str, engine, meta: dict | None = None) -> str:
     """Checkpoint of a ``RobustDataParallel`` engine (fp32 master parameters in the
     reference layout, buffers, momentum, step)."""
+    if hasattr(engine, "sync_master"):
+        engine.sync_master()   # collective in sharded runs
     mom = engine.momentum_vector() if hasattr(engine, "momentum_vector") else engine.mom
     return save(path, engine.model, engine.step_count, engine.flat.to_reference(mom), meta,
                 flat=engine.flat.reference_vector())

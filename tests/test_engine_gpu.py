@@ -159,3 +159,32 @@ def test_cuda_graph_never_writes_loader_tensors(cuda):
     assert eng._graph is not None
     for ld, y, x in zip(loaders, y0, x0):
         assert torch.equal(ld.y, y) and torch.equal(ld.x, x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule,f", [("krum", 2), ("median", 1), ("bulyan", 1)])
+def test_bucketed_exchange_overlap_loopback(cuda, rule, f, monkeypatch):
+    """Sharded aggregation with layer buckets on one rank, the exchange emulated by
+    copies on the side stream (GARFIELD_LOOPBACK_EXCHANGE=1) that start when the
+    HIP-graph backward records each bucket's event: fresh inputs every step, so a
+    copy that ran before its bucket was written would read the previous step's
+    gradients. Must equal the redundant (unsharded) path."""
+    monkeypatch.setenv("GARFIELD_LOOPBACK_EXCHANGE", "1")
+    outs = []
+    for shard in (False, True):
+        torch.manual_seed(0)
+        cfg = EngineConfig(gar=rule, f=f, workers_per_rank=8, shard_gar=shard, byzantine={5: "reverse"}, lr=0.01,
+                           cuda_graph=True)
+        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+        if shard:
+            assert eng._gexec is not None and len(eng._shard.buckets) == 3
+            assert eng._gexec.mark_events() is not None
+        for it in range(4):
+            b = synthetic_batches(8, 8, (3, 32, 32), 10, cuda, seed=100 + it)
+            eng.step(b)
+        torch.cuda.synchronize()
+        if shard:
+            assert eng._ggraph is not None
+        outs.append(eng.flat.reference_vector().clone())
+    rel = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
+    assert rel < 1e-5, rel
