@@ -425,7 +425,9 @@ void launch_tail_mfma_ks(int ks, const RowTable& rows, int n, int64_t groups, in
 template <int DT>
 bool launch_bulyan_tail_mfma(const RowTable& rows, int n, int64_t d, int beta, const float* W, int t, void* out,
                              int out_dt, hipStream_t s) {
-  if (DT == kF32 || n > 64 || t > 64 || t - beta > kTailMaxExcluded || W == nullptr) return false;
+  // measured (profiles/r2): the MFMA means win from t > 16 (n = 32: 1.9 vs 2.6 ms, n = 64: 6.5 vs
+  // 10.1 ms per Bulyan call at d = 23.5M); below, the incremental scalar form is faster
+  if (DT == kF32 || n > 64 || t > 64 || t <= 16 || t - beta > kTailMaxExcluded || W == nullptr) return false;
   const int64_t groups = d / 64;
   const int ks = (n + 15) / 16;
   if (groups > 0) {

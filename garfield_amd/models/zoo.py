@@ -36,7 +36,7 @@ class PreActBlock(nn.Module):
         self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
         self.shortcut = None
         if stride != 1 or cin != planes:
-            self.shortcut = nn.Conv2d(cin, planes, 1, stride, bias=False)
+            self.shortcut = nn.Sequential(nn.Conv2d(cin, planes, 1, stride, bias=False))
 
     def forward(self, x):
         out = F.relu(self.bn1(x))
@@ -47,13 +47,17 @@ class PreActBlock(nn.Module):
 
 
 class PreActResNet(nn.Module):
-    def __init__(self, block, blocks, num_classes=10):
+    """Pre-activation ResNet (He et al. 2016): no BatchNorm after the last block, as in
+    the reference ``models/preact_resnet.py`` (same parameter list, so its flat
+    vectors load here)."""
+
+    def __init__(self, block, blocks, num_classes=10, stem_bn=False):
         super().__init__()
         self.cin = 64
         self.conv1 = nn.Conv2d(3, 64, 3, 1, 1, bias=False)
-        self.layers = nn.Sequential(*[self._make(block, w, n, s) for w, n, s in
-                                      zip((64, 128, 256, 512), blocks, (1, 2, 2, 2))])
-        self.bn = nn.BatchNorm2d(512 * block.expansion)
+        self.bn1 = nn.BatchNorm2d(64) if stem_bn else None   # SENet's stem
+        for i, (w, n, s) in enumerate(zip((64, 128, 256, 512), blocks, (1, 2, 2, 2))):
+            setattr(self, f"layer{i + 1}", self._make(block, w, n, s))
         self.linear = nn.Linear(512 * block.expansion, num_classes)
 
     def _make(self, block, planes, n, stride):
@@ -64,7 +68,11 @@ class PreActResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x):
-        out = F.relu(self.bn(self.layers(self.conv1(x))))
+        out = self.conv1(x)
+        if self.bn1 is not None:
+            out = F.relu(self.bn1(out))
+        for i in range(1, 5):
+            out = getattr(self, f"layer{i}")(out)
         return self.linear(F.adaptive_avg_pool2d(out, 1).flatten(1))
 
 
@@ -89,18 +97,24 @@ class SEBlock(PreActBlock):
 
 
 def SENet18(num_classes=10):
-    return PreActResNet(SEBlock, [2, 2, 2, 2], num_classes)
+    """Pre-activation SE blocks behind a conv + BatchNorm stem (reference ``models/senet.py``)."""
+    return PreActResNet(SEBlock, [2, 2, 2, 2], num_classes, stem_bn=True)
 
 
 # ------------------------------------------------------------------ GoogLeNet
 
+def conv_b_bn(cin, cout, k):
+    """conv (with bias, as the reference GoogLeNet) + BatchNorm + ReLU, flattened into the caller."""
+    return [nn.Conv2d(cin, cout, k, 1, (k - 1) // 2), nn.BatchNorm2d(cout), nn.ReLU(True)]
+
+
 class Inception(nn.Module):
     def __init__(self, cin, n1, n3r, n3, n5r, n5, pool):
         super().__init__()
-        self.b1 = conv_bn(cin, n1, 1)
-        self.b2 = nn.Sequential(conv_bn(cin, n3r, 1), conv_bn(n3r, n3, 3))
-        self.b3 = nn.Sequential(conv_bn(cin, n5r, 1), conv_bn(n5r, n5, 3), conv_bn(n5, n5, 3))
-        self.b4 = nn.Sequential(nn.MaxPool2d(3, 1, 1), conv_bn(cin, pool, 1))
+        self.b1 = nn.Sequential(*conv_b_bn(cin, n1, 1))
+        self.b2 = nn.Sequential(*conv_b_bn(cin, n3r, 1), *conv_b_bn(n3r, n3, 3))
+        self.b3 = nn.Sequential(*conv_b_bn(cin, n5r, 1), *conv_b_bn(n5r, n5, 3), *conv_b_bn(n5, n5, 3))
+        self.b4 = nn.Sequential(nn.MaxPool2d(3, 1, 1), *conv_b_bn(cin, pool, 1))
 
     def forward(self, x):
         return torch.cat([self.b1(x), self.b2(x), self.b3(x), self.b4(x)], 1)
@@ -109,7 +123,7 @@ class Inception(nn.Module):
 class GoogLeNet(nn.Module):
     def __init__(self, num_classes=10):
         super().__init__()
-        self.pre = conv_bn(3, 192, 3)
+        self.pre = nn.Sequential(*conv_b_bn(3, 192, 3))
         cfg = [(192, 64, 96, 128, 16, 32, 32), (256, 128, 128, 192, 32, 96, 64), "M",
                (480, 192, 96, 208, 16, 48, 64), (512, 160, 112, 224, 24, 64, 64), (512, 128, 128, 256, 24, 64, 64),
                (512, 112, 144, 288, 32, 64, 64), (528, 256, 160, 320, 32, 128, 128), "M",
@@ -410,21 +424,34 @@ class ShuffleNetV2(nn.Module):
 # ------------------------------------------------------------------ EfficientNet-B0
 
 class MBConv(nn.Module):
+    """Expansion 1x1 -> depthwise kxk -> squeeze-excitation (swish) -> projection 1x1.
+
+    Parameter list as the reference ``models/efficientnet.py`` Block: the expansion
+    conv + BatchNorm exist even when expansion == 1 (unused in the forward), and the
+    SE width is a quarter of the block INPUT channels. The reference computes the
+    drop-connect rate from a block counter it never increments (every rate is 0);
+    ``drop`` keeps that default."""
+
     def __init__(self, cin, cout, expansion, k, stride, se_ratio=0.25, drop=0.0):
         super().__init__()
         hid = cin * expansion
+        self.expansion = expansion
         self.skip = stride == 1 and cin == cout
-        self.expand = conv_bn(cin, hid, 1) if expansion != 1 else nn.Identity()
-        self.dw = nn.Sequential(nn.Conv2d(hid, hid, k, stride, k // 2, groups=hid, bias=False), nn.BatchNorm2d(hid))
-        se = max(1, int(cin * se_ratio))
+        self.conv1 = nn.Conv2d(cin, hid, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(hid)
+        self.conv2 = nn.Conv2d(hid, hid, k, stride, k // 2, groups=hid, bias=False)
+        self.bn2 = nn.BatchNorm2d(hid)
+        se = int(cin * se_ratio)
         self.se1, self.se2 = nn.Conv2d(hid, se, 1), nn.Conv2d(se, hid, 1)
-        self.project = conv_bn(hid, cout, 1, act=False)
+        self.conv3 = nn.Conv2d(hid, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
         self.drop = drop
 
     def forward(self, x):
-        out = F.silu(self.dw(self.expand(x)))
+        out = x if self.expansion == 1 else F.silu(self.bn1(self.conv1(x)))
+        out = F.silu(self.bn2(self.conv2(out)))
         out = out * torch.sigmoid(self.se2(F.silu(self.se1(F.adaptive_avg_pool2d(out, 1)))))
-        out = self.project(out)
+        out = self.bn3(self.conv3(out))
         if self.skip:
             if self.training and self.drop > 0:
                 keep = torch.rand(x.shape[0], 1, 1, 1, device=x.device) >= self.drop
@@ -437,22 +464,22 @@ class EfficientNetB0(nn.Module):
     CFG = [(1, 16, 1, 3, 1), (6, 24, 2, 3, 2), (6, 40, 2, 5, 2), (6, 80, 3, 3, 2), (6, 112, 3, 5, 1),
            (6, 192, 4, 5, 2), (6, 320, 1, 3, 1)]
 
-    def __init__(self, num_classes=10):
+    def __init__(self, num_classes=10, drop_connect=0.0):
         super().__init__()
-        self.stem = nn.Sequential(nn.Conv2d(3, 32, 3, 1, 1, bias=False), nn.BatchNorm2d(32), nn.SiLU())
+        self.conv1 = nn.Conv2d(3, 32, 3, 1, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(32)
         cin, layers = 32, []
         total = sum(c[2] for c in self.CFG)
         b = 0
         for t, c, n, k, s in self.CFG:
             for i in range(n):
-                layers.append(MBConv(cin, c, t, k, s if i == 0 else 1, drop=0.2 * b / total))
+                layers.append(MBConv(cin, c, t, k, s if i == 0 else 1, drop=drop_connect * b / total))
                 cin, b = c, b + 1
-        self.blocks = nn.Sequential(*layers)
-        self.head = nn.Sequential(nn.Conv2d(cin, 1280, 1, bias=False), nn.BatchNorm2d(1280), nn.SiLU())
-        self.linear = nn.Linear(1280, num_classes)
+        self.layers = nn.Sequential(*layers)
+        self.linear = nn.Linear(cin, num_classes)
 
     def forward(self, x):
-        out = self.head(self.blocks(self.stem(x)))
+        out = self.layers(F.silu(self.bn1(self.conv1(x))))
         return self.linear(F.dropout(F.adaptive_avg_pool2d(out, 1).flatten(1), 0.2, self.training))
 
 
