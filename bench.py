@@ -98,6 +98,8 @@ def parse():
     p.add_argument("--shard-gar", action="store_true",
                    help="force the sharded, bucketed aggregation even on one GPU (with GARFIELD_LOOPBACK_EXCHANGE=1 "
                         "the exchange is emulated by side-stream copies: overlap traces)")
+    p.add_argument("--checkpoint", default="", help="save a checkpoint here after the timed steps (untimed)")
+    p.add_argument("--resume", default="", help="restore this checkpoint file before the warm-up")
     p.add_argument("--lr", type=float, default=0.01,
                    help="0.01: the reference lr (0.2) diverges from random init on the synthetic data")
     return p.parse_args()
@@ -154,7 +156,15 @@ def main():
     eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
     batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
                                 seed=1000 + ctx.rank, channels_last=a.channels_last)
+    if a.resume:
+        from garfield_amd.utils.checkpoint import load_engine
+
+        load_engine(a.resume, eng)
     elapsed, loss = timed_steps(eng, batches, a.steps, a.warmup, ctx)
+    if a.checkpoint:
+        from garfield_amd.utils.checkpoint import save_engine
+
+        save_engine(a.checkpoint, eng, meta={"bench": vars(a)}, write=ctx.rank == 0)
     n = eng.n
     imgs = n * a.batch * a.steps
     value = imgs / elapsed

@@ -34,6 +34,7 @@ from garfield_amd.models import build_model
 from garfield_amd.parallel.byzps import ByzantinePSDataParallel, ByzPSConfig
 from garfield_amd.parallel.comm import init_distributed, shutdown
 from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel
+from garfield_amd.utils.checkpoint import Checkpoints
 from garfield_amd.utils.logging import info, set_rank_prefix
 
 
@@ -66,6 +67,10 @@ def parse(argv=None):
     p.add_argument("--bench", type=str2bool, default=False)
     p.add_argument("--log", type=str2bool, default=False)
     p.add_argument("--acc_freq", type=int, default=0)
+    p.add_argument("--checkpoint", default="", help="checkpoint directory (reference-layout flat vector + "
+                   "momentum + BatchNorm buffers; utils/checkpoint.py)")
+    p.add_argument("--checkpoint_freq", type=int, default=0, help="save every this many iterations (0: at the end)")
+    p.add_argument("--resume", type=str2bool, default=False, help="restore the newest checkpoint of --checkpoint")
     return p.parse_args(argv)
 
 
@@ -117,9 +122,16 @@ def main(argv=None, results: dict | None = None):
         loaders.append(mgr.get_train_set())
     test = DatasetManager(a.dataset, a.batch, 1, 1, 0, device=ctx.device).get_test_set()
     iters = a.num_iter or a.epochs * min(len(ld) for ld in loaders)
+    ck = Checkpoints(a.checkpoint) if a.checkpoint else None
+    start = 0
+    if ck is not None and a.resume and ck.latest() is not None:
+        ck.restore(eng)
+        start = eng.step_count
+        if ctx.rank == 0:
+            info(f"resumed from {ck.path(start)} (iteration {start})")
     t0 = time.time()
     loss = None
-    for i in range(iters):
+    for i in range(start, iters):
         batches = [ld[i] for ld in loaders]
         ts = time.perf_counter()
         loss = eng.step(batches)
@@ -131,11 +143,17 @@ def main(argv=None, results: dict | None = None):
             info(f"iteration {i} loss {float(loss):.4f}")
         if a.acc_freq and (i % a.acc_freq == 0 or i == iters - 1) and ctx.rank == 0:
             info(f"iteration {i} accuracy {eng.evaluate(test, binary=ncls == 1):.2f} time {time.time() - t0:.1f}s")
+        if ck is not None and a.checkpoint_freq and (i + 1) % a.checkpoint_freq == 0:
+            ck.save(eng, write=ctx.rank == 0)   # every rank: collectives of the sharded engine
+    if ck is not None and not a.checkpoint_freq:
+        ck.save(eng, write=ctx.rank == 0)
     acc = eng.evaluate(test, binary=ncls == 1)
+    checksum = eng.replica_checksum()   # collective in sharded runs
     if ctx.rank == 0:
         info(f"final accuracy {acc:.2f} after {iters} iterations ({time.time() - t0:.1f}s)")
+        info(f"replica checksum {checksum:.12e}")
     if results is not None:
-        results.update(accuracy=acc, checksum=eng.replica_checksum(), loss=float(loss) if loss is not None else None)
+        results.update(accuracy=acc, checksum=checksum, loss=float(loss) if loss is not None else None)
     shutdown(ctx)
     return acc
 

@@ -124,26 +124,41 @@ def load_cifar10(train: bool) -> TensorDataset:
     return TensorDataset(x, y, CIFAR_MEAN, CIFAR_STD, "cifar10")
 
 
+PIMA_BUNDLED = pathlib.Path(__file__).with_name("pima_diabetes.npz")
+
+
 class PimaDiabetesDataset(TensorDataset):
-    """PIMA Indians diabetes (8 features, binary outcome), z-normalised with the
-    training statistics; 600 train / 168 test rows (reference datasets.py:52-94).
-    Reads ``$GARFIELD_PIMA_CSV`` (or ``<data root>/pima_diabetes.csv``); synthetic
-    rows of the same shape when absent."""
+    """PIMA Indians diabetes (8 features, binary outcome): the first 600 rows train, the
+    last 168 test, each split z-normalised with its OWN mean and sample standard
+    deviation (reference datasets.py:52-94, pandas ``std``).
+
+    Source, first found: ``csv`` / ``$GARFIELD_PIMA_CSV`` (the reference's CSV layout),
+    then the bundled ``pima_diabetes.npz`` (the same 768 rows as the reference's
+    ``pima_diabetes.csv``, the public UCI/NIDDK Pima Indians Diabetes data, stored as a
+    float32 array; loaded with ``allow_pickle=False``), else synthetic rows of the same
+    shape (with a warning)."""
+
+    TRAIN_SPLIT, TEST_SPLIT = 600, 168
 
     def __init__(self, train: bool = True, train_size: int | None = None, csv: str | None = None):
-        path = pathlib.Path(csv or os.environ.get("GARFIELD_PIMA_CSV", str(data_root() / "pima_diabetes.csv")))
-        ntrain = train_size or 600
-        if path.exists():
-            arr = np.loadtxt(path, delimiter=",", skiprows=1, dtype=np.float32)
-            feats, lab = arr[:, :8], arr[:, 8:9]
-            mu, sd = feats[:ntrain].mean(0), feats[:ntrain].std(0) + 1e-8
-            feats = (feats - mu) / sd
-            sl = slice(0, ntrain) if train else slice(ntrain, None)
-            super().__init__(torch.from_numpy(feats[sl].copy()), torch.from_numpy(lab[sl].copy()), name="pima")
-        else:
-            warning(f"PIMA csv not found at {path}; using synthetic PIMA-shape rows")
-            s = _synthetic("pima", train, n=ntrain if train else 168)
+        path = csv or os.environ.get("GARFIELD_PIMA_CSV")
+        arr = None
+        if path and pathlib.Path(path).exists():
+            arr = np.loadtxt(path, delimiter=",", skiprows=1, dtype=np.float64)
+        elif PIMA_BUNDLED.exists():
+            with np.load(PIMA_BUNDLED, allow_pickle=False) as z:
+                arr = z["rows"].astype(np.float64)
+        ntrain = min(train_size or self.TRAIN_SPLIT, self.TRAIN_SPLIT)
+        if arr is None:
+            warning("PIMA data not found; using synthetic PIMA-shape rows")
+            s = _synthetic("pima", train, n=ntrain if train else self.TEST_SPLIT)
             super().__init__(s.x, s.y, name="pima", synthetic=True)
+            return
+        rows = arr[:ntrain] if train else arr[-self.TEST_SPLIT:]
+        feats, lab = rows[:, :8], rows[:, 8:9]
+        feats = (feats - feats.mean(0)) / feats.std(0, ddof=1)
+        super().__init__(torch.from_numpy(feats.astype(np.float32)), torch.from_numpy(lab.astype(np.float32)),
+                         name="pima")
 
 
 @functools.lru_cache(maxsize=8)

@@ -68,14 +68,18 @@ def restore(model: nn.Module, state: dict) -> None:
                 b.copy_(s.to(b.device))
 
 
-def save_engine(path: str, engine, meta: dict | None = None) -> str:
+def save_engine(path: str, engine, meta: dict | None = None, write: bool = True) -> str:
     """Checkpoint of a ``RobustDataParallel`` engine (fp32 master parameters in the
-    reference layout, buffers, momentum, step)."""
+    reference layout, buffers, momentum, step). Collective in sharded multi-rank runs
+    (master and momentum are gathered): call it on every rank, with ``write`` True on
+    one of them."""
     if hasattr(engine, "sync_master"):
-        engine.sync_master()   # collective in sharded runs
+        engine.sync_master()
     mom = engine.momentum_vector() if hasattr(engine, "momentum_vector") else engine.mom
-    return save(path, engine.model, engine.step_count, engine.flat.to_reference(mom), meta,
-                flat=engine.flat.reference_vector())
+    mom_ref = engine.flat.to_reference(mom)
+    if not write:
+        return path
+    return save(path, engine.model, engine.step_count, mom_ref, meta, flat=engine.flat.reference_vector())
 
 
 def load_engine(path: str, engine) -> dict:
@@ -139,14 +143,17 @@ class Checkpoints:
         s = self.steps()
         return s[-1] if s else None
 
-    def save(self, target, step: int | None = None, meta: dict | None = None) -> str:
+    def save(self, target, step: int | None = None, meta: dict | None = None, write: bool = True) -> str:
+        """``write=False``: take part in the collectives of a sharded engine's
+        checkpoint without writing (every rank but one in a data-parallel job)."""
         if hasattr(target, "flat") and hasattr(target, "step_count"):
             step = target.step_count if step is None else step
-            p = save_engine(self.path(step), target, meta)
+            p = save_engine(self.path(step), target, meta, write=write)
         else:
-            p = save(self.path(step or 0), target, step or 0, None, meta)
-        for old in self.steps()[:-self.max_to_keep]:
-            os.remove(self.path(old))
+            p = save(self.path(step or 0), target, step or 0, None, meta) if write else self.path(step or 0)
+        if write:
+            for old in self.steps()[:-self.max_to_keep]:
+                os.remove(self.path(old))
         return p
 
     def restore(self, target, step: int | None = None) -> dict:

@@ -122,3 +122,24 @@ def test_garfield_cc_crash_mar():
     out = subprocess.run(base, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
     assert re.search(r"final accuracy ([0-9.]+)", out.stdout + out.stderr)
+
+
+def test_garfield_cc_checkpoint_resume_is_exact(tmp_path):
+    """2 ranks (gloo): 6 iterations straight == 3 iterations, checkpoint, fresh processes
+    resuming from it for the last 3 (parameters, momentum, BatchNorm buffers, step)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+
+    def run(extra):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+               "127.0.0.1", "--master-port", str(free_port()), "-m", "garfield_amd.apps.garfield_cc",
+               "--model", "mlp", "--dataset", "mnist", "--loss", "nll", "--lr", "0.05", "--aggregator", "krum",
+               "--fw", "1", "--attack", "reverse", "--workers_per_rank", "3", *extra]
+        out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+        return re.search(r"replica checksum ([-+0-9.e]+)", out.stdout + out.stderr).group(1)
+
+    straight = run(["--num_iter", "6"])
+    ck = str(tmp_path / "ck")
+    run(["--num_iter", "3", "--checkpoint", ck, "--checkpoint_freq", "3"])
+    resumed = run(["--num_iter", "6", "--checkpoint", ck, "--resume", "1"])
+    assert resumed == straight
