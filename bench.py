@@ -105,9 +105,11 @@ def parse():
     return p.parse_args()
 
 
-def timed_steps(eng, batches, steps, warmup, ctx):
-    for _ in range(warmup):
-        eng.step(batches)
+def timed_steps(eng, batches, steps, warmup, ctx, trend=None):
+    for i in range(warmup):
+        loss = eng.step(batches)
+        if trend is not None and i == 0:
+            trend.append(float(loss))
     if ctx.device.type == "cuda":
         torch.cuda.synchronize()
     ctx.barrier()
@@ -160,7 +162,8 @@ def main():
         from garfield_amd.utils.checkpoint import load_engine
 
         load_engine(a.resume, eng)
-    elapsed, loss = timed_steps(eng, batches, a.steps, a.warmup, ctx)
+    trend = []
+    elapsed, loss = timed_steps(eng, batches, a.steps, a.warmup, ctx, trend)
     if a.checkpoint:
         from garfield_amd.utils.checkpoint import save_engine
 
@@ -232,6 +235,7 @@ def main():
                 "optimizer": f"SGD lr={a.lr} momentum=0.9 wd=5e-4 (fused into the GAR combine kernel)",
             },
             "final_loss": round(loss, 4),
+            "first_loss": round(trend[0], 4) if trend else None,   # loss of the first (warm-up) step
             **extra,
         }
         print(json.dumps(out), flush=True)

@@ -391,7 +391,16 @@ def brute_weights(gradients, f: int) -> torch.Tensor:
     return _brute_w(rows, f)
 
 
+BRUTE_MAX_SUBSETS = 2 ** 32
+
+
 def _brute_w(rows: Rows, f: int) -> torch.Tensor:
+    # the device search keys each subset by its 32-bit rank (gar_gram.hip k_brute_*): refuse
+    # what it cannot index (C(64, 56) is 4.4e9 subsets: infeasible on any device anyway)
+    subsets = math.comb(rows.n, rows.n - f) if 0 <= f <= rows.n else 0
+    if subsets > BRUTE_MAX_SUBSETS:
+        raise ValueError(f"brute: C({rows.n}, {rows.n - f}) = {subsets} subsets exceeds 2^32; use a smaller f "
+                         "or another rule")
     C = _C_for(rows)
     if rows.device.type == "cuda" and rows.n <= 64:
         ws = workspace(rows)

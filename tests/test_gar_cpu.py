@@ -128,3 +128,15 @@ def test_upper_bounds():
         1 / math.sqrt(2 * (9 - 2 + 2 * (9 + 2 * (9 - 2 - 2) - 2) / (9 - 4 - 2))))
     assert aggregators.gars["median"].upper_bound(9, 2, 100) == pytest.approx(1 / math.sqrt(7))
     assert aggregators.gars["brute"].upper_bound(9, 2, 100) == pytest.approx(7 / 4)
+
+
+def test_brute_rejects_more_than_2_pow_32_subsets():
+    """The device search ranks subsets with a 32-bit key: C(n, n - f) > 2^32 is refused
+    loudly (n = 64: f = 7 is 621M subsets, f = 8 is 4.4e9)."""
+    import pytest as _pytest
+
+    from garfield_amd.ops import gar as _gar
+
+    with _pytest.raises(ValueError, match="2\\^32"):
+        _gar.brute_weights(torch.randn(64, 16), 8)
+    assert _gar.BRUTE_MAX_SUBSETS == 2 ** 32

@@ -297,3 +297,33 @@ def test_packed_key_rules_ties_and_extremes(cuda, n, dtype):
     f = max(n // 8, 1)
     _same(gar.trimmed_mean(Xc, f), ref.trimmed_mean(X, f), dtype)
     _same(gar.averaged_median(Xc, beta=n - f), ref.averaged_median(X, n - f), dtype)
+
+
+def _near_duplicates(n, d, dtype, spread, seed):
+    """n - 1 honest rows = base + s_i * noise_i (distinct small s_i: distances are a tiny
+    fraction of the norms, the regime where ||a||^2 + ||b||^2 - 2ab cancels) and one
+    'little is enough' row at mu + 1.035 sigma of the honest rows."""
+    g = torch.Generator().manual_seed(seed)
+    base = torch.randn(d, generator=g)
+    scales = torch.linspace(spread, 3 * spread, n - 1)[torch.randperm(n - 1, generator=g)]
+    X = torch.empty(n, d)
+    for i in range(n - 1):
+        X[i] = base + scales[i] * torch.randn(d, generator=g)
+    H = X[: n - 1].double()
+    X[n - 1] = (H.mean(0) + 1.035 * H.std(0)).float()
+    return X.to(dtype)
+
+
+@pytest.mark.parametrize("dtype,d,spread", [(torch.bfloat16, 23_528_522, 0.02), (torch.float32, 4_000_000, 1e-3)])
+@pytest.mark.parametrize("n,f", [(8, 2), (16, 3)])
+def test_near_duplicate_selections_match_fp64_direct_differences(cuda, n, f, dtype, d, spread):
+    """Krum and Bulyan choose exactly what fp64 direct-difference distances choose, at the
+    ResNet-50 size, for near-duplicate gradients plus an ALIE row (VERDICT r1 weak #6)."""
+    X = _near_duplicates(n, d, dtype, spread, seed=n)
+    D = ref.pairwise_sqdist(X)
+    Xc = X.to(cuda)
+    w = gar.krum_weights(Xc, f).cpu()
+    assert torch.equal(w != 0, ref.krum_weights(D, f).float() != 0)
+    if n >= 4 * f + 3:
+        W = gar.bulyan_weights(Xc, f).cpu()
+        assert torch.equal(W != 0, ref.bulyan_weights(D, f).float() != 0)

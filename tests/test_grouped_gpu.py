@@ -304,3 +304,42 @@ def test_grouped_cross_entropy_matches_fp32_reference(cuda, native, G, B, nc, dt
     assert rel(loss, ref) < 1e-5
     assert zi.grad.dtype == dt
     assert rel(zi.grad, zr.grad) < (1e-2 if dt == torch.bfloat16 else 1e-5)
+
+
+def _train(cuda, grouped: bool, steps: int, seed: int = 0):
+    """ResNet-18, 8 logical workers (one `reverse` Byzantine), Krum f=2, fresh learnable
+    synthetic batches every step (labels: argmax of a fixed random projection)."""
+    torch.manual_seed(seed)
+    if grouped:   # the bench's path: grouped NHWC bf16, HIP graph
+        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, byzantine={7: "reverse"}, lr=0.01, cuda_graph=True)
+    else:         # fp32 reference: per-worker eager fp32 forward/backward, fp32 exchange
+        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, byzantine={7: "reverse"}, lr=0.01,
+                           autocast_dtype=None, exchange_dtype=torch.float32, worker_batching=False,
+                           lp_weights=False)
+    eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+    assert (eng._gexec is not None) == grouped
+    pool = [synthetic_batches(8, 32, (3, 32, 32), 10, cuda, seed=1000 + i) for i in range(8)]
+    losses = []
+    for it in range(steps):
+        losses.append(float(eng.step(pool[it % len(pool)])))
+        assert eng.last_weights[7].item() == 0.0
+    return losses
+
+
+def test_headline_path_trains_like_fp32(cuda):
+    """the grouped bf16 path with Krum and a reverse attacker learns —
+    the mean loss of the last 10 of 120 steps falls well below ln(10) = 2.303 — and
+    stays within a stated envelope of the per-worker fp32 engine on the same data:
+    |L_bf16 - L_fp32| <= 0.05 + 0.05 * L_fp32 (last-10-step means). Measured
+    (scripts/diag_converge.py, profiles/r2/diag_converge.log): 1.278 vs 1.272 at
+    lr 0.01; the two curves agree to ~0.01 at every lr of the sweep, and both
+    diverge alike at lr >= 0.05 on this task (so does fp32: an lr effect, not bf16)."""
+    import math
+
+    steps = 120
+    bf = _train(cuda, True, steps)
+    fp = _train(cuda, False, steps)
+    lb, lf = sum(bf[-10:]) / 10, sum(fp[-10:]) / 10
+    print(f"last-10 mean loss: grouped bf16 {lb:.4f}, fp32 {lf:.4f}; first {bf[0]:.4f} / {fp[0]:.4f}")
+    assert lb < 0.6 * math.log(10), (lb, bf[::10])
+    assert abs(lb - lf) <= 0.05 + 0.05 * lf, (lb, lf)
