@@ -28,6 +28,10 @@ def parse(argv=None):
     p.add_argument("--num_nodes", type=int, default=3)
     p.add_argument("--f", type=int, default=0, help="Number of declared Byzantine nodes.")
     p.add_argument("--non_iid", type=int, default=0, help="1: run the log2(t) average-agreement rounds.")
+    p.add_argument("--collective", type=int, default=0,
+                   help="1: torch.distributed collectives (RCCL over xGMI on GPUs, gloo on CPU) instead of RPC; "
+                        "every pull is one all-gather (parallel/learn.py)")
+    p.add_argument("--backend", default=None, help="collective backend (default: nccl=RCCL on GPU, gloo on CPU)")
     p.set_defaults(port=29700)
     return p.parse_args(argv)
 
@@ -49,6 +53,8 @@ def main(argv=None, results: dict | None = None, progress=None):
         print_setup(a.rank, nodes=n, f=f, gar=a.gar, dataset=a.dataset, model=a.model, batch=a.batch,
                     optimizer=a.optimizer, opt_args=a.opt_args, non_iid=a.non_iid)
     seed_all(1234)
+    if a.collective:
+        return _main_collective(a, results, progress)
     init_rpc(f"node:{a.rank}", a.rank, n, a.master, a.port, a.rpc_timeout)
     gar = aggregators.get(a.gar)
     if a.attack and a.rank < f:
@@ -76,9 +82,48 @@ def main(argv=None, results: dict | None = None, progress=None):
             progress(i + 1, a.num_iter)
     if results is not None:
         results["accuracy"] = acc
+    info(f"Node {a.rank} model checksum {float(ps.flat.reference_vector().double().sum()):.12e}")
     import torch.distributed.rpc as rpc
 
     rpc.shutdown()
+
+
+
+def _main_collective(a, results, progress):
+    """LEARN with every pull as an all-gather (one node per rank; ``torchrun`` or --rank/--master)."""
+    import os
+
+    import torch
+
+    from garfield_amd.parallel.comm import init_distributed, shutdown
+    from garfield_amd.parallel.learn import CollectiveLearnNode
+
+    if "WORLD_SIZE" not in os.environ:
+        os.environ.update(RANK=str(a.rank), WORLD_SIZE=str(a.num_nodes), LOCAL_RANK=os.environ.get(
+            "LOCAL_RANK", str(a.rank % max(torch.cuda.device_count(), 1))), MASTER_ADDR=a.master,
+            MASTER_PORT=str(a.port))
+    ctx = init_distributed(backend=a.backend, device=a.device)
+    node = CollectiveLearnNode(ctx, a.model, a.dataset, a.batch, a.loss, a.optimizer, a.opt_args, a.gar, a.f,
+                               a.attack, bool(a.non_iid), train_size=a.train_size)
+    start = time.time()
+    acc = None
+    for i in range(a.num_iter):
+        with StepTimer(a.bench) as t:
+            loss = node.step(i)
+        if a.bench:
+            info(f"Training step {i} takes {t.seconds:.4f} s")
+        if a.log:
+            info(f"Node {ctx.rank} iteration {i} loss {loss:.4f}")
+        if (a.acc_freq and i % a.acc_freq == 0) or i == a.num_iter - 1:
+            acc = node.accuracy(binary=a.dataset == "pima")
+            info(f"Node {ctx.rank} iteration: {i} Accuracy: {acc:.2f} Time: {time.time() - start:.2f}")
+        if progress is not None:
+            progress(i + 1, a.num_iter)
+    if results is not None:
+        results["accuracy"] = acc
+    info(f"Node {ctx.rank} model checksum {float(node.model_vector().double().sum()):.12e}")
+    shutdown(ctx)
+    return acc
 
 
 if __name__ == "__main__":
