@@ -67,6 +67,9 @@ def parse(argv=None):
     p.add_argument("--bench", type=str2bool, default=False)
     p.add_argument("--log", type=str2bool, default=False)
     p.add_argument("--acc_freq", type=int, default=0)
+    p.add_argument("--layerwise", type=str2bool, default=False,
+                   help="apply the GAR per parameter tensor like the reference (trainer.py:90-140); the default "
+                        "aggregates the flat gradient (same result for coordinate-wise rules)")
     p.add_argument("--checkpoint", default="", help="checkpoint directory (reference-layout flat vector + "
                    "momentum + BatchNorm buffers; utils/checkpoint.py)")
     p.add_argument("--checkpoint_freq", type=int, default=0, help="save every this many iterations (0: at the end)")
@@ -107,6 +110,8 @@ def main(argv=None, results: dict | None = None):
     # f = fw as in the reference (gar(gradients, f=fw)); a rule whose check needs f >= 1 fails loudly
     common = dict(gar=gar_name, f=a.fw, workers_per_rank=k, lr=a.lr, momentum=a.momentum, weight_decay=a.wd,
                   exchange_dtype=xdt, byzantine=byz, cuda_graph=a.cuda_graph)
+    if a.layerwise:
+        common.update(layerwise=True, shard_gar=False)
     if byz_mode:
         eng = ByzantinePSDataParallel(model, loss_fn, ctx,
                                       ByzPSConfig(num_ps=a.num_ps, fps=a.fps, mar=mar, ps_attack=a.ps_attack,

@@ -50,6 +50,7 @@ os.environ.setdefault("MIOPEN_DEBUG_GROUP_CONV_IMPLICIT_GEMM_HIP_WRW_XDLOPS", "0
 WEIGHTED_RULES = {"average", "krum", "brute", "aksel"}
 _LP_MODULES = (nn.modules.conv._ConvNd, nn.Linear)
 COORD_RULES = {"median", "trimmed-mean", "averaged-median", "average-nan", "condense", "bulyan"}
+LAYERWISE_RULES = {"krum", "bulyan", "brute", "aksel"}   # per-layer != flat only for distance-based rules
 
 
 @dataclass
@@ -81,6 +82,11 @@ class EngineConfig:
     # all-reduce, sharded update, all-gather of the master; parallel/sharded.py)
     # instead of all-gathering every gradient to every rank. None: on when world > 1.
     shard_gar: bool | None = None
+    # Garfield_CC's per-layer aggregation (reference trainer.py:90-140: the GAR runs on each
+    # parameter tensor separately). Differs from the flat rule for the distance-based GARs
+    # (Krum, Bulyan, Brute, Aksel); identical for the coordinate-wise ones. Redundant
+    # (unsharded) aggregation only.
+    layerwise: bool = False
 
 
 class _SlotIssuer:
@@ -203,6 +209,10 @@ class RobustDataParallel:
             return False
         if self.ctx.world_size > 1 and not self.ctx.is_distributed:
             raise ValueError("sharded aggregation over several ranks needs an initialised process group")
+        if self.cfg.layerwise:
+            if self.cfg.shard_gar:
+                raise ValueError("layerwise aggregation runs on the redundant path (shard_gar=False)")
+            return False
         if self.cfg.gar not in SUPPORTED:
             raise ValueError(f"sharded aggregation does not support {self.cfg.gar!r} (shard_gar=False)")
         return True
@@ -358,6 +368,10 @@ class RobustDataParallel:
             return
         rule = cfg.gar
         kw = dict(cfg.gar_kwargs)
+        if cfg.layerwise and rule in LAYERWISE_RULES:
+            self._layerwise_update(rule, kw, first)
+            self.step_count += 1
+            return
         if self.device.type == "cuda":
             C = self._C
             param, mom = self.flat.data[: self.d], self.mom[: self.d]
@@ -382,6 +396,27 @@ class RobustDataParallel:
             g = gar.aggregate(rule, self.G.float(), **gkw).float()
             self._sgd_cpu(g, first)
         self.step_count += 1
+
+    def _layerwise_update(self, rule: str, kw: dict, first: bool) -> None:
+        """The GAR on every parameter tensor's slice of the [n, d] rows (each parameter is
+        one contiguous segment of the memory-order flat layout), then one update."""
+        cfg = self.cfg
+        gkw = dict(kw, f=cfg.f)
+        if cfg.m is not None and rule in ("krum", "bulyan"):
+            gkw["m"] = cfg.m
+        g = self._gagg if self._gagg is not None else torch.zeros(self.ld, dtype=torch.float32, device=self.device)
+        self._gagg = g
+        for off, numel in zip(self.flat.offsets, self.flat.numels):
+            seg = self.G[:, off:off + numel]
+            g[off:off + numel].copy_(gar.aggregate(rule, seg if self.device.type == "cuda" else seg.float(),
+                                                   **gkw).float())
+        self.last_weights = None
+        if self.device.type == "cuda":
+            self._C.gpu_combine_sgd(g.view(1, self.ld)[:, : self.d], self._one, self.flat.data[: self.d],
+                                    self.mom[: self.d], None, self._shadow, cfg.lr, cfg.momentum, cfg.dampening,
+                                    cfg.weight_decay, cfg.nesterov, first)
+        else:
+            self._sgd_cpu(g[: self.d], first)
 
     def _weights(self, rule: str, kw: dict) -> torch.Tensor:
         f = self.cfg.f

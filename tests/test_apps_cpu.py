@@ -143,3 +143,15 @@ def test_garfield_cc_checkpoint_resume_is_exact(tmp_path):
     run(["--num_iter", "3", "--checkpoint", ck, "--checkpoint_freq", "3"])
     resumed = run(["--num_iter", "6", "--checkpoint", ck, "--resume", "1"])
     assert resumed == straight
+
+
+def test_garfield_cc_layerwise():
+    """--layerwise: the GAR per parameter tensor (reference Garfield_CC semantics), 2 ranks."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), "-m", "garfield_amd.apps.garfield_cc", "--model", "mlp", "--dataset",
+           "mnist", "--loss", "nll", "--lr", "0.05", "--aggregator", "krum", "--fw", "1", "--attack", "reverse",
+           "--workers_per_rank", "3", "--num_iter", "10", "--layerwise", "1"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+    assert re.search(r"final accuracy ([0-9.]+)", out.stdout + out.stderr)

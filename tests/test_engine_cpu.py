@@ -143,3 +143,29 @@ def test_two_rank_grouped_workers_with_sharded_aggregation():
         assert torch.equal(r["1r0"], r["1r1"]) and torch.equal(r["0r0"], r["0r1"])
         rel = ((r["1r0"] - r["0r0"]).norm() / r["0r0"].norm()).item()
         assert rel < 1e-5, rel
+
+
+@pytest.mark.parametrize("rule,f", [("krum", 2), ("bulyan", 1)])
+def test_layerwise_gar_matches_per_tensor_oracle(rule, f):
+    """Garfield_CC's per-layer mode (reference trainer.py:90-140): the GAR runs on each
+    parameter tensor's gradients separately; one SGD step (no momentum / decay) must
+    equal the fp64 oracle applied tensor by tensor -- and differ from the flat rule."""
+    from garfield_amd.ops import reference as ref
+
+    torch.manual_seed(0)
+    k = 8
+    cfg = dict(gar=rule, f=f, workers_per_rank=k, byzantine={1: "reverse"}, lr=0.1, momentum=0.0,
+               weight_decay=0.0, exchange_dtype=torch.float32)
+    eng = RobustDataParallel(build_model("mlp"), F.nll_loss, DistContext(), EngineConfig(layerwise=True, **cfg))
+    b = synthetic_batches(k, 16, (1, 28, 28), 10, "cpu")
+    before = eng.flat.data[: eng.d].clone()
+    eng.step(b)
+    G = eng.G.double()
+    expect = torch.empty(eng.d, dtype=torch.float64)
+    for off, numel in zip(eng.flat.offsets, eng.flat.numels):
+        seg = G[:, off:off + numel]
+        expect[off:off + numel] = ref.krum(seg, f) if rule == "krum" else ref.bulyan(seg, f)
+    got = (before - eng.flat.data[: eng.d]).double() / 0.1
+    assert ((got - expect).norm() / expect.norm()).item() < 1e-5
+    flat = ref.krum(G, f) if rule == "krum" else ref.bulyan(G, f)
+    assert ((flat - expect).norm() / expect.norm()).item() > 1e-6   # a different rule than the flat one

@@ -188,3 +188,24 @@ def test_bucketed_exchange_overlap_loopback(cuda, rule, f, monkeypatch):
         outs.append(eng.flat.reference_vector().clone())
     rel = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
     assert rel < 1e-5, rel
+
+
+@pytest.mark.gpu
+def test_layerwise_krum_on_gpu_matches_per_segment_gar(cuda):
+    """Layer-wise Krum on the GPU path (grouped ResNet-18 rows, HIP GAR per parameter
+    segment): the update equals the per-segment HIP Krum of the same rows."""
+    from garfield_amd.ops import gar
+
+    torch.manual_seed(0)
+    cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, byzantine={3: "reverse"}, lr=0.1, momentum=0.0,
+                       weight_decay=0.0, layerwise=True, cuda_graph=False)
+    eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+    b = synthetic_batches(8, 8, (3, 32, 32), 10, cuda)
+    before = eng.flat.data[: eng.d].clone()
+    eng.step(b)
+    torch.cuda.synchronize()
+    expect = torch.empty(eng.d, dtype=torch.float32, device=cuda)
+    for off, numel in zip(eng.flat.offsets, eng.flat.numels):
+        expect[off:off + numel] = gar.krum(eng.G[:, off:off + numel], 2).float()
+    got = (before - eng.flat.data[: eng.d]) / 0.1
+    assert ((got - expect).norm() / expect.norm()).item() < 1e-4
