@@ -98,6 +98,11 @@ def parse():
     p.add_argument("--shard-gar", action="store_true",
                    help="force the sharded, bucketed aggregation even on one GPU (with GARFIELD_LOOPBACK_EXCHANGE=1 "
                         "the exchange is emulated by side-stream copies: overlap traces)")
+    p.add_argument("--num-ps", type=int, default=0,
+                   help="Byzantine-server mode (parallel/byzps.py): ranks < NUM_PS are server replicas")
+    p.add_argument("--fps", type=int, default=0, help="Byzantine servers tolerated by the model aggregation")
+    p.add_argument("--mar", default="median", help="model aggregation rule of the Byzantine-server mode")
+    p.add_argument("--ps-workers", action="store_true", help="server ranks also host logical workers")
     p.add_argument("--checkpoint", default="", help="save a checkpoint here after the timed steps (untimed)")
     p.add_argument("--resume", default="", help="restore this checkpoint file before the warm-up")
     p.add_argument("--lr", type=float, default=0.01,
@@ -155,7 +160,16 @@ def main():
                        cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=not a.no_lp_weights,
                        worker_batching=False if a.no_worker_batching else None,
                        shard_gar=True if a.shard_gar else None)
-    eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
+    if a.num_ps:
+        from dataclasses import asdict
+
+        from garfield_amd.parallel.byzps import ByzantinePSDataParallel, ByzPSConfig
+
+        eng = ByzantinePSDataParallel(model, F.cross_entropy, ctx,
+                                      ByzPSConfig(**asdict(cfg), num_ps=a.num_ps, fps=a.fps, mar=a.mar,
+                                                  ps_workers=a.ps_workers))
+    else:
+        eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
     batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
                                 seed=1000 + ctx.rank, channels_last=a.channels_last)
     if a.resume:
@@ -168,7 +182,7 @@ def main():
         from garfield_amd.utils.checkpoint import save_engine
 
         save_engine(a.checkpoint, eng, meta={"bench": vars(a)}, write=ctx.rank == 0)
-    n = eng.n
+    n = getattr(eng, "n_w", eng.n)   # Byzantine-server mode: only the worker slots train
     imgs = n * a.batch * a.steps
     value = imgs / elapsed
     ms = 1000.0 * elapsed / a.steps
@@ -222,7 +236,9 @@ def main():
                 "global_batch": n * a.batch,
                 "seq_len": None,
                 "image_shape": list(shape),
-                "parallelism": f"dp{world} (robust DP, {a.workers_per_gpu} logical workers/GPU, n={n})",
+                "parallelism": f"dp{world} (robust DP, {a.workers_per_gpu} logical workers/GPU, n={n})"
+                               + (f", {a.num_ps} Byzantine-resilient server replicas (fps={a.fps}, mar={a.mar}"
+                                  f"{', servers host workers' if a.ps_workers else ''})" if a.num_ps else ""),
                 "process_group": {"backend": ctx.backend,
                                   "world_size": dist.get_world_size() if ctx.is_distributed else 1},
                 "gar": a.gar,

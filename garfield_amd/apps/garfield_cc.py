@@ -61,6 +61,8 @@ def parse(argv=None):
     p.add_argument("--mar", default="median")
     p.add_argument("--attack", default="", help="attack of the fw Byzantine worker slots")
     p.add_argument("--ps_attack", default="", help="attack of the fps Byzantine servers")
+    p.add_argument("--ps_workers", type=str2bool, default=False,
+                   help="Byzantine-server mode: server ranks also host --workers_per_rank logical workers")
     p.add_argument("--backend", default=None, help="nccl (RCCL) or gloo")
     p.add_argument("--exchange_dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--cuda_graph", type=str2bool, default=True)
@@ -101,7 +103,8 @@ def main(argv=None, results: dict | None = None):
             raise SystemExit(f"--mar {mar} tolerates no Byzantine server: use --fps 0")
         mar = "average"
     byz_mode = a.num_ps >= 2 or (a.num_ps == 1 and a.fps > 0)
-    worker_ranks = list(range(a.num_ps, ctx.world_size)) if byz_mode else list(range(ctx.world_size))
+    worker_ranks = list(range(a.num_ps, ctx.world_size)) if (byz_mode and not a.ps_workers) \
+        else list(range(ctx.world_size))
     # Byzantine logical workers: the first fw global worker slots (slot = j * world + rank)
     slots = sorted(j * ctx.world_size + r for j in range(k) for r in worker_ranks)
     byz = {s: a.attack for s in slots[: a.fw]} if a.attack else {}
@@ -115,7 +118,7 @@ def main(argv=None, results: dict | None = None):
     if byz_mode:
         eng = ByzantinePSDataParallel(model, loss_fn, ctx,
                                       ByzPSConfig(num_ps=a.num_ps, fps=a.fps, mar=mar, ps_attack=a.ps_attack,
-                                                  **common))
+                                                  ps_workers=a.ps_workers, **common))
     else:
         eng = RobustDataParallel(model, loss_fn, ctx, EngineConfig(**common))
     # data: logical worker j of rank r trains on partition (its worker index)

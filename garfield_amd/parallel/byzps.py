@@ -9,7 +9,10 @@ again) and the RPC ``ByzSGD`` trainer (``get_models`` + model GAR).
 Collective form here, per step, on flat vectors (never per tensor):
 
 1. worker ranks (``rank >= num_ps``) compute their logical workers' gradients into
-   the exchange buffer ``X[k, world, ld]``; server ranks contribute zero rows;
+   the exchange buffer ``X[k, world, ld]`` -- with the grouped executor (one HIP graph
+   for the k workers, as in the plain engine) for the ResNet family; server ranks
+   contribute zero rows, or host logical workers too with ``ps_workers=True`` (no
+   idle GPUs: a server rank then trains like any worker rank);
 2. ``X`` is all-gathered (RCCL full mesh) slot by slot, overlapped with compute;
 3. every server replica runs the GAR (f = fw) on the worker rows only (a row
    table over the worker slots — no stacking copy) and applies its SGD update;
@@ -38,19 +41,25 @@ class ByzPSConfig(EngineConfig):
     fps: int = 1
     mar: str = "trimmed-mean"
     ps_attack: str = ""        # attack of the simulated Byzantine servers (ranks < fps)
+    ps_workers: bool = False   # server ranks also host workers_per_rank logical workers
 
 
 class ByzantinePSDataParallel(RobustDataParallel):
-    _supports_grouping = False   # server ranks contribute no gradients: per-worker path only
-    _supports_sharding = False   # servers aggregate the worker rows themselves (all-gather form)
+    # Every server replica aggregates ALL worker rows itself (all-gather form): sharding the
+    # servers' GAR across replicas would let one Byzantine server corrupt its shard of
+    # every honest server's aggregate, which is the failure this mode exists to tolerate.
+    _supports_sharding = False
 
     def __init__(self, model: nn.Module, loss_fn, ctx: DistContext, cfg: ByzPSConfig):
-        if not (0 < cfg.num_ps < ctx.world_size):
-            raise ValueError(f"need 0 < num_ps < world_size, got num_ps={cfg.num_ps} world={ctx.world_size}")
+        top = ctx.world_size if cfg.ps_workers else ctx.world_size - 1   # someone must compute gradients
+        if not (0 < cfg.num_ps <= top):
+            raise ValueError(f"need 0 < num_ps <= {top} (world {ctx.world_size}, ps_workers={cfg.ps_workers}), "
+                             f"got num_ps={cfg.num_ps}")
         self.num_ps = cfg.num_ps
         super().__init__(model, loss_fn, ctx, cfg)
         self.is_ps = ctx.rank < cfg.num_ps
-        self.worker_ranks = list(range(cfg.num_ps, ctx.world_size))
+        self.worker_ranks = list(range(0 if cfg.ps_workers else cfg.num_ps, ctx.world_size))
+        self.computes = (not self.is_ps) or cfg.ps_workers
         self.n_w = self.k * len(self.worker_ranks)
         self.M = torch.zeros((self.world, self.ld), dtype=torch.float32, device=self.device)
         self._ps_gen = torch.Generator(device=self.device)
@@ -60,7 +69,7 @@ class ByzantinePSDataParallel(RobustDataParallel):
         from garfield_amd import aggregators
 
         cfg = self.cfg
-        n_w = cfg.workers_per_rank * (self.ctx.world_size - cfg.num_ps)
+        n_w = cfg.workers_per_rank * (self.ctx.world_size - (0 if cfg.ps_workers else cfg.num_ps))
         msg = aggregators.get(cfg.gar).check(gradients=[torch.zeros(1)] * n_w, f=cfg.f, **cfg.gar_kwargs)
         if msg is not None:
             raise ValueError(f"GAR {cfg.gar!r} with {n_w} worker gradients: {msg}")
@@ -69,23 +78,35 @@ class ByzantinePSDataParallel(RobustDataParallel):
             raise ValueError(f"MAR {cfg.mar!r} with {cfg.num_ps} servers: {msg}")
 
     def graph_capturable(self) -> bool:
-        return False  # servers and workers run different bodies; keep it eager
+        return False  # per-worker graphs: servers and workers run different bodies (grouped: see _compute)
 
     def _worker_rows(self) -> list:
         return [self.X[j, r, : self.d] for j in range(self.k) for r in self.worker_ranks]
 
+    def _compute(self, batches) -> torch.Tensor:
+        """This rank's logical workers -> exchange rows (+ the slot all-gathers)."""
+        if self._gexec is not None and self._groupable(batches):
+            self._stage_grouped(batches)
+            self._grouped_compute()
+            self._attack_local_rows()
+            works = [w for w in (self._gather_slot(j) for j in range(self.k)) if w is not None]
+            for w in works:
+                w.wait()
+            return self._gloss.mean()
+        losses = self.compute_local(batches)
+        return torch.stack(losses).float().mean()
+
     def step(self, batches) -> torch.Tensor:
         cfg = self.cfg
-        # 1-2: gradients (workers) + exchange (everyone)
-        if self.is_ps:
+        # 1-2: gradients (worker ranks) + exchange (everyone)
+        if self.computes:
+            loss = self._compute(batches)
+        else:
             works = [all_gather_rows(self.X[j], self.rank, async_op=True) for j in range(self.k)] \
                 if self.world > 1 else []
             for w in works:
                 w.wait()
             loss = torch.zeros((), device=self.device)
-        else:
-            losses = self.compute_local(batches)
-            loss = torch.stack(losses).float().mean()
         # 3: servers aggregate + update
         if self.is_ps:
             self._server_update()

@@ -556,18 +556,22 @@ class RobustDataParallel:
             self._gsrc = key
             self._gsrc_refs = [t for xy in batches for t in xy]  # keep ids valid while cached
 
+    def _grouped_compute(self) -> None:
+        """The k local workers' forward/backward as one grouped pass (HIP graph from the
+        second step on); every worker's gradient lands in its exchange row."""
+        if (self.device.type == "cuda" and self.cfg.cuda_graph and not self._graph_failed and self.step_count >= 1
+                and self._ggraph is None):
+            self._capture_grouped()
+        if self._ggraph is not None:
+            self._ggraph.replay()
+        else:
+            self._gexec.run(self._gx, self._gy, self._gloss)
+
     def _grouped_step(self, batches) -> torch.Tensor:
-        cuda = self.device.type == "cuda"
         self._stage_grouped(batches)
         works = []
         with self.timer.phase("compute"):
-            if (cuda and self.cfg.cuda_graph and not self._graph_failed and self.step_count >= 1
-                    and self._ggraph is None):
-                self._capture_grouped()
-            if self._ggraph is not None:
-                self._ggraph.replay()
-            else:
-                self._gexec.run(self._gx, self._gy, self._gloss)
+            self._grouped_compute()
             if self._shard is not None:   # buckets leave as the backward finishes them
                 self._shard.start_exchange(self._gexec.mark_events())
             else:

@@ -155,3 +155,17 @@ def test_garfield_cc_layerwise():
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
     assert re.search(r"final accuracy ([0-9.]+)", out.stdout + out.stderr)
+
+
+def test_garfield_cc_byzantine_servers_hosting_workers():
+    """--ps_workers: the 3 server ranks also train (8 ranks x 2 logical workers, fw = 2 of 16)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "8", "--master-addr",
+                          "127.0.0.1", "--master-port", str(free_port()), "-m", "garfield_amd.apps.garfield_cc",
+                          "--num_ps", "3", "--fps", "1", "--fw", "2", "--attack", "reverse", "--ps_attack", "reverse",
+                          "--ps_workers", "1", "--workers_per_rank", "2", "--aggregator", "trimmed-mean", "--mar",
+                          "trimmed-mean", "--model", "mlp", "--dataset", "mnist", "--num_iter", "30", "--lr", "0.05",
+                          "--loss", "nll"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+    m = re.search(r"final accuracy ([0-9.]+)", out.stdout + out.stderr)
+    assert m and float(m.group(1)) > 15.0

@@ -209,3 +209,31 @@ def test_layerwise_krum_on_gpu_matches_per_segment_gar(cuda):
         expect[off:off + numel] = gar.krum(eng.G[:, off:off + numel], 2).float()
     got = (before - eng.flat.data[: eng.d]) / 0.1
     assert ((got - expect).norm() / expect.norm()).item() < 1e-4
+
+
+@pytest.mark.gpu
+def test_byzps_one_gpu_grouped_matches_plain_engine(cuda):
+    """Byzantine-server mode on one GPU (the rank is a server replica hosting its workers,
+    MAR median over one model = identity): the grouped HIP-graph worker path runs and the
+    parameters equal the plain engine's after 3 steps."""
+    from garfield_amd.parallel.byzps import ByzantinePSDataParallel, ByzPSConfig
+
+    outs = []
+    for byzps in (False, True):
+        torch.manual_seed(0)
+        kw = dict(gar="krum", f=2, workers_per_rank=8, byzantine={6: "reverse"}, lr=0.01, cuda_graph=True)
+        model = build_model("resnet18")
+        if byzps:
+            eng = ByzantinePSDataParallel(model, F.cross_entropy, DistContext(device=cuda),
+                                          ByzPSConfig(num_ps=1, fps=0, mar="median", ps_workers=True, **kw))
+            assert eng._gexec is not None
+        else:
+            eng = RobustDataParallel(model, F.cross_entropy, DistContext(device=cuda), EngineConfig(**kw))
+        b = synthetic_batches(8, 8, (3, 32, 32), 10, cuda)
+        for _ in range(3):
+            eng.step(b)
+        torch.cuda.synchronize()
+        if byzps:
+            assert eng._ggraph is not None
+        outs.append(eng.flat.reference_vector().clone())
+    assert torch.equal(outs[0], outs[1])
