@@ -54,6 +54,14 @@ __device__ __forceinline__ void oem_sort_i32(int (&v)[NP]) {
   }
 }
 
+// volatile read of a __shared__ object through an LDS-typed pointer (a generic volatile
+// pointer would become a system-coherent FLAT load)
+template <typename T>
+__device__ __forceinline__ T lds_volatile(const T& x) {
+  typedef __attribute__((address_space(3))) const volatile T lds_t;
+  return *(lds_t*)(&x);
+}
+
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
@@ -123,7 +131,7 @@ __global__ __launch_bounds__(256) void k_bulyan_tail(RowTable rows, int n, int64
       if (k < tt) {  // uniform
         // volatile LDS reads: the per-set mask and scale are tile-invariant, and hoisting
         // all t of them out of the tile loop would pin 2t SGPRs + t VGPRs (spills)
-        const uint64_t cur = uniform64(*reinterpret_cast<volatile uint64_t*>(&smask[k]));
+        const uint64_t cur = uniform64(lds_volatile(smask[k]));
         uint64_t add = cur & ~prev, rem = prev & ~cur;
 #pragma clang loop unroll(disable)
         while (add) { r += at(__builtin_ctzll(add), col); add &= add - 1; }
@@ -131,7 +139,7 @@ __global__ __launch_bounds__(256) void k_bulyan_tail(RowTable rows, int n, int64
         while (rem) { r -= at(__builtin_ctzll(rem), col); rem &= rem - 1; }
         prev = cur;
         exact = exact && isfinite(r);
-        v[k] = r * *reinterpret_cast<volatile float*>(&sscale[k]);
+        v[k] = r * lds_volatile(sscale[k]);
       } else {
         v[k] = kInf;
       }
@@ -140,11 +148,11 @@ __global__ __launch_bounds__(256) void k_bulyan_tail(RowTable rows, int n, int64
 #pragma unroll
       for (int k = 0; k < NP; ++k) {
         if (k < tt) {
-          uint64_t m = uniform64(*reinterpret_cast<volatile uint64_t*>(&smask[k]));
+          uint64_t m = uniform64(lds_volatile(smask[k]));
           float s = 0.f;
 #pragma clang loop unroll(disable)
           while (m) { s += at(__builtin_ctzll(m), col); m &= m - 1; }
-          v[k] = sanitize_inf(s * *reinterpret_cast<volatile float*>(&sscale[k]));
+          v[k] = sanitize_inf(s * lds_volatile(sscale[k]));
         }
       }
     }
@@ -213,6 +221,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));
 
@@ -228,63 +237,121 @@ __device__ __forceinline__ f32x16_t mfma32x32x16(s16x8_t a, s16x8_t b, f32x16_t 
                                                   0, 0, 0);
 }
 
-// key[idx] for a runtime idx: OR of masked terms (a select of one load and a
-// constant 0 per element is not folded back into one dynamically indexed load, and
-// needs no forced register copies)
-template <int N>
-__device__ __forceinline__ int pick_or(const int (&key)[N], int idx) {
-  int r = 0;
+// odd-even merge sort on floats (no NaN: callers map NaN to +inf first). The
+// inputs are arithmetic results, so fminf/fmaxf need no canonicalisation here
+template <int NP>
+__device__ __forceinline__ void oem_sort_f32(float (&v)[NP]) {
 #pragma unroll
-  for (int i = 0; i < N; ++i) r |= (i == idx) ? key[i] : 0;
-  return r;
+  for (int p = 1; p < NP; p <<= 1) {
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+      for (int j = k % p; j + k < NP; j += 2 * k) {
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
+          if (i + j + k < NP && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            const float a = v[i + j], b = v[i + j + k];
+            v[i + j] = __builtin_fminf(a, b);
+            v[i + j + k] = __builtin_fmaxf(a, b);
+          }
+        }
+      }
+    }
+  }
 }
 
-// sorted means -> mean of the beta closest to the median (window [a, a + beta))
-template <int NP>
-__device__ __forceinline__ float window_mean(float (&v)[NP], int tt, int bb, float inv_beta) {
-  int key[NP];
+// Sorted means -> mean of the beta closest to the median (window [a, a + beta)).
+// Valid for NP / 2 < t <= NP (the MFMA tail's MB = 1 / 2 ranges): the runtime
+// positions read (the median t / 2 and the excluded highs beta .. t - 1) are all
+// >= NP / 4, so the sorted values from NP / 4 up are spilled to this wave's LDS
+// scratch `ks` ((NP - NP / 4) x 64 floats, [position / 4][lane][position % 4])
+// with static b128 stores and read back at uniform addresses: no select chains
+// over the register array. EXACT: inputs may hold +-inf (NaN already mapped to
+// +inf), so distances are sanitised like the reference's.
+template <int NP, bool EXACT>
+__device__ __forceinline__ float window_mean(float (&v)[NP], int tt, int bb, float inv_beta, float* ks, int lane) {
+  constexpr int P0 = NP / 4;
+  static_assert(P0 % 4 == 0 && P0 <= kTailMaxExcluded, "window_mean layout");
+  oem_sort_f32<NP>(v);
 #pragma unroll
-  for (int k = 0; k < NP; ++k) key[k] = f32_key(sanitize_inf(v[k]));
-  oem_sort_i32<NP>(key);
-  const float med = key_f32(pick_or(key, tt / 2));
+  for (int i = P0; i < NP; i += 4)
+    *reinterpret_cast<float4*>(ks + (i - P0) * 64 + lane * 4) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+  asm volatile("" ::: "memory");
+  const float* kl = ks + lane * 4;
+  auto at = [&](int p) { return kl[((p - P0) >> 2) * 256 + (p & 3)]; };
+  const float med = at(tt / 2);
   const int ee = tt - bb;
   int a = 0;
 #pragma unroll
   for (int s = 0; s < kTailMaxExcluded; ++s) {
-    if (s < ee)
-      a += !(sanitize_inf(med - key_f32(key[s])) <= sanitize_inf(key_f32(pick_or(key, s + bb)) - med));
+    if (s < ee) {  // uniform
+      const float lo = v[s], hi = at(bb + s);
+      a += EXACT ? !(sanitize_inf(med - lo) <= sanitize_inf(hi - med)) : !(med - lo <= hi - med);
+    }
   }
+  const int lim = a + bb;
   float acc = 0.f;
 #pragma unroll
-  for (int i = 0; i < NP; ++i) acc += (i >= a && i < a + bb) ? key_f32(key[i]) : 0.f;
+  for (int i = 0; i < NP; ++i) acc += ((i >= kTailMaxExcluded || i >= a) && i < lim) ? v[i] : 0.f;
+  asm volatile("" ::: "memory");  // the scratch is the next group's tile
   return acc * inv_beta;
+}
+
+// One 64-coordinate group of the KR gradient rows: KR * 8 16-byte chunks, KR / 8 per lane.
+// Loads are unconditional (rows >= n point at row 0; zeroed when stored) and global, so
+// all of them are in flight at once; the next group's loads are issued before the current
+// group's compute (register double buffer).
+template <int KR>
+struct TileRegs {
+  static constexpr int NC = KR / 8;
+  u32x4 v[NC];
+};
+
+template <int KR>
+__device__ __forceinline__ void tile_load(TileRegs<KR>& r, const void* const* sptr, int64_t x0, int lane) {
+  typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+#pragma unroll
+  for (int c = 0; c < TileRegs<KR>::NC; ++c) {
+    const int idx = c * 64 + lane, row = idx >> 3, ch = idx & 7;
+    r.v[c] = *(g_u32x4*)(static_cast<const char*>(sptr[row]) + x0 * 2 + ch * 16);
+  }
+}
+
+template <int KR>
+__device__ __forceinline__ void tile_store(unsigned char* tile, const TileRegs<KR>& r, int nn, int lane) {
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int c = 0; c < TileRegs<KR>::NC; ++c) {
+    const int idx = c * 64 + lane, row = idx >> 3, ch = idx & 7;
+    *reinterpret_cast<u32x4*>(tile + row * kMfmaTailPitch + ch * 16) = row < nn ? r.v[c] : zero;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local LDS hand-off
 }
 
 template <int DT, int KR>
 __device__ __forceinline__ void stage_tile(unsigned char* tile, const void* const* sptr, int nn, int64_t x0, int lane) {
-#pragma unroll
-  for (int c0 = 0; c0 < KR * 8; c0 += 64) {
-    const int c = c0 + lane, row = c >> 3, ch = c & 7;
-    u32x4 val = {0u, 0u, 0u, 0u};
-    if (row < nn) val = *reinterpret_cast<const u32x4*>(static_cast<const char*>(sptr[row]) + x0 * 2 + ch * 16);
-    *reinterpret_cast<u32x4*>(tile + row * kMfmaTailPitch + ch * 16) = val;
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // wave-local LDS hand-off
+  TileRegs<KR> r;
+  tile_load<KR>(r, sptr, x0, lane);
+  tile_store<KR>(tile, r, nn, lane);
 }
 
 constexpr int kTailBadSlots = 32;  // per-wave list of 64-coordinate groups needing the exact path
 
 template <int DT, int MB, int KS>
-__global__ __launch_bounds__(256) void k_bulyan_tail_mfma(RowTable rows, int n, int64_t ngroups, int beta,
-                                                          const float* __restrict__ W, int t, void* out,
-                                                          int out_dt) {
-  constexpr int NP = 32 * MB;  // means per coordinate (padded)
-  constexpr int KR = 16 * KS;  // gradient rows (padded)
-  __shared__ __align__(16) unsigned char tiles[4][KR * kMfmaTailPitch];
-  __shared__ __align__(16) uint16_t sA[NP * KR];
+__global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int n, int64_t ngroups, int beta,
+                                                             const float* __restrict__ W, int t, void* out,
+                                                             int out_dt) {
+  constexpr int NP = 32 * MB;   // means per coordinate (padded)
+  constexpr int KR = 16 * KS;   // gradient rows (padded)
+  constexpr int KRP = KR + 8;   // sA pitch: 16-byte fragment reads of 8 consecutive lanes hit distinct banks
+  // per-wave LDS: the gradient tile, then (once its MFMA reads are done) the sorted-means scratch
+  constexpr int WAVE_LDS = KR * kMfmaTailPitch > (NP - NP / 4) * 256 ? KR * kMfmaTailPitch : (NP - NP / 4) * 256;
+  __shared__ __align__(16) unsigned char tiles[4][WAVE_LDS];
+  __shared__ __align__(16) uint16_t sA[NP * KRP];
   __shared__ const void* sptr[KR];
   __shared__ uint64_t smask[NP];
-  __shared__ float sscale[NP];
+  __shared__ __align__(16) float sscale[NP];
+  __shared__ __align__(16) float spad[NP];  // 0 for the t real means, +inf for the padding
   __shared__ int64_t sbad[4][kTailBadSlots];
   __shared__ int sbadn[4];
   const uint16_t one = DT == kBF16 ? 0x3F80 : 0x3C00;
@@ -293,28 +360,37 @@ __global__ __launch_bounds__(256) void k_bulyan_tail_mfma(RowTable rows, int n, 
     float sc = 0.f;
     for (int j = 0; j < KR; ++j) {
       const float w = (k < t && j < n) ? W[k * n + j] : 0.f;
-      sA[k * KR + j] = w != 0.f ? one : 0;
+      sA[k * KRP + j] = w != 0.f ? one : 0;
       if (w != 0.f) { m |= 1ull << j; sc = w; }
     }
     smask[k] = m;
     sscale[k] = sc;
+    spad[k] = k < t ? 0.f : kInf;
   }
   for (int j = threadIdx.x; j < KR; j += blockDim.x) sptr[j] = rows.p[j < n ? j : 0];
   if (threadIdx.x < 4) sbadn[threadIdx.x] = 0;
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned char* tile = tiles[wave];
+  float* ks = reinterpret_cast<float*>(tile);
   // ds_read_b64_tr_b16 addressing: group g = lane / 16 reads rows 8 (g >> 1) + q and
   // columns 16 (g & 1) + 4 p .. + 3 (lane = 16 g + 4 q + p); lane i of the group gets column i
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int tr_off = (8 * (g >> 1) + q) * kMfmaTailPitch + (16 * (g & 1) + 4 * p) * 2;
-  const int a_off = (lane & 31) * KR + 8 * (lane >> 5);
+  const int a_off = (lane & 31) * KRP + 8 * (lane >> 5);
   const float inv_beta = 1.f / static_cast<float>(beta);
   bool overflow = false;
-  for (int64_t gi = static_cast<int64_t>(blockIdx.x) * 4 + wave; gi < ngroups; gi += static_cast<int64_t>(gridDim.x) * 4) {
+  const int64_t gstep = static_cast<int64_t>(gridDim.x) * 4;
+  TileRegs<KR> pre;
+  if (static_cast<int64_t>(blockIdx.x) * 4 + wave < ngroups)
+    tile_load<KR>(pre, sptr, (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 64, lane);
+  for (int64_t gi = static_cast<int64_t>(blockIdx.x) * 4 + wave; gi < ngroups; gi += gstep) {
+    // the LDS tables (sA, scales, pads) are re-read every group: no hoisting into registers
+    asm volatile("" ::: "memory");
     const int64_t x0 = gi * 64;
     const int nn = opaque_uniform(n), tt = opaque_uniform(t), bb = opaque_uniform(beta);
-    stage_tile<DT, KR>(tile, sptr, nn, x0, lane);
+    tile_store<KR>(tile, pre, nn, lane);
+    if (gi + gstep < ngroups) tile_load<KR>(pre, sptr, (gi + gstep) * 64, lane);
     f32x16_t acc[MB][2];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
@@ -323,15 +399,15 @@ __global__ __launch_bounds__(256) void k_bulyan_tail_mfma(RowTable rows, int n, 
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[mb][nb][i] = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+    for (int ks_ = 0; ks_ < KS; ++ks_) {
       s16x8_t afrag[MB];  // S[32 mb + (l & 31)][16 ks + 8 (l >> 5) + 0..7], re-read (frees registers)
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb)
-        afrag[mb] = *reinterpret_cast<const volatile s16x8_t*>(&sA[a_off + 32 * mb * KR + 16 * ks]);
+        afrag[mb] = *reinterpret_cast<const s16x8_t*>(&sA[a_off + 32 * mb * KRP + 16 * ks_]);
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
-        const unsigned char* base = tile + ks * 16 * kMfmaTailPitch + nb * 64 + tr_off;
+        const unsigned char* base = tile + ks_ * 16 * kMfmaTailPitch + nb * 64 + tr_off;
         const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
         const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * kMfmaTailPitch));
         const s16x8_t bfrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -339,7 +415,7 @@ __global__ __launch_bounds__(256) void k_bulyan_tail_mfma(RowTable rows, int n, 
         for (int mb = 0; mb < MB; ++mb) acc[mb][nb] = mfma32x32x16<DT>(afrag[mb], bfrag, acc[mb][nb]);
       }
     }
-    // lane = coordinate: swap the halves so each lane holds all NP means of x0 + lane
+    // lane = coordinate: swap the halves so each lane holds all NP set sums of x0 + lane
     float v[NP];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
@@ -351,14 +427,21 @@ __global__ __launch_bounds__(256) void k_bulyan_tail_mfma(RowTable rows, int n, 
         v[k0] = __uint_as_float(sw[0]);
         v[k0 + 4] = __uint_as_float(sw[1]);
       }
-    bool finite = true;
+    // chk stays 0 unless a sum is inf / NaN (x * 0 is NaN exactly then): such groups
+    // go to the exact pass. mean = sum * scale (+ inf on the padding rows, whose sums are 0)
+    float chk = 0.f;
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const float sc = *reinterpret_cast<volatile float*>(&sscale[k]);
-      v[k] = k < tt ? v[k] * sc : kInf;
-      finite = finite && (k >= tt || isfinite(v[k]));
+    for (int k = 0; k < NP; k += 4) {
+      const f32x4_t sc = *reinterpret_cast<const f32x4_t*>(&sscale[k]);
+      const f32x4_t pd = *reinterpret_cast<const f32x4_t*>(&spad[k]);
+      const float scv[4] = {sc[0], sc[1], sc[2], sc[3]}, pdv[4] = {pd[0], pd[1], pd[2], pd[3]};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        chk = __builtin_fmaf(v[k + c], 0.f, chk);
+        v[k + c] = __builtin_fmaf(v[k + c], scv[c], pdv[c]);
+      }
     }
-    if (__builtin_amdgcn_ballot_w64(!finite)) {  // exact pass later (out of this loop's registers)
+    if (__builtin_amdgcn_ballot_w64(chk != 0.f)) {  // exact pass later (out of this loop's registers)
       const int slot = sbadn[wave];
       if (slot < kTailBadSlots) {
         if (lane == 0) sbad[wave][slot] = gi;
@@ -368,9 +451,9 @@ __global__ __launch_bounds__(256) void k_bulyan_tail_mfma(RowTable rows, int n, 
         overflow = true;
       }
     }
-    store_one(out, out_dt, x0 + lane, window_mean<NP>(v, tt, bb, inv_beta));
+    store_one(out, out_dt, x0 + lane, window_mean<NP, false>(v, tt, bb, inv_beta, ks, lane));
   }
-  // exact pass: groups whose MFMA means were not all finite (inf/NaN inputs), recomputed
+  // exact pass: groups whose MFMA sums were not all finite (inf/NaN inputs), recomputed
   // with direct per-set sums from the LDS tile; after an overflow of the list, every group
   // of this wave is re-examined
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -384,24 +467,24 @@ __global__ __launch_bounds__(256) void k_bulyan_tail_mfma(RowTable rows, int n, 
     stage_tile<DT, KR>(tile, sptr, nn, x0, lane);
     const uint16_t* col = reinterpret_cast<const uint16_t*>(tile) + lane;
     float v[NP];
-    bool finite = true;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       v[k] = kInf;
       if (k < tt) {
-        uint64_t m = uniform64(*reinterpret_cast<volatile uint64_t*>(&smask[k]));
+        uint64_t m = uniform64(lds_volatile(smask[k]));
         float s = 0.f;
 #pragma clang loop unroll(disable)
         while (m) {
           s += cvt16<DT>(col[__builtin_ctzll(m) * (kMfmaTailPitch / 2)]);
           m &= m - 1;
         }
-        v[k] = sanitize_inf(s * *reinterpret_cast<volatile float*>(&sscale[k]));
-        finite = finite && isfinite(v[k]);
+        v[k] = sanitize_inf(s * lds_volatile(sscale[k]));
       }
     }
-    if (__builtin_amdgcn_ballot_w64(!finite))  // only groups that really hold a non-finite mean
-      store_one(out, out_dt, x0 + lane, window_mean<NP>(v, tt, bb, inv_beta));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile reads done before the scratch is written
+    // every listed group is rewritten: its MFMA sums may be NaN (0 * inf from a row outside
+    // every set) while all its set means are finite (after an overflow of the list: every group)
+    store_one(out, out_dt, x0 + lane, window_mean<NP, true>(v, tt, bb, inv_beta, ks, lane));
   }
 }
 
@@ -428,6 +511,7 @@ bool launch_bulyan_tail_mfma(const RowTable& rows, int n, int64_t d, int beta, c
   // measured (profiles/r2): the MFMA means win from t > 16 (n = 32: 1.9 vs 2.6 ms, n = 64: 6.5 vs
   // 10.1 ms per Bulyan call at d = 23.5M); below, the incremental scalar form is faster
   if (DT == kF32 || n > 64 || t > 64 || t <= 16 || t - beta > kTailMaxExcluded || W == nullptr) return false;
+  if (beta < (t <= 32 ? 8 : 16)) return false;  // window_mean reads positions >= NP / 4 only
   const int64_t groups = d / 64;
   const int ks = (n + 15) / 16;
   if (groups > 0) {

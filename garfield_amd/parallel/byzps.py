@@ -126,6 +126,7 @@ class ByzantinePSDataParallel(RobustDataParallel):
     def _server_update(self) -> None:
         cfg = self.cfg
         rows = self._worker_rows()
+        self._collude(rows, [j * self.world + r for j in range(self.k) for r in self.worker_ranks])
         first = self.step_count == 0
         param, mom = self.flat.data[: self.d], self.mom[: self.d]
         if self.device.type == "cuda":

@@ -87,6 +87,11 @@ class EngineConfig:
     # (Krum, Bulyan, Brute, Aksel); identical for the coordinate-wise ones. Redundant
     # (unsharded) aggregation only.
     layerwise: bool = False
+    # estimates of the colluding attacks (lie, empire), applied to the EXCHANGED rows so
+    # they do not depend on how slots are placed on ranks: "fw" = the reference's
+    # (byzWorker.py:108-143: the attacker's own honest gradient + fw - 1 other honest
+    # gradients, here the lowest honest slots), "all" = every honest gradient
+    collusion: str = "fw"
 
 
 class _SlotIssuer:
@@ -366,6 +371,7 @@ class RobustDataParallel:
             self._shard.aggregate_and_update(first)   # starts the exchange unless already started
             self.step_count += 1
             return
+        self._collude([self.G[s] for s in range(self.n)])
         rule = cfg.gar
         kw = dict(cfg.gar_kwargs)
         if cfg.layerwise and rule in LAYERWISE_RULES:
@@ -589,7 +595,8 @@ class RobustDataParallel:
     def _attack_rows(self, lo: int, hi: int, slots=None, gen=_DEFAULT_GEN) -> None:
         """Simulated Byzantine workers of this rank (``slots``: local worker ids, default
         all), on coordinates [lo, hi) of their rows, which hold their honest gradient.
-        Every attack is coordinate-wise; colluders estimate from the honest rows' slices."""
+        Every attack is coordinate-wise. The colluding attacks are skipped here: they
+        run on the exchanged rows (``_collude``)."""
         cfg = self.cfg
         hi = min(hi, self.d)
         if lo >= hi or not cfg.byzantine:
@@ -597,32 +604,40 @@ class RobustDataParallel:
         gen = self._gen if gen is RobustDataParallel._DEFAULT_GEN else gen
         for j in (self.local_slots if slots is None else slots):
             attack = cfg.byzantine.get(self.slot(j))
-            if attack is None:
+            if attack is None or attack in NEEDS_ESTIMATES:
                 continue
             row = self.X[j, self.xr, lo:hi]
-            g = row.float()
-            est = None
-            if attack in NEEDS_ESTIMATES:
-                honest = [self.X[i, self.xr, lo:hi] for i in self.local_slots
-                          if self.slot(i) not in cfg.byzantine and i != j]
-                est = torch.stack([g] + [h.float() for h in honest])
-            row.copy_(apply_attack(attack, g, est, gen))
+            row.copy_(apply_attack(attack, row.float(), None, gen))
 
     def _attack_local_rows(self) -> None:
         """Overwrite the simulated Byzantine workers' rows (after the honest rows exist)."""
-        cfg = self.cfg
-        for j in self.local_slots:
-            attack = cfg.byzantine.get(self.slot(j))
-            if attack is None:
-                continue
-            row = self.X[j, self.xr, : self.d]
-            g = row.float()
-            est = None
-            if attack in NEEDS_ESTIMATES:
-                honest = [self.X[i, self.xr, : self.d] for i in self.local_slots
-                          if self.slot(i) not in cfg.byzantine and i != j]
-                est = torch.stack([g] + [h.float() for h in honest])
-            row.copy_(apply_attack(attack, g, est, self._gen))
+        self._attack_rows(0, self.d)
+
+    def _collude(self, rows, slots=None) -> None:
+        """The colluding attacks (lie, empire) on exchanged rows: ``rows[i]`` is (a
+        coordinate slice of) the row of global slot ``slots[i]`` (default: i) and still
+        holds that worker's honest gradient. Every rank holding the rows computes the
+        same result (deterministic, coordinate-wise), so the sharded form (each owner on
+        its coordinate shard) equals the redundant one.
+
+        Estimates (``cfg.collusion``): "fw" follows the reference
+        (``byzWorker.py:108-143``): the attacker's own honest gradient plus fw - 1 other
+        honest gradients (here: the lowest honest slots), fw = the Byzantine workers
+        among the rows; "all": every honest row."""
+        byz = self.cfg.byzantine
+        if not byz:
+            return
+        slots = list(range(len(rows))) if slots is None else list(slots)
+        targets = [(i, byz[s]) for i, s in enumerate(slots) if byz.get(s) in NEEDS_ESTIMATES]
+        if not targets:
+            return
+        honest = [i for i, s in enumerate(slots) if s not in byz]
+        fw = sum(1 for s in slots if s in byz)
+        peers = honest if self.cfg.collusion == "all" else honest[: max(fw - 1, 0)]
+        ests = [rows[i].float() for i in peers]
+        for i, attack in targets:
+            g = rows[i].float()
+            rows[i].copy_(apply_attack(attack, g, torch.stack([g, *ests]), self._gen))
 
     def _capture_grouped(self) -> None:
         """Capture the grouped forward/backward (+ gradient scatter) as one HIP graph."""

@@ -190,6 +190,7 @@ class ShardedAggregator:
         b.works = []
         if self.e.device.type == "cuda":
             torch.cuda.current_stream(self.e.device).wait_event(b.done)
+        self.e._collude(b.rows)   # colluding attacks on this rank's coordinate shard of every row
 
     def _sum_over_ranks(self, t: torch.Tensor) -> torch.Tensor:
         """Every rank's ``t`` summed in rank order (identical result on every rank)."""

@@ -169,3 +169,53 @@ def test_layerwise_gar_matches_per_tensor_oracle(rule, f):
     assert ((got - expect).norm() / expect.norm()).item() < 1e-5
     flat = ref.krum(G, f) if rule == "krum" else ref.bulyan(G, f)
     assert ((flat - expect).norm() / expect.norm()).item() > 1e-6   # a different rule than the flat one
+
+
+@pytest.mark.parametrize("collusion", ["fw", "all"])
+def test_colluding_attacks_use_exchanged_rows(collusion):
+    """lie / empire run on the exchanged rows: the attacker's own honest gradient plus
+    fw - 1 honest peers (reference byzWorker.py:108-143) or every honest row."""
+    from garfield_amd.runtime.attacks import empire_attack, lie_attack
+
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model("mlp"), F.nll_loss, DistContext(),
+                             EngineConfig(gar="average", f=2, workers_per_rank=8, byzantine={1: "lie", 5: "empire"},
+                                          collusion=collusion))
+    b = synthetic_batches(8, 16, (1, 28, 28), 10, "cpu")
+    eng.compute_local(b)
+    G0 = eng.G.clone()   # every row still honest: the colluders act after the exchange
+    honest = [0, 2, 3, 4, 6, 7]
+    peers = honest[:1] if collusion == "fw" else honest
+    eng.aggregate_and_update()
+    for s, fn in ((1, lie_attack), (5, empire_attack)):
+        want = fn(G0[s], torch.stack([G0[s].float(), *[G0[p].float() for p in peers]]))
+        assert torch.allclose(eng.G[s], want, rtol=1e-6, atol=1e-7)
+    assert torch.equal(eng.G[honest], G0[honest])
+
+
+def _collusion_worker(rank, world, port, outdir, shard):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from garfield_amd.parallel.comm import init_distributed, shutdown
+
+    ctx = init_distributed(backend="gloo", device="cpu")
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                             EngineConfig(gar="median", f=2, workers_per_rank=4, byzantine={1: "lie", 6: "empire"},
+                                          shard_gar=shard, lr=0.05, collusion="all"))
+    b = synthetic_batches(4, 8, (1, 28, 28), 10, "cpu", seed=rank)
+    for _ in range(3):
+        eng.step(b)
+    torch.save({"flat": eng.flat_model().clone()}, os.path.join(outdir, f"{int(shard)}r{rank}.pt"))
+    shutdown(ctx)
+
+
+def test_two_rank_collusion_sharded_matches_allgather():
+    """Colluders on a coordinate shard (owner side) == colluders on gathered rows."""
+    with tempfile.TemporaryDirectory() as d:
+        for shard in (False, True):
+            mp.spawn(_collusion_worker, args=(2, free_port(), d, shard), nprocs=2, join=True)
+        a = torch.load(os.path.join(d, "0r0.pt"), weights_only=True)["flat"]
+        for name in ("0r1.pt", "1r0.pt", "1r1.pt"):
+            other = torch.load(os.path.join(d, name), weights_only=True)["flat"]
+            assert torch.allclose(a, other, rtol=1e-5, atol=1e-6), name

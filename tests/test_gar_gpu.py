@@ -55,13 +55,34 @@ def test_krum_selection_and_output(cuda, n, f, dtype):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("n,f", [(7, 1), (11, 2), (15, 3), (23, 5), (31, 7), (40, 1), (64, 3)])
+@pytest.mark.parametrize("n,f", [(7, 1), (11, 2), (15, 3), (23, 5), (26, 2), (31, 7), (33, 5), (35, 8), (40, 1),
+                                 (64, 3)])
 def test_bulyan(cuda, n, f, dtype):
     X = separated(n, 1500, dtype, cuda, seed=100 + n)
     W = gar.bulyan_weights(X, f).cpu()
     W_ref = ref.bulyan_weights(ref.pairwise_sqdist(X), f).float()
     assert torch.equal(W != 0, W_ref != 0)
     assert close(gar.bulyan(X, f), ref.bulyan(X, f), dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,f", [(26, 2), (40, 1), (64, 3)])
+def test_bulyan_tail_nonfinite_rows_take_exact_pass(cuda, n, f, dtype):
+    """inf / NaN in a row that Krum never selects: the MFMA set sums of those
+    64-coordinate groups turn NaN (0 * inf), so the groups go through the exact
+    per-set pass; the result must equal set means taken by indexing (fp64 oracle)."""
+    d = 64 * 40 + 37
+    X = separated(n, d, torch.float32, "cpu", seed=n)
+    cols = torch.arange(3, d, 97)
+    X[0, cols] = torch.tensor([math.inf, -math.inf, math.nan])[torch.arange(cols.numel()) % 3]
+    X = X.to(dtype)
+    Xc = X.to(cuda)
+    W = gar.bulyan_weights(Xc, f).cpu().double()
+    assert (W[:, 0] == 0).all()
+    t, beta = n - 2 * f - 2, n - 4 * f - 2
+    V = torch.stack([X.double()[W[k] != 0].mean(0) for k in range(t)])
+    want = torch.tensor([ref._closest_mean(V[:, x].tolist(), beta) for x in range(d)])
+    assert close(gar.bulyan(Xc, f), want, dtype)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
