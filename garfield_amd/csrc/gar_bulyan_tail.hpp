@@ -261,17 +261,20 @@ __device__ __forceinline__ void oem_sort_f32(float (&v)[NP]) {
 }
 
 // Sorted means -> mean of the beta closest to the median (window [a, a + beta)).
-// Valid for NP / 2 < t <= NP (the MFMA tail's MB = 1 / 2 ranges): the runtime
-// positions read (the median t / 2 and the excluded highs beta .. t - 1) are all
-// >= NP / 4, so the sorted values from NP / 4 up are spilled to this wave's LDS
-// scratch `ks` ((NP - NP / 4) x 64 floats, [position / 4][lane][position % 4])
-// with static b128 stores and read back at uniform addresses: no select chains
-// over the register array. EXACT: inputs may hold +-inf (NaN already mapped to
-// +inf), so distances are sanitised like the reference's.
+// The runtime positions read (the median t / 2 and the excluded highs beta ..
+// t - 1) must be >= P0 = wm_p0(NP) (host-checked: t / 2 >= P0, beta >= P0): the
+// sorted values from P0 up are spilled to this wave's LDS scratch `ks` ((NP - P0)
+// x 64 floats, [position / 4][lane][position % 4]) with static b128 stores and read
+// back at uniform addresses -- no select chains over the register array. The e
+// lowest stay in registers (static indices). EXACT: inputs may hold +-inf (NaN
+// already mapped to +inf), so distances are sanitised like the reference's.
+constexpr int wm_p0(int np) { return (np / 4) & ~3; }
+
 template <int NP, bool EXACT>
 __device__ __forceinline__ float window_mean(float (&v)[NP], int tt, int bb, float inv_beta, float* ks, int lane) {
-  constexpr int P0 = NP / 4;
-  static_assert(P0 % 4 == 0 && P0 <= kTailMaxExcluded, "window_mean layout");
+  constexpr int P0 = wm_p0(NP);
+  constexpr int SMAX = NP < kTailMaxExcluded ? NP : kTailMaxExcluded;
+  static_assert(P0 <= kTailMaxExcluded, "window_mean layout");
   oem_sort_f32<NP>(v);
 #pragma unroll
   for (int i = P0; i < NP; i += 4)
@@ -283,7 +286,7 @@ __device__ __forceinline__ float window_mean(float (&v)[NP], int tt, int bb, flo
   const int ee = tt - bb;
   int a = 0;
 #pragma unroll
-  for (int s = 0; s < kTailMaxExcluded; ++s) {
+  for (int s = 0; s < SMAX; ++s) {
     if (s < ee) {  // uniform
       const float lo = v[s], hi = at(bb + s);
       a += EXACT ? !(sanitize_inf(med - lo) <= sanitize_inf(hi - med)) : !(med - lo <= hi - med);
@@ -292,7 +295,7 @@ __device__ __forceinline__ float window_mean(float (&v)[NP], int tt, int bb, flo
   const int lim = a + bb;
   float acc = 0.f;
 #pragma unroll
-  for (int i = 0; i < NP; ++i) acc += ((i >= kTailMaxExcluded || i >= a) && i < lim) ? v[i] : 0.f;
+  for (int i = 0; i < NP; ++i) acc += ((i >= SMAX || i >= a) && i < lim) ? v[i] : 0.f;
   asm volatile("" ::: "memory");  // the scratch is the next group's tile
   return acc * inv_beta;
 }
@@ -337,40 +340,51 @@ __device__ __forceinline__ void stage_tile(unsigned char* tile, const void* cons
 
 constexpr int kTailBadSlots = 32;  // per-wave list of 64-coordinate groups needing the exact path
 
-template <int DT, int MB, int KS>
-__global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int n, int64_t ngroups, int beta,
-                                                             const float* __restrict__ W, int t, void* out,
+// One wave per 64-coordinate group (grid-stride). NP = padded set count (8 .. 64),
+// KS = 16-row MFMA k-steps (KR = 16 KS >= n). The t set sums of the group come from
+// v_mfma_f32_32x32x16 (A = the 0/1 set masks in LDS, B = the gradient tile read with
+// ds_read_b64_tr_b16), scaled to means and padded with +inf rows, sorted
+// in registers (window_mean). Groups with a non-finite sum are listed and redone by
+// the exact pass; the partial last group (d % 64) is done there too.
+template <int DT, int NP, int KS>
+__global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int n, int64_t ngroups, int last_width,
+                                                             int beta, const float* __restrict__ W, int t, void* out,
                                                              int out_dt) {
-  constexpr int NP = 32 * MB;   // means per coordinate (padded)
-  constexpr int KR = 16 * KS;   // gradient rows (padded)
-  constexpr int KRP = KR + 8;   // sA pitch: 16-byte fragment reads of 8 consecutive lanes hit distinct banks
+  constexpr int MB = NP > 32 ? 2 : 1;   // 32-row MFMA blocks of sets
+  constexpr int KR = 16 * KS;           // gradient rows (padded)
+  constexpr int KRP = KR + 8;           // sA pitch: 16-byte fragment reads of 8 consecutive lanes hit distinct banks
+  constexpr int P0 = wm_p0(NP);
   // per-wave LDS: the gradient tile, then (once its MFMA reads are done) the sorted-means scratch
-  constexpr int WAVE_LDS = KR * kMfmaTailPitch > (NP - NP / 4) * 256 ? KR * kMfmaTailPitch : (NP - NP / 4) * 256;
+  constexpr int WAVE_LDS = KR * kMfmaTailPitch > (NP - P0) * 256 ? KR * kMfmaTailPitch : (NP - P0) * 256;
   __shared__ __align__(16) unsigned char tiles[4][WAVE_LDS];
-  __shared__ __align__(16) uint16_t sA[NP * KRP];
+  __shared__ __align__(16) uint16_t sA[32 * MB * KRP];
   __shared__ const void* sptr[KR];
   __shared__ uint64_t smask[NP];
   __shared__ __align__(16) float sscale[NP];
   __shared__ __align__(16) float spad[NP];  // 0 for the t real means, +inf for the padding
   __shared__ int64_t sbad[4][kTailBadSlots];
   __shared__ int sbadn[4];
-  const uint16_t one = DT == kBF16 ? 0x3F80 : 0x3C00;
-  for (int k = threadIdx.x; k < NP; k += blockDim.x) {
-    uint64_t m = 0;
-    float sc = 0.f;
-    for (int j = 0; j < KR; ++j) {
-      const float w = (k < t && j < n) ? W[k * n + j] : 0.f;
-      sA[k * KRP + j] = w != 0.f ? one : 0;
-      if (w != 0.f) { m |= 1ull << j; sc = w; }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  {  // set tables: one W row per wave iteration (n <= 64 = lanes), masks by ballot
+    const uint16_t one = DT == kBF16 ? 0x3F80 : 0x3C00;
+    for (int k = wave; k < 32 * MB; k += 4) {
+      const float w = (k < t && lane < n) ? W[k * n + lane] : 0.f;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(w != 0.f);
+      if (lane < KR) sA[k * KRP + lane] = w != 0.f ? one : 0;
+      if (k < NP) {
+        const int first = m ? __builtin_ctzll(m) : 0;
+        const float sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), first));
+        if (lane == 0) {
+          smask[k] = m;
+          sscale[k] = m ? sc : 0.f;
+          spad[k] = k < t ? 0.f : kInf;
+        }
+      }
     }
-    smask[k] = m;
-    sscale[k] = sc;
-    spad[k] = k < t ? 0.f : kInf;
   }
   for (int j = threadIdx.x; j < KR; j += blockDim.x) sptr[j] = rows.p[j < n ? j : 0];
   if (threadIdx.x < 4) sbadn[threadIdx.x] = 0;
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned char* tile = tiles[wave];
   float* ks = reinterpret_cast<float*>(tile);
   // ds_read_b64_tr_b16 addressing: group g = lane / 16 reads rows 8 (g >> 1) + q and
@@ -381,10 +395,10 @@ __global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int 
   const float inv_beta = 1.f / static_cast<float>(beta);
   bool overflow = false;
   const int64_t gstep = static_cast<int64_t>(gridDim.x) * 4;
+  const int64_t gfirst = static_cast<int64_t>(blockIdx.x) * 4 + wave;
   TileRegs<KR> pre;
-  if (static_cast<int64_t>(blockIdx.x) * 4 + wave < ngroups)
-    tile_load<KR>(pre, sptr, (static_cast<int64_t>(blockIdx.x) * 4 + wave) * 64, lane);
-  for (int64_t gi = static_cast<int64_t>(blockIdx.x) * 4 + wave; gi < ngroups; gi += gstep) {
+  if (gfirst < ngroups) tile_load<KR>(pre, sptr, gfirst * 64, lane);
+  for (int64_t gi = gfirst; gi < ngroups; gi += gstep) {
     // the LDS tables (sA, scales, pads) are re-read every group: no hoisting into registers
     asm volatile("" ::: "memory");
     const int64_t x0 = gi * 64;
@@ -400,7 +414,7 @@ __global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int 
         for (int i = 0; i < 16; ++i) acc[mb][nb][i] = 0.f;
 #pragma unroll
     for (int ks_ = 0; ks_ < KS; ++ks_) {
-      s16x8_t afrag[MB];  // S[32 mb + (l & 31)][16 ks + 8 (l >> 5) + 0..7], re-read (frees registers)
+      s16x8_t afrag[MB];  // S[32 mb + (l & 31)][16 ks + 8 (l >> 5) + 0..7]
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb)
         afrag[mb] = *reinterpret_cast<const s16x8_t*>(&sA[a_off + 32 * mb * KRP + 16 * ks_]);
@@ -415,17 +429,19 @@ __global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int 
         for (int mb = 0; mb < MB; ++mb) acc[mb][nb] = mfma32x32x16<DT>(afrag[mb], bfrag, acc[mb][nb]);
       }
     }
-    // lane = coordinate: swap the halves so each lane holds all NP set sums of x0 + lane
+    // lane = coordinate: swap the halves so each lane holds the NP set sums of x0 + lane
     float v[NP];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[mb][0][i]),
-                                                         __float_as_uint(acc[mb][1][i]), false, false);
         const int k0 = 32 * mb + (i & 3) + 8 * (i >> 2);
-        v[k0] = __uint_as_float(sw[0]);
-        v[k0 + 4] = __uint_as_float(sw[1]);
+        if (k0 < NP) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[mb][0][i]),
+                                                           __float_as_uint(acc[mb][1][i]), false, false);
+          v[k0] = __uint_as_float(sw[0]);
+          v[k0 + 4] = __uint_as_float(sw[1]);
+        }
       }
     // chk stays 0 unless a sum is inf / NaN (x * 0 is NaN exactly then): such groups
     // go to the exact pass. mean = sum * scale (+ inf on the padding rows, whose sums are 0)
@@ -454,17 +470,37 @@ __global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int 
     store_one(out, out_dt, x0 + lane, window_mean<NP, false>(v, tt, bb, inv_beta, ks, lane));
   }
   // exact pass: groups whose MFMA sums were not all finite (inf/NaN inputs), recomputed
-  // with direct per-set sums from the LDS tile; after an overflow of the list, every group
-  // of this wave is re-examined
+  // with direct per-set sums from the LDS tile (after an overflow of the list: every
+  // group of this wave); then the partial last group (last_width < 64 coordinates),
+  // which is block 0 / wave 0's
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   const int nbad = overflow ? 0 : sbadn[wave];
-  int64_t gi = overflow ? static_cast<int64_t>(blockIdx.x) * 4 + wave : 0;
-  for (int b = 0; overflow ? gi < ngroups : b < nbad; ++b) {
-    const int64_t gcur = overflow ? gi : sbad[wave][b];
-    if (overflow) gi += static_cast<int64_t>(gridDim.x) * 4;
+  bool partial_pending = last_width > 0 && gfirst == 0;
+  int64_t gi = overflow ? gfirst : 0;
+  for (int b = 0;; ++b) {
+    int64_t gcur;
+    int width = 64;
+    if (overflow ? gi < ngroups : b < nbad) {
+      gcur = overflow ? gi : sbad[wave][b];
+      if (overflow) gi += gstep;
+    } else if (partial_pending) {
+      gcur = ngroups;
+      width = last_width;
+      partial_pending = false;
+    } else {
+      break;
+    }
     const int64_t x0 = gcur * 64;
     const int nn = opaque_uniform(n), tt = opaque_uniform(t), bb = opaque_uniform(beta);
-    stage_tile<DT, KR>(tile, sptr, nn, x0, lane);
+    if (width == 64) {
+      stage_tile<DT, KR>(tile, sptr, nn, x0, lane);
+    } else {  // partial group: per-column loads, columns >= width repeat the first
+      const int64_t xs = x0 + (lane < width ? lane : 0);
+      for (int j = 0; j < KR; ++j)
+        reinterpret_cast<uint16_t*>(tile)[j * (kMfmaTailPitch / 2) + lane] =
+            j < nn ? static_cast<const uint16_t*>(sptr[j])[xs] : 0;
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
     const uint16_t* col = reinterpret_cast<const uint16_t*>(tile) + lane;
     float v[NP];
 #pragma unroll
@@ -483,53 +519,47 @@ __global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int 
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile reads done before the scratch is written
     // every listed group is rewritten: its MFMA sums may be NaN (0 * inf from a row outside
-    // every set) while all its set means are finite (after an overflow of the list: every group)
-    store_one(out, out_dt, x0 + lane, window_mean<NP, true>(v, tt, bb, inv_beta, ks, lane));
+    // every set) while all its set means are finite
+    const float r = window_mean<NP, true>(v, tt, bb, inv_beta, ks, lane);
+    if (lane < width) store_one(out, out_dt, x0 + lane, r);
   }
 }
 
-// t <= 64, n <= 64, bf16/fp16: MFMA means for the 64-coordinate groups, the
-// incremental kernel for the d % 64 tail
-template <int DT, int MB>
-void launch_tail_mfma_ks(int ks, const RowTable& rows, int n, int64_t groups, int beta, const float* W, int t,
-                         void* out, int out_dt, hipStream_t s) {
+template <int DT, int NP>
+void launch_tail_mfma_ks(int ks, const RowTable& rows, int n, int64_t groups, int last_width, int beta,
+                         const float* W, int t, void* out, int out_dt, hipStream_t s) {
   int64_t g = (groups + 3) / 4;
   if (g > 2048) g = 2048;
   if (g < 1) g = 1;
   const dim3 grid(static_cast<unsigned>(g)), block(256);
+#define GARFIELD_TAIL_MFMA(KS)                                                                                   \
+  hipLaunchKernelGGL((k_bulyan_tail_mfma<DT, NP, KS>), grid, block, 0, s, rows, n, groups, last_width, beta, W, t, \
+                     out, out_dt)
   switch (ks) {
-    case 1: hipLaunchKernelGGL((k_bulyan_tail_mfma<DT, MB, 1>), grid, block, 0, s, rows, n, groups, beta, W, t, out, out_dt); break;
-    case 2: hipLaunchKernelGGL((k_bulyan_tail_mfma<DT, MB, 2>), grid, block, 0, s, rows, n, groups, beta, W, t, out, out_dt); break;
-    case 3: hipLaunchKernelGGL((k_bulyan_tail_mfma<DT, MB, 3>), grid, block, 0, s, rows, n, groups, beta, W, t, out, out_dt); break;
-    default: hipLaunchKernelGGL((k_bulyan_tail_mfma<DT, MB, 4>), grid, block, 0, s, rows, n, groups, beta, W, t, out, out_dt); break;
+    case 1: GARFIELD_TAIL_MFMA(1); break;
+    case 2: GARFIELD_TAIL_MFMA(2); break;
+    case 3: GARFIELD_TAIL_MFMA(3); break;
+    default: GARFIELD_TAIL_MFMA(4); break;
   }
+#undef GARFIELD_TAIL_MFMA
 }
 
+// bf16/fp16, n <= 64, t <= 64, e = t - beta <= 16: the MFMA tail (every coordinate,
+// the d % 64 tail in its exact pass); otherwise false (generic kernels)
 template <int DT>
 bool launch_bulyan_tail_mfma(const RowTable& rows, int n, int64_t d, int beta, const float* W, int t, void* out,
                              int out_dt, hipStream_t s) {
-  // measured (profiles/r2): the MFMA means win from t > 16 (n = 32: 1.9 vs 2.6 ms, n = 64: 6.5 vs
-  // 10.1 ms per Bulyan call at d = 23.5M); below, the incremental scalar form is faster
-  if (DT == kF32 || n > 64 || t > 64 || t <= 16 || t - beta > kTailMaxExcluded || W == nullptr) return false;
-  if (beta < (t <= 32 ? 8 : 16)) return false;  // window_mean reads positions >= NP / 4 only
+  if (DT == kF32 || n > 64 || t > 64 || t < 1 || beta < 1 || t - beta > kTailMaxExcluded || W == nullptr) return false;
+  const int np = t <= 8 ? 8 : (t <= 16 ? 16 : (t <= 32 ? 32 : 64));
+  if (t / 2 < wm_p0(np) || beta < wm_p0(np)) return false;   // window_mean's spilled positions
   const int64_t groups = d / 64;
+  const int last = static_cast<int>(d - groups * 64);
   const int ks = (n + 15) / 16;
-  if (groups > 0) {
-    if (t <= 32) launch_tail_mfma_ks<DT, 1>(ks, rows, n, groups, beta, W, t, out, out_dt, s);
-    else launch_tail_mfma_ks<DT, 2>(ks, rows, n, groups, beta, W, t, out, out_dt, s);
-  }
-  const int64_t done = groups * 64;
-  if (done < d) {  // tail coordinates: shifted row table, generic incremental kernel
-    RowTable r2 = rows;
-    for (int i = 0; i < n; ++i) r2.p[i] = static_cast<const char*>(rows.p[i]) + done * 2;
-    void* o2 = static_cast<char*>(out) + done * (out_dt == kF32 ? 4 : 2);
-    const int np = t <= 8 ? 8 : (t <= 16 ? 16 : (t <= 32 ? 32 : 64));
-    switch (np) {
-      case 8: launch_bulyan_tail<DT, 8>(r2, n, d - done, beta, W, t, o2, out_dt, s); break;
-      case 16: launch_bulyan_tail<DT, 16>(r2, n, d - done, beta, W, t, o2, out_dt, s); break;
-      case 32: launch_bulyan_tail<DT, 32>(r2, n, d - done, beta, W, t, o2, out_dt, s); break;
-      default: launch_bulyan_tail<DT, 64>(r2, n, d - done, beta, W, t, o2, out_dt, s); break;
-    }
+  switch (np) {
+    case 8: launch_tail_mfma_ks<DT, 8>(ks, rows, n, groups, last, beta, W, t, out, out_dt, s); break;
+    case 16: launch_tail_mfma_ks<DT, 16>(ks, rows, n, groups, last, beta, W, t, out, out_dt, s); break;
+    case 32: launch_tail_mfma_ks<DT, 32>(ks, rows, n, groups, last, beta, W, t, out, out_dt, s); break;
+    default: launch_tail_mfma_ks<DT, 64>(ks, rows, n, groups, last, beta, W, t, out, out_dt, s); break;
   }
   return true;
 }

@@ -292,20 +292,30 @@ __global__ __launch_bounds__(1024) void k_bulyan_select(const float* __restrict_
     }
   }
   __syncthreads();
-  const int i = threadIdx.x;
+  // t selection steps; each rank count is split over G lanes of one wave (G = 16 for
+  // n <= 64, 8 for n <= 128) and summed with a 16/8-lane butterfly, so a step costs
+  // n / G LDS reads per lane instead of a serial pass over all n scores
+  const int G = n <= 64 ? 16 : 8;
+  const int i = threadIdx.x / G, c = threadIdx.x % G;
   for (int k = 0; k < t; ++k) {
     int mk = m - k;
     if (mk < 1) mk = 1;
+    int r = 0;
     if (i < n) {
-      const int r = score_rank(S, n, i);
+      const float si = sanitize_inf(S[i]);
+      for (int j = c; j < n; j += G) {
+        const float sj = sanitize_inf(S[j]);
+        r += (sj < si) || (sj == si && j < i);
+      }
+    }
+    for (int o = G / 2; o >= 1; o >>= 1) r += __shfl_xor(r, o, G);
+    if (i < n && c == 0) {
       W[k * n + i] = r < mk ? 1.f / static_cast<float>(mk) : 0.f;
       if (r == 0) best = i;
     }
     __syncthreads();
     const int id = best;
-    if (i < n && i != id) S[i] -= D[i * (n + 1) + id];
-    __syncthreads();
-    if (i == 0) S[id] = FLT_MAX;
+    if (i < n && c == 0) S[i] = i == id ? FLT_MAX : S[i] - D[i * (n + 1) + id];
     __syncthreads();
   }
 }
