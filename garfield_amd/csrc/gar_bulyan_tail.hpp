@@ -237,8 +237,7 @@ __device__ __forceinline__ f32x16_t mfma32x32x16(s16x8_t a, s16x8_t b, f32x16_t 
                                                   0, 0, 0);
 }
 
-// odd-even merge sort on floats (no NaN: callers map NaN to +inf first). The
-// inputs are arithmetic results, so fminf/fmaxf need no canonicalisation here
+// odd-even merge sort on floats (no NaN: callers map NaN to +inf first)
 template <int NP>
 __device__ __forceinline__ void oem_sort_f32(float (&v)[NP]) {
 #pragma unroll
@@ -311,12 +310,13 @@ struct TileRegs {
 };
 
 template <int KR>
-__device__ __forceinline__ void tile_load(TileRegs<KR>& r, const void* const* sptr, int64_t x0, int lane) {
+__device__ __forceinline__ void tile_load(TileRegs<KR>& r, const void* const* sptr, int64_t x0, int lane, int nn) {
   typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
 #pragma unroll
   for (int c = 0; c < TileRegs<KR>::NC; ++c) {
     const int idx = c * 64 + lane, row = idx >> 3, ch = idx & 7;
-    r.v[c] = *(g_u32x4*)(static_cast<const char*>(sptr[row]) + x0 * 2 + ch * 16);
+    if (c * 8 < nn)  // uniform: chunks of padding rows only are not loaded (tile_store zeroes them)
+      r.v[c] = *(g_u32x4*)(static_cast<const char*>(sptr[row]) + x0 * 2 + ch * 16);
   }
 }
 
@@ -334,7 +334,7 @@ __device__ __forceinline__ void tile_store(unsigned char* tile, const TileRegs<K
 template <int DT, int KR>
 __device__ __forceinline__ void stage_tile(unsigned char* tile, const void* const* sptr, int nn, int64_t x0, int lane) {
   TileRegs<KR> r;
-  tile_load<KR>(r, sptr, x0, lane);
+  tile_load<KR>(r, sptr, x0, lane, nn);
   tile_store<KR>(tile, r, nn, lane);
 }
 
@@ -397,14 +397,14 @@ __global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int 
   const int64_t gstep = static_cast<int64_t>(gridDim.x) * 4;
   const int64_t gfirst = static_cast<int64_t>(blockIdx.x) * 4 + wave;
   TileRegs<KR> pre;
-  if (gfirst < ngroups) tile_load<KR>(pre, sptr, gfirst * 64, lane);
+  if (gfirst < ngroups) tile_load<KR>(pre, sptr, gfirst * 64, lane, n);
   for (int64_t gi = gfirst; gi < ngroups; gi += gstep) {
     // the LDS tables (sA, scales, pads) are re-read every group: no hoisting into registers
     asm volatile("" ::: "memory");
     const int64_t x0 = gi * 64;
     const int nn = opaque_uniform(n), tt = opaque_uniform(t), bb = opaque_uniform(beta);
     tile_store<KR>(tile, pre, nn, lane);
-    if (gi + gstep < ngroups) tile_load<KR>(pre, sptr, (gi + gstep) * 64, lane);
+    if (gi + gstep < ngroups) tile_load<KR>(pre, sptr, (gi + gstep) * 64, lane, nn);  // flies during this group
     f32x16_t acc[MB][2];
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb)
@@ -448,6 +448,7 @@ __global__ __launch_bounds__(256, 2) void k_bulyan_tail_mfma(RowTable rows, int 
     float chk = 0.f;
 #pragma unroll
     for (int k = 0; k < NP; k += 4) {
+      if (k % 8 == 0) asm volatile("" ::: "memory");  // scale / pad reads in chunks (registers)
       const f32x4_t sc = *reinterpret_cast<const f32x4_t*>(&sscale[k]);
       const f32x4_t pd = *reinterpret_cast<const f32x4_t*>(&spad[k]);
       const float scv[4] = {sc[0], sc[1], sc[2], sc[3]}, pdv[4] = {pd[0], pd[1], pd[2], pd[3]};
