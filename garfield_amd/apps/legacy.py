@@ -23,10 +23,13 @@ PS
     the PSes (fastest 2·f_ps + 3, or all), take their median, apply it; otherwise
     apply the aggregate itself.
 
-On the ``MessageExchange`` service a PS publishes its aggregated gradients in its
-gradient history and uses its model history for the PS-to-PS exchange (entry
-t + 1 = aggregate of iteration t; entry 0 is the initial model that workers pull
-first, the reference's ``GetUnifiedModel``). Byzantine workers use the TF_CONFIG
+Nodes talk over the reference's legacy ``TrainMessageExchange`` service
+(``all.proto``; ``grpcnet/service.py:TrainMessageExchangeService``): a PS publishes
+its aggregated gradients in its gradient history (``GetGradients(iter)``) and uses
+its model history for the PS-to-PS exchange (``GetModel``: entry t + 1 = aggregate of
+iteration t; entry 0 is the initial model that workers pull first with
+``GetUnifiedModel``); workers serve their gradients with ``GetGradients`` (plus the
+Kardam Lipschitz value in ``--smart`` mode). Byzantine workers use the TF_CONFIG
 attack (``Poison1``/``Poison2`` = the malformed-input attack of ``mnistAttack``);
 a Byzantine PS corrupts the aggregate it publishes.
 """
@@ -107,6 +110,15 @@ def _quorum(n: int, f: int) -> int:
     return min(2 * f + 3, n)
 
 
+def _use_legacy_service(node) -> None:
+    """Talk to the peers over ``TrainMessageExchange`` (the reference's legacy service,
+    ``all.proto``); every node serves it next to ``MessageExchange``."""
+    for st in node.ps_connections + node.worker_connections:
+        st.close()
+    node.ps_connections = [svc.LegacyStub(h) for h in node.ps_hosts]
+    node.worker_connections = [svc.LegacyStub(h) for h in node.worker_hosts]
+
+
 class LegacyWorker(Worker):
     """Worker with its own replica (reference ``byzWorker.py``)."""
 
@@ -119,6 +131,7 @@ class LegacyWorker(Worker):
         self.poison = POISON.get(attack, 0)
         self.attacker = Attacker(attack, seed=1000 + self.task_id) if attack not in ("None", *POISON) else None
         self._gen = torch.Generator().manual_seed(3000 + self.task_id)
+        _use_legacy_service(self)
 
     def compute_gradients(self, iter):
         if not self.poison:
@@ -138,9 +151,15 @@ class LegacyWorker(Worker):
 
     def pull_aggregates(self, it: int, ps_index: int | None, quorum: int | None) -> list[torch.Tensor]:
         stubs = self.ps_connections if ps_index is None else [self.ps_connections[ps_index]]
-        replies = svc.pull(stubs, "GetGradient", it, self.job, self.task_id, quorum, retries=self.retries,
+        replies = svc.pull(stubs, "GetGradients", it, self.job, self.task_id, quorum, retries=self.retries,
                            retry_delay=self.retry_delay)
         return self._to_device(replies)
+
+    def unified_model(self) -> torch.Tensor:
+        """The initial model from PS 0 (``GetUnifiedModel``)."""
+        replies = svc.pull(self.ps_connections[:1], "GetUnifiedModel", 0, self.job, self.task_id, 1,
+                           retries=self.retries, retry_delay=self.retry_delay)
+        return self._to_device(replies)[0]
 
 
 class LegacyPS(Server):
@@ -154,13 +173,14 @@ class LegacyPS(Server):
         self.opt = _optimizer(self.model, a.rate)
         attack = network.get_my_attack()
         self.attacker = Attacker(attack, seed=2000 + self.task_id) if attack != "None" else None
+        _use_legacy_service(self)
 
     def publish(self, it: int, aggregate: torch.Tensor) -> None:
         out = self.attacker.attack(aggregate) if self.attacker is not None else aggregate
         self.service.gradients_history.put(it, out)
 
     def worker_gradients(self, it: int, quorum: int | None) -> list[torch.Tensor]:
-        replies = svc.pull(self.worker_connections, "GetGradient", it, self.job, self.task_id, quorum,
+        replies = svc.pull(self.worker_connections, "GetGradients", it, self.job, self.task_id, quorum,
                            retries=self.retries, retry_delay=self.retry_delay)
         return self._to_device(replies)
 
@@ -176,7 +196,7 @@ def run_worker(a, n: Network) -> dict:
     w.start()
     num_ps = len(n.get_all_ps())
     T = period(a)
-    w.write_model(w.get_models(0, 1)[0] if num_ps else w.flat_model())   # GetUnifiedModel from a PS
+    w.write_model(w.unified_model() if num_ps else w.flat_model())
     q_ps = _quorum(num_ps, a.nbbyzps) if a.asyncr else num_ps
     # the reference aggregates the PS replies with Krum(f_ps); Krum needs f >= 1 and
     # n >= 2f + 3, so without declared Byzantine PSes (or too few PSes) the median
@@ -203,6 +223,7 @@ def run_worker(a, n: Network) -> dict:
                                  "num_workers": len(n.get_all_workers())})
             if st is not None:
                 lip.append((it, st.lipschitz, st.threshold, st.accept))
+                w.service.legacy.lipschitz[it] = float(st.lipschitz)   # served with GetGradients(it)
         w.commit_gradients(grad)
         losses.append(loss)
     w.linger(a.max_steps, a.linger)

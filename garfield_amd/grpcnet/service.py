@@ -166,16 +166,71 @@ class MessageExchangeService:
         return proto.Response(iter=it, job="gradient")
 
 
+class TrainMessageExchangeService:
+    """The legacy ``TrainMessageExchange`` service (reference
+    ``Garfield_legacy/all.proto:5-65``, ``grpc_service_impl.py:42-66``) over a node's
+    MessageExchangeService histories:
+
+    * ``GetUnifiedModel(Empty)``: the initial model (model history entry 0);
+    * ``GetGradients(Request)``: gradient history entry ``iter`` -- a worker's gradient,
+      or the aggregated gradient a PS published for that iteration -- with the
+      Lipschitz value the node recorded for it (``lipschitz``, 0 if none);
+    * ``GetModel(Request)``: model history entry ``iter`` (the PS-to-PS exchange).
+
+    The hash / signature / public-key methods were never implemented by the reference
+    either; they answer UNIMPLEMENTED."""
+
+    def __init__(self, base: MessageExchangeService):
+        self.base = base
+        self.lipschitz: dict[int, float] = {}
+
+    def GetUnifiedModel(self, request, context):
+        b = self.base
+        data = b._get(b.model_weights_history, 0, context)
+        if data is None or not context.is_active():
+            return proto.LEGACY["Model"]()
+        b._mark("GetModel", 0)
+        return proto.LEGACY["Model"](model=data, init=True, iter=0)
+
+    def GetGradients(self, request, context):
+        b = self.base
+        data = b._get(b.gradients_history, request.iter, context)
+        if data is None or not context.is_active():
+            return proto.LEGACY["Gradients"]()
+        b._mark("GetGradient", request.iter)
+        return proto.LEGACY["Gradients"](gradients=data, iter=float(request.iter),
+                                           lipschitz=float(self.lipschitz.get(int(request.iter), 0.0)))
+
+    def GetModel(self, request, context):
+        b = self.base
+        data = b._get(b.model_weights_history, request.iter, context)
+        if data is None or not context.is_active():
+            return proto.LEGACY["Model"]()
+        b._mark("GetModel", request.iter)
+        return proto.LEGACY["Model"](model=data, init=True, iter=request.iter)
+
+    def _unimplemented(self, request, context):
+        context.abort(grpc.StatusCode.UNIMPLEMENTED, "not implemented (as in the reference)")
+
+    GetPublicKey = GetCompleteModel = GetOnlyHash = GetGradHashes = GetGradHash = _unimplemented
+
+
+def _handlers(impl, methods, classes) -> dict:
+    return {meth: grpc.unary_unary_rpc_method_handler(getattr(impl, meth), request_deserializer=classes[req].FromString,
+                                                      response_serializer=classes[resp].SerializeToString)
+            for meth, req, resp in methods}
+
+
 def make_server(service: MessageExchangeService, port: int | str, max_workers: int = 30,
                 host: str | None = None) -> tuple[grpc.Server, int]:
-    """gRPC server exposing ``service`` on ``host:port`` (port 0 → any free port)."""
-    handlers = {}
-    for meth, req, resp in proto.METHODS:
-        handlers[meth] = grpc.unary_unary_rpc_method_handler(
-            getattr(service, meth), request_deserializer=proto.CLASSES[req].FromString,
-            response_serializer=proto.CLASSES[resp].SerializeToString)
+    """gRPC server exposing ``service`` on ``host:port`` (port 0 → any free port), as
+    ``MessageExchange`` and as the legacy ``TrainMessageExchange`` (``service.legacy``)."""
+    service.legacy = TrainMessageExchangeService(service)
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers), options=GRPC_OPTIONS)
-    server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(proto.SERVICE, handlers),))
+    server.add_generic_rpc_handlers((
+        grpc.method_handlers_generic_handler(proto.SERVICE, _handlers(service, proto.METHODS, proto.CLASSES)),
+        grpc.method_handlers_generic_handler(proto.LEGACY_SERVICE, _handlers(service.legacy, proto.LEGACY_METHODS,
+                                                                             proto.LEGACY))))
     for h in ([host] if host else ["[::]", "0.0.0.0"]):
         try:
             bound = server.add_insecure_port(f"{h}:{port}")
@@ -200,6 +255,28 @@ class Stub:
     def close(self) -> None:
         self.channel.close()
 
+    @staticmethod
+    def request(method: str, it: int, job: str, req_id: int):
+        return proto.Request(iter=int(it), job=job, req_id=int(req_id))
+
+
+class LegacyStub(Stub):
+    """Client of a peer's ``TrainMessageExchange`` service (legacy Garfield clients)."""
+
+    def __init__(self, target: str):
+        self.target = target
+        self.channel = grpc.insecure_channel(target, options=GRPC_OPTIONS)
+        for meth, req, resp in proto.LEGACY_METHODS:
+            setattr(self, meth, self.channel.unary_unary(
+                f"/{proto.LEGACY_SERVICE}/{meth}", request_serializer=proto.LEGACY[req].SerializeToString,
+                response_deserializer=proto.LEGACY[resp].FromString))
+
+    @staticmethod
+    def request(method: str, it: int, job: str, req_id: int):
+        if method in ("GetUnifiedModel", "GetPublicKey"):
+            return proto.LEGACY["Empty"]()
+        return proto.LEGACY["Request"](iter=int(it), req_id=int(req_id))
+
 
 def set_connection(host: str) -> Stub:
     return Stub(host)
@@ -211,13 +288,13 @@ def _payload(resp) -> bytes:
 
 def pull(stubs: list[Stub], method: str, it: int, job: str, req_id: int, quorum: int | None = None,
          retries: int = 10, retry_delay: float = 5.0, timeout: float = 300.0) -> list[tuple[int, np.ndarray]]:
-    """Concurrent ``method`` (GetModel / GetGradient) on every stub; returns the first
+    """Concurrent ``method`` (GetModel / GetGradient; on ``LegacyStub``s GetUnifiedModel /
+    GetGradients / GetModel) on every stub; returns the first
     ``quorum`` replies (all by default) as ``(peer_index, fp32 vector)`` in arrival
     order. Failed peers are retried ``retries`` times with ``retry_delay`` seconds
     between attempts (reference: 5 s sleeps, 10 or 100 attempts)."""
     n = len(stubs)
     q = n if quorum is None or quorum < 0 else min(int(quorum), n)
-    req = proto.Request(iter=int(it), job=job, req_id=int(req_id))
     done: list[tuple[int, np.ndarray]] = []
     failed: dict[int, Exception] = {}
     cv = threading.Condition()
@@ -228,6 +305,7 @@ def pull(stubs: list[Stub], method: str, it: int, job: str, req_id: int, quorum:
         with cv:
             if len(done) >= q:
                 return
+            req = stubs[i].request(method, it, job, req_id)
             fut = getattr(stubs[i], method).future(req, timeout=timeout, wait_for_ready=True)
             pending[i] = fut
         fut.add_done_callback(lambda f, i=i: on_done(i, f))

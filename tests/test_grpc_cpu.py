@@ -163,3 +163,37 @@ def test_grpc_learn(tmp_path):
     for i in range(n):
         acc = json.loads((tmp_path / f"node{i}.json").read_text())["accuracy"]
         assert acc[-1][1] > acc[0][1] + 5, acc
+
+
+def test_legacy_train_message_exchange_service():
+    """Every node also serves the reference's legacy TrainMessageExchange (all.proto):
+    GetUnifiedModel / GetGradients / GetModel answer from the node's histories, the
+    hash / signature methods are UNIMPLEMENTED (as in the reference), and the wire
+    format follows all.proto's field numbers."""
+    import grpc
+
+    L = proto.LEGACY
+    assert L["Gradients"](gradients=b"ab", iter=2.0, lipschitz=1.5).SerializeToString() == \
+        b"\n\x02ab\x15\x00\x00\x00@\x1d\x00\x00\xc0?"
+    assert L["Request"](iter=3, req_id=-1).SerializeToString() == b"\x08\x03\x10\xff\xff\xff\xff\xff\xff\xff\xff\xff\x01"
+    base = S.MessageExchangeService(np.arange(4, dtype=np.float32), wait_timeout=10)
+    server, port = S.make_server(base, 0, host="127.0.0.1")
+    server.start()
+    try:
+        stub = S.LegacyStub(f"127.0.0.1:{port}")
+        m = stub.GetUnifiedModel(L["Empty"](), timeout=10)
+        assert m.init and S.from_bytes(m.model).tolist() == [0, 1, 2, 3]
+        base.gradients_history.put(0, np.full(3, 7, np.float32))
+        base.legacy.lipschitz[0] = 0.25
+        g = stub.GetGradients(L["Request"](iter=0, req_id=5), timeout=10)
+        assert S.from_bytes(g.gradients).tolist() == [7, 7, 7] and g.iter == 0 and g.lipschitz == 0.25
+        assert base.served("GetGradient", 0) == 1
+        base.model_weights_history.put(1, np.ones(2, np.float32))
+        got = S.pull([stub], "GetModel", 1, "ps", -1)
+        assert got[0][1].tolist() == [1, 1]
+        with pytest.raises(grpc.RpcError) as e:
+            stub.GetPublicKey(L["Empty"](), timeout=10)
+        assert e.value.code() == grpc.StatusCode.UNIMPLEMENTED
+        stub.close()
+    finally:
+        server.stop(0)
