@@ -34,6 +34,7 @@ from garfield_amd.models import build_model
 from garfield_amd.parallel.byzps import ByzantinePSDataParallel, ByzPSConfig
 from garfield_amd.parallel.comm import init_distributed, shutdown
 from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel
+from garfield_amd.parallel.quorum import QuorumConfig, QuorumDataParallel
 from garfield_amd.utils.checkpoint import Checkpoints
 from garfield_amd.utils.logging import info, set_rank_prefix
 
@@ -63,6 +64,10 @@ def parse(argv=None):
     p.add_argument("--ps_attack", default="", help="attack of the fps Byzantine servers")
     p.add_argument("--ps_workers", type=str2bool, default=False,
                    help="Byzantine-server mode: server ranks also host --workers_per_rank logical workers")
+    p.add_argument("--quorum", type=int, default=0,
+                   help="aggregate only the rows of the fastest QUORUM ranks each step (reference server.py:134-155, "
+                        "fastest n - f; parallel/quorum.py); 0 = wait for every rank")
+    p.add_argument("--straggler", default="", help="fault injection for --quorum: RANK:SECONDS[,RANK:SECONDS]")
     p.add_argument("--backend", default=None, help="nccl (RCCL) or gloo")
     p.add_argument("--exchange_dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--cuda_graph", type=str2bool, default=True)
@@ -119,6 +124,9 @@ def main(argv=None, results: dict | None = None):
         eng = ByzantinePSDataParallel(model, loss_fn, ctx,
                                       ByzPSConfig(num_ps=a.num_ps, fps=a.fps, mar=mar, ps_attack=a.ps_attack,
                                                   ps_workers=a.ps_workers, **common))
+    elif a.quorum:
+        delays = {int(r): float(t) for r, t in (x.split(":") for x in a.straggler.split(",") if x)}
+        eng = QuorumDataParallel(model, loss_fn, ctx, QuorumConfig(quorum=a.quorum, straggler_delay=delays, **common))
     else:
         eng = RobustDataParallel(model, loss_fn, ctx, EngineConfig(**common))
     # data: logical worker j of rank r trains on partition (its worker index)
@@ -155,6 +163,8 @@ def main(argv=None, results: dict | None = None):
             ck.save(eng, write=ctx.rank == 0)   # every rank: collectives of the sharded engine
     if ck is not None and not a.checkpoint_freq:
         ck.save(eng, write=ctx.rank == 0)
+    if hasattr(eng, "finish"):
+        eng.finish()   # quorum engine: late rows still in flight
     acc = eng.evaluate(test, binary=ncls == 1)
     checksum = eng.replica_checksum()   # collective in sharded runs
     if ctx.rank == 0:

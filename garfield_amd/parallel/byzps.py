@@ -124,45 +124,9 @@ class ByzantinePSDataParallel(RobustDataParallel):
         return loss
 
     def _server_update(self) -> None:
-        cfg = self.cfg
         rows = self._worker_rows()
         self._collude(rows, [j * self.world + r for j in range(self.k) for r in self.worker_ranks])
-        first = self.step_count == 0
-        param, mom = self.flat.data[: self.d], self.mom[: self.d]
-        if self.device.type == "cuda":
-            C = self._C
-            if cfg.gar in WEIGHTED_RULES:
-                kw = {}
-                if cfg.gar == "krum":
-                    w = gar.krum_weights(rows, cfg.f, cfg.m)
-                elif cfg.gar == "brute":
-                    w = gar.brute_weights(rows, cfg.f)
-                elif cfg.gar == "aksel":
-                    w = gar.aksel_weights(rows, cfg.f, cfg.gar_kwargs.get("mode", "mid"))
-                else:
-                    w = torch.full((len(rows),), 1.0 / len(rows), device=self.device)
-                del kw
-                self.last_weights = w
-                C.gpu_combine_sgd(rows, w, param, mom, None, None, cfg.lr, cfg.momentum, cfg.dampening,
-                                  cfg.weight_decay, cfg.nesterov, first)
-                return
-            g = gar.aggregate(cfg.gar, rows, **self._gar_kwargs()).float()
-            C.gpu_combine_sgd([g], self._one, param, mom, None, None, cfg.lr, cfg.momentum, cfg.dampening,
-                              cfg.weight_decay, cfg.nesterov, first)
-        else:
-            g = gar.aggregate(cfg.gar, rows, **self._gar_kwargs()).float()
-            self._sgd_cpu(g, first)
-
-    def _gar_kwargs(self) -> dict:
-        cfg = self.cfg
-        kw = dict(cfg.gar_kwargs)
-        if cfg.gar not in ("average", "median", "average-nan"):
-            kw["f"] = cfg.f
-        if cfg.m is not None and cfg.gar in ("krum", "bulyan"):
-            kw["m"] = cfg.m
-        if cfg.gar == "condense":
-            kw.setdefault("seed", cfg.seed + self.step_count)
-        return kw
+        self._update_from_rows(rows)
 
     def _write_mar(self, models: list) -> None:
         cfg = self.cfg

@@ -460,6 +460,45 @@ class RobustDataParallel:
         else:
             raise ValueError(rule)
 
+    def _rule_kwargs(self) -> dict:
+        cfg = self.cfg
+        kw = dict(cfg.gar_kwargs)
+        if cfg.gar not in ("average", "median", "average-nan"):
+            kw["f"] = cfg.f
+        if cfg.m is not None and cfg.gar in ("krum", "bulyan"):
+            kw["m"] = cfg.m
+        if cfg.gar == "condense":
+            kw.setdefault("seed", cfg.seed + self.step_count)
+        return kw
+
+    def _update_from_rows(self, rows: list) -> None:
+        """GAR over an explicit list of gradient rows (any subset of the slots, e.g. the
+        Byzantine-PS workers or a quorum) + the SGD update of this replica."""
+        cfg = self.cfg
+        first = self.step_count == 0
+        param, mom = self.flat.data[: self.d], self.mom[: self.d]
+        if self.device.type == "cuda":
+            C = self._C
+            if cfg.gar in WEIGHTED_RULES:
+                if cfg.gar == "krum":
+                    w = gar.krum_weights(rows, cfg.f, cfg.m)
+                elif cfg.gar == "brute":
+                    w = gar.brute_weights(rows, cfg.f)
+                elif cfg.gar == "aksel":
+                    w = gar.aksel_weights(rows, cfg.f, cfg.gar_kwargs.get("mode", "mid"))
+                else:
+                    w = torch.full((len(rows),), 1.0 / len(rows), device=self.device)
+                self.last_weights = w
+                C.gpu_combine_sgd(rows, w, param, mom, None, self._shadow, cfg.lr, cfg.momentum, cfg.dampening,
+                                  cfg.weight_decay, cfg.nesterov, first)
+                return
+            g = gar.aggregate(cfg.gar, rows, **self._rule_kwargs()).float()
+            C.gpu_combine_sgd([g], self._one, param, mom, None, self._shadow, cfg.lr, cfg.momentum, cfg.dampening,
+                              cfg.weight_decay, cfg.nesterov, first)
+        else:
+            g = gar.aggregate(cfg.gar, rows, **self._rule_kwargs()).float()
+            self._sgd_cpu(g, first)
+
     def _sgd_cpu(self, g: torch.Tensor, first: bool) -> None:
         cfg = self.cfg
         p, buf = self.flat.data[: self.d], self.mom[: self.d]

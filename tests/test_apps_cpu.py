@@ -169,3 +169,16 @@ def test_garfield_cc_byzantine_servers_hosting_workers():
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
     m = re.search(r"final accuracy ([0-9.]+)", out.stdout + out.stderr)
     assert m and float(m.group(1)) > 15.0
+
+
+def test_garfield_cc_fastest_quorum_with_straggler():
+    """--quorum 2 of 3 ranks with rank 2 delayed (fault injection): the run completes and
+    prints one replica checksum (all replicas applied the leader's quorum sets)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "3", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), "-m", "garfield_amd.apps.garfield_cc", "--model", "mlp", "--dataset",
+           "mnist", "--loss", "nll", "--lr", "0.05", "--aggregator", "median", "--fw", "1", "--attack", "reverse",
+           "--workers_per_rank", "2", "--num_iter", "8", "--quorum", "2", "--straggler", "2:0.3"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+    assert re.search(r"final accuracy ([0-9.]+)", out.stdout + out.stderr)

@@ -1,0 +1,76 @@
+"""Fastest-quorum aggregation on collectives (parallel/quorum.py), 3 gloo ranks on CPU.
+
+Reference semantics: the PS aggregates the fastest n - f gradients
+(pytorch_impl/libs/garfieldpp/server.py:134-155)."""
+import os
+import socket
+import tempfile
+import time
+
+import torch
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+from garfield_amd.models import build_model
+from garfield_amd.parallel.quorum import QuorumConfig, QuorumDataParallel
+from garfield_amd.parallel.engine import synthetic_batches
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+STEPS, DELAY = 6, 0.6
+
+
+def _worker(rank, world, port, outdir, quorum, delay):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from garfield_amd.parallel.comm import init_distributed, shutdown
+
+    ctx = init_distributed(backend="gloo", device="cpu")
+    torch.manual_seed(0)
+    eng = QuorumDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                             QuorumConfig(gar="median", f=1, workers_per_rank=2, quorum=quorum, lr=0.05,
+                                          byzantine={1: "reverse"}, straggler_delay={2: delay}))
+    b = synthetic_batches(2, 8, (1, 28, 28), 10, "cpu", seed=rank)
+    eng.step(b)   # warm-up (process groups connect)
+    t0 = time.time()
+    quorums = []
+    for _ in range(STEPS):
+        eng.step(b)
+        quorums.append(eng.last_quorum)
+    elapsed = time.time() - t0
+    eng.finish()
+    torch.save({"flat": eng.flat_model().clone(), "t": elapsed, "q": quorums, "skipped": eng.skipped},
+               os.path.join(outdir, f"r{rank}.pt"))
+    shutdown(ctx)
+
+
+def _run(quorum, delay):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(3, free_port(), d, quorum, delay), nprocs=3, join=True)
+        return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(3)]
+
+
+def test_straggler_outside_the_quorum_does_not_slow_the_others():
+    out = _run(quorum=2, delay=DELAY)
+    # every replica applied the same updates (the leader's quorum sets, the same rows)
+    assert torch.equal(out[0]["flat"], out[1]["flat"]) and torch.equal(out[0]["flat"], out[2]["flat"])
+    # ranks 0 / 1 never waited for rank 2's delayed rows
+    assert all(q == [0, 1] for q in out[0]["q"])
+    assert out[0]["t"] < STEPS * DELAY / 2, out[0]["t"]
+    assert out[1]["t"] < STEPS * DELAY / 2, out[1]["t"]
+    assert torch.isfinite(out[0]["flat"]).all()
+
+
+def test_full_quorum_waits_for_everyone_and_matches():
+    out = _run(quorum=3, delay=0.2)
+    assert all(q == [0, 1, 2] for q in out[0]["q"])
+    assert out[0]["t"] >= STEPS * 0.2 * 0.9
+    assert torch.equal(out[0]["flat"], out[2]["flat"])
