@@ -48,14 +48,21 @@ class DistContext:
 
 def init_distributed(backend: str | None = None, device: str | None = None, timeout_s: float = 1800.0) -> DistContext:
     """Initialise ``torch.distributed`` from the torchrun environment (RANK, WORLD_SIZE,
-    LOCAL_RANK, MASTER_ADDR/PORT). One process per GPU; RCCL when GPUs are present."""
+    LOCAL_RANK, MASTER_ADDR/PORT). One process per GPU; RCCL when GPUs are present.
+
+    Rehearsal knobs (multi-rank GPU code paths on a one-GPU box, where RCCL refuses
+    two ranks on one device): ``GARFIELD_DIST_BACKEND`` overrides the backend (e.g.
+    ``gloo``, which takes GPU tensors), ``GARFIELD_SHARE_GPU=1`` maps local rank r to
+    device ``r % device_count``."""
+    backend = backend or os.environ.get("GARFIELD_DIST_BACKEND") or None
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available() if device is None else device.startswith("cuda")
     if use_cuda:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        idx = local % max(torch.cuda.device_count(), 1) if os.environ.get("GARFIELD_SHARE_GPU") == "1" else local
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
     else:
         dev = torch.device("cpu")
     backend = backend or ("nccl" if use_cuda else "gloo")
@@ -76,13 +83,19 @@ def shutdown(ctx: DistContext) -> None:
         dist.destroy_process_group()
 
 
+def gloo_backend(group=None) -> bool:
+    """True when the collectives run on gloo (which rejects an input aliasing the output,
+    on CPU and GPU tensors alike)."""
+    return dist.is_initialized() and dist.get_backend(group) == "gloo"
+
+
 def all_gather_rows(out_rows: torch.Tensor, rank: int, group=None, async_op: bool = False):
     """In-place all-gather of ``out_rows[rank]`` into every row of ``out_rows`` ([world, ld], contiguous).
 
     The output is passed flat (gloo requires it; RCCL does not care) and the input
     is this rank's own row, i.e. NCCL/RCCL's in-place all-gather form."""
     assert out_rows.is_contiguous()
-    if out_rows.device.type == "cpu":
+    if gloo_backend(group):
         # gloo does not support the in-place form (input aliasing the output)
         return dist.all_gather_into_tensor(out_rows.view(-1), out_rows[rank].clone(), group=group,
                                            async_op=async_op)

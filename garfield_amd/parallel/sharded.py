@@ -51,6 +51,7 @@ import torch.distributed as dist
 from garfield_amd import _native
 from garfield_amd.ops import gar
 from garfield_amd.ops import reference as ref
+from garfield_amd.parallel.comm import gloo_backend
 
 DISTANCE_RULES = {"krum", "brute", "bulyan"}
 SUPPORTED = DISTANCE_RULES | {"average", "aksel", "median", "trimmed-mean", "averaged-median", "average-nan",
@@ -233,7 +234,7 @@ class ShardedAggregator:
         buf = e._shadow if lp else e.flat.data
         for b in sorted(self.buckets, key=lambda b: b.lo):   # the next forward reads low coordinates first
             full, mine = buf[b.lo:b.hi], buf[b.own]
-            if full.device.type == "cpu":
+            if gloo_backend():
                 mine = mine.clone()  # gloo rejects an input aliasing the output
             dist.all_gather_into_tensor(full, mine)
         if lp:
@@ -254,7 +255,7 @@ class ShardedAggregator:
         data = self.e.flat.data
         for b in sorted(self.buckets, key=lambda b: b.lo):
             mine = data[b.own]
-            if data.device.type == "cpu":
+            if gloo_backend():
                 mine = mine.clone()
             dist.all_gather_into_tensor(data[b.lo:b.hi], mine)
         self.master_stale = False

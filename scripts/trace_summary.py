@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--marker", default="spin")
+    ap.add_argument("--json", default="", help="also write {kernel: {ms_per_step, calls_per_step}} here")
     ap.add_argument("--sequence", default="", help="also write the last step's dispatches (start offset, "
                     "duration, kernel) to this file")
     a = ap.parse_args()
@@ -48,6 +49,12 @@ def main():
     print(f"{'ms/step':>9} {'%':>6} {'calls/step':>10}  kernel")
     for name, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[: a.top]:
         print(f"{t / 1e6 / k:9.3f} {100 * t / total:6.2f} {c / k:10.1f}  {name}")
+    if a.json:
+        import json
+        with open(a.json, "w") as fh:
+            json.dump({n: {"ms_per_step": t / 1e6 / k, "calls_per_step": c / k} for n, (c, t) in agg.items()}
+                      | {"__window__": {"ms_per_step": window / 1e6 / k, "busy_ms_per_step": busy / 1e6 / k}},
+                      fh, indent=1)
     if a.sequence:
         last = rows[-(len(rows) // k):]
         t0 = last[0][0]
