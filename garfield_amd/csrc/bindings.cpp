@@ -318,7 +318,8 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
                   double momentum, const c10::optional<at::Tensor>& run_mean,
                   const c10::optional<at::Tensor>& run_var, const at::Tensor& part, const at::Tensor& mean,
                   const at::Tensor& istd, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& y,
-                  bool relu, const c10::optional<at::Tensor>& mask, bool defer_running) {
+                  bool relu, const c10::optional<at::Tensor>& mask, bool defer_running,
+                  const c10::optional<at::Tensor>& tile_stats, int64_t tile_m) {
   const auto dev = x.device();
   check_bf16_rows(x, dev, "x");
   check_bf16_rows(y, dev, "y");
@@ -348,10 +349,16 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
   float* rm = opt_vec(run_mean, C, dev, "running_mean");
   float* rv = opt_vec(run_var, C, dev, "running_var");
   TORCH_CHECK((rm == nullptr) == (rv == nullptr), "garfield bn: pass both running statistics or neither");
+  const float* ts = nullptr;
+  if (tile_stats.has_value() && tile_stats->defined()) {
+    TORCH_CHECK(tile_m > 0 && tile_m <= rg, "garfield bn: tile statistics need 0 < tile_m <= rows per worker");
+    const int64_t tiles = (x.size(0) + tile_m - 1) / tile_m;
+    ts = ws_vec(*tile_stats, tiles * 4 * C, dev, "tile_stats");
+  }
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::bn_forward(u16(x), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
                             static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, u16_mut(y), relu, mp,
-                            defer_running, stream_of(dev));
+                            defer_running, stream_of(dev), ts, static_cast<int>(tile_m));
 }
 
 int xent_dtype(const at::Tensor& t, const char* what) {
@@ -581,6 +588,48 @@ void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, i
   c10::hip::HIPGuard guard(x.device().index());
   garfield::gpu::iconv_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap, static_cast<int>(pm),
                             transpose_w, stream_of(x.device()));
+}
+
+// Row-major NT GEMM (gemm_nt.hip): c = a · bᵀ (+ add); a [M, K], b [N, K], c/add [M, N], all contiguous
+// bf16 rows; stats (fp32, [ceil(M / BM)][2][2][N]): fused per-worker (rg rows) BatchNorm statistics.
+void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, const c10::optional<at::Tensor>& add,
+               const c10::optional<at::Tensor>& stats, int64_t rg, int64_t cfg) {
+  const auto dev = a.device();
+  auto chk = [&](const at::Tensor& t, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.device() == dev && t.scalar_type() == at::kBFloat16 && t.dim() == 2 &&
+                    t.stride(1) == 1 && t.stride(0) == t.size(1),
+                "gpu_gemm_nt: ", what, " must be contiguous 2-D bf16 rows on a's device");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "gpu_gemm_nt: ", what, " must be 16-byte aligned");
+  };
+  chk(a, "a");
+  chk(b, "b");
+  chk(c, "c");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gpu_gemm_nt: shapes a [M, K], b [N, K], c [M, N]");
+  TORCH_CHECK(K % 64 == 0 && K > 0, "gpu_gemm_nt: K must be a positive multiple of 64 (got ", K, ")");
+  TORCH_CHECK(M * std::max(K, N) < INT32_MAX, "gpu_gemm_nt: too large");
+  const uint16_t* ap = nullptr;
+  if (add.has_value() && add->defined()) {
+    chk(*add, "add");
+    TORCH_CHECK(add->sizes() == c.sizes(), "gpu_gemm_nt: add must be shaped like c");
+    ap = u16(*add);
+  }
+  float* sp = nullptr;
+  const bool want_stats = stats.has_value() && stats->defined();
+  if (want_stats) {
+    TORCH_CHECK(ap == nullptr, "gpu_gemm_nt: statistics and add are exclusive");
+    TORCH_CHECK(rg > 0 && M % rg == 0, "gpu_gemm_nt: statistics need M to split into rg-row workers");
+  }
+  if (cfg < 0) cfg = garfield::gpu::gemm_nt_pick(M, static_cast<int>(N), static_cast<int>(K), want_stats ? rg : 0);
+  const int bm = garfield::gpu::gemm_nt_tile_m(static_cast<int>(cfg)), bn = garfield::gpu::gemm_nt_tile_n(static_cast<int>(cfg));
+  TORCH_CHECK(bm > 0 && N % bn == 0, "gpu_gemm_nt: no tile configuration ", cfg, " for N = ", N);
+  if (want_stats) {
+    TORCH_CHECK(bm <= rg, "gpu_gemm_nt: tile of ", bm, " rows spans more than two workers of ", rg, " rows");
+    sp = ws_vec(*stats, ((M + bm - 1) / bm) * 4 * N, dev, "stats");
+  }
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::gemm_nt(u16(a), u16(b), static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), u16_mut(c),
+                         ap, sp, rg, static_cast<int>(cfg), stream_of(dev));
 }
 
 // Per-worker implicit weight gradient. out: fp32 [splits, groups, Cout, K] (contiguous partial
@@ -852,7 +901,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("res"), py::arg("groups"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
         py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"), py::arg("part"), py::arg("mean"),
         py::arg("istd"), py::arg("scale"), py::arg("shift"), py::arg("y"), py::arg("relu"),
-        py::arg("mask") = py::none(), py::arg("defer_running") = false);
+        py::arg("mask") = py::none(), py::arg("defer_running") = false, py::arg("tile_stats") = py::none(),
+        py::arg("tile_m") = 0);
   m.def("bn_small", [](int64_t rg) { return garfield::gpu::bn_small(rg); },
         "True when rg rows per worker take the single-kernel BatchNorm path (whose running statistics "
         "can be deferred to gpu_bn_running_update)");
@@ -875,6 +925,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dcol"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("dh"), py::arg("dw"), py::arg("dx"), py::arg("accumulate") = false);
 
+  m.def("gpu_gemm_nt", &g_gemm_nt,
+        "Row-major NT GEMM on MFMA: c = a · bᵀ (+ add); args (a [M,K], b [N,K], c [M,N], add=None, stats=None, "
+        "rg=0, cfg=-1); stats: fp32 [ceil(M/BM)][2][2][N] per-worker BatchNorm statistics of c (gpu_bn_forward's "
+        "tile_stats)",
+        py::arg("a"), py::arg("b"), py::arg("c"), py::arg("add") = py::none(), py::arg("stats") = py::none(),
+        py::arg("rg") = 0, py::arg("cfg") = -1);
+  m.def("gemm_nt_pick", [](int64_t M, int64_t N, int64_t K, int64_t rg_limit) {
+    return garfield::gpu::gemm_nt_pick(M, static_cast<int>(N), static_cast<int>(K), rg_limit);
+  }, "Tile configuration gpu_gemm_nt picks for M x N x K (rg_limit > 0: BM <= rg_limit); -1 if none");
+  m.def("gemm_nt_tile", [](int64_t cfg) {
+    return std::make_pair(garfield::gpu::gemm_nt_tile_m(static_cast<int>(cfg)),
+                          garfield::gpu::gemm_nt_tile_n(static_cast<int>(cfg)));
+  }, "(BM, BN) of a gpu_gemm_nt tile configuration");
   m.def("gpu_iconv", &g_iconv, "Implicit-GEMM NHWC convolution on MFMA: y = conv(x, w) (+ add); args (x, w, kh, kw, "
         "sh, sw, ph, pw, dh, dw, y, add=None, pm=0, transpose_w=False); x/y/add channels_last bf16, C % 32 == 0, "
         "Cout % 64 == 0; transpose_w: w is the forward weight [C, Cout, KH, KW] whose flipped transpose is applied "

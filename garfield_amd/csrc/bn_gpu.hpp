@@ -42,7 +42,20 @@ bool bn_small(int64_t rg);
 void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
                 float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
-                bool defer_running, hipStream_t stream);
+                bool defer_running, hipStream_t stream, const float* tile_stats = nullptr, int tile_m = 0);
+
+// Row-major NT GEMM on MFMA (gemm_nt.hip): C[M, N] = A[M, K] · B[N, K]ᵀ (+ add), bf16; K % 64 == 0,
+// N a multiple of the configuration's tile width. stats (nullable): per-tile, per-worker (rg rows)
+// BatchNorm statistics of C, [ceil(M / BM)][2][2][N] floats, merged by bn_finalize_tiles.
+void gemm_nt(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
+             float* stats, int64_t rg, int cfg, hipStream_t stream);
+// Tile configuration for an M x N x K problem (-1: none fits); rg_limit > 0: BM <= rg_limit (statistics).
+int gemm_nt_pick(int64_t M, int N, int K, int64_t rg_limit);
+int gemm_nt_tile_m(int cfg);
+int gemm_nt_tile_n(int cfg);
+void bn_finalize_tiles(const float* stats, int BM, int64_t M, int64_t rg, int groups, int C, const float* gamma,
+                       const float* beta, float eps, float* mean, float* istd, float* scale, float* shift,
+                       hipStream_t stream);
 
 // mask (nullable, relu only): bit (r*C + c) of the byte array = y[r, c] > 0, for the backward.
 // ReLU source of the backward: mask when given, else y (nullable) > 0. dres (nullable) receives dz.

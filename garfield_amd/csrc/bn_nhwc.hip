@@ -712,8 +712,8 @@ int64_t bn_part_floats(int64_t rg, int groups, int C) {
 void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
                 float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
-                bool defer_running, hipStream_t stream) {
-  if (rg <= kSmallRows) {
+                bool defer_running, hipStream_t stream, const float* tile_stats, int tile_m) {
+  if (rg <= kSmallRows && tile_stats == nullptr) {
     const dim3 sgrid((C + kSmallCh - 1) / kSmallCh, groups);
     if (res) {
       if (relu) hipLaunchKernelGGL((k_bn_fwd_small<true, true>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
@@ -730,13 +730,18 @@ void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, 
     }
     return;
   }
-  const Geo g = geometry(rg, groups, C);
-  const int ncb = (C + g.cb - 1) / g.cb;
-  hipLaunchKernelGGL((k_partial<false, 0>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
-                     nullptr, nullptr, nullptr, g, part);
-  const dim3 fgrid((C + kFinCh - 1) / kFinCh, groups);
-  hipLaunchKernelGGL(k_fwd_finalize, fgrid, dim3(kThreads), 0, stream, part, x, g, gamma, beta, eps, mean, istd,
-                     scale, shift);
+  if (tile_stats) {   // statistics from the producing GEMM's epilogue (gemm_nt.hip): no partial pass
+    bn_finalize_tiles(tile_stats, tile_m, rg * groups, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift,
+                      stream);
+  } else {
+    const Geo g = geometry(rg, groups, C);
+    const int ncb = (C + g.cb - 1) / g.cb;
+    hipLaunchKernelGGL((k_partial<false, 0>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
+                       nullptr, nullptr, nullptr, g, part);
+    const dim3 fgrid((C + kFinCh - 1) / kFinCh, groups);
+    hipLaunchKernelGGL(k_fwd_finalize, fgrid, dim3(kThreads), 0, stream, part, x, g, gamma, beta, eps, mean, istd,
+                       scale, shift);
+  }
   const RunStats rs{mean, istd, run_mean, run_var, eps, momentum, groups};
   int tch, rp;
   apply_geometry(C, &tch, &rp);

@@ -64,6 +64,12 @@ IWGRAD_1X1 = os.environ.get("GARFIELD_IWGRAD_1X1", "0") != "0"   # measured a wa
 # (7.23 vs 7.07 ms: per-layer fork/join dependencies leave 8% of the window idle), so off
 WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0") != "0"
 XENT = os.environ.get("GARFIELD_XENT", "1") != "0"   # fused per-worker cross-entropy kernel
+# Forward 1x1 convolutions with <= GEMM_NT_MAXN output channels on the hand-written MFMA GEMM
+# (gemm_nt.hip), which also emits the next BatchNorm's per-worker statistics (no partial pass).
+# Measured per shape against hipBLASLt (scripts/bench_1x1.py, profiles/r2/bench_1x1_r2.log):
+# 1.1-1.4x faster alone for N <= 128, slower above; but in the graphed step N <= 128 measured
+# 6.99 vs 6.96 ms/step (profiles/r2/ab_gemm_nt.log), so it is off by default (0).
+GEMM_NT_MAXN = int(os.environ.get("GARFIELD_GEMM_NT_MAXN", "0"))
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -203,6 +209,7 @@ class BNState:
         self.groups = groups
         self.C = bn.num_features
         self.mean = self.istd = self.scale = self.shift = None
+        self.tile = None          # (stats, BM): statistics of the next input, from the producing GEMM
 
     def ensure(self, device, dtype=torch.float32) -> None:
         if self.mean is None or self.mean.device != device or self.mean.dtype != dtype:
@@ -323,10 +330,13 @@ class _GroupedBN(torch.autograd.Function):
             track = bn.track_running_stats and bn.running_mean is not None
             # the backward's ReLU test reads one bit per element instead of y
             relu_state = torch.empty((x2.numel() // 8,), dtype=torch.uint8, device=x.device) if st.relu else None
-            defer = bool(track and ws.defer_running and C_.bn_small(rg))
+            tile, st.tile = st.tile, None
+            defer = bool(track and ws.defer_running and C_.bn_small(rg) and tile is None)
             C_.gpu_bn_forward(x2, r2, st.groups, bn.weight, bn.bias, float(bn.eps), float(bn.momentum),
                               bn.running_mean if track else None, bn.running_var if track else None,
-                              part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu, relu_state, defer)
+                              part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu, relu_state, defer,
+                              tile_stats=tile[0] if tile is not None else None,
+                              tile_m=tile[1] if tile is not None else 0)
             if defer:
                 ws.running_jobs.append((st.mean, st.istd, bn.running_mean, bn.running_var, rg, float(bn.eps),
                                         float(bn.momentum)))
@@ -394,6 +404,36 @@ class ConvSpec:
         self.dilation = tuple(conv.dilation)
         self.gemm = (self.kernel == (1, 1) and self.stride == (1, 1) and self.padding == (0, 0)
                      and self.dilation == (1, 1))
+        self.bn_next = None       # BNState of the BatchNorm that consumes this convolution's output
+
+
+def _gemm_nt_forward(x2: torch.Tensor, w2: torch.Tensor, spec: ConvSpec):
+    """y = x2 · w2ᵀ on gemm_nt.hip when it is the faster kernel for the shape (N <= GEMM_NT_MAXN,
+    K % 64 == 0); with ``spec.bn_next`` (the BatchNorm that consumes y, a large-layer one) the
+    kernel also writes that BatchNorm's per-worker tile statistics. None: use hipBLASLt."""
+    N, K = w2.shape
+    if not (x2.is_cuda and x2.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16 and N <= GEMM_NT_MAXN
+            and K % 64 == 0 and N % 64 == 0 and x2.is_contiguous() and w2.is_contiguous()):
+        return None
+    C_ = _native.native()
+    M = x2.shape[0]
+    st = spec.bn_next
+    rg = M // spec.groups
+    stats = None
+    if st is not None and M % spec.groups == 0 and not C_.bn_small(rg):
+        cfg = C_.gemm_nt_pick(M, N, K, rg)
+        if cfg >= 0:
+            bm = C_.gemm_nt_tile(cfg)[0]
+            stats = torch.empty((-(-M // bm)) * 4 * N, dtype=torch.float32, device=x2.device)
+    else:
+        cfg = C_.gemm_nt_pick(M, N, K, 0)
+    if cfg < 0:
+        return None
+    y2 = torch.empty((M, N), dtype=x2.dtype, device=x2.device)
+    C_.gpu_gemm_nt(x2, w2, y2, None, stats, rg if stats is not None else 0, cfg)
+    if stats is not None:
+        st.tile = (stats, C_.gemm_nt_tile(cfg)[0])
+    return y2
 
 
 def _conv_bwd(dy, x, w, spec: ConvSpec, mask):
@@ -598,7 +638,10 @@ class _GroupedConv(torch.autograd.Function):
         if spec.gemm:
             ctx.mode = "rows"
             ctx.save_for_backward(x, w)
-            return from_rows(torch.mm(rows2d(x), w.reshape(w.shape[0], -1).t()), n, h, wd)
+            y2 = _gemm_nt_forward(rows2d(x), w.reshape(w.shape[0], -1), spec)
+            if y2 is None:
+                y2 = torch.mm(rows2d(x), w.reshape(w.shape[0], -1).t())
+            return from_rows(y2, n, h, wd)
         if CONV_MODE == "gemm" and _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
             ctx.mode = "iconv"
             ctx.save_for_backward(x, w)

@@ -99,36 +99,50 @@ class GroupedResNet:
 
     # ------------------------------------------------------------------ #
 
-    def _bn(self, x, bn: nn.BatchNorm2d, relu: bool, res=None, res_join=None):
+    def _state(self, bn: nn.BatchNorm2d, relu: bool) -> BNState:
         st = self.bn.get(bn)
         if st is None:
             st = self.bn[bn] = BNState(bn, relu, self.sink, self.groups)
-        return grouped_bn(x, st, self.ws, res, res_join)
+        return st
+
+    def _bn(self, x, bn: nn.BatchNorm2d, relu: bool, res=None, res_join=None):
+        return grouped_bn(x, self._state(bn, relu), self.ws, res, res_join)
 
     def _conv(self, x, conv: nn.Conv2d, join=None):
         return grouped_conv(x, self.conv[conv], join)
+
+    def _conv_bn(self, x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, join=None, res=None, res_join=None):
+        """conv -> BatchNorm; the convolution may hand the BatchNorm its statistics (gemm_nt.hip)."""
+        st = self._state(bn, relu)
+        spec = self.conv[conv]
+        spec.bn_next = st
+        try:
+            y = grouped_conv(x, spec, join)
+        finally:
+            spec.bn_next = None
+        return grouped_bn(y, st, self.ws, res, res_join)
 
     def _block(self, blk, x):
         # x's two gradient branches (conv1 and the shortcut) are summed inside the
         # second branch's backward kernel instead of by an autograd add
         join = GradJoin() if self.join_residuals else None
-        out = self._bn(self._conv(x, blk.conv1, join), blk.bn1, True)
+        out = self._conv_bn(x, blk.conv1, blk.bn1, True, join)
         if isinstance(blk, Bottleneck):
-            out = self._bn(self._conv(out, blk.conv2), blk.bn2, True)
+            out = self._conv_bn(out, blk.conv2, blk.bn2, True)
             last_conv, last_bn = blk.conv3, blk.bn3
         else:
             last_conv, last_bn = blk.conv2, blk.bn2
         if blk.downsample is None:
-            return self._bn(self._conv(out, last_conv), last_bn, True, x, join)
-        sc = self._bn(self._conv(x, blk.downsample[0], join), blk.downsample[1], False)
-        return self._bn(self._conv(out, last_conv), last_bn, True, sc)
+            return self._conv_bn(out, last_conv, last_bn, True, res=x, res_join=join)
+        sc = self._conv_bn(x, blk.downsample[0], blk.downsample[1], False, join)
+        return self._conv_bn(out, last_conv, last_bn, True, res=sc)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         m = self.model
         # small layers' running statistics: one batched launch after the last BatchNorm
         self.ws.defer_running = x.is_cuda
         self.ws.running_jobs = []
-        x = self._bn(self._conv(x, m.conv1), m.bn1, True)
+        x = self._conv_bn(x, m.conv1, m.bn1, True)
         if isinstance(m.maxpool, nn.MaxPool2d):
             x = grouped_maxpool(x, m.maxpool)
         for name in ("layer1", "layer2", "layer3", "layer4"):

@@ -24,20 +24,33 @@ SHAPES = [
 
 
 def bench(fn, iters=30):
-    for _ in range(3):
-        fn()
+    """Device time per call: ``iters`` calls captured in one HIP graph and replayed
+    (host launch overhead, ~20 µs per hipBLASLt call from Python, is not counted,
+    exactly as in the graphed training step)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(iters):
-        fn()
+    for _ in range(5):
+        g.replay()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / iters * 1e6
+    return (time.perf_counter() - t0) / (5 * iters) * 1e6
 
 
 def main():
     dev = torch.device("cuda")
     C_ = _native.native()
-    has_g = hasattr(C_, "gpu_gemm1x1")
+    has_g = hasattr(C_, "gpu_gemm_nt")
     tot = {}
     for name, M, K, Co, cnt in SHAPES:
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
@@ -54,7 +67,7 @@ def main():
         w4 = w.view(Co, K, 1, 1)
         y4 = torch.empty((M, Co, 1, 1), device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
         dx4 = torch.empty((M, K, 1, 1), device=dev, dtype=torch.bfloat16, memory_format=torch.channels_last)
-        for pm in (11, 12, 14):
+        for pm in (() if has_g else (11, 12, 14)):
             f = lambda: C_.gpu_iconv(x4, w4, 1, 1, 1, 1, 0, 0, 1, 1, y4, None, pm, False)
             res[f"iconv{pm - 10} fwd"] = bench(f)
             f()
@@ -65,19 +78,62 @@ def main():
             g()
             err = (dx4.view(M, K).float() - dref.float()).abs().max().item()
             assert err < 0.05 * dref.float().abs().max().item() + 1e-2, (name, pm, "dgrad", err)
+        G = 8
+        rg = M // G
+        out = torch.empty((G, Co, K), device=dev, dtype=torch.bfloat16)
+        from garfield_amd.ops.grouped import _wgrad
+        res["wgrad bmm"] = bench(lambda: _wgrad(dy, x, G, out))
+        gi = torch.empty((G, Co, K), device=dev, dtype=torch.bfloat16)
+        for S in (() if has_g else (1, 4)):
+            part = torch.empty((S, G, Co, K), device=dev, dtype=torch.float32)
+            if S == 1:
+                f = lambda: C_.gpu_iwgrad(x4, dy4, 1, 1, 1, 1, 0, 0, 1, 1, G, gi, 1)
+            else:
+                f = lambda: (C_.gpu_iwgrad(x4, dy4, 1, 1, 1, 1, 0, 0, 1, 1, G, part, S), torch.sum(part, 0, out=gi))
+            res[f"iwgrad S{S}"] = bench(f)
         if has_g:
             y2 = torch.empty((M, Co), device=dev, dtype=torch.bfloat16)
             dx2 = torch.empty((M, K), device=dev, dtype=torch.bfloat16)
-            f = lambda: C_.gpu_gemm1x1(x, w, y2, None, False)
-            res["g1x1 fwd"] = bench(f)
-            f()
-            err = (y2.float() - yref.float()).abs().max().item()
-            assert err < 0.05 * yref.float().abs().max().item() + 1e-2, (name, "g1x1", err)
-            g = lambda: C_.gpu_gemm1x1(dy, w, dx2, None, True)
-            res["g1x1 dgrad"] = bench(g)
-            g()
-            err = (dx2.float() - dref.float()).abs().max().item()
-            assert err < 0.05 * dref.float().abs().max().item() + 1e-2, (name, "g1x1 dgrad", err)
+            wt = w.t().contiguous()
+            res["transpose w"] = bench(lambda: w.t().contiguous())
+            for cfg in range(9):
+                bm, bn = C_.gemm_nt_tile(cfg)
+                if Co % bn == 0:
+                    f = lambda: C_.gpu_gemm_nt(x, w, y2, None, None, 0, cfg)
+                    res[f"nt{cfg} fwd"] = bench(f)
+                    f()
+                    err = (y2.float() - yref.float()).abs().max().item()
+                    assert err < 0.02 * yref.float().abs().max().item() + 1e-2, (name, cfg, err)
+                if K % bn == 0:
+                    g = lambda: C_.gpu_gemm_nt(dy, wt, dx2, None, None, 0, cfg)
+                    res[f"nt{cfg} dgrad"] = bench(g)
+                    g()
+                    err = (dx2.float() - dref.float()).abs().max().item()
+                    assert err < 0.02 * dref.float().abs().max().item() + 1e-2, (name, cfg, "dgrad", err)
+            # fused BatchNorm statistics (rg rows per worker) vs torch on the stored output
+            for cfg in range(9):
+                bm, bn = C_.gemm_nt_tile(cfg)
+                if Co % bn == 0 and bm <= rg:
+                    st = torch.empty(((M + bm - 1) // bm) * 4 * Co, device=dev, dtype=torch.float32)
+                    res[f"nt{cfg}+st"] = bench(lambda: C_.gpu_gemm_nt(x, w, y2, None, st, rg, cfg))
+            cfg = C_.gemm_nt_pick(M, Co, K, rg)
+            bm, bn = C_.gemm_nt_tile(cfg)
+            st = torch.empty(((M + bm - 1) // bm) * 4 * Co, device=dev, dtype=torch.float32)
+            C_.gpu_gemm_nt(x, w, y2, None, st, rg, cfg)
+            mean = torch.empty((G, Co), device=dev)
+            istd, sc, sh = torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean)
+            ybn = torch.empty_like(y2)
+            gam = torch.rand(Co, device=dev) + 0.5
+            bet = torch.randn(Co, device=dev)
+            part = torch.empty(C_.bn_part_floats(rg, G, Co), device=dev)
+            C_.gpu_bn_forward(y2, None, G, gam, bet, 1e-5, 0.1, None, None, part, mean, istd, sc, sh, ybn, False,
+                              tile_stats=st, tile_m=bm)
+            yg = y2.float().view(G, rg, Co)
+            mref = yg.mean(1)
+            vref = yg.var(1, unbiased=False)
+            em = (mean - mref).abs().max().item()
+            ev = ((1.0 / istd ** 2 - 1e-5) - vref).abs().max().item() / vref.abs().max().item()
+            assert em < 1e-3 * (1 + mref.abs().max().item()) and ev < 1e-3, (name, "stats", em, ev)
         floor = byf / 6.3e12 * 1e6
         print(f"{name:18s} M={M:6d} K={K:5d} N={Co:5d} x{cnt} floor {floor:5.1f}us | "
               + " ".join(f"{k} {v:6.1f}" for k, v in res.items()), flush=True)

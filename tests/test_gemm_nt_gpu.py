@@ -1,0 +1,77 @@
+"""The 1x1-convolution GEMM (gemm_nt.hip) and its fused BatchNorm statistics on MI355X,
+against plain fp32 PyTorch references."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("M,K,N", [(128000, 64, 256), (4000, 256, 64), (2000, 512, 2048), (1000, 1024, 256),
+                                   (333, 128, 128), (77, 64, 64)])
+def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
+    torch.manual_seed(M + K + N)
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    add = torch.randn(M, N, device=cuda).to(torch.bfloat16)
+    ref = a.float() @ b.float().t()
+    ran = 0
+    for cfg in range(9):
+        bm, bn = native.gemm_nt_tile(cfg)
+        if N % bn:
+            continue
+        c = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+        native.gpu_gemm_nt(a, b, c, None, None, 0, cfg)
+        assert rel(c, ref) < 5e-3, cfg
+        c2 = add.clone()
+        native.gpu_gemm_nt(a, b, c2, c2, None, 0, cfg)        # in place: c = a·bᵀ + c
+        assert rel(c2, ref + add.float()) < 5e-3, cfg
+        ran += 1
+    assert ran >= 2
+    c = torch.empty((M, N), device=cuda, dtype=torch.bfloat16)
+    native.gpu_gemm_nt(a, b, c)                                 # automatic configuration
+    assert rel(c, ref) < 5e-3
+
+
+@pytest.mark.parametrize("G,rg,K,N,offset", [(8, 16000, 64, 256, 0.0), (8, 1000, 256, 64, 0.0),
+                                              (8, 250, 512, 128, 40.0), (3, 700, 128, 128, 25.0),
+                                              (2, 4000, 64, 64, 300.0)])
+def test_fused_bn_statistics_match_fp32(cuda, native, G, rg, K, N, offset):
+    """Per-worker mean / biased variance of the STORED GEMM output, merged from tile
+    statistics (tiles straddling worker boundaries included), even when |mean| >> std."""
+    torch.manual_seed(rg + N)
+    M = G * rg
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    for cfg in range(9):
+        bm, bn = native.gemm_nt_tile(cfg)
+        if N % bn or bm > rg:
+            continue
+        # a column of the input drives a constant offset into every output channel
+        a2 = a.clone()
+        a2[:, 0] = offset
+        b2 = b.clone()
+        b2[:, 0] = 1.0 if offset else b[:, 0]
+        y = torch.empty((M, N), device=cuda, dtype=torch.bfloat16)
+        st = torch.empty(((M + bm - 1) // bm) * 4 * N, device=cuda)
+        native.gpu_gemm_nt(a2, b2, y, None, st, rg, cfg)
+        assert rel(y, a2.float() @ b2.float().t()) < 5e-3
+        mean = torch.empty((G, N), device=cuda)
+        istd, sc, sh = torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean)
+        gam = torch.rand(N, device=cuda) + 0.5
+        bet = torch.randn(N, device=cuda)
+        part = torch.empty(native.bn_part_floats(rg, G, N), device=cuda)
+        out = torch.empty_like(y)
+        native.gpu_bn_forward(y, None, G, gam, bet, 1e-5, 0.1, None, None, part, mean, istd, sc, sh, out, False,
+                              tile_stats=st, tile_m=bm)
+        yg = y.double().view(G, rg, N)
+        mref, vref = yg.mean(1), yg.var(1, unbiased=False)
+        assert (mean.double() - mref).abs().max().item() < 1e-4 * (1 + mref.abs().max().item()), cfg
+        var = 1.0 / istd.double() ** 2 - 1e-5
+        assert ((var - vref).abs() / vref.clamp_min(1e-6)).max().item() < 2e-3, cfg
+        yref = ((yg - mref[:, None]) / torch.sqrt(vref[:, None] + 1e-5) * gam.double() + bet.double()).view(M, N)
+        assert rel(out, yref) < 1e-2, cfg
