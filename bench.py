@@ -105,14 +105,21 @@ def parse():
     p.add_argument("--ps-workers", action="store_true", help="server ranks also host logical workers")
     p.add_argument("--checkpoint", default="", help="save a checkpoint here after the timed steps (untimed)")
     p.add_argument("--resume", default="", help="restore this checkpoint file before the warm-up")
+    p.add_argument("--data", default="fresh", choices=["fresh", "static"],
+                   help="fresh: every step draws new samples from a GPU-resident synthetic uint8 dataset with random "
+                        "crop + flip + normalise (data_aug.hip, one launch); static: the same batches every step")
+    p.add_argument("--dataset-size", type=int, default=0,
+                   help="images in the synthetic dataset (default 50000 CIFAR-shape, 2000 ImageNet-shape)")
     p.add_argument("--lr", type=float, default=0.01,
                    help="0.01: the reference lr (0.2) diverges from random init on the synthetic data")
     return p.parse_args()
 
 
 def timed_steps(eng, batches, steps, warmup, ctx, trend=None):
+    """``batches``: the k micro-batches, or a callable returning the next step's."""
+    nxt = batches if callable(batches) else (lambda: batches)
     for i in range(warmup):
-        loss = eng.step(batches)
+        loss = eng.step(nxt())
         if trend is not None and i == 0:
             trend.append(float(loss))
     if ctx.device.type == "cuda":
@@ -124,7 +131,7 @@ def timed_steps(eng, batches, steps, warmup, ctx, trend=None):
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        loss = eng.step(batches)
+        loss = eng.step(nxt())
     if ctx.device.type == "cuda":
         torch.cuda.synchronize()
     ctx.barrier()
@@ -170,8 +177,16 @@ def main():
                                                   ps_workers=a.ps_workers))
     else:
         eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
-    batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
-                                seed=1000 + ctx.rank, channels_last=a.channels_last)
+    if a.data == "fresh":
+        from garfield_amd.data.fresh import DeviceBatches
+
+        size = a.dataset_size or (50000 if a.dataset == "cifar10" else 2000)
+        feed = DeviceBatches.synthetic(size, shape, num_classes, a.workers_per_gpu, a.batch, ctx.device,
+                                       seed=1000 + ctx.rank)
+        batches = feed.next
+    else:
+        batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
+                                    seed=1000 + ctx.rank, channels_last=a.channels_last)
     if a.resume:
         from garfield_amd.utils.checkpoint import load_engine
 
@@ -190,7 +205,7 @@ def main():
     if a.phases:
         eng.timer.reset()
         for _ in range(3):
-            eng.step(batches)
+            eng.step(batches() if callable(batches) else batches)
         extra["phase_ms"] = {k: round(v, 3) for k, v in eng.phase_times().items()}
     if a.overhead:
         cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
@@ -230,7 +245,9 @@ def main():
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16",
             "data": f"synthetic (random {'CIFAR-10' if a.dataset == 'cifar10' else 'ImageNet'}-shape images, "
-                    "random-init weights)",
+                    + ("fresh samples every step from a GPU-resident uint8 dataset with random crop + flip + "
+                       "normalise, " if a.data == "fresh" else "the same batches every step, ")
+                    + "random-init weights)",
             "config": {
                 "model": f"{a.model} (torchvision architecture, {num_classes} classes, {d} params)",
                 "global_batch": n * a.batch,

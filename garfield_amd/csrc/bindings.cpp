@@ -632,6 +632,37 @@ void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, co
                          ap, sp, rg, static_cast<int>(cfg), stream_of(dev));
 }
 
+// Fresh grouped batch: out [R, C, H, W] bf16 channels_last from uint8 NHWC images src[idx[r]].
+void g_augment_gather(const at::Tensor& src, const at::Tensor& idx, int64_t seed, int64_t step,
+                      const std::vector<double>& mean, const std::vector<double>& std, const at::Tensor& out,
+                      int64_t pad, bool flip) {
+  const auto dev = src.device();
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.dim() == 4 && src.is_contiguous(),
+              "gpu_augment_gather: src must be a contiguous uint8 [N, H, W, C] GPU tensor");
+  const int64_t H = src.size(1), W = src.size(2), C = src.size(3);
+  TORCH_CHECK(C >= 1 && C <= 4, "gpu_augment_gather: 1..4 channels");
+  TORCH_CHECK(idx.device() == dev && idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous(),
+              "gpu_augment_gather: idx must be a contiguous int64 vector on src's device");
+  TORCH_CHECK(out.device() == dev && out.scalar_type() == at::kBFloat16 && out.dim() == 4 && out.size(0) == idx.size(0) &&
+                  out.size(1) == C && out.size(2) == H && out.size(3) == W &&
+                  out.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "gpu_augment_gather: out must be a channels_last bf16 [len(idx), C, H, W] tensor");
+  TORCH_CHECK(static_cast<int64_t>(mean.size()) == C && static_cast<int64_t>(std.size()) == C,
+              "gpu_augment_gather: one mean / std per channel");
+  TORCH_CHECK(pad >= 0 && pad < H && pad < W, "gpu_augment_gather: invalid padding");
+  garfield::gpu::AugNorm n{};
+  for (int64_t c = 0; c < C; ++c) {
+    TORCH_CHECK(std[c] > 0, "gpu_augment_gather: std must be positive");
+    n.mean[c] = static_cast<float>(mean[c]);
+    n.inv_std[c] = static_cast<float>(1.0 / std[c]);
+  }
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::augment_gather(src.data_ptr<uint8_t>(), src.size(0), idx.data_ptr<int64_t>(), idx.size(0), static_cast<int>(H),
+                                static_cast<int>(W), static_cast<int>(C), static_cast<int>(pad), flip,
+                                static_cast<uint64_t>(seed), static_cast<uint64_t>(step), n, u16_mut(out),
+                                stream_of(dev));
+}
+
 // Per-worker implicit weight gradient. out: fp32 [splits, groups, Cout, K] (contiguous partial
 // slabs) or, with splits == 1, a bf16 [groups, Cout, K] view whose rows are contiguous (any group
 // stride: the exchange rows).
@@ -925,6 +956,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dcol"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("dh"), py::arg("dw"), py::arg("dx"), py::arg("accumulate") = false);
 
+  m.def("gpu_augment_gather", &g_augment_gather,
+        "Fresh batch in one launch: out[r] = normalise(random crop (pad) + flip of uint8 NHWC image src[idx[r]]), "
+        "bf16 channels_last; crop/flip per row from a hash of (seed, step, r); args (src, idx, seed, step, mean, std, "
+        "out, pad=4, flip=True)",
+        py::arg("src"), py::arg("idx"), py::arg("seed"), py::arg("step"), py::arg("mean"), py::arg("std"),
+        py::arg("out"), py::arg("pad") = 4, py::arg("flip") = true);
   m.def("gpu_gemm_nt", &g_gemm_nt,
         "Row-major NT GEMM on MFMA: c = a · bᵀ (+ add); args (a [M,K], b [N,K], c [M,N], add=None, stats=None, "
         "rg=0, cfg=-1); stats: fp32 [ceil(M/BM)][2][2][N] per-worker BatchNorm statistics of c (gpu_bn_forward's "

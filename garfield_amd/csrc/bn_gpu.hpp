@@ -44,6 +44,16 @@ void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, 
                 float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
                 bool defer_running, hipStream_t stream, const float* tile_stats = nullptr, int tile_m = 0);
 
+// Fresh batches (data_aug.hip): out[r] (bf16 channels_last [R, C, H, W]) = normalise(random crop
+// (pad) + random horizontal flip of uint8 NHWC image src[idx[r]]); the crop/flip of row r is a hash
+// of (seed, step, r). C <= 4.
+struct AugNorm {
+  float mean[4];
+  float inv_std[4];
+};
+void augment_gather(const uint8_t* src, int64_t nsrc, const int64_t* idx, int64_t R, int H, int W, int C, int pad, bool flip,
+                    uint64_t seed, uint64_t step, const AugNorm& nrm, uint16_t* out, hipStream_t stream);
+
 // Row-major NT GEMM on MFMA (gemm_nt.hip): C[M, N] = A[M, K] · B[N, K]ᵀ (+ add), bf16; K % 64 == 0,
 // N a multiple of the configuration's tile width. stats (nullable): per-tile, per-worker (rg rows)
 // BatchNorm statistics of C, [ceil(M / BM)][2][2][N] floats, merged by bn_finalize_tiles.

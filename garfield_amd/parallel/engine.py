@@ -118,6 +118,21 @@ class _SlotIssuer:
         return works
 
 
+def _stacked_view(ts):
+    """The [k*B, ...] tensor the k equal-shaped tensors ``ts`` are consecutive row blocks of
+    (views of one buffer), or None."""
+    t0 = ts[0]
+    B = t0.shape[0]
+    if B == 0:
+        return None
+    for j, t in enumerate(ts):
+        if (t.shape != t0.shape or t.stride() != t0.stride() or t.dtype != t0.dtype
+                or t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr()
+                or t.storage_offset() != t0.storage_offset() + j * B * t0.stride(0)):
+            return None
+    return t0.as_strided((len(ts) * B, *t0.shape[1:]), t0.stride(), t0.storage_offset())
+
+
 class RobustDataParallel:
     """Robust DP over one process per device (see module docstring)."""
 
@@ -595,9 +610,14 @@ class RobustDataParallel:
         key = tuple((id(x), x._version, id(y), y._version) for x, y in batches)
         if key != self._gsrc:
             with torch.no_grad():
-                for j, (x, y) in enumerate(batches):
-                    self._gx[j * B:(j + 1) * B].copy_(x)
-                    self._gy[j * B:(j + 1) * B].copy_(y)
+                gx, gy = _stacked_view([x for x, _ in batches]), _stacked_view([y for _, y in batches])
+                if gx is not None and gy is not None:   # the k batches are one buffer (DeviceBatches): 2 copies
+                    self._gx.copy_(gx)
+                    self._gy.copy_(gy)
+                else:
+                    for j, (x, y) in enumerate(batches):
+                        self._gx[j * B:(j + 1) * B].copy_(x)
+                        self._gy[j * B:(j + 1) * B].copy_(y)
             self._gsrc = key
             self._gsrc_refs = [t for xy in batches for t in xy]  # keep ids valid while cached
 
