@@ -632,6 +632,37 @@ void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, co
                          ap, sp, rg, static_cast<int>(cfg), stream_of(dev));
 }
 
+// Large gradient sets: x an [n, d] GPU matrix (unit column stride, row stride ld, 16-bit or fp32).
+int large_dtype(const at::Tensor& x, const at::Tensor& out) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 && x.size(0) >= 1 &&
+                  x.size(0) <= garfield::kLargeRows,
+              "garfield large: x must be an [n, d] GPU matrix with unit column stride, 1 <= n <= ", garfield::kLargeRows);
+  TORCH_CHECK(out.device() == x.device() && out.scalar_type() == x.scalar_type() && out.is_contiguous() &&
+                  out.numel() == x.size(1),
+              "garfield large: out must be a contiguous [d] tensor of x's dtype on x's device");
+  return dtype_code(x);
+}
+
+void g_large_combine(const at::Tensor& x, const at::Tensor& w, const at::Tensor& out) {
+  const int dt = large_dtype(x, out);
+  TORCH_CHECK(w.device() == x.device() && w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == x.size(0),
+              "gpu_large_combine: w must be a contiguous fp32 [n] tensor on x's device");
+  c10::hip::HIPGuard guard(x.device().index());
+  garfield::gpu::large_combine(x.data_ptr(), dt, static_cast<int>(x.size(0)), x.size(1), x.stride(0),
+                               w.data_ptr<float>(), out.data_ptr(), stream_of(x.device()));
+}
+
+void g_large_coord(const at::Tensor& x, int64_t mode, int64_t f, int64_t beta, const at::Tensor& out) {
+  const int dt = large_dtype(x, out);
+  const int64_t n = x.size(0);
+  TORCH_CHECK(mode >= 0 && mode <= 2, "gpu_large_coord: mode 0 median, 1 trimmed-mean, 2 averaged-median");
+  TORCH_CHECK(mode != 1 || (f >= 0 && 2 * f < n), "gpu_large_coord: trimmed-mean needs 0 <= 2f < n");
+  TORCH_CHECK(mode != 2 || (beta >= 1 && beta <= n), "gpu_large_coord: averaged-median needs 1 <= beta <= n");
+  c10::hip::HIPGuard guard(x.device().index());
+  garfield::gpu::large_coord(x.data_ptr(), dt, static_cast<int>(n), x.size(1), x.stride(0), static_cast<int>(mode),
+                             static_cast<int>(f), static_cast<int>(beta), out.data_ptr(), stream_of(x.device()));
+}
+
 // Fresh grouped batch: out [R, C, H, W] bf16 channels_last from uint8 NHWC images src[idx[r]].
 void g_augment_gather(const at::Tensor& src, const at::Tensor& idx, int64_t seed, int64_t step,
                       const std::vector<double>& mean, const std::vector<double>& std, const at::Tensor& out,
@@ -956,6 +987,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dcol"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
         py::arg("dh"), py::arg("dw"), py::arg("dx"), py::arg("accumulate") = false);
 
+  m.attr("LARGE_ROWS") = garfield::kLargeRows;
+  m.def("gpu_large_combine", &g_large_combine,
+        "out = w · x for an [n, d] gradient matrix with n <= LARGE_ROWS (fp32 accumulation); args (x, w, out)");
+  m.def("gpu_large_coord", &g_large_coord,
+        "Coordinate-wise rule on an [n, d] gradient matrix with n <= LARGE_ROWS by LDS radix select; "
+        "args (x, mode 0 median | 1 trimmed-mean | 2 averaged-median, f, beta, out)");
   m.def("gpu_augment_gather", &g_augment_gather,
         "Fresh batch in one launch: out[r] = normalise(random crop (pad) + flip of uint8 NHWC image src[idx[r]]), "
         "bf16 channels_last; crop/flip per row from a hash of (seed, step, r); args (src, idx, seed, step, mean, std, "

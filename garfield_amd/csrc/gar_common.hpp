@@ -13,6 +13,8 @@ namespace garfield {
 
 // Largest number of gradients a single RowTable addresses (1 KiB of kernarg).
 constexpr int kMaxRows = 128;
+// Largest gradient set of the large-n kernels (gar_large.hip: one [n, ld] matrix, LDS radix select).
+constexpr int kLargeRows = 1024;
 
 enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2, kF64 = 3 };
 

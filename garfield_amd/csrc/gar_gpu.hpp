@@ -58,6 +58,12 @@ void coordwise(const RowTable& rows, int n, int64_t d, int dt, int mode, int f, 
                int out_dt, hipStream_t stream);
 int coordwise_max_rows();
 
+// ---- Large gradient sets (kMaxRows < n <= kLargeRows), one [n, ld] matrix (gar_large.hip) ----
+// out[j] = Σ_i w[i] x[i, j] (out in x's dtype); mode 0 median, 1 trimmed-mean(f), 2 averaged-median(beta).
+void large_combine(const void* x, int dt, int n, int64_t d, int64_t ld, const float* w, void* out, hipStream_t stream);
+void large_coord(const void* x, int dt, int n, int64_t d, int64_t ld, int mode, int f, int beta, void* out,
+                 hipStream_t stream);
+
 // ---- Aksel: squared distances of every gradient to a centre vector ---------
 int sqdist_grid(int64_t d);
 void sqdist_partial(const RowTable& rows, int n, int64_t d, int dt, const float* center,

@@ -15,8 +15,13 @@ current stream, nothing copied to the host:
   sorting-network kernels;
 * Aksel: median kernel -> squared distance to it -> selection -> combine.
 
-CPU path: the C++ thread-pool implementations in the same extension. Inputs with
-more than ``MAX_ROWS`` (128) gradients use a vectorised PyTorch implementation.
+CPU path: the C++ thread-pool implementations in the same extension.
+
+More than ``MAX_ROWS`` (128) gradients (the reference's gar_bench sweeps n to 512): on
+the GPU, up to ``LARGE_ROWS`` (1024) rows run on ``gar_large.hip`` as one [n, d] matrix
+(combine with fp32 accumulation; median / trimmed-mean / averaged-median and the Bulyan
+tail by LDS radix select; the Krum/Bulyan Gram as one hipBLASLt GEMM with fp32 output);
+everything else, and the CPU, uses a vectorised PyTorch implementation.
 """
 from __future__ import annotations
 
@@ -30,6 +35,8 @@ from garfield_amd import _native
 from garfield_amd.ops import reference as ref
 
 MAX_ROWS = 128
+LARGE_ROWS = 1024
+_LARGE_MODE = {"median": 0, "trimmed-mean": 1, "averaged-median": 2}
 
 _MODE = {"median": 0, "trimmed-mean": 1, "averaged-median": 2, "average-nan": 3, "condense": 4, "bulyan-tail": 5}
 
@@ -183,6 +190,8 @@ def gram(gradients) -> torch.Tensor:
     if rows.device.type != "cuda":
         X = rows.stacked().double()
         return X @ X.T
+    if rows.n > MAX_ROWS:
+        return _large_gram(rows)
     C = _C_for(rows)
     ws = workspace(rows)
     g = _gram_into(C, rows, ws)
@@ -228,6 +237,8 @@ def pairwise_distances(gradients) -> torch.Tensor:
 
 def combine(gradients, weights: torch.Tensor) -> torch.Tensor:
     rows = prepare(gradients)
+    if _large(rows):
+        return _large_combine(rows, weights)
     if rows.n > MAX_ROWS:
         return _finish((weights.to(rows.device, torch.float32)[:, None] * rows.stacked().float()).sum(0), rows)
     C = _C_for(rows)
@@ -238,6 +249,23 @@ def combine(gradients, weights: torch.Tensor) -> torch.Tensor:
     if C is None:
         return ref.combine(rows.stacked(), weights.double()).to(rows.out_dtype)
     return _finish(C.cpu_combine(rows.obj, weights.float().cpu()), rows)
+
+
+def _large(rows: Rows) -> bool:
+    """GPU set of MAX_ROWS < n <= LARGE_ROWS gradients: the gar_large.hip kernels."""
+    return rows.device.type == "cuda" and MAX_ROWS < rows.n <= LARGE_ROWS
+
+
+def _matrix(rows: Rows) -> torch.Tensor:
+    X = rows.stacked()
+    return X if X.stride(1) == 1 else X.contiguous()
+
+
+def _large_combine(rows: Rows, w: torch.Tensor) -> torch.Tensor:
+    X = _matrix(rows)
+    out = torch.empty(rows.d, dtype=X.dtype, device=X.device)
+    _native.native().gpu_large_combine(X, w.to(X.device, torch.float32).contiguous(), out)
+    return _finish(out, rows)
 
 
 # --------------------------------------------------------------------------- #
@@ -256,6 +284,8 @@ def average(gradients, **_) -> torch.Tensor:
         out = torch.empty(rows.d, dtype=rows.dtype, device=rows.device)
         C.gpu_combine(rows.obj, w, out)
         return _finish(out, rows)
+    if _large(rows):
+        return _large_combine(rows, torch.full((rows.n,), 1.0 / rows.n, dtype=torch.float32, device=rows.device))
     return _finish(rows.stacked().float().mean(0) if rows.dtype != torch.float64 else rows.stacked().mean(0), rows)
 
 
@@ -292,6 +322,8 @@ def krum(gradients, f: int, m: int | None = None, **_) -> torch.Tensor:
 
 
 def _combine_rows(rows: Rows, w: torch.Tensor) -> torch.Tensor:
+    if _large(rows):
+        return _large_combine(rows, w)
     if rows.n > MAX_ROWS:
         return _finish((w.to(rows.device)[:, None] * rows.stacked().float()).sum(0), rows)
     C = _C_for(rows)
@@ -320,7 +352,9 @@ def _bulyan_W(rows: Rows, f: int, m: int) -> torch.Tensor:
         C.gpu_bulyan_select(g, rows.n, f, m, t, W)
         return W.view(t, rows.n)
     D = pairwise_distances(rows.obj) if C is not None else ref.pairwise_sqdist(rows.stacked())
-    if C is None or rows.n > MAX_ROWS:
+    if rows.n > MAX_ROWS:
+        return _large_bulyan_weights(D, f, m).float().to(rows.device)
+    if C is None:
         return ref.bulyan_weights(D, f, m).float().to(rows.device)
     return C.cpu_bulyan_weights(D, f, m, t)
 
@@ -331,6 +365,14 @@ def bulyan(gradients, f: int, m: int | None = None, **_) -> torch.Tensor:
     t = rows.n - 2 * f - 2
     beta = t - 2 * f
     W = _bulyan_W(rows, f, m)
+    if _large(rows):   # V = W·X column chunk by chunk (bounded fp32 memory), then the radix-select tail
+        X, Wd = _matrix(rows), W.to(rows.device, torch.float32)
+        out = torch.empty(rows.d, dtype=torch.float32, device=rows.device)
+        step = max(1, (1 << 28) // (4 * max(rows.n, t)))
+        for c0 in range(0, rows.d, step):
+            V = torch.mm(Wd, X[:, c0:c0 + step].float())
+            _native.native().gpu_large_coord(V, 2, 0, beta, out[c0:c0 + step])
+        return _finish(out, rows)
     if rows.n > MAX_ROWS:
         V = W.to(rows.device) @ rows.stacked().float()
         return _finish(_torch_closest_mean(V, beta), rows)
@@ -345,6 +387,11 @@ def bulyan(gradients, f: int, m: int | None = None, **_) -> torch.Tensor:
 
 
 def _coord(rows: Rows, mode: str, f: int = 0, beta: int = 0, seed: int = 0, p: float = 1.0) -> torch.Tensor:
+    if _large(rows) and mode in _LARGE_MODE:
+        X = _matrix(rows)
+        out = torch.empty(rows.d, dtype=X.dtype, device=X.device)
+        _native.native().gpu_large_coord(X, _LARGE_MODE[mode], f, beta, out)
+        return _finish(out, rows)
     if rows.n > MAX_ROWS:
         return _finish(_torch_coord(rows.stacked().float(), mode, f, beta, seed, p), rows)
     C = _C_for(rows)
@@ -460,9 +507,17 @@ def aksel(gradients, f: int, mode: str = "mid", **_) -> torch.Tensor:
 # Vectorised PyTorch implementations for n > MAX_ROWS (same semantics).
 
 
+def _large_gram(rows: Rows) -> torch.Tensor:
+    """fp32 Gram matrix of a large set: one hipBLASLt GEMM with fp32 output on 16-bit GPU rows."""
+    X = rows.stacked()
+    if X.is_cuda and X.dtype in (torch.bfloat16, torch.float16):
+        return torch.mm(X, X.T, out_dtype=torch.float32)
+    X = X.float()
+    return X @ X.T
+
+
 def _large_krum_weights(rows: Rows, f: int, m: int) -> torch.Tensor:
-    X = rows.stacked().float()
-    g = X @ X.T
+    g = _large_gram(rows)
     dg = torch.diagonal(g)
     D = (dg[:, None] + dg[None, :] - 2 * g)
     D = torch.where(torch.isfinite(D), D.clamp(min=0), torch.full_like(D, math.inf))
@@ -475,6 +530,35 @@ def _large_krum_weights(rows: Rows, f: int, m: int) -> torch.Tensor:
     w = torch.zeros(rows.n, dtype=torch.float32, device=rows.device)
     w[order[:m]] = 1.0 / m
     return w
+
+
+def _stable_order(v: torch.Tensor) -> torch.Tensor:
+    """Indices by (value, index), NaN last: reference._order."""
+    return torch.sort(_nan_inf(v), stable=True).indices
+
+
+def _large_bulyan_weights(D: torch.Tensor, f: int, m: int) -> torch.Tensor:
+    """reference.bulyan_weights vectorised over n (fp64, CPU: t sequential tiny steps):
+    each gradient's q nearest-neighbour distances P, scores = row sums, then t rounds of
+    'weights over the mk best scores; remove the best; subtract its column of P'."""
+    D = D.double().cpu()
+    n = D.shape[0]
+    t, q = n - 2 * f - 2, n - f - 2
+    Dn = _nan_inf(D.clone())
+    Dn.fill_diagonal_(math.inf)
+    near = torch.sort(Dn, dim=1, stable=True).indices[:, :q]
+    P = torch.zeros((n, n), dtype=torch.float64)
+    P.scatter_(1, near, D.gather(1, near))
+    scores = P.sum(1)
+    W = torch.zeros((t, n), dtype=torch.float64)
+    for k in range(t):
+        mk = max(m - k, 1)
+        order = _stable_order(scores)
+        W[k, order[:mk]] = 1.0 / mk
+        best = int(order[0])
+        scores -= P[:, best]
+        scores[best] = ref.FLT_MAX
+    return W
 
 
 def _nan_inf(X: torch.Tensor) -> torch.Tensor:

@@ -140,3 +140,18 @@ def test_brute_rejects_more_than_2_pow_32_subsets():
     with _pytest.raises(ValueError, match="2\\^32"):
         _gar.brute_weights(torch.randn(64, 16), 8)
     assert _gar.BRUTE_MAX_SUBSETS == 2 ** 32
+
+
+@pytest.mark.parametrize("n,f", [(20, 3), (45, 5), (140, 10)])
+def test_large_bulyan_selection_equals_reference(n, f):
+    """The vectorised selection of large sets (n > MAX_ROWS on the GPU path) reproduces
+    reference.bulyan_weights exactly, NaN rows and ties included."""
+    from garfield_amd.ops import gar as _gar
+    from garfield_amd.ops import reference as _ref
+
+    g = torch.Generator().manual_seed(n)
+    X = torch.randint(-3, 4, (n, 30), generator=g).double()
+    X[:f] += 5
+    X[f, 0] = float("nan")
+    D = _ref.pairwise_sqdist(X)
+    assert torch.equal(_gar._large_bulyan_weights(D, f, n - f - 2), _ref.bulyan_weights(D, f, n - f - 2))

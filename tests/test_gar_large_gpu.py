@@ -1,0 +1,71 @@
+"""Large gradient sets (128 < n <= 1024) on the GPU kernels of gar_large.hip, against the
+vectorised fp64 PyTorch semantics of ops/gar.py (ties and non-finite values included)."""
+import math
+
+import pytest
+import torch
+
+from garfield_amd.ops import gar
+from garfield_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, d, dtype, seed, ties=True, nonfinite=True):
+    g = torch.Generator().manual_seed(seed)
+    if ties:   # few distinct values: every tie rule is exercised
+        X = torch.randint(-24, 25, (n, d), generator=g).double() / 8.0
+    else:
+        X = torch.randn(n, d, generator=g, dtype=torch.float64)
+    if nonfinite:
+        X[torch.rand(n, d, generator=g) < 0.01] = math.nan
+        X[torch.rand(n, d, generator=g) < 0.005] = math.inf
+        X[torch.rand(n, d, generator=g) < 0.005] = -math.inf
+    return X.to(dtype)
+
+
+def _close(a, b, tol):
+    a, b = a.double().cpu(), b.double().cpu()
+    same_nonfinite = (torch.isnan(a) == torch.isnan(b)) & ((a == b) | torch.isnan(a) | torch.isfinite(a))
+    fin = torch.isfinite(a) & torch.isfinite(b)
+    assert bool(same_nonfinite.all()), "non-finite pattern differs"
+    err = ((a - b).abs()[fin] / (1 + b.abs()[fin])).max().item() if fin.any() else 0.0
+    assert err <= tol, err
+
+
+@pytest.mark.parametrize("n", [129, 256, 512, 1024])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_large_coordinate_rules(cuda, n, dtype):
+    d = 3000
+    X = _data(n, d, dtype, n)
+    Xd = X.double()
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    _close(gar.median(X.to(cuda)), gar._torch_coord(Xd, "median", 0, 0, 0, 1.0), tol)
+    f = n // 5
+    _close(gar.trimmed_mean(X.to(cuda), f=f), gar._torch_coord(Xd, "trimmed-mean", f, 0, 0, 1.0), tol)
+    beta = n - f
+    _close(gar.averaged_median(X.to(cuda), beta=beta), gar._torch_closest_mean(Xd, beta), tol)
+
+
+@pytest.mark.parametrize("n", [200, 700])
+def test_large_combine_and_average(cuda, n):
+    X = _data(n, 5000, torch.bfloat16, 3, ties=False, nonfinite=False)
+    w = torch.rand(n, dtype=torch.float64)
+    w[torch.rand(n) < 0.5] = 0
+    out = gar.combine(X.to(cuda), w.float())
+    _close(out, w @ X.double(), 1e-2)
+    _close(gar.average(X.to(cuda)), X.double().mean(0), 1e-2)
+
+
+def test_large_krum_and_bulyan_selections(cuda):
+    n, f, d = 160, 10, 4000
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(n, d, generator=g, dtype=torch.float64)
+    X[:f] += 50.0                      # f far-away (Byzantine) rows
+    Xg = X.float().to(cuda)
+    w = gar.krum_weights(Xg, f)
+    wref = ref.krum_weights(ref.pairwise_sqdist(X), f, n - f - 2)
+    assert torch.equal((w.cpu() > 0), (wref > 0))
+    _close(gar.krum(Xg, f), wref @ X, 1e-5)
+    out = gar.bulyan(Xg, f)
+    _close(out, ref.bulyan(X, f, n - f - 2), 1e-4)
