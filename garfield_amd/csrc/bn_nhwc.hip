@@ -444,16 +444,23 @@ dim3 apply_grid(int64_t R, int rp) {
 // replayed by k_running (one tiny launch, or batched for many layers by the caller).
 constexpr int kSmallRows = 1024;
 constexpr int kSmallThreads = 1024;             // 16 waves per workgroup to hide the load latency
-constexpr int kSmallCh = 32;                    // channels per workgroup (4 vectors of 8)
-constexpr int kSmallVec = kSmallCh / 8;
-constexpr int kSmallLanes = kSmallThreads / kSmallVec;   // 256 row lanes
-constexpr int kSmallSplit = kSmallThreads / kSmallCh;    // first-stage reduction splits per channel
-static_assert(kSmallRows % kSmallLanes == 0, "small-layer rows must tile the row lanes");
+// Channels per workgroup CH (16, 32 or 64; GARFIELD_BN_SMALL_CH): a layer of C channels and
+// k workers runs C / CH x k workgroups, e.g. 64 for CIFAR layer3 (C = 256) at CH = 32.
+template <int CH>
+struct SmallGeo {
+  static constexpr int Vec = CH / 8;                       // 16-byte vectors per row
+  static constexpr int Lanes = kSmallThreads / Vec;        // row lanes
+  static constexpr int Split = kSmallThreads / CH;         // first-stage reduction splits per channel
+  static constexpr int It = kSmallRows / Lanes;            // rows per thread, held in registers
+  static_assert(kSmallRows % Lanes == 0 && Lanes % Split == 0, "small-layer rows must tile the row lanes");
+};
 
 // Sums red[k][lane][c] over the kSmallLanes lanes for both k; result in red[k][0][c].
-__device__ __forceinline__ void small_reduce(float (&red)[2][kSmallLanes][kSmallCh]) {
+template <int CH>
+__device__ __forceinline__ void small_reduce(float (&red)[2][SmallGeo<CH>::Lanes][CH]) {
+  constexpr int kSmallCh = CH, kSmallSplit = SmallGeo<CH>::Split;
   const int c = threadIdx.x % kSmallCh, part = threadIdx.x / kSmallCh;
-  constexpr int per = kSmallLanes / kSmallSplit;
+  constexpr int per = SmallGeo<CH>::Lanes / kSmallSplit;
   float a = 0.f, b = 0.f;
 #pragma unroll 8
   for (int t = 0; t < per; ++t) { a += red[0][part * per + t][c]; b += red[1][part * per + t][c]; }
@@ -471,7 +478,6 @@ __device__ __forceinline__ void small_reduce(float (&red)[2][kSmallLanes][kSmall
   __syncthreads();
 }
 
-constexpr int kSmallIt = kSmallRows / kSmallLanes;   // rows per thread, held in registers
 
 __device__ __forceinline__ uint4 ld_raw8(const uint16_t* p, int64_t off) {
   return *reinterpret_cast<const uint4*>(p + off);
@@ -486,7 +492,7 @@ __device__ __forceinline__ void unpack8(const uint4 u, float (&v)[8]) {
 
 // Each thread keeps its (<= kSmallIt) rows of 8 channels in registers as packed bf16,
 // so the apply pass does not re-read x (or dy) from memory.
-template <bool RES, bool RELU>
+template <int CH, bool RES, bool RELU>
 __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* __restrict__ x,
                                                           const uint16_t* __restrict__ res, int64_t rg, int C,
                                                           const float* __restrict__ gamma,
@@ -494,6 +500,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* 
                                                           float* __restrict__ mean, float* __restrict__ istd,
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           uint16_t* __restrict__ y, uint8_t* __restrict__ mask) {
+  constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH>::Vec, kSmallLanes = SmallGeo<CH>::Lanes,
+                kSmallIt = SmallGeo<CH>::It;
   __shared__ float red[2][kSmallLanes][kSmallCh];
   __shared__ float lsc[kSmallCh], lsh[kSmallCh];
   const int tc = threadIdx.x % kSmallVec, tr = threadIdx.x / kSmallVec;
@@ -525,7 +533,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* 
 #pragma unroll
   for (int i = 0; i < 8; ++i) { red[0][tr][tc * 8 + i] = s[i]; red[1][tr][tc * 8 + i] = q[i]; }
   __syncthreads();
-  small_reduce(red);
+  small_reduce<CH>(red);
   if (threadIdx.x < kSmallCh) {
     const int c = blockIdx.x * kSmallCh + threadIdx.x;
     const float S = red[0][0][threadIdx.x], Q = red[1][0][threadIdx.x];
@@ -582,12 +590,14 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* 
   }
 }
 
-template <int RM, bool RES_OUT>
+template <int CH, int RM, bool RES_OUT>
 __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
     const uint8_t* __restrict__ mask, int64_t rg, int C, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ istd, uint16_t* __restrict__ dx,
     uint16_t* __restrict__ dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta) {
+  constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH>::Vec, kSmallLanes = SmallGeo<CH>::Lanes,
+                kSmallIt = SmallGeo<CH>::It;
   __shared__ float red[2][kSmallLanes][kSmallCh];
   __shared__ float la[kSmallCh], lb[kSmallCh], lc[kSmallCh];
   const int tc = threadIdx.x % kSmallVec, tr = threadIdx.x / kSmallVec;
@@ -642,7 +652,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
 #pragma unroll
   for (int i = 0; i < 8; ++i) { red[0][tr][tc * 8 + i] = A[i]; red[1][tr][tc * 8 + i] = B[i]; }
   __syncthreads();
-  small_reduce(red);
+  small_reduce<CH>(red);
   if (threadIdx.x < kSmallCh) {
     const int c = blockIdx.x * kSmallCh + threadIdx.x;
     const float SA = red[0][0][threadIdx.x], SB = red[1][0][threadIdx.x];
@@ -702,6 +712,45 @@ __global__ __launch_bounds__(kThreads) void k_running(RunJobs jobs) {
   }
 }
 
+// tuning knob: channels per small-layer workgroup (16 / 32 / 64)
+int small_ch() {
+  static const int ch = [] {
+    const char* e = std::getenv("GARFIELD_BN_SMALL_CH");
+    const int v = e ? std::atoi(e) : 0;
+    return (v == 16 || v == 64) ? v : 32;
+  }();
+  return ch;
+}
+
+template <int CH>
+void launch_fwd_small(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
+                      const float* beta, float eps, float* mean, float* istd, float* scale, float* shift, uint16_t* y,
+                      bool relu, uint8_t* mask, hipStream_t stream) {
+  const dim3 sgrid((C + CH - 1) / CH, groups);
+  if (res) {
+    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, true, true>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
+    else hipLaunchKernelGGL((k_bn_fwd_small<CH, true, false>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+  } else {
+    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, false, true>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
+    else hipLaunchKernelGGL((k_bn_fwd_small<CH, false, false>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+  }
+}
+
+template <int CH>
+void launch_bwd_small(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const uint8_t* mask, int64_t rg,
+                      int groups, int C, const float* gamma, const float* mean, const float* istd, uint16_t* dx,
+                      uint16_t* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
+                      int rm, hipStream_t stream) {
+  const dim3 sgrid((C + CH - 1) / CH, groups);
+#define GARFIELD_BWD_SMALL(RMV, RESV)                                                                           \
+  hipLaunchKernelGGL((k_bn_bwd_small<CH, RMV, RESV>), sgrid, dim3(kSmallThreads), 0, stream, x, dy, y, mask, rg, C, \
+                     gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta)
+  if (rm == 2) { if (dres) GARFIELD_BWD_SMALL(2, true); else GARFIELD_BWD_SMALL(2, false); }
+  else if (rm == 1) { if (dres) GARFIELD_BWD_SMALL(1, true); else GARFIELD_BWD_SMALL(1, false); }
+  else { if (dres) GARFIELD_BWD_SMALL(0, true); else GARFIELD_BWD_SMALL(0, false); }
+#undef GARFIELD_BWD_SMALL
+}
+
 }  // namespace
 
 int64_t bn_part_floats(int64_t rg, int groups, int C) {
@@ -714,14 +763,10 @@ void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, 
                 float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
                 bool defer_running, hipStream_t stream, const float* tile_stats, int tile_m) {
   if (rg <= kSmallRows && tile_stats == nullptr) {
-    const dim3 sgrid((C + kSmallCh - 1) / kSmallCh, groups);
-    if (res) {
-      if (relu) hipLaunchKernelGGL((k_bn_fwd_small<true, true>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
-      else hipLaunchKernelGGL((k_bn_fwd_small<true, false>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
-    } else {
-      if (relu) hipLaunchKernelGGL((k_bn_fwd_small<false, true>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
-      else hipLaunchKernelGGL((k_bn_fwd_small<false, false>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
-    }
+    const int ch = small_ch();
+    if (ch == 16) launch_fwd_small<16>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream);
+    else if (ch == 64) launch_fwd_small<64>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream);
+    else launch_fwd_small<32>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream);
     if (run_mean && !defer_running) {
       RunJobs jobs{};
       jobs.j[0] = RunJob{mean, istd, run_mean, run_var, rg, C, groups, eps, momentum};
@@ -762,14 +807,10 @@ void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const
                  hipStream_t stream) {
   const int rm = mask ? 2 : (y ? 1 : 0);
   if (rg <= kSmallRows) {
-    const dim3 sgrid((C + kSmallCh - 1) / kSmallCh, groups);
-#define GARFIELD_BWD_SMALL(RMV, RESV)                                                                           \
-  hipLaunchKernelGGL((k_bn_bwd_small<RMV, RESV>), sgrid, dim3(kSmallThreads), 0, stream, x, dy, y, mask, rg, C, gamma, \
-                     mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta)
-    if (rm == 2) { if (dres) GARFIELD_BWD_SMALL(2, true); else GARFIELD_BWD_SMALL(2, false); }
-    else if (rm == 1) { if (dres) GARFIELD_BWD_SMALL(1, true); else GARFIELD_BWD_SMALL(1, false); }
-    else { if (dres) GARFIELD_BWD_SMALL(0, true); else GARFIELD_BWD_SMALL(0, false); }
-#undef GARFIELD_BWD_SMALL
+    const int ch = small_ch();
+    if (ch == 16) launch_bwd_small<16>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream);
+    else if (ch == 64) launch_bwd_small<64>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream);
+    else launch_bwd_small<32>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream);
     return;
   }
   const Geo g = geometry(rg, groups, C);

@@ -11,8 +11,8 @@ if [ -n "$TESTS" ]; then
     || { echo "tests failed"; grep -E "FAILED|Error|assert" gpurun_out/pt_$TAG.log | head -20; tail -5 gpurun_out/pt_$TAG.log; exit 1; }
   tail -1 gpurun_out/pt_$TAG.log
 fi
-for i in 1 2 3; do
-  for v in $A $B; do
+for i in $(seq ${RUNS:-3}); do
+  for v in ${VALUES:-$A $B}; do
     env $KNOB=$v timeout -k 10 300 python bench.py --steps 30 --warmup 5 ${BENCH_ARGS} > gpurun_out/bench_${TAG}_${v}_$i.log 2>&1 || { echo "bench $v failed"; tail -5 gpurun_out/bench_${TAG}_${v}_$i.log; exit 1; }
     echo "$KNOB=$v run $i: $(grep '^{' gpurun_out/bench_${TAG}_${v}_$i.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"], d.get("final_loss"))')"
   done
