@@ -183,6 +183,8 @@ def main():
         size = a.dataset_size or (50000 if a.dataset == "cifar10" else 2000)
         feed = DeviceBatches.synthetic(size, shape, num_classes, a.workers_per_gpu, a.batch, ctx.device,
                                        seed=1000 + ctx.rank)
+        if hasattr(eng, "grouped_inputs"):   # write each batch straight into the step's input buffers
+            feed.attach(eng.grouped_inputs(a.batch, shape))
         batches = feed.next
     else:
         batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,

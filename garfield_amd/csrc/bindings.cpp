@@ -664,17 +664,37 @@ void g_large_coord(const at::Tensor& x, int64_t mode, int64_t f, int64_t beta, c
 }
 
 // Fresh grouped batch: out [R, C, H, W] bf16 channels_last from uint8 NHWC images src[idx[r]].
-void g_augment_gather(const at::Tensor& src, const at::Tensor& idx, int64_t seed, int64_t step,
+void g_augment_gather(const at::Tensor& src, const c10::optional<at::Tensor>& idx_opt, int64_t seed, int64_t step,
                       const std::vector<double>& mean, const std::vector<double>& std, const at::Tensor& out,
-                      int64_t pad, bool flip) {
+                      int64_t pad, bool flip, const c10::optional<at::Tensor>& labels,
+                      const c10::optional<at::Tensor>& labels_out) {
   const auto dev = src.device();
   TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.dim() == 4 && src.is_contiguous(),
               "gpu_augment_gather: src must be a contiguous uint8 [N, H, W, C] GPU tensor");
   const int64_t H = src.size(1), W = src.size(2), C = src.size(3);
   TORCH_CHECK(C >= 1 && C <= 4, "gpu_augment_gather: 1..4 channels");
-  TORCH_CHECK(idx.device() == dev && idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous(),
-              "gpu_augment_gather: idx must be a contiguous int64 vector on src's device");
-  TORCH_CHECK(out.device() == dev && out.scalar_type() == at::kBFloat16 && out.dim() == 4 && out.size(0) == idx.size(0) &&
+  const int64_t R = out.size(0);
+  const int64_t* ip = nullptr;
+  if (idx_opt.has_value() && idx_opt->defined()) {
+    const auto& idx = *idx_opt;
+    TORCH_CHECK(idx.device() == dev && idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous() &&
+                    idx.size(0) == R,
+                "gpu_augment_gather: idx must be a contiguous int64 [len(out)] vector on src's device");
+    ip = idx.data_ptr<int64_t>();
+  }
+  const int64_t* lp = nullptr;
+  int64_t* lo = nullptr;
+  if (labels_out.has_value() && labels_out->defined()) {
+    TORCH_CHECK(labels.has_value() && labels->defined() && labels->device() == dev &&
+                    labels->scalar_type() == at::kLong && labels->is_contiguous() && labels->numel() == src.size(0),
+                "gpu_augment_gather: labels must be a contiguous int64 [N] tensor on src's device");
+    TORCH_CHECK(labels_out->device() == dev && labels_out->scalar_type() == at::kLong && labels_out->is_contiguous() &&
+                    labels_out->numel() == R,
+                "gpu_augment_gather: labels_out must be a contiguous int64 [len(out)] tensor");
+    lp = labels->data_ptr<int64_t>();
+    lo = labels_out->data_ptr<int64_t>();
+  }
+  TORCH_CHECK(out.device() == dev && out.scalar_type() == at::kBFloat16 && out.dim() == 4 &&
                   out.size(1) == C && out.size(2) == H && out.size(3) == W &&
                   out.is_contiguous(at::MemoryFormat::ChannelsLast),
               "gpu_augment_gather: out must be a channels_last bf16 [len(idx), C, H, W] tensor");
@@ -688,7 +708,7 @@ void g_augment_gather(const at::Tensor& src, const at::Tensor& idx, int64_t seed
     n.inv_std[c] = static_cast<float>(1.0 / std[c]);
   }
   c10::hip::HIPGuard guard(dev.index());
-  garfield::gpu::augment_gather(src.data_ptr<uint8_t>(), src.size(0), idx.data_ptr<int64_t>(), idx.size(0), static_cast<int>(H),
+  garfield::gpu::augment_gather(src.data_ptr<uint8_t>(), src.size(0), ip, lp, lo, R, static_cast<int>(H),
                                 static_cast<int>(W), static_cast<int>(C), static_cast<int>(pad), flip,
                                 static_cast<uint64_t>(seed), static_cast<uint64_t>(step), n, u16_mut(out),
                                 stream_of(dev));
@@ -995,10 +1015,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "args (x, mode 0 median | 1 trimmed-mean | 2 averaged-median, f, beta, out)");
   m.def("gpu_augment_gather", &g_augment_gather,
         "Fresh batch in one launch: out[r] = normalise(random crop (pad) + flip of uint8 NHWC image src[idx[r]]), "
-        "bf16 channels_last; crop/flip per row from a hash of (seed, step, r); args (src, idx, seed, step, mean, std, "
-        "out, pad=4, flip=True)",
+        "bf16 channels_last; crop/flip per row from a hash of (seed, step, r); idx None: the image index is drawn "
+        "from the same hash; labels_out[r] = labels[image]; args (src, idx, seed, step, mean, std, out, pad=4, "
+        "flip=True, labels=None, labels_out=None)",
         py::arg("src"), py::arg("idx"), py::arg("seed"), py::arg("step"), py::arg("mean"), py::arg("std"),
-        py::arg("out"), py::arg("pad") = 4, py::arg("flip") = true);
+        py::arg("out"), py::arg("pad") = 4, py::arg("flip") = true, py::arg("labels") = py::none(),
+        py::arg("labels_out") = py::none());
   m.def("gpu_gemm_nt", &g_gemm_nt,
         "Row-major NT GEMM on MFMA: c = a · bᵀ (+ add); args (a [M,K], b [N,K], c [M,N], add=None, stats=None, "
         "rg=0, cfg=-1); stats: fp32 [ceil(M/BM)][2][2][N] per-worker BatchNorm statistics of c (gpu_bn_forward's "

@@ -51,7 +51,9 @@ struct AugNorm {
   float mean[4];
   float inv_std[4];
 };
-void augment_gather(const uint8_t* src, int64_t nsrc, const int64_t* idx, int64_t R, int H, int W, int C, int pad, bool flip,
+// idx null: row r samples image hash(seed, step, r) % nsrc; lab_out (nullable) receives lab_src[image].
+void augment_gather(const uint8_t* src, int64_t nsrc, const int64_t* idx, const int64_t* lab_src, int64_t* lab_out,
+                    int64_t R, int H, int W, int C, int pad, bool flip,
                     uint64_t seed, uint64_t step, const AugNorm& nrm, uint16_t* out, hipStream_t stream);
 
 // Row-major NT GEMM on MFMA (gemm_nt.hip): C[M, N] = A[M, K] · B[N, K]ᵀ (+ add), bf16; K % 64 == 0,

@@ -28,7 +28,9 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {
 }
 
 __global__ __launch_bounds__(256) void k_augment_gather(const uint8_t* __restrict__ src, int64_t nsrc,
-                                                        const int64_t* __restrict__ idx, int64_t R, int H, int W, int C, int pad, int flip,
+                                                        const int64_t* __restrict__ idx,
+                                                        const int64_t* __restrict__ lab_src,
+                                                        int64_t* __restrict__ lab_out, int64_t R, int H, int W, int C, int pad, int flip,
                                                         uint64_t key, AugNorm nrm, uint16_t* __restrict__ out) {
   const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t HW = static_cast<int64_t>(H) * W;
@@ -44,8 +46,16 @@ __global__ __launch_bounds__(256) void k_augment_gather(const uint8_t* __restric
   const int hs = h + oy;
   const int ws = (fl ? W - 1 - w : w) + ox;
   const bool in = hs >= 0 && hs < H && ws >= 0 && ws < W;
-  int64_t img = idx[r];
-  img = img < 0 ? 0 : (img >= nsrc ? nsrc - 1 : img);   // never read outside the dataset
+  int64_t img;
+  if (idx) {
+    img = idx[r];
+    img = img < 0 ? 0 : (img >= nsrc ? nsrc - 1 : img);   // never read outside the dataset
+  } else {  // sampling with replacement from the same counter-based hash
+    const uint64_t h = (static_cast<uint64_t>(mix32(key + 0x51ed270b27a3b9c1ull * (r + 1))) << 32) |
+                       mix32(~key ^ (static_cast<uint64_t>(r) * 0xbf58476d1ce4e5b9ull));
+    img = static_cast<int64_t>(h % static_cast<uint64_t>(nsrc));
+  }
+  if (lab_out && pix == 0) lab_out[r] = lab_src[img];
   uint16_t* o = out + p * C;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
@@ -59,13 +69,14 @@ __global__ __launch_bounds__(256) void k_augment_gather(const uint8_t* __restric
 
 }  // namespace
 
-void augment_gather(const uint8_t* src, int64_t nsrc, const int64_t* idx, int64_t R, int H, int W, int C, int pad, bool flip,
+void augment_gather(const uint8_t* src, int64_t nsrc, const int64_t* idx, const int64_t* lab_src, int64_t* lab_out,
+                    int64_t R, int H, int W, int C, int pad, bool flip,
                     uint64_t seed, uint64_t step, const AugNorm& nrm, uint16_t* out, hipStream_t stream) {
   const int64_t total = R * H * W;
   if (total <= 0) return;
   const uint64_t key = seed * 0xd1b54a32d192ed03ull + step * 0x2545f4914f6cdd1dull + 0x632be59bd9b4e019ull;
   hipLaunchKernelGGL(k_augment_gather, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, stream, src, nsrc,
-                     idx, R, H, W, C, pad, flip ? 1 : 0, key, nrm, out);
+                     idx, lab_src, lab_out, R, H, W, C, pad, flip ? 1 : 0, key, nrm, out);
 }
 
 }  // namespace gpu

@@ -46,8 +46,23 @@ class DeviceBatches:
                                    memory_format=torch.channels_last)
         else:
             self.out = torch.empty((R, c, h, w), dtype=torch.float32)
+        self.lab_out = torch.empty(R, dtype=torch.long, device=self.device)
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(self.seed)
+
+    def attach(self, buffers) -> bool:
+        """Write every batch straight into a consumer's input buffers (x [k*B, C, H, W] bf16
+        channels_last, y [k*B] int64: ``RobustDataParallel.grouped_inputs``); False (nothing
+        changed) when they do not fit."""
+        if buffers is None or self.device.type != "cuda":
+            return False
+        x, y = buffers
+        if (tuple(x.shape) != tuple(self.out.shape) or x.dtype != torch.bfloat16 or x.device != self.device
+                or not x.is_contiguous(memory_format=torch.channels_last) or y.dtype != torch.long
+                or tuple(y.shape) != (self.k * self.B,) or not y.is_contiguous()):
+            return False
+        self.out, self.lab_out = x, y
+        return True
 
     @classmethod
     def synthetic(cls, num_images: int, shape, num_classes: int, k: int, batch: int, device, seed: int = 0, **kw):
@@ -62,15 +77,18 @@ class DeviceBatches:
 
     def next(self):
         R = self.k * self.B
-        idx = torch.randint(0, self.src.shape[0], (R,), generator=self.gen, device=self.device)
         if self.device.type == "cuda":
-            _native.native().gpu_augment_gather(self.src, idx, self.seed, self.step, self.mean, self.std, self.out,
-                                                self.pad, self.flip)
+            # ONE launch: sample indices (hash), gather + crop + flip + normalise, labels
+            _native.native().gpu_augment_gather(self.src, None, self.seed, self.step, self.mean, self.std, self.out,
+                                                self.pad, self.flip, self.labels, self.lab_out)
             torch.autograd.graph.increment_version(self.out)   # written by a native kernel: consumers see a new version
+            torch.autograd.graph.increment_version(self.lab_out)
+            y = self.lab_out
         else:
+            idx = torch.randint(0, self.src.shape[0], (R,), generator=self.gen, device=self.device)
             self.out.copy_(self._cpu(idx))
+            y = self.labels[idx]
         self.step += 1
-        y = self.labels[idx]
         return [(self.out[j * self.B:(j + 1) * self.B], y[j * self.B:(j + 1) * self.B]) for j in range(self.k)]
 
     def _cpu(self, idx: torch.Tensor) -> torch.Tensor:

@@ -118,6 +118,11 @@ class _SlotIssuer:
         return works
 
 
+def _same_view(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return (a.data_ptr() == b.data_ptr() and a.shape == b.shape and a.stride() == b.stride()
+            and a.dtype == b.dtype)
+
+
 def _stacked_view(ts):
     """The [k*B, ...] tensor the k equal-shaped tensors ``ts`` are consecutive row blocks of
     (views of one buffer), or None."""
@@ -595,25 +600,40 @@ class RobustDataParallel:
         x0, y0 = batches[0]
         return x0.dim() == 4 and all(x.shape == x0.shape and y.shape == y0.shape for x, y in batches)
 
+    def _ensure_gbuf(self, B: int, sample_shape: tuple, label_shape: tuple = (), label_dtype=torch.int64) -> None:
+        shape = (self.k * B, *sample_shape)
+        if self._gx is None or tuple(self._gx.shape) != shape:
+            dt = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+            self._gx = torch.empty(shape, dtype=dt, device=self.device, memory_format=torch.channels_last)
+            self._gy = torch.empty((self.k * B, *label_shape), dtype=label_dtype, device=self.device)
+            self._ggraph = None
+            self._gsrc = None
+
+    def grouped_inputs(self, batch: int, sample_shape, label_dtype=torch.int64):
+        """The grouped step's static input buffers ([k*batch, *sample_shape] channels_last, and
+        the labels) for a producer that writes each step's batch in place
+        (``data.fresh.DeviceBatches.attach``): no staging copy. None when the step is not grouped."""
+        if self._gexec is None:
+            return None
+        self._ensure_gbuf(int(batch), tuple(sample_shape), (), label_dtype)
+        return self._gx, self._gy
+
     def _stage_grouped(self, batches) -> None:
         """Concatenate the k micro-batches into the static grouped input buffers
         (skipped when the caller passes the very same, unmodified tensors again)."""
         x0, y0 = batches[0]
         B = x0.shape[0]
-        shape = (self.k * B, *x0.shape[1:])
-        if self._gx is None or tuple(self._gx.shape) != shape:
-            dt = torch.bfloat16 if self.device.type == "cuda" else torch.float32
-            self._gx = torch.empty(shape, dtype=dt, device=self.device, memory_format=torch.channels_last)
-            self._gy = torch.empty((self.k * B, *y0.shape[1:]), dtype=y0.dtype, device=self.device)
-            self._ggraph = None
-            self._gsrc = None
+        self._ensure_gbuf(B, tuple(x0.shape[1:]), tuple(y0.shape[1:]), y0.dtype)
         key = tuple((id(x), x._version, id(y), y._version) for x, y in batches)
         if key != self._gsrc:
             with torch.no_grad():
                 gx, gy = _stacked_view([x for x, _ in batches]), _stacked_view([y for _, y in batches])
-                if gx is not None and gy is not None:   # the k batches are one buffer (DeviceBatches): 2 copies
-                    self._gx.copy_(gx)
-                    self._gy.copy_(gy)
+                if gx is not None and gy is not None:
+                    # the k batches are one buffer (DeviceBatches): written in place already, or 2 copies
+                    if not _same_view(gx, self._gx):
+                        self._gx.copy_(gx)
+                    if not _same_view(gy, self._gy):
+                        self._gy.copy_(gy)
                 else:
                     for j, (x, y) in enumerate(batches):
                         self._gx[j * B:(j + 1) * B].copy_(x)

@@ -67,3 +67,23 @@ def test_device_batches_feed_new_versions(cuda):
     assert b2[0][0]._version != v1 and not torch.equal(b2[0][0], x1)
     assert len(b2) == 4 and b2[0][0].shape == (16, 3, 32, 32) and b2[0][1].shape == (16,)
     assert b2[0][0].is_contiguous(memory_format=torch.channels_last)
+
+
+def test_hashed_sampling_labels_and_engine_buffers(cuda, native):
+    """idx=None: the kernel draws the images itself and writes their labels; attach() makes the
+    feed write straight into a consumer's buffers."""
+    feed = DeviceBatches.synthetic(64, (3, 8, 8), 10, 2, 8, cuda, seed=4)
+    x = torch.empty((16, 3, 8, 8), dtype=torch.bfloat16, device=cuda, memory_format=torch.channels_last)
+    y = torch.empty(16, dtype=torch.long, device=cuda)
+    assert feed.attach((x, y))
+    b = feed.next()
+    assert b[0][0].data_ptr() == x.data_ptr() and b[1][1].data_ptr() == y[8:].data_ptr()
+    # every row is some image of the dataset (pad 0 / no flip reproduces it exactly) with its label
+    feed2 = DeviceBatches(feed.src.cpu(), feed.labels.cpu(), 2, 8, cuda, pad=0, flip=False, seed=4)
+    xs, ys = zip(*feed2.next())
+    xs, ys = torch.cat(xs).double().cpu(), torch.cat(ys).cpu()
+    ref = _normalised(feed.src.cpu(), feed2.mean, feed2.std)
+    for r in range(16):
+        err = (ref - xs[r]).abs().flatten(1).max(1).values
+        j = int(err.argmin())
+        assert err[j] < 2e-2 and int(feed.labels[j]) == int(ys[r])
