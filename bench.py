@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--gar", default="krum")
     p.add_argument("--f", type=int, default=2)
     p.add_argument("--exchange-dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                   help="fp32: the reference's precision end to end (no autocast, fp32 exchange rows, fp32 weights; "
+                        "per-worker HIP graphs, since the grouped NHWC kernels are bf16)")
     p.add_argument("--channels-last", action="store_true")
     p.add_argument("--overhead", action="store_true",
                    help="also time the same job with the 'average' GAR and report the Krum overhead")
@@ -161,12 +164,16 @@ def main():
     torch.manual_seed(1234)
     model = build_model(a.model, num_classes=num_classes)
     d = num_parameters(model)
+    fp32 = a.precision == "fp32"
+    if fp32:
+        a.exchange_dtype, a.no_lp_weights, a.no_worker_batching = "fp32", True, True
     xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
+    amp = {} if not fp32 else {"autocast_dtype": None}
     cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                        weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
                        cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=not a.no_lp_weights,
                        worker_batching=False if a.no_worker_batching else None,
-                       shard_gar=True if a.shard_gar else None)
+                       shard_gar=True if a.shard_gar else None, **amp)
     if a.num_ps:
         from dataclasses import asdict
 
@@ -186,6 +193,8 @@ def main():
         if hasattr(eng, "grouped_inputs"):   # write each batch straight into the step's input buffers
             feed.attach(eng.grouped_inputs(a.batch, shape))
         batches = feed.next
+        if fp32:   # the kernel writes bf16 rows; the fp32 path takes fp32 inputs
+            batches = lambda: [(x.float(), y) for x, y in feed.next()]  # noqa: E731
     else:
         batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
                                     seed=1000 + ctx.rank, channels_last=a.channels_last)
@@ -213,7 +222,7 @@ def main():
         cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                                weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
                                cuda_graph=not a.no_graph, lp_weights=not a.no_lp_weights,
-                               worker_batching=False if a.no_worker_batching else None)
+                               worker_batching=False if a.no_worker_batching else None, **amp)
         torch.manual_seed(1234)
         eng_avg = RobustDataParallel(build_model(a.model, num_classes=num_classes), F.cross_entropy, ctx, cfg_avg)
         e_avg, _ = timed_steps(eng_avg, batches, a.steps, a.warmup, ctx)
@@ -225,7 +234,8 @@ def main():
 
         torch.manual_seed(1234)
         ref = ReferenceStyleDP(build_model(a.model, num_classes=num_classes), F.cross_entropy, ctx.device,
-                               a.workers_per_gpu, a.f, a.lr, gar=a.gar if a.gar in ("krum", "average") else "krum")
+                               a.workers_per_gpu, a.f, a.lr, gar=a.gar if a.gar in ("krum", "average") else "krum",
+                               autocast_dtype=None if fp32 else torch.bfloat16)
         e_ref, _ = timed_steps(ref, batches, a.steps, a.warmup, ctx)
         ms_ref = 1000.0 * e_ref / a.steps
         extra["ref_impl_ms_per_step"] = round(ms_ref, 3)
@@ -245,7 +255,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16",
+            "dtype": a.precision,
             "data": f"synthetic (random {'CIFAR-10' if a.dataset == 'cifar10' else 'ImageNet'}-shape images, "
                     + ("fresh samples every step from a GPU-resident uint8 dataset with random crop + flip + "
                        "normalise, " if a.data == "fresh" else "the same batches every step, ")
