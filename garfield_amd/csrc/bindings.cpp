@@ -663,6 +663,32 @@ void g_large_coord(const at::Tensor& x, int64_t mode, int64_t f, int64_t beta, c
                              static_cast<int>(f), static_cast<int>(beta), out.data_ptr(), stream_of(x.device()));
 }
 
+// Split-K slabs -> strided per-group output: part fp32 [S, G, *shape] (any slab/group strides,
+// contiguous inner), out [G, *shape] (any group stride, contiguous inner), fp32 / bf16 / fp16.
+void g_split_reduce(const at::Tensor& part, const at::Tensor& out) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() >= 3,
+              "gpu_split_reduce: part must be an fp32 [S, G, ...] GPU tensor");
+  TORCH_CHECK(out.device() == part.device() && out.dim() == part.dim() - 1 && out.size(0) == part.size(1),
+              "gpu_split_reduce: out must be [G, ...] on part's device");
+  const int64_t S = part.size(0), G = part.size(1);
+  int64_t N = 1;
+  for (int64_t k = 2; k < part.dim(); ++k) {
+    TORCH_CHECK(part.size(k) == out.size(k - 1), "gpu_split_reduce: part and out shapes differ");
+    N *= part.size(k);
+  }
+  // the inner dims must be dense (row-major) in both
+  int64_t acc = 1;
+  for (int64_t k = part.dim() - 1; k >= 2; --k) {
+    TORCH_CHECK(part.stride(k) == acc && out.stride(k - 1) == acc, "gpu_split_reduce: inner dims must be dense");
+    acc *= part.size(k);
+  }
+  const int odt = dtype_code(out);
+  TORCH_CHECK(odt != garfield::kF64, "gpu_split_reduce: out must be fp32, bf16 or fp16");
+  c10::hip::HIPGuard guard(part.device().index());
+  garfield::gpu::split_reduce(part.data_ptr<float>(), static_cast<int>(S), static_cast<int>(G), N, part.stride(0),
+                              part.stride(1), out.data_ptr(), odt, out.stride(0), stream_of(part.device()));
+}
+
 // Fresh grouped batch: out [R, C, H, W] bf16 channels_last from uint8 NHWC images src[idx[r]].
 void g_augment_gather(const at::Tensor& src, const c10::optional<at::Tensor>& idx_opt, int64_t seed, int64_t step,
                       const std::vector<double>& mean, const std::vector<double>& std, const at::Tensor& out,
@@ -1013,6 +1039,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_large_coord", &g_large_coord,
         "Coordinate-wise rule on an [n, d] gradient matrix with n <= LARGE_ROWS by LDS radix select; "
         "args (x, mode 0 median | 1 trimmed-mean | 2 averaged-median, f, beta, out)");
+  m.def("gpu_split_reduce", &g_split_reduce,
+        "out[g] = Σ_s part[s, g] (fp32 accumulation, one launch; out may be strided exchange rows); args (part, out)");
   m.def("gpu_augment_gather", &g_augment_gather,
         "Fresh batch in one launch: out[r] = normalise(random crop (pad) + flip of uint8 NHWC image src[idx[r]]), "
         "bf16 channels_last; crop/flip per row from a hash of (seed, step, r); idx None: the image index is drawn "

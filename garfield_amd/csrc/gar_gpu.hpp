@@ -71,6 +71,11 @@ void sqdist_partial(const RowTable& rows, int n, int64_t d, int dt, const float*
 void aksel_select(const float* slabs, int grid, int n, int c, float* weights, float* dists,
                   hipStream_t stream);
 
+// ---- Split-K partial sums -> exchange rows (gar_flatten.hip) -----------------
+// out[g * ostride + i] = Σ_s part[s * ss + g * gs + i] (cast to odt), 0 <= i < N, 0 <= g < G.
+void split_reduce(const float* part, int S, int G, int64_t N, int64_t ss, int64_t gs, void* out, int odt,
+                  int64_t ostride, hipStream_t stream);
+
 // ---- Multi-tensor flatten + cast (per-parameter grads -> exchange row) -----
 constexpr int kMaxFlatTensors = 96;  // tensors per launch (kernarg budget); more => several launches
 int flatten_cast(const void* const* srcs, const int* src_dts, const int64_t* numels, const int64_t* offsets,

@@ -527,7 +527,11 @@ def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int)
         return
     part = torch.empty((S, G, cout, K), dtype=torch.float32, device=dy.device)
     C_.gpu_iwgrad(x, dy, *_geom(spec), G, part, S)
-    spec.sink.put_groups(spec.conv.weight, part.sum(0) if S > 1 else part[0])
+    rows = spec.sink.rows_view(spec.conv.weight, (cout, K), spec.sink.flat.dtype)
+    if rows is not None:     # the S slabs summed straight into the exchange rows (one launch)
+        C_.gpu_split_reduce(part, rows)
+    else:
+        spec.sink.put_groups(spec.conv.weight, part.sum(0) if S > 1 else part[0])
 
 
 def _dgrad_weight_shape(w: torch.Tensor) -> torch.Tensor:
@@ -573,6 +577,12 @@ def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int, out: torch.Tensor | None
         if out is not None:
             return torch.bmm(dy2.view(G, M, cout).transpose(1, 2), a2.view(G, M, K), out=out)
         return torch.bmm(dy2.view(G, M, cout).transpose(1, 2), a2.view(G, M, K))
+    if dy2.is_cuda and out is not None and dy2.dtype in (torch.bfloat16, torch.float16):
+        # fp32 partials (no per-split rounding), summed into the exchange rows by one launch
+        part = torch.bmm(dy2.view(G * S, M // S, cout).transpose(1, 2), a2.view(G * S, M // S, K),
+                         out_dtype=torch.float32)
+        _native.native().gpu_split_reduce(part.view(G, S, cout, K).transpose(0, 1), out)
+        return out
     part = torch.bmm(dy2.view(G * S, M // S, cout).transpose(1, 2), a2.view(G * S, M // S, K))
     if out is not None:
         return torch.sum(part.view(G, S, cout, K), 1, out=out)   # fp32 accumulation, one rounding

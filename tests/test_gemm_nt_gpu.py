@@ -75,3 +75,26 @@ def test_fused_bn_statistics_match_fp32(cuda, native, G, rg, K, N, offset):
         assert ((var - vref).abs() / vref.clamp_min(1e-6)).max().item() < 2e-3, cfg
         yref = ((yg - mref[:, None]) / torch.sqrt(vref[:, None] + 1e-5) * gam.double() + bet.double()).view(M, N)
         assert rel(out, yref) < 1e-2, cfg
+
+
+@pytest.mark.parametrize("S,G,shape", [(4, 8, (64, 72)), (16, 3, (128, 9)), (2, 5, (7,))])
+def test_split_reduce_into_strided_rows(cuda, native, S, G, shape):
+    """Split-K slabs summed in fp32 straight into strided (exchange-row) outputs."""
+    torch.manual_seed(S * G)
+    part = torch.randn((S, G, *shape), device=cuda)
+    n = part[0, 0].numel()
+    for dt in (torch.bfloat16, torch.float32):
+        flat = torch.zeros(G * (n + 40) + 8, device=cuda, dtype=dt)
+        strides = [n + 40]
+        acc = 1
+        for d in reversed(shape):
+            strides.insert(1, acc)
+            acc *= d
+        out = flat.as_strided((G, *shape), tuple(strides), 8)
+        native.gpu_split_reduce(part, out)
+        assert rel(out, part.double().sum(0)) < (1e-6 if dt == torch.float32 else 5e-3)
+        # a transposed slab view ([G, S, ...] storage) works too
+        p2 = part.transpose(0, 1).contiguous().transpose(0, 1)
+        out.zero_()
+        native.gpu_split_reduce(p2, out)
+        assert rel(out, part.double().sum(0)) < (1e-6 if dt == torch.float32 else 5e-3)
