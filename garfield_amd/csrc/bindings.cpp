@@ -663,30 +663,39 @@ void g_large_coord(const at::Tensor& x, int64_t mode, int64_t f, int64_t beta, c
                              static_cast<int>(f), static_cast<int>(beta), out.data_ptr(), stream_of(x.device()));
 }
 
-// Split-K slabs -> strided per-group output: part fp32 [S, G, *shape] (any slab/group strides,
-// contiguous inner), out [G, *shape] (any group stride, contiguous inner), fp32 / bf16 / fp16.
+// Split-K slabs -> strided per-group output: part fp32 [S, G, ...] and out [G, ...] (fp32 / bf16 /
+// fp16) may have any slab / group strides and one row pitch each (the last dim contiguous, the
+// dims between it and the group dim dense), e.g. a padded GEMM result cropped into exchange rows.
 void g_split_reduce(const at::Tensor& part, const at::Tensor& out) {
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() >= 3,
               "gpu_split_reduce: part must be an fp32 [S, G, ...] GPU tensor");
   TORCH_CHECK(out.device() == part.device() && out.dim() == part.dim() - 1 && out.size(0) == part.size(1),
               "gpu_split_reduce: out must be [G, ...] on part's device");
-  const int64_t S = part.size(0), G = part.size(1);
-  int64_t N = 1;
-  for (int64_t k = 2; k < part.dim(); ++k) {
+  const int64_t S = part.size(0), G = part.size(1), D = part.dim();
+  for (int64_t k = 2; k < D; ++k)
     TORCH_CHECK(part.size(k) == out.size(k - 1), "gpu_split_reduce: part and out shapes differ");
-    N *= part.size(k);
-  }
-  // the inner dims must be dense (row-major) in both
-  int64_t acc = 1;
-  for (int64_t k = part.dim() - 1; k >= 2; --k) {
-    TORCH_CHECK(part.stride(k) == acc && out.stride(k - 1) == acc, "gpu_split_reduce: inner dims must be dense");
-    acc *= part.size(k);
+  const int64_t Cc = part.size(D - 1);
+  TORCH_CHECK(part.stride(D - 1) == 1 && out.stride(D - 2) == 1, "gpu_split_reduce: the last dim must be contiguous");
+  int64_t R = 1, ipitch = Cc, opitch = Cc;
+  if (D >= 4) {
+    ipitch = part.stride(D - 2);
+    opitch = out.stride(D - 3);
+    // dims [2, D-2) must be dense over the row pitch
+    int64_t ai = ipitch, ao = opitch;
+    for (int64_t k = D - 2; k >= 2; --k) {
+      TORCH_CHECK(part.stride(k) == ai && out.stride(k - 1) == ao, "gpu_split_reduce: outer inner dims must be dense");
+      ai *= part.size(k);
+      ao *= part.size(k);
+      R *= part.size(k);
+    }
+    TORCH_CHECK(ipitch >= Cc && opitch >= Cc, "gpu_split_reduce: row pitch below the row length");
   }
   const int odt = dtype_code(out);
   TORCH_CHECK(odt != garfield::kF64, "gpu_split_reduce: out must be fp32, bf16 or fp16");
   c10::hip::HIPGuard guard(part.device().index());
-  garfield::gpu::split_reduce(part.data_ptr<float>(), static_cast<int>(S), static_cast<int>(G), N, part.stride(0),
-                              part.stride(1), out.data_ptr(), odt, out.stride(0), stream_of(part.device()));
+  garfield::gpu::split_reduce(part.data_ptr<float>(), static_cast<int>(S), static_cast<int>(G), R, Cc, ipitch, opitch,
+                              part.stride(0), part.stride(1), out.data_ptr(), odt, out.stride(0),
+                              stream_of(part.device()));
 }
 
 // Fresh grouped batch: out [R, C, H, W] bf16 channels_last from uint8 NHWC images src[idx[r]].

@@ -98,28 +98,32 @@ int flatten_cast(const void* const* srcs, const int* src_dts, const int64_t* num
 }  // namespace garfield
 
 // ---------------------------------------------------------------------------
-// Split-K partial sums -> exchange rows: out[g * ostride + i] = cast(Σ_s part[s * ss + g * gs + i]),
-// i < N, for the per-worker weight gradients computed in S pixel splits (grouped step). One
-// launch replaces an ATen reduction + a cast/scatter; 4 fp32 per lane when everything is
-// 16-byte aligned.
+// Split-K partial sums -> exchange rows: out[g * ostride + r * opitch + c] =
+// cast(Σ_s part[s * ss + g * gs + r * ipitch + c]), r < R, c < Cc, for the per-worker weight
+// gradients computed in S pixel splits (grouped step). One launch replaces an ATen reduction +
+// a cast/scatter (and, with ipitch > Cc, the crop of padded GEMM columns); 4 fp32 per lane
+// when everything is 16-byte aligned.
 namespace garfield {
 namespace gpu {
 namespace {
 
 template <int ODT, bool VEC>
-__global__ __launch_bounds__(256) void k_split_reduce(const float* __restrict__ part, int S, int G, int64_t N,
-                                                      int64_t ss, int64_t gs, void* __restrict__ out,
-                                                      int64_t ostride) {
+__global__ __launch_bounds__(256) void k_split_reduce(const float* __restrict__ part, int S, int G, int64_t R,
+                                                      int64_t Cc, int64_t ipitch, int64_t opitch, int64_t ss,
+                                                      int64_t gs, void* __restrict__ out, int64_t ostride) {
   constexpr int V = VEC ? 4 : 1;
-  const int64_t per = (N + V - 1) / V;
+  const int64_t cv = (Cc + V - 1) / V;
+  const int64_t per = R * cv;
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= per * G) return;
   const int g = static_cast<int>(t / per);
-  const int64_t i = (t - static_cast<int64_t>(g) * per) * V;
+  const int64_t rem = t - static_cast<int64_t>(g) * per;
+  const int64_t r = rem / cv;
+  const int64_t c = (rem - r * cv) * V;
   float acc[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
-  const float* p = part + static_cast<int64_t>(g) * gs + i;
+  const float* p = part + static_cast<int64_t>(g) * gs + r * ipitch + c;
   for (int s = 0; s < S; ++s) {
     if constexpr (VEC) {
       const float4 a = *reinterpret_cast<const float4*>(p + static_cast<int64_t>(s) * ss);
@@ -128,22 +132,25 @@ __global__ __launch_bounds__(256) void k_split_reduce(const float* __restrict__ 
       acc[0] += p[static_cast<int64_t>(s) * ss];
     }
   }
-  const int64_t o = static_cast<int64_t>(g) * ostride + i;
+  const int64_t o = static_cast<int64_t>(g) * ostride + r * opitch + c;
 #pragma unroll
   for (int v = 0; v < V; ++v) dev::store_one(out, ODT, o + v, acc[v]);
 }
 
 }  // namespace
 
-void split_reduce(const float* part, int S, int G, int64_t N, int64_t ss, int64_t gs, void* out, int odt,
-                  int64_t ostride, hipStream_t stream) {
-  const bool vec = N % 4 == 0 && ss % 4 == 0 && gs % 4 == 0 && reinterpret_cast<uintptr_t>(part) % 16 == 0;
-  const int64_t work = (vec ? N / 4 : N) * G;
+void split_reduce(const float* part, int S, int G, int64_t R, int64_t Cc, int64_t ipitch, int64_t opitch, int64_t ss,
+                  int64_t gs, void* out, int odt, int64_t ostride, hipStream_t stream) {
+  const bool vec = Cc % 4 == 0 && ipitch % 4 == 0 && ss % 4 == 0 && gs % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(part) % 16 == 0;
+  const int64_t work = (vec ? Cc / 4 : Cc) * R * G;
   if (work <= 0) return;
   const dim3 grid(static_cast<unsigned>((work + 255) / 256));
-#define GARFIELD_SPLIT(ODT)                                                                                        \
-  if (vec) hipLaunchKernelGGL((k_split_reduce<ODT, true>), grid, dim3(256), 0, stream, part, S, G, N, ss, gs, out, ostride); \
-  else hipLaunchKernelGGL((k_split_reduce<ODT, false>), grid, dim3(256), 0, stream, part, S, G, N, ss, gs, out, ostride)
+#define GARFIELD_SPLIT(ODT)                                                                                     \
+  if (vec) hipLaunchKernelGGL((k_split_reduce<ODT, true>), grid, dim3(256), 0, stream, part, S, G, R, Cc, ipitch, \
+                              opitch, ss, gs, out, ostride);                                                      \
+  else hipLaunchKernelGGL((k_split_reduce<ODT, false>), grid, dim3(256), 0, stream, part, S, G, R, Cc, ipitch,    \
+                          opitch, ss, gs, out, ostride)
   if (odt == kBF16) { GARFIELD_SPLIT(kBF16); }
   else if (odt == kF16) { GARFIELD_SPLIT(kF16); }
   else { GARFIELD_SPLIT(kF32); }

@@ -72,9 +72,10 @@ void aksel_select(const float* slabs, int grid, int n, int c, float* weights, fl
                   hipStream_t stream);
 
 // ---- Split-K partial sums -> exchange rows (gar_flatten.hip) -----------------
-// out[g * ostride + i] = Σ_s part[s * ss + g * gs + i] (cast to odt), 0 <= i < N, 0 <= g < G.
-void split_reduce(const float* part, int S, int G, int64_t N, int64_t ss, int64_t gs, void* out, int odt,
-                  int64_t ostride, hipStream_t stream);
+// out[g * ostride + r * opitch + c] = Σ_s part[s * ss + g * gs + r * ipitch + c] (cast to odt),
+// r < R, c < Cc, g < G.
+void split_reduce(const float* part, int S, int G, int64_t R, int64_t Cc, int64_t ipitch, int64_t opitch, int64_t ss,
+                  int64_t gs, void* out, int odt, int64_t ostride, hipStream_t stream);
 
 // ---- Multi-tensor flatten + cast (per-parameter grads -> exchange row) -----
 constexpr int kMaxFlatTensors = 96;  // tensors per launch (kernarg budget); more => several launches

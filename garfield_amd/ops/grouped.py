@@ -405,6 +405,7 @@ class ConvSpec:
         self.gemm = (self.kernel == (1, 1) and self.stride == (1, 1) and self.padding == (0, 0)
                      and self.dilation == (1, 1))
         self.bn_next = None       # BNState of the BatchNorm that consumes this convolution's output
+        self.wpad = None          # persistent zero-padded [Cout, Kp] weight matrix (im2col + GEMM layers)
 
 
 def _gemm_nt_forward(x2: torch.Tensor, w2: torch.Tensor, spec: ConvSpec):
@@ -460,10 +461,20 @@ def _im2col(x: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
     return col
 
 
-def _wmat(w: torch.Tensor, kp: int) -> torch.Tensor:
-    """channels_last weight [Cout, Cin, KH, KW] -> [Cout, Kp] in (kh, kw, ci) column order."""
+def _wmat(w: torch.Tensor, kp: int, spec: "ConvSpec | None" = None) -> torch.Tensor:
+    """channels_last weight [Cout, Cin, KH, KW] -> [Cout, Kp] in (kh, kw, ci) column order. With
+    ``spec``, zero padding columns live in a persistent buffer and only the weight is copied
+    (one kernel instead of a fill + a copy per call)."""
     w2 = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
-    return F.pad(w2, (0, kp - w2.shape[1])) if kp != w2.shape[1] else w2
+    if kp == w2.shape[1]:
+        return w2
+    if spec is None:
+        return F.pad(w2, (0, kp - w2.shape[1]))
+    buf = spec.wpad
+    if buf is None or buf.shape != (w2.shape[0], kp) or buf.dtype != w2.dtype or buf.device != w2.device:
+        buf = spec.wpad = torch.zeros((w2.shape[0], kp), dtype=w2.dtype, device=w2.device)
+    buf[:, :w2.shape[1]].copy_(w2)
+    return buf
 
 
 def _iconv_ok(x: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
@@ -573,19 +584,21 @@ def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int, out: torch.Tensor | None
     # (scripts/bench_wgrad_1x1.py, profiles/bench_wgrad_1x1_r1.log); 1000 rows lose
     while S < 16 and M % (2 * S) == 0 and (M // (2 * S) >= 4000 or (S < 4 and M // (2 * S) >= 1000)):
         S *= 2
-    if S == 1:
+    Ko = out.shape[-1] if out is not None else K          # out may drop padding columns (K >= Ko)
+    if S == 1 and Ko == K:
         if out is not None:
             return torch.bmm(dy2.view(G, M, cout).transpose(1, 2), a2.view(G, M, K), out=out)
         return torch.bmm(dy2.view(G, M, cout).transpose(1, 2), a2.view(G, M, K))
     if dy2.is_cuda and out is not None and dy2.dtype in (torch.bfloat16, torch.float16):
-        # fp32 partials (no per-split rounding), summed into the exchange rows by one launch
+        # fp32 partials (no per-split rounding), summed (and cropped to Ko columns) into the
+        # exchange rows by one launch
         part = torch.bmm(dy2.view(G * S, M // S, cout).transpose(1, 2), a2.view(G * S, M // S, K),
                          out_dtype=torch.float32)
-        _native.native().gpu_split_reduce(part.view(G, S, cout, K).transpose(0, 1), out)
+        _native.native().gpu_split_reduce(part.view(G, S, cout, K).transpose(0, 1)[..., :Ko], out)
         return out
     part = torch.bmm(dy2.view(G * S, M // S, cout).transpose(1, 2), a2.view(G * S, M // S, K))
     if out is not None:
-        return torch.sum(part.view(G, S, cout, K), 1, out=out)   # fp32 accumulation, one rounding
+        return torch.sum(part.view(G, S, cout, K)[..., :Ko], 1, out=out)   # fp32 accumulation, one rounding
     return part.view(G, S, cout, K).float().sum(1)
 
 
@@ -660,7 +673,7 @@ class _GroupedConv(torch.autograd.Function):
             ctx.mode = "col"
             col = _im2col(x, spec)
             ho, wo = _out_hw(spec, h, wd)
-            y = from_rows(torch.mm(col, _wmat(w, col.shape[1]).t()), n, ho, wo)
+            y = from_rows(torch.mm(col, _wmat(w, col.shape[1], spec).t()), n, ho, wo)
             ctx.save_for_backward(col, w)
             return y
         ctx.mode = "aten"
@@ -711,7 +724,7 @@ class _GroupedConv(torch.autograd.Function):
                     dx = _iconv(dy, w, (kh, kw, 1, 1, kh - 1 - ph, kw - 1 - pw, 1, 1), (h, wd),
                                 _cl(prev) if prev is not None else None, transpose_w=True)
                 else:
-                    dcol = torch.mm(dy2, _wmat(w, kp))
+                    dcol = torch.mm(dy2, _wmat(w, kp, spec))
                     if prev is not None:
                         dx = _cl(prev)
                         _native.native().gpu_col2im(dcol, *_geom(spec), dx, True)
@@ -725,7 +738,8 @@ class _GroupedConv(torch.autograd.Function):
                     _iwgrad(a, dy, spec, G, K)
             elif spec.sink is not None:
                 with _wgrad_ctx(col, dy):
-                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if kp == K else None
+                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if (kp == K or dy2.is_cuda) \
+                        else None
                     dW = _wgrad(dy2, col, G, out)
                     if out is None:
                         if kp != K:
@@ -734,7 +748,7 @@ class _GroupedConv(torch.autograd.Function):
         elif mode == "col":                      # a = col [N*Ho*Wo, Kp]
             kp = a.shape[1]
             if need_dx:
-                dcol = torch.mm(dy2, _wmat(w, kp))
+                dcol = torch.mm(dy2, _wmat(w, kp, spec))
                 if prev is not None:
                     dx = _cl(prev)
                     _native.native().gpu_col2im(dcol, *_geom(spec), dx, True)
@@ -747,7 +761,8 @@ class _GroupedConv(torch.autograd.Function):
                 # weight's channels_last memory order, one batched GEMM for all workers
                 K = w.numel() // cout
                 with _wgrad_ctx(a, dy):
-                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if kp == K else None
+                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if (kp == K or dy2.is_cuda) \
+                        else None
                     dW = _wgrad(dy2, a, G, out)
                     if out is None:
                         if kp != K:

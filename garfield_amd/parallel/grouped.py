@@ -62,6 +62,7 @@ class GroupedResNet:
         self.conv = {m: ConvSpec(m, sink, self.groups) for m in model.modules() if isinstance(m, nn.Conv2d)}
         self.fc = LinearSpec(model.fc, sink, self.groups)
         self.bn: dict = {}
+        self._seed = None
         self.join_residuals = True
         # bucket marks: the backward records an event when it has produced every
         # gradient of the named layer and the layers after it (the exchange of that
@@ -169,7 +170,11 @@ class GroupedResNet:
         if x.shape[0] % self.groups:
             raise ValueError(f"batch of {x.shape[0]} rows is not divisible into {self.groups} workers")
         per = self.losses(self.forward(x), y)
-        per.sum().backward()
+        # d(Σ_g loss_g)/d loss_g = 1: seeded directly (no sum / fill / expand kernels)
+        if self._seed is None or self._seed.shape != per.shape or self._seed.device != per.device \
+                or self._seed.dtype != per.dtype:
+            self._seed = torch.ones_like(per)
+        per.backward(self._seed)
         if x.is_cuda:
             WgradStream.join(x.device)   # weight gradients computed on the side stream
         self.sink.flush()

@@ -98,3 +98,15 @@ def test_split_reduce_into_strided_rows(cuda, native, S, G, shape):
         out.zero_()
         native.gpu_split_reduce(p2, out)
         assert rel(out, part.double().sum(0)) < (1e-6 if dt == torch.float32 else 5e-3)
+
+
+def test_split_reduce_crops_padded_columns(cuda, native):
+    """A padded GEMM result [S, G, Cout, Kp] cropped to K columns into exchange rows (the stem)."""
+    torch.manual_seed(3)
+    S, G, co, kp, k = 8, 8, 64, 152, 147
+    part = torch.randn((G, S, co, kp), device=cuda).transpose(0, 1)     # the split-K bmm layout
+    flat = torch.zeros(G * (co * k + 100), device=cuda, dtype=torch.bfloat16)
+    out = flat.as_strided((G, co, k), (co * k + 100, k, 1), 0)
+    native.gpu_split_reduce(part[..., :k], out)
+    assert rel(out, part[..., :k].double().sum(0)) < 5e-3
+    assert int((flat.view(G, -1)[:, co * k:] != 0).sum()) == 0          # nothing written past the rows
