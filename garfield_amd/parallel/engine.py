@@ -261,8 +261,11 @@ class RobustDataParallel:
         sink = GradSink(self.X.view(-1), nrow * self.ld, self.xr * self.ld, offsets, self.k)
         # bucket marks (sharded multi-rank exchange): the backward records an event when
         # it has written the gradients of layer4 + fc, then of layer3
-        marks = ("layer4", "layer3") if self._sharded else ()
-        self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn, marks=marks, offsets=offsets)
+        from garfield_amd.parallel.sharded import overlap_enabled
+
+        buckets = ("layer4", "layer3") if self._sharded else ()
+        self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn, marks=buckets, offsets=offsets,
+                                    signals=overlap_enabled())
         self._gx = self._gy = None
         self._gsrc = None
         self._gsrc_refs = None

@@ -51,7 +51,7 @@ class GroupedResNet:
     exchange row through ``sink`` and returns the per-worker mean losses."""
 
     def __init__(self, model: ResNet, groups: int, sink: GradSink, loss_fn=F.cross_entropy, marks=(),
-                 offsets: dict | None = None):
+                 offsets: dict | None = None, signals: bool = True):
         if not supports(model):
             raise ValueError("GroupedResNet supports the zoo's ResNet models only")
         self.model = model
@@ -71,7 +71,7 @@ class GroupedResNet:
         self.marks = tuple(marks)
         self._offsets = offsets or {}
         self._events = None
-        if self.marks and next(model.parameters()).is_cuda:
+        if signals and self.marks and next(model.parameters()).is_cuda:   # else the marks only cut buckets
             dev = next(model.parameters()).device
             sig = {name: GraphSignal(dev) for name in self.marks}
             if all(x.available() for x in sig.values()):

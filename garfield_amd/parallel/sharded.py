@@ -64,8 +64,14 @@ def shard_pad(world: int, base: int = 64) -> int:
 
 
 def overlap_enabled() -> bool:
-    """GARFIELD_OVERLAP=0: exchange after the whole backward (A/B runs, debugging)."""
-    return os.environ.get("GARFIELD_OVERLAP", "1") != "0"
+    """GARFIELD_OVERLAP=1: each bucket's exchange waits on a signal written INSIDE the step's
+    graph (hipStreamWaitValue64), so it can leave during the backward. Off by default: on
+    ROCm 7 / MI355X every such command-processor wait measured ~0.45 ms of latency (the
+    world-1 bucketed step: 9.0 ms/step with the signals vs 7.2 ms without them,
+    profiles/r2/ab_overlap_signals.log), more than the overlap can hide. Without it the
+    buckets leave right after the backward and the per-bucket aggregation pipelines with
+    the later buckets' transfers."""
+    return os.environ.get("GARFIELD_OVERLAP", "0") != "0"
 
 
 class _Bucket:

@@ -162,14 +162,16 @@ def test_cuda_graph_never_writes_loader_tensors(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rule,f", [("krum", 2), ("median", 1), ("bulyan", 1)])
-def test_bucketed_exchange_overlap_loopback(cuda, rule, f, monkeypatch):
+@pytest.mark.parametrize("rule,f,overlap", [("krum", 2, "1"), ("median", 1, "1"), ("bulyan", 1, "1"),
+                                            ("krum", 2, "0")])
+def test_bucketed_exchange_overlap_loopback(cuda, rule, f, overlap, monkeypatch):
     """Sharded aggregation with layer buckets on one rank, the exchange emulated by
     copies on the side stream (GARFIELD_LOOPBACK_EXCHANGE=1) that start when the
     HIP-graph backward records each bucket's event: fresh inputs every step, so a
     copy that ran before its bucket was written would read the previous step's
     gradients. Must equal the redundant (unsharded) path."""
     monkeypatch.setenv("GARFIELD_LOOPBACK_EXCHANGE", "1")
+    monkeypatch.setenv("GARFIELD_OVERLAP", overlap)     # in-graph bucket signals, or after the backward
     outs = []
     for shard in (False, True):
         torch.manual_seed(0)
@@ -178,7 +180,7 @@ def test_bucketed_exchange_overlap_loopback(cuda, rule, f, monkeypatch):
         eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
         if shard:
             assert eng._gexec is not None and len(eng._shard.buckets) == 3
-            assert eng._gexec.mark_events() is not None
+            assert (eng._gexec.mark_events() is not None) == (overlap == "1")
         for it in range(4):
             b = synthetic_batches(8, 8, (3, 32, 32), 10, cuda, seed=100 + it)
             eng.step(b)
