@@ -29,9 +29,11 @@ CLASSES = [
     ("im2col / col2im", r"im2col|col2im"),
     ("max-pool", r"maxpool"),
     ("GAR (Gram / selection / coordinate rules / combine+SGD)", r"k_gram|k_select|k_combine|k_coord|k_krum|k_bulyan|"
-                                                               r"k_median|k_tail|k_brute|gar"),
+                                                               r"k_median|k_tail|k_brute|k_aksel|k_sqdist|k_large|"
+                                                               r"k_window|k_mean"),
     ("cross-entropy", r"k_xent"),
-    ("flatten / cast into the exchange rows", r"flatten|cast"),
+    ("fresh-batch gather / augmentation", r"k_augment"),
+    ("flatten / cast / split-K sums into the exchange rows", r"flatten|cast|split_reduce"),
     ("ATen reductions / elementwise", r"at::native"),
 ]
 
