@@ -98,3 +98,16 @@ def test_bench_py_rejects_world_mismatch():
                         "--model", "cifarnet", "--batch", "2", "--workers-per-gpu", "3", "--f", "1"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode != 0 and not _rows(r.stdout)
+
+
+def test_bench_py_fp32_and_static_data_modes():
+    """--precision fp32 reports dtype fp32 (reference precision end to end); --data static and
+    the default fresh-data feed both produce one JSON line with the data mode stated."""
+    for extra, dtype, word in ((["--precision", "fp32"], "fp32", "fresh samples"),
+                               (["--data", "static"], "bf16", "same batches")):
+        r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--steps", "1", "--warmup", "1",
+                            "--model", "cifarnet", "--batch", "4", "--workers-per-gpu", "5", "--f", "1", *extra],
+                           capture_output=True, text=True, timeout=600, env=_env())
+        assert r.returncode == 0, r.stderr[-3000:]
+        rows = _rows(r.stdout)
+        assert len(rows) == 1 and rows[0]["dtype"] == dtype and word in rows[0]["data"], rows
