@@ -62,7 +62,10 @@ IWGRAD = os.environ.get("GARFIELD_IWGRAD", "1") != "0"
 IWGRAD_1X1 = os.environ.get("GARFIELD_IWGRAD_1X1", "0") != "0"   # measured a wash: 7.715 vs 7.739 ms/step
 # weight gradients on a side stream (see WgradStream): measured slower in the graphed step
 # (7.23 vs 7.07 ms: per-layer fork/join dependencies leave 8% of the window idle), so off
-WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0") != "0"
+WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0")
+# "small": only layers with <= WGRAD_STREAM_ROWS output rows in the whole grouped batch (CIFAR
+# layer3/layer4), whose kernels are latency-bound and leave most CUs idle
+WGRAD_STREAM_ROWS = int(os.environ.get("GARFIELD_WGRAD_STREAM_ROWS", "8000"))
 XENT = os.environ.get("GARFIELD_XENT", "1") != "0"   # fused per-worker cross-entropy kernel
 # Forward 1x1 convolutions with <= GEMM_NT_MAXN output channels on the hand-written MFMA GEMM
 # (gemm_nt.hip), which also emits the next BatchNorm's per-worker statistics (no partial pass).
@@ -638,10 +641,16 @@ class WgradStream:
 
 
 def _wgrad_ctx(*tensors):
-    """Side-stream context for a weight-gradient computation (a no-op on CPU or when disabled)."""
-    if WGRAD_STREAM and tensors[0].is_cuda:
-        return WgradStream.fork(*tensors)
-    return contextlib.nullcontext()
+    """Side-stream context for a weight-gradient computation (a no-op on CPU or when disabled).
+    ``tensors[-1]`` is the layer's output gradient dy (its rows decide the "small" mode)."""
+    if WGRAD_STREAM == "0" or not tensors[0].is_cuda:
+        return contextlib.nullcontext()
+    if WGRAD_STREAM == "small":
+        dy = tensors[-1]
+        rows = dy.numel() // dy.shape[1] if dy.dim() >= 2 else dy.numel()
+        if rows > WGRAD_STREAM_ROWS:
+            return contextlib.nullcontext()
+    return WgradStream.fork(*tensors)
 
 
 class _GroupedConv(torch.autograd.Function):
