@@ -1048,6 +1048,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_large_coord", &g_large_coord,
         "Coordinate-wise rule on an [n, d] gradient matrix with n <= LARGE_ROWS by LDS radix select; "
         "args (x, mode 0 median | 1 trimmed-mean | 2 averaged-median, f, beta, out)");
+  m.def("iwgrad_taps_per_block", [](int64_t kw) { return garfield::gpu::iwgrad_taps_per_block(static_cast<int>(kw)); },
+        "Taps per workgroup gpu_iwgrad uses for kernel width kw (3: a kernel row shares each dy tile)");
   m.def("gpu_split_reduce", &g_split_reduce,
         "out[g] = Σ_s part[s, g] (fp32 accumulation, one launch; out may be strided exchange rows); args (part, out)");
   m.def("gpu_augment_gather", &g_augment_gather,

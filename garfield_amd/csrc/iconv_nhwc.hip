@@ -24,6 +24,8 @@
 // channels; grid (ceil(M / (64*PM)), Cout / 64). Requires C % 32 == 0 and
 // Cout % 64 == 0 (checked by the host wrapper). Out-of-range taps read a clamped
 // in-bounds address and are zeroed in registers (no branch around the load).
+#include <cstdlib>
+
 #include "bn_gpu.hpp"
 #include "gar_device.hpp"
 
@@ -487,6 +489,151 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
       }
 }
 
+
+// Weight gradient of all THREE taps of one kernel row per workgroup (KW == 3): the k-step's
+// 32-pixel dy tile is staged once and feeds the three taps' MFMAs (the per-tap kernel above
+// re-reads it for every tap: 9x dy traffic on a 3x3 layer, 3x here). Stage = dy tile + the
+// three shifted x tiles (16 KiB); wave tile = 2 output-channel fragments x 2 k-fragments per tap.
+template <int NS, bool OUT_BF16>
+__global__ __launch_bounds__(256) void k_iwgrad_row(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                    Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
+                                                    int64_t split_stride, int64_t group_stride) {
+  constexpr int TB = 32 * 128;  // one 32-pixel x 64-channel tile
+  constexpr int NT = 3;         // taps per kernel row
+  constexpr int SB = (1 + NT) * TB;
+  __shared__ __attribute__((aligned(16))) char lds[NS * SB];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int K = g.KH * g.KW * g.C;
+  const int ncb = g.C / 64;
+  const int nq = g.KH * ncb;
+  const int qb = blockIdx.x % nq, cb = blockIdx.x / nq;
+  const int ti = qb / ncb, c0 = (qb - ti * ncb) * 64;
+  const int co0 = cb * 64;
+  const int gi = blockIdx.y, sp = blockIdx.z;
+  const int64_t mbeg = static_cast<int64_t>(gi) * rg + static_cast<int64_t>(sp) * per_split;
+  int64_t mend = mbeg + per_split;
+  if (mend > static_cast<int64_t>(gi + 1) * rg) mend = static_cast<int64_t>(gi + 1) * rg;
+  const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
+
+  const int lrow = wave * 8 + (lane >> 3), lchunk = lane & 7;
+  const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
+  const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
+
+  auto issue = [&](int s, int slot) {
+    const int m = static_cast<int>(mbeg) + s * 32 + lrow;
+    const bool mv = m < static_cast<int>(mend);
+    const int mm = mv ? m : 0;
+    char* base = lds + slot * SB;
+    const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lchunk * 8);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? ady : az), (lds_ptr)(base + wave * 1024), 16,
+                                     0, 0);
+    const int wo = mm % g.Wo;
+    const int t = mm / g.Wo;
+    const int ho = t % g.Ho;
+    const int n = t / g.Ho;
+    const int hi = ho * g.sh - g.ph + ti * g.dh;
+    const bool rok = mv && hi >= 0 && hi < g.H;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int wi = wo * g.sw - g.pw + j * g.dw;
+      const bool ok = rok && wi >= 0 && wi < g.W;
+      const uint64_t ax = reinterpret_cast<uint64_t>(
+          x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 + lchunk * 8);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? ax : az),
+                                       (lds_ptr)(base + TB * (1 + j) + wave * 1024), 16, 0, 0);
+    }
+  };
+
+  const int cf0 = 2 * (wave >> 1), kf0 = 2 * (wave & 1);
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  f32x4 acc[NT][2][2];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[j][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)lds));
+  const uint32_t offA = (8 * grp + q) * 128 + (16 * cf0 + 4 * p) * 2;
+  const uint32_t offB = TB + (8 * grp + q) * 128 + (16 * kf0 + 4 * p) * 2;
+
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < steps) issue(s0, s0);
+  for (int s = 0; s < steps; ++s) {
+    const int ahead = (steps - 1 - s) < (NS - 2) ? (steps - 1 - s) : (NS - 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + NT)) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + NT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const uint32_t sb = lds0 + (s % NS) * SB;
+    s16x4 r[16];
+    asm volatile(
+        "ds_read_b64_tr_b16 %0, %16\n\t"
+        "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
+        "ds_read_b64_tr_b16 %2, %16 offset:32\n\t"
+        "ds_read_b64_tr_b16 %3, %16 offset:544\n\t"
+        "ds_read_b64_tr_b16 %4, %17\n\t"
+        "ds_read_b64_tr_b16 %5, %17 offset:512\n\t"
+        "ds_read_b64_tr_b16 %6, %17 offset:32\n\t"
+        "ds_read_b64_tr_b16 %7, %17 offset:544\n\t"
+        "ds_read_b64_tr_b16 %8, %18\n\t"
+        "ds_read_b64_tr_b16 %9, %18 offset:512\n\t"
+        "ds_read_b64_tr_b16 %10, %18 offset:32\n\t"
+        "ds_read_b64_tr_b16 %11, %18 offset:544\n\t"
+        "ds_read_b64_tr_b16 %12, %19\n\t"
+        "ds_read_b64_tr_b16 %13, %19 offset:512\n\t"
+        "ds_read_b64_tr_b16 %14, %19 offset:32\n\t"
+        "ds_read_b64_tr_b16 %15, %19 offset:544\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
+          "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]),
+          "=&v"(r[15])
+        : "v"(sb + offA), "v"(sb + offB), "v"(sb + offB + TB), "v"(sb + offB + 2 * TB)
+        : "memory");
+    if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
+    bf16x8 a[2], b[NT][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const short va[8] = {r[2 * u][0], r[2 * u][1], r[2 * u][2], r[2 * u][3],
+                           r[2 * u + 1][0], r[2 * u + 1][1], r[2 * u + 1][2], r[2 * u + 1][3]};
+      a[u] = __builtin_bit_cast(bf16x8, va);   // dy tile: A[co][m]
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int o = 4 + 4 * j + 2 * u;
+        const short vb[8] = {r[o][0], r[o][1], r[o][2], r[o][3], r[o + 1][0], r[o + 1][1], r[o + 1][2], r[o + 1][3]};
+        b[j][u] = __builtin_bit_cast(bf16x8, vb);   // x tile of tap j: B[m][k]
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          acc[j][u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[j][v], acc[j][u][v], 0, 0, 0);
+  }
+
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int k0 = (ti * g.KW + j) * g.C + c0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = co0 + (cf0 + u) * 16 + 4 * grp + e;
+          const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
+                            static_cast<int64_t>(co) * K + k0 + (kf0 + v) * 16 + li;
+          if constexpr (OUT_BF16) static_cast<uint16_t*>(out)[o] = f_to_bf16(acc[j][u][v][e]);
+          else static_cast<float*>(out)[o] = acc[j][u][v][e];
+        }
+  }
+}
+
 template <int PM>
 void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
             hipStream_t stream) {
@@ -527,11 +674,29 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   else launch<1>(x, w, g, Cout, y, add, stream);
 }
 
+int iwgrad_taps_per_block(int kw) {
+  static const bool row = [] {   // tuning knob: GARFIELD_IWGRAD_ROW=0 keeps one tap per workgroup
+    const char* e = std::getenv("GARFIELD_IWGRAD_ROW");
+    return !(e && e[0] == '0');
+  }();
+  return (row && kw == 3) ? 3 : 1;
+}
+
 void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
                  int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream) {
   const int K = g.KH * g.KW * g.C;
   if (splits < 1) splits = 1;
   const int64_t per_split = (rg + splits - 1) / splits;
+  if (iwgrad_taps_per_block(g.KW) == 3) {
+    const dim3 grid(g.KH * (g.C / 64) * (Cout / 64), groups, splits);
+    if (out_bf16)
+      hipLaunchKernelGGL((k_iwgrad_row<3, true>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                         split_stride, group_stride);
+    else
+      hipLaunchKernelGGL((k_iwgrad_row<3, false>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                         split_stride, group_stride);
+    return;
+  }
   const dim3 grid((K / 64) * (Cout / 64), groups, splits);
   if (out_bf16)
     hipLaunchKernelGGL((k_iwgrad<3, true>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
