@@ -650,9 +650,14 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   const int M = g.N * g.Ho * g.Wo;
   if (M <= 0) return;
   if (pm <= 0) {  // measured (scripts/bench_iconv.py): the largest pixel tile that keeps ~500 workgroups
+    static const int64_t min_wg = [] {   // tuning knob: GARFIELD_ICONV_PM_WG
+      const char* e = std::getenv("GARFIELD_ICONV_PM_WG");
+      const long v = e ? std::atol(e) : 0;
+      return static_cast<int64_t>(v > 0 ? v : 500);
+    }();
     const int64_t ncb = Cout / 64;
     pm = 4;
-    while (pm > 1 && ((M + 64 * pm - 1) / (64 * pm)) * ncb < 500) pm /= 2;
+    while (pm > 1 && ((M + 64 * pm - 1) / (64 * pm)) * ncb < min_wg) pm /= 2;
     if (g.C % 64 == 0) pm += 10;   // the LDS-staged kernel whenever its k-step fits
   }
   // pm 11 / 12 / 14: the LDS-staged kernel with 1 / 2 / 4 pixel fragments per wave (C % 64 == 0)
