@@ -666,12 +666,12 @@ void g_large_coord(const at::Tensor& x, int64_t mode, int64_t f, int64_t beta, c
 // Split-K slabs -> strided per-group output: part fp32 [S, G, ...] and out [G, ...] (fp32 / bf16 /
 // fp16) may have any slab / group strides and one row pitch each (the last dim contiguous, the
 // dims between it and the group dim dense), e.g. a padded GEMM result cropped into exchange rows.
-void g_split_reduce(const at::Tensor& part, const at::Tensor& out) {
+garfield::gpu::SplitJob split_job(const at::Tensor& part, const at::Tensor& out) {
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() >= 3,
               "gpu_split_reduce: part must be an fp32 [S, G, ...] GPU tensor");
   TORCH_CHECK(out.device() == part.device() && out.dim() == part.dim() - 1 && out.size(0) == part.size(1),
               "gpu_split_reduce: out must be [G, ...] on part's device");
-  const int64_t S = part.size(0), G = part.size(1), D = part.dim();
+  const int64_t D = part.dim();
   for (int64_t k = 2; k < D; ++k)
     TORCH_CHECK(part.size(k) == out.size(k - 1), "gpu_split_reduce: part and out shapes differ");
   const int64_t Cc = part.size(D - 1);
@@ -692,10 +692,44 @@ void g_split_reduce(const at::Tensor& part, const at::Tensor& out) {
   }
   const int odt = dtype_code(out);
   TORCH_CHECK(odt != garfield::kF64, "gpu_split_reduce: out must be fp32, bf16 or fp16");
+  garfield::gpu::SplitJob j{};
+  j.part = part.data_ptr<float>();
+  j.out = out.data_ptr();
+  j.R = R;
+  j.Cc = Cc;
+  j.ipitch = ipitch;
+  j.opitch = opitch;
+  j.ss = part.stride(0);
+  j.gs = part.stride(1);
+  j.ostride = out.stride(0);
+  j.S = static_cast<int>(part.size(0));
+  j.G = static_cast<int>(part.size(1));
+  j.odt = odt;
+  return j;
+}
+
+// Split-K slabs -> strided per-group output: part fp32 [S, G, ...] and out [G, ...] (fp32 / bf16 /
+// fp16) may have any slab / group strides and one row pitch each (the last dim contiguous, the
+// dims between it and the group dim dense), e.g. a padded GEMM result cropped into exchange rows.
+void g_split_reduce(const at::Tensor& part, const at::Tensor& out) {
+  const auto j = split_job(part, out);
   c10::hip::HIPGuard guard(part.device().index());
-  garfield::gpu::split_reduce(part.data_ptr<float>(), static_cast<int>(S), static_cast<int>(G), R, Cc, ipitch, opitch,
-                              part.stride(0), part.stride(1), out.data_ptr(), odt, out.stride(0),
+  garfield::gpu::split_reduce(j.part, j.S, j.G, j.R, j.Cc, j.ipitch, j.opitch, j.ss, j.gs, j.out, j.odt, j.ostride,
                               stream_of(part.device()));
+}
+
+// Many of them in one launch (the grouped backward's per-layer split-K sums).
+void g_split_reduce_multi(const std::vector<at::Tensor>& parts, const std::vector<at::Tensor>& outs) {
+  TORCH_CHECK(parts.size() == outs.size(), "gpu_split_reduce_multi: one out per part");
+  if (parts.empty()) return;
+  std::vector<garfield::gpu::SplitJob> jobs;
+  jobs.reserve(parts.size());
+  for (size_t i = 0; i < parts.size(); ++i) {
+    TORCH_CHECK(parts[i].device() == parts[0].device(), "gpu_split_reduce_multi: one device");
+    jobs.push_back(split_job(parts[i], outs[i]));
+  }
+  c10::hip::HIPGuard guard(parts[0].device().index());
+  garfield::gpu::split_reduce_multi(jobs.data(), static_cast<int>(jobs.size()), stream_of(parts[0].device()));
 }
 
 // Fresh grouped batch: out [R, C, H, W] bf16 channels_last from uint8 NHWC images src[idx[r]].
@@ -1050,6 +1084,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "args (x, mode 0 median | 1 trimmed-mean | 2 averaged-median, f, beta, out)");
   m.def("iwgrad_taps_per_block", [](int64_t kw) { return garfield::gpu::iwgrad_taps_per_block(static_cast<int>(kw)); },
         "Taps per workgroup gpu_iwgrad uses for kernel width kw (3: a kernel row shares each dy tile)");
+  m.def("gpu_split_reduce_multi", &g_split_reduce_multi,
+        "gpu_split_reduce for many (part, out) pairs in one launch; args (parts, outs)");
   m.def("gpu_split_reduce", &g_split_reduce,
         "out[g] = Σ_s part[s, g] (fp32 accumulation, one launch; out may be strided exchange rows); args (part, out)");
   m.def("gpu_augment_gather", &g_augment_gather,

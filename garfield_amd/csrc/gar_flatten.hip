@@ -159,3 +159,73 @@ void split_reduce(const float* part, int S, int G, int64_t R, int64_t Cc, int64_
 
 }  // namespace gpu
 }  // namespace garfield
+
+// ---------------------------------------------------------------------------
+// Many split-K reductions in ONE launch (the grouped backward queues one per layer and
+// runs them all after the last layer): block b finds its job through the prefix sum of
+// blocks per job, then does what k_split_reduce does for 256 x V elements of it.
+namespace garfield {
+namespace gpu {
+namespace {
+
+struct SplitTable {
+  SplitJob job[kMaxSplitJobs];
+  int32_t blk0[kMaxSplitJobs + 1];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void k_split_reduce_multi(SplitTable t) {
+  int j = 0;
+  while (j + 1 < t.count && static_cast<int>(blockIdx.x) >= t.blk0[j + 1]) ++j;
+  const SplitJob& J = t.job[j];
+  const int V = J.vec ? 4 : 1;
+  const int64_t cv = (J.Cc + V - 1) / V;
+  const int64_t per = J.R * cv;
+  const int64_t tid = static_cast<int64_t>(blockIdx.x - t.blk0[j]) * blockDim.x + threadIdx.x;
+  if (tid >= per * J.G) return;
+  const int g = static_cast<int>(tid / per);
+  const int64_t rem = tid - static_cast<int64_t>(g) * per;
+  const int64_t r = rem / cv;
+  const int64_t c = (rem - r * cv) * V;
+  const float* p = J.part + static_cast<int64_t>(g) * J.gs + r * J.ipitch + c;
+  const int64_t o = static_cast<int64_t>(g) * J.ostride + r * J.opitch + c;
+  if (J.vec) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < J.S; ++s) {
+      const float4 a = *reinterpret_cast<const float4*>(p + static_cast<int64_t>(s) * J.ss);
+      acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+    dev::store_one(J.out, J.odt, o, acc.x);
+    dev::store_one(J.out, J.odt, o + 1, acc.y);
+    dev::store_one(J.out, J.odt, o + 2, acc.z);
+    dev::store_one(J.out, J.odt, o + 3, acc.w);
+  } else {
+    float acc = 0.f;
+    for (int s = 0; s < J.S; ++s) acc += p[static_cast<int64_t>(s) * J.ss];
+    dev::store_one(J.out, J.odt, o, acc);
+  }
+}
+
+}  // namespace
+
+void split_reduce_multi(const SplitJob* jobs, int count, hipStream_t stream) {
+  for (int base = 0; base < count; base += kMaxSplitJobs) {
+    SplitTable t{};
+    t.count = count - base < kMaxSplitJobs ? count - base : kMaxSplitJobs;
+    int32_t blocks = 0;
+    for (int i = 0; i < t.count; ++i) {
+      SplitJob J = jobs[base + i];
+      J.vec = (J.Cc % 4 == 0 && J.ipitch % 4 == 0 && J.ss % 4 == 0 && J.gs % 4 == 0 &&
+               reinterpret_cast<uintptr_t>(J.part) % 16 == 0) ? 1 : 0;
+      t.job[i] = J;
+      t.blk0[i] = blocks;
+      const int64_t work = (J.vec ? J.Cc / 4 : J.Cc) * J.R * J.G;
+      blocks += static_cast<int32_t>((work + 255) / 256);
+    }
+    t.blk0[t.count] = blocks;
+    if (blocks > 0) hipLaunchKernelGGL(k_split_reduce_multi, dim3(blocks), dim3(256), 0, stream, t);
+  }
+}
+
+}  // namespace gpu
+}  // namespace garfield

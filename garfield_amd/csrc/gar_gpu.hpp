@@ -77,6 +77,16 @@ void aksel_select(const float* slabs, int grid, int n, int c, float* weights, fl
 void split_reduce(const float* part, int S, int G, int64_t R, int64_t Cc, int64_t ipitch, int64_t opitch, int64_t ss,
                   int64_t gs, void* out, int odt, int64_t ostride, hipStream_t stream);
 
+// The same for many (part, out) pairs in one launch (up to kMaxSplitJobs per launch).
+struct SplitJob {
+  const float* part;
+  void* out;
+  int64_t R, Cc, ipitch, opitch, ss, gs, ostride;
+  int S, G, odt, vec;
+};
+constexpr int kMaxSplitJobs = 32;   // kernarg budget: 32 x 80 B
+void split_reduce_multi(const SplitJob* jobs, int count, hipStream_t stream);
+
 // ---- Multi-tensor flatten + cast (per-parameter grads -> exchange row) -----
 constexpr int kMaxFlatTensors = 96;  // tensors per launch (kernarg budget); more => several launches
 int flatten_cast(const void* const* srcs, const int* src_dts, const int64_t* numels, const int64_t* offsets,

@@ -73,6 +73,8 @@ XENT = os.environ.get("GARFIELD_XENT", "1") != "0"   # fused per-worker cross-en
 # 1.1-1.4x faster alone for N <= 128, slower above; but in the graphed step N <= 128 measured
 # 6.99 vs 6.96 ms/step (profiles/r2/ab_gemm_nt.log), so it is off by default (0).
 GEMM_NT_MAXN = int(os.environ.get("GARFIELD_GEMM_NT_MAXN", "0"))
+# split-K weight-gradient sums of every layer deferred to one launch after the backward
+SPLIT_DEFER = os.environ.get("GARFIELD_SPLIT_DEFER", "1") != "0"
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -114,6 +116,10 @@ class GradSink:
         self.groups = int(groups)
         self._srcs: list = []
         self._offs: list = []
+        self._split_parts: list = []   # deferred split-K sums (part [S, G, ...] fp32, out [G, ...] rows)
+        self._split_outs: list = []
+        # off when a consumer reads rows DURING the backward (in-graph bucket signals)
+        self.defer_splits = True
 
     def offset(self, p: torch.Tensor) -> int:
         return self.offsets[id(p)]
@@ -143,12 +149,25 @@ class GradSink:
         return self.flat.as_strided((self.groups, *shape), (self.row_stride, *reversed(strides)),
                                     self.base + self.offsets[id(p)])
 
+    def queue_split(self, part: torch.Tensor, out: torch.Tensor) -> None:
+        """Σ_s part[s] -> out, deferred to ``flush`` where every queued layer's split-K sum runs
+        in ONE launch (the exchange rows are read only after the backward)."""
+        if SPLIT_DEFER and self.defer_splits and part.is_cuda:
+            self._split_parts.append(part)
+            self._split_outs.append(out)
+        else:
+            _native.native().gpu_split_reduce(part, out)
+
     def put_groups(self, p: torch.Tensor, grads) -> None:
         """``grads``: [groups, ...] tensor or a list of per-group tensors."""
         for g in range(self.groups):
             self.put(p, g, grads[g])
 
     def flush(self) -> None:
+        if self._split_parts:
+            _native.native().gpu_split_reduce_multi(self._split_parts, self._split_outs)
+            self._split_parts.clear()
+            self._split_outs.clear()
         if not self._srcs:
             return
         if self.flat.is_cuda:
@@ -542,8 +561,8 @@ def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int)
     part = torch.empty((S, G, cout, K), dtype=torch.float32, device=dy.device)
     C_.gpu_iwgrad(x, dy, *_geom(spec), G, part, S)
     rows = spec.sink.rows_view(spec.conv.weight, (cout, K), spec.sink.flat.dtype)
-    if rows is not None:     # the S slabs summed straight into the exchange rows (one launch)
-        C_.gpu_split_reduce(part, rows)
+    if rows is not None:     # the S slabs summed straight into the exchange rows (deferred, batched)
+        spec.sink.queue_split(part, rows)
     else:
         spec.sink.put_groups(spec.conv.weight, part.sum(0) if S > 1 else part[0])
 
@@ -570,7 +589,8 @@ def _match_layout(g: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
     return g.contiguous()
 
 
-def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int, out: torch.Tensor | None = None) -> torch.Tensor:
+def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int, out: torch.Tensor | None = None,
+           sink: "GradSink | None" = None) -> torch.Tensor:
     """Per-worker weight gradients ``dW_g = dy_gᵀ · a_g`` for all G workers: [G, Cout, K].
 
     One strided-batched GEMM; when each worker has many rows (the CIFAR stem and
@@ -597,7 +617,11 @@ def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int, out: torch.Tensor | None
         # exchange rows by one launch
         part = torch.bmm(dy2.view(G * S, M // S, cout).transpose(1, 2), a2.view(G * S, M // S, K),
                          out_dtype=torch.float32)
-        _native.native().gpu_split_reduce(part.view(G, S, cout, K).transpose(0, 1)[..., :Ko], out)
+        red = part.view(G, S, cout, K).transpose(0, 1)[..., :Ko]
+        if sink is not None:
+            sink.queue_split(red, out)
+        else:
+            _native.native().gpu_split_reduce(red, out)
         return out
     part = torch.bmm(dy2.view(G * S, M // S, cout).transpose(1, 2), a2.view(G * S, M // S, K))
     if out is not None:
@@ -718,7 +742,7 @@ class _GroupedConv(torch.autograd.Function):
                         _iwgrad(a, dy, spec, G, K)
                     else:
                         out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype)
-                        dW = _wgrad(dy2, rows2d(a), G, out)
+                        dW = _wgrad(dy2, rows2d(a), G, out, spec.sink)
                         if out is None:
                             spec.sink.put_groups(spec.conv.weight, dW)
         elif mode == "iconv":                    # a = x
@@ -749,7 +773,7 @@ class _GroupedConv(torch.autograd.Function):
                 with _wgrad_ctx(col, dy):
                     out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if (kp == K or dy2.is_cuda) \
                         else None
-                    dW = _wgrad(dy2, col, G, out)
+                    dW = _wgrad(dy2, col, G, out, spec.sink)
                     if out is None:
                         if kp != K:
                             dW = dW[:, :, :K].contiguous()
@@ -772,7 +796,7 @@ class _GroupedConv(torch.autograd.Function):
                 with _wgrad_ctx(a, dy):
                     out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if (kp == K or dy2.is_cuda) \
                         else None
-                    dW = _wgrad(dy2, a, G, out)
+                    dW = _wgrad(dy2, a, G, out, spec.sink)
                     if out is None:
                         if kp != K:
                             dW = dW[:, :, :K].contiguous()

@@ -76,6 +76,8 @@ class GroupedResNet:
             sig = {name: GraphSignal(dev) for name in self.marks}
             if all(x.available() for x in sig.values()):
                 self._events = sig
+        # a bucket's rows must be complete when its signal fires: no deferred split-K sums then
+        sink.defer_splits = self._events is None
 
     def bucket_offsets(self) -> list:
         """Flat offset where each marked layer's parameters start (bucket boundaries)."""

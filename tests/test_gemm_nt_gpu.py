@@ -110,3 +110,23 @@ def test_split_reduce_crops_padded_columns(cuda, native):
     native.gpu_split_reduce(part[..., :k], out)
     assert rel(out, part[..., :k].double().sum(0)) < 5e-3
     assert int((flat.view(G, -1)[:, co * k:] != 0).sum()) == 0          # nothing written past the rows
+
+
+def test_split_reduce_multi_matches_single(cuda, native):
+    """Many split-K sums in one launch (40 jobs: two launches of <= 32), mixed shapes, crops,
+    strides and output dtypes, equal to the one-job kernel."""
+    torch.manual_seed(7)
+    parts, outs, refs = [], [], []
+    for i in range(40):
+        S, G = 1 + i % 5, 1 + i % 8
+        co, k = 8 * (1 + i % 3), 3 + 5 * (i % 4)
+        kp = k + (i % 2) * 5                    # odd jobs: padded columns cropped away
+        p = torch.randn((G, S, co, kp), device=cuda).transpose(0, 1)[..., :k]
+        dt = torch.bfloat16 if i % 3 else torch.float32
+        flat = torch.zeros(G * (co * k + 16), device=cuda, dtype=dt)
+        parts.append(p)
+        outs.append(flat.as_strided((G, co, k), (co * k + 16, k, 1), 0))
+        refs.append(p.double().sum(0))
+    native.gpu_split_reduce_multi(parts, outs)
+    for o, r in zip(outs, refs):
+        assert rel(o, r) < (1e-6 if o.dtype == torch.float32 else 5e-3)
