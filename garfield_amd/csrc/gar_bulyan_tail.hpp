@@ -18,6 +18,7 @@
 // start a is found from the e = t - beta smallest and largest values (no second
 // sort by distance, unlike the generic closest_mean).
 #pragma once
+#include <cstdlib>
 #include "gar_device.hpp"
 
 namespace garfield {
@@ -188,12 +189,23 @@ __global__ __launch_bounds__(256) void k_bulyan_tail(RowTable rows, int n, int64
   }
 }
 
+// grid cap of the tail kernels (grid-stride over coordinate groups); GARFIELD_TAIL_GRID overrides
+inline int64_t tail_grid_cap(int64_t dflt) {
+  static const int64_t env = [] {
+    const char* e = std::getenv("GARFIELD_TAIL_GRID");
+    const long v = e ? std::atol(e) : 0;
+    return static_cast<int64_t>(v > 0 ? v : 0);
+  }();
+  return env > 0 ? env : dflt;
+}
+
 // W == nullptr: averaged median of the n rows themselves (t = n)
 template <int DT, int NP>
 void launch_bulyan_tail(const RowTable& rows, int n, int64_t d, int beta, const float* W, int t, void* out,
                         int out_dt, hipStream_t s) {
   int64_t g = d / kTailTile + 1;
-  if (g > 2048) g = 2048;
+  const int64_t cap = tail_grid_cap(4096);
+  if (g > cap) g = cap;
   if (W == nullptr)
     hipLaunchKernelGGL((k_bulyan_tail<DT, NP, true>), dim3(static_cast<unsigned>(g)), dim3(256), 0, s, rows, n, d,
                        beta, W, n, out, out_dt);
@@ -530,7 +542,8 @@ template <int DT, int NP>
 void launch_tail_mfma_ks(int ks, const RowTable& rows, int n, int64_t groups, int last_width, int beta,
                          const float* W, int t, void* out, int out_dt, hipStream_t s) {
   int64_t g = (groups + 3) / 4;
-  if (g > 2048) g = 2048;
+  const int64_t cap = tail_grid_cap(4096);
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   const dim3 grid(static_cast<unsigned>(g)), block(256);
 #define GARFIELD_TAIL_MFMA(KS)                                                                                   \

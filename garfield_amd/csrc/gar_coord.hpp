@@ -196,13 +196,18 @@ inline bool coord_mfma_tail_enabled() {  // GARFIELD_MFMA_TAIL=0: Bulyan tail wi
   }();
   return on;
 }
-inline int64_t coord16_grid_cap() {
-  static const int64_t cap = [] {
+// Grid cap of the packed 16-bit coordinate kernels (grid-stride loop). Measured at d = 23.5M
+// bf16 (profiles/r2/coord16_grid_sweep.log): small sets (NP <= 16, 8 coordinates per lane) are
+// fastest with one pass per lane (cap 16384: median n=8 0.080 vs 0.084 ms at 4096); large sets
+// with 4096 (n=64 0.611 vs 0.634 ms at 16384). GARFIELD_COORD16_GRID overrides both.
+inline int64_t coord16_grid_cap(int np) {
+  static const int64_t env = [] {
     const char* e = std::getenv("GARFIELD_COORD16_GRID");
     const long v = e ? std::atol(e) : 0;
-    return static_cast<int64_t>(v > 0 ? v : 4096);
+    return static_cast<int64_t>(v > 0 ? v : 0);
   }();
-  return cap;
+  if (env > 0) return env;
+  return np <= 16 ? 16384 : 4096;
 }
 
 }  // namespace coord

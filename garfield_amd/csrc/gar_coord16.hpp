@@ -299,7 +299,7 @@ void launch_coord16(const RowTable& rows, int n, int64_t d, int f, int beta, uin
                     int out_dt, hipStream_t s) {
   constexpr int P = Coord16Words<NP>::P;
   int64_t g = (d / (2 * P) + 255) / 256;
-  const int64_t cap = coord16_grid_cap();
+  const int64_t cap = coord16_grid_cap(NP);
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   hipLaunchKernelGGL((k_coord16<DT, NP, P, MODE>), dim3(static_cast<unsigned>(g)), dim3(256), 0, s, rows, n, d, f,
