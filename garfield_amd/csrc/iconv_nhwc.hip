@@ -490,25 +490,27 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
 }
 
 
-// Weight gradient of all THREE taps of one kernel row per workgroup (KW == 3): the k-step's
-// 32-pixel dy tile is staged once and feeds the three taps' MFMAs (the per-tap kernel above
-// re-reads it for every tap: 9x dy traffic on a 3x3 layer, 3x here). Stage = dy tile + the
-// three shifted x tiles (16 KiB); wave tile = 2 output-channel fragments x 2 k-fragments per tap.
-template <int NS, bool OUT_BF16>
-__global__ __launch_bounds__(256) void k_iwgrad_row(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                                                    Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
-                                                    int64_t split_stride, int64_t group_stride) {
-  constexpr int TB = 32 * 128;  // one 32-pixel x 64-channel tile
-  constexpr int NT = 3;         // taps per kernel row
-  constexpr int SB = (1 + NT) * TB;
+// Weight gradient of all THREE taps of NR kernel rows per workgroup (KW == 3, NR = 1 or
+// KH): the k-step's 32-pixel dy tile is staged once and feeds 3*NR taps' MFMAs (the per-tap
+// kernel above re-reads it for every tap: 9x dy traffic on a 3x3 layer; 3x at NR = 1, 1x at
+// NR = 3). Stage = dy tile + 3*NR shifted x tiles; wave tile = 2 output-channel fragments x 2
+// k-fragments per tap.
+template <int NS, bool OUT_BF16, int NR>
+__global__ __launch_bounds__(256) void k_iwgrad_rows(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                     Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
+                                                     int64_t split_stride, int64_t group_stride) {
+  constexpr int TB = 32 * 128;   // one 32-pixel x 64-channel tile
+  constexpr int NT = 3;          // taps per kernel row
+  constexpr int NX = NR * NT;    // x tiles per stage
+  constexpr int SB = (1 + NX) * TB;
   __shared__ __attribute__((aligned(16))) char lds[NS * SB];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int K = g.KH * g.KW * g.C;
   const int ncb = g.C / 64;
-  const int nq = g.KH * ncb;
+  const int nq = (g.KH / NR) * ncb;
   const int qb = blockIdx.x % nq, cb = blockIdx.x / nq;
-  const int ti = qb / ncb, c0 = (qb - ti * ncb) * 64;
+  const int ti0 = (qb / ncb) * NR, c0 = (qb - (qb / ncb) * ncb) * 64;
   const int co0 = cb * 64;
   const int gi = blockIdx.y, sp = blockIdx.z;
   const int64_t mbeg = static_cast<int64_t>(gi) * rg + static_cast<int64_t>(sp) * per_split;
@@ -532,24 +534,27 @@ __global__ __launch_bounds__(256) void k_iwgrad_row(const uint16_t* __restrict__
     const int t = mm / g.Wo;
     const int ho = t % g.Ho;
     const int n = t / g.Ho;
-    const int hi = ho * g.sh - g.ph + ti * g.dh;
-    const bool rok = mv && hi >= 0 && hi < g.H;
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int wi = wo * g.sw - g.pw + j * g.dw;
-      const bool ok = rok && wi >= 0 && wi < g.W;
-      const uint64_t ax = reinterpret_cast<uint64_t>(
-          x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 + lchunk * 8);
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? ax : az),
-                                       (lds_ptr)(base + TB * (1 + j) + wave * 1024), 16, 0, 0);
+    for (int r = 0; r < NR; ++r) {
+      const int hi = ho * g.sh - g.ph + (ti0 + r) * g.dh;
+      const bool rok = mv && hi >= 0 && hi < g.H;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int wi = wo * g.sw - g.pw + j * g.dw;
+        const bool ok = rok && wi >= 0 && wi < g.W;
+        const uint64_t ax = reinterpret_cast<uint64_t>(
+            x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 + lchunk * 8);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? ax : az),
+                                         (lds_ptr)(base + TB * (1 + r * NT + j) + wave * 1024), 16, 0, 0);
+      }
     }
   };
 
   const int cf0 = 2 * (wave >> 1), kf0 = 2 * (wave & 1);
   const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  f32x4 acc[NT][2][2];
+  f32x4 acc[NX][2][2];
 #pragma unroll
-  for (int j = 0; j < NT; ++j)
+  for (int j = 0; j < NX; ++j)
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -564,12 +569,13 @@ __global__ __launch_bounds__(256) void k_iwgrad_row(const uint16_t* __restrict__
     if (s0 < steps) issue(s0, s0);
   for (int s = 0; s < steps; ++s) {
     const int ahead = (steps - 1 - s) < (NS - 2) ? (steps - 1 - s) : (NS - 2);
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + NT)) : "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + NT) : "memory");
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + NX)) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + NX) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const uint32_t sb = lds0 + (s % NS) * SB;
-    s16x4 r[16];
+    s16x4 ra[4], rb[NR][12];
+    // A (dy) fragments + the first row's three B (x) fragments, then the other rows' B fragments
     asm volatile(
         "ds_read_b64_tr_b16 %0, %16\n\t"
         "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
@@ -588,50 +594,75 @@ __global__ __launch_bounds__(256) void k_iwgrad_row(const uint16_t* __restrict__
         "ds_read_b64_tr_b16 %14, %19 offset:32\n\t"
         "ds_read_b64_tr_b16 %15, %19 offset:544\n\t"
         "s_waitcnt lgkmcnt(0)"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
-          "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]),
-          "=&v"(r[15])
+        : "=&v"(ra[0]), "=&v"(ra[1]), "=&v"(ra[2]), "=&v"(ra[3]), "=&v"(rb[0][0]), "=&v"(rb[0][1]), "=&v"(rb[0][2]),
+          "=&v"(rb[0][3]), "=&v"(rb[0][4]), "=&v"(rb[0][5]), "=&v"(rb[0][6]), "=&v"(rb[0][7]), "=&v"(rb[0][8]),
+          "=&v"(rb[0][9]), "=&v"(rb[0][10]), "=&v"(rb[0][11])
         : "v"(sb + offA), "v"(sb + offB), "v"(sb + offB + TB), "v"(sb + offB + 2 * TB)
         : "memory");
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+      const uint32_t ob = sb + offB + static_cast<uint32_t>(r * NT) * TB;
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %12\n\t"
+          "ds_read_b64_tr_b16 %1, %12 offset:512\n\t"
+          "ds_read_b64_tr_b16 %2, %12 offset:32\n\t"
+          "ds_read_b64_tr_b16 %3, %12 offset:544\n\t"
+          "ds_read_b64_tr_b16 %4, %13\n\t"
+          "ds_read_b64_tr_b16 %5, %13 offset:512\n\t"
+          "ds_read_b64_tr_b16 %6, %13 offset:32\n\t"
+          "ds_read_b64_tr_b16 %7, %13 offset:544\n\t"
+          "ds_read_b64_tr_b16 %8, %14\n\t"
+          "ds_read_b64_tr_b16 %9, %14 offset:512\n\t"
+          "ds_read_b64_tr_b16 %10, %14 offset:32\n\t"
+          "ds_read_b64_tr_b16 %11, %14 offset:544\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(rb[r][0]), "=&v"(rb[r][1]), "=&v"(rb[r][2]), "=&v"(rb[r][3]), "=&v"(rb[r][4]), "=&v"(rb[r][5]),
+            "=&v"(rb[r][6]), "=&v"(rb[r][7]), "=&v"(rb[r][8]), "=&v"(rb[r][9]), "=&v"(rb[r][10]), "=&v"(rb[r][11])
+          : "v"(ob), "v"(ob + TB), "v"(ob + 2 * TB)
+          : "memory");
+    }
     if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
-    bf16x8 a[2], b[NT][2];
+    bf16x8 a[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const short va[8] = {r[2 * u][0], r[2 * u][1], r[2 * u][2], r[2 * u][3],
-                           r[2 * u + 1][0], r[2 * u + 1][1], r[2 * u + 1][2], r[2 * u + 1][3]};
+      const short va[8] = {ra[2 * u][0], ra[2 * u][1], ra[2 * u][2], ra[2 * u][3],
+                           ra[2 * u + 1][0], ra[2 * u + 1][1], ra[2 * u + 1][2], ra[2 * u + 1][3]};
       a[u] = __builtin_bit_cast(bf16x8, va);   // dy tile: A[co][m]
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int o = 4 + 4 * j + 2 * u;
-        const short vb[8] = {r[o][0], r[o][1], r[o][2], r[o][3], r[o + 1][0], r[o + 1][1], r[o + 1][2], r[o + 1][3]};
-        b[j][u] = __builtin_bit_cast(bf16x8, vb);   // x tile of tap j: B[m][k]
-      }
     }
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const int o = 4 * j + 2 * v;
+          const short vb[8] = {rb[r][o][0], rb[r][o][1], rb[r][o][2], rb[r][o][3],
+                               rb[r][o + 1][0], rb[r][o + 1][1], rb[r][o + 1][2], rb[r][o + 1][3]};
+          const bf16x8 bx = __builtin_bit_cast(bf16x8, vb);   // x tile of tap (r, j): B[m][k]
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            acc[r * NT + j][u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bx, acc[r * NT + j][u][v], 0, 0, 0);
+        }
+  }
+
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int k0 = ((ti0 + r) * g.KW + j) * g.C + c0;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int v = 0; v < 2; ++v)
-          acc[j][u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[j][v], acc[j][u][v], 0, 0, 0);
-  }
-
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int k0 = (ti * g.KW + j) * g.C + c0;
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int co = co0 + (cf0 + u) * 16 + 4 * grp + e;
-          const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
-                            static_cast<int64_t>(co) * K + k0 + (kf0 + v) * 16 + li;
-          if constexpr (OUT_BF16) static_cast<uint16_t*>(out)[o] = f_to_bf16(acc[j][u][v][e]);
-          else static_cast<float*>(out)[o] = acc[j][u][v][e];
-        }
-  }
+          for (int e = 0; e < 4; ++e) {
+            const int co = co0 + (cf0 + u) * 16 + 4 * grp + e;
+            const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
+                              static_cast<int64_t>(co) * K + k0 + (kf0 + v) * 16 + li;
+            if constexpr (OUT_BF16) static_cast<uint16_t*>(out)[o] = f_to_bf16(acc[r * NT + j][u][v][e]);
+            else static_cast<float*>(out)[o] = acc[r * NT + j][u][v][e];
+          }
+    }
 }
 
 template <int PM>
@@ -679,12 +710,20 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   else launch<1>(x, w, g, Cout, y, add, stream);
 }
 
-int iwgrad_taps_per_block(int kw) {
-  static const bool row = [] {   // tuning knob: GARFIELD_IWGRAD_ROW=0 keeps one tap per workgroup
+// GARFIELD_IWGRAD_ROW: 0 one tap per workgroup, 1 the three taps of a kernel row (default),
+// 3 all nine taps of a 3x3 kernel
+static int iwgrad_row_mode() {
+  static const int m = [] {
     const char* e = std::getenv("GARFIELD_IWGRAD_ROW");
-    return !(e && e[0] == '0');
+    return e ? std::atoi(e) : 1;
   }();
-  return (row && kw == 3) ? 3 : 1;
+  return m;
+}
+
+int iwgrad_taps_per_block(int kw) {
+  const int m = iwgrad_row_mode();
+  if (kw != 3 || m == 0) return 1;
+  return m == 3 ? 9 : 3;
 }
 
 void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
@@ -692,14 +731,20 @@ void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cou
   const int K = g.KH * g.KW * g.C;
   if (splits < 1) splits = 1;
   const int64_t per_split = (rg + splits - 1) / splits;
-  if (iwgrad_taps_per_block(g.KW) == 3) {
-    const dim3 grid(g.KH * (g.C / 64) * (Cout / 64), groups, splits);
-    if (out_bf16)
-      hipLaunchKernelGGL((k_iwgrad_row<3, true>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
-                         split_stride, group_stride);
-    else
-      hipLaunchKernelGGL((k_iwgrad_row<3, false>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
-                         split_stride, group_stride);
+  const int tpb = iwgrad_taps_per_block(g.KW);
+  if (tpb > 1 && (tpb == 3 || g.KH == 3)) {
+    const int nr = tpb == 9 ? 3 : 1;
+    const dim3 grid((g.KH / nr) * (g.C / 64) * (Cout / 64), groups, splits);
+#define GARFIELD_IWG_ROWS(NSV, NRV)                                                                                 \
+  if (out_bf16)                                                                                                     \
+    hipLaunchKernelGGL((k_iwgrad_rows<NSV, true, NRV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,  \
+                       out, split_stride, group_stride);                                                           \
+  else                                                                                                              \
+    hipLaunchKernelGGL((k_iwgrad_rows<NSV, false, NRV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, \
+                       out, split_stride, group_stride)
+    if (nr == 3) { GARFIELD_IWG_ROWS(2, 3); }
+    else { GARFIELD_IWG_ROWS(3, 1); }
+#undef GARFIELD_IWG_ROWS
     return;
   }
   const dim3 grid((K / 64) * (Cout / 64), groups, splits);
