@@ -269,6 +269,30 @@ def test_grouped_gradients_as_accurate_as_per_worker(cuda, name):
         assert grouped[j] < 1.25 * per_worker[j] + 0.02, (j, grouped, per_worker)
 
 
+def _grouped_rows(cuda, name, k, B):
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model(name, 10), F.cross_entropy, DistContext(device=cuda),
+                             EngineConfig(gar="average", f=0, workers_per_rank=k, exchange_dtype=torch.float32,
+                                          lr=0.0, momentum=0.0, weight_decay=0.0, cuda_graph=False,
+                                          worker_batching=True))
+    eng.step(synthetic_batches(k, B, (3, 32, 32), 10, cuda))
+    torch.cuda.synchronize()
+    return eng.X[:, 0].clone()
+
+
+def test_implicit_1x1_weight_gradients_match_gemm_path(cuda, monkeypatch):
+    """GARFIELD_IWGRAD_1X1: the 1x1 convolutions' per-worker weight gradients from the implicit
+    MFMA kernel equal the strided-batched GEMM ones (same forward, fp32 accumulation in both)."""
+    import garfield_amd.ops.grouped as grouped
+
+    monkeypatch.setattr(grouped, "IWGRAD_1X1", False)
+    a = _grouped_rows(cuda, "resnet50", 4, 16)
+    monkeypatch.setattr(grouped, "IWGRAD_1X1", True)
+    b = _grouped_rows(cuda, "resnet50", 4, 16)
+    for j in range(4):
+        assert rel(b[j], a[j]) < 1e-2, (j, rel(b[j], a[j]))
+
+
 def test_grouped_engine_graph_matches_eager_and_excludes_attacker(cuda):
     outs = []
     for graph in (False, True):

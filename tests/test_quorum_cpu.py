@@ -24,7 +24,7 @@ def free_port():
     return p
 
 
-STEPS, DELAY = 6, 0.6
+STEPS, DELAY = 6, 1.0
 
 
 def _worker(rank, world, port, outdir, quorum, delay):
@@ -64,8 +64,9 @@ def test_straggler_outside_the_quorum_does_not_slow_the_others():
     assert torch.equal(out[0]["flat"], out[1]["flat"]) and torch.equal(out[0]["flat"], out[2]["flat"])
     # ranks 0 / 1 never waited for rank 2's delayed rows
     assert all(q == [0, 1] for q in out[0]["q"])
-    assert out[0]["t"] < STEPS * DELAY / 2, out[0]["t"]
-    assert out[1]["t"] < STEPS * DELAY / 2, out[1]["t"]
+    # (waiting would take >= STEPS * DELAY; the margin absorbs a loaded CI host)
+    assert out[0]["t"] < 0.6 * STEPS * DELAY, out[0]["t"]
+    assert out[1]["t"] < 0.6 * STEPS * DELAY, out[1]["t"]
     assert torch.isfinite(out[0]["flat"]).all()
 
 
