@@ -104,9 +104,10 @@ void maxpool_bwd_nhwc(const uint16_t* dy, const uint8_t* idx, const Im2col& g, u
 // Per-worker implicit weight gradient (iconv_nhwc.hip): out[s][g][co][k] (fp32 partial slab s of
 // worker g, or bf16 when out_bf16, e.g. straight into the exchange rows) = Σ over the s-th of `splits`
 // pixel ranges of worker g of dy[m, co] · patch(x)[m, k]; C % 64 == 0, Cout % 64 == 0, x / dy 16-B aligned.
-// Taps per workgroup of iwgrad_nhwc for a kernel width kw (3: the three taps of a kernel row
-// share each staged dy tile; GARFIELD_IWGRAD_ROW=0 forces 1).
-int iwgrad_taps_per_block(int kw);
+// Taps per workgroup of iwgrad_nhwc for a kh x kw kernel over C input channels (3x3: the three
+// taps of a kernel row share each staged dy tile, GARFIELD_IWGRAD_ROW; 1x1: up to four 64-channel
+// input blocks share it, GARFIELD_IWGRAD_1X1_NT).
+int iwgrad_taps_per_block(int kw, int kh = 3, int C = 0);
 void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
                  int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream);
 // accumulate: dx += col2im(dcol) instead of dx = col2im(dcol).

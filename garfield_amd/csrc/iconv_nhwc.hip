@@ -710,6 +710,150 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   else launch<1>(x, w, g, Cout, y, add, stream);
 }
 
+// Weight gradient of a 1x1 convolution with NT 64-channel input blocks per workgroup: the
+// k-step's 32-pixel dy tile is staged once for NT x tiles (the per-tap kernel re-reads it for
+// every input-channel block). NT = 2 or 4.
+template <int NS, bool OUT_BF16, int NT>
+__global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                    Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
+                                                    int64_t split_stride, int64_t group_stride) {
+  constexpr int TB = 32 * 128;
+  constexpr int SB = (1 + NT) * TB;
+  __shared__ __attribute__((aligned(16))) char lds[NS * SB];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int K = g.C;
+  const int nq = g.C / (64 * NT);
+  const int qb = blockIdx.x % nq, cb = blockIdx.x / nq;
+  const int c0 = qb * 64 * NT, co0 = cb * 64;
+  const int gi = blockIdx.y, sp = blockIdx.z;
+  const int64_t mbeg = static_cast<int64_t>(gi) * rg + static_cast<int64_t>(sp) * per_split;
+  int64_t mend = mbeg + per_split;
+  if (mend > static_cast<int64_t>(gi + 1) * rg) mend = static_cast<int64_t>(gi + 1) * rg;
+  const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
+
+  const int lrow = wave * 8 + (lane >> 3), lchunk = lane & 7;
+  const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
+  const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
+
+  auto issue = [&](int s, int slot) {
+    const int m = static_cast<int>(mbeg) + s * 32 + lrow;
+    const bool mv = m < static_cast<int>(mend);
+    const int mm = mv ? m : 0;
+    char* base = lds + slot * SB;
+    const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lchunk * 8);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? ady : az), (lds_ptr)(base + wave * 1024), 16,
+                                     0, 0);
+    const int wo = mm % g.Wo;
+    const int t = mm / g.Wo;
+    const int ho = t % g.Ho;
+    const int n = t / g.Ho;
+    const int hi = ho * g.sh - g.ph, wi = wo * g.sw - g.pw;
+    const bool ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+    const uint16_t* xr = x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 +
+                         lchunk * 8;
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? reinterpret_cast<uint64_t>(xr + j * 64) : az),
+                                       (lds_ptr)(base + TB * (1 + j) + wave * 1024), 16, 0, 0);
+  };
+
+  const int cf0 = 2 * (wave >> 1), kf0 = 2 * (wave & 1);
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  f32x4 acc[NT][2][2];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[j][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)lds));
+  const uint32_t offA = (8 * grp + q) * 128 + (16 * cf0 + 4 * p) * 2;
+  const uint32_t offB = TB + (8 * grp + q) * 128 + (16 * kf0 + 4 * p) * 2;
+
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < steps) issue(s0, s0);
+  for (int s = 0; s < steps; ++s) {
+    const int ahead = (steps - 1 - s) < (NS - 2) ? (steps - 1 - s) : (NS - 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + NT)) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + NT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // inline-asm transposed reads (a ds_read_tr16 builtin makes the compiler drain every
+    // outstanding LDS-DMA load first: no prefetch would survive)
+    const uint32_t sb = lds0 + (s % NS) * SB;
+    s16x4 ra[4], rb[NT][4];
+    asm volatile(
+        "ds_read_b64_tr_b16 %0, %12\n\t"
+        "ds_read_b64_tr_b16 %1, %12 offset:512\n\t"
+        "ds_read_b64_tr_b16 %2, %12 offset:32\n\t"
+        "ds_read_b64_tr_b16 %3, %12 offset:544\n\t"
+        "ds_read_b64_tr_b16 %4, %13\n\t"
+        "ds_read_b64_tr_b16 %5, %13 offset:512\n\t"
+        "ds_read_b64_tr_b16 %6, %13 offset:32\n\t"
+        "ds_read_b64_tr_b16 %7, %13 offset:544\n\t"
+        "ds_read_b64_tr_b16 %8, %14\n\t"
+        "ds_read_b64_tr_b16 %9, %14 offset:512\n\t"
+        "ds_read_b64_tr_b16 %10, %14 offset:32\n\t"
+        "ds_read_b64_tr_b16 %11, %14 offset:544\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(ra[0]), "=&v"(ra[1]), "=&v"(ra[2]), "=&v"(ra[3]), "=&v"(rb[0][0]), "=&v"(rb[0][1]), "=&v"(rb[0][2]),
+          "=&v"(rb[0][3]), "=&v"(rb[1][0]), "=&v"(rb[1][1]), "=&v"(rb[1][2]), "=&v"(rb[1][3])
+        : "v"(sb + offA), "v"(sb + offB), "v"(sb + offB + TB)
+        : "memory");
+    if constexpr (NT == 4) {
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %8\n\t"
+          "ds_read_b64_tr_b16 %1, %8 offset:512\n\t"
+          "ds_read_b64_tr_b16 %2, %8 offset:32\n\t"
+          "ds_read_b64_tr_b16 %3, %8 offset:544\n\t"
+          "ds_read_b64_tr_b16 %4, %9\n\t"
+          "ds_read_b64_tr_b16 %5, %9 offset:512\n\t"
+          "ds_read_b64_tr_b16 %6, %9 offset:32\n\t"
+          "ds_read_b64_tr_b16 %7, %9 offset:544\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(rb[2][0]), "=&v"(rb[2][1]), "=&v"(rb[2][2]), "=&v"(rb[2][3]), "=&v"(rb[3][0]), "=&v"(rb[3][1]),
+            "=&v"(rb[3][2]), "=&v"(rb[3][3])
+          : "v"(sb + offB + 2 * TB), "v"(sb + offB + 3 * TB)
+          : "memory");
+    }
+    // the refilled slot was read in the previous k-step, before every wave passed this barrier
+    if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
+    bf16x8 a[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) a[u] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ra[2 * u], ra[2 * u + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const bf16x8 bx =
+            __builtin_bit_cast(bf16x8, __builtin_shufflevector(rb[j][2 * v], rb[j][2 * v + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          acc[j][u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bx, acc[j][u][v], 0, 0, 0);
+      }
+  }
+
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int k0 = c0 + j * 64;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = co0 + (cf0 + u) * 16 + 4 * grp + e;
+          const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
+                            static_cast<int64_t>(co) * K + k0 + (kf0 + v) * 16 + li;
+          if constexpr (OUT_BF16) static_cast<uint16_t*>(out)[o] = f_to_bf16(acc[j][u][v][e]);
+          else static_cast<float*>(out)[o] = acc[j][u][v][e];
+        }
+  }
+}
+
 // GARFIELD_IWGRAD_ROW: 0 one tap per workgroup, 1 the three taps of a kernel row (default),
 // 3 all nine taps of a 3x3 kernel
 static int iwgrad_row_mode() {
@@ -720,7 +864,20 @@ static int iwgrad_row_mode() {
   return m;
 }
 
-int iwgrad_taps_per_block(int kw) {
+// GARFIELD_IWGRAD_1X1_NT: input-channel blocks per workgroup of a 1x1 weight gradient
+// (4 / 2 / 1; a layer takes the largest that divides its C / 64)
+static int iwgrad_1x1_nt(int C) {
+  static const int m = [] {
+    const char* e = std::getenv("GARFIELD_IWGRAD_1X1_NT");
+    return e ? std::atoi(e) : 1;
+  }();
+  for (int nt = m; nt > 1; nt /= 2)
+    if (C % (64 * nt) == 0) return nt;
+  return 1;
+}
+
+int iwgrad_taps_per_block(int kw, int kh, int C) {
+  if (kw == 1 && kh == 1) return iwgrad_1x1_nt(C);
   const int m = iwgrad_row_mode();
   if (kw != 3 || m == 0) return 1;
   return m == 3 ? 9 : 3;
@@ -731,7 +888,21 @@ void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cou
   const int K = g.KH * g.KW * g.C;
   if (splits < 1) splits = 1;
   const int64_t per_split = (rg + splits - 1) / splits;
-  const int tpb = iwgrad_taps_per_block(g.KW);
+  const int tpb = iwgrad_taps_per_block(g.KW, g.KH, g.C);
+  if (tpb > 1 && g.KW == 1) {
+    const dim3 grid((g.C / (64 * tpb)) * (Cout / 64), groups, splits);
+#define GARFIELD_IWG_1X1(NTV)                                                                                      \
+  if (out_bf16)                                                                                                    \
+    hipLaunchKernelGGL((k_iwgrad_1x1<3, true, NTV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,   \
+                       out, split_stride, group_stride);                                                          \
+  else                                                                                                             \
+    hipLaunchKernelGGL((k_iwgrad_1x1<3, false, NTV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,  \
+                       out, split_stride, group_stride)
+    if (tpb == 4) { GARFIELD_IWG_1X1(4); }
+    else { GARFIELD_IWG_1X1(2); }
+#undef GARFIELD_IWG_1X1
+    return;
+  }
   if (tpb > 1 && (tpb == 3 || g.KH == 3)) {
     const int nr = tpb == 9 ? 3 : 1;
     const dim3 grid((g.KH / nr) * (g.C / 64) * (Cout / 64), groups, splits);

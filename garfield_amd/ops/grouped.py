@@ -553,7 +553,8 @@ def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int)
     cout = dy.shape[1]
     rows = dy.shape[0] * dy.shape[2] * dy.shape[3] // G
     C_ = _native.native()
-    S = _iwgrad_splits(rows, (K // 64) * (cout // 64) * G // C_.iwgrad_taps_per_block(spec.kernel[1]))
+    S = _iwgrad_splits(rows, (K // 64) * (cout // 64) * G //
+                      C_.iwgrad_taps_per_block(spec.kernel[1], spec.kernel[0], x.shape[1]))
     out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy.dtype) if S == 1 else None
     if out is not None:
         C_.gpu_iwgrad(x, dy, *_geom(spec), G, out, 1)
