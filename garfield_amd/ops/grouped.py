@@ -59,7 +59,8 @@ ICONV = os.environ.get("GARFIELD_ICONV", "1") != "0"
 # Their per-worker weight gradients by the implicit MFMA kernel (no im2col matrix).
 IWGRAD = os.environ.get("GARFIELD_IWGRAD", "1") != "0"
 # ... and for the 1x1 stride-1 convolutions too (else a split-K batched hipBLASLt GEMM).
-IWGRAD_1X1 = os.environ.get("GARFIELD_IWGRAD_1X1", "0") != "0"   # measured a wash: 7.715 vs 7.739 ms/step
+# 1x1 weight gradients on the implicit kernel too: 6.77-6.83 vs 6.82-6.88 ms/step (profiles/r2/ab_iwgrad_1x1.log)
+IWGRAD_1X1 = os.environ.get("GARFIELD_IWGRAD_1X1", "1") != "0"
 # weight gradients on a side stream (see WgradStream): measured slower in the graphed step
 # (7.23 vs 7.07 ms: per-layer fork/join dependencies leave 8% of the window idle), so off
 WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0")
