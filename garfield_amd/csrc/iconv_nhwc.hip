@@ -869,7 +869,7 @@ static int iwgrad_row_mode() {
 static int iwgrad_1x1_nt(int C) {
   static const int m = [] {
     const char* e = std::getenv("GARFIELD_IWGRAD_1X1_NT");
-    return e ? std::atoi(e) : 1;
+    return e ? std::atoi(e) : 2;   // profiles/r2/iwgrad_wg_nt_sweep.log
   }();
   for (int nt = m; nt > 1; nt /= 2)
     if (C % (64 * nt) == 0) return nt;

@@ -542,8 +542,9 @@ def _iwgrad_splits(rows_per_worker: int, tiles: int) -> int:
     return S
 
 
-# tuning knobs (profiles/iwgrad_split_sweep_r1.log)
-_IWGRAD_WG = int(os.environ.get("GARFIELD_IWGRAD_WG", "1024"))
+# tuning knobs (profiles/iwgrad_split_sweep_r1.log; 512 since the 1x1 layers joined the
+# implicit kernel: profiles/r2/iwgrad_wg_nt_sweep.log)
+_IWGRAD_WG = int(os.environ.get("GARFIELD_IWGRAD_WG", "512"))
 _IWGRAD_MINPIX = int(os.environ.get("GARFIELD_IWGRAD_MINPIX", "256"))
 
 
