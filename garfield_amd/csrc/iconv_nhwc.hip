@@ -891,15 +891,20 @@ void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cou
   const int tpb = iwgrad_taps_per_block(g.KW, g.KH, g.C);
   if (tpb > 1 && g.KW == 1) {
     const dim3 grid((g.C / (64 * tpb)) * (Cout / 64), groups, splits);
-#define GARFIELD_IWG_1X1(NTV)                                                                                      \
+#define GARFIELD_IWG_1X1(NSV, NTV)                                                                                 \
   if (out_bf16)                                                                                                    \
-    hipLaunchKernelGGL((k_iwgrad_1x1<3, true, NTV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,   \
+    hipLaunchKernelGGL((k_iwgrad_1x1<NSV, true, NTV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, \
                        out, split_stride, group_stride);                                                          \
   else                                                                                                             \
-    hipLaunchKernelGGL((k_iwgrad_1x1<3, false, NTV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,  \
+    hipLaunchKernelGGL((k_iwgrad_1x1<NSV, false, NTV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,\
                        out, split_stride, group_stride)
-    if (tpb == 4) { GARFIELD_IWG_1X1(4); }
-    else { GARFIELD_IWG_1X1(2); }
+    static const int ns = [] {   // GARFIELD_IWGRAD_1X1_NS: pipeline stages (3 or 4)
+      const char* e = std::getenv("GARFIELD_IWGRAD_1X1_NS");
+      return e && std::atoi(e) == 4 ? 4 : 3;
+    }();
+    if (tpb == 4) { GARFIELD_IWG_1X1(3, 4); }
+    else if (ns == 4) { GARFIELD_IWG_1X1(4, 2); }
+    else { GARFIELD_IWG_1X1(3, 2); }
 #undef GARFIELD_IWG_1X1
     return;
   }
