@@ -208,11 +208,20 @@ def main():
         from garfield_amd.utils.checkpoint import save_engine
 
         save_engine(a.checkpoint, eng, meta={"bench": vars(a)}, write=ctx.rank == 0)
+    checksums = None
+    if world > 1 and not a.num_ps:   # untimed: the replicas must be bit-identical
+        mine = torch.tensor([eng.replica_checksum()], dtype=torch.float64, device=ctx.device)
+        allc = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allc, mine)
+        checksums = [float(c.item()) for c in allc]
     n = getattr(eng, "n_w", eng.n)   # Byzantine-server mode: only the worker slots train
     imgs = n * a.batch * a.steps
     value = imgs / elapsed
     ms = 1000.0 * elapsed / a.steps
     extra = {}
+    if checksums is not None:
+        extra["replica_checksums"] = checksums
+        extra["replicas_identical"] = len(set(checksums)) == 1
     if a.phases:
         eng.timer.reset()
         for _ in range(3):

@@ -39,6 +39,13 @@ from garfield_amd.utils.checkpoint import Checkpoints
 from garfield_amd.utils.logging import info, set_rank_prefix
 
 
+def multistep_lr(base: float, milestones, gamma: float, epoch: int) -> float:
+    """Learning rate of 0-based ``epoch`` under the reference's schedule: ``MultiStepLR``
+    whose ``scheduler.step()`` runs at the START of every epoch (Garfield_CC
+    trainer.py:288-291), so the rate drops once epoch + 1 reaches a milestone."""
+    return base * gamma ** sum(1 for m in milestones if epoch + 1 >= m)
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser(description="Garfield_CC (Garfield-MI355X, collectives)")
     p.add_argument("--master", default=os.environ.get("MASTER_ADDR", "127.0.0.1"))
@@ -57,6 +64,10 @@ def parse(argv=None):
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--wd", type=float, default=5e-4)
     p.add_argument("--epochs", type=int, default=1)
+    p.add_argument("--lr_milestones", default=None,
+                   help="comma-separated epochs where the learning rate is multiplied by --lr_gamma (default: "
+                        "25,50 for resnet50, as the reference's MultiStepLR, trainer.py:273-274,290-291; none else)")
+    p.add_argument("--lr_gamma", type=float, default=0.1)
     p.add_argument("--num_iter", type=int, default=0, help="stop after this many iterations (0: epochs)")
     p.add_argument("--aggregator", default="vanilla", help="GAR name; vanilla = average (reference default)")
     p.add_argument("--mar", default="median")
@@ -145,9 +156,16 @@ def main(argv=None, results: dict | None = None):
         start = eng.step_count
         if ctx.rank == 0:
             info(f"resumed from {ck.path(start)} (iteration {start})")
+    per_epoch = max(min(len(ld) for ld in loaders), 1)
+    ms = a.lr_milestones if a.lr_milestones is not None else ("25,50" if a.model == "resnet50" else "")
+    milestones = [int(x) for x in ms.split(",") if x.strip()]
+    lrs = []
     t0 = time.time()
     loss = None
     for i in range(start, iters):
+        if i % per_epoch == 0 or i == start:   # the reference steps its scheduler at each epoch's start
+            eng.set_lr(multistep_lr(a.lr, milestones, a.lr_gamma, i // per_epoch))
+            lrs.append(eng.cfg.lr)
         batches = [ld[i] for ld in loaders]
         ts = time.perf_counter()
         loss = eng.step(batches)
@@ -171,7 +189,7 @@ def main(argv=None, results: dict | None = None):
         info(f"final accuracy {acc:.2f} after {iters} iterations ({time.time() - t0:.1f}s)")
         info(f"replica checksum {checksum:.12e}")
     if results is not None:
-        results.update(accuracy=acc, checksum=checksum, loss=float(loss) if loss is not None else None)
+        results.update(accuracy=acc, checksum=checksum, loss=float(loss) if loss is not None else None, lrs=lrs)
     shutdown(ctx)
     return acc
 

@@ -967,7 +967,137 @@ void stream_write_value(int64_t stream, int64_t p, int64_t value) {
               "garfield: hipStreamWriteValue64 failed");
 }
 
+// Events recorded / waited for at points INSIDE a captured HIP graph. Capture puts a
+// 1-thread marker kernel (k_signal_set on a per-mark word) at each point; after
+// capture (torch CUDAGraph(keep_graph=True)) the marker nodes are found in the raw
+// hipGraph_t and an event-record node is added behind each (another stream then
+// waits with hipStreamWaitEvent: an ordinary barrier packet, not a CP value poll),
+// or an event-wait node in front of the marker's dependents (the graph's later
+// kernels wait for work of another stream, e.g. a weight all-gather).
+// flags: 0 default (system-scope release on record), 1 device-scope release, 2 no system fence
+int64_t event_create(int64_t scope) {
+  hipEvent_t e = nullptr;
+  unsigned flags = hipEventDisableTiming;
+  if (scope == 1) flags |= hipEventReleaseToDevice;
+  if (scope == 2) flags |= hipEventDisableSystemFence;
+  TORCH_CHECK(hipEventCreateWithFlags(&e, flags) == hipSuccess, "garfield: hipEventCreate failed");
+  return reinterpret_cast<int64_t>(e);
+}
+void event_destroy(int64_t e) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e)); }
+void event_record(int64_t e, int64_t stream) {
+  TORCH_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), reinterpret_cast<hipStream_t>(stream)) == hipSuccess,
+              "garfield: hipEventRecord failed");
+}
+void event_wait(int64_t stream, int64_t e) {
+  TORCH_CHECK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<hipEvent_t>(e), 0) ==
+                  hipSuccess,
+              "garfield: hipStreamWaitEvent failed");
+}
+
+namespace {
+// marker nodes of the graph in insertion order, with the signal word each one stores to
+std::vector<std::pair<hipGraphNode_t, int64_t>> marker_nodes(hipGraph_t g) {
+  size_t count = 0;
+  TORCH_CHECK(hipGraphGetNodes(g, nullptr, &count) == hipSuccess, "garfield: hipGraphGetNodes failed");
+  std::vector<hipGraphNode_t> nodes(count);
+  TORCH_CHECK(hipGraphGetNodes(g, nodes.data(), &count) == hipSuccess, "garfield: hipGraphGetNodes failed");
+  std::vector<std::pair<hipGraphNode_t, int64_t>> out;
+  const void* fn = garfield::gpu::signal_kernel();
+  for (auto nd : nodes) {
+    hipGraphNodeType ty;
+    if (hipGraphNodeGetType(nd, &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) continue;
+    hipKernelNodeParams kp{};
+    if (hipGraphKernelNodeGetParams(nd, &kp) != hipSuccess || kp.func != fn) continue;
+    int64_t word = -1;   // -1: arguments not retrievable, matched by order
+    if (kp.kernelParams != nullptr && kp.kernelParams[0] != nullptr)
+      word = reinterpret_cast<int64_t>(*static_cast<unsigned long long* const*>(kp.kernelParams[0]));
+    out.emplace_back(nd, word);
+  }
+  (void)hipGetLastError();
+  return out;
+}
+
+hipGraphNode_t find_marker(const std::vector<std::pair<hipGraphNode_t, int64_t>>& marks, int64_t word, size_t i) {
+  for (const auto& m : marks)
+    if (m.second == word) return m.first;
+  const bool by_order = !marks.empty() && marks[0].second == -1;
+  TORCH_CHECK(by_order && i < marks.size(), "garfield: marker kernel for signal word ", word,
+              " not found in the captured graph");
+  return marks[i].first;
+}
+}  // namespace
+
+std::vector<hipGraphNode_t> dependents_of(hipGraphNode_t nd) {
+  size_t n = 0;
+  TORCH_CHECK(hipGraphNodeGetDependentNodes(nd, nullptr, &n) == hipSuccess, "garfield: dependents query failed");
+  std::vector<hipGraphNode_t> deps(n);
+  if (n) TORCH_CHECK(hipGraphNodeGetDependentNodes(nd, deps.data(), &n) == hipSuccess,
+                     "garfield: dependents query failed");
+  return deps;
+}
+
+// Put `node` between `mk` and mk's former dependents (the chain stays linear).
+void splice_after(hipGraph_t g, hipGraphNode_t mk, hipGraphNode_t node, const std::vector<hipGraphNode_t>& deps) {
+  for (auto d : deps) {
+    TORCH_CHECK(hipGraphRemoveDependencies(g, &mk, &d, 1) == hipSuccess, "garfield: hipGraphRemoveDependencies failed");
+    TORCH_CHECK(hipGraphAddDependencies(g, &node, &d, 1) == hipSuccess, "garfield: hipGraphAddDependencies failed");
+  }
+}
+
+int64_t graph_attach_record_events(int64_t graph, const std::vector<int64_t>& words,
+                                   const std::vector<int64_t>& events, bool inline_) {
+  TORCH_CHECK(words.size() == events.size(), "garfield: one event per marker");
+  auto g = reinterpret_cast<hipGraph_t>(graph);
+  const auto marks = marker_nodes(g);
+  for (size_t i = 0; i < words.size(); ++i) {
+    hipGraphNode_t dep = find_marker(marks, words[i], i);
+    const auto after = inline_ ? dependents_of(dep) : std::vector<hipGraphNode_t>{};
+    hipGraphNode_t node = nullptr;
+    TORCH_CHECK(hipGraphAddEventRecordNode(&node, g, &dep, 1, reinterpret_cast<hipEvent_t>(events[i])) == hipSuccess,
+                "garfield: hipGraphAddEventRecordNode failed");
+    splice_after(g, dep, node, after);
+  }
+  return static_cast<int64_t>(marks.size());
+}
+
+int64_t graph_attach_wait_events(int64_t graph, const std::vector<int64_t>& words,
+                                 const std::vector<int64_t>& events, bool inline_) {
+  TORCH_CHECK(words.size() == events.size(), "garfield: one event per marker");
+  auto g = reinterpret_cast<hipGraph_t>(graph);
+  const auto marks = marker_nodes(g);
+  for (size_t i = 0; i < words.size(); ++i) {
+    hipGraphNode_t mk = find_marker(marks, words[i], i);
+    const auto deps = dependents_of(mk);
+    hipGraphNode_t w = nullptr;
+    if (inline_) {   // marker -> wait -> the marker's former dependents
+      TORCH_CHECK(hipGraphAddEventWaitNode(&w, g, &mk, 1, reinterpret_cast<hipEvent_t>(events[i])) == hipSuccess,
+                  "garfield: hipGraphAddEventWaitNode failed");
+      splice_after(g, mk, w, deps);
+      continue;
+    }
+    TORCH_CHECK(hipGraphAddEventWaitNode(&w, g, nullptr, 0, reinterpret_cast<hipEvent_t>(events[i])) == hipSuccess,
+                "garfield: hipGraphAddEventWaitNode failed");
+    for (auto d : deps)
+      TORCH_CHECK(hipGraphAddDependencies(g, &w, &d, 1) == hipSuccess, "garfield: hipGraphAddDependencies failed");
+  }
+  return static_cast<int64_t>(marks.size());
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("event_create", &event_create, py::arg("scope") = 1,
+        "HIP event (no timing); scope 0: system-scope release on record (HIP default), 1: device-scope "
+        "release (enough for other streams of this device), 2: no system fence");
+  m.def("event_destroy", &event_destroy);
+  m.def("event_record", &event_record, py::arg("event"), py::arg("stream"));
+  m.def("event_wait", &event_wait, py::arg("stream"), py::arg("event"));
+  m.def("graph_attach_record_events", &graph_attach_record_events, py::arg("graph"), py::arg("words"),
+        py::arg("events"), py::arg("inline_") = true,
+        "Add an event-record node behind each marker kernel (signal word words[i]) of a captured, not yet "
+        "instantiated graph; returns the number of marker nodes found");
+  m.def("graph_attach_wait_events", &graph_attach_wait_events, py::arg("graph"), py::arg("words"),
+        py::arg("events"), py::arg("inline_") = true,
+        "Make the nodes that follow each marker kernel (signal word words[i]) wait for events[i] (event-wait "
+        "node); returns the number of marker nodes found");
   m.def("signal_alloc", &signal_alloc, py::arg("count"));
   m.def("signal_free", &signal_free);
   m.def("signal_wait_supported", &signal_wait_supported, py::arg("device"));

@@ -94,6 +94,8 @@ int flatten_cast(const void* const* srcs, const int* src_dts, const int64_t* num
 
 // ---- Stream signal: 1-thread kernel storing `value` (system-scope release) ----
 void signal_set(void* p, uint64_t value, hipStream_t stream);
+// host stub of the signal kernel (identifies its nodes in a captured graph)
+const void* signal_kernel();
 
 }  // namespace gpu
 }  // namespace garfield

@@ -16,6 +16,8 @@ __global__ void k_signal_set(unsigned long long* p, unsigned long long v) {
 }
 }  // namespace
 
+const void* signal_kernel() { return reinterpret_cast<const void*>(&k_signal_set); }
+
 void signal_set(void* p, uint64_t value, hipStream_t stream) {
   hipLaunchKernelGGL(k_signal_set, dim3(1), dim3(1), 0, stream, static_cast<unsigned long long*>(p),
                      static_cast<unsigned long long>(value));

@@ -65,12 +65,23 @@ class DeviceBatches:
         return True
 
     @classmethod
-    def synthetic(cls, num_images: int, shape, num_classes: int, k: int, batch: int, device, seed: int = 0, **kw):
-        """A random uint8 dataset of ``num_images`` images of ``shape`` (C, H, W)."""
+    def synthetic(cls, num_images: int, shape, num_classes: int, k: int, batch: int, device, seed: int = 0,
+                  learnable: bool = True, **kw):
+        """A random uint8 dataset of ``num_images`` images of ``shape`` (C, H, W).
+
+        ``learnable``: each class has a fixed random base colour (shared by every rank and
+        seed) and an image is its class colour plus uniform per-pixel noise of +-64, so the
+        label survives the crop (black padding) and the flip and training makes visible
+        progress (the loss falls below ln(num_classes)); else the labels are random."""
         g = torch.Generator().manual_seed(seed)
         c, h, w = shape
-        imgs = torch.randint(0, 256, (num_images, h, w, c), dtype=torch.uint8, generator=g)
         labels = torch.randint(0, num_classes, (num_images,), generator=g)
+        if learnable:
+            colours = torch.randint(64, 192, (num_classes, c), generator=torch.Generator().manual_seed(424242))
+            noise = torch.randint(-64, 65, (num_images, h, w, c), generator=g)
+            imgs = (colours[labels][:, None, None, :] + noise).clamp_(0, 255).to(torch.uint8)
+        else:
+            imgs = torch.randint(0, 256, (num_images, h, w, c), dtype=torch.uint8, generator=g)
         mean = kw.pop("mean", CIFAR_MEAN if c == 3 else (0.5,) * c)
         std = kw.pop("std", CIFAR_STD if c == 3 else (0.25,) * c)
         return cls(imgs, labels, k, batch, device, mean=mean, std=std, seed=seed, **kw)

@@ -517,17 +517,28 @@ def _large_gram(rows: Rows) -> torch.Tensor:
 
 
 def _large_krum_weights(rows: Rows, f: int, m: int) -> torch.Tensor:
-    g = _large_gram(rows)
+    return krum_weights_from_gram(_large_gram(rows), f, m)
+
+
+def distances_from_gram(g: torch.Tensor) -> torch.Tensor:
+    """Squared distances [n, n] from a Gram matrix: +inf on the diagonal and where non-finite."""
     dg = torch.diagonal(g)
     D = (dg[:, None] + dg[None, :] - 2 * g)
     D = torch.where(torch.isfinite(D), D.clamp(min=0), torch.full_like(D, math.inf))
     D.fill_diagonal_(math.inf)
-    q = rows.n - f - 2
+    return D
+
+
+def krum_weights_from_gram(g: torch.Tensor, f: int, m: int) -> torch.Tensor:
+    """Multi-Krum weights [n] (fp32, g's device) from a Gram matrix (vectorised, any n)."""
+    n = g.shape[0]
+    D = distances_from_gram(g)
+    q = n - f - 2
     near = torch.sort(D, dim=1, stable=True).values[:, :q]
     scores = near.sum(1)
     scores = torch.where(torch.isnan(scores), torch.full_like(scores, math.inf), scores)
     order = torch.sort(scores, stable=True).indices
-    w = torch.zeros(rows.n, dtype=torch.float32, device=rows.device)
+    w = torch.zeros(n, dtype=torch.float32, device=g.device)
     w[order[:m]] = 1.0 / m
     return w
 

@@ -119,7 +119,6 @@ class GradSink:
         self._offs: list = []
         self._split_parts: list = []   # deferred split-K sums (part [S, G, ...] fp32, out [G, ...] rows)
         self._split_outs: list = []
-        # off when a consumer reads rows DURING the backward (in-graph bucket signals)
         self.defer_splits = True
 
     def offset(self, p: torch.Tensor) -> int:
@@ -164,11 +163,15 @@ class GradSink:
         for g in range(self.groups):
             self.put(p, g, grads[g])
 
-    def flush(self) -> None:
+    def flush_splits(self) -> None:
+        """Run the queued split-K sums now (one launch), e.g. before a bucket mark."""
         if self._split_parts:
             _native.native().gpu_split_reduce_multi(self._split_parts, self._split_outs)
             self._split_parts.clear()
             self._split_outs.clear()
+
+    def flush(self) -> None:
+        self.flush_splits()
         if not self._srcs:
             return
         if self.flat.is_cuda:

@@ -17,10 +17,13 @@ Collective form here, per step, on flat vectors (never per tensor):
 3. every server replica runs the GAR (f = fw) on the worker rows only (a row
    table over the worker slots — no stacking copy) and applies its SGD update;
    simulated Byzantine servers (``ps_attack``, ranks < fps) then corrupt their model;
-4. every rank all-gathers the servers' models (``M[world, ld]``) and writes the
-   model aggregation rule (``mar``, f = fps) over the ``num_ps`` server rows into its
-   own parameters (HIP coordinate-wise kernel writing straight into the flat fp32
-   parameter buffer). Honest replicas therefore stay identical.
+4. each server broadcasts its fp32 model (``num_ps`` broadcasts into ``M[num_ps, ld]``:
+   only the server rows travel, ``num_ps * d * 4`` bytes received per rank) and every
+   rank writes the model aggregation rule (``mar``, f = fps) over them into its own
+   parameters (HIP coordinate-wise kernel writing straight into the flat fp32
+   parameter buffer). Honest replicas therefore stay identical. With one server the
+   rule over a single model is that model: the server keeps its update as it is and
+   the others receive it straight into their parameters.
 """
 from __future__ import annotations
 
@@ -61,7 +64,7 @@ class ByzantinePSDataParallel(RobustDataParallel):
         self.worker_ranks = list(range(0 if cfg.ps_workers else cfg.num_ps, ctx.world_size))
         self.computes = (not self.is_ps) or cfg.ps_workers
         self.n_w = self.k * len(self.worker_ranks)
-        self.M = torch.zeros((self.world, self.ld), dtype=torch.float32, device=self.device)
+        self.M = torch.zeros((self.num_ps, self.ld), dtype=torch.float32, device=self.device)
         self._ps_gen = torch.Generator(device=self.device)
         self._ps_gen.manual_seed(cfg.seed + 31 * ctx.rank)
 
@@ -113,15 +116,28 @@ class ByzantinePSDataParallel(RobustDataParallel):
             if cfg.ps_attack and self.rank < cfg.fps:
                 v = self.flat.data[: self.d]
                 v.copy_(SERVER_ATTACKS[cfg.ps_attack](v, generator=self._ps_gen))
-        # 4: model exchange + model aggregation on every rank
-        self.M[self.rank].copy_(self.flat.data)
-        if self.world > 1:
-            all_gather_rows(self.M, self.rank)
-        models = [self.M[p, : self.d] for p in range(self.num_ps)]
-        self._write_mar(models)
-        self.sync_shadow()   # master weights were rewritten by the model aggregation
+        # 4: model exchange (the servers' rows only) + model aggregation on every rank
+        self._exchange_models()
         self.step_count += 1
         return loss
+
+    def _exchange_models(self) -> None:
+        import torch.distributed as dist
+
+        if self.num_ps == 1:   # the rule over one model is that model
+            if self.world > 1:
+                dist.broadcast(self.flat.data, src=0)
+                if not self.is_ps:
+                    self.sync_shadow()
+            return
+        if self.is_ps:
+            self.M[self.rank].copy_(self.flat.data)
+        if self.world > 1:
+            works = [dist.broadcast(self.M[p], src=p, async_op=True) for p in range(self.num_ps)]
+            for w in works:
+                w.wait()
+        self._write_mar([self.M[p, : self.d] for p in range(self.num_ps)])
+        self.sync_shadow()   # master weights were rewritten by the model aggregation
 
     def _server_update(self) -> None:
         rows = self._worker_rows()

@@ -172,8 +172,8 @@ class RobustDataParallel:
         self.world = ctx.world_size
         self.rank = ctx.rank
         self.n = self.k * self.world
-        if self.n > gar.MAX_ROWS and self.device.type == "cuda":
-            raise ValueError(f"at most {gar.MAX_ROWS} logical workers per job on the GPU path, got {self.n}")
+        if self.n > gar.LARGE_ROWS and self.device.type == "cuda":
+            raise ValueError(f"at most {gar.LARGE_ROWS} logical workers per job on the GPU path, got {self.n}")
         # momentum: the whole vector, or this rank's shard when the aggregation is sharded
         self.mom = torch.zeros(self.ld // self.world if self._sharded else self.ld, dtype=torch.float32,
                                device=self.device)
@@ -248,6 +248,11 @@ class RobustDataParallel:
             return None
         return all_gather_rows(self.X[j], self.rank, async_op=True)
 
+    def set_lr(self, lr: float) -> None:
+        """Learning rate of the next updates (a scheduler hook): the fused combine + SGD
+        kernel reads ``cfg.lr`` at every launch (the GAR and update are never captured)."""
+        self.cfg.lr = float(lr)
+
     def momentum_vector(self) -> torch.Tensor:
         """The full momentum buffer (all-gathered when the optimizer state is sharded)."""
         return self._shard.momentum_vector() if self._shard is not None else self.mom
@@ -265,7 +270,7 @@ class RobustDataParallel:
 
         buckets = ("layer4", "layer3") if self._sharded else ()
         self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn, marks=buckets, offsets=offsets,
-                                    signals=overlap_enabled())
+                                    signals=overlap_enabled(self.ctx.world_size))
         self._gx = self._gy = None
         self._gsrc = None
         self._gsrc_refs = None
@@ -401,7 +406,9 @@ class RobustDataParallel:
             self._layerwise_update(rule, kw, first)
             self.step_count += 1
             return
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and self.n > gar.MAX_ROWS:
+            self._large_update(rule, kw, first)
+        elif self.device.type == "cuda":
             C = self._C
             param, mom = self.flat.data[: self.d], self.mom[: self.d]
             if rule in WEIGHTED_RULES:
@@ -425,6 +432,23 @@ class RobustDataParallel:
             g = gar.aggregate(rule, self.G.float(), **gkw).float()
             self._sgd_cpu(g, first)
         self.step_count += 1
+
+    def _large_update(self, rule: str, kw: dict, first: bool) -> None:
+        """More than MAX_ROWS (128) rows on the GPU (up to LARGE_ROWS = 1024, e.g. Bulyan with
+        32 workers per GPU on 8 GPUs): the [n, d] set as one matrix on ``gar_large.hip``
+        (compacted-weight combine, radix-select coordinate rules, hipBLASLt Gram for the
+        selections), the aggregate rounded to the exchange dtype, then the fused update."""
+        cfg = self.cfg
+        if rule in WEIGHTED_RULES:
+            w = self._weights(rule, kw)
+            self.last_weights = w
+            g = gar.combine(self.G, w)
+        else:
+            self.last_weights = None
+            g = gar.aggregate(rule, self.G, **self._rule_kwargs())
+        self._C.gpu_combine_sgd([g.contiguous()], self._one, self.flat.data[: self.d], self.mom[: self.d], None,
+                                self._shadow, cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov,
+                                first)
 
     def _layerwise_update(self, rule: str, kw: dict, first: bool) -> None:
         """The GAR on every parameter tensor's slice of the [n, d] rows (each parameter is
@@ -461,24 +485,28 @@ class RobustDataParallel:
             return gar.brute_weights(self.G, f)
         return gar.aksel_weights(self.G, f, kw.get("mode", "mid"))
 
-    def _coordinate(self, rule: str, kw: dict, out: torch.Tensor) -> None:
+    def _coordinate(self, rule: str, kw: dict, out: torch.Tensor, G=None) -> None:
+        """Coordinate-wise rule (or Bulyan) over ``G`` (default: the [n, d] exchange rows;
+        else a list of rows) into the fp32 vector ``out``."""
         C, f = self._C, self.cfg.f
         modes = gar._MODE
+        G = self.G if G is None else G
+        n = len(G) if isinstance(G, (list, tuple)) else G.shape[0]
         if rule == "bulyan":
-            t = self.n - 2 * f - 2
-            W = gar.bulyan_weights(self.G, f, self.cfg.m)
-            C.gpu_coordwise(self.G, modes["bulyan-tail"], f, t - 2 * f, W.reshape(-1), t, 0, 1.0, out)
+            t = n - 2 * f - 2
+            W = gar.bulyan_weights(G, f, self.cfg.m)
+            C.gpu_coordwise(G, modes["bulyan-tail"], f, t - 2 * f, W.reshape(-1), t, 0, 1.0, out)
         elif rule == "median":
-            C.gpu_coordwise(self.G, modes["median"], 0, 0, None, 0, 0, 1.0, out)
+            C.gpu_coordwise(G, modes["median"], 0, 0, None, 0, 0, 1.0, out)
         elif rule == "trimmed-mean":
-            C.gpu_coordwise(self.G, modes["trimmed-mean"], f, 0, None, 0, 0, 1.0, out)
+            C.gpu_coordwise(G, modes["trimmed-mean"], f, 0, None, 0, 0, 1.0, out)
         elif rule == "averaged-median":
-            beta = kw.get("beta") or self.n - f
-            C.gpu_coordwise(self.G, modes["averaged-median"], f, beta, None, 0, 0, 1.0, out)
+            beta = kw.get("beta") or n - f
+            C.gpu_coordwise(G, modes["averaged-median"], f, beta, None, 0, 0, 1.0, out)
         elif rule == "average-nan":
-            C.gpu_coordwise(self.G, modes["average-nan"], 0, 0, None, 0, 0, 1.0, out)
+            C.gpu_coordwise(G, modes["average-nan"], 0, 0, None, 0, 0, 1.0, out)
         elif rule == "condense":
-            C.gpu_coordwise(self.G, modes["condense"], f, 0, None, 0, self.cfg.seed + self.step_count,
+            C.gpu_coordwise(G, modes["condense"], f, 0, None, 0, self.cfg.seed + self.step_count,
                             float(kw.get("p", 0.9)), out)
         else:
             raise ValueError(rule)
@@ -515,11 +543,19 @@ class RobustDataParallel:
                 C.gpu_combine_sgd(rows, w, param, mom, None, self._shadow, cfg.lr, cfg.momentum, cfg.dampening,
                                   cfg.weight_decay, cfg.nesterov, first)
                 return
-            g = gar.aggregate(cfg.gar, rows, **self._rule_kwargs()).float()
+            if self._gagg is None:
+                self._gagg = torch.zeros(self.ld, dtype=torch.float32, device=self.device)
+            g = self._gagg[: self.d]
+            if len(rows) <= gar.MAX_ROWS:   # fp32 aggregate, as the synchronous step's
+                self._coordinate(cfg.gar, dict(cfg.gar_kwargs), g, rows)
+            else:
+                g.copy_(gar.aggregate(cfg.gar, rows, **self._rule_kwargs()))
             C.gpu_combine_sgd([g], self._one, param, mom, None, self._shadow, cfg.lr, cfg.momentum, cfg.dampening,
                               cfg.weight_decay, cfg.nesterov, first)
         else:
-            g = gar.aggregate(cfg.gar, rows, **self._rule_kwargs()).float()
+            # as a [rows, d] fp32 matrix: the aggregate keeps fp32 (a list of 16-bit rows
+            # would round it to the rows' dtype), as the synchronous step's
+            g = gar.aggregate(cfg.gar, torch.stack([r.float() for r in rows]), **self._rule_kwargs()).float()
             self._sgd_cpu(g, first)
 
     def _sgd_cpu(self, g: torch.Tensor, first: bool) -> None:
@@ -735,10 +771,16 @@ class RobustDataParallel:
             with torch.cuda.stream(s):  # warm-up on the capture stream (per-stream library state)
                 self._gexec.run(self._gx, self._gy, self._gloss)
             s.synchronize()
-            g = torch.cuda.CUDAGraph()
+            marks = self._gexec.mark_events() or []
+            g = torch.cuda.CUDAGraph(keep_graph=bool(marks))
             mode = "thread_local" if self.world > 1 else "global"
             with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
                 self._gexec.run(self._gx, self._gy, self._gloss)
+            if marks:   # bucket marks: event-record nodes behind the captured marker kernels
+                from garfield_amd.parallel.grouped import GraphSignal
+
+                GraphSignal.attach(g, marks)
+                g.instantiate()
             torch.cuda.current_stream(self.device).wait_stream(s)
             self._ggraph = g
         except Exception as e:  # capture unsupported: stay eager

@@ -76,8 +76,6 @@ class GroupedResNet:
             sig = {name: GraphSignal(dev) for name in self.marks}
             if all(x.available() for x in sig.values()):
                 self._events = sig
-        # a bucket's rows must be complete when its signal fires: no deferred split-K sums then
-        sink.defer_splits = self._events is None
 
     def bucket_offsets(self) -> list:
         """Flat offset where each marked layer's parameters start (bucket boundaries)."""
@@ -150,7 +148,7 @@ class GroupedResNet:
             x = grouped_maxpool(x, m.maxpool)
         for name in ("layer1", "layer2", "layer3", "layer4"):
             if self._events is not None and name in self._events:
-                x = _BucketMark.apply(x, self._events[name])
+                x = _BucketMark.apply(x, self._events[name], self.sink)
             for blk in getattr(m, name):
                 x = self._block(blk, x)
         self.ws.flush_running()
@@ -189,59 +187,79 @@ class GroupedResNet:
 class GraphSignal:
     """A point inside the step's HIP graph that another stream can wait for.
 
-    ``record(stream)`` launches a 1-thread kernel (captured into the graph like any
-    other) that stores 1 to an 8-byte signal word; ``wait_on(stream)`` enqueues a
-    command-processor wait for that word (``hipStreamWaitValue64``) and re-arms it
-    to 0 behind the wait, so every step's wait matches that step's record. (HIP
-    rejects external event-record nodes during capture, and torch refuses
-    ``Event(external=True)`` on ROCm.) ``available()`` is False when the device
-    cannot wait on a value: callers then wait for the whole stream instead."""
+    Eagerly, ``record(stream)`` records a HIP event. During capture it launches a
+    1-thread marker kernel instead (HIP rejects external event records during
+    capture, and torch refuses ``Event(external=True)`` on ROCm); after capture
+    ``attach(graph)`` finds the marker node in the raw ``hipGraph_t`` and splices an
+    event-record node in behind it (``bindings.cpp:graph_attach_record_events``),
+    so every replay records the same event at that point. ``wait_on(stream)`` is
+    then a plain ``hipStreamWaitEvent``.
 
-    _supported: dict = {}
+    Measured on MI355X (``scripts/probe_graph_events.py``,
+    ``profiles/r3/probe_graph_events.log``): the spliced record fires at its point
+    (0.85 ms into a 2.5 ms graph), and each event node costs ~40 us of device time
+    per replay (a marker kernel alone: ~1.4 us). A command-processor value wait
+    (``hipStreamWaitValue64``, the previous mechanism) measured ~450 us per wait."""
 
     def __init__(self, device: torch.device):
         from garfield_amd import _native
 
         self._C = _native.native()
-        dev = device.index if device.index is not None else torch.cuda.current_device()
-        if dev not in GraphSignal._supported:
-            GraphSignal._supported[dev] = bool(self._C.signal_wait_supported(dev))
-        self.ptr = self._C.signal_alloc(1) if GraphSignal._supported[dev] else 0
+        self.word = self._C.signal_alloc(1)      # the marker kernel's target (never waited on)
+        self.event = self._C.event_create()
 
     def available(self) -> bool:
-        return self.ptr != 0
+        return self.word != 0
 
     def record(self, stream) -> None:
-        if self.ptr:
-            self._C.signal_set(self.ptr, 1, stream.cuda_stream)
+        if torch.cuda.is_current_stream_capturing():
+            self._C.signal_set(self.word, 1, stream.cuda_stream)
+        else:
+            self._C.event_record(self.event, stream.cuda_stream)
 
     def wait_on(self, stream) -> None:
-        self._C.stream_wait_value(stream.cuda_stream, self.ptr, 1)
-        self._C.stream_write_value(stream.cuda_stream, self.ptr, 0)
+        self._C.event_wait(stream.cuda_stream, self.event)
+
+    @staticmethod
+    def attach(graph: "torch.cuda.CUDAGraph", signals) -> None:
+        """Splice an event-record node behind each signal's marker kernel of ``graph``
+        (captured with ``keep_graph=True``, not yet instantiated)."""
+        signals = list(signals)
+        if not signals:
+            return
+        C = signals[0]._C
+        found = C.graph_attach_record_events(graph.raw_cuda_graph(), [s.word for s in signals],
+                                             [s.event for s in signals], True)
+        if found < len(signals):
+            raise RuntimeError(f"graph has {found} marker kernels, expected {len(signals)}")
 
     def reset(self, stream) -> None:
-        """Re-arm after executions nobody waited for (warm-up / capture passes)."""
-        if self.ptr:
-            self._C.stream_write_value(stream.cuda_stream, self.ptr, 0)
+        """Nothing to re-arm: an event wait matches the latest record."""
 
     def __del__(self):
         try:
-            if self.ptr:
-                self._C.signal_free(self.ptr)
+            if self.word:
+                self._C.signal_free(self.word)
+            if self.event:
+                self._C.event_destroy(self.event)
         except Exception:
             pass
 
 
 class _BucketMark(torch.autograd.Function):
     """Identity whose backward records ``event`` (a GraphSignal) on the current stream:
-    by then the backward has produced every gradient of the layers after this point."""
+    by then the backward has produced every gradient of the layers after this point
+    (the split-K weight-gradient sums queued so far are flushed first, so the
+    bucket's rows are complete when the event fires)."""
 
     @staticmethod
-    def forward(ctx, x, event):
-        ctx.event = event
+    def forward(ctx, x, event, sink):
+        ctx.event, ctx.sink = event, sink
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.sink is not None:
+            ctx.sink.flush_splits()
         ctx.event.record(torch.cuda.current_stream(dy.device))
-        return dy, None
+        return dy, None, None

@@ -41,6 +41,7 @@ from torch import nn
 from garfield_amd import aggregators
 from garfield_amd.parallel.comm import DistContext
 from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel
+from garfield_amd.runtime.attacks import NEEDS_ESTIMATES
 
 
 @dataclass
@@ -75,6 +76,7 @@ class QuorumDataParallel(RobustDataParallel):
         self._dec = torch.zeros((2, W), dtype=torch.int32, device=self.device)
         self._inflight: list = []
         self._own = [None, None]   # this rank's send of each parity buffer
+        self._dec_send = [None, None]   # the leader's decision broadcast of each parity
         self.last_quorum: list[int] = list(range(self.world))
         self.skipped = 0           # steps this rank skipped because it was behind (catch-up)
 
@@ -151,8 +153,12 @@ class QuorumDataParallel(RobustDataParallel):
             chosen = sorted(arrived)
             mask = torch.zeros(W, dtype=torch.int32)
             mask[chosen] = 1
+            if self._dec_send[par] is not None:   # step t - 2's decision left this buffer
+                self._dec_send[par].wait()
             dec.copy_(mask)
-            dist.broadcast(dec, src=r0, group=self._gdec)
+            # asynchronous: on RCCL a synchronous broadcast would hold the leader's stream
+            # until every rank, a straggler included, has posted its receive
+            self._dec_send[par] = dist.broadcast(dec, src=r0, group=self._gdec, async_op=True)
         else:
             dec_work.wait()
             chosen = [r for r, v in enumerate(dec.tolist()) if v]
@@ -161,17 +167,23 @@ class QuorumDataParallel(RobustDataParallel):
                 works[r].wait()
         self._inflight += [works[r] for r in range(W) if r not in chosen and r != r0]
         self.last_quorum = chosen
-        # 5. GAR over the chosen rows (slot j * world + r) + the update
-        rows = [buf[r, j, : self.d] for r in chosen for j in range(self.k)]
-        self._collude(rows, [j * W + r for r in chosen for j in range(self.k)])
+        # 5. GAR over the chosen rows in slot order (slot j * world + r, as the synchronous
+        # engine's [n, d] input) + the update. A colluding attack rewrites its row: on a
+        # copy, since buf[r0] is the source of this rank's still-running broadcast and a
+        # late receiver must get the honest row (and attack it itself, identically)
+        slots = [j * W + r for j in range(self.k) for r in chosen]
+        rows = [buf[s % W, s // W, : self.d] for s in slots]
+        colluders = {s for s, a in cfg.byzantine.items() if a in NEEDS_ESTIMATES}
+        rows = [r.clone() if s in colluders else r for r, s in zip(rows, slots)]
+        self._collude(rows, slots)
         self._update_from_rows(rows)
         self.step_count += 1
         return loss
 
     def finish(self) -> None:
         """Wait for every broadcast still in flight (late rows of stragglers)."""
-        for w in self._inflight + [w for w in self._own if w is not None]:
+        for w in self._inflight + [w for w in self._own + self._dec_send if w is not None]:
             w.wait()
-        self._inflight, self._own = [], [None, None]
+        self._inflight, self._own, self._dec_send = [], [None, None], [None, None]
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)

@@ -63,28 +63,39 @@ def shard_pad(world: int, base: int = 64) -> int:
     return base * world
 
 
-def overlap_enabled() -> bool:
-    """GARFIELD_OVERLAP=1: each bucket's exchange waits on a signal written INSIDE the step's
-    graph (hipStreamWaitValue64), so it can leave during the backward. Off by default: on
-    ROCm 7 / MI355X every such command-processor wait measured ~0.45 ms of latency (the
-    world-1 bucketed step: 9.0 ms/step with the signals vs 7.2 ms without them,
-    profiles/r2/ab_overlap_signals.log), more than the overlap can hide. Without it the
-    buckets leave right after the backward and the per-bucket aggregation pipelines with
-    the later buckets' transfers."""
-    return os.environ.get("GARFIELD_OVERLAP", "0") != "0"
+def overlap_enabled(world: int = 1) -> bool:
+    """Whether each bucket's exchange starts INSIDE the step's backward: the grouped
+    executor records an event when the backward has written a bucket (an event-record
+    node spliced into the captured HIP graph, ``grouped.GraphSignal``), and the comm
+    stream waits for it. Each such node costs ~40 us of device time per replay on
+    MI355X (``profiles/r3/probe_graph_events.log``), so the default
+    (``GARFIELD_OVERLAP`` unset) is on only when there is something to overlap
+    (world > 1); ``GARFIELD_OVERLAP=1`` forces it (e.g. the world-1 loopback
+    exchange), ``0`` disables it."""
+    v = os.environ.get("GARFIELD_OVERLAP", "")
+    if v == "":
+        return world > 1
+    return v != "0"
 
 
 class _Bucket:
+    """One layer bucket [lo, hi) of the flat vector, cut into ``world`` shards of S.
+
+    ``send[dst, j]`` = local worker j's shard ``dst`` (packed so the whole bucket
+    leaves in ONE ``all_to_all_single``), ``recv[src, j]`` = shard ``rank`` of source
+    rank src's local worker j (the row of global slot j * world + src)."""
+
     def __init__(self, lo: int, hi: int, world: int, rank: int, k: int, dev, dt):
         self.lo, self.hi = lo, hi
         self.S = (hi - lo) // world
         self.own = slice(lo + rank * self.S, lo + (rank + 1) * self.S)
-        # recv[j, src] = shard `rank` of source rank src's local worker j
-        self.recv = torch.empty((k, world, self.S), dtype=dt, device=dev) if world > 1 else None
+        self.send = torch.empty((world, k, self.S), dtype=dt, device=dev) if world > 1 else None
+        self.recv = torch.empty((world, k, self.S), dtype=dt, device=dev) if world > 1 else None
         self.moff = 0          # offset of this bucket's shard in the momentum buffer
         self.works: list = []
         self.rows: list = []
         self.gagg = None
+        self.done = None
 
 
 class ShardedAggregator:
@@ -117,7 +128,10 @@ class ShardedAggregator:
         self._started = False
         self._gathers: list = []
         self.master_stale = False
-        self._comm_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self._comm_stream = None
+        if dev.type == "cuda":
+            self._comm_stream = (torch.cuda.Stream(dev) if os.environ.get("GARFIELD_COMM_STREAM", "1") != "0"
+                                 else torch.cuda.current_stream(dev))
         self._init_fp32_sync()
 
     # ------------------------------------------------------------------ #
@@ -128,7 +142,7 @@ class ShardedAggregator:
         e = self.e
         if self.world == 1:
             return [e.X[j, 0, b.lo:b.hi] for j in range(self.k)]
-        return [b.recv[s // self.world, s % self.world] for s in range(self.n)]
+        return [b.recv[s % self.world, s // self.world] for s in range(self.n)]
 
     def _init_fp32_sync(self) -> None:
         """fp32 parameters the forward reads directly (not mirrored by the bf16 working
@@ -157,19 +171,23 @@ class ShardedAggregator:
     # exchange
 
     def start_exchange(self, events=None) -> None:
-        """Issue every bucket's all-to-all, in ready order. ``events[i]`` (optional)
-        marks the point of the backward where bucket i's rows are complete; the
-        side stream waits on it, so the exchange overlaps the rest of the backward."""
+        """Issue every bucket's exchange, in ready order: the simulated attacks on the
+        bucket's slice of the local rows, one pack of the k rows into ``send[dst, j]``
+        and ONE ``all_to_all_single`` per bucket (3 collectives per step for the
+        ResNets). ``events[i]`` (optional) marks the point of the backward where bucket
+        i's rows are complete; the comm stream waits on it, so the exchange overlaps
+        the rest of the backward."""
         e = self.e
         cuda = e.device.type == "cuda"
         main = torch.cuda.current_stream(e.device) if cuda else None
+        use_events = events is not None and overlap_enabled(self.world)
         for i, b in enumerate(self.buckets):
             if cuda:
                 s = self._comm_stream
-                ev = events[i] if (events is not None and i < len(events) and overlap_enabled()) else None
+                ev = events[i] if (use_events and i < len(events)) else None
                 if ev is not None:
                     ev.wait_on(s)      # a point inside the step's graph (grouped.GraphSignal)
-                else:
+                elif _XS in ("both", "c_waits_main"):
                     s.wait_stream(main)
                 ctx = torch.cuda.stream(s)
             else:
@@ -177,17 +195,17 @@ class ShardedAggregator:
             with ctx:
                 e._attack_rows(b.lo, b.hi)
                 b.works = []
+                local = e.X[:, 0, b.lo:b.hi].view(self.k, self.world, b.S).transpose(0, 1)   # [dst, j, S]
                 if self.world > 1:
-                    for j in range(self.k):
-                        src = e.X[j, 0, b.lo:b.hi]
-                        b.works.append(dist.all_to_all_single(b.recv[j].view(-1), src, async_op=True))
+                    b.send.copy_(local)
+                    b.works.append(dist.all_to_all_single(b.recv.view(-1), b.send.view(-1), async_op=True))
                 elif cuda and loopback_enabled():   # world 1: emulate the transfer (traces / tests)
                     if b.recv is None:
-                        b.recv = torch.empty((self.k, 1, b.S), dtype=e.X.dtype, device=e.device)
-                        b.rows = [b.recv[j, 0] for j in range(self.k)]
-                    b.recv.copy_(e.X[:, :, b.lo:b.hi])
+                        b.recv = torch.empty((1, self.k, b.S), dtype=e.X.dtype, device=e.device)
+                        b.rows = [b.recv[0, j] for j in range(self.k)]
+                    b.recv.copy_(local)
                 if cuda:
-                    b.done = torch.cuda.Event()
+                    b.done = torch.cuda.Event(enable_timing=_TIMING)
                     b.done.record(s)
         self._started = True
 
@@ -195,7 +213,7 @@ class ShardedAggregator:
         for w in b.works:
             w.wait()
         b.works = []
-        if self.e.device.type == "cuda":
+        if self.e.device.type == "cuda" and _XS in ("both", "main_waits_c"):
             torch.cuda.current_stream(self.e.device).wait_event(b.done)
         self.e._collude(b.rows)   # colluding attacks on this rank's coordinate shard of every row
 
@@ -220,30 +238,40 @@ class ShardedAggregator:
         e, cfg = self.e, self.e.cfg
         if not self._started:
             self.start_exchange()
+        self._gathers = []
         if e.device.type == "cuda":
             self._gpu(cfg, first)
         else:
             self._cpu(cfg, first)
         self._started = False
-        self._gather_weights()
+        self._finish_gathers()
 
-    def _gather_weights(self) -> None:
-        """All-gather the updated parameters per bucket: the bf16 working weights (and
-        the compact fp32 parameters) when the forward reads those, else the fp32 master."""
+    def _gather_bucket(self, b: _Bucket) -> None:
+        """Start the all-gather of bucket b's updated parameters (the bf16 working weights
+        when the forward reads those, else the fp32 master) as soon as its update is
+        queued: on RCCL it runs beside the remaining buckets' updates."""
+        e = self.e
+        if self.world == 1:
+            return
+        buf = e._shadow if e._shadow is not None else e.flat.data
+        full, mine = buf[b.lo:b.hi], buf[b.own]
+        if gloo_backend():
+            mine = mine.clone()  # gloo rejects an input aliasing the output
+        self._gathers.append(dist.all_gather_into_tensor(full, mine, async_op=True))
+
+    def _finish_gathers(self) -> None:
+        """Wait (stream-ordered on RCCL) for the weight all-gathers, then exchange the compact
+        fp32 parameters the forward reads directly (BatchNorm affine) in one all-reduce."""
         e = self.e
         if self.world == 1:
             if e._shadow is not None and e.device.type != "cuda":
                 with torch.no_grad():
                     e._shadow.copy_(e.flat.data)
             return
-        lp = e._shadow is not None
-        buf = e._shadow if lp else e.flat.data
-        for b in sorted(self.buckets, key=lambda b: b.lo):   # the next forward reads low coordinates first
-            full, mine = buf[b.lo:b.hi], buf[b.own]
-            if gloo_backend():
-                mine = mine.clone()  # gloo rejects an input aliasing the output
-            dist.all_gather_into_tensor(full, mine)
-        if lp:
+        for w in self._gathers:
+            w.wait()
+        self._gathers = []
+        if e._shadow is not None:
             self.master_stale = True
             if self._np_idx is not None:
                 nb = self._np_buf
@@ -282,6 +310,8 @@ class ShardedAggregator:
         return e.flat.data[b.own], mom, shadow
 
     def _gpu(self, cfg, first: bool) -> None:
+        if self.n > gar.MAX_ROWS:
+            return self._gpu_large(cfg, first)
         e, C = self.e, self.e._C
         rule, f, kw = cfg.gar, cfg.f, dict(cfg.gar_kwargs)
         n = self.n
@@ -315,16 +345,18 @@ class ShardedAggregator:
                 w = self._select(C, total, rule, f, cfg)
             if rule != "bulyan":
                 e.last_weights = w
-                for b in self.buckets:
+                for b in self._update_order():
                     p, mom, sh = self._param(b)
                     C.gpu_combine_sgd(b.rows, w, p, mom, None, sh, *args)
+                    self._gather_bucket(b)
                 return
             t = n - 2 * f - 2
-            for b in self.buckets:
+            for b in self._update_order():
                 g = self._gagg(b)
                 C.gpu_coordwise(b.rows, modes["bulyan-tail"], f, t - 2 * f, w, t, 0, 1.0, g)
                 p, mom, sh = self._param(b)
                 C.gpu_combine_sgd([g], self._one, p, mom, None, sh, *args)
+                self._gather_bucket(b)
             return
         for b in self.buckets:
             self._wait(b)
@@ -332,6 +364,7 @@ class ShardedAggregator:
             if rule == "average":
                 e.last_weights = self._avg
                 C.gpu_combine_sgd(b.rows, self._avg, p, mom, None, sh, *args)
+                self._gather_bucket(b)
                 continue
             g = self._gagg(b)
             if rule == "median":
@@ -348,6 +381,81 @@ class ShardedAggregator:
             else:
                 raise ValueError(f"sharded aggregation does not support {rule!r}")
             C.gpu_combine_sgd([g], self._one, p, mom, None, sh, *args)
+            self._gather_bucket(b)
+
+    def _matrix(self, b: _Bucket) -> torch.Tensor:
+        """Bucket b's received shards as ONE [n, S] matrix (row src * k + j: the receive
+        buffer as it lands, no copy); ``self._perm[s]`` is the matrix row of global slot s."""
+        if self.world == 1:
+            return torch.stack(b.rows) if b.recv is None else b.recv.view(self.n, b.S)
+        return b.recv.view(self.n, b.S)
+
+    def _gpu_large(self, cfg, first: bool) -> None:
+        """More than MAX_ROWS rows (e.g. 8 GPUs x 32 workers): each bucket's shards as one
+        matrix on the gar_large.hip kernels (Gram by hipBLASLt with fp32 output, compacted
+        combine, radix-select coordinate rules). Selections are made in slot order (the
+        partial Grams permuted once), then mapped back to the matrix's row order."""
+        e, C = self.e, self.e._C
+        rule, f, kw = cfg.gar, cfg.f, dict(cfg.gar_kwargs)
+        n, k, world = self.n, self.k, self.world
+        args = (cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
+        perm = torch.tensor([(s % world) * k + s // world for s in range(n)], device=e.device)
+        mats = {}
+        for b in self.buckets:
+            self._wait(b)
+            mats[b.lo] = self._matrix(b)
+        if rule in ("krum", "bulyan", "brute"):
+            total = None
+            for b in self.buckets:
+                X = mats[b.lo]
+                g = torch.mm(X, X.T, out_dtype=torch.float32) if X.dtype != torch.float32 else X @ X.T
+                total = g if total is None else total.add_(g)
+            gs = self._sum_over_ranks(total)[perm][:, perm]          # slot order on every rank
+            m = cfg.m if cfg.m is not None else n - f - 2
+            if rule == "krum":
+                ws = gar.krum_weights_from_gram(gs, f, m)
+            elif rule == "brute":
+                from garfield_amd.ops import reference as _ref
+                ws = _ref.brute_weights(gar.distances_from_gram(gs.double()).cpu(), f).float().to(e.device)
+            else:
+                W = gar._large_bulyan_weights(gar.distances_from_gram(gs.double()), f, m).float().to(e.device)
+                Wm = torch.empty_like(W)
+                Wm[:, perm] = W
+                t, beta = n - 2 * f - 2, n - 4 * f - 2
+                e.last_weights = None
+                for b in self._update_order():
+                    V = torch.mm(Wm, mats[b.lo].float())          # [t, S] fp32 (bounded: one shard)
+                    g = self._gagg(b)
+                    C.gpu_large_coord(V, 2, 0, beta, g)
+                    p, mom, sh = self._param(b)
+                    C.gpu_combine_sgd([g], self._one, p, mom, None, sh, *args)
+                    self._gather_bucket(b)
+                return
+        elif rule == "average":
+            ws = torch.full((n,), 1.0 / n, dtype=torch.float32, device=e.device)
+        else:
+            ws = None
+        if ws is not None:
+            e.last_weights = ws
+            wm = torch.empty_like(ws)
+            wm[perm] = ws
+        for b in self._update_order():
+            X = mats[b.lo]
+            out = torch.empty(b.S, dtype=X.dtype, device=e.device)
+            if ws is not None:
+                C.gpu_large_combine(X, wm, out)
+            elif rule in gar._LARGE_MODE:
+                beta = kw.get("beta") or n - f
+                C.gpu_large_coord(X, gar._LARGE_MODE[rule], f, beta, out)
+            else:
+                raise ValueError(f"sharded aggregation of more than {gar.MAX_ROWS} rows does not support {rule!r}")
+            p, mom, sh = self._param(b)
+            C.gpu_combine_sgd([out], self._one, p, mom, None, sh, *args)
+            self._gather_bucket(b)
+
+    def _update_order(self) -> list:
+        """Buckets by ascending coordinates: the next forward reads the low ones first."""
+        return sorted(self.buckets, key=lambda b: b.lo)
 
     def _ws_any(self):
         return self._wsp(self.buckets[0])
@@ -392,6 +500,7 @@ class ShardedAggregator:
         pos = 0
         for b in order:
             self._sgd_cpu(b, g[pos:pos + b.S], first)
+            self._gather_bucket(b)
             pos += b.S
 
     def _cpu_rule(self, cfg, X: torch.Tensor) -> torch.Tensor:
@@ -479,6 +588,12 @@ class _nullctx:
 
     def __exit__(self, *a):
         return False
+
+
+# GARFIELD_EXCHANGE_TIMING=1: the per-bucket "exchange issued" events are timing events
+# (scripts/overlap_timing.py reads them against the step's start and its backward's end)
+_TIMING = os.environ.get("GARFIELD_EXCHANGE_TIMING", "0") == "1"
+_XS = os.environ.get("GARFIELD_XS_DEBUG", "both")   # DEBUG: which cross-stream waits to keep
 
 
 def loopback_enabled() -> bool:

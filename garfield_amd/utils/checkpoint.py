@@ -40,6 +40,7 @@ def save(path: str, model: nn.Module, step: int = 0, momentum: torch.Tensor | No
     state["step"] = int(step)
     if momentum is not None:
         state["momentum"] = momentum.detach().cpu()
+        state["momentum_layout"] = "reference"   # checkpoints without the key hold memory order
     state["meta"] = dict(meta or {})
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
@@ -96,7 +97,10 @@ def load_engine(path: str, engine) -> dict:
     if "momentum" in state:
         m = state["momentum"].to(engine.mom.device)
         full = torch.zeros(engine.flat.ld, dtype=engine.mom.dtype, device=engine.mom.device)
-        engine.flat.from_reference(m, full)        # reference layout -> this engine's memory order
+        if state.get("momentum_layout") == "reference":
+            engine.flat.from_reference(m, full)    # reference layout -> this engine's memory order
+        else:   # older checkpoints stored the engine's memory order as it was
+            full[: min(m.numel(), full.numel())] = m.reshape(-1)[: full.numel()].to(full.dtype)
         shard = getattr(engine, "_shard", None)
         if shard is not None and hasattr(shard, "load_momentum"):
             shard.load_momentum(full)
@@ -105,7 +109,13 @@ def load_engine(path: str, engine) -> dict:
         else:
             engine.mom.copy_(full[: engine.mom.numel()])
     engine.step_count = int(state.get("step", 0))
-    engine._graph = None  # re-capture against the restored state
+    # re-capture against the restored state: the per-worker graphs and the grouped graph
+    # (whose replays read the master / working weights and the BatchNorm buffers in place,
+    # so they would survive, but a restored engine must not depend on that)
+    engine._graph = None
+    if hasattr(engine, "_ggraph"):
+        engine._ggraph = None
+        engine._gsrc = None
     return state
 
 

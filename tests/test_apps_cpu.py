@@ -182,3 +182,16 @@ def test_garfield_cc_fastest_quorum_with_straggler():
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
     assert re.search(r"final accuracy ([0-9.]+)", out.stdout + out.stderr)
+
+
+def test_garfield_cc_multistep_lr_schedule():
+    """The reference's per-epoch MultiStepLR (Garfield_CC trainer.py:273-274,290-291: milestones [25, 50],
+    gamma 0.1 for resnet50, stepped at each epoch's start) drives the engine's fused update."""
+    from garfield_amd.apps import garfield_cc
+
+    assert [garfield_cc.multistep_lr(0.2, [25, 50], 0.1, e) for e in (0, 23, 24, 48, 49, 80)] == \
+        pytest.approx([0.2, 0.2, 0.02, 0.02, 0.002, 0.002])
+    res = {}
+    garfield_cc.main(["--model", "pimanet", "--dataset", "pima", "--loss", "binary-cross-entropy", "--batch", "200",
+                      "--epochs", "3", "--lr", "0.1", "--lr_milestones", "2,3", "--cuda_graph", "0"], results=res)
+    assert res["lrs"] == pytest.approx([0.1, 0.01, 0.001])

@@ -74,6 +74,7 @@ def test_bench_py_contract_two_ranks():
         assert key in row, key
     assert row["n_gpus"] == 2 and row["steps"] == 1 and row["warmup"] == 1 and row["scaling"] == "weak"
     assert row["config"]["global_batch"] == 2 * 3 * 4 and row["value"] > 0
+    assert row["replicas_identical"] and len(row["replica_checksums"]) == 2
 
 
 def test_bench_py_self_launches_ranks():
@@ -111,3 +112,14 @@ def test_bench_py_fp32_and_static_data_modes():
         assert r.returncode == 0, r.stderr[-3000:]
         rows = _rows(r.stdout)
         assert len(rows) == 1 and rows[0]["dtype"] == dtype and word in rows[0]["data"], rows
+
+
+def test_bench_py_loss_is_a_training_signal():
+    """The default fresh-data feed has learnable labels (class colour + noise, data/fresh.py):
+    the loss of the last timed step is below the first warm-up step's and below ln(10)."""
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--steps", "30", "--warmup", "1",
+                        "--model", "cifarnet", "--batch", "32", "--workers-per-gpu", "3", "--f", "0", "--gar",
+                        "average", "--lr", "0.02"], capture_output=True, text=True, timeout=600, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    row = _rows(r.stdout)[0]
+    assert row["final_loss"] < row["first_loss"] and row["final_loss"] < 2.3026, row

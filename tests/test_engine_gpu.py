@@ -239,3 +239,52 @@ def test_byzps_one_gpu_grouped_matches_plain_engine(cuda):
             assert eng._ggraph is not None
         outs.append(eng.flat.reference_vector().clone())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("rule,f", [("krum", 4), ("bulyan", 4), ("median", 8), ("trimmed-mean", 8), ("average", 1)])
+def test_engine_more_than_128_workers(cuda, rule, f):
+    """n = 256 logical workers (e.g. 8 GPUs x 32 workers): the [n, d] set runs on the
+    gar_large.hip path; the update equals the rule applied to the same rows (+ SGD)."""
+    from garfield_amd.ops import gar
+
+    torch.manual_seed(0)
+    k = 256
+    cfg = EngineConfig(gar=rule, f=f, workers_per_rank=k, lr=0.1, momentum=0.0, weight_decay=0.0,
+                       byzantine={3: "reverse", 77: "reverse"}, cuda_graph=False)
+    eng = RobustDataParallel(build_model("mlp"), F.nll_loss, DistContext(device=cuda), cfg)
+    batches = synthetic_batches(k, 2, (1, 28, 28), 10, cuda)
+    before = eng.flat.data[: eng.d].clone()
+    eng.step(batches)
+    torch.cuda.synchronize()
+    kw = {"f": f} if rule not in ("median", "average") else {}
+    want = gar.aggregate(rule, eng.G, **kw).float()
+    got = (before - eng.flat.data[: eng.d]) / 0.1
+    assert torch.allclose(got, want, rtol=2e-2, atol=1e-4), (got - want).abs().max()
+    if rule == "krum":
+        w = eng.last_weights.cpu()
+        assert w[3] == 0 and w[77] == 0 and abs(float(w.sum()) - 1) < 1e-5
+
+
+def test_grouped_resume_after_capture_is_exact(cuda, tmp_path):
+    """Restoring a checkpoint into an engine whose grouped step is already captured as a
+    HIP graph: the replayed continuation equals the uninterrupted run bit for bit."""
+    from garfield_amd.utils.checkpoint import load_engine, save_engine
+
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda),
+                             EngineConfig(gar="krum", f=1, workers_per_rank=5, lr=0.02, cuda_graph=True))
+    batches = synthetic_batches(5, 8, (3, 32, 32), 10, cuda)
+    for _ in range(3):
+        eng.step(batches)
+    assert eng._ggraph is not None
+    ck = str(tmp_path / "ck.pt")
+    save_engine(ck, eng)
+    for _ in range(2):
+        eng.step(batches)
+    straight = eng.flat_model().clone()
+    load_engine(ck, eng)
+    assert eng._ggraph is None and eng.step_count == 3
+    for _ in range(2):
+        eng.step(batches)
+    assert eng._ggraph is not None
+    assert torch.equal(eng.flat_model(), straight)

@@ -27,7 +27,7 @@ def free_port():
 STEPS, DELAY = 6, 1.0
 
 
-def _worker(rank, world, port, outdir, quorum, delay):
+def _worker(rank, world, port, outdir, quorum, delay, byz=None, gar="median", sync=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     torch.set_num_threads(1)
@@ -35,9 +35,18 @@ def _worker(rank, world, port, outdir, quorum, delay):
 
     ctx = init_distributed(backend="gloo", device="cpu")
     torch.manual_seed(0)
-    eng = QuorumDataParallel(build_model("mlp"), F.nll_loss, ctx,
-                             QuorumConfig(gar="median", f=1, workers_per_rank=2, quorum=quorum, lr=0.05,
-                                          byzantine={1: "reverse"}, straggler_delay={2: delay}))
+    byz = {1: "reverse"} if byz is None else byz
+    if sync:   # the synchronous engine, for comparison
+        from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel
+
+        eng = RobustDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                                 EngineConfig(gar=gar, f=1, workers_per_rank=2, lr=0.05, byzantine=byz,
+                                              shard_gar=False, collusion="all"))
+        eng.last_quorum, eng.skipped, eng.finish = None, 0, (lambda: None)
+    else:
+        eng = QuorumDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                                 QuorumConfig(gar=gar, f=1, workers_per_rank=2, quorum=quorum, lr=0.05,
+                                              byzantine=byz, straggler_delay={2: delay}, collusion="all"))
     b = synthetic_batches(2, 8, (1, 28, 28), 10, "cpu", seed=rank)
     eng.step(b)   # warm-up (process groups connect)
     t0 = time.time()
@@ -47,14 +56,14 @@ def _worker(rank, world, port, outdir, quorum, delay):
         quorums.append(eng.last_quorum)
     elapsed = time.time() - t0
     eng.finish()
-    torch.save({"flat": eng.flat_model().clone(), "t": elapsed, "q": quorums, "skipped": eng.skipped},
+    torch.save({"flat": eng.flat_model().clone(), "t": elapsed, "q": quorums, "skipped": eng.skipped, "w": eng.last_weights},
                os.path.join(outdir, f"r{rank}.pt"))
     shutdown(ctx)
 
 
-def _run(quorum, delay):
+def _run(quorum, delay, *extra):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(3, free_port(), d, quorum, delay), nprocs=3, join=True)
+        mp.spawn(_worker, args=(3, free_port(), d, quorum, delay, *extra), nprocs=3, join=True)
         return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(3)]
 
 
@@ -75,3 +84,19 @@ def test_full_quorum_waits_for_everyone_and_matches():
     assert all(q == [0, 1, 2] for q in out[0]["q"])
     assert out[0]["t"] >= STEPS * 0.2 * 0.9
     assert torch.equal(out[0]["flat"], out[2]["flat"])
+
+
+def test_colluding_attacker_with_straggler_keeps_replicas_identical():
+    """A lie (colluding) slot + a straggler outside the quorum: the attack runs on a copy of
+    the chosen rows, so the straggler, which receives the rows late, attacks the same
+    honest rows and every replica applies the same update."""
+    out = _run(2, 0.5, {1: "lie", 4: "empire"})
+    assert torch.equal(out[0]["flat"], out[1]["flat"]) and torch.equal(out[0]["flat"], out[2]["flat"])
+
+
+def test_full_quorum_equals_the_synchronous_engine():
+    """Quorum rows in slot order (j * world + r): with every rank in the quorum, Krum picks
+    and weighs exactly what the synchronous engine does."""
+    q = _run(3, 0.0, {1: "reverse"}, "krum")
+    s = _run(3, 0.0, {1: "reverse"}, "krum", True)
+    assert torch.equal(q[0]["flat"], s[0]["flat"])

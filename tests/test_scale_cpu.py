@@ -1,0 +1,187 @@
+"""Multi-rank rehearsals of the default multi-GPU path (sharded, bucketed aggregation)
+on gloo/CPU at 4 and 8 ranks: every rank runs what ``bench.py --gpus N`` runs on N
+MI355X (one process per device), with CPU tensors.
+
+* 8 ranks x 2 workers (n = 16): sharded == redundant (all-gather) aggregation,
+  BITWISE, for every distance-based and coordinate-wise rule, with a colluding
+  ``lie`` attacker and a ``reverse`` one; every replica's checksum equal;
+* 8 ranks x 8 grouped ResNet workers (n = 64): shard_pad(8), the three layer
+  buckets and the n = 64 Krum selection of the flagship configuration;
+* the exchange leaves in ONE ``all_to_all_single`` per bucket.
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import torch.nn.functional as F
+
+from garfield_amd.models import build_model
+from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synthetic_batches
+
+RULES = [("krum", 2), ("bulyan", 2), ("median", 2), ("trimmed-mean", 2), ("brute", 2), ("aksel", 2)]
+BYZ = {3: "lie", 12: "reverse"}
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from garfield_amd.parallel.comm import init_distributed
+
+    return init_distributed(backend="gloo", device="cpu")
+
+
+def _rules_worker(rank, world, port, outdir, shard):
+    from garfield_amd.parallel.comm import shutdown
+
+    ctx = _init(rank, world, port)
+    out = {}
+    for rule, f in RULES:
+        torch.manual_seed(0)
+        eng = RobustDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                                 EngineConfig(gar=rule, f=f, workers_per_rank=2, byzantine=BYZ, shard_gar=shard,
+                                              lr=0.05, collusion="all"))
+        assert (eng._shard is not None) == shard
+        b = synthetic_batches(2, 8, (1, 28, 28), 10, "cpu", seed=rank)
+        for _ in range(2):
+            eng.step(b)
+        out[rule] = {"flat": eng.flat_model().clone(), "sum": eng.replica_checksum()}
+    torch.save(out, os.path.join(outdir, f"{int(shard)}r{rank}.pt"))
+    shutdown(ctx)
+
+
+def test_eight_rank_sharded_equals_redundant_bitwise():
+    world = 8
+    with tempfile.TemporaryDirectory() as d:
+        for shard in (False, True):
+            mp.spawn(_rules_worker, args=(world, free_port(), d, shard), nprocs=world, join=True)
+        res = {(s, r): torch.load(os.path.join(d, f"{s}r{r}.pt"), weights_only=True)
+               for s in (0, 1) for r in range(world)}
+        for rule, _ in RULES:
+            ref = res[(0, 0)][rule]
+            for s in (0, 1):
+                for r in range(world):
+                    got = res[(s, r)][rule]
+                    assert got["sum"] == ref["sum"], (rule, s, r)
+                    assert torch.equal(got["flat"], ref["flat"]), (rule, s, r)
+
+
+def _grouped_worker(rank, world, port, outdir, shard, k):
+    from garfield_amd.parallel.comm import shutdown
+
+    ctx = _init(rank, world, port)
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, ctx,
+                             EngineConfig(gar="krum", f=2, workers_per_rank=k, byzantine={5: "reverse", 9: "lie"},
+                                          shard_gar=shard, worker_batching=True, autocast_dtype=None,
+                                          exchange_dtype=torch.float32, lr=0.01))
+    assert eng._gexec is not None and (eng._shard is not None) == shard
+    if shard:
+        assert len(eng._shard.buckets) == 3 and eng.ld % (64 * world) == 0
+    calls = []
+    if shard:
+        import torch.distributed as dist
+
+        orig = dist.all_to_all_single
+
+        def counting(*a, **kw):
+            calls.append(1)
+            return orig(*a, **kw)
+
+        dist.all_to_all_single = counting
+    b = synthetic_batches(k, 2, (3, 16, 16), 10, "cpu", seed=rank)
+    steps = 2
+    for _ in range(steps):
+        eng.step(b)
+    torch.save({"flat": eng.flat_model().clone(), "sum": eng.replica_checksum(), "a2a": len(calls),
+                "w": eng.last_weights, "n": eng.n}, os.path.join(outdir, f"{int(shard)}r{rank}.pt"))
+    shutdown(ctx)
+
+
+@pytest.mark.parametrize("world,k", [(4, 4), (8, 8)])
+def test_grouped_sharded_flagship_path(world, k):
+    """ResNet worker batching + sharded bucketed Krum at 4 x 4 (n = 16) and 8 x 8 (n = 64)
+    ranks x workers: replicas identical, sharded == redundant, 3 all_to_all per step."""
+    with tempfile.TemporaryDirectory() as d:
+        for shard in (False, True):
+            mp.spawn(_grouped_worker, args=(world, free_port(), d, shard, k), nprocs=world, join=True)
+        res = {(s, r): torch.load(os.path.join(d, f"{s}r{r}.pt"), weights_only=True)
+               for s in (0, 1) for r in range(world)}
+        ref = res[(0, 0)]
+        assert ref["n"] == world * k
+        for s in (0, 1):
+            for r in range(world):
+                got = res[(s, r)]
+                assert got["sum"] == res[(s, 0)]["sum"], (s, r)
+                assert torch.equal(got["flat"], res[(s, 0)]["flat"]), (s, r)
+        assert all(res[(1, r)]["a2a"] == 3 * 2 for r in range(world))   # one all_to_all per bucket and step
+        assert all(torch.equal(res[(1, r)]["w"], res[(1, 0)]["w"]) for r in range(world))   # one Krum selection
+        rel = ((res[(1, 0)]["flat"] - ref["flat"]).norm() / ref["flat"].norm()).item()
+        assert rel < 1e-5, rel
+
+
+def _byzps_worker(rank, world, port, outdir, num_ps):
+    import torch.distributed as dist
+
+    from garfield_amd.parallel.byzps import ByzantinePSDataParallel, ByzPSConfig
+    from garfield_amd.parallel.comm import shutdown
+
+    ctx = _init(rank, world, port)
+    torch.manual_seed(0)
+    eng = ByzantinePSDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                                  ByzPSConfig(gar="median", f=1, workers_per_rank=2, num_ps=num_ps, fps=1 if num_ps > 2
+                                              else 0, mar="median", byzantine={5: "reverse"}, lr=0.05))
+    moved = []
+    names = ("broadcast", "all_gather_into_tensor", "all_gather", "all_reduce", "all_to_all_single")
+    orig = {k: getattr(dist, k) for k in names}
+
+    def counting(name):
+        def f(t, *a, **kw):
+            moved.append(t.numel() * t.element_size() if isinstance(t, torch.Tensor) else
+                         sum(x.numel() * x.element_size() for x in t))
+            return orig[name](t, *a, **kw)
+        return f
+
+    inner = eng._exchange_models
+
+    def patched():
+        for k in names:
+            setattr(dist, k, counting(k))
+        try:
+            inner()
+        finally:
+            for k in names:
+                setattr(dist, k, orig[k])
+
+    eng._exchange_models = patched
+    b = synthetic_batches(2, 8, (1, 28, 28), 10, "cpu", seed=rank)
+    for _ in range(2):
+        eng.step(b)
+    torch.save({"bytes": sum(moved) / 2, "d": eng.d, "ld": eng.ld, "flat": eng.flat_model().clone()},
+               os.path.join(outdir, f"r{rank}.pt"))
+    shutdown(ctx)
+
+
+@pytest.mark.parametrize("num_ps", [1, 3])
+def test_byzantine_server_model_exchange_moves_only_server_rows(num_ps):
+    """The model exchange of the Byzantine-server mode moves <= num_ps x d x 4 bytes per rank
+    and step (the server rows only, never M[world, ld]); honest replicas stay identical."""
+    world = 5
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_byzps_worker, args=(world, free_port(), d, num_ps), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    for r in res:
+        assert 0 < r["bytes"] <= num_ps * r["ld"] * 4, (r["bytes"], num_ps * r["ld"] * 4)
+    honest = res[1:] if num_ps > 2 else res   # rank 0 is the Byzantine server when fps = 1
+    assert all(torch.equal(r["flat"], honest[-1]["flat"]) for r in honest)
