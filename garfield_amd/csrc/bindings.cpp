@@ -1098,6 +1098,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("events"), py::arg("inline_") = true,
         "Make the nodes that follow each marker kernel (signal word words[i]) wait for events[i] (event-wait "
         "node); returns the number of marker nodes found");
+  m.def("signal_add", [](int64_t p, int64_t stream) {
+    garfield::gpu::signal_add(reinterpret_cast<void*>(p), reinterpret_cast<hipStream_t>(stream));
+    TORCH_CHECK(hipGetLastError() == hipSuccess, "garfield: signal_add launch failed");
+  }, py::arg("ptr"), py::arg("stream"), "1-lane kernel: counter word += 1 (system-scope release)");
+  m.def("wait_geq", [](int64_t p, int64_t target, int64_t timeout_us, int64_t err, int64_t stream) {
+    garfield::gpu::wait_geq(reinterpret_cast<const void*>(p), static_cast<uint64_t>(target),
+                            static_cast<uint64_t>(timeout_us), reinterpret_cast<void*>(err),
+                            reinterpret_cast<hipStream_t>(stream));
+    TORCH_CHECK(hipGetLastError() == hipSuccess, "garfield: wait_geq launch failed");
+  }, py::arg("ptr"), py::arg("target"), py::arg("timeout_us"), py::arg("err"), py::arg("stream"),
+     "1-lane kernel on `stream`: wait until the counter word >= target (bounded by timeout_us; a miss "
+     "increments err[0])");
   m.def("signal_alloc", &signal_alloc, py::arg("count"));
   m.def("signal_free", &signal_free);
   m.def("signal_wait_supported", &signal_wait_supported, py::arg("device"));

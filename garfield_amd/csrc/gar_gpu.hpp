@@ -96,6 +96,10 @@ int flatten_cast(const void* const* srcs, const int* src_dts, const int64_t* num
 void signal_set(void* p, uint64_t value, hipStream_t stream);
 // host stub of the signal kernel (identifies its nodes in a captured graph)
 const void* signal_kernel();
+// counter signals: k_signal_add (+1, release) and a bounded device-side wait (>= target)
+const void* signal_add_kernel();
+void signal_add(void* p, hipStream_t stream);
+void wait_geq(const void* p, uint64_t target, uint64_t timeout_us, void* err, hipStream_t stream);
 
 }  // namespace gpu
 }  // namespace garfield

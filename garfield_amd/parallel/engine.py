@@ -688,6 +688,7 @@ class RobustDataParallel:
             self._capture_grouped()
         if self._ggraph is not None:
             self._ggraph.replay()
+            self._gexec.replayed()   # the bucket signals captured in the graph fired once more
         else:
             self._gexec.run(self._gx, self._gy, self._gloss)
 
@@ -771,23 +772,16 @@ class RobustDataParallel:
             with torch.cuda.stream(s):  # warm-up on the capture stream (per-stream library state)
                 self._gexec.run(self._gx, self._gy, self._gloss)
             s.synchronize()
-            marks = self._gexec.mark_events() or []
-            g = torch.cuda.CUDAGraph(keep_graph=bool(marks))
+            g = torch.cuda.CUDAGraph()
             mode = "thread_local" if self.world > 1 else "global"
             with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
                 self._gexec.run(self._gx, self._gy, self._gloss)
-            if marks:   # bucket marks: event-record nodes behind the captured marker kernels
-                from garfield_amd.parallel.grouped import GraphSignal
-
-                GraphSignal.attach(g, marks)
-                g.instantiate()
             torch.cuda.current_stream(self.device).wait_stream(s)
             self._ggraph = g
         except Exception as e:  # capture unsupported: stay eager
             warning(f"HIP graph capture of the grouped step failed, running eagerly: {e!r}")
             self._graph_failed = True
             self._ggraph = None
-        self._gexec.reset_marks(torch.cuda.current_stream(self.device))   # the warm-up pass set them
         torch.cuda.synchronize()
         with torch.no_grad():  # the warm-up pass must not count as an extra step of the running statistics
             for m, (rm, rv) in zip(bns, saved):

@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
+from garfield_amd.parallel.signals import DeviceSignal
 from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, grouped_bn,
                                       WgradStream, grouped_conv, grouped_cross_entropy, grouped_linear,
                                       grouped_maxpool)
@@ -64,18 +65,20 @@ class GroupedResNet:
         self.bn: dict = {}
         self._seed = None
         self.join_residuals = True
-        # bucket marks: the backward records an event when it has produced every
+        # bucket marks: the backward records a device signal when it has produced every
         # gradient of the named layer and the layers after it (the exchange of that
-        # bucket can start). External events: inside a captured HIP graph they become
-        # event-record nodes that each replay records.
+        # bucket can start), and one more at the very end (the last bucket). Inside the
+        # captured HIP graph each is a 1-lane counter kernel that fires on every replay
+        # (parallel/signals.py: no HIP event, so no cross-stream dependency on the main
+        # stream).
         self.marks = tuple(marks)
         self._offsets = offsets or {}
         self._events = None
+        self._end = None
         if signals and self.marks and next(model.parameters()).is_cuda:   # else the marks only cut buckets
             dev = next(model.parameters()).device
-            sig = {name: GraphSignal(dev) for name in self.marks}
-            if all(x.available() for x in sig.values()):
-                self._events = sig
+            self._events = {name: DeviceSignal(dev) for name in self.marks}
+            self._end = DeviceSignal(dev)
 
     def bucket_offsets(self) -> list:
         """Flat offset where each marked layer's parameters start (bucket boundaries)."""
@@ -88,15 +91,16 @@ class GroupedResNet:
         return out
 
     def mark_events(self):
-        """Signals in the order the backward records them (= the marks' order), or None."""
+        """Signals in the order the backward records them (the marks' order, then the end of
+        the backward), or None."""
         if self._events is None:
             return None
-        return [self._events[name] for name in self.marks]
+        return [self._events[name] for name in self.marks] + [self._end]
 
-    def reset_marks(self, stream) -> None:
-        if self._events is not None:
-            for sgn in self._events.values():
-                sgn.reset(stream)
+    def replayed(self) -> None:
+        """One replay of a captured run(): every signal fired once more."""
+        for sgn in self.mark_events() or ():
+            sgn.replayed()
 
     # ------------------------------------------------------------------ #
 
@@ -178,76 +182,16 @@ class GroupedResNet:
         if x.is_cuda:
             WgradStream.join(x.device)   # weight gradients computed on the side stream
         self.sink.flush()
+        if self._end is not None:
+            self._end.record(torch.cuda.current_stream(x.device))
         per = per.detach()
         if loss_out is not None:
             loss_out.copy_(per)
         return per
 
 
-class GraphSignal:
-    """A point inside the step's HIP graph that another stream can wait for.
-
-    Eagerly, ``record(stream)`` records a HIP event. During capture it launches a
-    1-thread marker kernel instead (HIP rejects external event records during
-    capture, and torch refuses ``Event(external=True)`` on ROCm); after capture
-    ``attach(graph)`` finds the marker node in the raw ``hipGraph_t`` and splices an
-    event-record node in behind it (``bindings.cpp:graph_attach_record_events``),
-    so every replay records the same event at that point. ``wait_on(stream)`` is
-    then a plain ``hipStreamWaitEvent``.
-
-    Measured on MI355X (``scripts/probe_graph_events.py``,
-    ``profiles/r3/probe_graph_events.log``): the spliced record fires at its point
-    (0.85 ms into a 2.5 ms graph), and each event node costs ~40 us of device time
-    per replay (a marker kernel alone: ~1.4 us). A command-processor value wait
-    (``hipStreamWaitValue64``, the previous mechanism) measured ~450 us per wait."""
-
-    def __init__(self, device: torch.device):
-        from garfield_amd import _native
-
-        self._C = _native.native()
-        self.word = self._C.signal_alloc(1)      # the marker kernel's target (never waited on)
-        self.event = self._C.event_create()
-
-    def available(self) -> bool:
-        return self.word != 0
-
-    def record(self, stream) -> None:
-        if torch.cuda.is_current_stream_capturing():
-            self._C.signal_set(self.word, 1, stream.cuda_stream)
-        else:
-            self._C.event_record(self.event, stream.cuda_stream)
-
-    def wait_on(self, stream) -> None:
-        self._C.event_wait(stream.cuda_stream, self.event)
-
-    @staticmethod
-    def attach(graph: "torch.cuda.CUDAGraph", signals) -> None:
-        """Splice an event-record node behind each signal's marker kernel of ``graph``
-        (captured with ``keep_graph=True``, not yet instantiated)."""
-        signals = list(signals)
-        if not signals:
-            return
-        C = signals[0]._C
-        found = C.graph_attach_record_events(graph.raw_cuda_graph(), [s.word for s in signals],
-                                             [s.event for s in signals], True)
-        if found < len(signals):
-            raise RuntimeError(f"graph has {found} marker kernels, expected {len(signals)}")
-
-    def reset(self, stream) -> None:
-        """Nothing to re-arm: an event wait matches the latest record."""
-
-    def __del__(self):
-        try:
-            if self.word:
-                self._C.signal_free(self.word)
-            if self.event:
-                self._C.event_destroy(self.event)
-        except Exception:
-            pass
-
-
 class _BucketMark(torch.autograd.Function):
-    """Identity whose backward records ``event`` (a GraphSignal) on the current stream:
+    """Identity whose backward records ``event`` (a DeviceSignal) on the current stream:
     by then the backward has produced every gradient of the layers after this point
     (the split-K weight-gradient sums queued so far are flushed first, so the
     bucket's rows are complete when the event fires)."""

@@ -15,11 +15,13 @@ squared distances, and squared distances are additive over coordinate blocks:
    each bucket is cut into ``world`` equal shards and rank r owns shard r of
    every bucket;
 2. a bucket is exchanged as soon as the backward has written it: the grouped
-   executor records an event when its backward crosses the bucket boundary
-   (an external event node inside the HIP graph), a side stream waits on it,
-   applies the simulated attacks to that slice and issues one zero-copy
-   ``all_to_all_single`` per local worker row (row slice in, ``[world, S_b]``
-   out) -- so most of the exchange runs under the rest of the backward;
+   executor's captured graph bumps a device-side counter when its backward crosses
+   the bucket boundary (``parallel/signals.py``), a comm stream waits for it ON THE
+   DEVICE, applies the simulated attacks to that slice, packs the k local rows as
+   ``[dst, worker, shard]`` and sends the whole bucket in ONE ``all_to_all_single``
+   -- so most of the exchange runs under the rest of the backward (every collective
+   of the step is issued from the comm stream: a HIP event dependency on the main
+   stream would slow the next graph replay, see signals.py);
 3. distance-based rules (Krum/Multi-Krum, Bulyan's selection, Brute): each rank
    adds the partial Gram matrices of its shards (split-K MFMA kernel, one per
    bucket as it lands), the ``[n, n]`` partials are all-gathered (a few KB) and
@@ -29,8 +31,9 @@ squared distances, and squared distances are additive over coordinate blocks:
    bucket on the owned shard (fp32 master shard, momentum shard: optimizer state
    is sharded) and write the bf16 working weights of the shard in the same pass;
 5. the updated bf16 working weights are all-gathered per bucket (2 bytes per
-   parameter, not the 4-byte fp32 master); the few fp32 parameters the
-   forward reads directly (BatchNorm affine) travel in one small all-reduce.
+   parameter, not the 4-byte fp32 master), each as soon as its bucket's update is
+   queued (low coordinates first); the few fp32 parameters the forward reads
+   directly (BatchNorm affine) travel in one small all-reduce.
    The fp32 master outside the owned shards is refreshed lazily
    (``sync_master``) for checkpoints and the reference-layout flat vector.
 
@@ -42,6 +45,7 @@ index, so its mask differs from the unsharded run's (same Bernoulli(p) law).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 
@@ -52,6 +56,7 @@ from garfield_amd import _native
 from garfield_amd.ops import gar
 from garfield_amd.ops import reference as ref
 from garfield_amd.parallel.comm import gloo_backend
+from garfield_amd.parallel.signals import Handoff
 
 DISTANCE_RULES = {"krum", "brute", "bulyan"}
 SUPPORTED = DISTANCE_RULES | {"average", "aksel", "median", "trimmed-mean", "averaged-median", "average-nan",
@@ -65,13 +70,10 @@ def shard_pad(world: int, base: int = 64) -> int:
 
 def overlap_enabled(world: int = 1) -> bool:
     """Whether each bucket's exchange starts INSIDE the step's backward: the grouped
-    executor records an event when the backward has written a bucket (an event-record
-    node spliced into the captured HIP graph, ``grouped.GraphSignal``), and the comm
-    stream waits for it. Each such node costs ~40 us of device time per replay on
-    MI355X (``profiles/r3/probe_graph_events.log``), so the default
-    (``GARFIELD_OVERLAP`` unset) is on only when there is something to overlap
-    (world > 1); ``GARFIELD_OVERLAP=1`` forces it (e.g. the world-1 loopback
-    exchange), ``0`` disables it."""
+    executor's captured graph carries a device-side counter signal per bucket mark
+    (``parallel/signals.py``) and the comm stream waits for it on the device. On by
+    default when there is something to overlap (world > 1); ``GARFIELD_OVERLAP=1``
+    forces it (e.g. the world-1 loopback exchange), ``0`` disables it."""
     v = os.environ.get("GARFIELD_OVERLAP", "")
     if v == "":
         return world > 1
@@ -128,10 +130,15 @@ class ShardedAggregator:
         self._started = False
         self._gathers: list = []
         self.master_stale = False
-        self._comm_stream = None
-        if dev.type == "cuda":
-            self._comm_stream = (torch.cuda.Stream(dev) if os.environ.get("GARFIELD_COMM_STREAM", "1") != "0"
-                                 else torch.cuda.current_stream(dev))
+        # every collective of the step is issued from the comm stream (so RCCL's internal
+        # stream depends on it, never on the main stream: parallel/signals.py), which
+        # follows the main stream through device-side hand-offs
+        # (world 1 without the loopback exchange: nothing to overlap, and a second active
+        # queue alone costs the main stream's graph ~4-5 % (profiles/r3/probe_cross_stream.log):
+        # everything stays on the main stream)
+        side = dev.type == "cuda" and (self.world > 1 or loopback_enabled() or overlap_enabled(self.world))
+        self._comm_stream = torch.cuda.Stream(dev) if side else None
+        self._handoff = Handoff(dev) if side else None
         self._init_fp32_sync()
 
     # ------------------------------------------------------------------ #
@@ -170,6 +177,20 @@ class ShardedAggregator:
     # ------------------------------------------------------------------ #
     # exchange
 
+    @contextlib.contextmanager
+    def _on_comm(self):
+        """Make the comm stream current, after everything the main stream has queued so far
+        (device-side hand-off). Collectives issued inside run after that work and leave the
+        main stream free of cross-stream dependencies; ``work.wait()`` outside (main
+        stream current) brings their results back."""
+        if self._comm_stream is None:
+            yield
+            return
+        main = torch.cuda.current_stream(self.e.device)
+        self._handoff.to_comm(main, self._comm_stream)
+        with torch.cuda.stream(self._comm_stream):
+            yield
+
     def start_exchange(self, events=None) -> None:
         """Issue every bucket's exchange, in ready order: the simulated attacks on the
         bucket's slice of the local rows, one pack of the k rows into ``send[dst, j]``
@@ -178,17 +199,16 @@ class ShardedAggregator:
         i's rows are complete; the comm stream waits on it, so the exchange overlaps
         the rest of the backward."""
         e = self.e
-        cuda = e.device.type == "cuda"
-        main = torch.cuda.current_stream(e.device) if cuda else None
-        use_events = events is not None and overlap_enabled(self.world)
+        side = self._comm_stream is not None
+        use_events = (side and events is not None and overlap_enabled(self.world)
+                      and len(events) >= len(self.buckets))
+        if side and not use_events:   # after the whole backward
+            self._handoff.to_comm(torch.cuda.current_stream(e.device), self._comm_stream)
         for i, b in enumerate(self.buckets):
-            if cuda:
+            if side:
                 s = self._comm_stream
-                ev = events[i] if (use_events and i < len(events)) else None
-                if ev is not None:
-                    ev.wait_on(s)      # a point inside the step's graph (grouped.GraphSignal)
-                elif _XS in ("both", "c_waits_main"):
-                    s.wait_stream(main)
+                if use_events:
+                    events[i].wait_on(s)      # a point inside the step's graph (signals.DeviceSignal)
                 ctx = torch.cuda.stream(s)
             else:
                 ctx = _nullctx()
@@ -199,12 +219,12 @@ class ShardedAggregator:
                 if self.world > 1:
                     b.send.copy_(local)
                     b.works.append(dist.all_to_all_single(b.recv.view(-1), b.send.view(-1), async_op=True))
-                elif cuda and loopback_enabled():   # world 1: emulate the transfer (traces / tests)
+                elif side and loopback_enabled():   # world 1: emulate the transfer (traces / tests)
                     if b.recv is None:
                         b.recv = torch.empty((1, self.k, b.S), dtype=e.X.dtype, device=e.device)
                         b.rows = [b.recv[0, j] for j in range(self.k)]
                     b.recv.copy_(local)
-                if cuda:
+                if side:
                     b.done = torch.cuda.Event(enable_timing=_TIMING)
                     b.done.record(s)
         self._started = True
@@ -213,24 +233,29 @@ class ShardedAggregator:
         for w in b.works:
             w.wait()
         b.works = []
-        if self.e.device.type == "cuda" and _XS in ("both", "main_waits_c"):
-            torch.cuda.current_stream(self.e.device).wait_event(b.done)
+        if b.done is not None:
+            torch.cuda.current_stream(self.e.device).wait_event(b.done)   # main waits on comm: cheap
         self.e._collude(b.rows)   # colluding attacks on this rank's coordinate shard of every row
 
     def _sum_over_ranks(self, t: torch.Tensor) -> torch.Tensor:
         """Every rank's ``t`` summed in rank order (identical result on every rank)."""
         if self.world == 1:
             return t.clone()
-        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1))
-        return out.sum(0)
+        return self._gather_ranks(t).sum(0)
 
     def _concat_ranks(self, t: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
             return t
+        return self._gather_ranks(t).view(-1, *t.shape[1:])
+
+    def _gather_ranks(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape]: every rank's t (a small all-gather issued from the comm stream)."""
         out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1))
-        return out.view(-1, *t.shape[1:])
+        src = t.contiguous().view(-1)
+        with self._on_comm():
+            work = dist.all_gather_into_tensor(out.view(-1), src, async_op=True)
+        work.wait()
+        return out
 
     # ------------------------------------------------------------------ #
 
@@ -257,7 +282,8 @@ class ShardedAggregator:
         full, mine = buf[b.lo:b.hi], buf[b.own]
         if gloo_backend():
             mine = mine.clone()  # gloo rejects an input aliasing the output
-        self._gathers.append(dist.all_gather_into_tensor(full, mine, async_op=True))
+        with self._on_comm():
+            self._gathers.append(dist.all_gather_into_tensor(full, mine, async_op=True))
 
     def _finish_gathers(self) -> None:
         """Wait (stream-ordered on RCCL) for the weight all-gathers, then exchange the compact
@@ -277,7 +303,9 @@ class ShardedAggregator:
                 nb = self._np_buf
                 nb.zero_()
                 nb[self._np_own_pos] = e.flat.data[self._np_own_idx]
-                dist.all_reduce(nb)
+                with self._on_comm():
+                    work = dist.all_reduce(nb, async_op=True)
+                work.wait()
                 e.flat.data[self._np_idx] = nb
 
     def sync_master(self) -> None:
@@ -593,7 +621,6 @@ class _nullctx:
 # GARFIELD_EXCHANGE_TIMING=1: the per-bucket "exchange issued" events are timing events
 # (scripts/overlap_timing.py reads them against the step's start and its backward's end)
 _TIMING = os.environ.get("GARFIELD_EXCHANGE_TIMING", "0") == "1"
-_XS = os.environ.get("GARFIELD_XS_DEBUG", "both")   # DEBUG: which cross-stream waits to keep
 
 
 def loopback_enabled() -> bool:

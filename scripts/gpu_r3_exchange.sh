@@ -26,6 +26,11 @@ for i in 1 2; do
   run shard_loop_noov_$i --shard-gar GARFIELD_LOOPBACK_EXCHANGE=1 GARFIELD_OVERLAP=0
   run shard_noloop_$i --shard-gar GARFIELD_OVERLAP=0
 done
+for v in 1 0; do
+  GARFIELD_LOOPBACK_EXCHANGE=1 GARFIELD_OVERLAP=$v timeout -k 10 300 python scripts/overlap_timing.py --steps 3 \
+      > $O/overlap_$v.log 2>&1 || { echo "overlap $v failed"; tail -20 $O/overlap_$v.log; exit 1; }
+  echo "overlap=$v $(grep '^{' $O/overlap_$v.log)"
+done
 if [ -n "$PROFILE" ]; then
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
   GARFIELD_LOOPBACK_EXCHANGE=1 GARFIELD_OVERLAP=1 GARFIELD_TRACE_MARK=1 timeout -k 10 300 \

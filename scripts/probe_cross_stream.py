@@ -111,6 +111,45 @@ def main():
             with torch.cuda.stream(side):
                 tiny.add_(1)
 
+    cnt_t = torch.zeros(2, dtype=torch.int64, device=dev)   # [counter, miss count] in device memory
+    cnt, err = cnt_t.data_ptr(), cnt_t.data_ptr() + 8
+    st = {"n": 0}
+
+    def v_device_flag():           # main: +1 marker after the graph; side: bounded device-side wait
+        g.replay()
+        C.signal_add(cnt, cur.cuda_stream)
+        st["n"] += 1
+        C.wait_geq(cnt, st["n"], 2_000_000, err, side.cuda_stream)
+        with torch.cuda.stream(side):
+            tiny.add_(1)
+
+    wv = C.signal_alloc(1)
+    st2 = {"n": 0}
+
+    def v_cp_value_wait():         # main: marker sets a value; side: command-processor wait
+        st2["n"] += 1
+        g.replay()
+        C.signal_set(wv, st2["n"], cur.cuda_stream)
+        C.stream_wait_value(side.cuda_stream, wv, st2["n"])
+        with torch.cuda.stream(side):
+            tiny.add_(1)
+
+    def v_side_sleep():           # an unrelated 1-wave kernel running on the side stream meanwhile
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(2_000_000)
+        g.replay()
+        cur.wait_stream(side)
+
+    def v_side_sleep_after():     # the same kernel, but queued after the graph on the main stream
+        g.replay()
+        torch.cuda._sleep(2_000_000)
+
+    variant("side_sleep_concurrent", v_side_sleep, iters=10)
+    variant("sleep_serial", v_side_sleep_after, iters=10)
+    variant("device_flag", v_device_flag)
+    variant("cp_value_wait", v_cp_value_wait)
+    torch.cuda.synchronize()
+    res["device_flag_misses"] = int(cnt_t[1])
     for name, fn in (("scope0_system", v_scoped(0)), ("scope1_device", v_scoped(1)), ("scope2_nofence", v_scoped(2)),
                      ("record_no_waiter", v_record_no_waiter), ("wait_every_5th", v_wait_once_then_plain)):
         variant(name, fn)
