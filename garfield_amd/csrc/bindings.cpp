@@ -1083,7 +1083,63 @@ int64_t graph_attach_wait_events(int64_t graph, const std::vector<int64_t>& word
   return static_cast<int64_t>(marks.size());
 }
 
+namespace garfield {
+namespace rccl {
+bool load(const std::string& path);
+void all_to_all(int64_t comm, const void* send, void* recv, size_t count, int dtype, hipStream_t stream);
+void all_gather(int64_t comm, const void* send, void* recv, size_t count, int dtype, hipStream_t stream);
+void all_reduce_sum(int64_t comm, const void* send, void* recv, size_t count, int dtype, hipStream_t stream);
+}  // namespace rccl
+}  // namespace garfield
+
+namespace {
+int nccl_dtype(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kBFloat16: return 9;
+    case at::kFloat: return 7;
+    case at::kHalf: return 6;
+    case at::kDouble: return 8;
+    case at::kLong: return 4;
+    case at::kInt: return 2;
+    default: TORCH_CHECK(false, "garfield rccl: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+void rccl_check(const at::Tensor& a, const at::Tensor& b, int64_t need_b) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.device() == b.device(), "garfield rccl: GPU tensors on one device");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous(), "garfield rccl: contiguous tensors");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), "garfield rccl: one dtype");
+  TORCH_CHECK(b.numel() == need_b, "garfield rccl: output has ", b.numel(), " elements, expected ", need_b);
+}
+}  // namespace
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("rccl_load", &garfield::rccl::load, py::arg("path"),
+        "Bind torch's librccl instance (dlopen RTLD_NOLOAD) for the direct collectives; False if not found");
+  m.def("rccl_all_to_all", [](int64_t comm, const at::Tensor& send, const at::Tensor& recv, int64_t world,
+                              int64_t stream) {
+    rccl_check(send, recv, send.numel());
+    TORCH_CHECK(send.numel() % world == 0, "garfield rccl: all_to_all input not divisible by world");
+    garfield::rccl::all_to_all(comm, send.data_ptr(), recv.data_ptr(), static_cast<size_t>(send.numel() / world),
+                               nccl_dtype(send), reinterpret_cast<hipStream_t>(stream));
+  }, py::arg("comm"), py::arg("send"), py::arg("recv"), py::arg("world"), py::arg("stream"),
+     "ncclAllToAll on `stream` (no cross-stream events): chunk r of send goes to rank r, chunk r of recv comes "
+     "from rank r");
+  m.def("rccl_all_gather", [](int64_t comm, const at::Tensor& send, const at::Tensor& recv, int64_t world,
+                              int64_t stream) {
+    TORCH_CHECK(send.is_cuda() && recv.is_cuda() && recv.is_contiguous() && send.is_contiguous(),
+                "garfield rccl: contiguous GPU tensors");
+    TORCH_CHECK(recv.numel() == send.numel() * world && send.scalar_type() == recv.scalar_type(),
+                "garfield rccl: all_gather output must be world x input");
+    garfield::rccl::all_gather(comm, send.data_ptr(), recv.data_ptr(), static_cast<size_t>(send.numel()),
+                               nccl_dtype(send), reinterpret_cast<hipStream_t>(stream));
+  }, py::arg("comm"), py::arg("send"), py::arg("recv"), py::arg("world"), py::arg("stream"),
+     "ncclAllGather on `stream` (in place when send is recv's own rank block)");
+  m.def("rccl_all_reduce_sum", [](int64_t comm, const at::Tensor& send, const at::Tensor& recv, int64_t stream) {
+    rccl_check(send, recv, send.numel());
+    garfield::rccl::all_reduce_sum(comm, send.data_ptr(), recv.data_ptr(), static_cast<size_t>(send.numel()),
+                                   nccl_dtype(send), reinterpret_cast<hipStream_t>(stream));
+  }, py::arg("comm"), py::arg("send"), py::arg("recv"), py::arg("stream"), "ncclAllReduce(sum) on `stream`");
   m.def("event_create", &event_create, py::arg("scope") = 1,
         "HIP event (no timing); scope 0: system-scope release on record (HIP default), 1: device-scope "
         "release (enough for other streams of this device), 2: no system fence");

@@ -33,7 +33,7 @@ HIP_SOURCES = [
     "gar_coord_m3.hip", "gar_coord_m4.hip", "gar_coord_m5.hip",
     "bn_nhwc.hip", "im2col_nhwc.hip", "iconv_nhwc.hip", "gemm_nt.hip", "data_aug.hip", "gar_large.hip", "loss_xent.hip", "stream_signal.hip",
 ]
-TORCH_SOURCES = ["bindings.cpp", "mailbox.cpp"]   # need torch + HIP headers
+TORCH_SOURCES = ["bindings.cpp", "mailbox.cpp", "rccl_direct.cpp"]   # need torch + HIP headers
 PLAIN_SOURCES = ["threadpool.cpp", "gar_cpu.cpp"]  # plain C++17
 
 
@@ -122,7 +122,7 @@ def build(verbose: bool = False, force: bool = False) -> Path:
     if force or todo or not out.exists() or any(Path(o).stat().st_mtime > out.stat().st_mtime for o in objs):
         link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", str(out),
                 f"-L{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
-                f"-L{ROCM / 'lib'}", "-lamdhip64", "-pthread",
+                f"-L{ROCM / 'lib'}", "-lamdhip64", "-pthread", "-ldl",
                 f"-Wl,-rpath,{libdir}", f"-Wl,-rpath,{ROCM / 'lib'}"]
         _run(link, verbose)
     return out

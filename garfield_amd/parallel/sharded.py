@@ -56,6 +56,7 @@ from garfield_amd import _native
 from garfield_amd.ops import gar
 from garfield_amd.ops import reference as ref
 from garfield_amd.parallel.comm import gloo_backend
+from garfield_amd.parallel.rccl import DirectRCCL
 from garfield_amd.parallel.signals import Handoff
 
 DISTANCE_RULES = {"krum", "brute", "bulyan"}
@@ -139,6 +140,8 @@ class ShardedAggregator:
         side = dev.type == "cuda" and (self.world > 1 or loopback_enabled() or overlap_enabled(self.world))
         self._comm_stream = torch.cuda.Stream(dev) if side else None
         self._handoff = Handoff(dev) if side else None
+        # RCCL kernels straight onto the comm stream (rccl.py); None: torch.distributed
+        self._rccl = DirectRCCL.create() if (side and self.world > 1) else None
         self._init_fp32_sync()
 
     # ------------------------------------------------------------------ #
@@ -218,7 +221,10 @@ class ShardedAggregator:
                 local = e.X[:, 0, b.lo:b.hi].view(self.k, self.world, b.S).transpose(0, 1)   # [dst, j, S]
                 if self.world > 1:
                     b.send.copy_(local)
-                    b.works.append(dist.all_to_all_single(b.recv.view(-1), b.send.view(-1), async_op=True))
+                    if self._rccl is not None:
+                        self._rccl.all_to_all(b.send.view(-1), b.recv.view(-1), s)
+                    else:
+                        b.works.append(dist.all_to_all_single(b.recv.view(-1), b.send.view(-1), async_op=True))
                 elif side and loopback_enabled():   # world 1: emulate the transfer (traces / tests)
                     if b.recv is None:
                         b.recv = torch.empty((1, self.k, b.S), dtype=e.X.dtype, device=e.device)
@@ -253,9 +259,21 @@ class ShardedAggregator:
         out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
         src = t.contiguous().view(-1)
         with self._on_comm():
-            work = dist.all_gather_into_tensor(out.view(-1), src, async_op=True)
-        work.wait()
+            if self._rccl is not None:
+                self._rccl.all_gather(src, out.view(-1), self._comm_stream)
+                work = None
+            else:
+                work = dist.all_gather_into_tensor(out.view(-1), src, async_op=True)
+        self._back_to_main(work)
         return out
+
+    def _back_to_main(self, work=None) -> None:
+        """The main stream waits for what was issued on the comm stream (and for a
+        torch.distributed work): an event the MAIN stream waits on."""
+        if work is not None:
+            work.wait()
+        if self._comm_stream is not None:
+            torch.cuda.current_stream(self.e.device).wait_stream(self._comm_stream)
 
     # ------------------------------------------------------------------ #
 
@@ -283,7 +301,10 @@ class ShardedAggregator:
         if gloo_backend():
             mine = mine.clone()  # gloo rejects an input aliasing the output
         with self._on_comm():
-            self._gathers.append(dist.all_gather_into_tensor(full, mine, async_op=True))
+            if self._rccl is not None:   # in place: this rank's block is its own shard
+                self._rccl.all_gather(mine, full, self._comm_stream)
+            else:
+                self._gathers.append(dist.all_gather_into_tensor(full, mine, async_op=True))
 
     def _finish_gathers(self) -> None:
         """Wait (stream-ordered on RCCL) for the weight all-gathers, then exchange the compact
@@ -294,23 +315,34 @@ class ShardedAggregator:
                 with torch.no_grad():
                     e._shadow.copy_(e.flat.data)
             return
+        if e._shadow is not None and self._np_idx is not None:
+            nb = self._np_buf
+            nb.zero_()
+            nb[self._np_own_pos] = e.flat.data[self._np_own_idx]
+            with self._on_comm():
+                if self._rccl is not None:
+                    self._rccl.all_reduce_sum(nb, self._comm_stream)
+                else:
+                    self._gathers.append(dist.all_reduce(nb, async_op=True))
         for w in self._gathers:
             w.wait()
         self._gathers = []
+        self._back_to_main()
         if e._shadow is not None:
             self.master_stale = True
             if self._np_idx is not None:
-                nb = self._np_buf
-                nb.zero_()
-                nb[self._np_own_pos] = e.flat.data[self._np_own_idx]
-                with self._on_comm():
-                    work = dist.all_reduce(nb, async_op=True)
-                work.wait()
-                e.flat.data[self._np_idx] = nb
+                e.flat.data[self._np_idx] = self._np_buf
+
+    def quiesce(self) -> None:
+        """Order torch.distributed collectives issued next after this aggregator's direct
+        ones (same communicator): the main stream waits for the comm stream."""
+        if self._comm_stream is not None:
+            torch.cuda.current_stream(self.e.device).wait_stream(self._comm_stream)
 
     def sync_master(self) -> None:
         """Collective: refresh the fp32 master outside this rank's shards (checkpoints,
         the reference-layout flat vector). Every rank must call it."""
+        self.quiesce()
         if not self.master_stale or self.world == 1:
             self.master_stale = False
             return
@@ -594,6 +626,7 @@ class ShardedAggregator:
 
     def momentum_vector(self) -> torch.Tensor:
         """The full (unsharded) momentum buffer, all-gathered (collective)."""
+        self.quiesce()
         e = self.e
         out = torch.zeros(e.ld, dtype=e.mom.dtype, device=e.mom.device)
         for b in sorted(self.buckets, key=lambda b: b.lo):

@@ -144,6 +144,21 @@ def main():
         g.replay()
         torch.cuda._sleep(2_000_000)
 
+    side2 = torch.cuda.Stream()
+
+    def v_device_flag_chain():     # + a third stream waiting (HIP event) on the side stream, as RCCL's would
+        g.replay()
+        C.signal_add(cnt, cur.cuda_stream)
+        st["n"] += 1
+        C.wait_geq(cnt, st["n"], 2_000_000, err, side.cuda_stream)
+        with torch.cuda.stream(side):
+            tiny.add_(1)
+        side2.wait_stream(side)
+        with torch.cuda.stream(side2):
+            tiny.mul_(1)
+        cur.wait_stream(side2)
+
+    variant("device_flag_chain", v_device_flag_chain)
     variant("side_sleep_concurrent", v_side_sleep, iters=10)
     variant("sleep_serial", v_side_sleep_after, iters=10)
     variant("device_flag", v_device_flag)
