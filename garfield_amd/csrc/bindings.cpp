@@ -1354,6 +1354,46 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   m.def("gpu_iwgrad", &g_iwgrad, "Per-worker implicit-GEMM weight gradient on MFMA: out[s, g] = Σ over pixel "
         "split s of worker g of dyᵀ · patches(x); args (x, dy, kh, kw, sh, sw, ph, pw, dh, dw, groups, out, splits)");
+  m.def("stem_supported", &garfield::gpu::stem_supported, py::arg("h"), py::arg("w"),
+        "True when the implicit stem kernels (7x7/2, 3 -> 64 channels) handle H x W images");
+  m.def("gpu_stem_fwd", [](const at::Tensor& x, const at::Tensor& w160, const at::Tensor& y) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_stem_fwd: x must be a channels_last bf16 [N, 3, H, W] tensor");
+    TORCH_CHECK(w160.scalar_type() == at::kBFloat16 && w160.is_contiguous() && w160.numel() == 64 * 160,
+                "gpu_stem_fwd: w must be the contiguous zero-padded [64, 160] bf16 matrix");
+    const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+    TORCH_CHECK(garfield::gpu::stem_supported(static_cast<int>(H), static_cast<int>(W)), "gpu_stem_fwd: unsupported size");
+    const int64_t Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
+    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == N && y.size(1) == 64 &&
+                    y.size(2) == Ho && y.size(3) == Wo && y.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_stem_fwd: y must be a channels_last bf16 [N, 64, Ho, Wo] tensor");
+    c10::hip::HIPGuard guard(x.device().index());
+    garfield::gpu::stem_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                            reinterpret_cast<const uint16_t*>(w160.data_ptr()), static_cast<int>(N), static_cast<int>(H),
+                            static_cast<int>(W), reinterpret_cast<uint16_t*>(y.data_ptr()), stream_of(x.device()));
+  }, py::arg("x"), py::arg("w"), py::arg("y"), "Implicit-GEMM ResNet stem forward (7x7/2, pad 3, 3 -> 64)");
+  m.def("gpu_stem_wgrad", [](const at::Tensor& x, const at::Tensor& dy, int64_t groups, const at::Tensor& part) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_stem_wgrad: x must be a channels_last bf16 [N, 3, H, W] tensor");
+    const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+    const int64_t Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
+    TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N && dy.size(1) == 64 &&
+                    dy.size(2) == Ho && dy.size(3) == Wo && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_stem_wgrad: dy must be a channels_last bf16 [N, 64, Ho, Wo] tensor");
+    TORCH_CHECK(groups >= 1 && N % groups == 0, "gpu_stem_wgrad: images not divisible into groups");
+    TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 4 &&
+                    part.size(1) == groups && part.size(2) == 64 && part.size(3) == 147,
+                "gpu_stem_wgrad: part must be a contiguous fp32 [slices, groups, 64, 147] tensor");
+    TORCH_CHECK(garfield::gpu::stem_supported(static_cast<int>(H), static_cast<int>(W)), "gpu_stem_wgrad: unsupported size");
+    c10::hip::HIPGuard guard(x.device().index());
+    garfield::gpu::stem_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                              reinterpret_cast<const uint16_t*>(dy.data_ptr()), static_cast<int>(N), static_cast<int>(H),
+                              static_cast<int>(W), static_cast<int>(groups), static_cast<int>(part.size(0)),
+                              part.data_ptr<float>(), stream_of(x.device()));
+  }, py::arg("x"), py::arg("dy"), py::arg("groups"), py::arg("part"),
+     "Implicit ResNet-stem weight gradient per worker: part[s, g] = slice s of worker g's dW [64, 147]");
   m.def("gpu_maxpool_fwd", &g_maxpool_fwd, "NHWC bf16 max pooling (k x k, stride s, padding p) keeping the "
         "argmax tap per element; args (x, k, s, p, y, idx)");
   m.def("gpu_maxpool_bwd", &g_maxpool_bwd, "Max-pooling backward as a gather; args (dy, idx, k, s, p, dx)");

@@ -56,6 +56,14 @@ void augment_gather(const uint8_t* src, int64_t nsrc, const int64_t* idx, const 
                     int64_t R, int H, int W, int C, int pad, bool flip,
                     uint64_t seed, uint64_t step, const AugNorm& nrm, uint16_t* out, hipStream_t stream);
 
+// ResNet stem (stem_nhwc.hip): 7x7 / stride 2 / padding 3 convolution of 3-channel NHWC bf16
+// images into 64 channels on MFMA, without a patch matrix. w: zero-padded [64][160] bf16.
+bool stem_supported(int H, int W);
+void stem_fwd(const uint16_t* x, const uint16_t* w, int N, int H, int W, uint16_t* y, hipStream_t stream);
+// per-worker weight gradients: part fp32 [slices][groups][64][147] (sum over slices = dW of the worker)
+void stem_wgrad(const uint16_t* x, const uint16_t* dy, int N, int H, int W, int groups, int slices, float* part,
+                hipStream_t stream);
+
 // Row-major NT GEMM on MFMA (gemm_nt.hip): C[M, N] = A[M, K] · B[N, K]ᵀ (+ add), bf16; K % 64 == 0,
 // N a multiple of the configuration's tile width. stats (nullable): per-tile, per-worker (rg rows)
 // BatchNorm statistics of C, [ceil(M / BM)][2][2][N] floats, merged by bn_finalize_tiles.

@@ -61,6 +61,10 @@ IWGRAD = os.environ.get("GARFIELD_IWGRAD", "1") != "0"
 # ... and for the 1x1 stride-1 convolutions too (else a split-K batched hipBLASLt GEMM).
 # 1x1 weight gradients on the implicit kernel too: 6.77-6.83 vs 6.82-6.88 ms/step (profiles/r2/ab_iwgrad_1x1.log)
 IWGRAD_1X1 = os.environ.get("GARFIELD_IWGRAD_1X1", "1") != "0"
+# The ResNet stem (7x7/2, 3 -> 64 channels) on its own implicit MFMA kernels (stem_nhwc.hip):
+# no im2col patch matrix in the forward or the weight gradient. "0" keeps im2col + GEMM.
+STEM = os.environ.get("GARFIELD_STEM", "1") != "0"
+_STEM_WG = int(os.environ.get("GARFIELD_STEM_WG", "512"))   # weight-gradient workgroups to aim for
 # weight gradients on a side stream (see WgradStream): measured slower in the graphed step
 # (7.23 vs 7.07 ms: per-layer fork/join dependencies leave 8% of the window idle), so off
 WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0")
@@ -573,6 +577,30 @@ def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int)
         spec.sink.put_groups(spec.conv.weight, part.sum(0) if S > 1 else part[0])
 
 
+def _stem_ok(x: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> bool:
+    """The 3-channel 7x7/2/pad-3 stem into 64 channels, bf16 channels_last, on sizes whose
+    staged input rows fit the kernels' LDS (every CIFAR/ImageNet-crop size up to 64 px)."""
+    return (STEM and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and tuple(w.shape) == (64, 3, 7, 7) and _channels_last_weight(w)
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and spec.stride == (2, 2) and spec.padding == (3, 3) and spec.dilation == (1, 1)
+            and _native.native().stem_supported(x.shape[2], x.shape[3]))
+
+
+def _stem_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> None:
+    """Per-worker stem weight gradients (``gpu_stem_wgrad``): fp32 slabs of image slices,
+    summed into the exchange rows by the deferred split-K reduction."""
+    per = x.shape[0] // G
+    S = max(1, min(per, -(-_STEM_WG // G)))
+    part = torch.empty((S, G, 64, 147), dtype=torch.float32, device=dy.device)
+    _native.native().gpu_stem_wgrad(x, dy, G, part)
+    rows = spec.sink.rows_view(spec.conv.weight, (64, 147), spec.sink.flat.dtype)
+    if rows is not None:
+        spec.sink.queue_split(part, rows)
+    else:
+        spec.sink.put_groups(spec.conv.weight, part.sum(0))
+
+
 def _dgrad_weight_shape(w: torch.Tensor) -> torch.Tensor:
     """A meta tensor shaped like ``_dgrad_weight(w)`` (for the kernel-choice test)."""
     return torch.empty((w.shape[1], w.shape[0], w.shape[2], w.shape[3]), dtype=w.dtype, device="meta")
@@ -704,6 +732,13 @@ class _GroupedConv(torch.autograd.Function):
             if y2 is None:
                 y2 = torch.mm(rows2d(x), w.reshape(w.shape[0], -1).t())
             return from_rows(y2, n, h, wd)
+        if CONV_MODE == "gemm" and _stem_ok(x, w, spec):
+            ctx.mode = "stem"
+            ctx.save_for_backward(x, w)
+            ho, wo = _out_hw(spec, h, wd)
+            y = torch.empty((n, 64, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            _native.native().gpu_stem_fwd(x, _wmat(w, 160, spec), y)
+            return y
         if CONV_MODE == "gemm" and _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
             ctx.mode = "iconv"
             ctx.save_for_backward(x, w)
@@ -784,6 +819,11 @@ class _GroupedConv(torch.autograd.Function):
                         if kp != K:
                             dW = dW[:, :, :K].contiguous()
                         spec.sink.put_groups(spec.conv.weight, dW)
+        elif mode == "stem":                     # a = x (the network input: dx is rarely wanted)
+            if need_dx:
+                dx = _cl(_conv_bwd(dy, a, w, spec, [True, False, False])[0])
+            if spec.sink is not None:
+                _stem_wgrad(a, dy, spec, G)
         elif mode == "col":                      # a = col [N*Ho*Wo, Kp]
             kp = a.shape[1]
             if need_dx:
