@@ -36,7 +36,6 @@ constexpr int kMaxPatch = 24576;           // elements (48 KB) of staged input p
 
 struct StemGeo {
   int N, H, W, Ho, Wo;
-  int rows_in;     // staged input rows per forward workgroup (or per image row band)
   int pw;          // staged row width in pixels = W + 2P
 };
 
@@ -50,24 +49,46 @@ __device__ __forceinline__ int tap_offset(int k, int pw, int zero) {
 }
 
 // Stage input rows [iy0, iy0 + rows) of image n into LDS as [rows][pw][3] (zero outside the image).
+// A staged row is the image row's 3W contiguous elements between 3P zero elements on each side;
+// the (row, column) position advances without divisions, and each thread issues kStageBatch
+// independent loads before its LDS stores (one memory latency per batch, not per element).
+constexpr int kStageBatch = 8;
 __device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ x, const StemGeo& g, int n, int iy0, int rows,
                                            uint16_t* patch) {
-  const int per_row = g.pw * kC;
+  const int per_row = g.pw * kC, row_len = g.W * kC;
   const int total = rows * per_row;
-  const int64_t img = static_cast<int64_t>(n) * g.H * g.W * kC;
-  for (int e = threadIdx.x; e < total; e += kThreads) {
-    const int r = e / per_row, c = e - r * per_row;
-    const int iy = iy0 + r, ix = c / kC - kP, ci = c - (c / kC) * kC;
-    uint16_t v = 0;
-    if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W) v = x[img + (static_cast<int64_t>(iy) * g.W + ix) * kC + ci];
-    patch[e] = v;
+  const uint16_t* src = x + static_cast<int64_t>(n) * g.H * row_len - kP * kC;   // (iy, c) at src + iy*row_len + c
+  const int dr = kThreads / per_row, dc = kThreads - dr * per_row;
+  int e = threadIdx.x, r = e / per_row, c = e - r * per_row;
+  while (e < total) {
+    uint16_t v[kStageBatch];
+    int pos[kStageBatch];
+#pragma unroll
+    for (int b = 0; b < kStageBatch; ++b) {
+      const int iy = iy0 + r;
+      v[b] = 0;
+      if (e < total && iy >= 0 && iy < g.H && c >= kP * kC && c < kP * kC + row_len)
+        v[b] = src[static_cast<int64_t>(iy) * row_len + c];
+      pos[b] = e;
+      e += kThreads;
+      c += dc;
+      r += dr;
+      if (c >= per_row) {
+        c -= per_row;
+        ++r;
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < kStageBatch; ++b)
+      if (pos[b] < total) patch[pos[b]] = v[b];
   }
 }
 
 __global__ __launch_bounds__(kThreads) void k_stem_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                        StemGeo g, uint16_t* __restrict__ y) {
-  // LDS: weights [64][160] | staged input rows (+1 zero) ; the output tile reuses the input area
-  __shared__ __attribute__((aligned(16))) uint16_t lds[kCout * kKP + kMaxPatch + 8];
+  // LDS (dynamic, sized by the host for this geometry): weights [64][160] | staged input rows
+  // (+1 zero); the [128][64] output tile reuses the whole area
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* wl = lds;
   uint16_t* patch = lds + kCout * kKP;
   const int tiles = (g.Ho * g.Wo + kTile - 1) / kTile;
@@ -125,8 +146,8 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const uint16_t* __restric
     }
   }
   // epilogue: D lane = pixel fr of fragment f, channels 16c + 4fq .. +3 -> LDS tile [128][64] -> 16-byte rows
-  __syncthreads();   // every wave's patch reads are done: reuse the input area
-  uint16_t* tile = patch;
+  __syncthreads();   // every wave's weight and patch reads are done: reuse the area
+  uint16_t* tile = lds;
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
     const int pl = wave * 32 + f * 16 + fr;
@@ -153,7 +174,7 @@ constexpr int kDyPitch = 40;   // bf16 per transposed dy row (32 + 8: 16-byte al
 __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const uint16_t* __restrict__ x,
                                                          const uint16_t* __restrict__ dy, StemGeo g, int imgs_per_worker,
                                                          int slices, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[kCout * kDyPitch + kMaxPatch + 8];
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];   // dynamic: sized by the host
   uint16_t* dyt = lds;                       // [64][kDyPitch]
   uint16_t* patch = lds + kCout * kDyPitch;  // one image's input rows
   const int s = blockIdx.x, grp = blockIdx.y;
@@ -178,33 +199,43 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const uint16_t* __restr
     stage_rows(x, g, n, -kP, rows, patch);
     if (threadIdx.x == 0) patch[zero] = 0;
     const uint16_t* dyi = dy + static_cast<int64_t>(n) * npix * kCout;
+    // this thread's 16 bytes of a dy tile: pixel q0 + pq, channels 8 cv .. +7; the next
+    // tile's load is issued before the current tile's MFMAs (one latency per image, not per tile)
+    const int pq = threadIdx.x >> 3, cv = threadIdx.x & 7;
+    auto load_dy = [&](int q0) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (q0 + pq < npix) v = *reinterpret_cast<const uint4*>(dyi + static_cast<int64_t>(q0 + pq) * kCout + cv * 8);
+      return v;
+    };
+    uint4 vnext = load_dy(0);
     for (int q0 = 0; q0 < npix; q0 += 32) {
       __syncthreads();   // previous dy tile consumed (and, first time, the patch staged)
-      // dy rows q0 .. q0+31 (64 channels each = 8 x 16 B) -> transposed [ch][pixel]
       {
-        const int pq = threadIdx.x >> 3, cv = threadIdx.x & 7;   // 32 pixels x 8 channel vectors
-        const int p = q0 + pq;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (p < npix) v = *reinterpret_cast<const uint4*>(dyi + static_cast<int64_t>(p) * kCout + cv * 8);
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t wv[4] = {vnext.x, vnext.y, vnext.z, vnext.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           dyt[(cv * 8 + 2 * i) * kDyPitch + pq] = static_cast<uint16_t>(wv[i] & 0xffffu);
           dyt[(cv * 8 + 2 * i + 1) * kDyPitch + pq] = static_cast<uint16_t>(wv[i] >> 16);
         }
       }
+      if (q0 + 32 < npix) vnext = load_dy(q0 + 32);
       __syncthreads();
       // A = dyᵀ: lane holds channel (16 wave + fr), pixels q0 + 8 fq .. +7
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(dyt + (wave * 16 + fr) * kDyPitch + fq * 8);
       // B: pixels q0 + 8 fq + j (rows of the reduction), tap k = 16 kb + fr (column)
+      // (the 8 pixels are consecutive: one division, then column steps with a row wrap)
       int pb[8];
+      {
+        const int p = q0 + fq * 8;
+        int oy = p / g.Wo, ox = p - oy * g.Wo;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        int p = q0 + fq * 8 + j;
-        const bool ok = p < npix;
-        p = ok ? p : 0;
-        const int oy = p / g.Wo, ox = p - oy * g.Wo;
-        pb[j] = ok ? (oy * kS * g.pw + ox * kS) * kC : -1;   // rows staged from input row -P
+        for (int j = 0; j < 8; ++j) {
+          pb[j] = p + j < npix ? (oy * kS * g.pw + ox * kS) * kC : -1;   // rows staged from input row -P
+          if (++ox == g.Wo) {
+            ox = 0;
+            ++oy;
+          }
+        }
       }
 #pragma unroll
       for (int kb = 0; kb < kKP / 16; ++kb) {
@@ -240,26 +271,29 @@ StemGeo geo(int N, int H, int W) {
   return g;
 }
 
+int fwd_rows(const StemGeo& g) { return ((kTile + g.Wo - 1) / g.Wo) * kS + kKH; }   // max staged rows per tile
+int wg_rows(const StemGeo& g) { return (g.Ho - 1) * kS + kKH; }                     // every row an image reads
+
 }  // namespace
 
 bool stem_supported(int H, int W) {
+  if (H <= 0 || W <= 0) return false;
   const StemGeo g = geo(1, H, W);
-  // forward: a 128-pixel tile spans at most ceil(128 / Wo) + 1 output rows
-  const int fwd_rows = ((kTile + g.Wo - 1) / g.Wo) * kS + kKH;
-  const int wg_rows = (g.Ho - 1) * kS + kKH;
-  return H > 0 && W > 0 && fwd_rows * g.pw * kC < kMaxPatch && wg_rows * g.pw * kC < kMaxPatch;
+  return fwd_rows(g) * g.pw * kC < kMaxPatch && wg_rows(g) * g.pw * kC < kMaxPatch;
 }
 
 void stem_fwd(const uint16_t* x, const uint16_t* w, int N, int H, int W, uint16_t* y, hipStream_t stream) {
   const StemGeo g = geo(N, H, W);
   const int tiles = (g.Ho * g.Wo + kTile - 1) / kTile;
-  hipLaunchKernelGGL(k_stem_fwd, dim3(N * tiles), dim3(kThreads), 0, stream, x, w, g, y);
+  const size_t lds = (static_cast<size_t>(kCout) * kKP + static_cast<size_t>(fwd_rows(g)) * g.pw * kC + 8) * 2;
+  hipLaunchKernelGGL(k_stem_fwd, dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
 }
 
 void stem_wgrad(const uint16_t* x, const uint16_t* dy, int N, int H, int W, int groups, int slices, float* part,
                 hipStream_t stream) {
   const StemGeo g = geo(N, H, W);
-  hipLaunchKernelGGL(k_stem_wgrad, dim3(slices, groups), dim3(kThreads), 0, stream, x, dy, g, N / groups, slices,
+  const size_t lds = (static_cast<size_t>(kCout) * kDyPitch + static_cast<size_t>(wg_rows(g)) * g.pw * kC + 8) * 2;
+  hipLaunchKernelGGL(k_stem_wgrad, dim3(slices, groups), dim3(kThreads), lds, stream, x, dy, g, N / groups, slices,
                      part);
 }
 

@@ -64,7 +64,7 @@ IWGRAD_1X1 = os.environ.get("GARFIELD_IWGRAD_1X1", "1") != "0"
 # The ResNet stem (7x7/2, 3 -> 64 channels) on its own implicit MFMA kernels (stem_nhwc.hip):
 # no im2col patch matrix in the forward or the weight gradient. "0" keeps im2col + GEMM.
 STEM = os.environ.get("GARFIELD_STEM", "1") != "0"
-_STEM_WG = int(os.environ.get("GARFIELD_STEM_WG", "512"))   # weight-gradient workgroups to aim for
+_STEM_WG = int(os.environ.get("GARFIELD_STEM_WG", "1024"))   # weight-gradient workgroups to aim for
 # weight gradients on a side stream (see WgradStream): measured slower in the graphed step
 # (7.23 vs 7.07 ms: per-layer fork/join dependencies leave 8% of the window idle), so off
 WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0")
