@@ -352,7 +352,7 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
                   const c10::optional<at::Tensor>& run_var, const at::Tensor& part, const at::Tensor& mean,
                   const at::Tensor& istd, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& y,
                   bool relu, const c10::optional<at::Tensor>& mask, bool defer_running,
-                  const c10::optional<at::Tensor>& tile_stats, int64_t tile_m) {
+                  const c10::optional<at::Tensor>& tile_stats, int64_t tile_m, int64_t tile_e) {
   const auto dev = x.device();
   check_bf16_rows(x, dev, "x");
   check_bf16_rows(y, dev, "y");
@@ -385,13 +385,14 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
   const float* ts = nullptr;
   if (tile_stats.has_value() && tile_stats->defined()) {
     TORCH_CHECK(tile_m > 0 && tile_m <= rg, "garfield bn: tile statistics need 0 < tile_m <= rows per worker");
+    TORCH_CHECK(tile_e >= 1, "garfield bn: tile_e must be >= 1");
     const int64_t tiles = (x.size(0) + tile_m - 1) / tile_m;
-    ts = ws_vec(*tile_stats, tiles * 4 * C, dev, "tile_stats");
+    ts = ws_vec(*tile_stats, tiles * tile_e * 6 * C, dev, "tile_stats");
   }
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::bn_forward(u16(x), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
                             static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, u16_mut(y), relu, mp,
-                            defer_running, stream_of(dev), ts, static_cast<int>(tile_m));
+                            defer_running, stream_of(dev), ts, tile_m, static_cast<int>(tile_e));
 }
 
 int xent_dtype(const at::Tensor& t, const char* what) {
@@ -654,15 +655,48 @@ void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, co
     TORCH_CHECK(rg > 0 && M % rg == 0, "gpu_gemm_nt: statistics need M to split into rg-row workers");
   }
   if (cfg < 0) cfg = garfield::gpu::gemm_nt_pick(M, static_cast<int>(N), static_cast<int>(K), want_stats ? rg : 0);
-  const int bm = garfield::gpu::gemm_nt_tile_m(static_cast<int>(cfg)), bn = garfield::gpu::gemm_nt_tile_n(static_cast<int>(cfg));
-  TORCH_CHECK(bm > 0 && N % bn == 0, "gpu_gemm_nt: no tile configuration ", cfg, " for N = ", N);
+  TORCH_CHECK(garfield::gpu::gemm_nt_valid(static_cast<int>(cfg), static_cast<int>(N), static_cast<int>(K)),
+              "gpu_gemm_nt: no tile configuration ", cfg, " for N = ", N, ", K = ", K);
   if (want_stats) {
-    TORCH_CHECK(bm <= rg, "gpu_gemm_nt: tile of ", bm, " rows spans more than two workers of ", rg, " rows");
-    sp = ws_vec(*stats, ((M + bm - 1) / bm) * 4 * N, dev, "stats");
+    const int sr = garfield::gpu::gemm_nt_stats_rows(static_cast<int>(cfg));
+    TORCH_CHECK(sr <= rg, "gpu_gemm_nt: statistics tile of ", sr, " rows spans more than two workers of ", rg, " rows");
+    int64_t H = 0;
+    int E = 0;
+    garfield::gpu::gemm_nt_stats_geometry(static_cast<int>(cfg), M, static_cast<int>(N), static_cast<int>(K), rg, &H, &E);
+    sp = ws_vec(*stats, ((M + H - 1) / H) * E * 6 * N, dev, "stats");
   }
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::gemm_nt(u16(a), u16(b), static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), u16_mut(c),
                          ap, sp, rg, static_cast<int>(cfg), stream_of(dev));
+}
+
+// Transposes of many bf16 matrices in one launch: dsts[i] = srcs[i]ᵀ (2-D, contiguous, 16-B aligned,
+// both dims multiples of 8).
+void g_transpose_multi(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size(), "gpu_transpose_multi: one dst per src");
+  if (srcs.empty()) return;
+  std::vector<const uint16_t*> sp;
+  std::vector<uint16_t*> dp;
+  std::vector<int> R, C;
+  const auto dev = srcs[0].device();
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const auto& a = srcs[i];
+    const auto& b = dsts[i];
+    TORCH_CHECK(a.is_cuda() && a.device() == dev && a.scalar_type() == at::kBFloat16 && a.dim() == 2 &&
+                    a.is_contiguous() && b.device() == dev && b.scalar_type() == at::kBFloat16 && b.dim() == 2 &&
+                    b.is_contiguous() && b.size(0) == a.size(1) && b.size(1) == a.size(0),
+                "gpu_transpose_multi: src [R, C] and dst [C, R] contiguous bf16 on one device");
+    TORCH_CHECK(a.size(0) % 8 == 0 && a.size(1) % 8 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
+                "gpu_transpose_multi: dims multiples of 8, 16-byte aligned");
+    sp.push_back(u16(a));
+    dp.push_back(u16_mut(b));
+    R.push_back(static_cast<int>(a.size(0)));
+    C.push_back(static_cast<int>(a.size(1)));
+  }
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::transpose_multi(sp.data(), dp.data(), R.data(), C.data(), static_cast<int>(sp.size()),
+                                 stream_of(dev));
 }
 
 // Large gradient sets: x an [n, d] GPU matrix (unit column stride, row stride ld, 16-bit or fp32).
@@ -1284,7 +1318,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"), py::arg("part"), py::arg("mean"),
         py::arg("istd"), py::arg("scale"), py::arg("shift"), py::arg("y"), py::arg("relu"),
         py::arg("mask") = py::none(), py::arg("defer_running") = false, py::arg("tile_stats") = py::none(),
-        py::arg("tile_m") = 0);
+        py::arg("tile_m") = 0, py::arg("tile_e") = 1);
   m.def("bn_small", [](int64_t rg) { return garfield::gpu::bn_small(rg); },
         "True when rg rows per worker take the single-kernel BatchNorm path (whose running statistics "
         "can be deferred to gpu_bn_running_update)");
@@ -1333,17 +1367,33 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("labels_out") = py::none());
   m.def("gpu_gemm_nt", &g_gemm_nt,
         "Row-major NT GEMM on MFMA: c = a · bᵀ (+ add); args (a [M,K], b [N,K], c [M,N], add=None, stats=None, "
-        "rg=0, cfg=-1); stats: fp32 [ceil(M/BM)][2][2][N] per-worker BatchNorm statistics of c (gpu_bn_forward's "
-        "tile_stats)",
+        "rg=0, cfg=-1); stats: fp32 per-worker BatchNorm statistics of c, laid out as gemm_nt_stats_geometry "
+        "says (gpu_bn_forward's tile_stats / tile_m / tile_e)",
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("add") = py::none(), py::arg("stats") = py::none(),
         py::arg("rg") = 0, py::arg("cfg") = -1);
   m.def("gemm_nt_pick", [](int64_t M, int64_t N, int64_t K, int64_t rg_limit) {
     return garfield::gpu::gemm_nt_pick(M, static_cast<int>(N), static_cast<int>(K), rg_limit);
-  }, "Tile configuration gpu_gemm_nt picks for M x N x K (rg_limit > 0: BM <= rg_limit); -1 if none");
+  }, "Tile configuration gpu_gemm_nt picks for M x N x K (rg_limit > 0: stats rows <= rg_limit); -1 if none");
   m.def("gemm_nt_tile", [](int64_t cfg) {
     return std::make_pair(garfield::gpu::gemm_nt_tile_m(static_cast<int>(cfg)),
                           garfield::gpu::gemm_nt_tile_n(static_cast<int>(cfg)));
   }, "(BM, BN) of a gpu_gemm_nt tile configuration");
+  m.def("gpu_transpose_multi", &g_transpose_multi,
+        "dsts[i] = srcs[i]ᵀ for 2-D bf16 matrices (dims multiples of 8), one launch per 40 matrices",
+        py::arg("srcs"), py::arg("dsts"));
+  m.def("gemm_nt_num_cfg", &garfield::gpu::gemm_nt_num_cfg, "Number of gpu_gemm_nt tile configurations");
+  m.def("gemm_nt_valid", [](int64_t cfg, int64_t N, int64_t K) {
+    return garfield::gpu::gemm_nt_valid(static_cast<int>(cfg), static_cast<int>(N), static_cast<int>(K));
+  }, "Whether configuration cfg runs an N x K weight");
+  m.def("gemm_nt_stats_rows", [](int64_t cfg) { return garfield::gpu::gemm_nt_stats_rows(static_cast<int>(cfg)); },
+        "Least rows per worker that configuration cfg's fused statistics need");
+  m.def("gemm_nt_stats_geometry", [](int64_t cfg, int64_t M, int64_t N, int64_t K, int64_t rg) {
+    int64_t H = 0;
+    int E = 0;
+    garfield::gpu::gemm_nt_stats_geometry(static_cast<int>(cfg), M, static_cast<int>(N), static_cast<int>(K), rg, &H, &E);
+    return std::make_tuple(H, E, ((M + H - 1) / H) * E * 6 * N);
+  }, "(H, E, floats): statistics tiles of H rows with E entries each (gpu_bn_forward's tile_m, tile_e) and the "
+     "stats buffer size of a gpu_gemm_nt launch with fused statistics");
   m.def("gpu_iconv", &g_iconv, "Implicit-GEMM NHWC convolution on MFMA: y = conv(x, w) (+ add); args (x, w, kh, kw, "
         "sh, sw, ph, pw, dh, dw, y, add=None, pm=0, transpose_w=False); x/y/add channels_last bf16, C % 32 == 0, "
         "Cout % 64 == 0; transpose_w: w is the forward weight [C, Cout, KH, KW] whose flipped transpose is applied "

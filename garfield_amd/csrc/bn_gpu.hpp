@@ -42,7 +42,8 @@ bool bn_small(int64_t rg);
 void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
                 float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
-                bool defer_running, hipStream_t stream, const float* tile_stats = nullptr, int tile_m = 0);
+                bool defer_running, hipStream_t stream, const float* tile_stats = nullptr, int64_t tile_m = 0,
+                int tile_e = 1);
 
 // Fresh batches (data_aug.hip): out[r] (bf16 channels_last [R, C, H, W]) = normalise(random crop
 // (pad) + random horizontal flip of uint8 NHWC image src[idx[r]]); the crop/flip of row r is a hash
@@ -65,17 +66,28 @@ void stem_wgrad(const uint16_t* x, const uint16_t* dy, int N, int H, int W, int 
                 hipStream_t stream);
 
 // Row-major NT GEMM on MFMA (gemm_nt.hip): C[M, N] = A[M, K] · B[N, K]ᵀ (+ add), bf16; K % 64 == 0,
-// N a multiple of the configuration's tile width. stats (nullable): per-tile, per-worker (rg rows)
-// BatchNorm statistics of C, [ceil(M / BM)][2][2][N] floats, merged by bn_finalize_tiles.
+// N a multiple of the configuration's tile width. stats (nullable): per-stats-tile, per-worker (rg rows)
+// BatchNorm statistics of C, [ceil(M / SR)][2][2][N] floats (SR = gemm_nt_stats_rows(cfg)), merged by
+// bn_finalize_tiles. Configurations 0..8 stream K through an LDS ring; 9..14 keep the weight slice
+// resident in LDS and stream row tiles through a persistent workgroup (K <= 256).
 void gemm_nt(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
              float* stats, int64_t rg, int cfg, hipStream_t stream);
-// Tile configuration for an M x N x K problem (-1: none fits); rg_limit > 0: BM <= rg_limit (statistics).
+// Configuration for an M x N x K problem (-1: none fits); rg_limit > 0: stats tiles <= rg_limit rows.
 int gemm_nt_pick(int64_t M, int N, int K, int64_t rg_limit);
+int gemm_nt_num_cfg();
+bool gemm_nt_valid(int cfg, int N, int K);
 int gemm_nt_tile_m(int cfg);
 int gemm_nt_tile_n(int cfg);
-void bn_finalize_tiles(const float* stats, int BM, int64_t M, int64_t rg, int groups, int C, const float* gamma,
-                       const float* beta, float eps, float* mean, float* istd, float* scale, float* shift,
-                       hipStream_t stream);
+int gemm_nt_stats_rows(int cfg);
+// statistics tiles of an M x N x K launch of cfg with rg-row workers: H rows, E entries each
+// (stats buffer: ceil(M / H) * E * 6 * N floats)
+void gemm_nt_stats_geometry(int cfg, int64_t M, int N, int K, int64_t rg, int64_t* H, int* E);
+// dst_i [C_i, R_i] = src_i [R_i, C_i]ᵀ for bf16 matrices (R_i, C_i multiples of 8), in one launch per 40
+void transpose_multi(const uint16_t* const* srcs, uint16_t* const* dsts, const int* R, const int* C, int count,
+                     hipStream_t stream);
+void bn_finalize_tiles(const float* stats, int64_t H, int E, int64_t M, int64_t rg, int groups, int C,
+                       const float* gamma, const float* beta, float eps, float* mean, float* istd, float* scale,
+                       float* shift, hipStream_t stream);
 
 // mask (nullable, relu only): bit (r*C + c) of the byte array = y[r, c] > 0, for the backward.
 // ReLU source of the backward: mask when given, else y (nullable) > 0. dres (nullable) receives dz.

@@ -761,7 +761,8 @@ int64_t bn_part_floats(int64_t rg, int groups, int C) {
 void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
                 float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
-                bool defer_running, hipStream_t stream, const float* tile_stats, int tile_m) {
+                bool defer_running, hipStream_t stream, const float* tile_stats, int64_t tile_m,
+                int tile_e) {
   if (rg <= kSmallRows && tile_stats == nullptr) {
     const int ch = small_ch();
     if (ch == 16) launch_fwd_small<16>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream);
@@ -776,8 +777,8 @@ void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, 
     return;
   }
   if (tile_stats) {   // statistics from the producing GEMM's epilogue (gemm_nt.hip): no partial pass
-    bn_finalize_tiles(tile_stats, tile_m, rg * groups, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift,
-                      stream);
+    bn_finalize_tiles(tile_stats, tile_m, tile_e, rg * groups, rg, groups, C, gamma, beta, eps, mean, istd, scale,
+                      shift, stream);
   } else {
     const Geo g = geometry(rg, groups, C);
     const int ncb = (C + g.cb - 1) / g.cb;

@@ -23,11 +23,16 @@ __device__ __forceinline__ float bf16_to_f(uint32_t u16) { return __uint_as_floa
 __device__ __forceinline__ float f16_to_f(uint32_t u16) {
   return static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(u16)));
 }
+// fp32 -> bf16 round-to-nearest-even on the gfx950 converter (v_cvt_pk_bf16_f32), one
+// instruction instead of the integer rounding sequence; NaN stays a (quiet) NaN.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint16_t f_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<uint16_t>(u >> 16);
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
+}
+// two floats -> packed bf16 pair (a in the low half), one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
 }
 __device__ __forceinline__ uint16_t f_to_f16(float f) {
   return __builtin_bit_cast(uint16_t, static_cast<_Float16>(f));

@@ -1,4 +1,4 @@
-// Row-major "NT" GEMM for the grouped step's 1x1 convolutions, on MFMA (bf16 in, fp32
+// Row-major "NT" GEMMs for the grouped step's 1x1 convolutions, on MFMA (bf16 in, fp32
 // accumulate, bf16 out), gfx950, with the producer-side BatchNorm statistics fused in.
 //
 //   C[M, N] = A[M, K] · B[N, K]ᵀ  (+ add[M, N])
@@ -7,25 +7,35 @@
 // B = the weight [Cout, Cin]. Data gradient: A = dy rows [pixels, Cout], B = the
 // transposed weight [Cin, Cout]; ``add`` folds in the residual branch's gradient.
 //
-// Why not hipBLASLt: the step's 1x1 GEMMs are skinny (M = 2k..128k pixels, N, K =
-// 64..2048) and memory-bound; hipBLASLt measured 2.2x the compulsory-byte time on
-// them, with a ~10 µs floor per call (scripts/bench_1x1.py), and its epilogue cannot
-// produce the per-WORKER BatchNorm statistics that the next layer needs, so a
-// separate pass re-read every output (bn_nhwc.hip k_partial). Here:
+// The step's 1x1 GEMMs are skinny (M = 2k..128k pixels, N, K = 64..2048) and mostly
+// memory-bound; hipBLASLt measured 1.5-2.5x the compulsory-byte time on them with a
+// ~10 µs floor per call (scripts/bench_1x1.py), and its epilogue cannot produce the
+// per-WORKER BatchNorm statistics the next layer needs. Two kernels:
 //
-// * workgroup tile BM pixels x BN channels (4 waves, WM x WN, each 16*WPM x 16*WPN),
-//   64-deep k-steps staged global -> LDS by global_load_lds (16 B per lane, no VGPR
-//   round trip) in an NS-deep ring, chunk index XOR-swizzled by (row & 7) on the
-//   global side so the 16-row fragment reads hit 8 different bank groups;
-// * v_mfma_f32_16x16x32_bf16 with the WEIGHT as the MFMA A operand, so D's lane holds
-//   4 consecutive output channels of one pixel: one 8-byte store per fragment;
-// * tiles are numbered XCD-aware (the N blocks of one M block run on the same XCD
-//   and share its L2 copy of the A rows);
-// * EPI_STATS: every tile also emits, per channel and per worker group its rows
-//   belong to (a tile spans <= 2 groups: BM <= rows per worker), the count-free pair
-//   (Σ y, Σ (y - ȳ_tile)²) of the STORED bf16 values. ``bn_finalize_tiles`` merges
-//   the tiles of a worker with Chan's parallel-variance update (no cancellation,
-//   whatever |mean| / std), so the BatchNorm forward only runs its apply pass.
+// * k_gemm_ws (K <= 256, the big-M layers): weight-stationary and persistent. A
+//   workgroup loads its [BN, K] weight slice into LDS ONCE and then streams row tiles
+//   [BM, K] through a 2-slot global_load_lds ring (tile t+1 in flight while tile t is
+//   multiplied and written). Each of the 4 waves owns RW rows x 64 channels, so its
+//   epilogue is wave-private: the bf16 tile goes through the wave's own XOR-swizzled LDS
+//   slice and leaves as whole 128-B row lines (16 B per lane), with no workgroup barrier.
+//   Workgroups streaming the same row tiles (different N slices) share an XCD (L2).
+// * k_gemm_nt (any K % 64): a K-loop over 64-deep steps staged by global_load_lds in an
+//   NS-deep ring, XCD-aware tile order, whole-tile LDS epilogue.
+//
+// v_mfma_f32_16x16x32_bf16 takes the WEIGHT as the MFMA A operand, so the accumulator's
+// lane holds 4 consecutive output channels of one pixel, and the 16 lanes of a DPP row
+// hold one channel quad for 16 pixels. EPI_STATS therefore reduces the per-channel
+// statistics of the STORED bf16 values in registers: a 4-step DPP row reduction gives
+// Σy over the wave's rows, then Σ(y - ȳ)² around that sub-tile mean (count-free pairs,
+// no cancellation whatever |mean| / std). Each wave's RW-row sub-tile is one statistics
+// tile (split in two slots where it straddles a worker boundary); ``bn_finalize_tiles``
+// merges a worker's tiles with Chan's parallel-variance update, so the BatchNorm forward
+// runs only its apply pass.
+//
+// Statistics layout: stats[T][E][slot][q][N] floats, q = {n, Σy, Σ(y - ȳ)²}: stats tile T covers
+// rows [T*H, (T+1)*H) (H <= rows per worker, so at most two workers: slot 0 the first, slot 1
+// the next); its E entries (e.g. the waves that share it) each cover a subset of those rows and
+// carry their own count.
 #include "bn_gpu.hpp"
 #include "gar_device.hpp"
 
@@ -38,6 +48,81 @@ using lds_ptr = __attribute__((address_space(3))) void*;
 __device__ __attribute__((aligned(16))) uint4 g_gemm_zero[8];  // 128 zero bytes: source of padded rows
 
 constexpr int EPI_PLAIN = 0, EPI_ADD = 1, EPI_STATS = 2;
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the 16 lanes of a DPP row, returned in every lane of the row.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+  v += dpp_mov<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+  v += dpp_mov<0x141>(v);   // row_half_mirror
+  v += dpp_mov<0x140>(v);   // row_mirror
+  return v;
+}
+
+__device__ __forceinline__ float bf16_round(float x) { return bf16_to_f(f_to_bf16(x)); }
+
+// Statistics of one wave's sub-tile: rows r0 + r*16 + fr (r < WPM), channels chb + c*16 + 4*fq + i.
+// v: the stored (bf16-rounded) values. Writes stats[((t*2 + slot)*2 + {0: Σy, 1: Σ(y-ȳ)²})*N + ch]
+// for t = r0 / (16*WPM); slot 1 holds the rows past the first worker boundary inside the tile.
+template <int WPM, int WPN>
+__device__ __forceinline__ void wave_stats(const float (&v)[WPM][WPN][4], int64_t r0, int64_t M, int64_t rg, int N,
+                                           int chb, float* __restrict__ stats) {
+  constexpr int RW = 16 * WPM;
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+  const int64_t t = r0 / RW;
+  const int64_t end = r0 + RW < M ? r0 + RW : M;
+  const int64_t gb = (r0 / rg + 1) * rg;
+  const int split = static_cast<int>((gb < end ? gb : end) - r0);   // rows of slot 0
+  const int rows = static_cast<int>(end - r0);
+  const int nslot = split < rows ? 2 : 1;
+  for (int slot = 0; slot < nslot; ++slot) {
+    const int lo = slot ? split : 0, hi = slot ? rows : split;
+    const float cnt = static_cast<float>(hi - lo);
+    float s[WPN][4], q[WPN][4];
+#pragma unroll
+    for (int c = 0; c < WPN; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float a = 0.f;
+#pragma unroll
+        for (int r = 0; r < WPM; ++r) {
+          const int rr = r * 16 + fr;
+          a += (rr >= lo && rr < hi) ? v[r][c][i] : 0.f;
+        }
+        s[c][i] = row16_sum(a);
+      }
+#pragma unroll
+    for (int c = 0; c < WPN; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float mu = s[c][i] / cnt;
+        float a = 0.f;
+#pragma unroll
+        for (int r = 0; r < WPM; ++r) {
+          const int rr = r * 16 + fr;
+          const float d = v[r][c][i] - mu;
+          a += (rr >= lo && rr < hi) ? d * d : 0.f;
+        }
+        q[c][i] = row16_sum(a);
+      }
+    if (fr == 0) {
+      float* ps = stats + ((t * 2 + slot) * 3) * N + chb + 4 * fq;
+#pragma unroll
+      for (int c = 0; c < WPN; ++c) {
+        *reinterpret_cast<float4*>(ps + c * 16) = make_float4(cnt, cnt, cnt, cnt);
+        *reinterpret_cast<float4*>(ps + N + c * 16) = make_float4(s[c][0], s[c][1], s[c][2], s[c][3]);
+        *reinterpret_cast<float4*>(ps + 2 * N + c * 16) = make_float4(q[c][0], q[c][1], q[c][2], q[c][3]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K-loop kernel
 
 template <int WPM, int WPN, int WM, int WN, int NS, int EPI>
 __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
@@ -136,18 +221,18 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 
-  // ---- epilogue. The fragments hold 4 channels of one pixel per lane; written straight
-  // to global memory that is 16 rows x 32 B per store instruction. Instead the tile goes
-  // through LDS (bf16, padded row pitch) and leaves as 16-byte-per-lane row segments
-  // (whole 128-B lines per 8 lanes); the statistics are read back from the same image.
+  // ---- epilogue. The fragments hold 4 channels of one pixel per lane; the tile goes through
+  // LDS (bf16, padded row pitch) and leaves as 16-byte-per-lane row segments (whole 128-B
+  // lines per 8 lanes). Statistics come from the registers (wave_stats).
   constexpr int TP = BN * 2 + 16;                       // LDS row pitch (bytes)
   constexpr int CPR = BN / 8;                           // 16-byte chunks per tile row
   constexpr int RL = 256 / CPR;                         // tile rows per pass of the workgroup
-  static_assert(BM * TP + 2 * 256 * 8 * 4 + 2 * BN * 4 <= NS * SB, "epilogue tile fits the ring");
+  static_assert(BM * TP <= NS * SB, "epilogue tile fits the ring");
   __syncthreads();                                      // every wave's last ring reads are done
   {
     const int mwl = wm * 16 * WPM;                      // first tile row of this wave
     const int nwl = wn * 16 * WPN + 4 * fq;             // first tile channel of this lane (c = 0)
+    float vs[WPM][WPN][4];
 #pragma unroll
     for (int r = 0; r < WPM; ++r) {
       const int m = m0 + mwl + r * 16 + fr;
@@ -167,89 +252,278 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
         o.x = static_cast<uint32_t>(f_to_bf16(v[0])) | (static_cast<uint32_t>(f_to_bf16(v[1])) << 16);
         o.y = static_cast<uint32_t>(f_to_bf16(v[2])) | (static_cast<uint32_t>(f_to_bf16(v[3])) << 16);
         *reinterpret_cast<uint2*>(lds + (mwl + r * 16 + fr) * TP + (nwl + c * 16) * 2) = o;
+        if constexpr (EPI == EPI_STATS) {
+          vs[r][c][0] = bf16_to_f(o.x & 0xffffu);
+          vs[r][c][1] = bf16_to_f(o.x >> 16);
+          vs[r][c][2] = bf16_to_f(o.y & 0xffffu);
+          vs[r][c][3] = bf16_to_f(o.y >> 16);
+        }
       }
     }
+    if constexpr (EPI == EPI_STATS)
+      if (m0 + mwl < M) wave_stats<WPM, WPN>(vs, m0 + mwl, M, rg, N, n0 + wn * 16 * WPN, stats);
   }
   __syncthreads();
   const int ck = threadIdx.x % CPR, rl = threadIdx.x / CPR;
   const int rows = M - m0 < BM ? M - m0 : BM;
-  float s0[8], s1[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { s0[i] = 0.f; s1[i] = 0.f; }
-  // worker groups of this tile (statistics): rows [m0, mb) -> slot 0, [mb, m0 + rows) -> slot 1
-  const int64_t gb = EPI == EPI_STATS ? (static_cast<int64_t>(m0) / rg + 1) * rg : 0;
-  const int rb = EPI == EPI_STATS ? (gb - m0 < rows ? static_cast<int>(gb - m0) : rows) : rows;
   for (int rr = rl; rr < rows; rr += RL) {
     const uint4 v = *reinterpret_cast<const uint4*>(lds + rr * TP + ck * 16);
     *reinterpret_cast<uint4*>(C + static_cast<int64_t>(m0 + rr) * N + n0 + ck * 8) = v;
-    if constexpr (EPI == EPI_STATS) {
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      const bool lo = rr < rb;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float a = bf16_to_f(w[i] & 0xffffu), b = bf16_to_f(w[i] >> 16);
-        s0[2 * i] += lo ? a : 0.f;
-        s0[2 * i + 1] += lo ? b : 0.f;
-        s1[2 * i] += lo ? 0.f : a;
-        s1[2 * i + 1] += lo ? 0.f : b;
-      }
-    }
-  }
-
-  if constexpr (EPI == EPI_STATS) {
-    // per-(slot, channel) totals over the RL row lanes: red[slot][rl][channel]
-    float* red = reinterpret_cast<float*>(lds + BM * TP);
-    float* mean = red + 2 * RL * BN;                    // [2][BN]
-    const float cnt0 = static_cast<float>(rb), cnt1 = static_cast<float>(rows - rb);
-    auto reduce = [&](float (&x0)[8], float (&x1)[8], int which) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        red[(0 * RL + rl) * BN + ck * 8 + i] = x0[i];
-        red[(1 * RL + rl) * BN + ck * 8 + i] = x1[i];
-      }
-      __syncthreads();
-      for (int i = threadIdx.x; i < 2 * BN; i += 256) {
-        const int slot = i / BN, ch = i - slot * BN;
-        float t = 0.f;
-        for (int l = 0; l < RL; ++l) t += red[(slot * RL + l) * BN + ch];
-        const float cnt = slot ? cnt1 : cnt0;
-        if (which == 0) mean[i] = cnt > 0.f ? t / cnt : 0.f;
-        if (cnt > 0.f) stats[((static_cast<int64_t>(tm) * 2 + slot) * 2 + which) * N + n0 + ch] = t;
-      }
-      __syncthreads();
-    };
-    reduce(s0, s1, 0);
-    float mu0[8], mu1[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      mu0[i] = mean[ck * 8 + i];
-      mu1[i] = mean[BN + ck * 8 + i];
-      s0[i] = 0.f;
-      s1[i] = 0.f;
-    }
-    for (int rr = rl; rr < rows; rr += RL) {
-      const uint4 v = *reinterpret_cast<const uint4*>(lds + rr * TP + ck * 16);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      const bool lo = rr < rb;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const float x = bf16_to_f(h ? (w[i] >> 16) : (w[i] & 0xffffu));
-          const float d0 = x - mu0[2 * i + h], d1 = x - mu1[2 * i + h];
-          s0[2 * i + h] += lo ? d0 * d0 : 0.f;
-          s1[2 * i + h] += lo ? 0.f : d1 * d1;
-        }
-      }
-    }
-    reduce(s0, s1, 1);
   }
 }
 
-// Merge of one worker's tile statistics (Chan et al.): 64 channels x 16 tile lanes per
-// workgroup, each lane folding every 16th tile of the worker (all its loads issued
-// before they are used), the 16 lane partials merged in a fixed order through LDS.
-constexpr int kMergeCh = 64, kMergeLanes = 16;
+// ---------------------------------------------------------------------------------------------
+// Weight-stationary persistent kernel (K = 64 * KB <= 256)
+//
+// LDS: [KB][BN][128 B] weights | 2 x [KB][BM][128 B] row-tile ring | 4 x [RW][128 B] wave slices.
+// The row tiles are dealt in CHUNKS of `per` consecutive tiles: block b streams N slice
+// tn = (b / 8) % tiles_n and chunks p, p + P, ... with p = b % 8 + 8 * (b / (8 * tiles_n)), so
+// the tiles_n blocks that read the same row tiles have equal b % 8 (one XCD under the
+// round-robin placement; a speed choice only). Tile t + 1 is in flight while tile t is
+// multiplied and written.
+// EPI_STATS: each wave accumulates, over the whole chunk, the shifted sums Σ(y - s), Σ(y - s)²
+// of its stored bf16 values per channel in registers (s: the wave's first stored row of the
+// chunk), and reduces them over the 16 lanes of a DPP row only when the chunk (or the worker)
+// ends: one statistics tile per chunk (H = per * BM rows), one entry per wave row (E = WM).
+template <int BN, int RW, int KB, int EPI>
+__global__ __launch_bounds__(256) void k_gemm_ws(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                 int M, int N, uint16_t* __restrict__ C,
+                                                 const uint16_t* __restrict__ add, float* __restrict__ stats,
+                                                 int64_t rg, int tiles_m, int P, int per, int nchunks) {
+  constexpr int WN = BN / 64, WM = 4 / WN, BM = WM * RW, WPM = RW / 16, K = KB * 64;
+  static_assert(WN * WM == 4 && RW % 16 == 0 && BM % 32 == 0, "4 waves of RW x 64");
+  constexpr int BB = BN * K * 2, AB = BM * K * 2, EB = RW * 128;
+  constexpr int AI = BM * KB / 32, BI = BN * KB / 32;   // glds per wave: a row tile / the weights
+  __shared__ __attribute__((aligned(16))) char lds[BB + 2 * AB + 4 * EB];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tiles_n = N / BN;
+  const int b = blockIdx.x;
+  const int tn = (b >> 3) % tiles_n;
+  const int p = (b & 7) + 8 * (b / (8 * tiles_n));
+  if (p >= nchunks) return;                             // whole workgroup: before any barrier
+  const int n0 = tn * BN;
+  const int lrow = lane >> 3, lchunk = lane & 7;
+  char* const el = lds + BB + 2 * AB + wave * EB;
+
+#pragma unroll
+  for (int u = 0; u < BI; ++u) {
+    const int q = wave * BI + u, kb = q / (BN / 8), rb = q - kb * (BN / 8);
+    const uint16_t* src = B + static_cast<int64_t>(n0 + rb * 8 + lrow) * K + kb * 64 + (lchunk ^ lrow) * 8;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), (lds_ptr)(lds + kb * BN * 128 + rb * 1024),
+                                     16, 0, 0);
+  }
+  const uint16_t* az = reinterpret_cast<const uint16_t*>(g_gemm_zero) + lchunk * 8;
+  auto issue = [&](int tm, int slot) {
+    const int m0 = tm * BM;
+#pragma unroll
+    for (int u = 0; u < AI; ++u) {
+      const int q = wave * AI + u, kb = q / (BM / 8), rb = q - kb * (BM / 8);
+      const int row = m0 + rb * 8 + lrow;
+      const uint16_t* src = row < M ? A + static_cast<int64_t>(row) * K + kb * 64 + (lchunk ^ lrow) * 8 : az;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                       (lds_ptr)(lds + BB + slot * AB + kb * BM * 128 + rb * 1024), 16, 0, 0);
+    }
+  };
+
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nc = n0 + wn * 64;
+
+  // statistics state of this wave (EPI_STATS)
+  float sh[4][4] = {}, sd[4][4], sq[4][4];
+  int cs = 0, cnt = 0;
+  bool have_shift = false;
+  int64_t gb = 0, c1 = 0;
+  auto reset = [&]() {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sd[c][i] = sq[c][i] = 0.f;
+    cnt = 0;
+  };
+  auto flush = [&](int T) {
+    const float n = static_cast<float>(cnt);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sd[c][i] = row16_sum(sd[c][i]);
+        sq[c][i] = row16_sum(sq[c][i]);
+      }
+    if (fr == 0) {
+      float* ps = stats + ((static_cast<int64_t>(T) * WM + wm) * 2 + cs) * 3 * N + nc + 4 * fq;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float sy[4], m2[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sy[i] = sd[c][i] + n * sh[c][i];
+          m2[i] = cnt > 0 ? fmaxf(sq[c][i] - sd[c][i] * sd[c][i] / n, 0.f) : 0.f;
+        }
+        *reinterpret_cast<float4*>(ps + c * 16) = make_float4(n, n, n, n);
+        *reinterpret_cast<float4*>(ps + N + c * 16) = make_float4(sy[0], sy[1], sy[2], sy[3]);
+        *reinterpret_cast<float4*>(ps + 2 * N + c * 16) = make_float4(m2[0], m2[1], m2[2], m2[3]);
+      }
+    }
+    reset();
+  };
+  // rows [mlo, mhi) of this wave's tile rows r0 + r*16 + fr join the current slot's sums
+  auto accumulate = [&](const uint32_t (&pk)[WPM][4][2], int r0, int64_t mlo, int64_t mhi) {
+    const int64_t a = r0 > mlo ? r0 : mlo;
+    const int64_t z = r0 + RW < mhi ? r0 + RW : mhi;
+    if (z <= a) return;
+    cnt += static_cast<int>(z - a);
+    const bool full = a == r0 && z == r0 + RW;
+#pragma unroll
+    for (int r = 0; r < WPM; ++r) {
+      const int m = r0 + r * 16 + fr;
+      const float w = (full || (m >= mlo && m < mhi)) ? 1.f : 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t h = pk[r][c][i >> 1];
+          const float y = bf16_to_f((i & 1) ? (h >> 16) : (h & 0xffffu));
+          const float d = (y - sh[c][i]) * w;
+          sd[c][i] += d;
+          sq[c][i] = fmaf(d, d, sq[c][i]);
+        }
+    }
+  };
+
+  int T = p, tm = p * per;
+  issue(tm, 0);
+  int slot = 0;
+  if constexpr (EPI == EPI_STATS) {
+    reset();
+    const int64_t c0 = static_cast<int64_t>(T) * per * BM;
+    c1 = c0 + static_cast<int64_t>(per) * BM < M ? c0 + static_cast<int64_t>(per) * BM : M;
+    gb = (c0 / rg + 1) * rg;
+    cs = 0;
+    have_shift = false;
+  }
+  while (true) {
+    // this tile's rows (and the weights) have landed for every wave; every wave is done
+    // reading the other slot (the previous tile), which is refilled next
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int T2 = T, tm2 = tm + 1;
+    const int cend = (T + 1) * per < tiles_m ? (T + 1) * per : tiles_m;
+    if (tm2 >= cend) {
+      T2 = T + P;
+      tm2 = T2 * per;
+    }
+    const bool more = T2 < nchunks;
+    if (more) issue(tm2, slot ^ 1);
+    f32x4 acc[WPM][4];
+#pragma unroll
+    for (int r = 0; r < WPM; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* as = lds + BB + slot * AB;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int chunk = (ks * 4 + fq) ^ (fr & 7);
+        bf16x8 wf[4], xf[WPM];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          wf[c] = *reinterpret_cast<const bf16x8*>(lds + kb * BN * 128 + (wn * 64 + c * 16 + fr) * 128 + chunk * 16);
+#pragma unroll
+        for (int r = 0; r < WPM; ++r)
+          xf[r] = *reinterpret_cast<const bf16x8*>(as + kb * BM * 128 + (wm * RW + r * 16 + fr) * 128 + chunk * 16);
+#pragma unroll
+        for (int r = 0; r < WPM; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], xf[r], acc[r][c], 0, 0, 0);
+      }
+
+    // ---- wave-private epilogue: rows r0 .. r0 + RW, channels nc .. nc + 64
+    const int r0 = tm * BM + wm * RW;
+    uint32_t pk[WPM][4][2];
+#pragma unroll
+    for (int r = 0; r < WPM; ++r) {
+      const int rr = r * 16 + fr;
+      const int m = r0 + rr;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float v[4] = {acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]};
+        if constexpr (EPI == EPI_ADD) {
+          if (m < M) {
+            const uint2 a = *reinterpret_cast<const uint2*>(add + static_cast<int64_t>(m) * N + nc + c * 16 + 4 * fq);
+            v[0] += bf16_to_f(a.x & 0xffffu);
+            v[1] += bf16_to_f(a.x >> 16);
+            v[2] += bf16_to_f(a.y & 0xffffu);
+            v[3] += bf16_to_f(a.y >> 16);
+          }
+        }
+        pk[r][c][0] = pack_bf16x2(v[0], v[1]);
+        pk[r][c][1] = pack_bf16x2(v[2], v[3]);
+        const int ch16 = (c * 2 + (fq >> 1)) ^ (rr & 7);                // swizzled 16-B chunk of the row
+        *reinterpret_cast<uint2*>(el + rr * 128 + ch16 * 16 + (fq & 1) * 8) = make_uint2(pk[r][c][0], pk[r][c][1]);
+      }
+    }
+    // LDS accesses of one wave execute in order: the slice written above is read back
+    // whole-line by the same wave (compiler ordering pinned by the clobber)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < RW / 8; ++it) {
+      const int rr = it * 8 + lrow;
+      const uint4 v = *reinterpret_cast<const uint4*>(el + rr * 128 + ((lchunk ^ (rr & 7)) * 16));
+      if (r0 + rr < M) *reinterpret_cast<uint4*>(C + static_cast<int64_t>(r0 + rr) * N + nc + lchunk * 8) = v;
+    }
+
+    if constexpr (EPI == EPI_STATS) {
+      if (!have_shift && r0 < M) {                      // the wave's first stored row of the chunk
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t h = pk[0][c][i >> 1];
+            const float y = bf16_to_f((i & 1) ? (h >> 16) : (h & 0xffffu));
+            sh[c][i] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, y), 0x150,
+                                                                             0xF, 0xF, false));   // row_newbcast:0
+          }
+        have_shift = true;
+      }
+      if (cs == 0) {
+        const int64_t hi0 = gb < c1 ? gb : c1;
+        accumulate(pk, r0, static_cast<int64_t>(T) * per * BM, hi0);
+        if (gb < c1 && r0 + RW > gb) {                  // the worker boundary falls in this tile
+          flush(T);
+          cs = 1;
+        }
+      }
+      if (cs == 1) accumulate(pk, r0, gb, c1);
+      if (T2 != T || !more) {                           // chunk ends: its last slot
+        flush(T);
+        if (gb < c1 && cs == 0) {                       // a straddling chunk whose second worker's
+          cs = 1;                                       // rows this wave never held: n = 0 entry
+          flush(T);
+        }
+        if (more) {
+          const int64_t c0 = static_cast<int64_t>(T2) * per * BM;
+          c1 = c0 + static_cast<int64_t>(per) * BM < M ? c0 + static_cast<int64_t>(per) * BM : M;
+          gb = (c0 / rg + 1) * rg;
+          cs = 0;
+          have_shift = false;
+        }
+      }
+    }
+    if (!more) break;
+    T = T2;
+    tm = tm2;
+    slot ^= 1;
+  }
+}
+
+// Merge of one worker's tile statistics (Chan et al.): 16 channels x 64 lanes per workgroup,
+// each lane folding every 64th (tile, entry) of the worker (four loads in flight before they are
+// used), the 64 lane partials merged by a fixed-order tree in LDS (deterministic).
+constexpr int kMergeCh = 16, kMergeLanes = 64;
 
 __device__ __forceinline__ void chan_merge(float& n, float& mu, float& m2, float nb, float mub, float m2b) {
   if (nb <= 0.f) return;
@@ -261,7 +535,7 @@ __device__ __forceinline__ void chan_merge(float& n, float& mu, float& m2, float
 }
 
 __global__ __launch_bounds__(kMergeCh * kMergeLanes) void k_finalize_tiles(
-    const float* __restrict__ stats, int BM, int64_t M, int64_t rg, int C, const float* __restrict__ gamma,
+    const float* __restrict__ stats, int H, int E, int64_t M, int64_t rg, int C, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ mean, float* __restrict__ istd,
     float* __restrict__ scale, float* __restrict__ shift) {
   __shared__ float sn[kMergeLanes][kMergeCh], smu[kMergeLanes][kMergeCh], sm2[kMergeLanes][kMergeCh];
@@ -269,23 +543,24 @@ __global__ __launch_bounds__(kMergeCh * kMergeLanes) void k_finalize_tiles(
   const int c = blockIdx.x * kMergeCh + tc;
   const int g = blockIdx.y;
   const int64_t g0 = static_cast<int64_t>(g) * rg, g1 = g0 + rg < M ? g0 + rg : M;
-  const int64_t t_lo = g0 / BM, t_hi = (g1 - 1) / BM;
+  const int64_t t_lo = g0 / H, t_hi = (g1 - 1) / H;
+  const int64_t nent = (t_hi - t_lo + 1) * E;          // (tile, entry) pairs of this worker
   float n = 0.f, mu = 0.f, m2 = 0.f;
   if (c < C) {
-    for (int64_t t0 = t_lo + lane; t0 <= t_hi; t0 += kMergeLanes * 4) {
+    for (int64_t i0 = lane; i0 < nent; i0 += kMergeLanes * 4) {
       float sv[4], qv[4], nv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int64_t t = t0 + static_cast<int64_t>(u) * kMergeLanes;
+        const int64_t i = i0 + static_cast<int64_t>(u) * kMergeLanes;
         nv[u] = 0.f;
         sv[u] = qv[u] = 0.f;
-        if (t <= t_hi) {
-          const int64_t lo = t * BM > g0 ? t * BM : g0;
-          const int64_t hi = (t + 1) * BM < g1 ? (t + 1) * BM : g1;
-          const int slot = t * BM < g0 ? 1 : 0;   // the tile started in the previous worker
-          nv[u] = static_cast<float>(hi - lo);
-          sv[u] = stats[((t * 2 + slot) * 2 + 0) * C + c];
-          qv[u] = stats[((t * 2 + slot) * 2 + 1) * C + c];
+        if (i < nent) {
+          const int64_t t = t_lo + i / E, e = i - (i / E) * E;
+          const int slot = t * H < g0 ? 1 : 0;          // the tile started in the previous worker
+          const float* p = stats + ((t * E + e) * 2 + slot) * 3 * C + c;
+          nv[u] = p[0];
+          sv[u] = p[C];
+          qv[u] = p[2 * C];
         }
       }
 #pragma unroll
@@ -296,9 +571,19 @@ __global__ __launch_bounds__(kMergeCh * kMergeLanes) void k_finalize_tiles(
   smu[lane][tc] = mu;
   sm2[lane][tc] = m2;
   __syncthreads();
+#pragma unroll
+  for (int h = kMergeLanes / 2; h >= 1; h >>= 1) {
+    if (lane < h) {
+      float a = sn[lane][tc], b = smu[lane][tc], q = sm2[lane][tc];
+      chan_merge(a, b, q, sn[lane + h][tc], smu[lane + h][tc], sm2[lane + h][tc]);
+      sn[lane][tc] = a;
+      smu[lane][tc] = b;
+      sm2[lane][tc] = q;
+    }
+    __syncthreads();
+  }
   if (lane != 0 || c >= C) return;
-  float N0 = sn[0][tc], MU = smu[0][tc], M2 = sm2[0][tc];
-  for (int l = 1; l < kMergeLanes; ++l) chan_merge(N0, MU, M2, sn[l][tc], smu[l][tc], sm2[l][tc]);
+  const float N0 = sn[0][tc], MU = smu[0][tc], M2 = sm2[0][tc];
   float var = N0 > 0.f ? M2 / N0 : 0.f;
   var = var > 0.f ? var : 0.f;
   const float is = rsqrtf(var + eps);
@@ -326,30 +611,211 @@ void launch_cfg(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint1
                        add, stats, rg);
 }
 
-// tile configurations: {BM, BN}
+constexpr int ws_bm(int BN, int RW) { return (4 / (BN / 64)) * RW; }
+constexpr int ws_lds(int BN, int RW, int KB) { return BN * KB * 128 + 2 * ws_bm(BN, RW) * KB * 128 + 4 * RW * 128; }
+constexpr int ws_occ(int lds) { return (160 * 1024) / lds >= 2 ? 2 : 1; }
+
+// Chunking of a weight-stationary launch: P persistent blocks per N slice (a multiple of 8),
+// chunks of `per` row tiles; with statistics (rg > 0) a chunk spans at most rg rows.
+struct WsPlan {
+  int P, per, nchunks, tiles_m, bm;
+};
+WsPlan ws_plan(int BN, int RW, int KB, int64_t M, int N, int64_t rg) {
+  WsPlan w{};
+  w.bm = ws_bm(BN, RW);
+  w.tiles_m = static_cast<int>((M + w.bm - 1) / w.bm);
+  const int tiles_n = N / BN;
+  const int P0 = (256 * ws_occ(ws_lds(BN, RW, KB)) + tiles_n - 1) / tiles_n;
+  w.per = (w.tiles_m + P0 - 1) / P0;
+  if (rg > 0) {
+    const int cap = static_cast<int>(rg / w.bm);
+    w.per = w.per < cap ? w.per : cap;
+  }
+  if (w.per < 1) w.per = 1;
+  w.nchunks = (w.tiles_m + w.per - 1) / w.per;
+  const int P = w.nchunks < P0 ? w.nchunks : P0;
+  w.P = (P + 7) / 8 * 8;
+  return w;
+}
+
+template <int BN, int RW, int KB>
+void launch_ws(const uint16_t* A, const uint16_t* B, int M, int N, uint16_t* C, const uint16_t* add, float* stats,
+               int64_t rg, hipStream_t stream) {
+  static_assert(ws_lds(BN, RW, KB) <= 160 * 1024, "LDS");
+  const WsPlan w = ws_plan(BN, RW, KB, M, N, stats ? rg : 0);
+  const dim3 grid(w.P * (N / BN));
+  if (stats)
+    hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_STATS>), grid, dim3(256), 0, stream, A, B, M, N, C, add, stats, rg,
+                       w.tiles_m, w.P, w.per, w.nchunks);
+  else if (add)
+    hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_ADD>), grid, dim3(256), 0, stream, A, B, M, N, C, add, stats, rg,
+                       w.tiles_m, w.P, w.per, w.nchunks);
+  else
+    hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_PLAIN>), grid, dim3(256), 0, stream, A, B, M, N, C, add, stats, rg,
+                       w.tiles_m, w.P, w.per, w.nchunks);
+}
+
+template <int BN, int RW>
+void launch_ws_k(int K, const uint16_t* A, const uint16_t* B, int M, int N, uint16_t* C, const uint16_t* add,
+                 float* stats, int64_t rg, hipStream_t stream) {
+  switch (K) {
+    case 64: launch_ws<BN, RW, 1>(A, B, M, N, C, add, stats, rg, stream); break;
+    case 128: launch_ws<BN, RW, 2>(A, B, M, N, C, add, stats, rg, stream); break;
+    default:
+      if constexpr (BN <= 128 && ws_lds(BN, RW, 4) <= 160 * 1024) launch_ws<BN, RW, 4>(A, B, M, N, C, add, stats, rg, stream);
+      break;
+  }
+}
+
+// tile configurations: K-loop {BM, BN, stats rows} 0..8, weight-stationary {BN, RW} 9..14
+constexpr int kNumNt = 9;
 constexpr int kCfgBM[] = {128, 256, 64, 64, 64, 128, 128, 64, 32};
 constexpr int kCfgBN[] = {128, 64, 128, 256, 64, 256, 128, 64, 256};
-constexpr int kNumCfg = 9;
+constexpr int kCfgSR[] = {64, 64, 32, 64, 32, 64, 64, 32, 32};
+constexpr int kWsBN[] = {256, 256, 128, 128, 64, 64};
+constexpr int kWsRW[] = {32, 64, 16, 32, 16, 32};
+constexpr int kNumCfg = kNumNt + 6;
+
+bool ws_fits(int i, int K) {
+  const int kb = K / 64;
+  if (K % 64 || kb < 1 || kb > 4 || kb == 3) return false;
+  if (kWsBN[i] * K * 2 > 64 * 1024) return false;     // the weight slice stays <= 64 KB of LDS
+  return ws_lds(kWsBN[i], kWsRW[i], kb) <= 160 * 1024;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Transposes of many bf16 matrices in one launch: dst_j [C_j, R_j] = src_j [R_j, C_j]ᵀ (the
+// data-gradient GEMMs' B = Wᵀ of every 1x1 convolution, refreshed once per step). 64 x 64 tiles
+// through LDS (padded pitch), 16-byte loads and stores; R_j, C_j multiples of 8.
+struct TJob {
+  const uint16_t* src;
+  uint16_t* dst;
+  int R, C;
+  int tile0;               // first tile of this job in the launch
+};
+constexpr int kTJobs = 40;
+struct TTable {
+  TJob j[kTJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void k_transpose_multi(TTable t) {
+  __shared__ uint16_t tile[64][64 + 8];
+  int ji = 0;
+  while (ji + 1 < t.n && static_cast<int>(blockIdx.x) >= t.j[ji + 1].tile0) ++ji;
+  const TJob jb = t.j[ji];
+  const int tl = blockIdx.x - jb.tile0;
+  const int tcol = (jb.C + 63) / 64;
+  const int r0 = (tl / tcol) * 64, c0 = (tl % tcol) * 64;
+  const int lr = threadIdx.x >> 3, lc = (threadIdx.x & 7) * 8;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int r = r0 + lr + 32 * k, c = c0 + lc;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r < jb.R && c < jb.C) v = *reinterpret_cast<const uint4*>(jb.src + static_cast<int64_t>(r) * jb.C + c);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      tile[lr + 32 * k][lc + 2 * e] = static_cast<uint16_t>(w[e] & 0xffffu);
+      tile[lr + 32 * k][lc + 2 * e + 1] = static_cast<uint16_t>(w[e] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = c0 + lr + 32 * k, r = r0 + lc;     // dst row c, columns r .. r + 8
+    if (c < jb.C && r < jb.R) {
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        w[e] = static_cast<uint32_t>(tile[lc + 2 * e][lr + 32 * k]) |
+               (static_cast<uint32_t>(tile[lc + 2 * e + 1][lr + 32 * k]) << 16);
+      *reinterpret_cast<uint4*>(jb.dst + static_cast<int64_t>(c) * jb.R + r) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
 
 }  // namespace
 
-int gemm_nt_tile_m(int cfg) { return (cfg >= 0 && cfg < kNumCfg) ? kCfgBM[cfg] : 0; }
-int gemm_nt_tile_n(int cfg) { return (cfg >= 0 && cfg < kNumCfg) ? kCfgBN[cfg] : 0; }
+void transpose_multi(const uint16_t* const* srcs, uint16_t* const* dsts, const int* R, const int* C, int count,
+                     hipStream_t stream) {
+  for (int b = 0; b < count; b += kTJobs) {
+    TTable t{};
+    int tiles = 0;
+    t.n = count - b < kTJobs ? count - b : kTJobs;
+    for (int i = 0; i < t.n; ++i) {
+      t.j[i] = TJob{srcs[b + i], dsts[b + i], R[b + i], C[b + i], tiles};
+      tiles += ((R[b + i] + 63) / 64) * ((C[b + i] + 63) / 64);
+    }
+    if (tiles > 0) hipLaunchKernelGGL(k_transpose_multi, dim3(tiles), dim3(256), 0, stream, t);
+  }
+}
+
+int gemm_nt_num_cfg() { return kNumCfg; }
+
+bool gemm_nt_valid(int cfg, int N, int K) {
+  if (cfg < 0 || cfg >= kNumCfg || K % 64 || K <= 0) return false;
+  if (cfg < kNumNt) return N % kCfgBN[cfg] == 0;
+  return N % kWsBN[cfg - kNumNt] == 0 && ws_fits(cfg - kNumNt, K);
+}
+
+int gemm_nt_tile_m(int cfg) {
+  if (cfg >= 0 && cfg < kNumNt) return kCfgBM[cfg];
+  if (cfg >= kNumNt && cfg < kNumCfg) return (4 / (kWsBN[cfg - kNumNt] / 64)) * kWsRW[cfg - kNumNt];
+  return 0;
+}
+int gemm_nt_tile_n(int cfg) {
+  if (cfg >= 0 && cfg < kNumNt) return kCfgBN[cfg];
+  if (cfg >= kNumNt && cfg < kNumCfg) return kWsBN[cfg - kNumNt];
+  return 0;
+}
+int gemm_nt_stats_rows(int cfg) {
+  if (cfg >= 0 && cfg < kNumNt) return kCfgSR[cfg];
+  if (cfg >= kNumNt && cfg < kNumCfg) return ws_bm(kWsBN[cfg - kNumNt], kWsRW[cfg - kNumNt]);
+  return 0;
+}
+
+void gemm_nt_stats_geometry(int cfg, int64_t M, int N, int K, int64_t rg, int64_t* H, int* E) {
+  if (cfg >= 0 && cfg < kNumNt) {
+    *H = kCfgSR[cfg];
+    *E = 1;
+    return;
+  }
+  const int i = cfg - kNumNt;
+  const WsPlan w = ws_plan(kWsBN[i], kWsRW[i], K / 64, M, N, rg);
+  *H = static_cast<int64_t>(w.per) * w.bm;
+  *E = 4 / (kWsBN[i] / 64);
+}
 
 int gemm_nt_pick(int64_t M, int N, int K, int64_t rg_limit) {
-  // largest tile that still gives >= 512 workgroups (2 per CU); BN never above N;
-  // with statistics a tile must not span more than two workers (BM <= rows per worker)
+  // K <= 256: the weight-stationary kernel, widest weight slice, then the row height whose
+  // LDS admits two workgroups per CU where there is one
+  if (K <= 256) {
+    int best = -1, best_occ = 0;
+    for (int i = 0; i < 6; ++i) {
+      const int cfg = kNumNt + i;
+      if (!gemm_nt_valid(cfg, N, K) || (rg_limit > 0 && ws_bm(kWsBN[i], kWsRW[i]) > rg_limit)) continue;
+      if (best >= 0 && kWsBN[i] < kWsBN[best - kNumNt]) break;
+      const int occ = (160 * 1024) / ws_lds(kWsBN[i], kWsRW[i], K / 64) >= 2 ? 2 : 1;
+      if (best < 0 || occ > best_occ || (occ == best_occ && kWsRW[i] > kWsRW[best - kNumNt] && M >= 32000)) {
+        best = cfg;
+        best_occ = occ;
+      }
+    }
+    if (best >= 0) return best;
+  }
+  // K-loop: largest tile that still gives >= 512 workgroups (2 per CU); BN never above N;
+  // with statistics a wave's stats tile must not span more than two workers
   static const int order[] = {5, 0, 1, 3, 2, 4};
   int best = -1;
   int64_t best_wg = -1;
   for (int cfg : order) {
     const int bm = kCfgBM[cfg], bn = kCfgBN[cfg];
-    if (N % bn != 0 || (rg_limit > 0 && bm > rg_limit)) continue;
+    if (N % bn != 0 || (rg_limit > 0 && kCfgSR[cfg] > rg_limit)) continue;
     const int64_t wg = ((M + bm - 1) / bm) * (N / bn);
     if (wg >= 512) return cfg;
     if (wg > best_wg) { best_wg = wg; best = cfg; }
   }
-  (void)K;
   return best;
 }
 
@@ -365,16 +831,22 @@ void gemm_nt(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t
     case 2: launch_cfg<2, 4, 2, 2, 3>(A, B, M, N, K, C, add, stats, rg, stream); break;
     case 3: launch_cfg<4, 4, 1, 4, 2>(A, B, M, N, K, C, add, stats, rg, stream); break;
     case 4: launch_cfg<2, 2, 2, 2, 4>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    default: launch_cfg<4, 8, 2, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream); break;
+    case 5: launch_cfg<4, 8, 2, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream); break;
+    case 9: launch_ws_k<256, 32>(K, A, B, M, N, C, add, stats, rg, stream); break;
+    case 10: launch_ws_k<256, 64>(K, A, B, M, N, C, add, stats, rg, stream); break;
+    case 11: launch_ws_k<128, 16>(K, A, B, M, N, C, add, stats, rg, stream); break;
+    case 12: launch_ws_k<128, 32>(K, A, B, M, N, C, add, stats, rg, stream); break;
+    case 13: launch_ws_k<64, 16>(K, A, B, M, N, C, add, stats, rg, stream); break;
+    default: launch_ws_k<64, 32>(K, A, B, M, N, C, add, stats, rg, stream); break;
   }
 }
 
-void bn_finalize_tiles(const float* stats, int BM, int64_t M, int64_t rg, int groups, int C, const float* gamma,
-                       const float* beta, float eps, float* mean, float* istd, float* scale, float* shift,
-                       hipStream_t stream) {
+void bn_finalize_tiles(const float* stats, int64_t H, int E, int64_t M, int64_t rg, int groups, int C,
+                       const float* gamma, const float* beta, float eps, float* mean, float* istd, float* scale,
+                       float* shift, hipStream_t stream) {
   const dim3 grid((C + kMergeCh - 1) / kMergeCh, groups);
-  hipLaunchKernelGGL(k_finalize_tiles, grid, dim3(kMergeCh * kMergeLanes), 0, stream, stats, BM, M, rg, C, gamma,
-                     beta, eps, mean, istd, scale, shift);
+  hipLaunchKernelGGL(k_finalize_tiles, grid, dim3(kMergeCh * kMergeLanes), 0, stream, stats, static_cast<int>(H), E, M,
+                     rg, C, gamma, beta, eps, mean, istd, scale, shift);
 }
 
 }  // namespace gpu

@@ -72,12 +72,13 @@ WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0")
 # layer3/layer4), whose kernels are latency-bound and leave most CUs idle
 WGRAD_STREAM_ROWS = int(os.environ.get("GARFIELD_WGRAD_STREAM_ROWS", "8000"))
 XENT = os.environ.get("GARFIELD_XENT", "1") != "0"   # fused per-worker cross-entropy kernel
-# Forward 1x1 convolutions with <= GEMM_NT_MAXN output channels on the hand-written MFMA GEMM
-# (gemm_nt.hip), which also emits the next BatchNorm's per-worker statistics (no partial pass).
-# Measured per shape against hipBLASLt (scripts/bench_1x1.py, profiles/r2/bench_1x1_r2.log):
-# 1.1-1.4x faster alone for N <= 128, slower above; but in the graphed step N <= 128 measured
-# 6.99 vs 6.96 ms/step (profiles/r2/ab_gemm_nt.log), so it is off by default (0).
-GEMM_NT_MAXN = int(os.environ.get("GARFIELD_GEMM_NT_MAXN", "0"))
+# 1x1 stride-1 convolutions (forward and data gradient) on the hand-written MFMA GEMMs of
+# gemm_nt.hip instead of hipBLASLt: the weight-stationary persistent kernel for K <= 256, the
+# K-loop kernel otherwise. The forward also emits the next (large-layer) BatchNorm's
+# per-worker statistics from its registers, so that BatchNorm runs no partial-sum pass.
+# "0" keeps hipBLASLt (torch.mm / addmm_).
+GEMM_NT = os.environ.get("GARFIELD_GEMM_NT", "1") != "0"
+GEMM_NT_DGRAD = os.environ.get("GARFIELD_GEMM_NT_DGRAD", "1") != "0"
 # split-K weight-gradient sums of every layer deferred to one launch after the backward
 SPLIT_DEFER = os.environ.get("GARFIELD_SPLIT_DEFER", "1") != "0"
 
@@ -239,7 +240,7 @@ class BNState:
         self.groups = groups
         self.C = bn.num_features
         self.mean = self.istd = self.scale = self.shift = None
-        self.tile = None          # (stats, BM): statistics of the next input, from the producing GEMM
+        self.tile = None          # (stats, H, E): statistics of the next input, from the producing GEMM
 
     def ensure(self, device, dtype=torch.float32) -> None:
         if self.mean is None or self.mean.device != device or self.mean.dtype != dtype:
@@ -366,7 +367,7 @@ class _GroupedBN(torch.autograd.Function):
                               bn.running_mean if track else None, bn.running_var if track else None,
                               part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu, relu_state, defer,
                               tile_stats=tile[0] if tile is not None else None,
-                              tile_m=tile[1] if tile is not None else 0)
+                              tile_m=tile[1] if tile is not None else 0, tile_e=tile[2] if tile is not None else 1)
             if defer:
                 ws.running_jobs.append((st.mean, st.istd, bn.running_mean, bn.running_var, rg, float(bn.eps),
                                         float(bn.momentum)))
@@ -436,35 +437,124 @@ class ConvSpec:
                      and self.dilation == (1, 1))
         self.bn_next = None       # BNState of the BatchNorm that consumes this convolution's output
         self.wpad = None          # persistent zero-padded [Cout, Kp] weight matrix (im2col + GEMM layers)
+        self.wt = None            # [Cin, Cout] transposed 1x1 weight of the data-gradient GEMM (refresh_dgrad_weights)
+
+
+def _gemm_nt_ok(a2: torch.Tensor, b2: torch.Tensor) -> bool:
+    M, K = a2.shape
+    N = b2.shape[0]
+    return (a2.is_cuda and a2.dtype == torch.bfloat16 and b2.dtype == torch.bfloat16 and K % 64 == 0
+            and N % 64 == 0 and b2.shape[1] == K and a2.is_contiguous() and b2.is_contiguous()
+            and M * max(K, N) < 2 ** 31)
+
+
+# Configuration of each gemm_nt problem, measured once: key (M, N, K, rg or 0, add) -> cfg. The
+# step's first (eager) run times every valid tile configuration on the real operands (scratch
+# outputs, 3 calls each after a warm call) and keeps the fastest; graph captures and replays
+# reuse it. GARFIELD_GEMM_TUNE=0 takes the static choice of gemm_nt_pick instead.
+GEMM_TUNE = os.environ.get("GARFIELD_GEMM_TUNE", "1") != "0"
+_GEMM_CFG: dict = {}
+
+
+def _gemm_cfg(a2: torch.Tensor, b2: torch.Tensor, rg: int, add: torch.Tensor | None) -> int:
+    C_ = _native.native()
+    M, K = a2.shape
+    N = b2.shape[0]
+    key = (M, N, K, rg, add is not None)
+    cfg = _GEMM_CFG.get(key)
+    if cfg is not None:
+        return cfg
+    cfg = C_.gemm_nt_pick(M, N, K, rg)
+    if not GEMM_TUNE or cfg < 0 or torch.cuda.is_current_stream_capturing():
+        return cfg
+    cands = [c for c in range(C_.gemm_nt_num_cfg())
+             if C_.gemm_nt_valid(c, N, K) and (rg == 0 or C_.gemm_nt_stats_rows(c) <= rg)]
+    out = torch.empty((M, N), dtype=a2.dtype, device=a2.device)
+    addc = add.clone() if add is not None else None
+    best, best_t = cfg, float("inf")
+    for c in cands:
+        st = torch.empty(C_.gemm_nt_stats_geometry(c, M, N, K, rg)[2], device=a2.device) if rg else None
+        C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c)   # warm
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(3):
+            C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c)
+        t1.record()
+        t1.synchronize()
+        t = t0.elapsed_time(t1)
+        if t < best_t:
+            best, best_t = c, t
+    _GEMM_CFG[key] = best
+    return best
 
 
 def _gemm_nt_forward(x2: torch.Tensor, w2: torch.Tensor, spec: ConvSpec):
-    """y = x2 · w2ᵀ on gemm_nt.hip when it is the faster kernel for the shape (N <= GEMM_NT_MAXN,
-    K % 64 == 0); with ``spec.bn_next`` (the BatchNorm that consumes y, a large-layer one) the
-    kernel also writes that BatchNorm's per-worker tile statistics. None: use hipBLASLt."""
-    N, K = w2.shape
-    if not (x2.is_cuda and x2.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16 and N <= GEMM_NT_MAXN
-            and K % 64 == 0 and N % 64 == 0 and x2.is_contiguous() and w2.is_contiguous()):
+    """y = x2 · w2ᵀ on gemm_nt.hip; with ``spec.bn_next`` (the BatchNorm that consumes y, a
+    large-layer one) the kernel also writes that BatchNorm's per-worker tile statistics.
+    None: use hipBLASLt."""
+    if not (GEMM_NT and _gemm_nt_ok(x2, w2)):
         return None
     C_ = _native.native()
-    M = x2.shape[0]
+    M, K = x2.shape
+    N = w2.shape[0]
     st = spec.bn_next
     rg = M // spec.groups
-    stats = None
-    if st is not None and M % spec.groups == 0 and not C_.bn_small(rg):
-        cfg = C_.gemm_nt_pick(M, N, K, rg)
-        if cfg >= 0:
-            bm = C_.gemm_nt_tile(cfg)[0]
-            stats = torch.empty((-(-M // bm)) * 4 * N, dtype=torch.float32, device=x2.device)
-    else:
-        cfg = C_.gemm_nt_pick(M, N, K, 0)
+    stats_rg = rg if (st is not None and M % spec.groups == 0 and not C_.bn_small(rg)) else 0
+    cfg = _gemm_cfg(x2, w2, stats_rg, None) if stats_rg else -1
+    if cfg < 0:
+        stats_rg = 0
+        cfg = _gemm_cfg(x2, w2, 0, None)
     if cfg < 0:
         return None
     y2 = torch.empty((M, N), dtype=x2.dtype, device=x2.device)
-    C_.gpu_gemm_nt(x2, w2, y2, None, stats, rg if stats is not None else 0, cfg)
+    stats = None
+    if stats_rg:
+        geo = C_.gemm_nt_stats_geometry(cfg, M, N, K, stats_rg)
+        stats = torch.empty(geo[2], dtype=torch.float32, device=x2.device)
+    C_.gpu_gemm_nt(x2, w2, y2, None, stats, stats_rg, cfg)
     if stats is not None:
-        st.tile = (stats, C_.gemm_nt_tile(cfg)[0])
+        st.tile = (stats, geo[0], geo[1])
     return y2
+
+
+def refresh_dgrad_weights(specs) -> None:
+    """Transposed copies Wᵀ [Cin, Cout] of every 1x1 stride-1 convolution weight, for the
+    data-gradient GEMMs of this step: ONE launch for the whole network (the weights change
+    once per step, in the update kernel)."""
+    if not (GEMM_NT and GEMM_NT_DGRAD):
+        return
+    srcs, dsts = [], []
+    for spec in specs:
+        w = spec.conv.weight
+        if not (spec.gemm and w.is_cuda and w.dtype == torch.bfloat16 and w.shape[0] % 64 == 0
+                and w.shape[1] % 64 == 0):
+            continue
+        w2 = w.detach().reshape(w.shape[0], -1)
+        if not w2.is_contiguous():
+            continue
+        if spec.wt is None or spec.wt.shape != (w2.shape[1], w2.shape[0]) or spec.wt.device != w2.device:
+            spec.wt = torch.empty((w2.shape[1], w2.shape[0]), dtype=w2.dtype, device=w2.device)
+        srcs.append(w2)
+        dsts.append(spec.wt)
+    if srcs:
+        _native.native().gpu_transpose_multi(srcs, dsts)
+
+
+def _gemm_nt_dgrad(dy2: torch.Tensor, w2: torch.Tensor, add: torch.Tensor | None, spec: "ConvSpec | None" = None):
+    """dx = dy2 · w2 (+ add, in place of add) on gemm_nt.hip with the transposed weight (the step's
+    ``spec.wt`` when refreshed, else transposed here); None: use hipBLASLt."""
+    if not (GEMM_NT and GEMM_NT_DGRAD and dy2.is_cuda and w2.shape[1] % 64 == 0):
+        return None
+    wt = spec.wt if (spec is not None and spec.wt is not None) else w2.t().contiguous()
+    if not _gemm_nt_ok(dy2, wt) or (add is not None and not add.is_contiguous()):
+        return None
+    C_ = _native.native()
+    cfg = _gemm_cfg(dy2, wt, 0, add)
+    if cfg < 0:
+        return None
+    out = add if add is not None else torch.empty((dy2.shape[0], wt.shape[0]), dtype=dy2.dtype, device=dy2.device)
+    C_.gpu_gemm_nt(dy2, wt, out, add, None, 0, cfg)
+    return out
 
 
 def _conv_bwd(dy, x, w, spec: ConvSpec, mask):
@@ -772,10 +862,12 @@ class _GroupedConv(torch.autograd.Function):
                 w2 = w.reshape(cout, -1)
                 if prev is not None:             # the other branch's gradient, folded into the GEMM
                     p2 = rows2d(_cl(prev))
-                    dx = from_rows(p2.addmm_(dy2, w2), n, h, wd)
+                    d2 = _gemm_nt_dgrad(dy2, w2, p2, spec)
+                    dx = from_rows(d2 if d2 is not None else p2.addmm_(dy2, w2), n, h, wd)
                     prev = None
                 else:
-                    dx = from_rows(torch.mm(dy2, w2), n, h, wd)
+                    d2 = _gemm_nt_dgrad(dy2, w2, None, spec)
+                    dx = from_rows(d2 if d2 is not None else torch.mm(dy2, w2), n, h, wd)
             if spec.sink is not None:
                 K = w.numel() // cout
                 with _wgrad_ctx(a, dy):

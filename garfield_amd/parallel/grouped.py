@@ -23,7 +23,7 @@ from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
 from garfield_amd.parallel.signals import DeviceSignal
 from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, grouped_bn,
                                       WgradStream, grouped_conv, grouped_cross_entropy, grouped_linear,
-                                      grouped_maxpool)
+                                      grouped_maxpool, refresh_dgrad_weights)
 
 
 def supports(model: nn.Module) -> bool:
@@ -173,6 +173,8 @@ class GroupedResNet:
     def run(self, x: torch.Tensor, y: torch.Tensor, loss_out: torch.Tensor | None = None) -> torch.Tensor:
         if x.shape[0] % self.groups:
             raise ValueError(f"batch of {x.shape[0]} rows is not divisible into {self.groups} workers")
+        if x.is_cuda:
+            refresh_dgrad_weights(self.conv.values())   # Wᵀ of every 1x1 layer: one launch
         per = self.losses(self.forward(x), y)
         # d(Σ_g loss_g)/d loss_g = 1: seeded directly (no sum / fill / expand kernels)
         if self._seed is None or self._seed.shape != per.shape or self._seed.device != per.device \

@@ -96,29 +96,32 @@ def main():
             dx2 = torch.empty((M, K), device=dev, dtype=torch.bfloat16)
             wt = w.t().contiguous()
             res["transpose w"] = bench(lambda: w.t().contiguous())
-            for cfg in range(9):
-                bm, bn = C_.gemm_nt_tile(cfg)
-                if Co % bn == 0:
+            for cfg in range(C_.gemm_nt_num_cfg()):
+                if C_.gemm_nt_valid(cfg, Co, K):
                     f = lambda: C_.gpu_gemm_nt(x, w, y2, None, None, 0, cfg)
                     res[f"nt{cfg} fwd"] = bench(f)
                     f()
                     err = (y2.float() - yref.float()).abs().max().item()
                     assert err < 0.02 * yref.float().abs().max().item() + 1e-2, (name, cfg, err)
-                if K % bn == 0:
+                if C_.gemm_nt_valid(cfg, K, Co):
                     g = lambda: C_.gpu_gemm_nt(dy, wt, dx2, None, None, 0, cfg)
                     res[f"nt{cfg} dgrad"] = bench(g)
                     g()
                     err = (dx2.float() - dref.float()).abs().max().item()
                     assert err < 0.02 * dref.float().abs().max().item() + 1e-2, (name, cfg, "dgrad", err)
             # fused BatchNorm statistics (rg rows per worker) vs torch on the stored output
-            for cfg in range(9):
-                bm, bn = C_.gemm_nt_tile(cfg)
-                if Co % bn == 0 and bm <= rg:
-                    st = torch.empty(((M + bm - 1) // bm) * 4 * Co, device=dev, dtype=torch.float32)
+            for cfg in range(C_.gemm_nt_num_cfg()):
+                sr = C_.gemm_nt_stats_rows(cfg)
+                if C_.gemm_nt_valid(cfg, Co, K) and sr <= rg:
+                    st = torch.empty(C_.gemm_nt_stats_geometry(cfg, M, Co, K, rg)[2], device=dev, dtype=torch.float32)
                     res[f"nt{cfg}+st"] = bench(lambda: C_.gpu_gemm_nt(x, w, y2, None, st, rg, cfg))
+            pf, pd, ps = C_.gemm_nt_pick(M, Co, K, 0), C_.gemm_nt_pick(M, K, Co, 0), C_.gemm_nt_pick(M, Co, K, rg)
+            res[f"auto fwd(nt{pf})"] = res.get(f"nt{pf} fwd", float("nan"))
+            res[f"auto dgrad(nt{pd})"] = res.get(f"nt{pd} dgrad", float("nan"))
+            res[f"auto+st(nt{ps})"] = res.get(f"nt{ps}+st", float("nan"))
             cfg = C_.gemm_nt_pick(M, Co, K, rg)
-            bm, bn = C_.gemm_nt_tile(cfg)
-            st = torch.empty(((M + bm - 1) // bm) * 4 * Co, device=dev, dtype=torch.float32)
+            bm, be, nst = C_.gemm_nt_stats_geometry(cfg, M, Co, K, rg)
+            st = torch.empty(nst, device=dev, dtype=torch.float32)
             C_.gpu_gemm_nt(x, w, y2, None, st, rg, cfg)
             mean = torch.empty((G, Co), device=dev)
             istd, sc, sh = torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean)
@@ -127,7 +130,7 @@ def main():
             bet = torch.randn(Co, device=dev)
             part = torch.empty(C_.bn_part_floats(rg, G, Co), device=dev)
             C_.gpu_bn_forward(y2, None, G, gam, bet, 1e-5, 0.1, None, None, part, mean, istd, sc, sh, ybn, False,
-                              tile_stats=st, tile_m=bm)
+                              tile_stats=st, tile_m=bm, tile_e=be)
             yg = y2.float().view(G, rg, Co)
             mref = yg.mean(1)
             vref = yg.var(1, unbiased=False)
@@ -138,6 +141,7 @@ def main():
         print(f"{name:18s} M={M:6d} K={K:5d} N={Co:5d} x{cnt} floor {floor:5.1f}us | "
               + " ".join(f"{k} {v:6.1f}" for k, v in res.items()), flush=True)
         for k, v in res.items():
+            k = k.split("(")[0]
             tot[k] = tot.get(k, 0.0) + cnt * v
     print("per-step totals (us):", {k: round(v, 1) for k, v in tot.items()})
 

@@ -12,7 +12,8 @@ def rel(a, b):
 
 
 @pytest.mark.parametrize("M,K,N", [(128000, 64, 256), (4000, 256, 64), (2000, 512, 2048), (1000, 1024, 256),
-                                   (333, 128, 128), (77, 64, 64)])
+                                   (333, 128, 128), (77, 64, 64), (128000, 256, 128), (32000, 128, 512),
+                                   (8000, 256, 1024), (5000, 192, 64)])
 def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
     torch.manual_seed(M + K + N)
     a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
@@ -20,9 +21,8 @@ def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
     add = torch.randn(M, N, device=cuda).to(torch.bfloat16)
     ref = a.float() @ b.float().t()
     ran = 0
-    for cfg in range(9):
-        bm, bn = native.gemm_nt_tile(cfg)
-        if N % bn:
+    for cfg in range(native.gemm_nt_num_cfg()):
+        if not native.gemm_nt_valid(cfg, N, K):
             continue
         c = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
         native.gpu_gemm_nt(a, b, c, None, None, 0, cfg)
@@ -39,7 +39,8 @@ def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
 
 @pytest.mark.parametrize("G,rg,K,N,offset", [(8, 16000, 64, 256, 0.0), (8, 1000, 256, 64, 0.0),
                                               (8, 250, 512, 128, 40.0), (3, 700, 128, 128, 25.0),
-                                              (2, 4000, 64, 64, 300.0)])
+                                              (2, 4000, 64, 64, 300.0), (8, 4000, 128, 512, 10.0),
+                                              (5, 40, 256, 128, 0.0)])
 def test_fused_bn_statistics_match_fp32(cuda, native, G, rg, K, N, offset):
     """Per-worker mean / biased variance of the STORED GEMM output, merged from tile
     statistics (tiles straddling worker boundaries included), even when |mean| >> std."""
@@ -47,17 +48,20 @@ def test_fused_bn_statistics_match_fp32(cuda, native, G, rg, K, N, offset):
     M = G * rg
     a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
     b = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
-    for cfg in range(9):
-        bm, bn = native.gemm_nt_tile(cfg)
-        if N % bn or bm > rg:
+    ran = 0
+    for cfg in range(native.gemm_nt_num_cfg()):
+        if not native.gemm_nt_valid(cfg, N, K) or native.gemm_nt_stats_rows(cfg) > rg:
             continue
+        ran += 1
+        H, E, nst = native.gemm_nt_stats_geometry(cfg, M, N, K, rg)
+        assert H <= rg
         # a column of the input drives a constant offset into every output channel
         a2 = a.clone()
         a2[:, 0] = offset
         b2 = b.clone()
         b2[:, 0] = 1.0 if offset else b[:, 0]
         y = torch.empty((M, N), device=cuda, dtype=torch.bfloat16)
-        st = torch.empty(((M + bm - 1) // bm) * 4 * N, device=cuda)
+        st = torch.full((nst,), float("nan"), device=cuda)
         native.gpu_gemm_nt(a2, b2, y, None, st, rg, cfg)
         assert rel(y, a2.float() @ b2.float().t()) < 5e-3
         mean = torch.empty((G, N), device=cuda)
@@ -67,7 +71,7 @@ def test_fused_bn_statistics_match_fp32(cuda, native, G, rg, K, N, offset):
         part = torch.empty(native.bn_part_floats(rg, G, N), device=cuda)
         out = torch.empty_like(y)
         native.gpu_bn_forward(y, None, G, gam, bet, 1e-5, 0.1, None, None, part, mean, istd, sc, sh, out, False,
-                              tile_stats=st, tile_m=bm)
+                              tile_stats=st, tile_m=H, tile_e=E)
         yg = y.double().view(G, rg, N)
         mref, vref = yg.mean(1), yg.var(1, unbiased=False)
         assert (mean.double() - mref).abs().max().item() < 1e-4 * (1 + mref.abs().max().item()), cfg
@@ -75,6 +79,7 @@ def test_fused_bn_statistics_match_fp32(cuda, native, G, rg, K, N, offset):
         assert ((var - vref).abs() / vref.clamp_min(1e-6)).max().item() < 2e-3, cfg
         yref = ((yg - mref[:, None]) / torch.sqrt(vref[:, None] + 1e-5) * gam.double() + bet.double()).view(M, N)
         assert rel(out, yref) < 1e-2, cfg
+    assert ran >= 1
 
 
 @pytest.mark.parametrize("S,G,shape", [(4, 8, (64, 72)), (16, 3, (128, 9)), (2, 5, (7,))])
@@ -130,3 +135,15 @@ def test_split_reduce_multi_matches_single(cuda, native):
     native.gpu_split_reduce_multi(parts, outs)
     for o, r in zip(outs, refs):
         assert rel(o, r) < (1e-6 if o.dtype == torch.float32 else 5e-3)
+
+
+def test_transpose_multi_matches_torch(cuda, native):
+    """Every 1x1 weight's Wᵀ in one launch (the data-gradient GEMMs' B operand), more jobs than one
+    launch's table, ragged tile edges."""
+    torch.manual_seed(11)
+    shapes = [(64, 64), (256, 64), (64, 256), (2048, 512), (8, 8), (72, 136)] * 8
+    srcs = [torch.randn(r, c, device=cuda).to(torch.bfloat16) for r, c in shapes]
+    dsts = [torch.empty(c, r, device=cuda, dtype=torch.bfloat16) for r, c in shapes]
+    native.gpu_transpose_multi(srcs, dsts)
+    for a, b in zip(srcs, dsts):
+        assert torch.equal(b, a.t())
