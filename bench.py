@@ -98,6 +98,8 @@ def parse():
     p.add_argument("--ref-impl", action="store_true",
                    help="also time the reference's algorithms run as-is (BASELINE.md (a)) and report the speedup")
     p.add_argument("--phases", action="store_true", help="report per-phase device time (compute / exchange / GAR)")
+    p.add_argument("--layerwise", action="store_true",
+                   help="the GAR on every parameter tensor separately (reference Garfield_CC --layerwise)")
     p.add_argument("--shard-gar", action="store_true",
                    help="force the sharded, bucketed aggregation even on one GPU (with GARFIELD_LOOPBACK_EXCHANGE=1 "
                         "the exchange is emulated by side-stream copies: overlap traces)")
@@ -173,7 +175,8 @@ def main():
                        weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
                        cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=not a.no_lp_weights,
                        worker_batching=False if a.no_worker_batching else None,
-                       shard_gar=True if a.shard_gar else None, **amp)
+                       shard_gar=True if a.shard_gar else (False if a.layerwise else None),
+                       layerwise=a.layerwise, **amp)
     if a.num_ps:
         from dataclasses import asdict
 
@@ -279,7 +282,7 @@ def main():
                                   f"{', servers host workers' if a.ps_workers else ''})" if a.num_ps else ""),
                 "process_group": {"backend": ctx.backend,
                                   "world_size": dist.get_world_size() if ctx.is_distributed else 1},
-                "gar": a.gar,
+                "gar": a.gar + (" (layer-wise: per parameter tensor)" if a.layerwise else ""),
                 "f": a.f,
                 "batch_per_worker": a.batch,
                 "exchange_dtype": a.exchange_dtype,

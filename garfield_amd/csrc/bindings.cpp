@@ -1228,12 +1228,67 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            [](const std::vector<at::Tensor>& L, const at::Tensor& s, const at::Tensor& g) { g_gram(rows_from_list(L, true), s, g); },
            "Split-K MFMA Gram matrix G·Gᵀ (fp32 [np, np])");
   m.def("gpu_krum_select", [](const at::Tensor& gram, int n, int f, int mm, const at::Tensor& w, const at::Tensor& order,
-                              const at::Tensor& scores) {
+                              const at::Tensor& scores, int batch) {
     c10::hip::HIPGuard guard(gram.device().index());
     TORCH_CHECK(order.scalar_type() == at::kInt, "order must be int32");
+    TORCH_CHECK(batch >= 1, "batch must be >= 1");
     const int np = garfield::gpu::gram_padded(n);
-    garfield::gpu::krum_select(fptr(gram), np, n, f, mm, fptr(w), order.data_ptr<int>(), fptr(scores), stream_of(gram.device()));
-  });
+    TORCH_CHECK(gram.numel() >= static_cast<int64_t>(batch) * np * np && w.numel() >= static_cast<int64_t>(batch) * n &&
+                    order.numel() >= static_cast<int64_t>(batch) * n && scores.numel() >= static_cast<int64_t>(batch) * n,
+                "gpu_krum_select: buffers too small for the batch");
+    garfield::gpu::krum_select(fptr(gram), np, n, f, mm, fptr(w), order.data_ptr<int>(), fptr(scores),
+                               stream_of(gram.device()), batch);
+  }, py::arg("gram"), py::arg("n"), py::arg("f"), py::arg("m"), py::arg("weights"), py::arg("order"),
+     py::arg("scores"), py::arg("batch") = 1,
+     "Multi-Krum selection weights on device; batch > 1: gram [batch, np, np] -> weights [batch, n]");
+  m.def("gpu_lw_gram", [](const at::Tensor& G, const at::Tensor& jobs, const at::Tensor& seg_lo,
+                          const at::Tensor& slabs, const at::Tensor& gram) {
+    const RowSet rs = rows_from_2d(G, true);
+    check_gpu(rs);
+    TORCH_CHECK(jobs.device() == rs.device && jobs.scalar_type() == at::kLong && jobs.dim() == 2 && jobs.size(1) == 3 &&
+                    jobs.is_contiguous(), "gpu_lw_gram: jobs must be a contiguous int64 [J, 3] tensor on G's device");
+    TORCH_CHECK(seg_lo.device() == rs.device && seg_lo.scalar_type() == at::kInt && seg_lo.dim() == 1 &&
+                    seg_lo.is_contiguous() && seg_lo.numel() >= 2,
+                "gpu_lw_gram: seg_lo must be a contiguous int32 [L + 1] tensor on G's device");
+    const int J = static_cast<int>(jobs.size(0)), L = static_cast<int>(seg_lo.numel() - 1);
+    const int np = garfield::gpu::gram_padded(rs.n);
+    TORCH_CHECK(slabs.numel() >= static_cast<int64_t>(J) * garfield::gpu::gram_slab_floats(rs.n),
+                "gpu_lw_gram: slab workspace too small");
+    TORCH_CHECK(gram.numel() >= static_cast<int64_t>(L) * np * np, "gpu_lw_gram: gram output too small");
+    c10::hip::HIPGuard guard(rs.device.index());
+    garfield::gpu::lw_gram(rs.table, rs.n, rs.dt, jobs.data_ptr<int64_t>(), J, seg_lo.data_ptr<int>(), L,
+                           fptr(slabs), fptr(gram), stream_of(rs.device));
+  }, "Per-segment MFMA Gram matrices of the [n, d] rows: gram [L, np, np]; jobs [J, 3] int64 (start, end, "
+     "segment) ranges inside one segment each, in segment order; seg_lo [L + 1] int32 first job per segment");
+  m.def("gpu_lw_combine_sgd", [](const at::Tensor& G, const at::Tensor& jobs, const at::Tensor& seg_off,
+                                 const at::Tensor& weights, const at::Tensor& param, const at::Tensor& mom,
+                                 const c10::optional<at::Tensor>& shadow, double lr, double momentum, double dampening,
+                                 double weight_decay, bool nesterov, bool first_step) {
+    const RowSet rs = rows_from_2d(G, true);
+    check_gpu(rs);
+    TORCH_CHECK(jobs.device() == rs.device && jobs.scalar_type() == at::kLong && jobs.dim() == 2 && jobs.size(1) == 3 &&
+                    jobs.is_contiguous(), "gpu_lw_combine_sgd: jobs must be a contiguous int64 [J, 3] tensor");
+    TORCH_CHECK(seg_off.device() == rs.device && seg_off.scalar_type() == at::kLong && seg_off.is_contiguous(),
+                "gpu_lw_combine_sgd: seg_off must be a contiguous int64 [L + 1] tensor");
+    const int64_t L = seg_off.numel() - 1;
+    TORCH_CHECK(weights.numel() >= L * rs.n, "gpu_lw_combine_sgd: weights must be [L, n]");
+    TORCH_CHECK(param.numel() >= rs.d && mom.numel() >= rs.d, "gpu_lw_combine_sgd: parameter/momentum too small");
+    void* sh = nullptr;
+    int sh_dt = garfield::kBF16;
+    if (shadow.has_value() && shadow->defined()) {
+      TORCH_CHECK(shadow->is_cuda() && shadow->device() == rs.device && shadow->is_contiguous() && shadow->numel() >= rs.d,
+                  "gpu_lw_combine_sgd: shadow must be a contiguous tensor of >= d elements on G's device");
+      sh_dt = dtype_code(*shadow);
+      sh = shadow->data_ptr();
+    }
+    garfield::gpu::SgdArgs a{static_cast<float>(lr), static_cast<float>(momentum), static_cast<float>(dampening),
+                             static_cast<float>(weight_decay), nesterov ? 1 : 0, first_step ? 1 : 0};
+    c10::hip::HIPGuard guard(rs.device.index());
+    garfield::gpu::lw_combine_sgd(rs.table, rs.n, rs.dt, jobs.data_ptr<int64_t>(), static_cast<int>(jobs.size(0)),
+                                  fptr(weights), fptr(param), fptr(mom), sh, sh_dt, a, seg_off.data_ptr<int64_t>(),
+                                  stream_of(rs.device));
+  }, "Per-segment weighted combine of the [n, d] rows (weights [L, n]) fused with the SGD update; args (G, jobs, "
+     "seg_off, weights, param, mom, shadow|None, lr, momentum, dampening, weight_decay, nesterov, first_step)");
   m.def("gpu_bulyan_select", [](const at::Tensor& gram, int n, int f, int mm, int t, const at::Tensor& W) {
     c10::hip::HIPGuard guard(gram.device().index());
     TORCH_CHECK(W.numel() >= static_cast<int64_t>(t) * n, "W too small");

@@ -24,8 +24,10 @@ void gram(const RowTable& rows, int n, int64_t d, int dt, float* slabs, int grid
 
 // ---- Selection (one workgroup, on device, no host round-trip) --------------
 // weights[n] (fp32), order[n] (gradient ids by increasing score), scores[n]
+// batch > 1: `batch` independent problems, gram [batch][np][np] -> weights/order/scores [batch][n]
 void krum_select(const float* gram, int np, int n, int f, int m, float* weights,
-                 int* order, float* scores, hipStream_t stream);
+                 int* order, float* scores, hipStream_t stream, int batch = 1);
+
 // W[t][n]: row k = uniform weights of the (m-k) best-scoring gradients at step k
 void bulyan_select(const float* gram, int np, int n, int f, int m, int t, float* W,
                    hipStream_t stream);
@@ -50,6 +52,19 @@ struct SgdArgs {
 void combine_sgd(const RowTable& rows, int n, int64_t d, int dt, const float* weights,
                  float* param, float* momentum_buf, float* grad_out, void* shadow, int shadow_dt,
                  SgdArgs args, hipStream_t stream);
+
+// ---- Layer-wise GAR: the rule on every parameter segment of the flat rows ----
+// jobs: [njobs][3] int64 (start, end, segment) coordinate ranges, each inside one segment, in
+// segment order; seg_lo: [L + 1] int32, the first job of each segment (seg_lo[L] = njobs).
+// lw_gram: gram [L][np][np] = per-segment G·Gᵀ (slabs: [njobs][gram_slab_floats(n)] workspace).
+void lw_gram(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const int* seg_lo, int L,
+             float* slabs, float* gram, hipStream_t stream);
+// lw_combine_sgd: per coordinate of segment s, g = Σ_j weights[s][j] row_j, then the SGD update
+// of param / momentum (and the shadow copy), as combine_sgd does with one weight vector.
+// seg_off: [L + 1] int64 segment offsets (jobs start at a multiple of 8 from their segment start).
+void lw_combine_sgd(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const float* weights,
+                    float* param, float* momentum_buf, void* shadow, int shadow_dt, SgdArgs args,
+                    const int64_t* seg_off, hipStream_t stream);
 
 // ---- Coordinate-wise rules (median, trimmed mean, MeaMed, ...) -------------
 // W/t are only read for kBulyanTail; seed/threshold only for kCondense.

@@ -237,6 +237,11 @@ __global__ __launch_bounds__(1024) void k_krum_select(const float* __restrict__ 
                                                       int f, int m, float* __restrict__ weights,
                                                       int* __restrict__ order, float* __restrict__ scores) {
   extern __shared__ float lds[];
+  // workgroup b selects problem b of a batch (the layer-wise GAR: one Gram per parameter segment)
+  gram += static_cast<int64_t>(blockIdx.x) * np * np;
+  weights += static_cast<int64_t>(blockIdx.x) * n;
+  order += static_cast<int64_t>(blockIdx.x) * n;
+  scores += static_cast<int64_t>(blockIdx.x) * n;
   float* D = lds;                    // n * (n + 1)
   float* S = lds + n * (n + 1);      // n
   fill_distances(gram, np, n, D);
@@ -485,10 +490,10 @@ static void allow_big_lds(const void* fn) {
 }
 
 void krum_select(const float* gram_in, int np, int n, int f, int m, float* weights, int* order, float* scores,
-                 hipStream_t stream) {
+                 hipStream_t stream, int batch) {
   static bool once = (allow_big_lds(reinterpret_cast<const void*>(&k_krum_select)), true);
   (void)once;
-  hipLaunchKernelGGL(k_krum_select, dim3(1), dim3(1024), select_lds_bytes(n), stream, gram_in, np, n, f, m,
+  hipLaunchKernelGGL(k_krum_select, dim3(batch), dim3(1024), select_lds_bytes(n), stream, gram_in, np, n, f, m,
                      weights, order, scores);
 }
 

@@ -1,0 +1,298 @@
+// Layer-wise robust aggregation on gfx950: the GAR applied to every parameter segment of the
+// flat [n, d] gradient rows in a handful of launches instead of one Gram / selection / combine
+// per parameter tensor.
+//
+// Reference semantics: pytorch_impl/applications/Garfield_CC/trainer.py:100,125 (--layerwise:
+// the rule runs on each layer's gradient slice separately). A ResNet-50 has 161 parameter
+// tensors, so a per-tensor loop is ~480 launches with tiny grids; here:
+//
+//   lw_gram         one split-K MFMA Gram launch over a JOB table (each job a coordinate range
+//                   inside one segment) writing a partial [np, np] slab per job, then one
+//                   fixed-order segmented reduction into gram[L][np][np];
+//   krum_select     the existing one-workgroup selection, batched: workgroup s selects segment s;
+//   lw_combine_sgd  one launch: job j combines its coordinates with its segment's weights and
+//                   applies the fused SGD update (the same per-element arithmetic as k_combine +
+//                   k_combine_sgd: 8-wide groups from the segment start, 4 rows per step, a scalar
+//                   tail), so the result is bitwise that of the per-segment path.
+//
+// Segment boundaries are arbitrary element offsets (a BatchNorm bias of 64, a 9408-element
+// stem): 16-byte loads where a group is aligned, element loads where it is not.
+#include "gar_device.hpp"
+
+namespace garfield {
+namespace gpu {
+using namespace dev;
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// Segmented Gram partials: the k_gram_partial scheme (gar_gram.hip) over [start, end) of one
+// job; pieces straddling the range ends are masked element by element.
+template <int DT, int NB>
+__global__ __launch_bounds__(256) void k_lw_gram_partial(RowTable rows, int n, const int64_t* __restrict__ jobs,
+                                                         float* __restrict__ slabs) {
+  constexpr int NPAIR = NB * (NB + 1) / 2;
+  constexpr int ESZ = (DT == kF32) ? 4 : 2;
+  constexpr int KSPAN = 256 / ESZ;   // elements per row per wave step
+  constexpr int QSPAN = KSPAN / 4;   // elements per lane per wave step
+  constexpr int PE = 16 / ESZ;       // elements per 16-byte piece
+  __shared__ float red[NPAIR * 256];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r16 = lane & 15;
+  const int q = lane >> 4;
+  const int64_t a = jobs[3 * blockIdx.x], b = jobs[3 * blockIdx.x + 1];
+  const int64_t base = a - (a % PE);                  // piece-aligned start
+
+  const char* rp[NB];
+  bool rv[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int row = i * 16 + r16;
+    rv[i] = row < n;
+    rp[i] = rv[i] ? static_cast<const char*>(rows.p[row]) : nullptr;
+  }
+  f32x4 acc[NPAIR];
+#pragma unroll
+  for (int p = 0; p < NPAIR; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t k = base + static_cast<int64_t>(wave) * KSPAN; k < b; k += 4 * KSPAN) {
+    uint4 u[NB][4];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int64_t e0 = k + static_cast<int64_t>(q) * QSPAN + PE * s;   // first element of the piece
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (rv[i]) {
+          const bool aligned = (reinterpret_cast<uintptr_t>(rp[i] + e0 * ESZ) & 15) == 0;
+          if (e0 >= a && e0 + PE <= b && aligned) {
+            v = *reinterpret_cast<const uint4*>(rp[i] + e0 * ESZ);
+          } else if (e0 + PE > a && e0 < b) {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int e = 0; e < PE; ++e) {
+              const int64_t x = e0 + e;
+              if (x >= a && x < b) {
+                if constexpr (ESZ == 4) {
+                  w[e] = *reinterpret_cast<const uint32_t*>(rp[i] + x * 4);
+                } else {
+                  const uint32_t h = *reinterpret_cast<const uint16_t*>(rp[i] + x * 2);
+                  w[e >> 1] |= (e & 1) ? (h << 16) : h;
+                }
+              }
+            }
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+          }
+        }
+        u[i][s] = v;
+      }
+    }
+    int p = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+#pragma unroll
+      for (int j = i; j < NB; ++j) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if constexpr (DT == kBF16) {
+            acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, u[i][s]),
+                                                             __builtin_bit_cast(bf16x8, u[j][s]), acc[p], 0, 0, 0);
+          } else if constexpr (DT == kF16) {
+            acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, u[i][s]),
+                                                            __builtin_bit_cast(f16x8, u[j][s]), acc[p], 0, 0, 0);
+          } else {
+            const float4 xa = __builtin_bit_cast(float4, u[i][s]);
+            const float4 xb = __builtin_bit_cast(float4, u[j][s]);
+            acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, xb.x, acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, xb.y, acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, xb.z, acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.w, xb.w, acc[p], 0, 0, 0);
+          }
+        }
+        ++p;
+      }
+    }
+  }
+  // the 4 waves in LDS, in a fixed order (deterministic); C/D map: col = lane & 15, row = 4q + reg
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int idx = p * 256 + (q * 4 + r) * 16 + r16;
+          red[idx] = (w == 0 ? 0.f : red[idx]) + acc[p][r];
+        }
+    }
+    __syncthreads();
+  }
+  float* slab = slabs + static_cast<int64_t>(blockIdx.x) * (NPAIR * 256);
+  for (int e = threadIdx.x; e < NPAIR * 256; e += 256) slab[e] = red[e];
+}
+
+// gram[s] (symmetric np x np) = Σ over the jobs of segment s of their slabs, in job order.
+__global__ __launch_bounds__(256) void k_lw_gram_reduce(const float* __restrict__ slabs, const int* __restrict__ seg_lo,
+                                                        int nb, float* __restrict__ gram) {
+  const int npair = nb * (nb + 1) / 2;
+  const int E = npair * 256;
+  const int s = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= E) return;
+  float tot = 0.f;
+  for (int j = seg_lo[s]; j < seg_lo[s + 1]; ++j) tot += slabs[static_cast<int64_t>(j) * E + e];
+  int p = e >> 8, ia = 0;
+  while (p >= nb - ia) { p -= nb - ia; ++ia; }
+  const int ib = ia + p;
+  const int i = ia * 16 + ((e >> 4) & 15);
+  const int jj = ib * 16 + (e & 15);
+  const int np = nb * 16;
+  float* g = gram + static_cast<int64_t>(s) * np * np;
+  g[i * np + jj] = tot;
+  g[jj * np + i] = tot;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Segmented combine + SGD
+
+template <int DT>
+__device__ __forceinline__ void load8_any(const void* row, int64_t x, float (&v)[8]) {
+  constexpr int ESZ = (DT == kF32) ? 4 : 2;
+  if ((reinterpret_cast<uintptr_t>(static_cast<const char*>(row) + x * ESZ) & 15) == 0) {
+    load_vec<DT, 8>(row, x, v);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = load_one<DT>(row, x + c);
+  }
+}
+
+// k_combine's arithmetic (gar_combine.hip gather_weighted), loads of any alignment
+template <int DT>
+__device__ __forceinline__ void gather8(const RowTable& rows, const int* sel, const float* wsel, int cnt, int64_t x,
+                                        float (&acc)[8]) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+  int j = 0;
+  for (; j + 4 <= cnt; j += 4) {
+    float v0[8], v1[8], v2[8], v3[8];
+    load8_any<DT>(rows.p[sel[j]], x, v0);
+    load8_any<DT>(rows.p[sel[j + 1]], x, v1);
+    load8_any<DT>(rows.p[sel[j + 2]], x, v2);
+    load8_any<DT>(rows.p[sel[j + 3]], x, v3);
+    const float w0 = wsel[j], w1 = wsel[j + 1], w2 = wsel[j + 2], w3 = wsel[j + 3];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] += w0 * v0[c] + w1 * v1[c] + w2 * v2[c] + w3 * v3[c];
+  }
+  for (; j < cnt; ++j) {
+    float v[8];
+    load8_any<DT>(rows.p[sel[j]], x, v);
+    const float w = wsel[j];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] += w * v[c];
+  }
+}
+
+__device__ __forceinline__ void sgd_one(float g, float& p, float& buf, const SgdArgs& a) {
+  if (a.weight_decay != 0.f) g += a.weight_decay * p;
+  if (a.momentum != 0.f) {
+    buf = a.first_step ? g : a.momentum * buf + (1.f - a.dampening) * g;
+    g = a.nesterov ? g + a.momentum * buf : buf;
+  }
+  p -= a.lr * g;
+}
+
+// jobs: (start, end, segment, segment start) rows of 4 int64 here (lw_combine_sgd expands them)
+template <int DT>
+__global__ __launch_bounds__(256) void k_lw_combine_sgd(RowTable rows, int n, const int64_t* __restrict__ jobs,
+                                                        const float* __restrict__ weights, float* __restrict__ param,
+                                                        float* __restrict__ mom, void* __restrict__ shadow,
+                                                        int shadow_dt, SgdArgs args, const int64_t* __restrict__ seg_off) {
+  __shared__ int sel[kMaxRows];
+  __shared__ float wsel[kMaxRows];
+  __shared__ int cnt_s;
+  const int64_t a = jobs[3 * blockIdx.x], b = jobs[3 * blockIdx.x + 1];
+  const int s = static_cast<int>(jobs[3 * blockIdx.x + 2]);
+  const int64_t s0 = seg_off[s], s1 = seg_off[s + 1];
+  if (threadIdx.x == 0) {
+    int c = 0;
+    for (int j = 0; j < n; ++j) {
+      const float w = weights[static_cast<int64_t>(s) * n + j];
+      if (w != 0.f) { sel[c] = j; wsel[c] = w; ++c; }
+    }
+    cnt_s = c;
+  }
+  __syncthreads();
+  const int cnt = cnt_s;
+  // 8-wide groups counted from the SEGMENT start (as a per-segment combine sees them); the
+  // segment's last (s1 - s0) % 8 elements are its scalar tail
+  const int64_t sv = s0 + ((s1 - s0) & ~static_cast<int64_t>(7));
+  for (int64_t x = a + static_cast<int64_t>(threadIdx.x) * 8; x < (b < sv ? b : sv); x += 256 * 8) {
+    float acc[8];
+    gather8<DT>(rows, sel, wsel, cnt, x, acc);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float p = param[x + c];
+      float bf = (args.momentum != 0.f && !args.first_step) ? mom[x + c] : 0.f;
+      sgd_one(acc[c], p, bf, args);
+      param[x + c] = p;
+      if (shadow) store_one(shadow, shadow_dt, x + c, p);
+      if (args.momentum != 0.f) mom[x + c] = bf;
+    }
+  }
+  const int64_t t0 = a > sv ? a : sv;
+  for (int64_t x = t0 + threadIdx.x; x < b; x += 256) {
+    float g = 0.f;
+    for (int j = 0; j < cnt; ++j) g += wsel[j] * load_one<DT>(rows.p[sel[j]], x);
+    float p = param[x];
+    float bf = (args.momentum != 0.f && !args.first_step) ? mom[x] : 0.f;
+    sgd_one(g, p, bf, args);
+    param[x] = p;
+    if (shadow) store_one(shadow, shadow_dt, x, p);
+    if (args.momentum != 0.f) mom[x] = bf;
+  }
+}
+
+template <int DT, int NB>
+void launch_lw_gram(const RowTable& rows, int n, const int64_t* jobs, int njobs, float* slabs, hipStream_t s) {
+  hipLaunchKernelGGL((k_lw_gram_partial<DT, NB>), dim3(njobs), dim3(256), 0, s, rows, n, jobs, slabs);
+}
+template <int DT> struct LwGram {
+  static void run(const RowTable& rows, int n, const int64_t* jobs, int njobs, float* slabs, hipStream_t s) {
+    switch (gram_nb(n)) {
+      case 1: launch_lw_gram<DT, 1>(rows, n, jobs, njobs, slabs, s); break;
+      case 2: launch_lw_gram<DT, 2>(rows, n, jobs, njobs, slabs, s); break;
+      case 4: launch_lw_gram<DT, 4>(rows, n, jobs, njobs, slabs, s); break;
+      default: launch_lw_gram<DT, 8>(rows, n, jobs, njobs, slabs, s); break;
+    }
+  }
+};
+template <int DT> struct LwCombine {
+  static void run(const RowTable& rows, int n, const int64_t* jobs, int njobs, const float* w, float* param,
+                  float* mom, void* shadow, int shadow_dt, SgdArgs a, const int64_t* seg_off, hipStream_t s) {
+    hipLaunchKernelGGL(k_lw_combine_sgd<DT>, dim3(njobs), dim3(256), 0, s, rows, n, jobs, w, param, mom, shadow,
+                       shadow_dt, a, seg_off);
+  }
+};
+
+}  // namespace
+
+void lw_gram(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const int* seg_lo, int L,
+             float* slabs, float* gram, hipStream_t stream) {
+  if (njobs <= 0 || L <= 0) return;
+  by_dtype<LwGram>(dt, rows, n, jobs, njobs, slabs, stream);
+  const int nb = gram_nb(n);
+  const int E = nb * (nb + 1) / 2 * 256;
+  hipLaunchKernelGGL(k_lw_gram_reduce, dim3((E + 255) / 256, L), dim3(256), 0, stream, slabs, seg_lo, nb, gram);
+}
+
+void lw_combine_sgd(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const float* weights,
+                    float* param, float* momentum_buf, void* shadow, int shadow_dt, SgdArgs args,
+                    const int64_t* seg_off, hipStream_t stream) {
+  if (njobs <= 0) return;
+  by_dtype<LwCombine>(dt, rows, n, jobs, njobs, weights, param, momentum_buf, shadow, shadow_dt, args, seg_off,
+                      stream);
+}
+
+}  // namespace gpu
+}  // namespace garfield

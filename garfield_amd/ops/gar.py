@@ -251,6 +251,20 @@ def combine(gradients, weights: torch.Tensor) -> torch.Tensor:
     return _finish(C.cpu_combine(rows.obj, weights.float().cpu()), rows)
 
 
+def combine_into(gradients, weights: torch.Tensor, out: torch.Tensor) -> None:
+    """out (fp32, [d]) = Σ_j w_j g_j in fp32 (the GPU combine kernel's arithmetic, no rounding to
+    the gradients' dtype): the layer-wise loop's per-segment combine."""
+    rows = prepare(gradients)
+    if rows.device.type == "cuda" and rows.n <= MAX_ROWS:
+        dst = out if (out.is_contiguous() and _aligned(out)) else torch.empty_like(out)
+        _C_for(rows).gpu_combine(rows.obj, weights.to(rows.device, torch.float32).contiguous(), dst)
+        if dst is not out:
+            out.copy_(dst)
+        return
+    X = rows.stacked().double() if rows.dtype == torch.float64 else rows.stacked().float()
+    out.copy_((weights.to(X.device, X.dtype)[:, None] * X).sum(0))
+
+
 def _large(rows: Rows) -> bool:
     """GPU set of MAX_ROWS < n <= LARGE_ROWS gradients: the gar_large.hip kernels."""
     return rows.device.type == "cuda" and MAX_ROWS < rows.n <= LARGE_ROWS

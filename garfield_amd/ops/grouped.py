@@ -437,7 +437,8 @@ class ConvSpec:
                      and self.dilation == (1, 1))
         self.bn_next = None       # BNState of the BatchNorm that consumes this convolution's output
         self.wpad = None          # persistent zero-padded [Cout, Kp] weight matrix (im2col + GEMM layers)
-        self.wt = None            # [Cin, Cout] transposed 1x1 weight of the data-gradient GEMM (refresh_dgrad_weights)
+        self.wt = None            # [K, Cout] transposed weight matrix of the data-gradient GEMM (refresh_dgrad_weights)
+        self.dcol = False         # its data gradient runs dcol = dy · Wmat + col2im (Wmatᵀ refreshed per step)
 
 
 def _gemm_nt_ok(a2: torch.Tensor, b2: torch.Tensor) -> bool:
@@ -517,6 +518,35 @@ def _gemm_nt_forward(x2: torch.Tensor, w2: torch.Tensor, spec: ConvSpec):
     return y2
 
 
+def _mm_nt(a2: torch.Tensor, b2: torch.Tensor) -> torch.Tensor:
+    """a2 · b2ᵀ: gemm_nt.hip when the shapes fit it, else hipBLASLt."""
+    if GEMM_NT and _gemm_nt_ok(a2, b2):
+        cfg = _gemm_cfg(a2, b2, 0, None)
+        if cfg >= 0:
+            out = torch.empty((a2.shape[0], b2.shape[0]), dtype=a2.dtype, device=a2.device)
+            _native.native().gpu_gemm_nt(a2, b2, out, None, None, 0, cfg)
+            return out
+    return torch.mm(a2, b2.t())
+
+
+def _dcol(dy2: torch.Tensor, w: torch.Tensor, kp: int, spec: "ConvSpec") -> torch.Tensor:
+    """dcol = dy2 · Wmat ([rows, Cout] x [Cout, Kp]) for col2im: gemm_nt.hip with the step's Wmatᵀ
+    (refresh_dgrad_weights, flagged on first use) when Kp is the unpadded K, else hipBLASLt."""
+    K = w.numel() // w.shape[0]
+    if GEMM_NT and GEMM_NT_DGRAD and dy2.is_cuda and kp == K and K % 64 == 0 and w.shape[0] % 64 == 0:
+        spec.dcol = True
+        wt = spec.wt
+        if wt is None or wt.shape != (K, w.shape[0]):
+            wt = _wmat(w, kp).t().contiguous()
+        if _gemm_nt_ok(dy2, wt):
+            cfg = _gemm_cfg(dy2, wt, 0, None)
+            if cfg >= 0:
+                out = torch.empty((dy2.shape[0], K), dtype=dy2.dtype, device=dy2.device)
+                _native.native().gpu_gemm_nt(dy2, wt, out, None, None, 0, cfg)
+                return out
+    return torch.mm(dy2, _wmat(w, kp, spec))
+
+
 def refresh_dgrad_weights(specs) -> None:
     """Transposed copies Wᵀ [Cin, Cout] of every 1x1 stride-1 convolution weight, for the
     data-gradient GEMMs of this step: ONE launch for the whole network (the weights change
@@ -526,10 +556,10 @@ def refresh_dgrad_weights(specs) -> None:
     srcs, dsts = [], []
     for spec in specs:
         w = spec.conv.weight
-        if not (spec.gemm and w.is_cuda and w.dtype == torch.bfloat16 and w.shape[0] % 64 == 0
-                and w.shape[1] % 64 == 0):
+        if not ((spec.gemm or spec.dcol) and w.is_cuda and w.dtype == torch.bfloat16 and w.shape[0] % 64 == 0
+                and (w.numel() // w.shape[0]) % 64 == 0 and _channels_last_weight(w)):
             continue
-        w2 = w.detach().reshape(w.shape[0], -1)
+        w2 = w.detach().permute(0, 2, 3, 1).reshape(w.shape[0], -1)   # [Cout, (kh, kw, ci)]: a view
         if not w2.is_contiguous():
             continue
         if spec.wt is None or spec.wt.shape != (w2.shape[1], w2.shape[0]) or spec.wt.device != w2.device:
@@ -837,8 +867,9 @@ class _GroupedConv(torch.autograd.Function):
             ctx.mode = "col"
             col = _im2col(x, spec)
             ho, wo = _out_hw(spec, h, wd)
-            y = from_rows(torch.mm(col, _wmat(w, col.shape[1], spec).t()), n, ho, wo)
+            y = from_rows(_mm_nt(col, _wmat(w, col.shape[1], spec)), n, ho, wo)
             ctx.save_for_backward(col, w)
+            ctx.x = x if (spec.sink is not None and _iwgrad_ok(x, y)) else None   # implicit weight gradient
             return y
         ctx.mode = "aten"
         ctx.save_for_backward(x, w)
@@ -890,7 +921,7 @@ class _GroupedConv(torch.autograd.Function):
                     dx = _iconv(dy, w, (kh, kw, 1, 1, kh - 1 - ph, kw - 1 - pw, 1, 1), (h, wd),
                                 _cl(prev) if prev is not None else None, transpose_w=True)
                 else:
-                    dcol = torch.mm(dy2, _wmat(w, kp, spec))
+                    dcol = _dcol(dy2, w, kp, spec)
                     if prev is not None:
                         dx = _cl(prev)
                         _native.native().gpu_col2im(dcol, *_geom(spec), dx, True)
@@ -919,7 +950,7 @@ class _GroupedConv(torch.autograd.Function):
         elif mode == "col":                      # a = col [N*Ho*Wo, Kp]
             kp = a.shape[1]
             if need_dx:
-                dcol = torch.mm(dy2, _wmat(w, kp, spec))
+                dcol = _dcol(dy2, w, kp, spec)
                 if prev is not None:
                     dx = _cl(prev)
                     _native.native().gpu_col2im(dcol, *_geom(spec), dx, True)
@@ -927,7 +958,10 @@ class _GroupedConv(torch.autograd.Function):
                 else:
                     dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
                     _native.native().gpu_col2im(dcol, *_geom(spec), dx)
-            if spec.sink is not None:
+            if spec.sink is not None and getattr(ctx, "x", None) is not None:
+                _iwgrad(ctx.x, dy, spec, G, w.numel() // cout)    # no patch matrix, no batched GEMM
+                ctx.x = None
+            elif spec.sink is not None:
                 # dW_g[co, (i, j, ci)] = Σ_rows dy_g[row, co] · col_g[row, (i, j, ci)]: the
                 # weight's channels_last memory order, one batched GEMM for all workers
                 K = w.numel() // cout

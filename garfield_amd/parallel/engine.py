@@ -51,6 +51,10 @@ WEIGHTED_RULES = {"average", "krum", "brute", "aksel"}
 _LP_MODULES = (nn.modules.conv._ConvNd, nn.Linear)
 COORD_RULES = {"median", "trimmed-mean", "averaged-median", "average-nan", "condense", "bulyan"}
 LAYERWISE_RULES = {"krum", "bulyan", "brute", "aksel"}   # per-layer != flat only for distance-based rules
+# Layer-wise Krum as device operations (gar_layerwise.hip: one segmented Gram launch, a batched
+# selection, one segmented combine + SGD); "0" runs the per-segment loop (the reference form).
+LW_DEVICE = os.environ.get("GARFIELD_LW_DEVICE", "1") != "0"
+LW_JOB = 32768   # coordinates per job of the segmented kernels (a multiple of 8)
 
 
 @dataclass
@@ -452,27 +456,82 @@ class RobustDataParallel:
 
     def _layerwise_update(self, rule: str, kw: dict, first: bool) -> None:
         """The GAR on every parameter tensor's slice of the [n, d] rows (each parameter is
-        one contiguous segment of the memory-order flat layout), then one update."""
+        one contiguous segment of the memory-order flat layout), then one update.
+
+        GPU Krum runs as three device launches over all segments (``_layerwise_device``);
+        otherwise a loop over the segments: weighted rules compute each segment's weights and
+        combine it in fp32 (exactly the arithmetic of the device path), other rules aggregate
+        the segment with the rule itself."""
         cfg = self.cfg
         gkw = dict(kw, f=cfg.f)
         if cfg.m is not None and rule in ("krum", "bulyan"):
             gkw["m"] = cfg.m
+        cuda = self.device.type == "cuda"
+        if cuda and LW_DEVICE and rule == "krum" and self.n <= gar.MAX_ROWS:
+            self._layerwise_device(first)
+            return
         g = self._gagg if self._gagg is not None else torch.zeros(self.ld, dtype=torch.float32, device=self.device)
         self._gagg = g
-        for off, numel in zip(self.flat.offsets, self.flat.numels):
+        ws = []
+        for off, numel in self._segments():
             seg = self.G[:, off:off + numel]
-            g[off:off + numel].copy_(gar.aggregate(rule, seg if self.device.type == "cuda" else seg.float(),
-                                                   **gkw).float())
-        self.last_weights = None
-        if self.device.type == "cuda":
+            if cuda and rule in WEIGHTED_RULES:
+                w = self._weights(rule, kw, seg)
+                ws.append(w.clone())
+                gar.combine_into(seg, w, g[off:off + numel])
+            else:
+                g[off:off + numel].copy_(gar.aggregate(rule, seg if cuda else seg.float(), **gkw).float())
+        self.last_weights = torch.stack(ws) if ws else None
+        if cuda:
             self._C.gpu_combine_sgd(g.view(1, self.ld)[:, : self.d], self._one, self.flat.data[: self.d],
                                     self.mom[: self.d], None, self._shadow, cfg.lr, cfg.momentum, cfg.dampening,
                                     cfg.weight_decay, cfg.nesterov, first)
         else:
             self._sgd_cpu(g[: self.d], first)
 
-    def _weights(self, rule: str, kw: dict) -> torch.Tensor:
+    def _segments(self) -> list:
+        """(offset, numel) of every parameter segment, by offset."""
+        return sorted(zip(self.flat.offsets, self.flat.numels))
+
+    def _layerwise_device(self, first: bool) -> None:
+        """Layer-wise Krum on device: per-segment Grams (one launch over a job table + one
+        segmented reduction), every segment's selection in one batched launch, and one
+        segmented combine fused with the SGD update."""
+        cfg = self.cfg
+        C = self._C
+        lw = getattr(self, "_lw", None)
+        if lw is None:
+            segs = self._segments()
+            jobs, seg_lo = [], [0]
+            for s, (off, numel) in enumerate(segs):
+                for a in range(off, off + numel, LW_JOB):
+                    jobs.append((a, min(a + LW_JOB, off + numel), s))
+                seg_lo.append(len(jobs))
+            offs = [o for o, _ in segs] + [segs[-1][0] + segs[-1][1]]
+            L, n = len(segs), self.n
+            np_ = C.gram_padded(n)
+            dev = self.device
+            lw = self._lw = dict(
+                jobs=torch.tensor(jobs, dtype=torch.int64, device=dev),
+                seg_lo=torch.tensor(seg_lo, dtype=torch.int32, device=dev),
+                seg_off=torch.tensor(offs, dtype=torch.int64, device=dev),
+                slabs=torch.empty(len(jobs) * C.gram_slab_floats(n), dtype=torch.float32, device=dev),
+                gram=torch.empty(L * np_ * np_, dtype=torch.float32, device=dev),
+                w=torch.empty((L, n), dtype=torch.float32, device=dev),
+                order=torch.empty((L, n), dtype=torch.int32, device=dev),
+                scores=torch.empty((L, n), dtype=torch.float32, device=dev), L=L)
+        n, f = self.n, cfg.f
+        m = cfg.m if cfg.m is not None else n - f - 2
+        G = self.G[:, : self.d]
+        C.gpu_lw_gram(G, lw["jobs"], lw["seg_lo"], lw["slabs"], lw["gram"])
+        C.gpu_krum_select(lw["gram"], n, f, m, lw["w"], lw["order"], lw["scores"], lw["L"])
+        C.gpu_lw_combine_sgd(G, lw["jobs"], lw["seg_off"], lw["w"], self.flat.data[: self.d], self.mom[: self.d],
+                             self._shadow, cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
+        self.last_weights = lw["w"]
+
+    def _weights(self, rule: str, kw: dict, G=None) -> torch.Tensor:
         f = self.cfg.f
+        G = self.G if G is None else G
         if rule == "average":
             w = getattr(self, "_avg_w", None)
             if w is None:
@@ -480,10 +539,10 @@ class RobustDataParallel:
                 self._avg_w = w
             return w
         if rule == "krum":
-            return gar.krum_weights(self.G, f, self.cfg.m)
+            return gar.krum_weights(G, f, self.cfg.m)
         if rule == "brute":
-            return gar.brute_weights(self.G, f)
-        return gar.aksel_weights(self.G, f, kw.get("mode", "mid"))
+            return gar.brute_weights(G, f)
+        return gar.aksel_weights(G, f, kw.get("mode", "mid"))
 
     def _coordinate(self, rule: str, kw: dict, out: torch.Tensor, G=None) -> None:
         """Coordinate-wise rule (or Bulyan) over ``G`` (default: the [n, d] exchange rows;

@@ -195,7 +195,8 @@ def test_bucketed_exchange_overlap_loopback(cuda, rule, f, overlap, monkeypatch)
 @pytest.mark.gpu
 def test_layerwise_krum_on_gpu_matches_per_segment_gar(cuda):
     """Layer-wise Krum on the GPU path (grouped ResNet-18 rows, HIP GAR per parameter
-    segment): the update equals the per-segment HIP Krum of the same rows."""
+    segment): the update equals the per-segment HIP Krum selection of the same rows, combined
+    in fp32."""
     from garfield_amd.ops import gar
 
     torch.manual_seed(0)
@@ -208,9 +209,63 @@ def test_layerwise_krum_on_gpu_matches_per_segment_gar(cuda):
     torch.cuda.synchronize()
     expect = torch.empty(eng.d, dtype=torch.float32, device=cuda)
     for off, numel in zip(eng.flat.offsets, eng.flat.numels):
-        expect[off:off + numel] = gar.krum(eng.G[:, off:off + numel], 2).float()
+        seg = eng.G[:, off:off + numel]
+        w = gar.krum_weights(seg, 2)
+        expect[off:off + numel] = (w[:, None] * seg.float()).sum(0)    # combined in fp32
     got = (before - eng.flat.data[: eng.d]) / 0.1
     assert ((got - expect).norm() / expect.norm()).item() < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,n,steps", [("resnet18", 8, 2), ("resnet50", 16, 1)])
+def test_layerwise_krum_device_equals_segment_loop_bitwise(cuda, monkeypatch, model, n, steps):
+    """Layer-wise Krum as device operations (segmented Gram, batched selection, segmented
+    combine + SGD) against the per-segment loop (HIP Krum weights of each segment's rows, an fp32
+    HIP combine per segment, then the fused update). The two Grams are summed in different
+    orders, so a segment whose Krum scores TIE at the selection boundary (honest iid workers,
+    n = 16) may select differently: every segment whose weights differ must be such a near-tie
+    (fp64 scores of the m-th and (m+1)-th best within 1e-4 relative), and every other segment's
+    parameters and momentum agree to fp32 rounding (bit for bit on the n = 8 ResNet-18 case, two
+    steps)."""
+    import garfield_amd.parallel.engine as E
+
+    outs = []
+    f = 2
+    for dev_path in (False, True):
+        monkeypatch.setattr(E, "LW_DEVICE", dev_path)
+        torch.manual_seed(0)
+        cfg = EngineConfig(gar="krum", f=f, workers_per_rank=n, byzantine={3: "reverse"}, lr=0.05, momentum=0.9,
+                           weight_decay=5e-4, layerwise=True, cuda_graph=False)
+        eng = RobustDataParallel(build_model(model), F.cross_entropy, DistContext(device=cuda), cfg)
+        for it in range(steps):
+            eng.step(synthetic_batches(n, 4, (3, 32, 32), 10, cuda, seed=7 + it))
+        torch.cuda.synchronize()
+        outs.append((eng.flat.data[: eng.d].clone(), eng.mom[: eng.d].clone(), eng.last_weights.clone(),
+                     eng.G[:, : eng.d].clone()))
+    (p0, m0, w0, G0), (p1, m1, w1, G1) = outs
+    segs = sorted(zip(eng.flat.offsets, eng.flat.numels))
+    assert w0.shape == w1.shape == (len(segs), n)
+    assert float(w1[:, 3].abs().max()) == 0.0          # the reversed gradient is never selected
+    assert torch.equal(G0, G1)                          # the same gradient rows reached the GAR
+    m = n - f - 2
+    differ = [s for s in range(len(segs)) if not torch.equal(w0[s], w1[s])]
+    for s in differ:
+        off, numel = segs[s]
+        X = G1[:, off:off + numel].double()
+        D = torch.cdist(X, X) ** 2
+        D.fill_diagonal_(float("inf"))
+        score = D.sort(1).values[:, : n - f - 2].sum(1).sort().values
+        assert (score[m] - score[m - 1]).abs() <= 1e-4 * score[m - 1].abs(), (s, score[m - 1:m + 1])
+    if steps == 1:
+        assert len(differ) <= len(segs) // 10
+        for s, (off, numel) in enumerate(segs):
+            if s not in differ:      # same selection: equal up to fp32 rounding of 12-row sums
+                for a0, a1 in ((p0, p1), (m0, m1)):
+                    x0, x1 = a0[off:off + numel].double(), a1[off:off + numel].double()
+                    assert ((x0 - x1).norm() / x0.norm().clamp_min(1e-30)).item() < 1e-6, s
+    else:
+        assert not differ
+        assert torch.equal(p0, p1) and torch.equal(m0, m1)
 
 
 @pytest.mark.gpu
