@@ -168,7 +168,7 @@ def main():
     d = num_parameters(model)
     fp32 = a.precision == "fp32"
     if fp32:
-        a.exchange_dtype, a.no_lp_weights, a.no_worker_batching = "fp32", True, True
+        a.exchange_dtype, a.no_lp_weights = "fp32", True   # worker batching: the grouped-channel executor
     xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
     amp = {} if not fp32 else {"autocast_dtype": None}
     cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,

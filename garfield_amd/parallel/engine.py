@@ -55,6 +55,9 @@ LAYERWISE_RULES = {"krum", "bulyan", "brute", "aksel"}   # per-layer != flat onl
 # selection, one segmented combine + SGD); "0" runs the per-segment loop (the reference form).
 LW_DEVICE = os.environ.get("GARFIELD_LW_DEVICE", "1") != "0"
 LW_JOB = 32768   # coordinates per job of the segmented kernels (a multiple of 8)
+# fp32 (no autocast) worker batching on the GPU: the grouped-channel executor (parallel/grouped_fp32.py);
+# "0" keeps the per-worker path.
+FP32_GROUPED = os.environ.get("GARFIELD_FP32_GROUPED", "1") != "0"
 
 
 @dataclass
@@ -218,15 +221,25 @@ class RobustDataParallel:
     def _want_grouping(self, model: nn.Module) -> bool:
         from garfield_amd.parallel import grouped
 
+        from garfield_amd.parallel import grouped_fp32
+
         wb = self.cfg.worker_batching
         if wb is None:
             wb = self.device.type == "cuda"
-        if not (wb and self._supports_grouping and grouped.supports(model)):
+        self._fp32_grouped = False
+        if not (wb and self._supports_grouping):
             return False
         if self.device.type == "cuda":
             # bf16 activations with bf16 working weights (the grouped kernels' contract)
-            return self.cfg.lp_weights and self.cfg.autocast_dtype == torch.bfloat16
-        return True
+            if self.cfg.lp_weights and self.cfg.autocast_dtype == torch.bfloat16:
+                return grouped.supports(model)
+            # the reference's fp32: the grouped-channel executor (ATen / MIOpen grouped convolutions)
+            if (self.cfg.autocast_dtype is None and not self.cfg.lp_weights and not self.cfg.channels_last
+                    and FP32_GROUPED and grouped_fp32.supports(model)):
+                self._fp32_grouped = True
+                return True
+            return False
+        return grouped.supports(model)
 
     def _want_sharded(self) -> bool:
         from garfield_amd.parallel.sharded import SUPPORTED
@@ -273,8 +286,13 @@ class RobustDataParallel:
         from garfield_amd.parallel.sharded import overlap_enabled
 
         buckets = ("layer4", "layer3") if self._sharded else ()
-        self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn, marks=buckets, offsets=offsets,
-                                    signals=overlap_enabled(self.ctx.world_size))
+        if getattr(self, "_fp32_grouped", False):
+            from garfield_amd.parallel.grouped_fp32 import GroupedChannelResNet
+
+            self._gexec = GroupedChannelResNet(self.model, self.k, sink, loss_fn, offsets=offsets)
+        else:
+            self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn, marks=buckets, offsets=offsets,
+                                        signals=overlap_enabled(self.ctx.world_size))
         self._gx = self._gy = None
         self._gsrc = None
         self._gsrc_refs = None
@@ -701,8 +719,10 @@ class RobustDataParallel:
     def _ensure_gbuf(self, B: int, sample_shape: tuple, label_shape: tuple = (), label_dtype=torch.int64) -> None:
         shape = (self.k * B, *sample_shape)
         if self._gx is None or tuple(self._gx.shape) != shape:
-            dt = torch.bfloat16 if self.device.type == "cuda" else torch.float32
-            self._gx = torch.empty(shape, dtype=dt, device=self.device, memory_format=torch.channels_last)
+            fp32 = getattr(self, "_fp32_grouped", False)
+            dt = torch.bfloat16 if (self.device.type == "cuda" and not fp32) else torch.float32
+            fmt = torch.contiguous_format if fp32 else torch.channels_last
+            self._gx = torch.empty(shape, dtype=dt, device=self.device, memory_format=fmt)
             self._gy = torch.empty((self.k * B, *label_shape), dtype=label_dtype, device=self.device)
             self._ggraph = None
             self._gsrc = None
@@ -711,7 +731,7 @@ class RobustDataParallel:
         """The grouped step's static input buffers ([k*batch, *sample_shape] channels_last, and
         the labels) for a producer that writes each step's batch in place
         (``data.fresh.DeviceBatches.attach``): no staging copy. None when the step is not grouped."""
-        if self._gexec is None:
+        if self._gexec is None or getattr(self, "_fp32_grouped", False):   # the producer writes bf16 rows
             return None
         self._ensure_gbuf(int(batch), tuple(sample_shape), (), label_dtype)
         return self._gx, self._gy

@@ -269,6 +269,38 @@ def test_layerwise_krum_device_equals_segment_loop_bitwise(cuda, monkeypatch, mo
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_fp32_grouped_channel_path_matches_per_worker_engine(cuda, graph):
+    """fp32 (the reference's precision) with worker batching: the grouped-channel executor
+    (MIOpen grouped convolutions, per-(worker, channel) BatchNorm) against the per-worker fp32
+    engine. The two run different convolution algorithms (fp32 rounding differs by ~1e-3 of a
+    gradient), so: the first update within 2e-2 and the parameters within 2e-3 after 3 averaged
+    steps (reference layout), HIP-graph replays included. The exact math
+    is checked in fp64 on the CPU (tests/test_grouped_fp32_cpu.py)."""
+    outs, deltas = [], []
+    for wb in (False, True):
+        torch.manual_seed(0)
+        cfg = EngineConfig(gar="average", f=0, workers_per_rank=8, lr=0.05, momentum=0.9, weight_decay=5e-4,
+                           autocast_dtype=None, lp_weights=False, worker_batching=wb, cuda_graph=graph,
+                           exchange_dtype=torch.float32)
+        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+        assert (eng._gexec is not None) == wb
+        p0 = eng.flat.reference_vector().clone()     # reference layout: both engines comparable
+        for it in range(3):
+            eng.step(synthetic_batches(8, 8, (3, 32, 32), 10, cuda, seed=40 + it))
+            if it == 0:
+                deltas.append(eng.flat.reference_vector() - p0)
+        torch.cuda.synchronize()
+        if wb and graph:
+            assert eng._ggraph is not None
+        outs.append(eng.flat.reference_vector().clone())
+    rel = ((deltas[1] - deltas[0]).norm() / deltas[0].norm()).item()     # the first update
+    assert rel < 2e-2, rel
+    rel = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
+    assert rel < 2e-3, rel
+
+
+@pytest.mark.gpu
 def test_byzps_one_gpu_grouped_matches_plain_engine(cuda):
     """Byzantine-server mode on one GPU (the rank is a server replica hosting its workers,
     MAR median over one model = identity): the grouped HIP-graph worker path runs and the
