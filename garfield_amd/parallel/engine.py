@@ -763,7 +763,7 @@ class RobustDataParallel:
         """The k local workers' forward/backward as one grouped pass (HIP graph from the
         second step on); every worker's gradient lands in its exchange row."""
         if (self.device.type == "cuda" and self.cfg.cuda_graph and not self._graph_failed and self.step_count >= 1
-                and self._ggraph is None):
+                and self._ggraph is None and getattr(self._gexec, "graph_safe", True)):
             self._capture_grouped()
         if self._ggraph is not None:
             self._ggraph.replay()

@@ -1,27 +1,31 @@
-"""Worker-grouped fp32 execution: the k logical workers of a rank as ONE pass in a
-GROUPED-CHANNEL layout, for the reference's fp32 precision.
+"""Worker-grouped fp32 execution: the k logical workers of a rank as ONE pass, for the
+reference's fp32 precision (``pytorch_impl/applications/Garfield_CC/trainer.py:296-303``: no
+autocast).
 
-The bf16 grouped executor (``parallel/grouped.py``) relies on hand-written bf16 kernels. At
-the reference's fp32 precision (``pytorch_impl/applications/Garfield_CC/trainer.py:296-303``:
-no autocast) the engine used to fall back to k per-worker forward/backward passes (MIOpen
-graphs, ~7.5k small kernels per ResNet-50 step). Here the k workers' activations are laid out
-as ONE tensor ``[B, k*C, H, W]`` (worker g owns channels ``[g*C, (g+1)*C)``), so that every
-per-worker quantity is an ordinary per-CHANNEL quantity of a single ATen call:
+The bf16 grouped executor (``parallel/grouped.py``) relies on hand-written bf16 kernels; at fp32
+the engine used to fall back to k per-worker forward/backward passes (~7.5k small kernels per
+ResNet-50 step). MIOpen's grouped fp32 convolutions are no way out either: their weight-gradient
+solvers for strided / 7x7 grouped layers are the naive reference kernels (25 ms of a 90 ms step,
+profiles/r3/rocprof_fp32_miopen_grouped.txt) and their Winograd kernels are not HIP-graph replay
+safe. Here every activation lives in a WORKER-MAJOR layout ``[k, C, B*H*W]`` (worker g's
+channels, then its B images' pixels), and every layer is a batched GEMM over the k workers:
 
-* a convolution is ``conv2d(x, W_rep, groups=k)`` with ``W_rep = W`` repeated k times along
-  the output channels: group g sees only worker g's channels, and the weight gradient of the
-  grouped convolution IS the per-worker weight gradient ([k*Cout, Cin, kh, kw] = [k][Cout]...);
-* BatchNorm over k*C channels normalises each (worker, channel) with that worker's batch
-  statistics, and its dγ/dβ of length k*C are the per-worker gradients; the k sequential
-  running-statistics updates of k independent workers are replayed from the per-worker
-  batch statistics by one ``gpu_bn_running_update`` launch;
-* ReLU, max/avg pooling and the residual additions are channel-wise, so unchanged;
-* the classifier is a batched matmul against the repeated weight, and the loss the mean
-  cross-entropy of every worker.
+* a 1x1 stride-1 convolution is ``bmm(W_rep [k, Cout, Cin], x [k, Cin, B*H*W])`` with ``W_rep``
+  the weight repeated k times: its weight gradient IS the k per-worker gradients;
+* a k x k (or strided) convolution first gathers its patches ``[k, Cin*KH*KW, B*Ho*Wo]`` in one
+  strided copy (``_Patches``), then the same batched GEMM; the data gradient adds each tap's
+  slice back (the adjoint gather);
+* BatchNorm is ``batch_norm`` of the ``[1, k*C, B*H*W]`` view: every (worker, channel) is
+  normalised with that worker's own batch statistics, and dγ/dβ of length k*C are the per-worker
+  gradients; the k sequential running-statistics updates of k independent workers are replayed
+  from the per-worker batch statistics (``gpu_bn_running_update``);
+* ReLU, pooling and the residual additions are elementwise / per plane;
+* the classifier is one more batched GEMM and the loss each worker's mean cross-entropy.
 
-Every per-worker weight gradient lands in that worker's exchange row through the GradSink
-(one multi-tensor cast kernel). Same math as k separate fp32 workers (checked on CPU against
-k independent forward/backward passes, tests/test_grouped_fp32_cpu.py).
+All GEMMs are plain fp32 library GEMMs (hipBLASLt through ``torch.bmm``). Every per-worker
+weight gradient lands in that worker's exchange row through the GradSink (one multi-tensor cast
+kernel). Exact against k independent workers run one after the other (fp64 on the CPU,
+tests/test_grouped_fp32_cpu.py).
 """
 from __future__ import annotations
 
@@ -50,6 +54,47 @@ def supports(model: nn.Module) -> bool:
     return isinstance(model.maxpool, (nn.MaxPool2d, nn.Identity))
 
 
+class _Act:
+    """A worker-major activation: t [k, C, B*H*W] and its image geometry."""
+
+    __slots__ = ("t", "B", "H", "W")
+
+    def __init__(self, t, B, H, W):
+        self.t, self.B, self.H, self.W = t, B, H, W
+
+    @property
+    def C(self):
+        return self.t.shape[1]
+
+
+class _Patches(torch.autograd.Function):
+    """[k, C, B, H, W] -> the patch matrix [k, C*KH*KW, B*Ho*Wo] (unfold's (ci, i, j) row order)
+    as ONE strided copy (ATen's unfold launches one im2col kernel per image: 5000 launches per
+    ResNet-50 step); the backward adds each tap's gradient slice back, KH*KW strided adds."""
+
+    @staticmethod
+    def forward(ctx, x5, k, d, p, s):
+        G, C, B, H, W = x5.shape
+        (kh, kw), (dh, dw), (ph, pw), (sh, sw) = k, d, p, s
+        xp = F.pad(x5, (pw, pw, ph, ph)) if (ph or pw) else x5
+        Hp, Wp = H + 2 * ph, W + 2 * pw
+        Ho, Wo = (Hp - dh * (kh - 1) - 1) // sh + 1, (Wp - dw * (kw - 1) - 1) // sw + 1
+        st = xp.stride()
+        v = xp.as_strided((G, C, kh, kw, B, Ho, Wo), (st[0], st[1], dh * st[3], dw * st[4], st[2], sh * st[3], sw * st[4]))
+        ctx.geom = (G, C, B, H, W, kh, kw, dh, dw, ph, pw, sh, sw, Ho, Wo)
+        return v.reshape(G, C * kh * kw, B * Ho * Wo)
+
+    @staticmethod
+    def backward(ctx, gcol):
+        G, C, B, H, W, kh, kw, dh, dw, ph, pw, sh, sw, Ho, Wo = ctx.geom
+        g7 = gcol.reshape(G, C, kh, kw, B, Ho, Wo)
+        gx = torch.zeros((G, C, B, H + 2 * ph, W + 2 * pw), dtype=gcol.dtype, device=gcol.device)
+        for i in range(kh):
+            for j in range(kw):
+                gx[:, :, :, i * dh: i * dh + sh * (Ho - 1) + 1: sh, j * dw: j * dw + sw * (Wo - 1) + 1: sw] += g7[:, :, i, j]
+        return gx[:, :, :, ph: ph + H, pw: pw + W], None, None, None, None
+
+
 class GroupedChannelResNet:
     """``run(x, y)``: x [k*B, C, H, W] (worker g = rows [g*B, (g+1)*B)) and labels [k*B]; writes
     every worker's parameter gradient into its exchange row through ``sink`` and returns the
@@ -65,8 +110,9 @@ class GroupedChannelResNet:
         self.groups = int(groups)
         self.sink = sink
         self.marks = ()
+        self.graph_safe = True
         self._offsets = offsets or {}
-        self._leaves: list = []      # (parameter, repeated leaf, view shape of the per-worker gradient)
+        self._leaves: list = []      # (parameter, repeated leaf [k, ...])
         self._run_jobs: list = []
 
     # interface of GroupedResNet (no bucket marks on this path)
@@ -81,58 +127,71 @@ class GroupedChannelResNet:
 
     # ------------------------------------------------------------------ #
 
-    def _rep(self, p: torch.Tensor, dim0_shape) -> torch.Tensor:
-        """A leaf copy of p repeated k times along dim 0 (its gradient: the k per-worker ones)."""
+    def _rep(self, p: torch.Tensor, shape) -> torch.Tensor:
+        """A leaf copy of p repeated k times (leading dim k): its gradient holds the k per-worker ones."""
         G = self.groups
-        r = p.detach().unsqueeze(0).expand(G, *p.shape).reshape(*dim0_shape).requires_grad_(True)
+        r = p.detach().reshape(1, *shape).expand(G, *shape).contiguous().requires_grad_(True)
         self._leaves.append((p, r))
         return r
 
-    def _conv(self, x, conv: nn.Conv2d):
+    def _conv(self, a: _Act, conv: nn.Conv2d) -> _Act:
+        kh, kw = conv.kernel_size
+        cout, cin = conv.out_channels, conv.in_channels
+        # weight [Cout, Cin, KH, KW] -> [Cout, Cin*KH*KW] in unfold's (ci, i, j) column order
+        w = self._rep(conv.weight, (cout, cin * kh * kw))
+        if (kh, kw) == (1, 1) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (0, 0):
+            return _Act(torch.bmm(w, a.t), a.B, a.H, a.W)
         G = self.groups
-        w = self._rep(conv.weight, (G * conv.out_channels, *conv.weight.shape[1:]))
-        return F.conv2d(x, w, None, conv.stride, conv.padding, conv.dilation, G)
+        Ho = (a.H + 2 * conv.padding[0] - conv.dilation[0] * (kh - 1) - 1) // conv.stride[0] + 1
+        Wo = (a.W + 2 * conv.padding[1] - conv.dilation[1] * (kw - 1) - 1) // conv.stride[1] + 1
+        col = _Patches.apply(a.t.reshape(G, cin, a.B, a.H, a.W), (kh, kw), tuple(conv.dilation),
+                             tuple(conv.padding), tuple(conv.stride))
+        return _Act(torch.bmm(w, col), a.B, Ho, Wo)
 
-    def _bn(self, x, bn: nn.BatchNorm2d, relu: bool, res=None):
-        G = self.groups
-        gamma = self._rep(bn.weight, (G * bn.num_features,))
-        beta = self._rep(bn.bias, (G * bn.num_features,))
-        y, mean, invstd = torch.ops.aten.native_batch_norm(x, gamma, beta, None, None, True, 0.0, bn.eps)
+    def _bn(self, a: _Act, bn: nn.BatchNorm2d, relu: bool, res: "_Act | None" = None) -> _Act:
+        G, C = self.groups, a.C
+        gamma = self._rep(bn.weight, (C,)).view(G * C)
+        beta = self._rep(bn.bias, (C,)).view(G * C)
+        x3 = a.t.reshape(1, G * C, -1)
+        y, mean, invstd = torch.ops.aten.native_batch_norm(x3, gamma, beta, None, None, True, 0.0, bn.eps)
         if bn.running_mean is not None:
-            rows = x.shape[0] * x.shape[2] * x.shape[3]          # rows per worker
-            self._run_jobs.append((mean.detach(), invstd.detach(), bn, rows))
+            self._run_jobs.append((mean.detach(), invstd.detach(), bn, x3.shape[2]))
+        y = y.view(G, C, -1)
         if res is not None:
-            y = y + res
-        return F.relu(y) if relu else y
+            y = y + res.t
+        return _Act(F.relu(y) if relu else y, a.B, a.H, a.W)
 
-    def _block(self, blk, x):
-        out = self._bn(self._conv(x, blk.conv1), blk.bn1, True)
+    def _block(self, blk, a: _Act) -> _Act:
+        out = self._bn(self._conv(a, blk.conv1), blk.bn1, True)
         if isinstance(blk, Bottleneck):
             out = self._bn(self._conv(out, blk.conv2), blk.bn2, True)
             last_conv, last_bn = blk.conv3, blk.bn3
         else:
             last_conv, last_bn = blk.conv2, blk.bn2
-        sc = x if blk.downsample is None else self._bn(self._conv(x, blk.downsample[0]), blk.downsample[1], False)
+        sc = a if blk.downsample is None else self._bn(self._conv(a, blk.downsample[0]), blk.downsample[1], False)
         return self._bn(self._conv(out, last_conv), last_bn, True, res=sc)
 
-    def forward(self, xg: torch.Tensor) -> torch.Tensor:
-        """xg: [B, k*C, H, W] -> logits [k, B, classes]."""
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x [k*B, C, H, W] -> logits [k, B, classes]."""
         m, G = self.model, self.groups
-        x = self._bn(self._conv(xg, m.conv1), m.bn1, True)
+        B = x.shape[0] // G
+        t = x.reshape(G, B, x.shape[1], -1).transpose(1, 2).reshape(G, x.shape[1], -1)
+        a = self._bn(self._conv(_Act(t, B, x.shape[2], x.shape[3]), m.conv1), m.bn1, True)
         if isinstance(m.maxpool, nn.MaxPool2d):
-            x = F.max_pool2d(x, m.maxpool.kernel_size, m.maxpool.stride, m.maxpool.padding, m.maxpool.dilation,
-                             m.maxpool.ceil_mode)
+            mp = m.maxpool
+            img = a.t.reshape(1, G * a.C * a.B, a.H, a.W)     # pooling is per plane: no layout change
+            y = F.max_pool2d(img, mp.kernel_size, mp.stride, mp.padding, mp.dilation, mp.ceil_mode)
+            a = _Act(y.reshape(G, a.C, -1), a.B, y.shape[2], y.shape[3])
         for name in ("layer1", "layer2", "layer3", "layer4"):
             for blk in getattr(m, name):
-                x = self._block(blk, x)
-        B = x.shape[0]
-        pooled = x.mean((2, 3)).view(B, G, -1).transpose(0, 1)           # [k, B, F]
+                a = self._block(blk, a)
+        pooled = a.t.reshape(G, a.C, a.B, a.H * a.W).mean(3)             # [k, F, B]
         fc = m.fc
-        w = self._rep(fc.weight, (G, *fc.weight.shape))                  # [k, O, F]
-        logits = torch.bmm(pooled, w.transpose(1, 2))
+        w = self._rep(fc.weight, tuple(fc.weight.shape))                 # [k, O, F]
+        logits = torch.bmm(w, pooled)                                    # [k, O, B]
         if fc.bias is not None:
-            logits = logits + self._rep(fc.bias, (G, fc.bias.shape[0]))[:, None, :]
-        return logits
+            logits = logits + self._rep(fc.bias, (fc.bias.shape[0],))[:, :, None]
+        return logits.transpose(1, 2)                                    # [k, B, O]
 
     def _running_updates(self) -> None:
         """The k sequential running-statistics updates of k workers, per BatchNorm."""
@@ -164,8 +223,7 @@ class GroupedChannelResNet:
         B = x.shape[0] // G
         self._leaves = []
         self._run_jobs = []
-        xg = x.reshape(G, B, *x.shape[1:]).transpose(0, 1).reshape(B, G * x.shape[1], *x.shape[2:])
-        logits = self.forward(xg.contiguous())                           # [k, B, O]
+        logits = self.forward(x.contiguous())                            # [k, B, O]
         per = F.cross_entropy(logits.reshape(G * B, -1), y.view(G * B), reduction="none").view(G, B).mean(1)
         per.sum().backward()
         self._running_updates()
