@@ -699,6 +699,53 @@ void g_transpose_multi(const std::vector<at::Tensor>& srcs, const std::vector<at
                                  stream_of(dev));
 }
 
+// Layer-wise GAR building blocks (gar_layerwise.hip)
+void g_lw_gram(const RowSet& rs, const at::Tensor& jobs, const at::Tensor& seg_lo, const at::Tensor& slabs,
+               const at::Tensor& gram) {
+  check_gpu(rs);
+  TORCH_CHECK(jobs.device() == rs.device && jobs.scalar_type() == at::kLong && jobs.dim() == 2 && jobs.size(1) == 3 &&
+                  jobs.is_contiguous(), "gpu_lw_gram: jobs must be a contiguous int64 [J, 3] tensor on the rows' device");
+  TORCH_CHECK(seg_lo.device() == rs.device && seg_lo.scalar_type() == at::kInt && seg_lo.dim() == 1 &&
+                  seg_lo.is_contiguous() && seg_lo.numel() >= 2,
+              "gpu_lw_gram: seg_lo must be a contiguous int32 [L + 1] tensor on the rows' device");
+  const int J = static_cast<int>(jobs.size(0)), L = static_cast<int>(seg_lo.numel() - 1);
+  const int np = garfield::gpu::gram_padded(rs.n);
+  TORCH_CHECK(slabs.numel() >= static_cast<int64_t>(J) * garfield::gpu::gram_slab_floats(rs.n),
+              "gpu_lw_gram: slab workspace too small");
+  TORCH_CHECK(gram.numel() >= static_cast<int64_t>(L) * np * np, "gpu_lw_gram: gram output too small");
+  c10::hip::HIPGuard guard(rs.device.index());
+  garfield::gpu::lw_gram(rs.table, rs.n, rs.dt, jobs.data_ptr<int64_t>(), J, seg_lo.data_ptr<int>(), L, fptr(slabs),
+                         fptr(gram), stream_of(rs.device));
+}
+
+void g_lw_combine_sgd(const RowSet& rs, const at::Tensor& jobs, const at::Tensor& seg_off, int64_t base,
+                      const at::Tensor& weights, const at::Tensor& param, const at::Tensor& mom,
+                      const c10::optional<at::Tensor>& shadow, double lr, double momentum, double dampening,
+                      double weight_decay, bool nesterov, bool first_step) {
+  check_gpu(rs);
+  TORCH_CHECK(jobs.device() == rs.device && jobs.scalar_type() == at::kLong && jobs.dim() == 2 && jobs.size(1) == 3 &&
+                  jobs.is_contiguous(), "gpu_lw_combine_sgd: jobs must be a contiguous int64 [J, 3] tensor");
+  TORCH_CHECK(seg_off.device() == rs.device && seg_off.scalar_type() == at::kLong && seg_off.is_contiguous(),
+              "gpu_lw_combine_sgd: seg_off must be a contiguous int64 [L + 1] tensor");
+  const int64_t L = seg_off.numel() - 1;
+  TORCH_CHECK(weights.numel() >= L * rs.n, "gpu_lw_combine_sgd: weights must be [L, n]");
+  TORCH_CHECK(param.numel() >= rs.d && mom.numel() >= rs.d, "gpu_lw_combine_sgd: parameter/momentum too small");
+  void* sh = nullptr;
+  int sh_dt = garfield::kBF16;
+  if (shadow.has_value() && shadow->defined()) {
+    TORCH_CHECK(shadow->is_cuda() && shadow->device() == rs.device && shadow->is_contiguous() && shadow->numel() >= rs.d,
+                "gpu_lw_combine_sgd: shadow must be a contiguous tensor of >= d elements on the rows' device");
+    sh_dt = dtype_code(*shadow);
+    sh = shadow->data_ptr();
+  }
+  garfield::gpu::SgdArgs a{static_cast<float>(lr), static_cast<float>(momentum), static_cast<float>(dampening),
+                           static_cast<float>(weight_decay), nesterov ? 1 : 0, first_step ? 1 : 0};
+  c10::hip::HIPGuard guard(rs.device.index());
+  garfield::gpu::lw_combine_sgd(rs.table, rs.n, rs.dt, jobs.data_ptr<int64_t>(), static_cast<int>(jobs.size(0)),
+                                fptr(weights), fptr(param), fptr(mom), sh, sh_dt, a, seg_off.data_ptr<int64_t>(), base,
+                                stream_of(rs.device));
+}
+
 // Large gradient sets: x an [n, d] GPU matrix (unit column stride, row stride ld, 16-bit or fp32).
 int large_dtype(const at::Tensor& x, const at::Tensor& out) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 && x.size(0) >= 1 &&
@@ -1241,54 +1288,27 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, py::arg("gram"), py::arg("n"), py::arg("f"), py::arg("m"), py::arg("weights"), py::arg("order"),
      py::arg("scores"), py::arg("batch") = 1,
      "Multi-Krum selection weights on device; batch > 1: gram [batch, np, np] -> weights [batch, n]");
-  m.def("gpu_lw_gram", [](const at::Tensor& G, const at::Tensor& jobs, const at::Tensor& seg_lo,
-                          const at::Tensor& slabs, const at::Tensor& gram) {
-    const RowSet rs = rows_from_2d(G, true);
-    check_gpu(rs);
-    TORCH_CHECK(jobs.device() == rs.device && jobs.scalar_type() == at::kLong && jobs.dim() == 2 && jobs.size(1) == 3 &&
-                    jobs.is_contiguous(), "gpu_lw_gram: jobs must be a contiguous int64 [J, 3] tensor on G's device");
-    TORCH_CHECK(seg_lo.device() == rs.device && seg_lo.scalar_type() == at::kInt && seg_lo.dim() == 1 &&
-                    seg_lo.is_contiguous() && seg_lo.numel() >= 2,
-                "gpu_lw_gram: seg_lo must be a contiguous int32 [L + 1] tensor on G's device");
-    const int J = static_cast<int>(jobs.size(0)), L = static_cast<int>(seg_lo.numel() - 1);
-    const int np = garfield::gpu::gram_padded(rs.n);
-    TORCH_CHECK(slabs.numel() >= static_cast<int64_t>(J) * garfield::gpu::gram_slab_floats(rs.n),
-                "gpu_lw_gram: slab workspace too small");
-    TORCH_CHECK(gram.numel() >= static_cast<int64_t>(L) * np * np, "gpu_lw_gram: gram output too small");
-    c10::hip::HIPGuard guard(rs.device.index());
-    garfield::gpu::lw_gram(rs.table, rs.n, rs.dt, jobs.data_ptr<int64_t>(), J, seg_lo.data_ptr<int>(), L,
-                           fptr(slabs), fptr(gram), stream_of(rs.device));
-  }, "Per-segment MFMA Gram matrices of the [n, d] rows: gram [L, np, np]; jobs [J, 3] int64 (start, end, "
-     "segment) ranges inside one segment each, in segment order; seg_lo [L + 1] int32 first job per segment");
-  m.def("gpu_lw_combine_sgd", [](const at::Tensor& G, const at::Tensor& jobs, const at::Tensor& seg_off,
-                                 const at::Tensor& weights, const at::Tensor& param, const at::Tensor& mom,
-                                 const c10::optional<at::Tensor>& shadow, double lr, double momentum, double dampening,
-                                 double weight_decay, bool nesterov, bool first_step) {
-    const RowSet rs = rows_from_2d(G, true);
-    check_gpu(rs);
-    TORCH_CHECK(jobs.device() == rs.device && jobs.scalar_type() == at::kLong && jobs.dim() == 2 && jobs.size(1) == 3 &&
-                    jobs.is_contiguous(), "gpu_lw_combine_sgd: jobs must be a contiguous int64 [J, 3] tensor");
-    TORCH_CHECK(seg_off.device() == rs.device && seg_off.scalar_type() == at::kLong && seg_off.is_contiguous(),
-                "gpu_lw_combine_sgd: seg_off must be a contiguous int64 [L + 1] tensor");
-    const int64_t L = seg_off.numel() - 1;
-    TORCH_CHECK(weights.numel() >= L * rs.n, "gpu_lw_combine_sgd: weights must be [L, n]");
-    TORCH_CHECK(param.numel() >= rs.d && mom.numel() >= rs.d, "gpu_lw_combine_sgd: parameter/momentum too small");
-    void* sh = nullptr;
-    int sh_dt = garfield::kBF16;
-    if (shadow.has_value() && shadow->defined()) {
-      TORCH_CHECK(shadow->is_cuda() && shadow->device() == rs.device && shadow->is_contiguous() && shadow->numel() >= rs.d,
-                  "gpu_lw_combine_sgd: shadow must be a contiguous tensor of >= d elements on G's device");
-      sh_dt = dtype_code(*shadow);
-      sh = shadow->data_ptr();
-    }
-    garfield::gpu::SgdArgs a{static_cast<float>(lr), static_cast<float>(momentum), static_cast<float>(dampening),
-                             static_cast<float>(weight_decay), nesterov ? 1 : 0, first_step ? 1 : 0};
-    c10::hip::HIPGuard guard(rs.device.index());
-    garfield::gpu::lw_combine_sgd(rs.table, rs.n, rs.dt, jobs.data_ptr<int64_t>(), static_cast<int>(jobs.size(0)),
-                                  fptr(weights), fptr(param), fptr(mom), sh, sh_dt, a, seg_off.data_ptr<int64_t>(),
-                                  stream_of(rs.device));
-  }, "Per-segment weighted combine of the [n, d] rows (weights [L, n]) fused with the SGD update; args (G, jobs, "
-     "seg_off, weights, param, mom, shadow|None, lr, momentum, dampening, weight_decay, nesterov, first_step)");
+  def_rows(m, "gpu_lw_gram",
+           [](const at::Tensor& G, const at::Tensor& jobs, const at::Tensor& seg_lo, const at::Tensor& slabs,
+              const at::Tensor& gram) { g_lw_gram(rows_from_2d(G, true), jobs, seg_lo, slabs, gram); },
+           [](const std::vector<at::Tensor>& L, const at::Tensor& jobs, const at::Tensor& seg_lo, const at::Tensor& slabs,
+              const at::Tensor& gram) { g_lw_gram(rows_from_list(L, true), jobs, seg_lo, slabs, gram); },
+           "Per-segment MFMA Gram matrices of the rows: gram [L, np, np]; jobs [J, 3] int64 (start, end, segment) "
+           "ranges inside one segment each, in segment order; seg_lo [L + 1] int32 first job per segment");
+  def_rows(m, "gpu_lw_combine_sgd",
+           [](const at::Tensor& G, const at::Tensor& jobs, const at::Tensor& seg_off, int64_t base, const at::Tensor& w,
+              const at::Tensor& p, const at::Tensor& mom, const c10::optional<at::Tensor>& sh, double lr, double mo,
+              double da, double wd, bool ne, bool first) {
+             g_lw_combine_sgd(rows_from_2d(G, true), jobs, seg_off, base, w, p, mom, sh, lr, mo, da, wd, ne, first);
+           },
+           [](const std::vector<at::Tensor>& L, const at::Tensor& jobs, const at::Tensor& seg_off, int64_t base,
+              const at::Tensor& w, const at::Tensor& p, const at::Tensor& mom, const c10::optional<at::Tensor>& sh,
+              double lr, double mo, double da, double wd, bool ne, bool first) {
+             g_lw_combine_sgd(rows_from_list(L, true), jobs, seg_off, base, w, p, mom, sh, lr, mo, da, wd, ne, first);
+           },
+           "Per-segment weighted combine of the rows (weights [L, n]) fused with the SGD update; args (rows, jobs "
+           "(local coordinates), seg_off (global), base (global coordinate of local 0), weights, param, mom, "
+           "shadow|None, lr, momentum, dampening, weight_decay, nesterov, first_step)");
   m.def("gpu_bulyan_select", [](const at::Tensor& gram, int n, int f, int mm, int t, const at::Tensor& W) {
     c10::hip::HIPGuard guard(gram.device().index());
     TORCH_CHECK(W.numel() >= static_cast<int64_t>(t) * n, "W too small");

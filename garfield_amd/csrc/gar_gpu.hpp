@@ -61,10 +61,11 @@ void lw_gram(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs
              float* slabs, float* gram, hipStream_t stream);
 // lw_combine_sgd: per coordinate of segment s, g = Σ_j weights[s][j] row_j, then the SGD update
 // of param / momentum (and the shadow copy), as combine_sgd does with one weight vector.
-// seg_off: [L + 1] int64 segment offsets (jobs start at a multiple of 8 from their segment start).
+// jobs in LOCAL coordinates of rows / param / momentum / shadow, base = the global coordinate of
+// local 0 (a sharded bucket's owned range); seg_off: [L + 1] int64 global segment offsets.
 void lw_combine_sgd(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const float* weights,
                     float* param, float* momentum_buf, void* shadow, int shadow_dt, SgdArgs args,
-                    const int64_t* seg_off, hipStream_t stream);
+                    const int64_t* seg_off, int64_t base, hipStream_t stream);
 
 // ---- Coordinate-wise rules (median, trimmed mean, MeaMed, ...) -------------
 // W/t are only read for kBulyanTail; seed/threshold only for kCondense.

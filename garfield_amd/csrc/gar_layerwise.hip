@@ -193,6 +193,23 @@ __device__ __forceinline__ void gather8(const RowTable& rows, const int* sel, co
   }
 }
 
+// one element with gather8's arithmetic (4 rows per step): a group's elements that a job boundary
+// splits (a shard edge inside an 8-wide group) get the bits the 8-wide path would give them
+template <int DT>
+__device__ __forceinline__ float gather1_grouped(const RowTable& rows, const int* sel, const float* wsel, int cnt,
+                                                 int64_t x) {
+  float acc = 0.f;
+  int j = 0;
+  for (; j + 4 <= cnt; j += 4) {
+    const float v0 = load_one<DT>(rows.p[sel[j]], x), v1 = load_one<DT>(rows.p[sel[j + 1]], x);
+    const float v2 = load_one<DT>(rows.p[sel[j + 2]], x), v3 = load_one<DT>(rows.p[sel[j + 3]], x);
+    const float w0 = wsel[j], w1 = wsel[j + 1], w2 = wsel[j + 2], w3 = wsel[j + 3];
+    acc += w0 * v0 + w1 * v1 + w2 * v2 + w3 * v3;
+  }
+  for (; j < cnt; ++j) acc += wsel[j] * load_one<DT>(rows.p[sel[j]], x);
+  return acc;
+}
+
 __device__ __forceinline__ void sgd_one(float g, float& p, float& buf, const SgdArgs& a) {
   if (a.weight_decay != 0.f) g += a.weight_decay * p;
   if (a.momentum != 0.f) {
@@ -202,18 +219,20 @@ __device__ __forceinline__ void sgd_one(float g, float& p, float& buf, const Sgd
   p -= a.lr * g;
 }
 
-// jobs: (start, end, segment, segment start) rows of 4 int64 here (lw_combine_sgd expands them)
+// jobs: (start, end, segment) in LOCAL coordinates of the rows / param / mom / shadow; base: the
+// global (flat-vector) coordinate of local 0 (a sharded bucket's owned range), seg_off global.
 template <int DT>
 __global__ __launch_bounds__(256) void k_lw_combine_sgd(RowTable rows, int n, const int64_t* __restrict__ jobs,
                                                         const float* __restrict__ weights, float* __restrict__ param,
                                                         float* __restrict__ mom, void* __restrict__ shadow,
-                                                        int shadow_dt, SgdArgs args, const int64_t* __restrict__ seg_off) {
+                                                        int shadow_dt, SgdArgs args, const int64_t* __restrict__ seg_off,
+                                                        int64_t base) {
   __shared__ int sel[kMaxRows];
   __shared__ float wsel[kMaxRows];
   __shared__ int cnt_s;
   const int64_t a = jobs[3 * blockIdx.x], b = jobs[3 * blockIdx.x + 1];
   const int s = static_cast<int>(jobs[3 * blockIdx.x + 2]);
-  const int64_t s0 = seg_off[s], s1 = seg_off[s + 1];
+  const int64_t s0 = seg_off[s] - base, s1 = seg_off[s + 1] - base;   // local segment bounds
   if (threadIdx.x == 0) {
     int c = 0;
     for (int j = 0; j < n; ++j) {
@@ -224,32 +243,37 @@ __global__ __launch_bounds__(256) void k_lw_combine_sgd(RowTable rows, int n, co
   }
   __syncthreads();
   const int cnt = cnt_s;
-  // 8-wide groups counted from the SEGMENT start (as a per-segment combine sees them); the
-  // segment's last (s1 - s0) % 8 elements are its scalar tail
-  const int64_t sv = s0 + ((s1 - s0) & ~static_cast<int64_t>(7));
-  for (int64_t x = a + static_cast<int64_t>(threadIdx.x) * 8; x < (b < sv ? b : sv); x += 256 * 8) {
-    float acc[8];
-    gather8<DT>(rows, sel, wsel, cnt, x, acc);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      float p = param[x + c];
-      float bf = (args.momentum != 0.f && !args.first_step) ? mom[x + c] : 0.f;
-      sgd_one(acc[c], p, bf, args);
-      param[x + c] = p;
-      if (shadow) store_one(shadow, shadow_dt, x + c, p);
-      if (args.momentum != 0.f) mom[x + c] = bf;
-    }
-  }
-  const int64_t t0 = a > sv ? a : sv;
-  for (int64_t x = t0 + threadIdx.x; x < b; x += 256) {
-    float g = 0.f;
-    for (int j = 0; j < cnt; ++j) g += wsel[j] * load_one<DT>(rows.p[sel[j]], x);
+  auto update = [&](int64_t x, float g) {
     float p = param[x];
     float bf = (args.momentum != 0.f && !args.first_step) ? mom[x] : 0.f;
     sgd_one(g, p, bf, args);
     param[x] = p;
     if (shadow) store_one(shadow, shadow_dt, x, p);
     if (args.momentum != 0.f) mom[x] = bf;
+  };
+  // 8-wide groups counted from the SEGMENT start (as a per-segment combine sees them); the
+  // segment's last (s1 - s0) % 8 elements are its scalar tail
+  const int64_t sv = s0 + ((s1 - s0) & ~static_cast<int64_t>(7));
+  const int64_t va = s0 + ((a - s0 + 7) & ~static_cast<int64_t>(7));        // first whole group in [a, b)
+  const int64_t ve_max = b < sv ? b : sv;
+  const int64_t ve = va + ((ve_max > va ? ve_max - va : 0) & ~static_cast<int64_t>(7));   // end of whole groups
+  auto tail_one = [&](int64_t x) {
+    float g = 0.f;
+    for (int j = 0; j < cnt; ++j) g += wsel[j] * load_one<DT>(rows.p[sel[j]], x);
+    return g;
+  };
+  for (int64_t x = a + threadIdx.x; x < (va < b ? va : b); x += 256)        // a split group's head
+    update(x, x < sv ? gather1_grouped<DT>(rows, sel, wsel, cnt, x) : tail_one(x));
+  for (int64_t x = va + static_cast<int64_t>(threadIdx.x) * 8; x < ve; x += 256 * 8) {
+    float acc[8];
+    gather8<DT>(rows, sel, wsel, cnt, x, acc);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) update(x + c, acc[c]);
+  }
+  for (int64_t x = (ve > a ? ve : a) + threadIdx.x; x < b; x += 256) {
+    if (x < va) continue;
+    // a split group's rest, or the segment tail
+    update(x, x < sv ? gather1_grouped<DT>(rows, sel, wsel, cnt, x) : tail_one(x));
   }
 }
 
@@ -269,9 +293,10 @@ template <int DT> struct LwGram {
 };
 template <int DT> struct LwCombine {
   static void run(const RowTable& rows, int n, const int64_t* jobs, int njobs, const float* w, float* param,
-                  float* mom, void* shadow, int shadow_dt, SgdArgs a, const int64_t* seg_off, hipStream_t s) {
+                  float* mom, void* shadow, int shadow_dt, SgdArgs a, const int64_t* seg_off, int64_t base,
+                  hipStream_t s) {
     hipLaunchKernelGGL(k_lw_combine_sgd<DT>, dim3(njobs), dim3(256), 0, s, rows, n, jobs, w, param, mom, shadow,
-                       shadow_dt, a, seg_off);
+                       shadow_dt, a, seg_off, base);
   }
 };
 
@@ -288,9 +313,9 @@ void lw_gram(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs
 
 void lw_combine_sgd(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const float* weights,
                     float* param, float* momentum_buf, void* shadow, int shadow_dt, SgdArgs args,
-                    const int64_t* seg_off, hipStream_t stream) {
+                    const int64_t* seg_off, int64_t base, hipStream_t stream) {
   if (njobs <= 0) return;
-  by_dtype<LwCombine>(dt, rows, n, jobs, njobs, weights, param, momentum_buf, shadow, shadow_dt, args, seg_off,
+  by_dtype<LwCombine>(dt, rows, n, jobs, njobs, weights, param, momentum_buf, shadow, shadow_dt, args, seg_off, base,
                       stream);
 }
 

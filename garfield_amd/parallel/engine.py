@@ -252,9 +252,11 @@ class RobustDataParallel:
         if self.ctx.world_size > 1 and not self.ctx.is_distributed:
             raise ValueError("sharded aggregation over several ranks needs an initialised process group")
         if self.cfg.layerwise:
-            if self.cfg.shard_gar:
-                raise ValueError("layerwise aggregation runs on the redundant path (shard_gar=False)")
-            return False
+            if self.cfg.gar != "krum":      # layer-wise Krum shards: per-segment partial Grams are additive
+                if self.cfg.shard_gar:
+                    raise ValueError("sharded layer-wise aggregation supports krum (shard_gar=False for others)")
+                return False
+            return True
         if self.cfg.gar not in SUPPORTED:
             raise ValueError(f"sharded aggregation does not support {self.cfg.gar!r} (shard_gar=False)")
         return True
@@ -493,8 +495,8 @@ class RobustDataParallel:
         ws = []
         for off, numel in self._segments():
             seg = self.G[:, off:off + numel]
-            if cuda and rule in WEIGHTED_RULES:
-                w = self._weights(rule, kw, seg)
+            if rule in WEIGHTED_RULES:
+                w = self._weights(rule, kw, seg if cuda else seg.float())
                 ws.append(w.clone())
                 gar.combine_into(seg, w, g[off:off + numel])
             else:
@@ -543,7 +545,7 @@ class RobustDataParallel:
         G = self.G[:, : self.d]
         C.gpu_lw_gram(G, lw["jobs"], lw["seg_lo"], lw["slabs"], lw["gram"])
         C.gpu_krum_select(lw["gram"], n, f, m, lw["w"], lw["order"], lw["scores"], lw["L"])
-        C.gpu_lw_combine_sgd(G, lw["jobs"], lw["seg_off"], lw["w"], self.flat.data[: self.d], self.mom[: self.d],
+        C.gpu_lw_combine_sgd(G, lw["jobs"], lw["seg_off"], 0, lw["w"], self.flat.data[: self.d], self.mom[: self.d],
                              self._shadow, cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
         self.last_weights = lw["w"]
 

@@ -282,7 +282,9 @@ class ShardedAggregator:
         if not self._started:
             self.start_exchange()
         self._gathers = []
-        if e.device.type == "cuda":
+        if cfg.layerwise:
+            self._layerwise(cfg, first)
+        elif e.device.type == "cuda":
             self._gpu(cfg, first)
         else:
             self._cpu(cfg, first)
@@ -546,6 +548,109 @@ class ShardedAggregator:
         W = ws.get("bulyan_W", t * n)
         C.gpu_bulyan_select(gram_total, n, f, m, t, W)
         return W
+
+    # ------------------------------------------------------------------ #
+    # Layer-wise Krum, sharded: per-parameter-segment squared distances are additive over the
+    # coordinate shards too, so each rank adds the partial Grams of its owned coordinates per
+    # segment ([L, n, n]), the partials are summed over ranks in rank order, every rank selects
+    # every segment (identically), and each rank combines + updates its owned coordinates with
+    # their segment's weights.
+
+    def _lw_plan(self):
+        """Per bucket: the owned range's pieces of every parameter segment (local coordinates)."""
+        plan = getattr(self, "_lwp", None)
+        if plan is not None:
+            return plan
+        e = self.e
+        from garfield_amd.parallel.engine import LW_JOB
+
+        segs = sorted(zip(e.flat.offsets, e.flat.numels))
+        offs = [o for o, _ in segs] + [segs[-1][0] + segs[-1][1]]
+        L = len(segs)
+        plan = {"L": L, "offs": offs, "buckets": {}}
+        for b in self.buckets:
+            o0, o1 = b.own.start, b.own.stop
+            jobs, seg_lo = [], [0]
+            for si in range(L):
+                x0, x1 = max(offs[si], o0), min(offs[si + 1], o1)
+                for a in range(x0, x1, LW_JOB):
+                    jobs.append((a - o0, min(a + LW_JOB, x1) - o0, si))
+                seg_lo.append(len(jobs))
+            plan["buckets"][b.lo] = (jobs, seg_lo)
+        if e.device.type == "cuda":
+            C, dev, n = e._C, e.device, self.n
+            np_ = C.gram_padded(n)
+            plan["seg_off"] = torch.tensor(offs, dtype=torch.int64, device=dev)
+            for lo, (jobs, seg_lo) in list(plan["buckets"].items()):
+                J = max(len(jobs), 1)
+                plan["buckets"][lo] = dict(
+                    J=len(jobs),
+                    jobs=torch.tensor(jobs if jobs else [(0, 0, 0)], dtype=torch.int64, device=dev),
+                    seg_lo=torch.tensor(seg_lo, dtype=torch.int32, device=dev),
+                    slabs=torch.empty(J * C.gram_slab_floats(n), dtype=torch.float32, device=dev),
+                    gram=torch.empty(L * np_ * np_, dtype=torch.float32, device=dev))
+            plan["w"] = torch.empty((L, n), dtype=torch.float32, device=dev)
+            plan["order"] = torch.empty((L, n), dtype=torch.int32, device=dev)
+            plan["scores"] = torch.empty((L, n), dtype=torch.float32, device=dev)
+        self._lwp = plan
+        return plan
+
+    def _layerwise(self, cfg, first: bool) -> None:
+        e = self.e
+        n, f = self.n, cfg.f
+        m = cfg.m if cfg.m is not None else n - f - 2
+        plan = self._lw_plan()
+        L = plan["L"]
+        if e.device.type == "cuda":
+            C = e._C
+            total = None
+            for b in self.buckets:          # partial per-segment Grams as the buckets land
+                self._wait(b)
+                bp = plan["buckets"][b.lo]
+                if bp["J"] == 0:
+                    continue
+                C.gpu_lw_gram(b.rows, bp["jobs"], bp["seg_lo"], bp["slabs"], bp["gram"])
+                total = bp["gram"].clone() if total is None else total.add_(bp["gram"])
+            if total is None:
+                total = torch.zeros_like(next(iter(plan["buckets"].values()))["gram"])
+            total = self._sum_over_ranks(total)
+            C.gpu_krum_select(total, n, f, m, plan["w"], plan["order"], plan["scores"], L)
+            e.last_weights = plan["w"]
+            args = (cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
+            for b in self._update_order():
+                bp = plan["buckets"][b.lo]
+                if bp["J"]:
+                    p, mom, sh = self._param(b)
+                    C.gpu_lw_combine_sgd(b.rows, bp["jobs"][: bp["J"]], plan["seg_off"], b.own.start, plan["w"],
+                                         p, mom, sh, *args)
+                self._gather_bucket(b)
+            return
+        # CPU (gloo): per-segment partial squared distances of the owned coordinates (fp64)
+        for b in self.buckets:
+            self._wait(b)
+        D = torch.zeros((L, n, n), dtype=torch.float64)
+        Xs = {}
+        for b in self.buckets:
+            X = torch.stack([r.double() for r in b.rows])                 # [n, S] owned shard of b
+            Xs[b.lo] = X
+            for a, z, si in plan["buckets"][b.lo][0]:
+                Y = X[:, a:z]
+                sq = (Y * Y).sum(1)
+                D[si] += sq[:, None] + sq[None, :] - 2.0 * (Y @ Y.T)
+        D = self._sum_over_ranks(D)
+        W = torch.zeros((L, n), dtype=torch.float32)
+        for si in range(L):
+            Ds = D[si].clamp_min(0)
+            Ds.fill_diagonal_(math.inf)
+            W[si] = ref.krum_weights(Ds, f, m).float()
+        e.last_weights = W
+        for b in self._update_order():
+            X = Xs[b.lo].float()
+            g = torch.zeros(b.S, dtype=torch.float32)
+            for a, z, si in plan["buckets"][b.lo][0]:
+                g[a:z] = (W[si][:, None] * X[:, a:z]).sum(0)
+            self._sgd_cpu(b, g, first)
+            self._gather_bucket(b)
 
     # ------------------------------------------------------------------ #
     # CPU (gloo): the owned shards concatenated, the C++ / oracle building blocks

@@ -219,3 +219,43 @@ def test_two_rank_collusion_sharded_matches_allgather():
         for name in ("0r1.pt", "1r0.pt", "1r1.pt"):
             other = torch.load(os.path.join(d, name), weights_only=True)["flat"]
             assert torch.allclose(a, other, rtol=1e-5, atol=1e-6), name
+
+
+def _lw_sharded_worker(rank, world, port, outdir, shard):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from garfield_amd.parallel.comm import init_distributed, shutdown
+
+    ctx = init_distributed(backend="gloo", device="cpu")
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                             EngineConfig(gar="krum", f=1, workers_per_rank=4, byzantine={3: "reverse"},
+                                          shard_gar=shard, layerwise=True, lr=0.05))
+    assert (eng._shard is not None) == shard
+    b = synthetic_batches(4, 8, (1, 28, 28), 10, "cpu", seed=rank)
+    for _ in range(3):
+        eng.step(b)
+    w = eng.last_weights
+    torch.save({"flat": eng.flat_model().clone(), "mom": eng.momentum_vector()[: eng.d].clone(),
+                "w": w.clone() if w is not None else None}, os.path.join(outdir, f"{int(shard)}r{rank}.pt"))
+    shutdown(ctx)
+
+
+def test_two_rank_sharded_layerwise_krum_matches_redundant():
+    """Layer-wise Krum with the sharded exchange (per-segment partial distances summed over
+    ranks, per-segment selections, owned coordinates combined by segment) == the redundant
+    layer-wise path; replicas identical."""
+    with tempfile.TemporaryDirectory() as d:
+        for shard in (False, True):
+            mp.spawn(_lw_sharded_worker, args=(2, free_port(), d, shard), nprocs=2, join=True)
+        r = {k: torch.load(os.path.join(d, f"{k}.pt"), weights_only=True) for k in ("0r0", "0r1", "1r0", "1r1")}
+        assert torch.equal(r["1r0"]["flat"], r["1r1"]["flat"]) and torch.equal(r["0r0"]["flat"], r["0r1"]["flat"])
+        w0, w1 = r["0r0"]["w"], r["1r0"]["w"]
+        assert w1.shape == w0.shape and w1.shape[0] >= 2                  # one selection per parameter tensor
+        assert torch.equal(w1, w0.to(w1.dtype))                            # the same per-segment selections
+        assert float(w1[:, 3].abs().max()) == 0.0                          # the reversed slot is never selected
+        ref_flat = r["0r0"]["flat"]
+        rel = ((r["1r0"]["flat"] - ref_flat).norm() / ref_flat.norm()).item()
+        assert rel < 1e-5, rel
+        m0, m1 = r["0r0"]["mom"], r["1r0"]["mom"]
+        assert ((m1 - m0).norm() / m0.norm()).item() < 1e-5

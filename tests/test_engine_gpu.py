@@ -301,6 +301,27 @@ def test_fp32_grouped_channel_path_matches_per_worker_engine(cuda, graph):
 
 
 @pytest.mark.gpu
+def test_sharded_layerwise_krum_matches_unsharded_on_gpu(cuda):
+    """Layer-wise Krum through the sharded aggregator (one rank: per-bucket segment Grams over the
+    owned ranges, batched selection, per-bucket segmented combine with the bucket's base offset)
+    equals the unsharded device path: same per-segment weights, parameters to fp32 rounding."""
+    outs = []
+    for shard in (False, True):
+        torch.manual_seed(0)
+        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, byzantine={3: "reverse"}, lr=0.05, momentum=0.9,
+                           weight_decay=5e-4, layerwise=True, shard_gar=shard, cuda_graph=False)
+        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+        assert (eng._shard is not None) == shard
+        eng.step(synthetic_batches(8, 4, (3, 32, 32), 10, cuda, seed=3))
+        torch.cuda.synchronize()
+        outs.append((eng.flat.reference_vector().clone(), eng.last_weights.clone()))
+    (p0, w0), (p1, w1) = outs
+    assert torch.equal(w0, w1)
+    rel = ((p1 - p0).norm() / p0.norm()).item()
+    assert rel < 1e-6, rel
+
+
+@pytest.mark.gpu
 def test_byzps_one_gpu_grouped_matches_plain_engine(cuda):
     """Byzantine-server mode on one GPU (the rank is a server replica hosting its workers,
     MAR median over one model = identity): the grouped HIP-graph worker path runs and the
