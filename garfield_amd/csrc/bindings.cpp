@@ -12,6 +12,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -620,8 +621,31 @@ void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, i
   TORCH_CHECK(static_cast<int64_t>(g.N) * g.H * g.W * g.C < INT32_MAX && static_cast<int64_t>(g.N) * g.Ho * g.Wo < INT32_MAX,
               "gpu_iconv: tensor too large");
   c10::hip::HIPGuard guard(x.device().index());
+  // pm 0 (auto): the halo-staged 3x3 kernel whenever it fits (GARFIELD_CONV3X3=0 disables it);
+  // pm 22 / 24: force it with 2 / 4 pixel fragments per wave; 1..14: the implicit-GEMM kernel
+  static const bool c3 = [] {
+    const char* e = std::getenv("GARFIELD_CONV3X3");
+    return !(e && e[0] == '0');
+  }();
+  if (!transpose_w && (pm == 22 || pm == 24)) {
+    TORCH_CHECK(garfield::gpu::conv3x3_pick(g, static_cast<int>(cout)) != 0 &&
+                    garfield::gpu::conv3x3_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap,
+                                                static_cast<int>(pm - 20), stream_of(x.device())),
+                "gpu_iconv: pm ", pm, " (halo-staged 3x3 kernel) does not fit this shape");
+    return;
+  }
+  if (!transpose_w && pm == 0 && c3 &&
+      garfield::gpu::conv3x3_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap, 0,
+                                  stream_of(x.device())))
+    return;
   garfield::gpu::iconv_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap, static_cast<int>(pm),
                             transpose_w, stream_of(x.device()));
+}
+
+int64_t g_conv3x3_pick(int64_t n, int64_t h, int64_t w, int64_t c, int64_t cout) {
+  garfield::gpu::Im2col g{static_cast<int>(n), static_cast<int>(h), static_cast<int>(w), static_cast<int>(c), 3, 3,
+                          1, 1, 1, 1, 1, 1, static_cast<int>(h), static_cast<int>(w), 0};
+  return garfield::gpu::conv3x3_pick(g, static_cast<int>(cout));
 }
 
 // Row-major NT GEMM (gemm_nt.hip): c = a · bᵀ (+ add); a [M, K], b [N, K], c/add [M, N], all contiguous
@@ -671,21 +695,32 @@ void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, co
 }
 
 // Transposes of many bf16 matrices in one launch: dsts[i] = srcs[i]ᵀ (2-D, contiguous, 16-B aligned,
-// both dims multiples of 8).
+// both dims multiples of 8). A 4-D pair is a k x k convolution weight: src the channels_last
+// [Cout, Cin, KH, KW] weight, dst the channels_last [Cin, Cout, KH, KW] flipped transpose
+// dst[ci, co, i, j] = src[co, ci, KH-1-i, KW-1-j] (its data gradient's weight).
 void g_transpose_multi(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
   TORCH_CHECK(srcs.size() == dsts.size(), "gpu_transpose_multi: one dst per src");
   if (srcs.empty()) return;
   std::vector<const uint16_t*> sp;
   std::vector<uint16_t*> dp;
-  std::vector<int> R, C;
+  std::vector<int> R, C, T;
   const auto dev = srcs[0].device();
   for (size_t i = 0; i < srcs.size(); ++i) {
     const auto& a = srcs[i];
     const auto& b = dsts[i];
-    TORCH_CHECK(a.is_cuda() && a.device() == dev && a.scalar_type() == at::kBFloat16 && a.dim() == 2 &&
-                    a.is_contiguous() && b.device() == dev && b.scalar_type() == at::kBFloat16 && b.dim() == 2 &&
-                    b.is_contiguous() && b.size(0) == a.size(1) && b.size(1) == a.size(0),
-                "gpu_transpose_multi: src [R, C] and dst [C, R] contiguous bf16 on one device");
+    TORCH_CHECK(a.is_cuda() && a.device() == dev && a.scalar_type() == at::kBFloat16 && b.device() == dev &&
+                    b.scalar_type() == at::kBFloat16 && a.dim() == b.dim() && b.size(0) == a.size(1) &&
+                    b.size(1) == a.size(0),
+                "gpu_transpose_multi: src [R, C(, KH, KW)] and dst [C, R(, KH, KW)] bf16 on one device");
+    if (a.dim() == 2) {
+      TORCH_CHECK(a.is_contiguous() && b.is_contiguous(), "gpu_transpose_multi: 2-D matrices must be contiguous");
+      T.push_back(1);
+    } else {
+      TORCH_CHECK(a.dim() == 4 && a.size(2) == b.size(2) && a.size(3) == b.size(3) &&
+                      a.is_contiguous(at::MemoryFormat::ChannelsLast) && b.is_contiguous(at::MemoryFormat::ChannelsLast),
+                  "gpu_transpose_multi: 4-D weights must be channels_last [Cout, Cin, KH, KW] -> [Cin, Cout, KH, KW]");
+      T.push_back(static_cast<int>(a.size(2) * a.size(3)));
+    }
     TORCH_CHECK(a.size(0) % 8 == 0 && a.size(1) % 8 == 0 && reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0,
                 "gpu_transpose_multi: dims multiples of 8, 16-byte aligned");
@@ -696,7 +731,7 @@ void g_transpose_multi(const std::vector<at::Tensor>& srcs, const std::vector<at
   }
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::transpose_multi(sp.data(), dp.data(), R.data(), C.data(), static_cast<int>(sp.size()),
-                                 stream_of(dev));
+                                 stream_of(dev), T.data());
 }
 
 // Layer-wise GAR building blocks (gar_layerwise.hip)
@@ -937,8 +972,24 @@ void g_iwgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw,
     gs = out.stride(0);
   }
   c10::hip::HIPGuard guard(x.device().index());
+  // the halo-staged 3x3 kernel whenever it fits (GARFIELD_WGRAD3X3=0 keeps the implicit kernel)
+  static const bool h3 = [] {
+    const char* e = std::getenv("GARFIELD_WGRAD3X3");
+    return !(e && e[0] == '0');
+  }();
+  if (h3 && garfield::gpu::wgrad3x3_nhwc(u16(x), u16(dy), g, static_cast<int>(cout), static_cast<int>(groups),
+                                         M / groups, static_cast<int>(splits), out.data_ptr(), bf16, ss, gs,
+                                         stream_of(x.device())))
+    return;
   garfield::gpu::iwgrad_nhwc(u16(x), u16(dy), g, static_cast<int>(cout), static_cast<int>(groups), M / groups,
                              static_cast<int>(splits), out.data_ptr(), bf16, ss, gs, stream_of(x.device()));
+}
+
+bool g_wgrad3x3_fits(int64_t n, int64_t h, int64_t w, int64_t c, int64_t cout, int64_t groups) {
+  garfield::gpu::Im2col g{static_cast<int>(n), static_cast<int>(h), static_cast<int>(w), static_cast<int>(c), 3, 3,
+                          1, 1, 1, 1, 1, 1, static_cast<int>(h), static_cast<int>(w), 0};
+  if (groups < 1 || n % groups) return false;
+  return garfield::gpu::wgrad3x3_fits(g, static_cast<int>(cout), n / groups * h * w);
 }
 
 garfield::gpu::Im2col pool_geometry(const at::Tensor& x, const at::Tensor& y, const at::Tensor& idx, int64_t k,
@@ -1477,6 +1528,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("y"), py::arg("add") = py::none(), py::arg("pm") = 0,
         py::arg("transpose_w") = false);
 
+  m.def("conv3x3_pick", &g_conv3x3_pick, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("c"), py::arg("cout"),
+        "Pixel fragments per wave the halo-staged 3x3 kernel uses for this NHWC shape (0: it does not fit)");
+  m.def("wgrad3x3_fits", &g_wgrad3x3_fits, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("c"), py::arg("cout"),
+        py::arg("groups"), "True when gpu_iwgrad of this 3x3 / stride-1 / pad-1 shape runs the halo-staged kernel");
   m.def("gpu_iwgrad", &g_iwgrad, "Per-worker implicit-GEMM weight gradient on MFMA: out[s, g] = Σ over pixel "
         "split s of worker g of dyᵀ · patches(x); args (x, dy, kh, kw, sh, sw, ph, pw, dh, dw, groups, out, splits)");
   m.def("stem_supported", &garfield::gpu::stem_supported, py::arg("h"), py::arg("w"),

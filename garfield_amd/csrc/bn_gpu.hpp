@@ -82,9 +82,11 @@ int gemm_nt_stats_rows(int cfg);
 // statistics tiles of an M x N x K launch of cfg with rg-row workers: H rows, E entries each
 // (stats buffer: ceil(M / H) * E * 6 * N floats)
 void gemm_nt_stats_geometry(int cfg, int64_t M, int N, int K, int64_t rg, int64_t* H, int* E);
-// dst_i [C_i, R_i] = src_i [R_i, C_i]ᵀ for bf16 matrices (R_i, C_i multiples of 8), in one launch per 40
+// dst_i [C_i, R_i] = src_i [R_i, C_i]ᵀ for bf16 matrices (R_i, C_i multiples of 8), in one launch per 40;
+// taps[i] > 1: src_i is [R][taps][C], dst_i [C][taps][R] with the taps reversed (the flipped transposed
+// weight of a k x k convolution's data gradient)
 void transpose_multi(const uint16_t* const* srcs, uint16_t* const* dsts, const int* R, const int* C, int count,
-                     hipStream_t stream);
+                     hipStream_t stream, const int* taps = nullptr);
 void bn_finalize_tiles(const float* stats, int64_t H, int E, int64_t M, int64_t rg, int groups, int C,
                        const float* gamma, const float* beta, float eps, float* mean, float* istd, float* scale,
                        float* shift, hipStream_t stream);
@@ -117,6 +119,21 @@ void im2col_nhwc(const uint16_t* x, const Im2col& g, uint16_t* col, hipStream_t 
 // gradient this computes (flipped taps, swapped channel roles).
 void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
                 int pm, bool transpose_w, hipStream_t stream);
+// Halo-staged 3x3 / stride-1 / pad-1 convolution (conv3x3_nhwc.hip): same contract as iconv_nhwc
+// without transpose_w; C % 64 == 0, Cout % 64 == 0, tiles of whole image rows. conv3x3_pick returns
+// the pixel fragments per wave (4 or 2) it would use, 0 when the shape does not fit; conv3x3_nhwc
+// returns false (and launches nothing) in that case. pmf <= 0: auto.
+int conv3x3_pick(const Im2col& g, int Cout);
+bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
+                  int pmf, hipStream_t stream);
+// Halo-staged per-worker weight gradient of the same 3x3 convolutions (conv3x3_nhwc.hip), same
+// contract as iwgrad_nhwc; splits cut each worker's 128-pixel tiles into contiguous ranges (an empty
+// range writes a zero slab). wgrad3x3_fits: the shape fits (rg whole images); otherwise
+// wgrad3x3_nhwc launches nothing and returns false.
+bool wgrad3x3_fits(const Im2col& g, int Cout, int64_t rg);
+bool wgrad3x3_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
+                   int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride,
+                   hipStream_t stream);
 // Max pooling over NHWC bf16 (C % 8 == 0); idx: the window tap of each output maximum
 // (one byte per output element), consumed by the gather backward.
 void maxpool_fwd_nhwc(const uint16_t* x, const Im2col& g, uint16_t* y, uint8_t* idx, hipStream_t stream);

@@ -1,0 +1,459 @@
+// Halo-staged 3x3 / stride-1 / pad-1 convolution on MFMA (NHWC, bf16 in, fp32 accumulate), gfx950.
+//
+// The implicit-GEMM kernel of iconv_nhwc.hip stages, for every one of the nine taps, the shifted
+// 64-channel input tile of its output pixels: the same input bytes travel L2 -> LDS nine times
+// (a 256-pixel x 64-channel tile: 9 x 32 KB per 64-channel block, plus 9 x 8 KB of weights), and the
+// one-stage-ahead ring of its 256-pixel variant leaves the load latency exposed. Measured on the
+// CIFAR ResNet-18 step this is 26 % of the bf16 MFMA peak (profiles/r3/configs/rocprof_r18_krum_f2.txt).
+//
+// Here a workgroup's output tile is TR WHOLE image rows (BM = 64 * PMF pixels, W | BM), and its
+// input is staged ONCE per 64-channel block as a zero-padded halo: per image segment of the tile,
+// (rows + 2) x (W + 2) pixels (a 32-wide image: 10 x 34 pixels for 256 outputs, 1.33x instead of
+// 9x). The nine taps then read their B fragments from the halo at a uniform shift (i * (W + 2) + j),
+// and only the weight tap tiles stream through a 3-stage global_load_lds ring. Tiles spanning
+// several small images (8x8, 4x4) stage one padded image per segment, so image borders are zeros
+// in LDS and no tap needs a mask.
+//
+//   y[m, co] = Σ_{i, j, ci} x[n, h + i - 1, w + j - 1, ci] · W[co, i, j, ci]   (+ add[m, co])
+//
+// GEMM view as in iconv_nhwc.hip: A = weight rows (co), B = input pixels, v_mfma_f32_16x16x32_bf16,
+// wave tile 16*PMF pixels x 64 channels, 4 waves stacked over pixels (workgroup 64*PMF x 64).
+// LDS images are 128-byte rows (one pixel's or one channel's 64 bf16) with the 16-byte chunk
+// index XOR-swizzled by (row & 7) on the global side (glds writes lane-linear), so a fragment read
+// (16 rows x one chunk) touches every bank once on consecutive rows.
+//
+// The data gradient of this convolution is the same kernel on dy with the flipped, transposed
+// weight Wd[ci][i'][j'][co] = W[co][2-i'][2-j'][ci] (refreshed once per step for every layer by
+// transpose_multi with taps = 9), padding 1 again.
+#include <cstdlib>
+
+#include "bn_gpu.hpp"
+#include "gar_device.hpp"
+
+namespace garfield {
+namespace gpu {
+using namespace dev;
+namespace {
+
+using lds_ptr = __attribute__((address_space(3))) void*;
+
+__device__ __attribute__((aligned(16))) uint4 g_c3_zero[8];   // 128 zero bytes: padded pixels
+
+struct Halo {
+  int TR;    // output rows per tile (BM / W)
+  int TRI;   // output rows per image segment: min(TR, H)
+  int SW;    // staged columns: W + 2
+  int SEGP;  // staged pixels per segment: (TRI + 2) * SW
+  int NPIX;  // staged pixels per tile: (TR / TRI) * SEGP
+  int nu;    // halo glds instructions per wave: ceil(NPIX / 32) <= NU
+  int lw;    // log2 W (W divides the power-of-two tile, so W and TRI are powers of two)
+  int lt;    // log2 TRI
+};
+
+template <int PMF, int NU, bool ADD>
+__global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                 Im2col g, Halo hp, int Cout, uint16_t* y, const uint16_t* add) {
+  constexpr int NSW = 3;               // weight ring stages
+  constexpr int BM = 64 * PMF;         // output pixels per workgroup
+  constexpr int XB = NU * 4096;        // halo bytes (NU glds rounds of 4 waves x 8 pixels)
+  constexpr int WB = 64 * 128;         // one weight tap tile: 64 co x 64 ci
+  __shared__ __attribute__((aligned(16))) char lds[XB + NSW * WB];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int M = g.N * g.H * g.W;
+  const int rows = g.N * g.H;
+  const int R0 = blockIdx.x * hp.TR;   // first output (global) row of the tile
+  const int m0 = blockIdx.x * BM;
+  const int co0 = blockIdx.y * 64;
+  const int lc = lane & 7;             // this lane's 16-byte slot of a staged row
+
+  // halo sources, computed once: element offset of (pixel, logical chunk) or -1 for a zero pixel
+  int soff[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int p = (u * 4 + wave) * 8 + (lane >> 3);
+    const int seg = p / hp.SEGP;
+    const int rem = p - seg * hp.SEGP;
+    const int r = rem / hp.SW, c = rem - (rem / hp.SW) * hp.SW;
+    const int grow = R0 + seg * hp.TRI + r - 1;                    // global input row
+    const int hl = (R0 + seg * hp.TRI) % g.H + r - 1;              // its row inside the image
+    const bool ok = p < hp.NPIX && grow < rows && hl >= 0 && hl < g.H && c >= 1 && c <= g.W;
+    soff[u] = ok ? (grow * g.W + c - 1) * g.C + (lc ^ (p & 7)) * 8 : -1;
+  }
+  const uint64_t az = reinterpret_cast<uint64_t>(reinterpret_cast<const uint16_t*>(g_c3_zero) + lc * 8);
+
+  // weight tap tile sources: rows (wave*2 + u)*8 + lane/8 of the 64-row tile
+  const int K = 9 * g.C;
+  const uint16_t* wsrc[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = (wave * 2 + u) * 8 + (lane >> 3);
+    wsrc[u] = w + static_cast<int64_t>(co0 + row) * K + (lc ^ (row & 7)) * 8;
+  }
+
+  auto issue_halo = [&](int cb) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      if (u < hp.nu) {
+        const uint64_t ax = reinterpret_cast<uint64_t>(x + soff[u] + cb * 64);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(soff[u] >= 0 ? ax : az),
+                                         (lds_ptr)(lds + (u * 4 + wave) * 1024), 16, 0, 0);
+      }
+    }
+  };
+  auto issue_w = [&](int s, int slot) {
+    const int cb = s / 9, tap = s - (s / 9) * 9;
+    const int off = tap * g.C + cb * 64;
+    char* base = lds + XB + slot * WB;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      __builtin_amdgcn_global_load_lds(wsrc[u] + off, (lds_ptr)(base + (wave * 2 + u) * 1024), 16, 0, 0);
+  };
+
+  // this lane's B rows: staged pixel of tap (0, 0) for each pixel fragment
+  const int fr = lane & 15, fq = lane >> 4;
+  int sp0[PMF];
+#pragma unroll
+  for (int r = 0; r < PMF; ++r) {
+    const int ml = (wave * PMF + r) * 16 + fr;
+    const int t = ml / g.W, col = ml - (ml / g.W) * g.W;
+    const int seg = t / hp.TRI;
+    sp0[r] = seg * hp.SEGP + (t - seg * hp.TRI) * hp.SW + col;
+  }
+
+  f32x4 acc[PMF][4];
+#pragma unroll
+  for (int r = 0; r < PMF; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ncb = g.C / 64;
+  const int steps = ncb * 9;
+  issue_halo(0);
+#pragma unroll
+  for (int s0 = 0; s0 < NSW - 1; ++s0)
+    if (s0 < steps) issue_w(s0, s0);
+
+  int tap = 0, cb = 0;
+  for (int s = 0; s < steps; ++s) {
+    if (tap == 0 || s + 1 >= steps) {
+      // a new halo (issued after the ring loads in flight), or the last stage: drain
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // W(s + 1) may stay in flight
+    }
+    __builtin_amdgcn_s_barrier();
+    if (s + NSW - 1 < steps) issue_w(s + NSW - 1, (s + NSW - 1) % NSW);
+    const char* wb = lds + XB + (s % NSW) * WB;
+    const int ti = tap / 3;
+    const int toff = ti * hp.SW + (tap - ti * 3);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 a[4], b[PMF];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int row = c * 16 + fr;
+        a[c] = *reinterpret_cast<const bf16x8*>(wb + row * 128 + (((ks * 4 + fq) ^ (row & 7)) * 16));
+      }
+#pragma unroll
+      for (int r = 0; r < PMF; ++r) {
+        const int sp = sp0[r] + toff;
+        b[r] = *reinterpret_cast<const bf16x8*>(lds + sp * 128 + (((ks * 4 + fq) ^ (sp & 7)) * 16));
+      }
+#pragma unroll
+      for (int r = 0; r < PMF; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[r], acc[r][c], 0, 0, 0);
+    }
+    // every wave's reads of this ring slot (and of the halo) retire before the next barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (++tap == 9) {
+      tap = 0;
+      if (++cb < ncb) {
+        __builtin_amdgcn_s_barrier();   // the halo is refilled only once every wave is done with it
+        issue_halo(cb);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int r = 0; r < PMF; ++r) {
+    const int m = m0 + (wave * PMF + r) * 16 + fr;
+    if (m >= M) continue;
+    const int64_t rowoff = static_cast<int64_t>(m) * Cout;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t off = rowoff + co0 + c * 16 + fq * 4;
+      float v[4] = {acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]};
+      if constexpr (ADD) {
+        const uint2 a = *reinterpret_cast<const uint2*>(add + off);
+        v[0] += bf16_to_f(static_cast<uint16_t>(a.x & 0xffffu));
+        v[1] += bf16_to_f(static_cast<uint16_t>(a.x >> 16));
+        v[2] += bf16_to_f(static_cast<uint16_t>(a.y & 0xffffu));
+        v[3] += bf16_to_f(static_cast<uint16_t>(a.y >> 16));
+      }
+      uint2 o;
+      o.x = static_cast<uint32_t>(f_to_bf16(v[0])) | (static_cast<uint32_t>(f_to_bf16(v[1])) << 16);
+      o.y = static_cast<uint32_t>(f_to_bf16(v[2])) | (static_cast<uint32_t>(f_to_bf16(v[3])) << 16);
+      *reinterpret_cast<uint2*>(y + off) = o;
+    }
+  }
+}
+
+// tile geometry for PMF pixel fragments per wave; false when the shape does not fit
+bool plan(const Im2col& g, int pmf, int nu_max, Halo& hp) {
+  const int BM = 64 * pmf;
+  if (g.W > BM || BM % g.W) return false;
+  hp.TR = BM / g.W;
+  hp.TRI = hp.TR < g.H ? hp.TR : g.H;
+  if ((hp.TR <= g.H && g.H % hp.TR) || (hp.TR > g.H && hp.TR % g.H)) return false;
+  hp.SW = g.W + 2;
+  hp.SEGP = (hp.TRI + 2) * hp.SW;
+  hp.NPIX = (hp.TR / hp.TRI) * hp.SEGP;
+  hp.nu = (hp.NPIX + 31) / 32;
+  hp.lw = 0;
+  while ((1 << hp.lw) < g.W) ++hp.lw;
+  hp.lt = 0;
+  while ((1 << hp.lt) < hp.TRI) ++hp.lt;
+  if ((1 << hp.lw) != g.W || (1 << hp.lt) != hp.TRI) return false;
+  return hp.nu <= nu_max;
+}
+
+template <int PMF, int NU>
+void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, const Halo& hp, int Cout, uint16_t* y,
+            const uint16_t* add, hipStream_t stream) {
+  const int tiles = (g.N * g.H + hp.TR - 1) / hp.TR;
+  const dim3 grid(tiles, Cout / 64);
+  if (add) hipLaunchKernelGGL((k_conv3x3<PMF, NU, true>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add);
+  else hipLaunchKernelGGL((k_conv3x3<PMF, NU, false>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add);
+}
+
+constexpr int kNuBig = 14;    // PMF 4: 14 x 4 KB halo + 3 x 8 KB ring = 80 KB (two workgroups per CU)
+constexpr int kNuSmall = 10;  // PMF 2: 40 + 24 = 64 KB
+
+// ---------------------------------------------------------------------------------------------
+// Per-worker weight gradient of the same convolutions, halo-staged:
+//
+//   dW_g[co, (i, j, ci)] = Σ_{m in worker g} dy[m, co] · x[n, h + i - 1, w + j - 1, ci]
+//
+// A workgroup owns one (64 co, 64 ci) block of ALL nine taps for one worker (and one pixel split of
+// it) and walks that worker's pixels in tiles of 128 (whole rows, as in the forward): per tile the dy
+// tile [128 px x 64 co] and the input halo [(rows + 2) x (W + 2) px x 64 ci] are staged ONCE, and each
+// 32-pixel k-step feeds the nine taps' MFMAs from the same dy fragments (the implicit kernel of
+// iconv_nhwc.hip stages one shifted input tile per tap row and re-reads dy per kernel row).
+// Both operands are reduced over pixels, so fragments are read transposed (ds_read_b64_tr_b16:
+// lane 4q+p of a 16-lane group addresses pixel row 8*grp + 4h + q, channels 16f + 4p .. +3). The
+// staged 128-byte rows carry their 16-byte chunks XOR-swizzled by bits 1 and 3 of the row, which makes
+// those reads conflict-free on consecutive rows. Wave tile: 2 co fragments x 2 ci fragments x 9 taps.
+__device__ __forceinline__ int tr_swz(int row) { return (((row >> 3) & 1) << 2) | (((row >> 1) & 1) << 1); }
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// ds_read_b64_tr_b16 through the compiler builtin (no LDS-DMA is in flight at the reads of this
+// kernel, so the vmcnt(0) the compiler puts in front of it costs nothing; the compiler then also
+// tracks the returned registers: inline-asm reads raced with co-resident workgroups' timing)
+__device__ __forceinline__ s16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)((lds_ptr)p));
+}
+
+template <int NU, bool OUT_BF16>
+__global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                  Im2col g, Halo hp, int Cout, int64_t rg, int tiles_per_split,
+                                                  void* out, int64_t split_stride, int64_t group_stride) {
+  constexpr int TP = 128;               // output pixels per tile
+  constexpr int DB = TP * 128;          // dy tile bytes
+  __shared__ __attribute__((aligned(16))) char lds[DB + NU * 4096];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int ncb = g.C / 64;
+  const int cb = blockIdx.x % ncb, ob = blockIdx.x / ncb;
+  const int c0 = cb * 64, co0 = ob * 64;
+  const int gi = blockIdx.y, sp = blockIdx.z;
+  const int K = 9 * g.C;
+  const int rows = g.N * g.H;
+  const int64_t pbeg = static_cast<int64_t>(gi) * rg;       // the worker's first pixel (an image start)
+  const int64_t pend = pbeg + rg;
+  const int ntiles = static_cast<int>((rg + TP - 1) / TP);
+  const int t0 = sp * tiles_per_split;
+  const int t1 = t0 + tiles_per_split < ntiles ? t0 + tiles_per_split : ntiles;
+  const int lc = lane & 7;
+  const uint64_t az = reinterpret_cast<uint64_t>(reinterpret_cast<const uint16_t*>(g_c3_zero) + lc * 8);
+
+  // halo pixel decomposition of this lane's glds rows (tile-independent)
+  int hrow[NU], hcol[NU], hsw[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int p = (u * 4 + wave) * 8 + (lane >> 3);
+    const int seg = p / hp.SEGP;
+    const int rem = p - seg * hp.SEGP;
+    const int r = rem / hp.SW;
+    const int c = rem - r * hp.SW;
+    const bool ok = u < hp.nu && p < hp.NPIX && c >= 1 && c <= g.W;
+    hrow[u] = ok ? (seg * hp.TRI + r - 1) : -(1 << 28);   // input row relative to the tile's first row
+    hcol[u] = (c - 1) * g.C + c0 + ((lc ^ tr_swz(p)) * 8);
+    hsw[u] = r - 1;                                        // row shift inside the segment's image
+  }
+
+  // transposed-read addresses: lane (grp, q, p) of pixel rows 8*grp + 4h + q of each 32-pixel step
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const int cf0 = 2 * (wave >> 1), kf0 = 2 * (wave & 1);
+
+  f32x4 acc[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[t][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int tile = t0; tile < t1; ++tile) {
+    const int64_t P0 = pbeg + static_cast<int64_t>(tile) * TP;   // first pixel of the tile
+    const int R0 = static_cast<int>(P0 / g.W);
+    const int h0 = R0 % g.H;
+    // dy tile: 128 pixels x 8 chunks, 4 glds per lane
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int m = (u * 4 + wave) * 8 + (lane >> 3);
+      const int64_t P = P0 + m;
+      const uint64_t a = reinterpret_cast<uint64_t>(dy + P * Cout + co0 + ((lc ^ tr_swz(m)) * 8));
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(P < pend ? a : az),
+                                       (lds_ptr)(lds + (u * 4 + wave) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      if (u < hp.nu) {
+        const int gr = R0 + hrow[u];
+        const int hl = h0 + hsw[u];
+        const bool ok = hrow[u] > -(1 << 27) && gr < rows && hl >= 0 && hl < g.H;
+        const uint64_t a = reinterpret_cast<uint64_t>(x + static_cast<int64_t>(gr) * g.W * g.C + hcol[u]);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? a : az),
+                                         (lds_ptr)(lds + DB + (u * 4 + wave) * 1024), 16, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // (a runtime loop: unrolled, the compiler hoists every tap's fragment address out of the tile
+    // loop and spills)
+#pragma unroll 1
+    for (int c = 0; c < 4; ++c) {
+      int hp0[2];   // halo pixel of tap (0, 0) for tile pixel 32*c + 8*grp + 4*h + q
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = 32 * c + 8 * grp + 4 * h + q;
+        const int t = m >> hp.lw, col = m & (g.W - 1);
+        const int seg = t >> hp.lt;
+        hp0[h] = seg * hp.SEGP + (t & (hp.TRI - 1)) * hp.SW + col;
+      }
+      // A = dyᵀ fragments of co fragments cf0, cf0 + 1: dy rows 32c + 8grp + 4h + q
+      s16x4 ra[4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int m = 32 * c + 8 * grp + 4 * h + q;
+          const int ch = 2 * (cf0 + u) + (pp >> 1);
+          ra[2 * u + h] = tr_read(lds + m * 128 + ((ch ^ tr_swz(m)) * 16) + (pp & 1) * 8);
+        }
+      bf16x8 a[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        a[u] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ra[2 * u], ra[2 * u + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int toff = (tap / 3) * hp.SW + (tap % 3);
+        s16x4 rb[4];
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int s = hp0[h] + toff;
+            const int ch = 2 * (kf0 + v) + (pp >> 1);
+            rb[2 * v + h] = tr_read(lds + DB + s * 128 + ((ch ^ tr_swz(s)) * 16) + (pp & 1) * 8);
+          }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const bf16x8 b = __builtin_bit_cast(bf16x8,
+                                              __builtin_shufflevector(rb[2 * v], rb[2 * v + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            acc[tap][u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b, acc[tap][u][v], 0, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_s_barrier();   // every wave is done with the tile before it is refilled
+  }
+
+  // D[co = 16 (cf0 + u) + 4 grp + e][ci = 16 (kf0 + v) + li] of every tap
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = co0 + (cf0 + u) * 16 + 4 * grp + e;
+          const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
+                            static_cast<int64_t>(co) * K + tap * g.C + c0 + (kf0 + v) * 16 + li;
+          if constexpr (OUT_BF16) static_cast<uint16_t*>(out)[o] = f_to_bf16(acc[tap][u][v][e]);
+          else static_cast<float*>(out)[o] = acc[tap][u][v][e];
+        }
+}
+
+constexpr int kNuWgrad = 10;   // 16 KB dy tile + 40 KB halo: two workgroups per CU
+
+}  // namespace
+
+bool wgrad3x3_fits(const Im2col& g, int Cout, int64_t rg) {
+  Halo hp;
+  return conv3x3_pick(g, Cout) != 0 && plan(g, 2, kNuWgrad, hp) && rg > 0 &&
+         rg % (static_cast<int64_t>(g.H) * g.W) == 0;
+}
+
+bool wgrad3x3_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
+                   int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride,
+                   hipStream_t stream) {
+  Halo hp;
+  if (!wgrad3x3_fits(g, Cout, rg) || !plan(g, 2, kNuWgrad, hp)) return false;
+  const int ntiles = static_cast<int>((rg + 127) / 128);
+  if (splits < 1) splits = 1;
+  const int per = (ntiles + splits - 1) / splits;
+  const dim3 grid((g.C / 64) * (Cout / 64), groups, splits);
+  if (out_bf16)
+    hipLaunchKernelGGL((k_wgrad3x3<kNuWgrad, true>), grid, dim3(256), 0, stream, x, dy, g, hp, Cout, rg, per, out,
+                       split_stride, group_stride);
+  else
+    hipLaunchKernelGGL((k_wgrad3x3<kNuWgrad, false>), grid, dim3(256), 0, stream, x, dy, g, hp, Cout, rg, per, out,
+                       split_stride, group_stride);
+  return true;
+}
+
+int conv3x3_pick(const Im2col& g, int Cout) {
+  if (g.KH != 3 || g.KW != 3 || g.sh != 1 || g.sw != 1 || g.ph != 1 || g.pw != 1 || g.dh != 1 || g.dw != 1 ||
+      g.C % 64 || Cout % 64 || g.Ho != g.H || g.Wo != g.W)
+    return 0;
+  Halo hp;
+  if (plan(g, 4, kNuBig, hp)) return 4;
+  if (plan(g, 2, kNuSmall, hp)) return 2;
+  return 0;
+}
+
+bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
+                  int pmf, hipStream_t stream) {
+  if (pmf <= 0) pmf = conv3x3_pick(g, Cout);
+  Halo hp;
+  if (pmf == 4 && conv3x3_pick(g, Cout) && plan(g, 4, kNuBig, hp)) {
+    launch<4, kNuBig>(x, w, g, hp, Cout, y, add, stream);
+    return true;
+  }
+  if (pmf == 2 && conv3x3_pick(g, Cout) && plan(g, 2, kNuSmall, hp)) {
+    launch<2, kNuSmall>(x, w, g, hp, Cout, y, add, stream);
+    return true;
+  }
+  return false;
+}
+
+}  // namespace gpu
+}  // namespace garfield

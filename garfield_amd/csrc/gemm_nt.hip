@@ -687,10 +687,13 @@ bool ws_fits(int i, int K) {
 // Transposes of many bf16 matrices in one launch: dst_j [C_j, R_j] = src_j [R_j, C_j]ᵀ (the
 // data-gradient GEMMs' B = Wᵀ of every 1x1 convolution, refreshed once per step). 64 x 64 tiles
 // through LDS (padded pitch), 16-byte loads and stores; R_j, C_j multiples of 8.
+// taps > 1: src is [R][taps][C] and dst [C][taps][R] with the taps reversed, dst[c][T-1-t][r] =
+// src[r][t][c]: the flipped, transposed weight of a k x k convolution's data gradient.
 struct TJob {
   const uint16_t* src;
   uint16_t* dst;
   int R, C;
+  int taps;
   int tile0;               // first tile of this job in the launch
 };
 constexpr int kTJobs = 40;
@@ -704,15 +707,20 @@ __global__ __launch_bounds__(256) void k_transpose_multi(TTable t) {
   int ji = 0;
   while (ji + 1 < t.n && static_cast<int>(blockIdx.x) >= t.j[ji + 1].tile0) ++ji;
   const TJob jb = t.j[ji];
-  const int tl = blockIdx.x - jb.tile0;
   const int tcol = (jb.C + 63) / 64;
+  const int per_tap = ((jb.R + 63) / 64) * tcol;
+  const int tap = (blockIdx.x - jb.tile0) / per_tap;
+  const int tl = blockIdx.x - jb.tile0 - tap * per_tap;
   const int r0 = (tl / tcol) * 64, c0 = (tl % tcol) * 64;
+  const int64_t sld = static_cast<int64_t>(jb.taps) * jb.C, dld = static_cast<int64_t>(jb.taps) * jb.R;
+  const uint16_t* src = jb.src + static_cast<int64_t>(tap) * jb.C;
+  uint16_t* dst = jb.dst + static_cast<int64_t>(jb.taps - 1 - tap) * jb.R;
   const int lr = threadIdx.x >> 3, lc = (threadIdx.x & 7) * 8;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int r = r0 + lr + 32 * k, c = c0 + lc;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (r < jb.R && c < jb.C) v = *reinterpret_cast<const uint4*>(jb.src + static_cast<int64_t>(r) * jb.C + c);
+    if (r < jb.R && c < jb.C) v = *reinterpret_cast<const uint4*>(src + r * sld + c);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -730,7 +738,7 @@ __global__ __launch_bounds__(256) void k_transpose_multi(TTable t) {
       for (int e = 0; e < 4; ++e)
         w[e] = static_cast<uint32_t>(tile[lc + 2 * e][lr + 32 * k]) |
                (static_cast<uint32_t>(tile[lc + 2 * e + 1][lr + 32 * k]) << 16);
-      *reinterpret_cast<uint4*>(jb.dst + static_cast<int64_t>(c) * jb.R + r) = make_uint4(w[0], w[1], w[2], w[3]);
+      *reinterpret_cast<uint4*>(dst + c * dld + r) = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
 }
@@ -738,14 +746,15 @@ __global__ __launch_bounds__(256) void k_transpose_multi(TTable t) {
 }  // namespace
 
 void transpose_multi(const uint16_t* const* srcs, uint16_t* const* dsts, const int* R, const int* C, int count,
-                     hipStream_t stream) {
+                     hipStream_t stream, const int* taps) {
   for (int b = 0; b < count; b += kTJobs) {
     TTable t{};
     int tiles = 0;
     t.n = count - b < kTJobs ? count - b : kTJobs;
     for (int i = 0; i < t.n; ++i) {
-      t.j[i] = TJob{srcs[b + i], dsts[b + i], R[b + i], C[b + i], tiles};
-      tiles += ((R[b + i] + 63) / 64) * ((C[b + i] + 63) / 64);
+      const int tp = taps ? taps[b + i] : 1;
+      t.j[i] = TJob{srcs[b + i], dsts[b + i], R[b + i], C[b + i], tp, tiles};
+      tiles += tp * ((R[b + i] + 63) / 64) * ((C[b + i] + 63) / 64);
     }
     if (tiles > 0) hipLaunchKernelGGL(k_transpose_multi, dim3(tiles), dim3(256), 0, stream, t);
   }

@@ -79,6 +79,10 @@ XENT = os.environ.get("GARFIELD_XENT", "1") != "0"   # fused per-worker cross-en
 # "0" keeps hipBLASLt (torch.mm / addmm_).
 GEMM_NT = os.environ.get("GARFIELD_GEMM_NT", "1") != "0"
 GEMM_NT_DGRAD = os.environ.get("GARFIELD_GEMM_NT_DGRAD", "1") != "0"
+# 3x3 / stride-1 / pad-1 convolutions on the halo-staged kernel (conv3x3_nhwc.hip) wherever its tiles
+# fit: the forward through gpu_iconv's automatic choice, the data gradient on the flipped transposed
+# weight (refresh_dgrad_weights). "0" keeps the implicit-GEMM kernel for both.
+CONV3X3 = os.environ.get("GARFIELD_CONV3X3", "1") != "0"
 # split-K weight-gradient sums of every layer deferred to one launch after the backward
 SPLIT_DEFER = os.environ.get("GARFIELD_SPLIT_DEFER", "1") != "0"
 
@@ -439,6 +443,8 @@ class ConvSpec:
         self.wpad = None          # persistent zero-padded [Cout, Kp] weight matrix (im2col + GEMM layers)
         self.wt = None            # [K, Cout] transposed weight matrix of the data-gradient GEMM (refresh_dgrad_weights)
         self.dcol = False         # its data gradient runs dcol = dy · Wmat + col2im (Wmatᵀ refreshed per step)
+        self.wd = None            # flipped transposed weight [Cin, Cout, 3, 3] of the halo-kernel data gradient
+        self.flip = False         # its data gradient runs on the halo kernel (wd refreshed per step)
 
 
 def _gemm_nt_ok(a2: torch.Tensor, b2: torch.Tensor) -> bool:
@@ -550,12 +556,17 @@ def _dcol(dy2: torch.Tensor, w: torch.Tensor, kp: int, spec: "ConvSpec") -> torc
 def refresh_dgrad_weights(specs) -> None:
     """Transposed copies Wᵀ [Cin, Cout] of every 1x1 stride-1 convolution weight, for the
     data-gradient GEMMs of this step: ONE launch for the whole network (the weights change
-    once per step, in the update kernel)."""
-    if not (GEMM_NT and GEMM_NT_DGRAD):
-        return
+    once per step, in the update kernel), and the flipped transposed weights of the 3x3 layers whose
+    data gradient runs on the halo kernel (``spec.flip``), in the same launch."""
     srcs, dsts = [], []
     for spec in specs:
         w = spec.conv.weight
+        if spec.flip:
+            srcs.append(w.detach())
+            dsts.append(_flip_weight_buf(spec))
+            continue
+        if not (GEMM_NT and GEMM_NT_DGRAD):
+            continue
         if not ((spec.gemm or spec.dcol) and w.is_cuda and w.dtype == torch.bfloat16 and w.shape[0] % 64 == 0
                 and (w.numel() // w.shape[0]) % 64 == 0 and _channels_last_weight(w)):
             continue
@@ -568,6 +579,31 @@ def refresh_dgrad_weights(specs) -> None:
         dsts.append(spec.wt)
     if srcs:
         _native.native().gpu_transpose_multi(srcs, dsts)
+
+
+def _flip_weight_buf(spec: "ConvSpec") -> torch.Tensor:
+    """The persistent [Cin, Cout, KH, KW] channels_last buffer of spec's flipped transposed weight."""
+    w = spec.conv.weight
+    shape = (w.shape[1], w.shape[0], w.shape[2], w.shape[3])
+    if spec.wd is None or tuple(spec.wd.shape) != shape or spec.wd.device != w.device or spec.wd.dtype != w.dtype:
+        spec.wd = torch.empty(shape, dtype=w.dtype, device=w.device).contiguous(memory_format=torch.channels_last)
+    return spec.wd
+
+
+def _halo_dgrad_ok(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> bool:
+    """The 3x3 / stride-1 / pad-1 data gradient on the halo-staged kernel (conv3x3_nhwc.hip): a forward
+    convolution of dy with the flipped transposed weight (refreshed once per step)."""
+    return (CONV3X3 and dy.is_cuda and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and spec.kernel == (3, 3) and spec.stride == (1, 1) and spec.padding == (1, 1) and spec.dilation == (1, 1)
+            and _channels_last_weight(w)
+            and _native.native().conv3x3_pick(dy.shape[0], dy.shape[2], dy.shape[3], w.shape[0], w.shape[1]) > 0)
+
+
+def _halo_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", add: torch.Tensor | None) -> torch.Tensor:
+    if not spec.flip or spec.wd is None:       # first use (eager): make the flipped weight now
+        spec.flip = True
+        _native.native().gpu_transpose_multi([w.detach()], [_flip_weight_buf(spec)])
+    return _iconv(dy, spec.wd, (3, 3, 1, 1, 1, 1, 1, 1), (dy.shape[2], dy.shape[3]), add)
 
 
 def _gemm_nt_dgrad(dy2: torch.Tensor, w2: torch.Tensor, add: torch.Tensor | None, spec: "ConvSpec | None" = None):
@@ -669,6 +705,21 @@ def _iwgrad_splits(rows_per_worker: int, tiles: int) -> int:
     return S
 
 
+def _wgrad3x3_splits(rows_per_worker: int, blocks: int) -> int:
+    """Pixel splits of the halo-staged 3x3 weight gradient (one workgroup per (64 co, 64 ci) block,
+    worker and split, all nine taps): enough workgroups to fill the chip twice over (two per CU),
+    each split at least ``_WGRAD3_MINTILES`` 128-pixel tiles."""
+    tiles = -(-rows_per_worker // 128)
+    S = 1
+    while S < 64 and blocks * S < _WGRAD3_WG and tiles // (2 * S) >= _WGRAD3_MINTILES:
+        S *= 2
+    return S
+
+
+_WGRAD3_WG = int(os.environ.get("GARFIELD_WGRAD3X3_WG", "512"))
+_WGRAD3_MINTILES = int(os.environ.get("GARFIELD_WGRAD3X3_MINTILES", "4"))
+
+
 # tuning knobs (profiles/iwgrad_split_sweep_r1.log; 512 since the 1x1 layers joined the
 # implicit kernel: profiles/r2/iwgrad_wg_nt_sweep.log)
 _IWGRAD_WG = int(os.environ.get("GARFIELD_IWGRAD_WG", "512"))
@@ -682,8 +733,12 @@ def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int)
     cout = dy.shape[1]
     rows = dy.shape[0] * dy.shape[2] * dy.shape[3] // G
     C_ = _native.native()
-    S = _iwgrad_splits(rows, (K // 64) * (cout // 64) * G //
-                      C_.iwgrad_taps_per_block(spec.kernel[1], spec.kernel[0], x.shape[1]))
+    if (CONV3X3 and spec.kernel == (3, 3) and spec.stride == (1, 1) and spec.padding == (1, 1)
+            and spec.dilation == (1, 1) and C_.wgrad3x3_fits(x.shape[0], x.shape[2], x.shape[3], x.shape[1], cout, G)):
+        S = _wgrad3x3_splits(rows, (x.shape[1] // 64) * (cout // 64) * G)
+    else:
+        S = _iwgrad_splits(rows, (K // 64) * (cout // 64) * G //
+                          C_.iwgrad_taps_per_block(spec.kernel[1], spec.kernel[0], x.shape[1]))
     out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy.dtype) if S == 1 else None
     if out is not None:
         C_.gpu_iwgrad(x, dy, *_geom(spec), G, out, 1)
@@ -916,7 +971,9 @@ class _GroupedConv(torch.autograd.Function):
             col = None if use_iw else _im2col(a, spec)
             kp = col.shape[1] if col is not None else K
             if need_dx:
-                if ((sh, sw, dh, dw) == (1, 1, 1, 1) and ph <= kh - 1 and pw <= kw - 1
+                if _halo_dgrad_ok(dy, w, spec):
+                    dx = _halo_dgrad(dy, w, spec, _cl(prev) if prev is not None else None)
+                elif ((sh, sw, dh, dw) == (1, 1, 1, 1) and ph <= kh - 1 and pw <= kw - 1
                         and _iconv_ok(dy, _dgrad_weight_shape(w), dy2.shape[0])):
                     dx = _iconv(dy, w, (kh, kw, 1, 1, kh - 1 - ph, kw - 1 - pw, 1, 1), (h, wd),
                                 _cl(prev) if prev is not None else None, transpose_w=True)

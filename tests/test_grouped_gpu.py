@@ -205,6 +205,75 @@ def test_stem_unsupported_sizes(native):
     assert native.stem_supported(32, 32)
 
 
+@pytest.mark.parametrize("N,C,Co,H,pm", [(3, 64, 64, 32, 24), (2, 64, 128, 32, 22), (5, 128, 128, 16, 24),
+                                         (10, 64, 128, 8, 24), (9, 128, 64, 4, 22), (7, 256, 192, 8, 22),
+                                         (33, 512, 512, 4, 22), (6, 64, 64, 16, 0), (13, 192, 256, 8, 0)])
+def test_conv3x3_halo_matches_conv2d(cuda, native, N, C, Co, H, pm):
+    """Halo-staged 3x3 kernel (conv3x3_nhwc.hip) vs an fp32 conv2d of the same bf16 operands: tiles
+    inside one image (32x32, 16x16), tiles of several padded images (8x8, 4x4), a ragged last tile,
+    several 64-channel halo refills, and the fused add."""
+    assert native.conv3x3_pick(N, H, H, C, Co) in (2, 4)
+    x = torch.randn(N, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, 3, 3, device=cuda) / (C * 9) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.float(), w.float(), None, 1, 1)
+    y = torch.full(ref.shape, float("nan"), dtype=torch.bfloat16, device=cuda).contiguous(
+        memory_format=torch.channels_last)
+    native.gpu_iconv(x, w, 3, 3, 1, 1, 1, 1, 1, 1, y, None, pm)
+    assert rel(y.float(), ref) < 1e-2
+    add = torch.randn(ref.shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref2 = ref + add.float()
+    native.gpu_iconv(x, w, 3, 3, 1, 1, 1, 1, 1, 1, add, add, pm)
+    assert rel(add.float(), ref2) < 1e-2
+
+
+@pytest.mark.parametrize("G,B,C,Co,H,S", [(8, 8, 512, 512, 4, 1), (8, 8, 256, 256, 8, 1), (8, 8, 128, 128, 16, 4),
+                                          (8, 8, 64, 64, 32, 16), (3, 5, 64, 128, 8, 2), (2, 7, 128, 64, 4, 3),
+                                          (4, 3, 192, 64, 16, 64)])
+def test_wgrad3x3_halo_matches_conv_weight_grad(cuda, native, G, B, C, Co, H, S):
+    """Halo-staged per-worker 3x3 weight gradient (conv3x3_nhwc.hip) vs fp32 conv2d_weight of each
+    worker's images: ragged last tiles, empty splits (zero slabs), NaN-prefilled outputs, both the
+    fp32 slab and the bf16 exchange-row outputs, repeated launches."""
+    assert native.wgrad3x3_fits(G * B, H, H, C, Co, G)
+    x = torch.randn(G * B, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(G * B, Co, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    K = 9 * C
+    ref = torch.stack([torch.nn.grad.conv2d_weight(x[g * B:(g + 1) * B].float(), (Co, C, 3, 3),
+                                                   dy[g * B:(g + 1) * B].float(), 1, 1).permute(0, 2, 3, 1)
+                       .reshape(Co, K) for g in range(G)])
+    for _ in range(3):
+        part = torch.full((S, G, Co, K), float("nan"), device=cuda)
+        native.gpu_iwgrad(x, dy, 3, 3, 1, 1, 1, 1, 1, 1, G, part, S)
+        assert torch.isfinite(part).all()
+        assert rel(part.sum(0), ref) < 1e-2
+    flat = torch.full((G * (Co * K + 64),), float("nan"), dtype=torch.bfloat16, device=cuda)
+    view = flat.as_strided((G, Co, K), (Co * K + 64, K, 1), 32)
+    native.gpu_iwgrad(x, dy, 3, 3, 1, 1, 1, 1, 1, 1, G, view, 1)
+    assert torch.isfinite(view).all()
+    assert rel(view.float(), ref) < 1e-2
+
+
+def test_conv3x3_halo_refuses_unfit_shapes(native):
+    assert native.conv3x3_pick(4, 2, 2, 256, 256) == 0      # 2x2 images: the halo exceeds the LDS budget
+    assert native.conv3x3_pick(4, 7, 7, 64, 64) == 0        # 7 does not divide a pixel tile
+    assert native.conv3x3_pick(4, 32, 32, 32, 64) == 0      # C % 64
+
+
+def test_transpose_multi_flipped_3x3(cuda, native):
+    """One launch: 2-D transposes and 4-D flipped transposes (the data-gradient weights)."""
+    from garfield_amd.ops.grouped import _dgrad_weight
+    ws = [(torch.randn(co, ci, 3, 3, device=cuda)).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+          for co, ci in ((64, 128), (192, 64), (512, 512))]
+    m = torch.randn(96, 136, device=cuda).to(torch.bfloat16)
+    outs = [torch.empty((w.shape[1], w.shape[0], 3, 3), dtype=torch.bfloat16, device=cuda).contiguous(
+        memory_format=torch.channels_last) for w in ws]
+    mt = torch.empty(136, 96, dtype=torch.bfloat16, device=cuda)
+    native.gpu_transpose_multi([ws[0], m, ws[1], ws[2]], [outs[0], mt, outs[1], outs[2]])
+    for w, o in zip(ws, outs):
+        assert torch.equal(o, _dgrad_weight(w))
+    assert torch.equal(mt, m.t())
+
+
 def test_iconv_dgrad_matches_autograd(cuda, native):
     """The stride-1 data gradient as a convolution with the flipped, transposed weight."""
     from garfield_amd.ops.grouped import _dgrad_weight
