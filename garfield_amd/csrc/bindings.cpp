@@ -581,7 +581,7 @@ void g_col2im(const at::Tensor& dcol, int64_t kh, int64_t kw, int64_t sh, int64_
 // [Cout, KH, KW, C]-ordered weight (a channels_last 4-D weight or its [Cout, K] matrix).
 void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
              int64_t pw, int64_t dh, int64_t dw, const at::Tensor& y, const c10::optional<at::Tensor>& add,
-             int64_t pm, bool transpose_w) {
+             int64_t pm, bool transpose_w, const c10::optional<at::Tensor>& stats, int64_t rg) {
   auto g = conv_geometry(x, kh, kw, sh, sw, ph, pw, dh, dw);
   TORCH_CHECK(g.C % 32 == 0, "gpu_iconv: input channels must be a multiple of 32 (got ", g.C, ")");
   TORCH_CHECK(y.is_cuda() && y.device() == x.device() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 &&
@@ -620,7 +620,27 @@ void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, i
               "gpu_iconv: x and w must be 16-byte aligned, y and add 8-byte aligned");
   TORCH_CHECK(static_cast<int64_t>(g.N) * g.H * g.W * g.C < INT32_MAX && static_cast<int64_t>(g.N) * g.Ho * g.Wo < INT32_MAX,
               "gpu_iconv: tensor too large");
+  float* sp = nullptr;
+  if (stats.has_value()) {
+    const auto& st = *stats;
+    const int pmf = pm == 22 || pm == 24 ? static_cast<int>(pm - 20) : garfield::gpu::conv3x3_pick(g, static_cast<int>(cout));
+    TORCH_CHECK(!transpose_w && !add.has_value() && pmf > 0 && (pm == 0 || pm == 22 || pm == 24),
+                "gpu_iconv: stats need the halo-staged 3x3 kernel (no add, no transpose_w)");
+    const int64_t M = static_cast<int64_t>(g.N) * g.Ho * g.Wo;
+    const int64_t H = 16 * pmf;
+    TORCH_CHECK(rg >= H && M % rg == 0, "gpu_iconv: stats need rg >= ", H, " rows per worker dividing ", M);
+    TORCH_CHECK(st.is_cuda() && st.device() == x.device() && st.scalar_type() == at::kFloat && st.is_contiguous() &&
+                    st.numel() >= (M + H - 1) / H * 6 * cout,
+                "gpu_iconv: stats must be a contiguous fp32 tensor of ", (M + H - 1) / H * 6 * cout, " floats");
+    sp = st.data_ptr<float>();
+  }
   c10::hip::HIPGuard guard(x.device().index());
+  if (sp) {
+    TORCH_CHECK(garfield::gpu::conv3x3_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), nullptr,
+                                            pm == 0 ? 0 : static_cast<int>(pm - 20), stream_of(x.device()), sp, rg),
+                "gpu_iconv: the halo-staged kernel refused the statistics launch");
+    return;
+  }
   // pm 0 (auto): the halo-staged 3x3 kernel whenever it fits (GARFIELD_CONV3X3=0 disables it);
   // pm 22 / 24: force it with 2 / 4 pixel fragments per wave; 1..14: the implicit-GEMM kernel
   static const bool c3 = [] {
@@ -1526,7 +1546,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "(the data gradient of that convolution)",
         py::arg("x"), py::arg("w"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
         py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("y"), py::arg("add") = py::none(), py::arg("pm") = 0,
-        py::arg("transpose_w") = false);
+        py::arg("transpose_w") = false, py::arg("stats") = py::none(), py::arg("rg") = 0);
+  m.def("conv3x3_stats_rows", [](int64_t n, int64_t h, int64_t w, int64_t c, int64_t cout) -> int64_t {
+          return 16 * g_conv3x3_pick(n, h, w, c, cout);
+        }, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("c"), py::arg("cout"),
+        "Rows per statistics tile of the halo-staged 3x3 kernel's BatchNorm-statistics epilogue (0: no fit); "
+        "the stats buffer holds ceil(M / rows) * 6 * Cout floats (E = 1)");
 
   m.def("conv3x3_pick", &g_conv3x3_pick, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("c"), py::arg("cout"),
         "Pixel fragments per wave the halo-staged 3x3 kernel uses for this NHWC shape (0: it does not fit)");

@@ -28,6 +28,7 @@
 #include <cstdlib>
 
 #include "bn_gpu.hpp"
+#include "bn_stats.hpp"
 #include "gar_device.hpp"
 
 namespace garfield {
@@ -50,9 +51,55 @@ struct Halo {
   int lt;    // log2 TRI
 };
 
-template <int PMF, int NU, bool ADD>
+constexpr int EPI_PLAIN = 0, EPI_ADD = 1, EPI_STATS = 2;
+
+// Output of one wave's 16*PMF-pixel x 64-channel tile (pixels mw + 16 r + fr): D[co = 4 fq + e][pixel fr]
+// of every fragment is 4 consecutive channels of one pixel (one 8-byte store); EPI_ADD adds add (the
+// other gradient branch), EPI_STATS writes the wave's per-worker statistics tile (bn_stats.hpp).
+template <int PMF, int EPI>
+__device__ __forceinline__ void conv_epilogue(const f32x4 (&acc)[PMF][4], int mw, int M, int Cout, int co0, uint16_t* y,
+                                              const uint16_t* add, float* __restrict__ stats, int64_t rg) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+  float vs[PMF][4][4];   // the stored (bf16-rounded) values, for the statistics
+#pragma unroll
+  for (int r = 0; r < PMF; ++r) {
+    const int m = mw + r * 16 + fr;
+    const int64_t rowoff = static_cast<int64_t>(m < M ? m : 0) * Cout;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t off = rowoff + co0 + c * 16 + fq * 4;
+      float v[4] = {acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]};
+      if constexpr (EPI == EPI_ADD) {
+        if (m < M) {
+          const uint2 a = *reinterpret_cast<const uint2*>(add + off);
+          v[0] += bf16_to_f(static_cast<uint16_t>(a.x & 0xffffu));
+          v[1] += bf16_to_f(static_cast<uint16_t>(a.x >> 16));
+          v[2] += bf16_to_f(static_cast<uint16_t>(a.y & 0xffffu));
+          v[3] += bf16_to_f(static_cast<uint16_t>(a.y >> 16));
+        }
+      }
+      uint2 o;
+      o.x = static_cast<uint32_t>(f_to_bf16(v[0])) | (static_cast<uint32_t>(f_to_bf16(v[1])) << 16);
+      o.y = static_cast<uint32_t>(f_to_bf16(v[2])) | (static_cast<uint32_t>(f_to_bf16(v[3])) << 16);
+      if (m < M) *reinterpret_cast<uint2*>(y + off) = o;
+      if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vs[r][c][i] = bf16_round(v[i]);
+      }
+    }
+  }
+  if constexpr (EPI == EPI_STATS) {
+    if (mw < M) wave_stats<PMF, 4>(vs, mw, M, rg, Cout, co0, stats);
+  }
+}
+
+// EPI_STATS: the per-worker (rg pixels) statistics of the stored bf16 outputs for the BatchNorm that
+// consumes y, one statistics tile per wave (16 * PMF pixels, bn_stats.hpp), so its forward skips the
+// partial-sum pass over y.
+template <int PMF, int NU, int EPI>
 __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
-                                                 Im2col g, Halo hp, int Cout, uint16_t* y, const uint16_t* add) {
+                                                 Im2col g, Halo hp, int Cout, uint16_t* y, const uint16_t* add,
+                                                 float* __restrict__ stats, int64_t rg) {
   constexpr int NSW = 3;               // weight ring stages
   constexpr int BM = 64 * PMF;         // output pixels per workgroup
   constexpr int XB = NU * 4096;        // halo bytes (NU glds rounds of 4 waves x 8 pixels)
@@ -148,25 +195,29 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
     const char* wb = lds + XB + (s % NSW) * WB;
     const int ti = tap / 3;
     const int toff = ti * hp.SW + (tap - ti * 3);
+    // both 32-channel halves' fragments are read up front: the second half's reads are in flight
+    // while the first half's MFMAs run
+    bf16x8 a[2][4], b[2][PMF];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 a[4], b[PMF];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int row = c * 16 + fr;
-        a[c] = *reinterpret_cast<const bf16x8*>(wb + row * 128 + (((ks * 4 + fq) ^ (row & 7)) * 16));
+        a[ks][c] = *reinterpret_cast<const bf16x8*>(wb + row * 128 + (((ks * 4 + fq) ^ (row & 7)) * 16));
       }
 #pragma unroll
       for (int r = 0; r < PMF; ++r) {
         const int sp = sp0[r] + toff;
-        b[r] = *reinterpret_cast<const bf16x8*>(lds + sp * 128 + (((ks * 4 + fq) ^ (sp & 7)) * 16));
+        b[ks][r] = *reinterpret_cast<const bf16x8*>(lds + sp * 128 + (((ks * 4 + fq) ^ (sp & 7)) * 16));
       }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int r = 0; r < PMF; ++r)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[r], acc[r][c], 0, 0, 0);
-    }
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks][c], b[ks][r], acc[r][c], 0, 0, 0);
     // every wave's reads of this ring slot (and of the halo) retire before the next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (++tap == 9) {
@@ -178,27 +229,136 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
     }
   }
 
+  conv_epilogue<PMF, EPI>(acc, m0 + wave * PMF * 16, M, Cout, co0, y, add, stats, rg);
+}
+
+// 64 input channels (one halo block per tile: ResNet layer1-type layers). The one-shot kernel above
+// stages a 43 KB halo and nine weight taps per 256-pixel tile and computes for only nine k-steps,
+// so every tile pays the full load latency. Here a persistent workgroup keeps its 64-channel output
+// block's whole weight (9 taps x 64 x 64, 72 KB) resident in LDS, double-buffers the halo (2 x 44 KB:
+// the 160 KB of LDS exactly), and walks tiles blockIdx.x, + gridDim.x, ...: the next tile's halo
+// streams in while the nine taps of the current one run.
+constexpr int kNuRes = 11;   // 256-pixel tiles of 32- or 16-wide images: 340 / 324 halo pixels
+
+template <int EPI>
+__global__ __launch_bounds__(256) void k_conv3x3_res(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                     Im2col g, Halo hp, int Cout, int tiles, uint16_t* y,
+                                                     const uint16_t* add, float* __restrict__ stats, int64_t rg) {
+  constexpr int PMF = 4, BM = 256, NU = kNuRes;
+  constexpr int XB = NU * 4096;
+  constexpr int WB = 9 * 64 * 128;
+  __shared__ __attribute__((aligned(16))) char lds[WB + 2 * XB];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int M = g.N * g.H * g.W;
+  const int rows = g.N * g.H;
+  const int co0 = blockIdx.y * 64;
+  const int lc = lane & 7;
+  const uint64_t az = reinterpret_cast<uint64_t>(reinterpret_cast<const uint16_t*>(g_c3_zero) + lc * 8);
+
+  // resident weight: tap t rows co0 .. co0 + 63 at lds + t * 8 KB (18 glds per lane)
+#pragma unroll
+  for (int u = 0; u < 18; ++u) {
+    const int tap = u >> 1;
+    const int row = ((u & 1) * 4 + wave) * 8 + (lane >> 3);
+    __builtin_amdgcn_global_load_lds(w + static_cast<int64_t>(co0 + row) * (9 * 64) + tap * 64 + (lc ^ (row & 7)) * 8,
+                                     (lds_ptr)(lds + tap * 8192 + ((u & 1) * 4 + wave) * 1024), 16, 0, 0);
+  }
+  // halo pixel decomposition of this lane's glds rows (tile-independent)
+  int hrow[NU], hcol[NU], hsw[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int p = (u * 4 + wave) * 8 + (lane >> 3);
+    const int seg = p / hp.SEGP;
+    const int rem = p - seg * hp.SEGP;
+    const int r = rem / hp.SW;
+    const int c = rem - r * hp.SW;
+    const bool ok = u < hp.nu && p < hp.NPIX && c >= 1 && c <= g.W;
+    hrow[u] = ok ? (seg * hp.TRI + r - 1) : -(1 << 28);
+    hcol[u] = (c - 1) * 64 + ((lc ^ (p & 7)) * 8);
+    hsw[u] = r - 1;
+  }
+  auto issue_halo = [&](int tile, int buf) {
+    const int R0 = tile * hp.TR;
+    const int h0 = R0 % g.H;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      if (u < hp.nu) {
+        const int gr = R0 + hrow[u];
+        const int hl = h0 + hsw[u];
+        const bool ok = hrow[u] > -(1 << 27) && gr < rows && hl >= 0 && hl < g.H;
+        const uint64_t a = reinterpret_cast<uint64_t>(x + static_cast<int64_t>(gr) * g.W * 64 + hcol[u]);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? a : az),
+                                         (lds_ptr)(lds + WB + buf * XB + (u * 4 + wave) * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  const int fr = lane & 15, fq = lane >> 4;
+  int sp0[PMF];
 #pragma unroll
   for (int r = 0; r < PMF; ++r) {
-    const int m = m0 + (wave * PMF + r) * 16 + fr;
-    if (m >= M) continue;
-    const int64_t rowoff = static_cast<int64_t>(m) * Cout;
+    const int ml = (wave * PMF + r) * 16 + fr;
+    const int t = ml >> hp.lw, col = ml & (g.W - 1);
+    const int seg = t >> hp.lt;
+    sp0[r] = seg * hp.SEGP + (t & (hp.TRI - 1)) * hp.SW + col;
+  }
+
+  int tile = blockIdx.x;
+  if (tile < tiles) issue_halo(tile, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int it = 0; tile < tiles; ++it, tile += gridDim.x) {
+    const int buf = it & 1;
+    if (tile + static_cast<int>(gridDim.x) < tiles) issue_halo(tile + gridDim.x, buf ^ 1);
+    const char* hb = lds + WB + buf * XB;
+    f32x4 acc[PMF][4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int64_t off = rowoff + co0 + c * 16 + fq * 4;
-      float v[4] = {acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]};
-      if constexpr (ADD) {
-        const uint2 a = *reinterpret_cast<const uint2*>(add + off);
-        v[0] += bf16_to_f(static_cast<uint16_t>(a.x & 0xffffu));
-        v[1] += bf16_to_f(static_cast<uint16_t>(a.x >> 16));
-        v[2] += bf16_to_f(static_cast<uint16_t>(a.y & 0xffffu));
-        v[3] += bf16_to_f(static_cast<uint16_t>(a.y >> 16));
+    for (int r = 0; r < PMF; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // 18 k-steps (tap, 32-channel half); the fragments of step s + 1 are read from LDS while the
+    // MFMAs of step s run (one wave per SIMD: nothing else hides the LDS latency)
+    auto frags = [&](int st, bf16x8 (&a)[4], bf16x8 (&b)[PMF]) {
+      const int tap = st >> 1, ks = st & 1;
+      const char* wb = lds + tap * 8192;
+      const int ti = tap / 3;
+      const int toff = ti * hp.SW + (tap - ti * 3);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int row = c * 16 + fr;
+        a[c] = *reinterpret_cast<const bf16x8*>(wb + row * 128 + (((ks * 4 + fq) ^ (row & 7)) * 16));
       }
-      uint2 o;
-      o.x = static_cast<uint32_t>(f_to_bf16(v[0])) | (static_cast<uint32_t>(f_to_bf16(v[1])) << 16);
-      o.y = static_cast<uint32_t>(f_to_bf16(v[2])) | (static_cast<uint32_t>(f_to_bf16(v[3])) << 16);
-      *reinterpret_cast<uint2*>(y + off) = o;
+#pragma unroll
+      for (int r = 0; r < PMF; ++r) {
+        const int sp = sp0[r] + toff;
+        b[r] = *reinterpret_cast<const bf16x8*>(hb + sp * 128 + (((ks * 4 + fq) ^ (sp & 7)) * 16));
+      }
+    };
+    auto mma = [&](const bf16x8 (&a)[4], const bf16x8 (&b)[PMF]) {
+#pragma unroll
+      for (int r = 0; r < PMF; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[r], acc[r][c], 0, 0, 0);
+    };
+    bf16x8 a0[4], b0[PMF], a1[4], b1[PMF];
+    frags(0, a0, b0);
+#pragma unroll 1
+    for (int st = 0; st < 18; st += 2) {
+      frags(st + 1, a1, b1);
+      mma(a0, b0);
+      if (st + 2 < 18) frags(st + 2, a0, b0);
+      mma(a1, b1);
     }
+    conv_epilogue<PMF, EPI>(acc, tile * BM + wave * PMF * 16, M, Cout, co0, y, add, stats, rg);
+    // the next halo has landed and every wave is done with this one before it is refilled. The
+    // epilogue's 16 output stores (PMF x 4 global_store_dwordx2, issued after the halo loads) may stay
+    // in flight: waiting for them too exposed the store latency once per tile. A ragged last tile
+    // may branch around stores, so it drains everything.
+    if (tile * BM + BM <= M) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 }
 
@@ -223,11 +383,18 @@ bool plan(const Im2col& g, int pmf, int nu_max, Halo& hp) {
 
 template <int PMF, int NU>
 void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, const Halo& hp, int Cout, uint16_t* y,
-            const uint16_t* add, hipStream_t stream) {
+            const uint16_t* add, float* stats, int64_t rg, hipStream_t stream) {
   const int tiles = (g.N * g.H + hp.TR - 1) / hp.TR;
   const dim3 grid(tiles, Cout / 64);
-  if (add) hipLaunchKernelGGL((k_conv3x3<PMF, NU, true>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add);
-  else hipLaunchKernelGGL((k_conv3x3<PMF, NU, false>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add);
+  if (add)
+    hipLaunchKernelGGL((k_conv3x3<PMF, NU, EPI_ADD>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add, stats,
+                       rg);
+  else if (stats)
+    hipLaunchKernelGGL((k_conv3x3<PMF, NU, EPI_STATS>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add, stats,
+                       rg);
+  else
+    hipLaunchKernelGGL((k_conv3x3<PMF, NU, EPI_PLAIN>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add, stats,
+                       rg);
 }
 
 constexpr int kNuBig = 14;    // PMF 4: 14 x 4 KB halo + 3 x 8 KB ring = 80 KB (two workgroups per CU)
@@ -440,16 +607,54 @@ int conv3x3_pick(const Im2col& g, int Cout) {
   return 0;
 }
 
+namespace {
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+// GARFIELD_CONV3X3_RES=0 keeps the one-shot kernel for 64-channel inputs
+bool res_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("GARFIELD_CONV3X3_RES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+}  // namespace
+
 bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
-                  int pmf, hipStream_t stream) {
+                  int pmf, hipStream_t stream, float* stats, int64_t rg) {
   if (pmf <= 0) pmf = conv3x3_pick(g, Cout);
+  if (stats && (add || rg < 16 * pmf)) return false;
   Halo hp;
+  if (pmf == 4 && g.C == 64 && res_enabled() && conv3x3_pick(g, Cout) == 4 && plan(g, 4, kNuRes, hp)) {
+    const int tiles = (g.N * g.H + hp.TR - 1) / hp.TR;
+    int gx = cu_count() / (Cout / 64);
+    gx = gx < 1 ? 1 : (gx > tiles ? tiles : gx);
+    const dim3 grid(gx, Cout / 64);
+    if (add)
+      hipLaunchKernelGGL((k_conv3x3_res<EPI_ADD>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, tiles, y, add, stats,
+                         rg);
+    else if (stats)
+      hipLaunchKernelGGL((k_conv3x3_res<EPI_STATS>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, tiles, y, add,
+                         stats, rg);
+    else
+      hipLaunchKernelGGL((k_conv3x3_res<EPI_PLAIN>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, tiles, y, add,
+                         stats, rg);
+    return true;
+  }
   if (pmf == 4 && conv3x3_pick(g, Cout) && plan(g, 4, kNuBig, hp)) {
-    launch<4, kNuBig>(x, w, g, hp, Cout, y, add, stream);
+    launch<4, kNuBig>(x, w, g, hp, Cout, y, add, stats, rg, stream);
     return true;
   }
   if (pmf == 2 && conv3x3_pick(g, Cout) && plan(g, 2, kNuSmall, hp)) {
-    launch<2, kNuSmall>(x, w, g, hp, Cout, y, add, stream);
+    launch<2, kNuSmall>(x, w, g, hp, Cout, y, add, stats, rg, stream);
     return true;
   }
   return false;

@@ -190,7 +190,10 @@ __global__ __launch_bounds__(256) void k_split_reduce_multi(SplitTable t) {
   const float* p = J.part + static_cast<int64_t>(g) * J.gs + r * J.ipitch + c;
   const int64_t o = static_cast<int64_t>(g) * J.ostride + r * J.opitch + c;
   if (J.vec) {
+    // unrolled: the S slab loads are independent and issue back to back (a rolled loop waits on
+    // each one: at S = 64-128 slabs that latency chain dominated the launch)
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
     for (int s = 0; s < J.S; ++s) {
       const float4 a = *reinterpret_cast<const float4*>(p + static_cast<int64_t>(s) * J.ss);
       acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
@@ -201,6 +204,7 @@ __global__ __launch_bounds__(256) void k_split_reduce_multi(SplitTable t) {
     dev::store_one(J.out, J.odt, o + 3, acc.w);
   } else {
     float acc = 0.f;
+#pragma unroll 8
     for (int s = 0; s < J.S; ++s) acc += p[static_cast<int64_t>(s) * J.ss];
     dev::store_one(J.out, J.odt, o, acc);
   }

@@ -37,6 +37,7 @@
 // the next); its E entries (e.g. the waves that share it) each cover a subset of those rows and
 // carry their own count.
 #include "bn_gpu.hpp"
+#include "bn_stats.hpp"
 #include "gar_device.hpp"
 
 namespace garfield {
@@ -48,78 +49,6 @@ using lds_ptr = __attribute__((address_space(3))) void*;
 __device__ __attribute__((aligned(16))) uint4 g_gemm_zero[8];  // 128 zero bytes: source of padded rows
 
 constexpr int EPI_PLAIN = 0, EPI_ADD = 1, EPI_STATS = 2;
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-
-// Sum over the 16 lanes of a DPP row, returned in every lane of the row.
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_mov<0xB1>(v);    // quad_perm [1, 0, 3, 2]
-  v += dpp_mov<0x4E>(v);    // quad_perm [2, 3, 0, 1]
-  v += dpp_mov<0x141>(v);   // row_half_mirror
-  v += dpp_mov<0x140>(v);   // row_mirror
-  return v;
-}
-
-__device__ __forceinline__ float bf16_round(float x) { return bf16_to_f(f_to_bf16(x)); }
-
-// Statistics of one wave's sub-tile: rows r0 + r*16 + fr (r < WPM), channels chb + c*16 + 4*fq + i.
-// v: the stored (bf16-rounded) values. Writes stats[((t*2 + slot)*2 + {0: Σy, 1: Σ(y-ȳ)²})*N + ch]
-// for t = r0 / (16*WPM); slot 1 holds the rows past the first worker boundary inside the tile.
-template <int WPM, int WPN>
-__device__ __forceinline__ void wave_stats(const float (&v)[WPM][WPN][4], int64_t r0, int64_t M, int64_t rg, int N,
-                                           int chb, float* __restrict__ stats) {
-  constexpr int RW = 16 * WPM;
-  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
-  const int64_t t = r0 / RW;
-  const int64_t end = r0 + RW < M ? r0 + RW : M;
-  const int64_t gb = (r0 / rg + 1) * rg;
-  const int split = static_cast<int>((gb < end ? gb : end) - r0);   // rows of slot 0
-  const int rows = static_cast<int>(end - r0);
-  const int nslot = split < rows ? 2 : 1;
-  for (int slot = 0; slot < nslot; ++slot) {
-    const int lo = slot ? split : 0, hi = slot ? rows : split;
-    const float cnt = static_cast<float>(hi - lo);
-    float s[WPN][4], q[WPN][4];
-#pragma unroll
-    for (int c = 0; c < WPN; ++c)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float a = 0.f;
-#pragma unroll
-        for (int r = 0; r < WPM; ++r) {
-          const int rr = r * 16 + fr;
-          a += (rr >= lo && rr < hi) ? v[r][c][i] : 0.f;
-        }
-        s[c][i] = row16_sum(a);
-      }
-#pragma unroll
-    for (int c = 0; c < WPN; ++c)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float mu = s[c][i] / cnt;
-        float a = 0.f;
-#pragma unroll
-        for (int r = 0; r < WPM; ++r) {
-          const int rr = r * 16 + fr;
-          const float d = v[r][c][i] - mu;
-          a += (rr >= lo && rr < hi) ? d * d : 0.f;
-        }
-        q[c][i] = row16_sum(a);
-      }
-    if (fr == 0) {
-      float* ps = stats + ((t * 2 + slot) * 3) * N + chb + 4 * fq;
-#pragma unroll
-      for (int c = 0; c < WPN; ++c) {
-        *reinterpret_cast<float4*>(ps + c * 16) = make_float4(cnt, cnt, cnt, cnt);
-        *reinterpret_cast<float4*>(ps + N + c * 16) = make_float4(s[c][0], s[c][1], s[c][2], s[c][3]);
-        *reinterpret_cast<float4*>(ps + 2 * N + c * 16) = make_float4(q[c][0], q[c][1], q[c][2], q[c][3]);
-      }
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------------------------
 // K-loop kernel

@@ -83,6 +83,11 @@ GEMM_NT_DGRAD = os.environ.get("GARFIELD_GEMM_NT_DGRAD", "1") != "0"
 # fit: the forward through gpu_iconv's automatic choice, the data gradient on the flipped transposed
 # weight (refresh_dgrad_weights). "0" keeps the implicit-GEMM kernel for both.
 CONV3X3 = os.environ.get("GARFIELD_CONV3X3", "1") != "0"
+# ... with the consuming BatchNorm's statistics from the forward's epilogue (bn_stats.hpp). Off by
+# default: on the ResNet-18 step the epilogue reductions (+25-100 µs per layer-1 launch) and the
+# per-wave tile merge (k_finalize_tiles) cost more than the partial-sum pass they remove
+# (profiles/r3/conv3x3/rocprof_r18_krum_f2_stats.txt).
+CONV3X3_STATS = os.environ.get("GARFIELD_CONV3X3_STATS", "0") != "0"
 # split-K weight-gradient sums of every layer deferred to one launch after the backward
 SPLIT_DEFER = os.environ.get("GARFIELD_SPLIT_DEFER", "1") != "0"
 
@@ -590,6 +595,31 @@ def _flip_weight_buf(spec: "ConvSpec") -> torch.Tensor:
     return spec.wd
 
 
+def _halo_forward_stats(x: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> torch.Tensor | None:
+    """y = conv3x3(x, w) on the halo-staged kernel with the consuming (large-layer) BatchNorm's per-worker
+    statistics written by its epilogue (``spec.bn_next.tile``), so that BatchNorm runs no partial-sum
+    pass; None when the shape or the BatchNorm does not qualify."""
+    st = spec.bn_next
+    if not (CONV3X3 and CONV3X3_STATS and st is not None and x.is_cuda and x.dtype == torch.bfloat16 and spec.kernel == (3, 3)
+            and spec.stride == (1, 1) and spec.padding == (1, 1) and spec.dilation == (1, 1)):
+        return None
+    C_ = _native.native()
+    n, cin, h, wd = x.shape
+    cout = w.shape[0]
+    H = C_.conv3x3_stats_rows(n, h, wd, cin, cout)
+    M = n * h * wd
+    if H <= 0 or M % spec.groups:
+        return None
+    rg = M // spec.groups
+    if rg < H or C_.bn_small(rg):
+        return None
+    stats = torch.empty((-(-M // H) * 6 * cout,), dtype=torch.float32, device=x.device)
+    y = torch.empty((n, cout, h, wd), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    C_.gpu_iconv(x, w, 3, 3, 1, 1, 1, 1, 1, 1, y, None, 0, False, stats, rg)
+    st.tile = (stats, H, 1)
+    return y
+
+
 def _halo_dgrad_ok(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> bool:
     """The 3x3 / stride-1 / pad-1 data gradient on the halo-staged kernel (conv3x3_nhwc.hip): a forward
     convolution of dy with the flipped transposed weight (refreshed once per step)."""
@@ -717,7 +747,7 @@ def _wgrad3x3_splits(rows_per_worker: int, blocks: int) -> int:
 
 
 _WGRAD3_WG = int(os.environ.get("GARFIELD_WGRAD3X3_WG", "512"))
-_WGRAD3_MINTILES = int(os.environ.get("GARFIELD_WGRAD3X3_MINTILES", "4"))
+_WGRAD3_MINTILES = int(os.environ.get("GARFIELD_WGRAD3X3_MINTILES", "1"))   # profiles/r3/conv3x3/bench_conv3x3_shapes.log
 
 
 # tuning knobs (profiles/iwgrad_split_sweep_r1.log; 512 since the 1x1 layers joined the
@@ -917,7 +947,8 @@ class _GroupedConv(torch.autograd.Function):
         if CONV_MODE == "gemm" and _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
             ctx.mode = "iconv"
             ctx.save_for_backward(x, w)
-            return _iconv(x, w, _geom(spec), _out_hw(spec, h, wd))
+            y = _halo_forward_stats(x, w, spec)
+            return y if y is not None else _iconv(x, w, _geom(spec), _out_hw(spec, h, wd))
         if x.is_cuda and CONV_MODE == "gemm" and _channels_last_weight(w):
             ctx.mode = "col"
             col = _im2col(x, spec)

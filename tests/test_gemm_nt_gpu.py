@@ -2,6 +2,7 @@
 against plain fp32 PyTorch references."""
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
@@ -80,6 +81,46 @@ def test_fused_bn_statistics_match_fp32(cuda, native, G, rg, K, N, offset):
         yref = ((yg - mref[:, None]) / torch.sqrt(vref[:, None] + 1e-5) * gam.double() + bet.double()).view(M, N)
         assert rel(out, yref) < 1e-2, cfg
     assert ran >= 1
+
+
+@pytest.mark.parametrize("G,B,C,Co,H,pm,offset", [(8, 4, 64, 64, 32, 24, 0.0), (3, 5, 128, 128, 16, 24, 30.0),
+                                                  (4, 3, 64, 128, 8, 22, 0.0), (5, 7, 128, 64, 4, 22, 10.0),
+                                                  (2, 9, 64, 64, 8, 0, 0.0)])
+def test_conv3x3_bn_statistics_match_fp32(cuda, native, G, B, C, Co, H, pm, offset):
+    """The halo-staged 3x3 kernel's BatchNorm-statistics epilogue: per-worker mean / biased variance of
+    the STORED convolution output merged from per-wave tiles (tiles straddling worker boundaries: 8x8
+    and 4x4 images), |mean| >> std included, and the BatchNorm forward from them."""
+    torch.manual_seed(C + H)
+    x = torch.randn(G * B, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, 3, 3, device=cuda) / (9 * C) ** 0.5).to(torch.bfloat16)
+    x[:, 0] = 1.0
+    w[:, 0] = 0.0
+    w[:, 0, 1, 1] = offset     # the constant channel drives an offset into every output channel
+    w = w.contiguous(memory_format=torch.channels_last)
+    M = G * B * H * H
+    rg = M // G
+    rows = native.conv3x3_stats_rows(G * B, H, H, C, Co) if pm == 0 else 16 * (pm - 20)   # forced tile size
+    assert rows in (32, 64)
+    st = torch.full((-(-M // rows) * 6 * Co,), float("nan"), device=cuda)
+    y = torch.empty((G * B, Co, H, H), dtype=torch.bfloat16, device=cuda).contiguous(memory_format=torch.channels_last)
+    native.gpu_iconv(x, w, 3, 3, 1, 1, 1, 1, 1, 1, y, None, pm, False, st, rg)
+    assert rel(y.float(), F.conv2d(x.float(), w.float(), None, 1, 1)) < 1e-2
+    y2 = y.permute(0, 2, 3, 1).reshape(M, Co)
+    mean = torch.empty((G, Co), device=cuda)
+    istd, sc, sh = torch.empty_like(mean), torch.empty_like(mean), torch.empty_like(mean)
+    gam = torch.rand(Co, device=cuda) + 0.5
+    bet = torch.randn(Co, device=cuda)
+    part = torch.empty(native.bn_part_floats(rg, G, Co), device=cuda)
+    out = torch.empty_like(y2)
+    native.gpu_bn_forward(y2, None, G, gam, bet, 1e-5, 0.1, None, None, part, mean, istd, sc, sh, out, False,
+                          tile_stats=st, tile_m=rows, tile_e=1)
+    yg = y2.double().view(G, rg, Co)
+    mref, vref = yg.mean(1), yg.var(1, unbiased=False)
+    assert (mean.double() - mref).abs().max().item() < 1e-4 * (1 + mref.abs().max().item())
+    var = 1.0 / istd.double() ** 2 - 1e-5
+    assert ((var - vref).abs() / vref.clamp_min(1e-6)).max().item() < 2e-3
+    yref = ((yg - mref[:, None]) / torch.sqrt(vref[:, None] + 1e-5) * gam.double() + bet.double()).view(M, Co)
+    assert rel(out, yref) < 1e-2
 
 
 @pytest.mark.parametrize("S,G,shape", [(4, 8, (64, 72)), (16, 3, (128, 9)), (2, 5, (7,))])

@@ -207,7 +207,10 @@ def test_stem_unsupported_sizes(native):
 
 @pytest.mark.parametrize("N,C,Co,H,pm", [(3, 64, 64, 32, 24), (2, 64, 128, 32, 22), (5, 128, 128, 16, 24),
                                          (10, 64, 128, 8, 24), (9, 128, 64, 4, 22), (7, 256, 192, 8, 22),
-                                         (33, 512, 512, 4, 22), (6, 64, 64, 16, 0), (13, 192, 256, 8, 0)])
+                                         (33, 512, 512, 4, 22), (6, 64, 64, 16, 0), (13, 192, 256, 8, 0),
+                                         # 64 input channels: the weight-resident persistent kernel (more
+                                         # tiles than workgroups: 280 / 272 tiles)
+                                         (70, 64, 64, 32, 24), (4, 64, 128, 32, 24), (17, 64, 64, 16, 0)])
 def test_conv3x3_halo_matches_conv2d(cuda, native, N, C, Co, H, pm):
     """Halo-staged 3x3 kernel (conv3x3_nhwc.hip) vs an fp32 conv2d of the same bf16 operands: tiles
     inside one image (32x32, 16x16), tiles of several padded images (8x8, 4x4), a ragged last tile,
