@@ -108,14 +108,16 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int M = g.N * g.H * g.W;
-  const int rows = g.N * g.H;
+  const int M = g.N * g.Ho * g.Wo;
+  const int st = g.sh;                 // 1, or 2 (a downsampling convolution)
   const int R0 = blockIdx.x * hp.TR;   // first output (global) row of the tile
   const int m0 = blockIdx.x * BM;
   const int co0 = blockIdx.y * 64;
   const int lc = lane & 7;             // this lane's 16-byte slot of a staged row
 
-  // halo sources, computed once: element offset of (pixel, logical chunk) or -1 for a zero pixel
+  // halo sources, computed once: element offset of (pixel, logical chunk) or -1 for a zero pixel.
+  // Staged row r of segment seg is input row st * h0 - 1 + r of the segment's image (h0 its first
+  // output row), staged column c input column c - 1.
   int soff[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
@@ -123,10 +125,11 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
     const int seg = p / hp.SEGP;
     const int rem = p - seg * hp.SEGP;
     const int r = rem / hp.SW, c = rem - (rem / hp.SW) * hp.SW;
-    const int grow = R0 + seg * hp.TRI + r - 1;                    // global input row
-    const int hl = (R0 + seg * hp.TRI) % g.H + r - 1;              // its row inside the image
-    const bool ok = p < hp.NPIX && grow < rows && hl >= 0 && hl < g.H && c >= 1 && c <= g.W;
-    soff[u] = ok ? (grow * g.W + c - 1) * g.C + (lc ^ (p & 7)) * 8 : -1;
+    const int orow = R0 + seg * hp.TRI;                            // the segment's first output row
+    const int n = orow / g.Ho;
+    const int hl = (orow - n * g.Ho) * st - 1 + r;                 // input row inside the image
+    const bool ok = p < hp.NPIX && n < g.N && hl >= 0 && hl < g.H && c >= 1 && c <= g.W;
+    soff[u] = ok ? ((n * g.H + hl) * g.W + c - 1) * g.C + (lc ^ (p & 7)) * 8 : -1;
   }
   const uint64_t az = reinterpret_cast<uint64_t>(reinterpret_cast<const uint16_t*>(g_c3_zero) + lc * 8);
 
@@ -164,9 +167,9 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
 #pragma unroll
   for (int r = 0; r < PMF; ++r) {
     const int ml = (wave * PMF + r) * 16 + fr;
-    const int t = ml / g.W, col = ml - (ml / g.W) * g.W;
+    const int t = ml / g.Wo, col = ml - (ml / g.Wo) * g.Wo;
     const int seg = t / hp.TRI;
-    sp0[r] = seg * hp.SEGP + (t - seg * hp.TRI) * hp.SW + col;
+    sp0[r] = seg * hp.SEGP + (t - seg * hp.TRI) * st * hp.SW + col * st;
   }
 
   f32x4 acc[PMF][4];
@@ -364,27 +367,30 @@ __global__ __launch_bounds__(256) void k_conv3x3_res(const uint16_t* __restrict_
 
 // tile geometry for PMF pixel fragments per wave; false when the shape does not fit
 bool plan(const Im2col& g, int pmf, int nu_max, Halo& hp) {
+  // output tiles of TR whole output rows; stride st stages ((TRI - 1) * st + 3) input rows x
+  // ((Wo - 1) * st + 3) input columns per image segment
+  const int st = g.sh;
   const int BM = 64 * pmf;
-  if (g.W > BM || BM % g.W) return false;
-  hp.TR = BM / g.W;
-  hp.TRI = hp.TR < g.H ? hp.TR : g.H;
-  if ((hp.TR <= g.H && g.H % hp.TR) || (hp.TR > g.H && hp.TR % g.H)) return false;
-  hp.SW = g.W + 2;
-  hp.SEGP = (hp.TRI + 2) * hp.SW;
+  if (g.Wo > BM || BM % g.Wo) return false;
+  hp.TR = BM / g.Wo;
+  hp.TRI = hp.TR < g.Ho ? hp.TR : g.Ho;
+  if ((hp.TR <= g.Ho && g.Ho % hp.TR) || (hp.TR > g.Ho && hp.TR % g.Ho)) return false;
+  hp.SW = (g.Wo - 1) * st + 3;
+  hp.SEGP = ((hp.TRI - 1) * st + 3) * hp.SW;
   hp.NPIX = (hp.TR / hp.TRI) * hp.SEGP;
   hp.nu = (hp.NPIX + 31) / 32;
   hp.lw = 0;
-  while ((1 << hp.lw) < g.W) ++hp.lw;
+  while ((1 << hp.lw) < g.Wo) ++hp.lw;
   hp.lt = 0;
   while ((1 << hp.lt) < hp.TRI) ++hp.lt;
-  if ((1 << hp.lw) != g.W || (1 << hp.lt) != hp.TRI) return false;
+  if ((1 << hp.lw) != g.Wo || (1 << hp.lt) != hp.TRI) return false;
   return hp.nu <= nu_max;
 }
 
 template <int PMF, int NU>
 void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, const Halo& hp, int Cout, uint16_t* y,
             const uint16_t* add, float* stats, int64_t rg, hipStream_t stream) {
-  const int tiles = (g.N * g.H + hp.TR - 1) / hp.TR;
+  const int tiles = (g.N * g.Ho + hp.TR - 1) / hp.TR;
   const dim3 grid(tiles, Cout / 64);
   if (add)
     hipLaunchKernelGGL((k_conv3x3<PMF, NU, EPI_ADD>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add, stats,
@@ -399,6 +405,7 @@ void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, const Halo& h
 
 constexpr int kNuBig = 14;    // PMF 4: 14 x 4 KB halo + 3 x 8 KB ring = 80 KB (two workgroups per CU)
 constexpr int kNuSmall = 10;  // PMF 2: 40 + 24 = 64 KB
+constexpr int kNuS2 = 12;     // stride 2, PMF 1: 48 + 24 = 72 KB (9 x 33, 17 x 17, 4 x 9 x 9 staged pixels)
 
 // ---------------------------------------------------------------------------------------------
 // Per-worker weight gradient of the same convolutions, halo-staged:
@@ -575,7 +582,7 @@ constexpr int kNuWgrad = 10;   // 16 KB dy tile + 40 KB halo: two workgroups per
 
 bool wgrad3x3_fits(const Im2col& g, int Cout, int64_t rg) {
   Halo hp;
-  return conv3x3_pick(g, Cout) != 0 && plan(g, 2, kNuWgrad, hp) && rg > 0 &&
+  return g.sh == 1 && g.sw == 1 && conv3x3_pick(g, Cout) != 0 && plan(g, 2, kNuWgrad, hp) && rg > 0 &&
          rg % (static_cast<int64_t>(g.H) * g.W) == 0;
 }
 
@@ -598,10 +605,21 @@ bool wgrad3x3_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int C
 }
 
 int conv3x3_pick(const Im2col& g, int Cout) {
-  if (g.KH != 3 || g.KW != 3 || g.sh != 1 || g.sw != 1 || g.ph != 1 || g.pw != 1 || g.dh != 1 || g.dw != 1 ||
-      g.C % 64 || Cout % 64 || g.Ho != g.H || g.Wo != g.W)
+  if (g.KH != 3 || g.KW != 3 || g.ph != 1 || g.pw != 1 || g.dh != 1 || g.dw != 1 || g.C % 64 || Cout % 64)
     return 0;
   Halo hp;
+  if (g.sh == 2 && g.sw == 2) {   // downsampling: 64-pixel tiles (the halo is ~4x the output tile)
+    // off by default: 222 vs 176 us per ResNet-18 downsampling layer against the implicit-GEMM
+    // kernel (one 16-pixel fragment per wave re-reads four weight fragments per MFMA pair, and the
+    // stride-2 B rows hit 2-way bank conflicts); GARFIELD_CONV3X3_S2=1 enables it
+    static const bool s2 = [] {
+      const char* e = std::getenv("GARFIELD_CONV3X3_S2");
+      return e && e[0] == '1';
+    }();
+    if (!s2 || g.H != 2 * g.Ho || g.W != 2 * g.Wo) return 0;
+    return plan(g, 1, kNuS2, hp) ? 1 : 0;
+  }
+  if (g.sh != 1 || g.sw != 1 || g.Ho != g.H || g.Wo != g.W) return 0;
   if (plan(g, 4, kNuBig, hp)) return 4;
   if (plan(g, 2, kNuSmall, hp)) return 2;
   return 0;
@@ -649,12 +667,18 @@ bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cou
                          stats, rg);
     return true;
   }
-  if (pmf == 4 && conv3x3_pick(g, Cout) && plan(g, 4, kNuBig, hp)) {
+  const int pick = conv3x3_pick(g, Cout);
+  const bool s1 = g.sh == 1;
+  if (pmf == 4 && pick && s1 && plan(g, 4, kNuBig, hp)) {
     launch<4, kNuBig>(x, w, g, hp, Cout, y, add, stats, rg, stream);
     return true;
   }
-  if (pmf == 2 && conv3x3_pick(g, Cout) && plan(g, 2, kNuSmall, hp)) {
+  if (pmf == 2 && pick && s1 && plan(g, 2, kNuSmall, hp)) {
     launch<2, kNuSmall>(x, w, g, hp, Cout, y, add, stats, rg, stream);
+    return true;
+  }
+  if (pmf == 1 && pick == 1 && plan(g, 1, kNuS2, hp)) {
+    launch<1, kNuS2>(x, w, g, hp, Cout, y, add, stats, rg, stream);
     return true;
   }
   return false;

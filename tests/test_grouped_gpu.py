@@ -256,6 +256,26 @@ def test_wgrad3x3_halo_matches_conv_weight_grad(cuda, native, G, B, C, Co, H, S)
     assert rel(view.float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,C,Co,H", [(3, 64, 128, 32), (5, 128, 256, 16), (9, 256, 512, 8), (7, 64, 64, 16),
+                                      (3, 128, 64, 32)])
+def test_conv3x3_halo_stride2_matches_conv2d(cuda, native, N, C, Co, H):
+    """The downsampling 3x3 / stride-2 / pad-1 convolution on the halo-staged kernel (64-pixel tiles,
+    (2 rows + 1) x (2 W + 1) staged input pixels per segment) vs an fp32 conv2d of the same operands.
+    The variant is opt-in (GARFIELD_CONV3X3_S2=1, read once per process): without it the automatic
+    choice is the implicit-GEMM kernel and the two launches below compare it with itself."""
+    x = torch.randn(N, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, 3, 3, device=cuda) / (C * 9) ** 0.5).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.float(), w.float(), None, 2, 1)
+    y = torch.full(ref.shape, float("nan"), dtype=torch.bfloat16, device=cuda).contiguous(
+        memory_format=torch.channels_last)
+    native.gpu_iconv(x, w, 3, 3, 2, 2, 1, 1, 1, 1, y, None, 0)
+    assert rel(y.float(), ref) < 1e-2
+    y2 = torch.empty_like(y)
+    native.gpu_iconv(x, w, 3, 3, 2, 2, 1, 1, 1, 1, y2, None, 14)    # the implicit-GEMM kernel agrees
+    assert rel(y.float(), y2.float()) < 1e-2
+
+
 def test_conv3x3_halo_refuses_unfit_shapes(native):
     assert native.conv3x3_pick(4, 2, 2, 256, 256) == 0      # 2x2 images: the halo exceeds the LDS budget
     assert native.conv3x3_pick(4, 7, 7, 64, 64) == 0        # 7 does not divide a pixel tile
