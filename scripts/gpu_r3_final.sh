@@ -17,13 +17,15 @@ timeout -k 10 200 python -u bench.py > $O/bench.json.log 2>&1 || { echo "bench f
 tail -1 $O/bench.json.log | cut -c1-160
 CONFIGS="r50_krum_f2 r18_krum_f2" bash scripts/gpu_r3_configs.sh > $O/cfg.log 2>&1 || { echo "cfg failed"; exit 1; }
 cat $O/cfg.log
+[ -n "$LEAN" ] && { cp gpurun_out/cfg/rocprof_r50_krum_f2.txt gpurun_out/cfg/rocprof_r18_krum_f2.txt gpurun_out/cfg/*.json.log $O/; echo done; exit 0; }
 NOPROF=1 CONFIGS="r50_bulyan_f3_k16 r50_trimmed_f2 r50_median_f1 r50_byzps_trimmed" bash scripts/gpu_r3_configs.sh > $O/cfg2.log 2>&1 \
   || { echo "cfg2 failed"; exit 1; }
 cat $O/cfg2.log
 for f in r50_krum_f2 r18_krum_f2 r50_bulyan_f3_k16 r50_trimmed_f2 r50_median_f1 r50_byzps_trimmed; do
   cp gpurun_out/cfg/$f.json.log $O/ 2>/dev/null
 done
-cp gpurun_out/cfg/rocprof_r50_krum_f2.txt gpurun_out/cfg/rocprof_r18_krum_f2.txt $O/
+cp gpurun_out/cfg/rocprof_r50_krum_f2.txt gpurun_out/cfg/rocprof_r18_krum_f2.txt gpurun_out/cfg/*.json.log $O/
+[ -n "$LEAN" ] && { echo done; exit 0; }
 GARFIELD_WGRAD3X3_MINTILES=4 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/ab_r50_mintiles4.json.log 2>&1 && \
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/ab_r50_mintiles1.json.log 2>&1 && \
   GARFIELD_CONV3X3_RES=0 timeout -k 10 300 python -u bench.py --model resnet18 --steps 10 --warmup 3 > $O/ab_r18_res0.json.log 2>&1 && \
