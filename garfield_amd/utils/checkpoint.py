@@ -40,7 +40,7 @@ def save(path: str, model: nn.Module, step: int = 0, momentum: torch.Tensor | No
     state["step"] = int(step)
     if momentum is not None:
         state["momentum"] = momentum.detach().cpu()
-        state["momentum_layout"] = "reference"   # checkpoints without the key hold memory order
+        state["momentum_layout"] = "reference"   # checkpoints without the key hold the same layout
     state["meta"] = dict(meta or {})
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
@@ -97,9 +97,12 @@ def load_engine(path: str, engine) -> dict:
     if "momentum" in state:
         m = state["momentum"].to(engine.mom.device)
         full = torch.zeros(engine.flat.ld, dtype=engine.mom.dtype, device=engine.mom.device)
-        if state.get("momentum_layout") == "reference":
+        # every save_engine writes the reference layout; checkpoints from before the
+        # "momentum_layout" key existed hold it too, so a missing key means "reference".
+        # Only an explicit "memory" value marks a raw memory-order vector.
+        if state.get("momentum_layout", "reference") == "reference":
             engine.flat.from_reference(m, full)    # reference layout -> this engine's memory order
-        else:   # older checkpoints stored the engine's memory order as it was
+        else:
             full[: min(m.numel(), full.numel())] = m.reshape(-1)[: full.numel()].to(full.dtype)
         shard = getattr(engine, "_shard", None)
         if shard is not None and hasattr(shard, "load_momentum"):

@@ -107,3 +107,28 @@ def test_checkpoint_channels_last_to_nchw_roundtrip(tmp_path):
     c.step(b)
     ra, rc = a.flat.reference_vector(), c.flat.reference_vector()
     assert ((ra - rc).norm() / ra.norm()).item() < 1e-5
+
+
+def test_checkpoint_without_layout_key_is_reference_layout(tmp_path):
+    """Checkpoints written before the ``momentum_layout`` key existed already held the momentum
+    in the reference layout: loading one into a channels_last (grouped) engine must reorder it."""
+    from garfield_amd.utils.checkpoint import load_engine, save_engine
+
+    kw = dict(gar="krum", f=1, workers_per_rank=5, lr=0.05, autocast_dtype=None, exchange_dtype=torch.float32)
+    torch.manual_seed(0)
+    a = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(),
+                           EngineConfig(worker_batching=True, **kw))
+    b = synthetic_batches(5, 2, (3, 32, 32), 10, "cpu")
+    a.step(b)
+    p = str(tmp_path / "a.pt")
+    save_engine(p, a)
+    state = torch.load(p, weights_only=True)
+    del state["momentum_layout"]                    # the format of the earlier revision
+    torch.save(state, p)
+    torch.manual_seed(1)
+    c = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(),
+                           EngineConfig(worker_batching=True, **kw))
+    assert not torch.equal(a.flat.to_reference(a.mom), a.mom)   # memory order differs from reference order
+    load_engine(p, c)
+    assert torch.equal(c.mom, a.mom)
+    assert torch.equal(c.flat.to_reference(c.mom), a.flat.to_reference(a.mom))
