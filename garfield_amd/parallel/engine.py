@@ -99,6 +99,10 @@ class EngineConfig:
     # (byzWorker.py:108-143: the attacker's own honest gradient + fw - 1 other honest
     # gradients, here the lowest honest slots), "all" = every honest gradient
     collusion: str = "fw"
+    # CPU rehearsal of the GPU's working-weight exchange: install the shadow (here fp32, the
+    # master's dtype) on the CPU too, so the sharded path's weight all-gathers and compact
+    # all-reduce of the non-shadowed parameters run in the multi-rank gloo tests
+    shadow_cpu: bool = False
 
 
 class _SlotIssuer:
@@ -317,7 +321,9 @@ class RobustDataParallel:
         gradient of that cast. BatchNorm and other parameters stay fp32 views of the
         master buffer."""
         lp = self.cfg.autocast_dtype
-        if not (self.cfg.lp_weights and self.device.type == "cuda" and lp in (torch.bfloat16, torch.float16)):
+        if self.cfg.shadow_cpu and self.device.type == "cpu":
+            lp = torch.float32
+        elif not (self.cfg.lp_weights and self.device.type == "cuda" and lp in (torch.bfloat16, torch.float16)):
             return
         index = {id(p): i for i, p in enumerate(self.flat.params)}
         self._shadow = torch.zeros(self.ld, dtype=lp, device=self.device)
@@ -336,6 +342,14 @@ class RobustDataParallel:
                     self.work_params[i] = replaced[id(p)]
                 mod._parameters[name] = replaced[id(p)]
         self.sync_shadow()
+
+    def shadow_param_ids(self) -> set:
+        """ids of the working parameters that are views of the shadow (the rest are fp32 master
+        views the forward reads directly)."""
+        if self._shadow is None:
+            return set()
+        lo, hi = self._shadow.data_ptr(), self._shadow.data_ptr() + self._shadow.numel() * self._shadow.element_size()
+        return {id(p) for p in self.work_params if lo <= p.data_ptr() < hi}
 
     def sync_shadow(self) -> None:
         """Refresh the low-precision working weights from the fp32 master weights
@@ -407,7 +421,7 @@ class RobustDataParallel:
                 grads.append(g if g is not None else torch.zeros_like(p))
             self._C.gpu_flatten_cast(grads, row)   # fp32 and bf16 sources, one launch
         else:
-            self.flat.grads_flat(row)
+            self.flat.grads_flat(row, self.work_params)
 
     def _grad_vector(self) -> torch.Tensor:
         """Current local gradient as one fp32 vector (memory order)."""
@@ -650,6 +664,8 @@ class RobustDataParallel:
                     buf.mul_(cfg.momentum).add_(g, alpha=1 - cfg.dampening)
                 g = g + cfg.momentum * buf if cfg.nesterov else buf
             p.add_(g, alpha=-cfg.lr)
+            if self._shadow is not None:
+                self._shadow[: self.d].copy_(p)
 
     def _eager_step(self, batches) -> torch.Tensor:
         with self.timer.phase("compute+exchange"):

@@ -17,6 +17,7 @@ communicator (barriers, checkpoints) are ordered after ours by the callers
 """
 from __future__ import annotations
 
+import collections
 import os
 
 import torch
@@ -62,3 +63,87 @@ class DirectRCCL:
 
     def all_reduce_sum(self, t: torch.Tensor, stream) -> None:
         self._C.rccl_all_reduce_sum(self.comm, t, t, stream.cuda_stream)
+
+
+# --------------------------------------------------------------------------- #
+# The same call contract over torch.distributed, for multi-rank CPU rehearsals
+
+
+class GlooDirect:
+    """``DirectRCCL``'s exact call contract carried by torch.distributed (gloo on the CPU), so
+    the multi-rank CPU tests run every ``self._rccl is not None`` branch of the exchange
+    (``sharded.py``) that 8 MI355X will run, and check its layout assumptions:
+
+    * ``all_to_all(send, recv)``: flat, contiguous, equal sizes; chunk r of ``send`` goes to
+      rank r, chunk r of ``recv`` comes from rank r (``ncclAllToAll``);
+    * ``all_gather(send, recv)``: ``recv`` = world x ``send``; when ``send`` overlaps ``recv`` it
+      must be EXACTLY recv's own rank block (RCCL's in-place form), anything else is refused;
+    * ``all_reduce_sum(t)``: in place.
+
+    ``calls`` counts the collectives by kind (the tests assert the per-step pattern)."""
+
+    def __init__(self, world: int, rank: int):
+        self.world = int(world)
+        self.rank = int(rank)
+        self.calls = collections.Counter()
+
+    @staticmethod
+    def _span(t: torch.Tensor):
+        a = t.data_ptr()
+        return a, a + t.numel() * t.element_size()
+
+    def _overlap(self, a: torch.Tensor, b: torch.Tensor) -> bool:
+        (a0, a1), (b0, b1) = self._span(a), self._span(b)
+        return a0 < b1 and b0 < a1
+
+    def all_to_all(self, send: torch.Tensor, recv: torch.Tensor, stream=None) -> None:
+        if not (send.is_contiguous() and recv.is_contiguous() and send.dim() == 1 and recv.dim() == 1):
+            raise ValueError("direct all_to_all: flat contiguous buffers")
+        if send.numel() != recv.numel() or send.dtype != recv.dtype or send.numel() % self.world:
+            raise ValueError("direct all_to_all: equal sizes divisible by the world size")
+        if self._overlap(send, recv):
+            raise ValueError("direct all_to_all: send and recv overlap")
+        self.calls["all_to_all"] += 1
+        dist.all_to_all_single(recv, send)
+
+    def all_gather(self, send: torch.Tensor, recv: torch.Tensor, stream=None) -> None:
+        if not (send.is_contiguous() and recv.is_contiguous()):
+            raise ValueError("direct all_gather: contiguous buffers")
+        if recv.numel() != send.numel() * self.world or send.dtype != recv.dtype:
+            raise ValueError("direct all_gather: output must be world x input")
+        if self._overlap(send, recv):
+            own = recv.data_ptr() + self.rank * send.numel() * send.element_size()
+            if send.data_ptr() != own:
+                raise ValueError("direct all_gather: an input inside the output must be this rank's block")
+            send = send.clone()      # gloo refuses aliasing; RCCL reads its own block in place
+            self.calls["all_gather_inplace"] += 1
+        else:
+            self.calls["all_gather"] += 1
+        dist.all_gather_into_tensor(recv, send)
+
+    def all_reduce_sum(self, t: torch.Tensor, stream=None) -> None:
+        if not t.is_contiguous():
+            raise ValueError("direct all_reduce: contiguous buffer")
+        self.calls["all_reduce"] += 1
+        dist.all_reduce(t)
+
+
+_OVERRIDE = None
+
+
+def set_direct_backend(factory) -> None:
+    """``factory(world, rank)`` -> the direct backend every ``ShardedAggregator`` built next
+    uses at world > 1 (e.g. ``GlooDirect`` in the CPU rehearsals); None restores the default
+    (``DirectRCCL`` on RCCL process groups)."""
+    global _OVERRIDE
+    _OVERRIDE = factory
+
+
+def direct_backend(world: int, rank: int, side: bool):
+    """The direct backend of a sharded exchange: the override when set, else DirectRCCL when the
+    exchange has its own comm stream and several ranks."""
+    if world <= 1:
+        return None
+    if _OVERRIDE is not None:
+        return _OVERRIDE(world, rank)
+    return DirectRCCL.create() if side else None

@@ -56,7 +56,7 @@ from garfield_amd import _native
 from garfield_amd.ops import gar
 from garfield_amd.ops import reference as ref
 from garfield_amd.parallel.comm import gloo_backend
-from garfield_amd.parallel.rccl import DirectRCCL
+from garfield_amd.parallel.rccl import direct_backend
 from garfield_amd.parallel.signals import Handoff
 
 DISTANCE_RULES = {"krum", "brute", "bulyan"}
@@ -141,7 +141,7 @@ class ShardedAggregator:
         self._comm_stream = torch.cuda.Stream(dev) if side else None
         self._handoff = Handoff(dev) if side else None
         # RCCL kernels straight onto the comm stream (rccl.py); None: torch.distributed
-        self._rccl = DirectRCCL.create() if (side and self.world > 1) else None
+        self._rccl = direct_backend(self.world, self.rank, side)
         self._init_fp32_sync()
 
     # ------------------------------------------------------------------ #
@@ -161,7 +161,7 @@ class ShardedAggregator:
         self._np_idx = None
         if e._shadow is None or self.world == 1:
             return
-        lp = {id(p) for p in e.work_params if p.dtype != torch.float32}
+        lp = e.shadow_param_ids()
         idx = []
         for p, wp, off, numel in zip(e.flat.params, e.work_params, e.flat.offsets, e.flat.numels):
             if id(wp) not in lp:
@@ -222,7 +222,7 @@ class ShardedAggregator:
                 if self.world > 1:
                     b.send.copy_(local)
                     if self._rccl is not None:
-                        self._rccl.all_to_all(b.send.view(-1), b.recv.view(-1), s)
+                        self._rccl.all_to_all(b.send.view(-1), b.recv.view(-1), self._comm_stream)
                     else:
                         b.works.append(dist.all_to_all_single(b.recv.view(-1), b.send.view(-1), async_op=True))
                 elif side and loopback_enabled():   # world 1: emulate the transfer (traces / tests)
@@ -300,12 +300,12 @@ class ShardedAggregator:
             return
         buf = e._shadow if e._shadow is not None else e.flat.data
         full, mine = buf[b.lo:b.hi], buf[b.own]
-        if gloo_backend():
-            mine = mine.clone()  # gloo rejects an input aliasing the output
         with self._on_comm():
             if self._rccl is not None:   # in place: this rank's block is its own shard
                 self._rccl.all_gather(mine, full, self._comm_stream)
             else:
+                if gloo_backend():
+                    mine = mine.clone()  # gloo rejects an input aliasing the output
                 self._gathers.append(dist.all_gather_into_tensor(full, mine, async_op=True))
 
     def _finish_gathers(self) -> None:

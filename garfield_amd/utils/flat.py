@@ -166,10 +166,12 @@ class FlatParams:
                 pos += n
         return buf
 
-    def grads_flat(self, out: torch.Tensor) -> torch.Tensor:
-        """Write the current per-parameter gradients (memory order) into ``out[:d]``."""
+    def grads_flat(self, out: torch.Tensor, params=None) -> torch.Tensor:
+        """Write the current per-parameter gradients (memory order) into ``out[:d]``;
+        ``params``: the tensors whose ``.grad`` to read, one per parameter (e.g. an engine's
+        working copies), default the parameters themselves."""
         pos = 0
-        for p, n in zip(self.params, self.numels):
+        for p, n in zip(self.params if params is None else params, self.numels):
             g = p.grad
             if g is None:
                 out[pos:pos + n].zero_()

@@ -7,7 +7,10 @@ MI355X (one process per device), with CPU tensors.
   ``lie`` attacker and a ``reverse`` one; every replica's checksum equal;
 * 8 ranks x 8 grouped ResNet workers (n = 64): shard_pad(8), the three layer
   buckets and the n = 64 Krum selection of the flagship configuration;
-* the exchange leaves in ONE ``all_to_all_single`` per bucket.
+* the exchange leaves in ONE ``all_to_all_single`` per bucket;
+* the same runs through ``GlooDirect`` (``parallel/rccl.py``): the direct-RCCL branch of the
+  exchange that 8 GPUs take, with its call contract checked (flat all-to-all, in-place
+  all-gather of this rank's block), bitwise equal to the torch.distributed branch.
 """
 import os
 import socket
@@ -42,55 +45,84 @@ def _init(rank, world, port):
     return init_distributed(backend="gloo", device="cpu")
 
 
-def _rules_worker(rank, world, port, outdir, shard):
+def _direct(mode):
+    """mode 2: the sharded exchange through GlooDirect, DirectRCCL's call contract (the branch
+    8 GPUs take), with the CPU shadow so the weight all-gathers and the compact all-reduce run."""
+    from garfield_amd.parallel import rccl
+
+    if mode != 2:
+        rccl.set_direct_backend(None)
+        return None
+    made = []
+
+    def factory(world, rank):
+        made.append(rccl.GlooDirect(world, rank))
+        return made[-1]
+
+    rccl.set_direct_backend(factory)
+    return made
+
+
+def _rules_worker(rank, world, port, outdir, mode):
     from garfield_amd.parallel.comm import shutdown
 
     ctx = _init(rank, world, port)
+    made = _direct(mode)
     out = {}
     for rule, f in RULES:
         torch.manual_seed(0)
         eng = RobustDataParallel(build_model("mlp"), F.nll_loss, ctx,
-                                 EngineConfig(gar=rule, f=f, workers_per_rank=2, byzantine=BYZ, shard_gar=shard,
-                                              lr=0.05, collusion="all"))
-        assert (eng._shard is not None) == shard
+                                 EngineConfig(gar=rule, f=f, workers_per_rank=2, byzantine=BYZ, shard_gar=mode > 0,
+                                              lr=0.05, collusion="all", shadow_cpu=mode == 2))
+        assert (eng._shard is not None) == (mode > 0)
+        if mode == 2:
+            assert eng._shard._rccl is made[-1] and eng._shadow is not None
         b = synthetic_batches(2, 8, (1, 28, 28), 10, "cpu", seed=rank)
         for _ in range(2):
             eng.step(b)
-        out[rule] = {"flat": eng.flat_model().clone(), "sum": eng.replica_checksum()}
-    torch.save(out, os.path.join(outdir, f"{int(shard)}r{rank}.pt"))
+        out[rule] = {"flat": eng.flat_model().clone(), "sum": eng.replica_checksum(),
+                     "calls": dict(made[-1].calls) if mode == 2 else {}}
+    torch.save(out, os.path.join(outdir, f"{mode}r{rank}.pt"))
     shutdown(ctx)
 
 
 def test_eight_rank_sharded_equals_redundant_bitwise():
+    """Redundant (0), sharded over torch.distributed (1) and sharded through the direct-RCCL
+    contract (2): bitwise equal for every rule, on every rank."""
     world = 8
     with tempfile.TemporaryDirectory() as d:
-        for shard in (False, True):
-            mp.spawn(_rules_worker, args=(world, free_port(), d, shard), nprocs=world, join=True)
+        for mode in (0, 1, 2):
+            mp.spawn(_rules_worker, args=(world, free_port(), d, mode), nprocs=world, join=True)
         res = {(s, r): torch.load(os.path.join(d, f"{s}r{r}.pt"), weights_only=True)
-               for s in (0, 1) for r in range(world)}
+               for s in (0, 1, 2) for r in range(world)}
         for rule, _ in RULES:
             ref = res[(0, 0)][rule]
-            for s in (0, 1):
+            for s in (0, 1, 2):
                 for r in range(world):
                     got = res[(s, r)][rule]
                     assert got["sum"] == ref["sum"], (rule, s, r)
                     assert torch.equal(got["flat"], ref["flat"]), (rule, s, r)
+            calls = res[(2, 0)][rule]["calls"]
+            assert calls["all_to_all"] == 2 and calls["all_gather_inplace"] == 2, (rule, calls)
+            assert "all_reduce" not in calls, (rule, calls)   # every MLP parameter is a shadow view
 
 
-def _grouped_worker(rank, world, port, outdir, shard, k):
+def _grouped_worker(rank, world, port, outdir, mode, k):
     from garfield_amd.parallel.comm import shutdown
 
     ctx = _init(rank, world, port)
+    made = _direct(mode)
+    shard = mode > 0
     torch.manual_seed(0)
     eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, ctx,
                              EngineConfig(gar="krum", f=2, workers_per_rank=k, byzantine={5: "reverse", 9: "lie"},
                                           shard_gar=shard, worker_batching=True, autocast_dtype=None,
-                                          exchange_dtype=torch.float32, lr=0.01))
+                                          exchange_dtype=torch.float32, lr=0.01, shadow_cpu=mode == 2))
     assert eng._gexec is not None and (eng._shard is not None) == shard
     if shard:
         assert len(eng._shard.buckets) == 3 and eng.ld % (64 * world) == 0
     calls = []
-    if shard:
+    if mode == 1:
         import torch.distributed as dist
 
         orig = dist.all_to_all_single
@@ -102,25 +134,33 @@ def _grouped_worker(rank, world, port, outdir, shard, k):
         dist.all_to_all_single = counting
     b = synthetic_batches(k, 2, (3, 16, 16), 10, "cpu", seed=rank)
     steps = 2
+    per_step = []
     for _ in range(steps):
+        before = dict(made[-1].calls) if mode == 2 else {}
         eng.step(b)
+        if mode == 2:
+            per_step.append({kk: v - before.get(kk, 0) for kk, v in made[-1].calls.items()})
     torch.save({"flat": eng.flat_model().clone(), "sum": eng.replica_checksum(), "a2a": len(calls),
-                "w": eng.last_weights, "n": eng.n}, os.path.join(outdir, f"{int(shard)}r{rank}.pt"))
+                "w": eng.last_weights, "n": eng.n, "per_step": per_step},
+               os.path.join(outdir, f"{mode}r{rank}.pt"))
     shutdown(ctx)
 
 
 @pytest.mark.parametrize("world,k", [(4, 4), (8, 8)])
 def test_grouped_sharded_flagship_path(world, k):
     """ResNet worker batching + sharded bucketed Krum at 4 x 4 (n = 16) and 8 x 8 (n = 64)
-    ranks x workers: replicas identical, sharded == redundant, 3 all_to_all per step."""
+    ranks x workers: replicas identical, sharded == redundant, 3 all_to_all per step; the
+    direct-RCCL contract (mode 2) bitwise equal to the torch.distributed branch, with the exact
+    collective pattern of a GPU step: 3 all_to_all + 1 Gram all-gather + 3 in-place weight
+    all-gathers + 1 all-reduce of the BatchNorm affine parameters."""
     with tempfile.TemporaryDirectory() as d:
-        for shard in (False, True):
-            mp.spawn(_grouped_worker, args=(world, free_port(), d, shard, k), nprocs=world, join=True)
+        for mode in (0, 1, 2):
+            mp.spawn(_grouped_worker, args=(world, free_port(), d, mode, k), nprocs=world, join=True)
         res = {(s, r): torch.load(os.path.join(d, f"{s}r{r}.pt"), weights_only=True)
-               for s in (0, 1) for r in range(world)}
+               for s in (0, 1, 2) for r in range(world)}
         ref = res[(0, 0)]
         assert ref["n"] == world * k
-        for s in (0, 1):
+        for s in (0, 1, 2):
             for r in range(world):
                 got = res[(s, r)]
                 assert got["sum"] == res[(s, 0)]["sum"], (s, r)
@@ -129,6 +169,10 @@ def test_grouped_sharded_flagship_path(world, k):
         assert all(torch.equal(res[(1, r)]["w"], res[(1, 0)]["w"]) for r in range(world))   # one Krum selection
         rel = ((res[(1, 0)]["flat"] - ref["flat"]).norm() / ref["flat"].norm()).item()
         assert rel < 1e-5, rel
+        assert torch.equal(res[(2, 0)]["flat"], res[(1, 0)]["flat"])     # direct contract == dist branch
+        for r in range(world):
+            for calls in res[(2, r)]["per_step"]:
+                assert calls == {"all_to_all": 3, "all_gather": 1, "all_gather_inplace": 3, "all_reduce": 1}, calls
 
 
 def _byzps_worker(rank, world, port, outdir, num_ps):
