@@ -168,7 +168,7 @@ def main():
     d = num_parameters(model)
     fp32 = a.precision == "fp32"
     if fp32:
-        a.exchange_dtype, a.no_lp_weights = "fp32", True   # worker batching: the grouped-channel executor
+        a.exchange_dtype, a.no_lp_weights = "fp32", True   # worker batching: the grouped NHWC executor in fp32
     xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
     amp = {} if not fp32 else {"autocast_dtype": None}
     cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
@@ -196,7 +196,7 @@ def main():
         if hasattr(eng, "grouped_inputs"):   # write each batch straight into the step's input buffers
             feed.attach(eng.grouped_inputs(a.batch, shape))
         batches = feed.next
-        if fp32:   # the kernel writes bf16 rows; the fp32 path takes fp32 inputs
+        if fp32 and feed.out.dtype != torch.float32:   # not attached: the fp32 step takes fp32 inputs
             batches = lambda: [(x.float(), y) for x, y in feed.next()]  # noqa: E731
     else:
         batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,

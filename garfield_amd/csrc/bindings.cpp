@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "bn_gpu.hpp"
+#include "conv_f32.hpp"
 #include "gar_common.hpp"
 #include "gar_cpu.hpp"
 #include "gar_gpu.hpp"
@@ -315,6 +316,19 @@ void check_bf16_rows(const at::Tensor& t, const at::Device& dev, const char* wha
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "garfield: ", what, " must be 16-byte aligned");
 }
 
+// Activation rows of the grouped layers: bf16, or fp32 for the reference-precision step; every
+// tensor of one call must share x's dtype. Returns the dtype code.
+int check_act_rows(const at::Tensor& t, const at::Device& dev, const char* what, int want = -1) {
+  TORCH_CHECK(t.is_cuda() && t.device() == dev &&
+                  (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat),
+              "garfield: ", what, " must be a bf16 or fp32 tensor on ", dev);
+  TORCH_CHECK(t.dim() == 2 && t.is_contiguous(), "garfield: ", what, " must be a contiguous [rows, C] matrix");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "garfield: ", what, " must be 16-byte aligned");
+  const int dt = t.scalar_type() == at::kFloat ? garfield::kF32 : garfield::kBF16;
+  TORCH_CHECK(want < 0 || dt == want, "garfield: ", what, " must have x's dtype");
+  return dt;
+}
+
 const uint16_t* u16(const at::Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
 uint16_t* u16_mut(const at::Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 
@@ -355,8 +369,8 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
                   bool relu, const c10::optional<at::Tensor>& mask, bool defer_running,
                   const c10::optional<at::Tensor>& tile_stats, int64_t tile_m, int64_t tile_e) {
   const auto dev = x.device();
-  check_bf16_rows(x, dev, "x");
-  check_bf16_rows(y, dev, "y");
+  const int dt = check_act_rows(x, dev, "x");
+  check_act_rows(y, dev, "y", dt);
   TORCH_CHECK(y.sizes() == x.sizes(), "garfield bn: y must have x's shape");
   uint8_t* mp = nullptr;
   if (mask.has_value() && mask->defined()) {
@@ -366,11 +380,11 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
   }
   const int64_t rg = bn_groups(x, groups);
   const int64_t C = x.size(1);
-  const uint16_t* r = nullptr;
+  const void* r = nullptr;
   if (res.has_value() && res->defined()) {
-    check_bf16_rows(*res, dev, "res");
+    check_act_rows(*res, dev, "res", dt);
     TORCH_CHECK(res->sizes() == x.sizes(), "garfield bn: the residual must have x's shape");
-    r = u16(*res);
+    r = res->data_ptr();
   }
   const int G = static_cast<int>(groups);
   float* pw = ws_vec(part, garfield::gpu::bn_part_floats(rg, G, static_cast<int>(C)), dev, "part");
@@ -391,9 +405,9 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
     ts = ws_vec(*tile_stats, tiles * tile_e * 6 * C, dev, "tile_stats");
   }
   c10::hip::HIPGuard guard(dev.index());
-  garfield::gpu::bn_forward(u16(x), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
-                            static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, u16_mut(y), relu, mp,
-                            defer_running, stream_of(dev), ts, tile_m, static_cast<int>(tile_e));
+  garfield::gpu::bn_forward(x.data_ptr(), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
+                            static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, y.data_ptr(), relu, mp,
+                            defer_running, stream_of(dev), ts, tile_m, static_cast<int>(tile_e), dt);
 }
 
 int xent_dtype(const at::Tensor& t, const char* what) {
@@ -474,29 +488,29 @@ void g_bn_backward(const at::Tensor& x, const at::Tensor& dy, const c10::optiona
                    const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& grow, int64_t row_stride,
                    int64_t off_gamma, int64_t off_beta) {
   const auto dev = x.device();
-  check_bf16_rows(x, dev, "x");
-  check_bf16_rows(dy, dev, "dy");
-  check_bf16_rows(dx, dev, "dx");
+  const int dt = check_act_rows(x, dev, "x");
+  check_act_rows(dy, dev, "dy", dt);
+  check_act_rows(dx, dev, "dx", dt);
   TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes(), "garfield bn: dy/dx must have x's shape");
   const int64_t rg = bn_groups(x, groups);
   const int64_t C = x.size(1);
-  const uint16_t* yp = nullptr;
+  const void* yp = nullptr;
   const uint8_t* mp = nullptr;
   if (y.has_value() && y->defined()) {
     if (y->scalar_type() == at::kByte) {   // the forward's ReLU bit mask
       check_relu_mask(*y, x);
       mp = static_cast<const uint8_t*>(y->data_ptr());
     } else {
-      check_bf16_rows(*y, dev, "y");
+      check_act_rows(*y, dev, "y", dt);
       TORCH_CHECK(y->sizes() == x.sizes(), "garfield bn: y must have x's shape");
-      yp = u16(*y);
+      yp = y->data_ptr();
     }
   }
-  uint16_t* dr = nullptr;
+  void* dr = nullptr;
   if (dres.has_value() && dres->defined()) {
-    check_bf16_rows(*dres, dev, "dres");
+    check_act_rows(*dres, dev, "dres", dt);
     TORCH_CHECK(dres->sizes() == x.sizes(), "garfield bn: dres must have x's shape");
-    dr = u16_mut(*dres);
+    dr = dres->data_ptr();
   }
   const int G = static_cast<int>(groups);
   float* pw = ws_vec(part, garfield::gpu::bn_part_floats(rg, G, static_cast<int>(C)), dev, "part");
@@ -518,14 +532,15 @@ void g_bn_backward(const at::Tensor& x, const at::Tensor& dy, const c10::optiona
     gp = grow->data_ptr();
   }
   c10::hip::HIPGuard guard(dev.index());
-  garfield::gpu::bn_backward(u16(x), u16(dy), yp, mp, rg, G, static_cast<int>(C), g, m, is, pw, cw, u16_mut(dx), dr,
-                             gp, gdt, row_stride, off_gamma, off_beta, stream_of(dev));
+  garfield::gpu::bn_backward(x.data_ptr(), dy.data_ptr(), yp, mp, rg, G, static_cast<int>(C), g, m, is, pw, cw,
+                             dx.data_ptr(), dr, gp, gdt, row_stride, off_gamma, off_beta, stream_of(dev), dt);
 }
 
 garfield::gpu::Im2col conv_geometry(const at::Tensor& x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
-                                    int64_t pw, int64_t dh, int64_t dw) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4,
-              "garfield im2col: x must be a 4-D bf16 device tensor");
+                                    int64_t pw, int64_t dh, int64_t dw, bool allow_f32 = false) {
+  TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kBFloat16 || (allow_f32 && x.scalar_type() == at::kFloat)) &&
+                  x.dim() == 4,
+              "garfield im2col: x must be a 4-D bf16", allow_f32 ? " or fp32" : "", " device tensor");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "garfield im2col: x must be channels_last");
   TORCH_CHECK(kh >= 1 && kw >= 1 && sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0 && dh >= 1 && dw >= 1,
               "garfield im2col: invalid kernel geometry");
@@ -932,10 +947,11 @@ void g_augment_gather(const at::Tensor& src, const c10::optional<at::Tensor>& id
     lp = labels->data_ptr<int64_t>();
     lo = labels_out->data_ptr<int64_t>();
   }
-  TORCH_CHECK(out.device() == dev && out.scalar_type() == at::kBFloat16 && out.dim() == 4 &&
+  TORCH_CHECK(out.device() == dev && (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat) &&
+                  out.dim() == 4 &&
                   out.size(1) == C && out.size(2) == H && out.size(3) == W &&
                   out.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "gpu_augment_gather: out must be a channels_last bf16 [len(idx), C, H, W] tensor");
+              "gpu_augment_gather: out must be a channels_last bf16 or fp32 [len(idx), C, H, W] tensor");
   TORCH_CHECK(static_cast<int64_t>(mean.size()) == C && static_cast<int64_t>(std.size()) == C,
               "gpu_augment_gather: one mean / std per channel");
   TORCH_CHECK(pad >= 0 && pad < H && pad < W, "gpu_augment_gather: invalid padding");
@@ -948,13 +964,160 @@ void g_augment_gather(const at::Tensor& src, const c10::optional<at::Tensor>& id
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::augment_gather(src.data_ptr<uint8_t>(), src.size(0), ip, lp, lo, R, static_cast<int>(H),
                                 static_cast<int>(W), static_cast<int>(C), static_cast<int>(pad), flip,
-                                static_cast<uint64_t>(seed), static_cast<uint64_t>(step), n, u16_mut(out),
-                                stream_of(dev));
+                                static_cast<uint64_t>(seed), static_cast<uint64_t>(step), n, out.data_ptr(),
+                                stream_of(dev), dtype_code(out));
 }
 
 // Per-worker implicit weight gradient. out: fp32 [splits, groups, Cout, K] (contiguous partial
 // slabs) or, with splits == 1, a bf16 [groups, Cout, K] view whose rows are contiguous (any group
 // stride: the exchange rows).
+// ------------------------------------------- fp32 (reference-precision) step ----
+
+void check_f32_cl(const at::Tensor& t, const at::Device& dev, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.device() == dev && t.scalar_type() == at::kFloat && t.dim() == 4 &&
+                  t.is_contiguous(at::MemoryFormat::ChannelsLast) && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              "garfield conv_f32: ", what, " must be a 16-byte aligned channels_last fp32 4-D tensor on ", dev);
+  TORCH_CHECK(t.numel() < INT32_MAX, "garfield conv_f32: ", what, " is too large");
+}
+
+int64_t conv_out(int64_t in, int64_t k, int64_t s, int64_t p, int64_t d) { return (in + 2 * p - d * (k - 1) - 1) / s + 1; }
+
+// out = conv(src) (forward: w [Co][kh][kw][Cs] split) or the data gradient of a convolution with this
+// geometry (dgrad: src = dy, out = dx, w = Wt [Co = Cin][kh][kw][Cs = Cout] split); (+ add)
+void g_conv_f32(const at::Tensor& src, const at::Tensor& w3, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
+                int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool dgrad, const at::Tensor& out,
+                const c10::optional<at::Tensor>& add, int64_t pm) {
+  const auto dev = src.device();
+  check_f32_cl(src, dev, "src");
+  check_f32_cl(out, dev, "out");
+  TORCH_CHECK(kh >= 1 && kw >= 1 && sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0 && dh >= 1 && dw >= 1,
+              "gpu_conv_f32: invalid kernel geometry");
+  garfield::gpu::ConvF32Geo g{};
+  g.N = static_cast<int>(src.size(0));
+  g.Cs = static_cast<int>(src.size(1));
+  g.Hs = static_cast<int>(src.size(2));
+  g.Ws = static_cast<int>(src.size(3));
+  g.Co = static_cast<int>(out.size(1));
+  g.Ho = static_cast<int>(out.size(2));
+  g.Wo = static_cast<int>(out.size(3));
+  g.KH = static_cast<int>(kh); g.KW = static_cast<int>(kw);
+  g.sh = static_cast<int>(sh); g.sw = static_cast<int>(sw);
+  g.ph = static_cast<int>(ph); g.pw = static_cast<int>(pw);
+  g.dh = static_cast<int>(dh); g.dw = static_cast<int>(dw);
+  TORCH_CHECK(out.size(0) == g.N, "gpu_conv_f32: src and out must hold the same images");
+  if (dgrad) {
+    TORCH_CHECK(conv_out(g.Ho, kh, sh, ph, dh) == g.Hs && conv_out(g.Wo, kw, sw, pw, dw) == g.Ws,
+                "gpu_conv_f32: dy [", g.Hs, "x", g.Ws, "] is not the forward output of dx [", g.Ho, "x", g.Wo, "]");
+  } else {
+    TORCH_CHECK(conv_out(g.Hs, kh, sh, ph, dh) == g.Ho && conv_out(g.Ws, kw, sw, pw, dw) == g.Wo,
+                "gpu_conv_f32: out [", g.Ho, "x", g.Wo, "] is not the forward output of src [", g.Hs, "x", g.Ws, "]");
+  }
+  TORCH_CHECK(garfield::gpu::conv_f32_supported(g), "gpu_conv_f32: needs Co % 64 == 0 (got ", g.Co, ")");
+  TORCH_CHECK(g.Cs % 32 == 0 || !dgrad, "gpu_conv_f32: a data gradient needs Cs % 32 == 0");
+  // Cs % 32 != 0 (gathered k): weight rows of the flattened (tap, channel) index padded to a multiple of 32
+  const int64_t kr = kh * kw * g.Cs;
+  const int64_t wn = static_cast<int64_t>(g.Co) * (g.Cs % 32 ? (kr + 31) / 32 * 32 : kr);
+  TORCH_CHECK(w3.device() == dev && w3.scalar_type() == at::kBFloat16 && w3.is_contiguous() && w3.numel() == 3 * wn &&
+                  reinterpret_cast<uintptr_t>(w3.data_ptr()) % 16 == 0,
+              "gpu_conv_f32: w must be the contiguous bf16 pieces [3, Co, K] (", 3 * wn, " elements)");
+  const float* ap = nullptr;
+  if (add.has_value() && add->defined()) {
+    check_f32_cl(*add, dev, "add");
+    TORCH_CHECK(add->sizes() == out.sizes(), "gpu_conv_f32: add must have out's shape");
+    ap = add->data_ptr<float>();
+  }
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::conv_f32(src.data_ptr<float>(), reinterpret_cast<const uint16_t*>(w3.data_ptr()), g, dgrad,
+                          out.data_ptr<float>(), ap, static_cast<int>(pm), stream_of(dev));
+}
+
+// per-worker weight gradients of a convolution (forward geometry from x, dy): out fp32
+// [splits, groups, Cout, K] contiguous, or (splits == 1) a [groups, Cout, K] view with contiguous rows
+void g_wgrad_f32(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
+                 int64_t pw, int64_t dh, int64_t dw, int64_t groups, const at::Tensor& out, int64_t splits) {
+  const auto dev = x.device();
+  check_f32_cl(x, dev, "x");
+  check_f32_cl(dy, dev, "dy");
+  garfield::gpu::ConvF32Geo g{};
+  g.N = static_cast<int>(x.size(0));
+  g.Cs = static_cast<int>(x.size(1));
+  g.Hs = static_cast<int>(x.size(2));
+  g.Ws = static_cast<int>(x.size(3));
+  g.Co = static_cast<int>(dy.size(1));
+  g.Ho = static_cast<int>(dy.size(2));
+  g.Wo = static_cast<int>(dy.size(3));
+  g.KH = static_cast<int>(kh); g.KW = static_cast<int>(kw);
+  g.sh = static_cast<int>(sh); g.sw = static_cast<int>(sw);
+  g.ph = static_cast<int>(ph); g.pw = static_cast<int>(pw);
+  g.dh = static_cast<int>(dh); g.dw = static_cast<int>(dw);
+  TORCH_CHECK(dy.size(0) == g.N && conv_out(g.Hs, kh, sh, ph, dh) == g.Ho && conv_out(g.Ws, kw, sw, pw, dw) == g.Wo,
+              "gpu_wgrad_f32: dy is not the forward output of x");
+  TORCH_CHECK(garfield::gpu::wgrad_f32_supported(g), "gpu_wgrad_f32: needs Cout % 64 == 0");
+  const int64_t M = static_cast<int64_t>(g.N) * g.Ho * g.Wo;
+  TORCH_CHECK(groups >= 1 && M % groups == 0, "gpu_wgrad_f32: ", M, " output pixels do not split into ", groups,
+              " workers");
+  TORCH_CHECK(splits >= 1 && splits <= 64, "gpu_wgrad_f32: splits must be in [1, 64]");
+  const int64_t K = static_cast<int64_t>(kh) * kw * g.Cs, cout = g.Co;
+  TORCH_CHECK(out.device() == dev && out.scalar_type() == at::kFloat, "gpu_wgrad_f32: out must be fp32 on x's device");
+  int64_t ss = 0, gs = 0;
+  if (out.dim() == 4) {
+    TORCH_CHECK(out.is_contiguous() && out.size(0) == splits && out.size(1) == groups && out.size(2) == cout &&
+                    out.size(3) == K,
+                "gpu_wgrad_f32: a 4-D out must be contiguous [splits, groups, Cout, K]");
+    ss = groups * cout * K;
+    gs = cout * K;
+  } else {
+    TORCH_CHECK(splits == 1 && out.dim() == 3 && out.size(0) == groups && out.size(1) == cout && out.size(2) == K &&
+                    out.stride(2) == 1 && out.stride(1) == K && out.stride(0) >= cout * K,
+                "gpu_wgrad_f32: a 3-D out must be a [groups, Cout, K] view with contiguous rows (splits == 1)");
+    gs = out.stride(0);
+  }
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::wgrad_f32(x.data_ptr<float>(), dy.data_ptr<float>(), g, static_cast<int>(groups), M / groups,
+                           static_cast<int>(splits), out.data_ptr<float>(), ss, gs, stream_of(dev));
+}
+
+// jobs: (w fp32 [R, T, C] memory order, pieces bf16 [3, R, ld], tpieces [3, C, T, R] or None, R, T, C, ld)
+void g_wsplit_multi(const std::vector<py::tuple>& jobs) {
+  if (jobs.empty()) return;
+  std::vector<garfield::gpu::WSplitJob> js;
+  js.reserve(jobs.size());
+  c10::Device dev = jobs[0][0].cast<at::Tensor>().device();
+  for (const auto& t : jobs) {
+    TORCH_CHECK(t.size() == 7, "gpu_wsplit_multi: each job is (w, pieces, tpieces, R, T, C, ld)");
+    auto w = t[0].cast<at::Tensor>(), pc = t[1].cast<at::Tensor>();
+    const int64_t R = t[3].cast<int64_t>(), T = t[4].cast<int64_t>(), C = t[5].cast<int64_t>(), ld = t[6].cast<int64_t>();
+    TORCH_CHECK(w.is_cuda() && w.device() == dev && w.scalar_type() == at::kFloat && w.numel() == R * T * C,
+                "gpu_wsplit_multi: w must be an fp32 tensor of R*T*C elements on one device");
+    TORCH_CHECK(w.is_contiguous() || w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_wsplit_multi: w must be dense (memory order [R][T][C])");
+    const int64_t rows = ld > 0 ? ld : T * C;
+    TORCH_CHECK(ld == 0 || ld >= T * C, "gpu_wsplit_multi: ld < T*C");
+    TORCH_CHECK(pc.device() == dev && pc.scalar_type() == at::kBFloat16 && pc.is_contiguous() &&
+                    pc.numel() == 3 * R * rows,
+                "gpu_wsplit_multi: pieces must be a contiguous bf16 [3, R, ld] tensor");
+    uint16_t* tp = nullptr;
+    if (!t[2].is_none()) {
+      auto a = t[2].cast<at::Tensor>();
+      TORCH_CHECK(a.device() == dev && a.scalar_type() == at::kBFloat16 && a.is_contiguous() &&
+                      a.numel() == 3 * R * T * C,
+                  "gpu_wsplit_multi: tpieces must be a contiguous bf16 [3, C, T, R] tensor");
+      tp = reinterpret_cast<uint16_t*>(a.data_ptr());
+    }
+    js.push_back(garfield::gpu::WSplitJob{w.data_ptr<float>(), reinterpret_cast<uint16_t*>(pc.data_ptr()), tp,
+                                           static_cast<int>(R), static_cast<int>(T), static_cast<int>(C),
+                                           static_cast<int>(ld)});
+  }
+  c10::hip::HIPGuard guard(dev.index());
+  garfield::gpu::wsplit_multi(js.data(), static_cast<int>(js.size()), stream_of(dev));
+}
+
+void check_f32_mat(const at::Tensor& t, const at::Device& dev, int64_t r, int64_t c, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.device() == dev && t.scalar_type() == at::kFloat && t.is_contiguous() &&
+                  t.numel() == r * c,
+              "garfield linear_f32: ", what, " must be a contiguous fp32 [", r, ", ", c, "] tensor on ", dev);
+}
+
 void g_iwgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
               int64_t pw, int64_t dh, int64_t dw, int64_t groups, const at::Tensor& out, int64_t splits) {
   auto g = conv_geometry(x, kh, kw, sh, sw, ph, pw, dh, dw);
@@ -992,12 +1155,8 @@ void g_iwgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw,
     gs = out.stride(0);
   }
   c10::hip::HIPGuard guard(x.device().index());
-  // the halo-staged 3x3 kernel whenever it fits (GARFIELD_WGRAD3X3=0 keeps the implicit kernel)
-  static const bool h3 = [] {
-    const char* e = std::getenv("GARFIELD_WGRAD3X3");
-    return !(e && e[0] == '0');
-  }();
-  if (h3 && garfield::gpu::wgrad3x3_nhwc(u16(x), u16(dy), g, static_cast<int>(cout), static_cast<int>(groups),
+  // the halo-staged 3x3 kernel whenever it fits
+  if (garfield::gpu::wgrad3x3_nhwc(u16(x), u16(dy), g, static_cast<int>(cout), static_cast<int>(groups),
                                          M / groups, static_cast<int>(splits), out.data_ptr(), bf16, ss, gs,
                                          stream_of(x.device())))
     return;
@@ -1014,13 +1173,13 @@ bool g_wgrad3x3_fits(int64_t n, int64_t h, int64_t w, int64_t c, int64_t cout, i
 
 garfield::gpu::Im2col pool_geometry(const at::Tensor& x, const at::Tensor& y, const at::Tensor& idx, int64_t k,
                                     int64_t s, int64_t p) {
-  auto g = conv_geometry(x, k, k, s, s, p, p, 1, 1);
+  auto g = conv_geometry(x, k, k, s, s, p, p, 1, 1, true);
   TORCH_CHECK(g.C % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
               "garfield maxpool: channels must be a multiple of 8 and x 16-byte aligned");
-  TORCH_CHECK(y.device() == x.device() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == g.N &&
+  TORCH_CHECK(y.device() == x.device() && y.scalar_type() == x.scalar_type() && y.dim() == 4 && y.size(0) == g.N &&
                   y.size(1) == g.C && y.size(2) == g.Ho && y.size(3) == g.Wo &&
                   y.is_contiguous(at::MemoryFormat::ChannelsLast) && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
-              "garfield maxpool: y must be a channels_last bf16 [", g.N, ", ", g.C, ", ", g.Ho, ", ", g.Wo, "] tensor");
+              "garfield maxpool: y must be a channels_last [", g.N, ", ", g.C, ", ", g.Ho, ", ", g.Wo, "] tensor of x's dtype");
   TORCH_CHECK(idx.device() == x.device() && idx.scalar_type() == at::kByte && idx.numel() == y.numel() &&
                   idx.is_contiguous() && reinterpret_cast<uintptr_t>(idx.data_ptr()) % 8 == 0 && k * k <= 256,
               "garfield maxpool: idx must be a contiguous uint8 tensor of y's element count");
@@ -1030,14 +1189,15 @@ garfield::gpu::Im2col pool_geometry(const at::Tensor& x, const at::Tensor& y, co
 void g_maxpool_fwd(const at::Tensor& x, int64_t k, int64_t s, int64_t p, const at::Tensor& y, const at::Tensor& idx) {
   auto g = pool_geometry(x, y, idx, k, s, p);
   c10::hip::HIPGuard guard(x.device().index());
-  garfield::gpu::maxpool_fwd_nhwc(u16(x), g, u16_mut(y), static_cast<uint8_t*>(idx.data_ptr()), stream_of(x.device()));
+  garfield::gpu::maxpool_fwd_nhwc(x.data_ptr(), g, y.data_ptr(), static_cast<uint8_t*>(idx.data_ptr()),
+                                  stream_of(x.device()), dtype_code(x));
 }
 
 void g_maxpool_bwd(const at::Tensor& dy, const at::Tensor& idx, int64_t k, int64_t s, int64_t p, const at::Tensor& dx) {
   auto g = pool_geometry(dx, dy, idx, k, s, p);
   c10::hip::HIPGuard guard(dx.device().index());
-  garfield::gpu::maxpool_bwd_nhwc(u16(dy), static_cast<const uint8_t*>(idx.data_ptr()), g, u16_mut(dx),
-                                  stream_of(dx.device()));
+  garfield::gpu::maxpool_bwd_nhwc(dy.data_ptr(), static_cast<const uint8_t*>(idx.data_ptr()), g, dx.data_ptr(),
+                                  stream_of(dx.device()), dtype_code(dx));
 }
 
 int g_flatten_cast_at(const std::vector<at::Tensor>& srcs, const std::vector<int64_t>& offsets,
@@ -1559,46 +1719,129 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("groups"), "True when gpu_iwgrad of this 3x3 / stride-1 / pad-1 shape runs the halo-staged kernel");
   m.def("gpu_iwgrad", &g_iwgrad, "Per-worker implicit-GEMM weight gradient on MFMA: out[s, g] = Σ over pixel "
         "split s of worker g of dyᵀ · patches(x); args (x, dy, kh, kw, sh, sw, ph, pw, dh, dw, groups, out, splits)");
+  m.def("gpu_conv_f32", &g_conv_f32, py::arg("src"), py::arg("w"), py::arg("kh"), py::arg("kw"),
+        py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("dgrad"),
+        py::arg("out"), py::arg("add") = py::none(), py::arg("pm") = 0,
+        "fp32 NHWC implicit-GEMM convolution (forward, or with dgrad the data gradient of a convolution of this "
+        "geometry, any stride) on split-bf16 MFMA (three bf16 pieces per operand, the six products of order <= 2, "
+        "fp32 accumulation); w: the weight's pieces [3, Co, K]");
+  m.def("conv_f32_supported", [](int64_t cs, int64_t co) {
+    garfield::gpu::ConvF32Geo g{};
+    g.Cs = static_cast<int>(cs);
+    g.Co = static_cast<int>(co);
+    return garfield::gpu::conv_f32_supported(g);
+  }, py::arg("cs"), py::arg("co"));
+  m.def("gpu_wgrad_f32", &g_wgrad_f32, "Per-worker fp32 weight gradient on split-bf16 MFMA; args (x, dy, kh, kw, "
+        "sh, sw, ph, pw, dh, dw, groups, out, splits)");
+  m.def("gpu_wsplit_multi", &g_wsplit_multi, "Per-step weight split of many fp32 weights: W -> its three bf16 "
+        "pieces (row pitch ld) and, optionally, the channel-transposed pieces of the data gradient");
+  m.def("gpu_linear_f32_fwd", [](const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                                 const at::Tensor& y) {
+    const auto dev = x.device();
+    const int64_t R = x.size(0), F = x.size(1), O = w.size(0);
+    check_f32_mat(x, dev, R, F, "x");
+    check_f32_mat(w, dev, O, F, "w");
+    check_f32_mat(y, dev, R, O, "y");
+    const float* bp = nullptr;
+    if (b.has_value() && b->defined()) {
+      check_f32_mat(*b, dev, 1, O, "b");
+      bp = b->data_ptr<float>();
+    }
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::linear_f32_fwd(x.data_ptr<float>(), w.data_ptr<float>(), bp, static_cast<int>(R),
+                                  static_cast<int>(F), static_cast<int>(O), y.data_ptr<float>(), stream_of(dev));
+  }, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), "fp32 classifier forward y = x wᵀ + b");
+  m.def("gpu_linear_f32_dgrad", [](const at::Tensor& dl, const at::Tensor& w, const at::Tensor& dx) {
+    const auto dev = dl.device();
+    const int64_t R = dl.size(0), O = dl.size(1), F = w.size(1);
+    check_f32_mat(dl, dev, R, O, "dl");
+    check_f32_mat(w, dev, O, F, "w");
+    check_f32_mat(dx, dev, R, F, "dx");
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::linear_f32_dgrad(dl.data_ptr<float>(), w.data_ptr<float>(), static_cast<int>(R),
+                                    static_cast<int>(F), static_cast<int>(O), dx.data_ptr<float>(), stream_of(dev));
+  }, py::arg("dl"), py::arg("w"), py::arg("dx"), "fp32 classifier data gradient dx = dl w");
+  m.def("gpu_linear_f32_wgrad", [](const at::Tensor& x, const at::Tensor& dl, int64_t groups, const at::Tensor& rows,
+                                   int64_t row_stride, int64_t off_w, int64_t off_b) {
+    const auto dev = x.device();
+    const int64_t R = x.size(0), F = x.size(1), O = dl.size(1);
+    check_f32_mat(x, dev, R, F, "x");
+    check_f32_mat(dl, dev, R, O, "dl");
+    TORCH_CHECK(groups >= 1 && R % groups == 0, "gpu_linear_f32_wgrad: rows do not split into groups");
+    TORCH_CHECK(rows.is_cuda() && rows.device() == dev && rows.scalar_type() == at::kFloat && rows.is_contiguous(),
+                "gpu_linear_f32_wgrad: rows must be a contiguous fp32 exchange buffer");
+    TORCH_CHECK(off_w >= 0 && row_stride >= 0 && (groups - 1) * row_stride + off_w + O * F <= rows.numel() &&
+                    (off_b < 0 || (groups - 1) * row_stride + off_b + O <= rows.numel()),
+                "gpu_linear_f32_wgrad: row offsets out of bounds");
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::linear_f32_wgrad(x.data_ptr<float>(), dl.data_ptr<float>(), static_cast<int>(groups),
+                                    static_cast<int>(R / groups), static_cast<int>(F), static_cast<int>(O),
+                                    rows.data_ptr<float>(), row_stride, off_w, off_b, stream_of(dev));
+  }, py::arg("x"), py::arg("dl"), py::arg("groups"), py::arg("rows"), py::arg("row_stride"), py::arg("off_w"),
+     py::arg("off_b"), "Per-worker fp32 classifier dW / db written into the exchange rows");
+  m.def("gpu_avgpool_f32", [](const at::Tensor& x, const at::Tensor& y, bool backward) {
+    // forward: x [N, C, H, W] channels_last -> y [N, C]; backward: x = dy [N, C] -> y = dx [N, C, H, W]
+    const at::Tensor& big = backward ? y : x;
+    const at::Tensor& small = backward ? x : y;
+    const auto dev = big.device();
+    check_f32_cl(big, dev, "activation");
+    const int64_t N = big.size(0), C = big.size(1), HW = big.size(2) * big.size(3);
+    check_f32_mat(small, dev, N, C, "pooled");
+    c10::hip::HIPGuard guard(dev.index());
+    if (backward)
+      garfield::gpu::avgpool_f32_bwd(x.data_ptr<float>(), static_cast<int>(N), static_cast<int>(HW),
+                                     static_cast<int>(C), y.data_ptr<float>(), stream_of(dev));
+    else
+      garfield::gpu::avgpool_f32_fwd(x.data_ptr<float>(), static_cast<int>(N), static_cast<int>(HW),
+                                     static_cast<int>(C), y.data_ptr<float>(), stream_of(dev));
+  }, py::arg("x"), py::arg("y"), py::arg("backward"), "fp32 NHWC global average pool (forward / backward)");
   m.def("stem_supported", &garfield::gpu::stem_supported, py::arg("h"), py::arg("w"),
         "True when the implicit stem kernels (7x7/2, 3 -> 64 channels) handle H x W images");
   m.def("gpu_stem_fwd", [](const at::Tensor& x, const at::Tensor& w160, const at::Tensor& y) {
-    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3 &&
+    const bool split = x.scalar_type() == at::kFloat;
+    TORCH_CHECK(x.is_cuda() && (split || x.scalar_type() == at::kBFloat16) && x.dim() == 4 && x.size(1) == 3 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "gpu_stem_fwd: x must be a channels_last bf16 [N, 3, H, W] tensor");
-    TORCH_CHECK(w160.scalar_type() == at::kBFloat16 && w160.is_contiguous() && w160.numel() == 64 * 160,
-                "gpu_stem_fwd: w must be the contiguous zero-padded [64, 160] bf16 matrix");
+                "gpu_stem_fwd: x must be a channels_last bf16 or fp32 [N, 3, H, W] tensor");
+    TORCH_CHECK(w160.device() == x.device() && w160.scalar_type() == at::kBFloat16 && w160.is_contiguous() &&
+                    w160.numel() == (split ? 3 : 1) * 64 * 160,
+                "gpu_stem_fwd: w must be the contiguous zero-padded [64, 160] bf16 matrix (fp32 x: its pieces "
+                "[3, 64, 160])");
     const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
     TORCH_CHECK(garfield::gpu::stem_supported(static_cast<int>(H), static_cast<int>(W)), "gpu_stem_fwd: unsupported size");
     const int64_t Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
-    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == N && y.size(1) == 64 &&
-                    y.size(2) == Ho && y.size(3) == Wo && y.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "gpu_stem_fwd: y must be a channels_last bf16 [N, 64, Ho, Wo] tensor");
+    TORCH_CHECK(y.device() == x.device() && y.scalar_type() == x.scalar_type() && y.dim() == 4 && y.size(0) == N &&
+                    y.size(1) == 64 && y.size(2) == Ho && y.size(3) == Wo &&
+                    y.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_stem_fwd: y must be a channels_last [N, 64, Ho, Wo] tensor of x's dtype");
     c10::hip::HIPGuard guard(x.device().index());
-    garfield::gpu::stem_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                            reinterpret_cast<const uint16_t*>(w160.data_ptr()), static_cast<int>(N), static_cast<int>(H),
-                            static_cast<int>(W), reinterpret_cast<uint16_t*>(y.data_ptr()), stream_of(x.device()));
-  }, py::arg("x"), py::arg("w"), py::arg("y"), "Implicit-GEMM ResNet stem forward (7x7/2, pad 3, 3 -> 64)");
+    garfield::gpu::stem_fwd(x.data_ptr(), reinterpret_cast<const uint16_t*>(w160.data_ptr()), split,
+                            static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), y.data_ptr(),
+                            stream_of(x.device()));
+  }, py::arg("x"), py::arg("w"), py::arg("y"),
+     "Implicit-GEMM ResNet stem forward (7x7/2, pad 3, 3 -> 64); fp32 x: split-bf16 MFMA on the weight's pieces");
   m.def("gpu_stem_wgrad", [](const at::Tensor& x, const at::Tensor& dy, int64_t groups, const at::Tensor& part) {
-    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3 &&
+    const bool split = x.scalar_type() == at::kFloat;
+    TORCH_CHECK(x.is_cuda() && (split || x.scalar_type() == at::kBFloat16) && x.dim() == 4 && x.size(1) == 3 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "gpu_stem_wgrad: x must be a channels_last bf16 [N, 3, H, W] tensor");
+                "gpu_stem_wgrad: x must be a channels_last bf16 or fp32 [N, 3, H, W] tensor");
     const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
     const int64_t Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
-    TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N && dy.size(1) == 64 &&
-                    dy.size(2) == Ho && dy.size(3) == Wo && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "gpu_stem_wgrad: dy must be a channels_last bf16 [N, 64, Ho, Wo] tensor");
+    TORCH_CHECK(dy.device() == x.device() && dy.scalar_type() == x.scalar_type() && dy.dim() == 4 && dy.size(0) == N &&
+                    dy.size(1) == 64 && dy.size(2) == Ho && dy.size(3) == Wo &&
+                    dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_stem_wgrad: dy must be a channels_last [N, 64, Ho, Wo] tensor of x's dtype");
     TORCH_CHECK(groups >= 1 && N % groups == 0, "gpu_stem_wgrad: images not divisible into groups");
     TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 4 &&
                     part.size(1) == groups && part.size(2) == 64 && part.size(3) == 147,
                 "gpu_stem_wgrad: part must be a contiguous fp32 [slices, groups, 64, 147] tensor");
     TORCH_CHECK(garfield::gpu::stem_supported(static_cast<int>(H), static_cast<int>(W)), "gpu_stem_wgrad: unsupported size");
     c10::hip::HIPGuard guard(x.device().index());
-    garfield::gpu::stem_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                              reinterpret_cast<const uint16_t*>(dy.data_ptr()), static_cast<int>(N), static_cast<int>(H),
+    garfield::gpu::stem_wgrad(x.data_ptr(), dy.data_ptr(), static_cast<int>(N), static_cast<int>(H),
                               static_cast<int>(W), static_cast<int>(groups), static_cast<int>(part.size(0)),
-                              part.data_ptr<float>(), stream_of(x.device()));
+                              part.data_ptr<float>(), split, stream_of(x.device()));
   }, py::arg("x"), py::arg("dy"), py::arg("groups"), py::arg("part"),
-     "Implicit ResNet-stem weight gradient per worker: part[s, g] = slice s of worker g's dW [64, 147]");
+     "Implicit ResNet-stem weight gradient per worker: part[s, g] = slice s of worker g's dW [64, 147] (bf16 or "
+     "fp32 x / dy)");
   m.def("gpu_maxpool_fwd", &g_maxpool_fwd, "NHWC bf16 max pooling (k x k, stride s, padding p) keeping the "
         "argmax tap per element; args (x, k, s, p, y, idx)");
   m.def("gpu_maxpool_bwd", &g_maxpool_bwd, "Max-pooling backward as a gather; args (dy, idx, k, s, p, dx)");

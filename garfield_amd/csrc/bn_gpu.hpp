@@ -39,11 +39,12 @@ bool bn_small(int64_t rg);
 
 // defer_running (small-layer path only): skip the running-statistics replay; the caller
 // batches it with bn_running_update.
-void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
+// dt: the activations' dtype (kBF16, or kF32 for the reference-precision step)
+void bn_forward(const void* x, const void* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
-                float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
+                float* mean, float* istd, float* scale, float* shift, void* y, bool relu, uint8_t* mask,
                 bool defer_running, hipStream_t stream, const float* tile_stats = nullptr, int64_t tile_m = 0,
-                int tile_e = 1);
+                int tile_e = 1, int dt = 1);
 
 // Fresh batches (data_aug.hip): out[r] (bf16 channels_last [R, C, H, W]) = normalise(random crop
 // (pad) + random horizontal flip of uint8 NHWC image src[idx[r]]); the crop/flip of row r is a hash
@@ -55,14 +56,16 @@ struct AugNorm {
 // idx null: row r samples image hash(seed, step, r) % nsrc; lab_out (nullable) receives lab_src[image].
 void augment_gather(const uint8_t* src, int64_t nsrc, const int64_t* idx, const int64_t* lab_src, int64_t* lab_out,
                     int64_t R, int H, int W, int C, int pad, bool flip,
-                    uint64_t seed, uint64_t step, const AugNorm& nrm, uint16_t* out, hipStream_t stream);
+                    uint64_t seed, uint64_t step, const AugNorm& nrm, void* out, hipStream_t stream, int out_dt = 1);
 
-// ResNet stem (stem_nhwc.hip): 7x7 / stride 2 / padding 3 convolution of 3-channel NHWC bf16
+// ResNet stem (stem_nhwc.hip): 7x7 / stride 2 / padding 3 convolution of 3-channel NHWC
 // images into 64 channels on MFMA, without a patch matrix. w: zero-padded [64][160] bf16.
+// split: the fp32 form — x / y fp32, w = the weight's three bf16 pieces [3][64][160].
 bool stem_supported(int H, int W);
-void stem_fwd(const uint16_t* x, const uint16_t* w, int N, int H, int W, uint16_t* y, hipStream_t stream);
-// per-worker weight gradients: part fp32 [slices][groups][64][147] (sum over slices = dW of the worker)
-void stem_wgrad(const uint16_t* x, const uint16_t* dy, int N, int H, int W, int groups, int slices, float* part,
+void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream);
+// per-worker weight gradients: part fp32 [slices][groups][64][147] (sum over slices = dW of the worker);
+// split: x / dy fp32
+void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,
                 hipStream_t stream);
 
 // Row-major NT GEMM on MFMA (gemm_nt.hip): C[M, N] = A[M, K] · B[N, K]ᵀ (+ add), bf16; K % 64 == 0,
@@ -96,11 +99,11 @@ void bn_finalize_tiles(const float* stats, int64_t H, int E, int64_t M, int64_t 
 // grow (nullable): exchange buffer; group g's dγ[c] goes to grow[g*row_stride + off_gamma + c]
 // (dβ likewise at off_beta; a negative offset skips it), cast to grow_dt.
 // coef: [groups, 3, C] fp32 workspace.
-void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const uint8_t* mask, int64_t rg, int groups,
+void bn_backward(const void* x, const void* dy, const void* y, const uint8_t* mask, int64_t rg, int groups,
                  int C,
-                 const float* gamma, const float* mean, const float* istd, float* part, float* coef, uint16_t* dx,
-                 uint16_t* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
-                 hipStream_t stream);
+                 const float* gamma, const float* mean, const float* istd, float* part, float* coef, void* dx,
+                 void* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
+                 hipStream_t stream, int dt = 1);
 
 // NHWC im2col (bf16): col[(n*Ho + ho)*Wo + wo][(i*KW + j)*C + c] = x[n][ho*sh - ph + i*dh][wo*sw - pw + j*dw][c]
 // (0 outside the image). col: [N*Ho*Wo, ldc] with ldc >= KH*KW*C; columns past KH*KW*C are zeroed
@@ -138,8 +141,8 @@ bool wgrad3x3_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int C
                    hipStream_t stream);
 // Max pooling over NHWC bf16 (C % 8 == 0); idx: the window tap of each output maximum
 // (one byte per output element), consumed by the gather backward.
-void maxpool_fwd_nhwc(const uint16_t* x, const Im2col& g, uint16_t* y, uint8_t* idx, hipStream_t stream);
-void maxpool_bwd_nhwc(const uint16_t* dy, const uint8_t* idx, const Im2col& g, uint16_t* dx, hipStream_t stream);
+void maxpool_fwd_nhwc(const void* x, const Im2col& g, void* y, uint8_t* idx, hipStream_t stream, int dt = 1);
+void maxpool_bwd_nhwc(const void* dy, const uint8_t* idx, const Im2col& g, void* dx, hipStream_t stream, int dt = 1);
 // Per-worker implicit weight gradient (iconv_nhwc.hip): out[s][g][co][k] (fp32 partial slab s of
 // worker g, or bf16 when out_bf16, e.g. straight into the exchange rows) = Σ over the s-th of `splits`
 // pixel ranges of worker g of dy[m, co] · patch(x)[m, k]; C % 64 == 0, Cout % 64 == 0, x / dy 16-B aligned.

@@ -24,6 +24,7 @@
 // Launch boundaries order the stages (no inter-workgroup hand-off inside a
 // launch); every reduction runs in a fixed order, so results are deterministic.
 #include <cstdlib>
+#include <type_traits>
 
 #include "bn_gpu.hpp"
 #include "gar_device.hpp"
@@ -58,28 +59,27 @@ Geo geometry(int64_t rg, int groups, int C) {
   // enough row chunks to give the partial kernel ~1024 workgroups, each at least 4 row passes
   const int ncb = (C + g.cb - 1) / g.cb;
   const int64_t wg = static_cast<int64_t>(groups) * ncb;
-  static const int64_t target = [] {   // tuning knob: total partial-pass workgroups
-    const char* e = std::getenv("GARFIELD_BN_PARTIAL_WG");
-    const long v = e ? std::atol(e) : 0;
-    return static_cast<int64_t>(v > 0 ? v : 1024);
-  }();
+  constexpr int64_t target = 1024;   // total partial-pass workgroups
   int64_t want = (target + wg - 1) / wg;
   int64_t maxc = (rg + 4 * g.rp - 1) / (4 * g.rp);
   int64_t c = want < maxc ? want : maxc;
   if (c < 1) c = 1;
-  static const int64_t max_chunks = [] {   // tuning knob: cap on row chunks
-    const char* e = std::getenv("GARFIELD_BN_MAX_CHUNKS");
-    const long v = e ? std::atol(e) : 0;
-    return static_cast<int64_t>(v > 0 ? v : kBnMaxChunks);
-  }();
-  if (c > max_chunks) c = max_chunks;
+  if (c > kBnMaxChunks) c = kBnMaxChunks;
   g.rows_per_chunk = (rg + c - 1) / c;
   g.chunks = static_cast<int>((rg + g.rows_per_chunk - 1) / g.rows_per_chunk);
   return g;
 }
 
-__device__ __forceinline__ void load8(const uint16_t* p, int64_t off, float (&v)[8]) {
-  load_vec<kBF16, 8>(p, off, v);
+template <int DT>
+__device__ __forceinline__ void load8(const void* p, int64_t off, float (&v)[8]) {
+  load_vec<DT, 8>(p, off, v);
+}
+
+// bit of the ReLU mask: the STORED value is > 0 (what a y > 0 test reads back)
+template <int DT>
+__device__ __forceinline__ bool stored_pos(float o) {
+  if constexpr (DT == kF32) return o > 0.f;
+  else return f_to_bf16(o) != 0;
 }
 
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
@@ -94,9 +94,9 @@ __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
 //   backward: s = Σ dz, q = Σ dz (x - mean)
 // RM: ReLU mask source of the backward: 0 none, 1 the bf16 output y (> 0), 2 the
 // forward's bit mask (one byte per 8 channels: 1/16 of y's bytes).
-template <bool BWD, int RM>
-__global__ __launch_bounds__(kThreads) void k_partial(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                                                     const uint16_t* __restrict__ y, const uint8_t* __restrict__ mask,
+template <bool BWD, int RM, int DT>
+__global__ __launch_bounds__(kThreads) void k_partial(const void* __restrict__ x, const void* __restrict__ dy,
+                                                     const void* __restrict__ y, const uint8_t* __restrict__ mask,
                                                      const float* __restrict__ mean, Geo geo,
                                                      float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float red[2][kThreads * 8];
@@ -118,22 +118,22 @@ __global__ __launch_bounds__(kThreads) void k_partial(const uint16_t* __restrict
   for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; sh[i] = 0.f; }
   if (active) {
     if constexpr (BWD) load8f(mean + static_cast<int64_t>(g) * C + c0, sh);
-    else load8(x, base * C + c0, sh);
+    else load8<DT>(x, base * C + c0, sh);
     int64_t r = r0 + tr;
     // two rows in flight per lane
     for (; r + geo.rp < r1; r += 2 * geo.rp) {
       const int64_t o0 = (base + r) * C + c0, o1 = o0 + static_cast<int64_t>(geo.rp) * C;
       float a0[8], a1[8];
-      load8(x, o0, a0);
-      load8(x, o1, a1);
+      load8<DT>(x, o0, a0);
+      load8<DT>(x, o1, a1);
       if constexpr (BWD) {
         float d0[8], d1[8];
-        load8(dy, o0, d0);
-        load8(dy, o1, d1);
+        load8<DT>(dy, o0, d0);
+        load8<DT>(dy, o1, d1);
         if constexpr (RM == 1) {
           float y0[8], y1[8];
-          load8(y, o0, y0);
-          load8(y, o1, y1);
+          load8<DT>(y, o0, y0);
+          load8<DT>(y, o1, y1);
 #pragma unroll
           for (int i = 0; i < 8; ++i) { d0[i] = y0[i] > 0.f ? d0[i] : 0.f; d1[i] = y1[i] > 0.f ? d1[i] : 0.f; }
         } else if constexpr (RM == 2) {
@@ -161,13 +161,13 @@ __global__ __launch_bounds__(kThreads) void k_partial(const uint16_t* __restrict
     for (; r < r1; r += geo.rp) {
       const int64_t o0 = (base + r) * C + c0;
       float a0[8];
-      load8(x, o0, a0);
+      load8<DT>(x, o0, a0);
       if constexpr (BWD) {
         float d0[8];
-        load8(dy, o0, d0);
+        load8<DT>(dy, o0, d0);
         if constexpr (RM == 1) {
           float y0[8];
-          load8(y, o0, y0);
+          load8<DT>(y, o0, y0);
 #pragma unroll
           for (int i = 0; i < 8; ++i) d0[i] = y0[i] > 0.f ? d0[i] : 0.f;
         } else if constexpr (RM == 2) {
@@ -239,7 +239,8 @@ __device__ __forceinline__ void chunk_sums(const float* __restrict__ part, const
 }
 
 // Forward finalize of one (group, 64-channel block): mean, 1/std, scale, shift.
-__global__ __launch_bounds__(kThreads) void k_fwd_finalize(const float* __restrict__ part, const uint16_t* __restrict__ x,
+template <int DT>
+__global__ __launch_bounds__(kThreads) void k_fwd_finalize(const float* __restrict__ part, const void* __restrict__ x,
                                                           Geo geo, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps,
                                                           float* __restrict__ mean, float* __restrict__ istd,
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(kThreads) void k_fwd_finalize(const float* __restri
   chunk_sums(part, geo, g, c, sred, qred, S, Q);
   if (threadIdx.x >= kFinCh || c >= C) return;
   const float M = static_cast<float>(geo.rg);
-  const float sh = bf16_to_f(x[static_cast<int64_t>(g) * geo.rg * C + c]);
+  const float sh = load_one<DT>(x, static_cast<int64_t>(g) * geo.rg * C + c);
   const float m1 = S / M;
   float var = Q / M - m1 * m1;
   var = var > 0.f ? var : 0.f;
@@ -300,11 +301,11 @@ struct RunStats {
   int groups;
 };
 
-template <bool RES, bool RELU>
-__global__ __launch_bounds__(kThreads) void k_fwd_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+template <bool RES, bool RELU, int DT>
+__global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__ x, const void* __restrict__ res,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        int64_t rg, int64_t R, int C, int tch, int rp,
-                                                       uint16_t* __restrict__ y, uint8_t* __restrict__ mask,
+                                                       void* __restrict__ y, uint8_t* __restrict__ mask,
                                                        RunStats rs) {
   if (blockIdx.x == 0 && rs.run_mean)
     running_update(rs.mean, rs.istd, rs.groups, C, rg, rs.eps, rs.momentum, rs.run_mean, rs.run_var);
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const uint16_t* __restri
       const int c = v * 8;
       const int64_t off = row * C + c;
       float a[8], sc[8], sf[8];
-      load8(x, off, a);
+      load8<DT>(x, off, a);
       load8f(scale + static_cast<int64_t>(g) * C + c, sc);
       load8f(shift + static_cast<int64_t>(g) * C + c, sf);
       float o[8];
@@ -329,21 +330,21 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const uint16_t* __restri
       for (int i = 0; i < 8; ++i) o[i] = a[i] * sc[i] + sf[i];
       if constexpr (RES) {
         float r[8];
-        load8(res, off, r);
+        load8<DT>(res, off, r);
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] += r[i];
       }
       if constexpr (RELU) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = o[i] > 0.f ? o[i] : 0.f;
-        if (mask) {  // bit i: the STORED (bf16) value is > 0, exactly what a y > 0 test reads back
+        if (mask) {  // bit i: the STORED value is > 0, exactly what a y > 0 test reads back
           uint32_t bits = 0;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) bits |= (f_to_bf16(o[i]) != 0 ? 1u : 0u) << i;
+          for (int i = 0; i < 8; ++i) bits |= (stored_pos<DT>(o[i]) ? 1u : 0u) << i;
           mask[off >> 3] = static_cast<uint8_t>(bits);
         }
       }
-      store_vec<8>(y, kBF16, off, o);
+      store_vec<8>(y, DT, off, o);
     }
   }
 }
@@ -377,13 +378,13 @@ __global__ __launch_bounds__(kThreads) void k_bwd_finalize(const float* __restri
   coef[o3 + 2 * C + c] = dgamma / M * is;       // c  (x̂·dγ/M = (x-μ)·c)
 }
 
-template <int RM, bool RES_OUT>
-__global__ __launch_bounds__(kThreads) void k_bwd_apply(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                                                       const uint16_t* __restrict__ y, const uint8_t* __restrict__ mask,
+template <int RM, bool RES_OUT, int DT>
+__global__ __launch_bounds__(kThreads) void k_bwd_apply(const void* __restrict__ x, const void* __restrict__ dy,
+                                                       const void* __restrict__ y, const uint8_t* __restrict__ mask,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ coef, int64_t rg, int64_t R, int C,
-                                                       int tch, int rp, uint16_t* __restrict__ dx,
-                                                       uint16_t* __restrict__ dres) {
+                                                       int tch, int rp, void* __restrict__ dx,
+                                                       void* __restrict__ dres) {
   const int tr = threadIdx.x / tch;
   if (tr >= rp) return;
   const int nv = C / 8;
@@ -398,11 +399,11 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const uint16_t* __restri
       const int c = v * 8;
       const int64_t off = row * C + c;
       float a[8], d[8], mu[8], ca[8], cb[8], cc[8];
-      load8(x, off, a);
-      load8(dy, off, d);
+      load8<DT>(x, off, a);
+      load8<DT>(dy, off, d);
       if constexpr (RM == 1) {
         float yy[8];
-        load8(y, off, yy);
+        load8<DT>(y, off, yy);
 #pragma unroll
         for (int i = 0; i < 8; ++i) d[i] = yy[i] > 0.f ? d[i] : 0.f;
       } else if constexpr (RM == 2) {
@@ -417,8 +418,8 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const uint16_t* __restri
       float o[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = ca[i] * (d[i] - cb[i] - (a[i] - mu[i]) * cc[i]);
-      store_vec<8>(dx, kBF16, off, o);
-      if constexpr (RES_OUT) store_vec<8>(dres, kBF16, off, d);
+      store_vec<8>(dx, DT, off, o);
+      if constexpr (RES_OUT) store_vec<8>(dres, DT, off, d);
     }
   }
 }
@@ -444,8 +445,8 @@ dim3 apply_grid(int64_t R, int rp) {
 // replayed by k_running (one tiny launch, or batched for many layers by the caller).
 constexpr int kSmallRows = 1024;
 constexpr int kSmallThreads = 1024;             // 16 waves per workgroup to hide the load latency
-// Channels per workgroup CH (16, 32 or 64; GARFIELD_BN_SMALL_CH): a layer of C channels and
-// k workers runs C / CH x k workgroups, e.g. 64 for CIFAR layer3 (C = 256) at CH = 32.
+// Channels per workgroup CH (32): a layer of C channels and k workers runs C / CH x k workgroups,
+// e.g. 64 for CIFAR layer3 (C = 256).
 template <int CH>
 struct SmallGeo {
   static constexpr int Vec = CH / 8;                       // 16-byte vectors per row
@@ -479,8 +480,32 @@ __device__ __forceinline__ void small_reduce(float (&red)[2][SmallGeo<CH>::Lanes
 }
 
 
-__device__ __forceinline__ uint4 ld_raw8(const uint16_t* p, int64_t off) {
-  return *reinterpret_cast<const uint4*>(p + off);
+// 8 channels of one row as stored: packed bf16 (one uint4) or fp32 (two float4)
+struct F8 {
+  float4 a, b;
+};
+template <int DT>
+using Raw8 = typename std::conditional<DT == kF32, F8, uint4>::type;
+
+template <int DT>
+__device__ __forceinline__ Raw8<DT> ld_raw8(const void* p, int64_t off) {
+  if constexpr (DT == kF32) {
+    const float* f = static_cast<const float*>(p) + off;
+    return F8{*reinterpret_cast<const float4*>(f), *reinterpret_cast<const float4*>(f + 4)};
+  } else {
+    return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + off);
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void st_raw8(void* p, int64_t off, const Raw8<DT>& r) {
+  if constexpr (DT == kF32) {
+    float* f = static_cast<float*>(p) + off;
+    *reinterpret_cast<float4*>(f) = r.a;
+    *reinterpret_cast<float4*>(f + 4) = r.b;
+  } else {
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + off) = r;
+  }
 }
 
 __device__ __forceinline__ void unpack8(const uint4 u, float (&v)[8]) {
@@ -489,17 +514,54 @@ __device__ __forceinline__ void unpack8(const uint4 u, float (&v)[8]) {
   v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
   v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
 }
+__device__ __forceinline__ void unpack8(const F8& u, float (&v)[8]) {
+  v[0] = u.a.x; v[1] = u.a.y; v[2] = u.a.z; v[3] = u.a.w;
+  v[4] = u.b.x; v[5] = u.b.y; v[6] = u.b.z; v[7] = u.b.w;
+}
 
-// Each thread keeps its (<= kSmallIt) rows of 8 channels in registers as packed bf16,
-// so the apply pass does not re-read x (or dy) from memory.
-template <int CH, bool RES, bool RELU>
-__global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* __restrict__ x,
-                                                          const uint16_t* __restrict__ res, int64_t rg, int C,
+// dz = dy where the forward output y > 0 (RM 1) / its mask bit is set (RM 2), else 0
+__device__ __forceinline__ uint4 keep_pos(uint4 d, const uint4 yy) {
+  // bf16 > 0: sign bit clear and non-zero
+  auto keep = [](uint32_t dv, uint32_t yv) {
+    const uint32_t lo = ((yv & 0x8000u) == 0 && (yv & 0x7fffu) != 0) ? 0x0000ffffu : 0u;
+    const uint32_t hi = ((yv & 0x80000000u) == 0 && (yv & 0x7fff0000u) != 0) ? 0xffff0000u : 0u;
+    return dv & (lo | hi);
+  };
+  d.x = keep(d.x, yy.x); d.y = keep(d.y, yy.y); d.z = keep(d.z, yy.z); d.w = keep(d.w, yy.w);
+  return d;
+}
+__device__ __forceinline__ F8 keep_pos(F8 d, const F8& yy) {
+  d.a.x = yy.a.x > 0.f ? d.a.x : 0.f; d.a.y = yy.a.y > 0.f ? d.a.y : 0.f;
+  d.a.z = yy.a.z > 0.f ? d.a.z : 0.f; d.a.w = yy.a.w > 0.f ? d.a.w : 0.f;
+  d.b.x = yy.b.x > 0.f ? d.b.x : 0.f; d.b.y = yy.b.y > 0.f ? d.b.y : 0.f;
+  d.b.z = yy.b.z > 0.f ? d.b.z : 0.f; d.b.w = yy.b.w > 0.f ? d.b.w : 0.f;
+  return d;
+}
+__device__ __forceinline__ uint4 keep_bits(uint4 d, uint32_t mb) {
+  auto keep = [](uint32_t dv, uint32_t m2) {
+    return dv & (((m2 & 1u) ? 0x0000ffffu : 0u) | ((m2 & 2u) ? 0xffff0000u : 0u));
+  };
+  d.x = keep(d.x, mb); d.y = keep(d.y, mb >> 2); d.z = keep(d.z, mb >> 4); d.w = keep(d.w, mb >> 6);
+  return d;
+}
+__device__ __forceinline__ F8 keep_bits(F8 d, uint32_t mb) {
+  d.a.x = (mb & 1u) ? d.a.x : 0.f; d.a.y = (mb & 2u) ? d.a.y : 0.f;
+  d.a.z = (mb & 4u) ? d.a.z : 0.f; d.a.w = (mb & 8u) ? d.a.w : 0.f;
+  d.b.x = (mb & 16u) ? d.b.x : 0.f; d.b.y = (mb & 32u) ? d.b.y : 0.f;
+  d.b.z = (mb & 64u) ? d.b.z : 0.f; d.b.w = (mb & 128u) ? d.b.w : 0.f;
+  return d;
+}
+
+// Each thread keeps its (<= kSmallIt) rows of 8 channels in registers as stored (packed
+// bf16 or fp32), so the apply pass does not re-read x (or dy) from memory.
+template <int CH, bool RES, bool RELU, int DT>
+__global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const void* __restrict__ x,
+                                                          const void* __restrict__ res, int64_t rg, int C,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps,
                                                           float* __restrict__ mean, float* __restrict__ istd,
                                                           float* __restrict__ scale, float* __restrict__ shift,
-                                                          uint16_t* __restrict__ y, uint8_t* __restrict__ mask) {
+                                                          void* __restrict__ y, uint8_t* __restrict__ mask) {
   constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH>::Vec, kSmallLanes = SmallGeo<CH>::Lanes,
                 kSmallIt = SmallGeo<CH>::It;
   __shared__ float red[2][kSmallLanes][kSmallCh];
@@ -510,15 +572,15 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* 
   const bool act = c0 < C;
   const int64_t base = static_cast<int64_t>(g) * rg;
   float s[8], q[8], sh[8];
-  uint4 xr[kSmallIt];
+  Raw8<DT> xr[kSmallIt];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; sh[i] = 0.f; }
   if (act) {
-    load8(x, base * C + c0, sh);   // shifted sums (see k_partial)
+    load8<DT>(x, base * C + c0, sh);   // shifted sums (see k_partial)
 #pragma unroll
     for (int it = 0; it < kSmallIt; ++it) {
       const int64_t r = tr + it * kSmallLanes;
-      if (r < rg) xr[it] = ld_raw8(x, (base + r) * C + c0);
+      if (r < rg) xr[it] = ld_raw8<DT>(x, (base + r) * C + c0);
     }
 #pragma unroll
     for (int it = 0; it < kSmallIt; ++it) {
@@ -543,7 +605,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* 
       const float m1 = S / M;
       float var = Q / M - m1 * m1;
       var = var > 0.f ? var : 0.f;
-      const float mu = bf16_to_f(x[base * C + c]) + m1;
+      const float mu = load_one<DT>(x, base * C + c) + m1;
       const float is = rsqrtf(var + eps);
       const int64_t gc = static_cast<int64_t>(g) * C + c;
       mean[gc] = mu;
@@ -572,7 +634,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* 
     for (int i = 0; i < 8; ++i) o[i] = a[i] * sc[i] + sf[i];
     if constexpr (RES) {
       float rr[8];
-      load8(res, off, rr);
+      load8<DT>(res, off, rr);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] += rr[i];
     }
@@ -582,20 +644,20 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const uint16_t* 
       if (mask) {
         uint32_t bits = 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) bits |= (f_to_bf16(o[i]) != 0 ? 1u : 0u) << i;
+        for (int i = 0; i < 8; ++i) bits |= (stored_pos<DT>(o[i]) ? 1u : 0u) << i;
         mask[off >> 3] = static_cast<uint8_t>(bits);
       }
     }
-    store_vec<8>(y, kBF16, off, o);
+    store_vec<8>(y, DT, off, o);
   }
 }
 
-template <int CH, int RM, bool RES_OUT>
+template <int CH, int RM, bool RES_OUT, int DT>
 __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+    const void* __restrict__ x, const void* __restrict__ dy, const void* __restrict__ y,
     const uint8_t* __restrict__ mask, int64_t rg, int C, const float* __restrict__ gamma,
-    const float* __restrict__ mean, const float* __restrict__ istd, uint16_t* __restrict__ dx,
-    uint16_t* __restrict__ dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta) {
+    const float* __restrict__ mean, const float* __restrict__ istd, void* __restrict__ dx,
+    void* __restrict__ dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta) {
   constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH>::Vec, kSmallLanes = SmallGeo<CH>::Lanes,
                 kSmallIt = SmallGeo<CH>::It;
   __shared__ float red[2][kSmallLanes][kSmallCh];
@@ -605,8 +667,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
   const int c0 = blockIdx.x * kSmallCh + tc * 8;
   const bool act = c0 < C;
   const int64_t base = static_cast<int64_t>(g) * rg;
-  // dz = dy masked by the forward ReLU, kept packed (bf16) in registers with x
-  uint4 xr[kSmallIt], dr[kSmallIt];
+  // dz = dy masked by the forward ReLU, kept as stored in registers with x
+  Raw8<DT> xr[kSmallIt], dr[kSmallIt];
   float A[8], B[8], mu[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { A[i] = 0.f; B[i] = 0.f; mu[i] = 0.f; }
@@ -617,24 +679,10 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
       const int64_t r = tr + it * kSmallLanes;
       if (r < rg) {
         const int64_t off = (base + r) * C + c0;
-        xr[it] = ld_raw8(x, off);
-        uint4 d = ld_raw8(dy, off);
-        if constexpr (RM == 1) {
-          const uint4 yy = ld_raw8(y, off);
-          // bf16 > 0: sign bit clear and non-zero
-          auto keep = [](uint32_t dv, uint32_t yv) {
-            const uint32_t lo = ((yv & 0x8000u) == 0 && (yv & 0x7fffu) != 0) ? 0x0000ffffu : 0u;
-            const uint32_t hi = ((yv & 0x80000000u) == 0 && (yv & 0x7fff0000u) != 0) ? 0xffff0000u : 0u;
-            return dv & (lo | hi);
-          };
-          d.x = keep(d.x, yy.x); d.y = keep(d.y, yy.y); d.z = keep(d.z, yy.z); d.w = keep(d.w, yy.w);
-        } else if constexpr (RM == 2) {
-          const uint32_t mb = mask[off >> 3];
-          auto keep = [](uint32_t dv, uint32_t m2) {
-            return dv & (((m2 & 1u) ? 0x0000ffffu : 0u) | ((m2 & 2u) ? 0xffff0000u : 0u));
-          };
-          d.x = keep(d.x, mb); d.y = keep(d.y, mb >> 2); d.z = keep(d.z, mb >> 4); d.w = keep(d.w, mb >> 6);
-        }
+        xr[it] = ld_raw8<DT>(x, off);
+        Raw8<DT> d = ld_raw8<DT>(dy, off);
+        if constexpr (RM == 1) d = keep_pos(d, ld_raw8<DT>(y, off));
+        else if constexpr (RM == 2) d = keep_bits(d, mask[off >> 3]);
         dr[it] = d;
       }
     }
@@ -688,8 +736,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
     unpack8(dr[it], d);
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = ca[i] * (d[i] - cb[i] - (a[i] - mu[i]) * cc[i]);
-    store_vec<8>(dx, kBF16, off, o);
-    if constexpr (RES_OUT) *reinterpret_cast<uint4*>(dres + off) = dr[it];
+    store_vec<8>(dx, DT, off, o);
+    if constexpr (RES_OUT) st_raw8<DT>(dres, off, dr[it]);
   }
 }
 
@@ -712,38 +760,28 @@ __global__ __launch_bounds__(kThreads) void k_running(RunJobs jobs) {
   }
 }
 
-// tuning knob: channels per small-layer workgroup (16 / 32 / 64)
-int small_ch() {
-  static const int ch = [] {
-    const char* e = std::getenv("GARFIELD_BN_SMALL_CH");
-    const int v = e ? std::atoi(e) : 0;
-    return (v == 16 || v == 64) ? v : 32;
-  }();
-  return ch;
-}
-
-template <int CH>
-void launch_fwd_small(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
-                      const float* beta, float eps, float* mean, float* istd, float* scale, float* shift, uint16_t* y,
+template <int CH, int DT>
+void launch_fwd_small(const void* x, const void* res, int64_t rg, int groups, int C, const float* gamma,
+                      const float* beta, float eps, float* mean, float* istd, float* scale, float* shift, void* y,
                       bool relu, uint8_t* mask, hipStream_t stream) {
   const dim3 sgrid((C + CH - 1) / CH, groups);
   if (res) {
-    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, true, true>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
-    else hipLaunchKernelGGL((k_bn_fwd_small<CH, true, false>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, true, true, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
+    else hipLaunchKernelGGL((k_bn_fwd_small<CH, true, false, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
   } else {
-    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, false, true>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
-    else hipLaunchKernelGGL((k_bn_fwd_small<CH, false, false>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, false, true, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
+    else hipLaunchKernelGGL((k_bn_fwd_small<CH, false, false, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
   }
 }
 
-template <int CH>
-void launch_bwd_small(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const uint8_t* mask, int64_t rg,
-                      int groups, int C, const float* gamma, const float* mean, const float* istd, uint16_t* dx,
-                      uint16_t* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
+template <int CH, int DT>
+void launch_bwd_small(const void* x, const void* dy, const void* y, const uint8_t* mask, int64_t rg,
+                      int groups, int C, const float* gamma, const float* mean, const float* istd, void* dx,
+                      void* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
                       int rm, hipStream_t stream) {
   const dim3 sgrid((C + CH - 1) / CH, groups);
 #define GARFIELD_BWD_SMALL(RMV, RESV)                                                                           \
-  hipLaunchKernelGGL((k_bn_bwd_small<CH, RMV, RESV>), sgrid, dim3(kSmallThreads), 0, stream, x, dy, y, mask, rg, C, \
+  hipLaunchKernelGGL((k_bn_bwd_small<CH, RMV, RESV, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, dy, y, mask, rg, C, \
                      gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta)
   if (rm == 2) { if (dres) GARFIELD_BWD_SMALL(2, true); else GARFIELD_BWD_SMALL(2, false); }
   else if (rm == 1) { if (dres) GARFIELD_BWD_SMALL(1, true); else GARFIELD_BWD_SMALL(1, false); }
@@ -751,23 +789,14 @@ void launch_bwd_small(const uint16_t* x, const uint16_t* dy, const uint16_t* y, 
 #undef GARFIELD_BWD_SMALL
 }
 
-}  // namespace
-
-int64_t bn_part_floats(int64_t rg, int groups, int C) {
-  const Geo g = geometry(rg, groups, C);
-  return static_cast<int64_t>(groups) * g.chunks * 2 * C;
-}
-
-void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, int C, const float* gamma,
+template <int DT>
+void forward_dt(const void* x, const void* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
-                float* mean, float* istd, float* scale, float* shift, uint16_t* y, bool relu, uint8_t* mask,
-                bool defer_running, hipStream_t stream, const float* tile_stats, int64_t tile_m,
-                int tile_e) {
+                float* mean, float* istd, float* scale, float* shift, void* y, bool relu, uint8_t* mask,
+                bool defer_running, hipStream_t stream, const float* tile_stats, int64_t tile_m, int tile_e) {
   if (rg <= kSmallRows && tile_stats == nullptr) {
-    const int ch = small_ch();
-    if (ch == 16) launch_fwd_small<16>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream);
-    else if (ch == 64) launch_fwd_small<64>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream);
-    else launch_fwd_small<32>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream);
+    // 32 channels per workgroup (16 / 64 measured slower: profiles/r2/bn_small_ch_sweep.log)
+    launch_fwd_small<32, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream);
     if (run_mean && !defer_running) {
       RunJobs jobs{};
       jobs.j[0] = RunJob{mean, istd, run_mean, run_var, rg, C, groups, eps, momentum};
@@ -782,10 +811,10 @@ void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, 
   } else {
     const Geo g = geometry(rg, groups, C);
     const int ncb = (C + g.cb - 1) / g.cb;
-    hipLaunchKernelGGL((k_partial<false, 0>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
+    hipLaunchKernelGGL((k_partial<false, 0, DT>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
                        nullptr, nullptr, nullptr, g, part);
     const dim3 fgrid((C + kFinCh - 1) / kFinCh, groups);
-    hipLaunchKernelGGL(k_fwd_finalize, fgrid, dim3(kThreads), 0, stream, part, x, g, gamma, beta, eps, mean, istd,
+    hipLaunchKernelGGL((k_fwd_finalize<DT>), fgrid, dim3(kThreads), 0, stream, part, x, g, gamma, beta, eps, mean, istd,
                        scale, shift);
   }
   const RunStats rs{mean, istd, run_mean, run_var, eps, momentum, groups};
@@ -794,32 +823,30 @@ void bn_forward(const uint16_t* x, const uint16_t* res, int64_t rg, int groups, 
   const int64_t R = rg * groups;
   const dim3 grid = apply_grid(R, rp);
   if (res) {
-    if (relu) hipLaunchKernelGGL((k_fwd_apply<true, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, mask, rs);
-    else hipLaunchKernelGGL((k_fwd_apply<true, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, nullptr, rs);
+    if (relu) hipLaunchKernelGGL((k_fwd_apply<true, true, DT>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, mask, rs);
+    else hipLaunchKernelGGL((k_fwd_apply<true, false, DT>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, nullptr, rs);
   } else {
-    if (relu) hipLaunchKernelGGL((k_fwd_apply<false, true>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, mask, rs);
-    else hipLaunchKernelGGL((k_fwd_apply<false, false>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, nullptr, rs);
+    if (relu) hipLaunchKernelGGL((k_fwd_apply<false, true, DT>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, mask, rs);
+    else hipLaunchKernelGGL((k_fwd_apply<false, false, DT>), grid, dim3(kThreads), 0, stream, x, res, scale, shift, rg, R, C, tch, rp, y, nullptr, rs);
   }
 }
 
-void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const uint8_t* mask, int64_t rg, int groups,
-                 int C, const float* gamma, const float* mean, const float* istd, float* part, float* coef, uint16_t* dx,
-                 uint16_t* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
+template <int DT>
+void backward_dt(const void* x, const void* dy, const void* y, const uint8_t* mask, int64_t rg, int groups,
+                 int C, const float* gamma, const float* mean, const float* istd, float* part, float* coef, void* dx,
+                 void* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
                  hipStream_t stream) {
   const int rm = mask ? 2 : (y ? 1 : 0);
   if (rg <= kSmallRows) {
-    const int ch = small_ch();
-    if (ch == 16) launch_bwd_small<16>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream);
-    else if (ch == 64) launch_bwd_small<64>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream);
-    else launch_bwd_small<32>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream);
+    launch_bwd_small<32, DT>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream);
     return;
   }
   const Geo g = geometry(rg, groups, C);
   const int ncb = (C + g.cb - 1) / g.cb;
   const dim3 pgrid(g.chunks, ncb, groups);
-  if (rm == 2) hipLaunchKernelGGL((k_partial<true, 2>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
-  else if (rm == 1) hipLaunchKernelGGL((k_partial<true, 1>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
-  else hipLaunchKernelGGL((k_partial<true, 0>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
+  if (rm == 2) hipLaunchKernelGGL((k_partial<true, 2, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
+  else if (rm == 1) hipLaunchKernelGGL((k_partial<true, 1, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
+  else hipLaunchKernelGGL((k_partial<true, 0, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
   hipLaunchKernelGGL(k_bwd_finalize, dim3((C + kFinCh - 1) / kFinCh, groups), dim3(kThreads), 0, stream, part, g,
                      gamma, istd, coef, grow, grow_dt, row_stride, off_gamma, off_beta);
   int tch, rp;
@@ -827,11 +854,43 @@ void bn_backward(const uint16_t* x, const uint16_t* dy, const uint16_t* y, const
   const int64_t R = rg * groups;
   const dim3 grid = apply_grid(R, rp);
 #define GARFIELD_BWD_APPLY(RMV, RESV) \
-  hipLaunchKernelGGL((k_bwd_apply<RMV, RESV>), grid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, coef, rg, R, C, tch, rp, dx, dres)
+  hipLaunchKernelGGL((k_bwd_apply<RMV, RESV, DT>), grid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, coef, rg, R, C, tch, rp, dx, dres)
   if (rm == 2) { if (dres) GARFIELD_BWD_APPLY(2, true); else GARFIELD_BWD_APPLY(2, false); }
   else if (rm == 1) { if (dres) GARFIELD_BWD_APPLY(1, true); else GARFIELD_BWD_APPLY(1, false); }
   else { if (dres) GARFIELD_BWD_APPLY(0, true); else GARFIELD_BWD_APPLY(0, false); }
 #undef GARFIELD_BWD_APPLY
+}
+
+}  // namespace
+
+int64_t bn_part_floats(int64_t rg, int groups, int C) {
+  const Geo g = geometry(rg, groups, C);
+  return static_cast<int64_t>(groups) * g.chunks * 2 * C;
+}
+
+void bn_forward(const void* x, const void* res, int64_t rg, int groups, int C, const float* gamma,
+                const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
+                float* mean, float* istd, float* scale, float* shift, void* y, bool relu, uint8_t* mask,
+                bool defer_running, hipStream_t stream, const float* tile_stats, int64_t tile_m,
+                int tile_e, int dt) {
+  if (dt == kF32)
+    forward_dt<kF32>(x, res, rg, groups, C, gamma, beta, eps, momentum, run_mean, run_var, part, mean, istd, scale,
+                     shift, y, relu, mask, defer_running, stream, tile_stats, tile_m, tile_e);
+  else
+    forward_dt<kBF16>(x, res, rg, groups, C, gamma, beta, eps, momentum, run_mean, run_var, part, mean, istd, scale,
+                      shift, y, relu, mask, defer_running, stream, tile_stats, tile_m, tile_e);
+}
+
+void bn_backward(const void* x, const void* dy, const void* y, const uint8_t* mask, int64_t rg, int groups,
+                 int C, const float* gamma, const float* mean, const float* istd, float* part, float* coef, void* dx,
+                 void* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
+                 hipStream_t stream, int dt) {
+  if (dt == kF32)
+    backward_dt<kF32>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, part, coef, dx, dres, grow, grow_dt, row_stride,
+                      off_gamma, off_beta, stream);
+  else
+    backward_dt<kBF16>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, part, coef, dx, dres, grow, grow_dt,
+                       row_stride, off_gamma, off_beta, stream);
 }
 
 void bn_running_update(const RunJobs& jobs, hipStream_t stream) {

@@ -405,7 +405,6 @@ void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, const Halo& h
 
 constexpr int kNuBig = 14;    // PMF 4: 14 x 4 KB halo + 3 x 8 KB ring = 80 KB (two workgroups per CU)
 constexpr int kNuSmall = 10;  // PMF 2: 40 + 24 = 64 KB
-constexpr int kNuS2 = 12;     // stride 2, PMF 1: 48 + 24 = 72 KB (9 x 33, 17 x 17, 4 x 9 x 9 staged pixels)
 
 // ---------------------------------------------------------------------------------------------
 // Per-worker weight gradient of the same convolutions, halo-staged:
@@ -608,17 +607,9 @@ int conv3x3_pick(const Im2col& g, int Cout) {
   if (g.KH != 3 || g.KW != 3 || g.ph != 1 || g.pw != 1 || g.dh != 1 || g.dw != 1 || g.C % 64 || Cout % 64)
     return 0;
   Halo hp;
-  if (g.sh == 2 && g.sw == 2) {   // downsampling: 64-pixel tiles (the halo is ~4x the output tile)
-    // off by default: 222 vs 176 us per ResNet-18 downsampling layer against the implicit-GEMM
-    // kernel (one 16-pixel fragment per wave re-reads four weight fragments per MFMA pair, and the
-    // stride-2 B rows hit 2-way bank conflicts); GARFIELD_CONV3X3_S2=1 enables it
-    static const bool s2 = [] {
-      const char* e = std::getenv("GARFIELD_CONV3X3_S2");
-      return e && e[0] == '1';
-    }();
-    if (!s2 || g.H != 2 * g.Ho || g.W != 2 * g.Wo) return 0;
-    return plan(g, 1, kNuS2, hp) ? 1 : 0;
-  }
+  // stride 2 stays on the implicit-GEMM kernel: a halo-staged stride-2 variant measured 222 vs 176 us
+  // per ResNet-18 downsampling layer (one 16-pixel fragment per wave re-reads four weight fragments per
+  // MFMA pair, and the stride-2 B rows hit 2-way bank conflicts) and was removed
   if (g.sh != 1 || g.sw != 1 || g.Ho != g.H || g.Wo != g.W) return 0;
   if (plan(g, 4, kNuBig, hp)) return 4;
   if (plan(g, 2, kNuSmall, hp)) return 2;
@@ -636,14 +627,6 @@ int cu_count() {
   return n;
 }
 
-// GARFIELD_CONV3X3_RES=0 keeps the one-shot kernel for 64-channel inputs
-bool res_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("GARFIELD_CONV3X3_RES");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 }  // namespace
 
 bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
@@ -651,7 +634,7 @@ bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cou
   if (pmf <= 0) pmf = conv3x3_pick(g, Cout);
   if (stats && (add || rg < 16 * pmf)) return false;
   Halo hp;
-  if (pmf == 4 && g.C == 64 && res_enabled() && conv3x3_pick(g, Cout) == 4 && plan(g, 4, kNuRes, hp)) {
+  if (pmf == 4 && g.C == 64 && conv3x3_pick(g, Cout) == 4 && plan(g, 4, kNuRes, hp)) {
     const int tiles = (g.N * g.H + hp.TR - 1) / hp.TR;
     int gx = cu_count() / (Cout / 64);
     gx = gx < 1 ? 1 : (gx > tiles ? tiles : gx);
@@ -675,10 +658,6 @@ bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cou
   }
   if (pmf == 2 && pick && s1 && plan(g, 2, kNuSmall, hp)) {
     launch<2, kNuSmall>(x, w, g, hp, Cout, y, add, stats, rg, stream);
-    return true;
-  }
-  if (pmf == 1 && pick == 1 && plan(g, 1, kNuS2, hp)) {
-    launch<1, kNuS2>(x, w, g, hp, Cout, y, add, stats, rg, stream);
     return true;
   }
   return false;

@@ -1,0 +1,830 @@
+// fp32 NHWC convolutions for the reference-precision grouped step, on bf16 MFMA (gfx950).
+//
+// The reference trains in fp32 (pytorch_impl/applications/Garfield_CC/trainer.py:296-303, no
+// autocast). gfx950 has no xf32 MFMA and its f32-input MFMA runs at the f32 vector rate (1/16 of
+// bf16: 157 TF/s), so an fp32 product is formed from bf16 pieces: every fp32 operand is split as
+//   v = v0 + v1 + v2 + r,  v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 - v1),  |r| <~ 2^-27 |v|
+// and a·b ≈ Σ_{i + j <= 2} a_i·b_j (a0b0 + a0b1 + a1b0 + a0b2 + a2b0 + a1b1; the dropped terms are
+// ~2^-26 of the product, under fp32's own rounding): six v_mfma_f32_16x16x32_bf16 with fp32
+// accumulation, 96 cycles per 16x16x32 block against 256 for the f32 MFMA. Two pieces (three
+// products) leave ~2^-17 per product, which a BatchNorm network's backward (cancellation in
+// dz - mean(dz) - x̂·mean(dz·x̂)) amplifies to ~1e-2 of the gradient: not the reference's precision.
+// Activations stay fp32 in HBM; the weights are split once per step (k_wsplit: W -> the three
+// pieces [3][Cout][K] and the channel-transposed pieces [3][Cin][KH][KW][Cout] of the data gradient).
+//
+// * k_cf32_conv: implicit-GEMM convolution y[m, co] = Σ_{tap, c} src[pixel(m, tap), c] · A[co, tap, c]
+//   (+ add). Forward: src = x, A = W [Cout][KH][KW][Cin]. Data gradient (DG): src = dy, A = Wt
+//   [Cin][KH][KW][Cout], and input pixel (h, w) gathers dy[(h + ph - i·dh) / sh, (w + pw - j·dw) / sw]
+//   where the division is exact (the transposed convolution; any stride). The weight is the
+//   MFMA A operand (a lane holds 8 consecutive k of one output channel: 16 bytes of each piece),
+//   the activation the B operand (8 consecutive channels of one pixel: two float4 loads, split in
+//   registers); the loads of k-step s + 1 are in flight while step s multiplies. Workgroup: 4 waves
+//   x 16·PM pixels x 64 output channels.
+// * k_cf32_wgrad: per-worker weight gradient dW_g[co, (tap, ci)] = Σ_{m in worker g} dy[m, co] ·
+//   x[pixel(m, tap), ci]: the reduction runs over pixels, so both operands are staged (fp32 ->
+//   split in registers -> [32 pixel][64 channel] bf16 piece tiles in LDS, double-buffered) and read
+//   with ds_read_b64_tr_b16 (16 lanes gather 4 rows x 16 columns). Tile: 64 co x 64 k, 32 pixels
+//   per k-step, the worker's pixels optionally split into `splits` fp32 slabs.
+// * k_f32_linear_*: the classifier (per-worker dW, db straight into the exchange rows), and the
+//   global average pool: VALU kernels (tens of MFLOP), so the fp32 step runs no library GEMM.
+#include "bn_gpu.hpp"
+#include "conv_f32.hpp"
+#include "gar_device.hpp"
+
+namespace garfield {
+namespace gpu {
+using namespace dev;
+namespace {
+
+using lds_ptr = __attribute__((address_space(3))) void*;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kNP = 3;   // bf16 pieces per fp32 value
+
+// (a, b) -> three packed bf16 pairs p[0..2] with a ≈ Σ p_i.lo, b ≈ Σ p_i.hi
+__device__ __forceinline__ void split2(float a, float b, uint32_t (&p)[kNP]) {
+#pragma unroll
+  for (int i = 0; i < kNP; ++i) {
+    p[i] = pack_bf16x2(a, b);
+    a -= __uint_as_float(p[i] << 16);
+    b -= __uint_as_float(p[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8 (&v)[kNP]) {
+  uint32_t q[4][kNP];
+  split2(a.x, a.y, q[0]);
+  split2(a.z, a.w, q[1]);
+  split2(b.x, b.y, q[2]);
+  split2(b.z, b.w, q[3]);
+#pragma unroll
+  for (int i = 0; i < kNP; ++i) v[i] = __builtin_bit_cast(bf16x8, make_uint4(q[0][i], q[1][i], q[2][i], q[3][i]));
+}
+
+// acc += Σ_{i + j <= 2} a_i · b_j, the small terms first
+__device__ __forceinline__ f32x4 mma6(const bf16x8 (&a)[kNP], const bf16x8 (&b)[kNP], f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// implicit-GEMM convolution
+
+template <int PM>
+struct Step {
+  bf16x8 a[4][kNP];
+  float4 b0[PM], b1[PM];
+};
+
+// GATHER (a forward over Cs % 32 != 0 channels, e.g. the 3-channel CIFAR stem): the reduction
+// runs over the flattened (tap, channel) index k < K padded to Kp = 32·steps, each lane gathering its
+// 8 consecutive k one element at a time; the weight rows are [Co][Kp] (zero padding).
+template <int PM, bool DG, bool ADD, bool GATHER>
+__global__ __launch_bounds__(256) void k_cf32_conv(const float* __restrict__ src, const uint16_t* __restrict__ w3,
+                                                   ConvF32Geo g, float* __restrict__ out, const float* __restrict__ add) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pl = lane & 15, kq = lane >> 4;
+  const int M = g.N * g.Ho * g.Wo;
+  const int Kr = g.KH * g.KW * g.Cs;                        // real reduction length
+  const int K = GATHER ? (Kr + 31) / 32 * 32 : Kr;          // weight row stride
+  const int m0 = blockIdx.x * (64 * PM) + wave * 16 * PM;
+  const int co0 = blockIdx.y * 64;
+
+  int hb[PM], wb[PM], nb[PM];
+  bool pv[PM];
+#pragma unroll
+  for (int r = 0; r < PM; ++r) {
+    const int m = m0 + r * 16 + pl;
+    pv[r] = m < M;
+    const int mm = pv[r] ? m : 0;
+    const int wo = mm % g.Wo;
+    const int t = mm / g.Wo;
+    const int ho = t % g.Ho;
+    nb[r] = t / g.Ho;
+    if constexpr (DG) {
+      hb[r] = ho + g.ph;
+      wb[r] = wo + g.pw;
+    } else {
+      hb[r] = ho * g.sh - g.ph;
+      wb[r] = wo * g.sw - g.pw;
+    }
+  }
+  // w3: the weight's three pieces [3][Co][K]
+  const int64_t piece = static_cast<int64_t>(g.Co) * K;
+  const uint16_t* wp[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) wp[c] = w3 + static_cast<int64_t>(co0 + c * 16 + pl) * K + kq * 8;
+  const int csteps = GATHER ? 1 : g.Cs / 32;
+  const int steps = GATHER ? K / 32 : g.KH * g.KW * csteps;
+
+  auto load = [&](int s, Step<PM>& f) {
+    const int tap = s / csteps;
+    const int c0 = (s - tap * csteps) * 32;
+    const int i = tap / g.KW, j = tap - (tap / g.KW) * g.KW;
+    const int koff = GATHER ? s * 32 : tap * g.Cs + c0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < kNP; ++i) f.a[c][i] = *reinterpret_cast<const bf16x8*>(wp[c] + i * piece + koff);
+    if constexpr (GATHER) {
+#pragma unroll
+      for (int r = 0; r < PM; ++r) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = s * 32 + kq * 8 + e;
+          const int tp = k / g.Cs, ch = k - tp * g.Cs;
+          const int ti = tp / g.KW, tj = tp - ti * g.KW;
+          const int hs = hb[r] + ti * g.dh, ws = wb[r] + tj * g.dw;
+          const bool ok = pv[r] && k < Kr && hs >= 0 && hs < g.Hs && ws >= 0 && ws < g.Ws;
+          const int64_t pix = (static_cast<int64_t>(nb[r]) * g.Hs + (ok ? hs : 0)) * g.Ws + (ok ? ws : 0);
+          const float a = src[pix * g.Cs + (ok ? ch : 0)];
+          v[e] = ok ? a : 0.f;
+        }
+        f.b0[r] = make_float4(v[0], v[1], v[2], v[3]);
+        f.b1[r] = make_float4(v[4], v[5], v[6], v[7]);
+      }
+      return;
+    }
+#pragma unroll
+    for (int r = 0; r < PM; ++r) {
+      int hs, ws;
+      bool ok;
+      if constexpr (DG) {
+        const int th = hb[r] - i * g.dh, tw = wb[r] - j * g.dw;
+        hs = th / g.sh;
+        ws = tw / g.sw;
+        ok = pv[r] && th >= 0 && tw >= 0 && hs * g.sh == th && ws * g.sw == tw && hs < g.Hs && ws < g.Ws;
+      } else {
+        hs = hb[r] + i * g.dh;
+        ws = wb[r] + j * g.dw;
+        ok = pv[r] && hs >= 0 && hs < g.Hs && ws >= 0 && ws < g.Ws;
+      }
+      const int64_t pix = (static_cast<int64_t>(nb[r]) * g.Hs + (ok ? hs : 0)) * g.Ws + (ok ? ws : 0);
+      const float* p = src + pix * g.Cs + c0 + kq * 8;
+      const float4 a = *reinterpret_cast<const float4*>(p);
+      const float4 b = *reinterpret_cast<const float4*>(p + 4);
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      f.b0[r] = ok ? a : z;
+      f.b1[r] = ok ? b : z;
+    }
+  };
+
+  f32x4 acc[PM][4];
+#pragma unroll
+  for (int r = 0; r < PM; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Step<PM> cur, nxt;
+  load(0, cur);
+  for (int s = 0; s < steps; ++s) {
+    if (s + 1 < steps) load(s + 1, nxt);
+#pragma unroll
+    for (int r = 0; r < PM; ++r) {
+      bf16x8 b[kNP];
+      split8(cur.b0[r], cur.b1[r], b);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = mma6(cur.a[c], b, acc[r][c]);
+    }
+    cur = nxt;
+  }
+
+  // D[co = 4*kq + e][pixel = pl]: four consecutive output channels of one pixel per lane
+#pragma unroll
+  for (int r = 0; r < PM; ++r) {
+    if (!pv[r]) continue;
+    const int64_t rowoff = static_cast<int64_t>(m0 + r * 16 + pl) * g.Co;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t off = rowoff + co0 + c * 16 + kq * 4;
+      float4 v = make_float4(acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]);
+      if constexpr (ADD) {
+        const float4 a = *reinterpret_cast<const float4*>(add + off);
+        v.x += a.x;
+        v.y += a.y;
+        v.z += a.z;
+        v.w += a.w;
+      }
+      *reinterpret_cast<float4*>(out + off) = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-staged implicit-GEMM convolution (Cs % 32 == 0): every k-step (one tap, 32 source channels)
+// stages the three weight pieces [3][64 co][32 k] bf16 and the activation tile [64·PM pixels][32
+// channels] fp32 by global_load_lds (no VGPR round trip; chunks XOR-swizzled on the global side so
+// the fragment reads below spread over the banks) through an NS-deep ring: NS-1 k-steps of loads in
+// flight. A wave reads its B fragments as fp32 (two ds_read_b128) and splits them in registers.
+// Data gradient of a strided convolution: the output pixels are processed in parity classes
+// (blockIdx.z = (h mod sh, w mod sw)); a class gathers dy only through the taps that hit it
+// (i ≡ h + ph mod sh), so no MFMA is spent on the zero taps of the transposed convolution
+// (9 taps over the 4 classes of a 3x3 / stride-2 layer, not 36).
+
+__device__ __attribute__((aligned(16))) float g_cf32_zero[8];   // 32 zero bytes: source of padded taps
+
+template <int PM, int NS, bool DG, bool ADD>
+__global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__ src, const uint16_t* __restrict__ w3,
+                                                       ConvF32Geo g, float* __restrict__ out,
+                                                       const float* __restrict__ add) {
+  constexpr int BM = 64 * PM;
+  constexpr int WB = kNP * 64 * 64;     // weight pieces per stage (bytes): 3 x 64 rows x 64 B
+  constexpr int XB = BM * 128;          // activation tile per stage (bytes): BM rows x 128 B
+  constexpr int SB = WB + XB;
+  constexpr int WI = WB / 1024 / 4;     // glds per wave per stage: weights (3)
+  constexpr int XI = XB / 1024 / 4;     // ... activations (2 PM)
+  constexpr int PER = WI + XI;
+  __shared__ __attribute__((aligned(16))) char lds[NS * SB];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = g.KH * g.KW * g.Cs;
+  // parity class of this workgroup's output pixels (data gradient of a strided convolution)
+  const int csh = DG ? g.sh : 1, csw = DG ? g.sw : 1;
+  const int ca = DG ? static_cast<int>(blockIdx.z) / g.sw : 0, cb = DG ? static_cast<int>(blockIdx.z) % g.sw : 0;
+  const int Hc = (g.Ho - ca + csh - 1) / csh, Wc = (g.Wo - cb + csw - 1) / csw;
+  const int Mc = g.N * Hc * Wc;
+  const int m0 = blockIdx.x * BM;
+  if (m0 >= Mc) return;   // whole workgroup (a class with fewer pixels than the grid covers)
+  const int co0 = blockIdx.y * 64;
+  // taps of this class: i = ti0 + t * tstep_i (forward: every tap)
+  int ti0 = 0, tj0 = 0, tsi = 1, tsj = 1;
+  if constexpr (DG) {
+    ti0 = (ca + g.ph) % g.sh;
+    tj0 = (cb + g.pw) % g.sw;
+    tsi = g.sh;
+    tsj = g.sw;
+  }
+  const int ni = ti0 < g.KH ? (g.KH - ti0 + tsi - 1) / tsi : 0;
+  const int nj = tj0 < g.KW ? (g.KW - tj0 + tsj - 1) / tsj : 0;
+  const int csteps = g.Cs / 32;
+  const int steps = ni * nj * csteps;
+
+  // this lane's activation rows: rows (wave * XI + u) * 8 + lane / 8 of the tile, chunk lane % 8
+  const int xr = lane >> 3, xc = lane & 7;
+  int xh[XI], xw[XI], xn[XI];
+  bool xv[XI];
+#pragma unroll
+  for (int u = 0; u < XI; ++u) {
+    const int row = (wave * XI + u) * 8 + xr;
+    const int m = m0 + row;
+    xv[u] = m < Mc;
+    const int mm = xv[u] ? m : 0;
+    const int wc = mm % Wc;
+    const int t = mm / Wc;
+    const int hc = t % Hc;
+    xn[u] = t / Hc;
+    if constexpr (DG) {   // source dy row of tap i: hc + (ca + ph - i) / sh (exact in this class)
+      xh[u] = hc;
+      xw[u] = wc;
+    } else {
+      xh[u] = hc * g.sh - g.ph;
+      xw[u] = wc * g.sw - g.pw;
+    }
+  }
+  const int xsw = 2 * ((xr >> 1) & 3);          // chunk swizzle of the activation rows (even: pairs stay adjacent)
+  // weight rows: glds block q covers rows 16 q .. 16 q + 15 of one piece, lane -> row lane / 4, chunk lane % 4
+  const int wr = lane >> 2, wcn = lane & 3;
+  const int64_t piece = static_cast<int64_t>(g.Co) * K;
+  const uint16_t* wsrc[WI];
+#pragma unroll
+  for (int u = 0; u < WI; ++u) {
+    const int q = wave * WI + u;                 // 0 .. 11: piece q / 4, rows 16 (q % 4) + wr
+    const int row = 16 * (q & 3) + wr;
+    wsrc[u] = w3 + (q >> 2) * piece + static_cast<int64_t>(co0 + row) * K + ((wcn ^ ((row >> 2) & 3)) * 8);
+  }
+  const uint64_t az = reinterpret_cast<uint64_t>(g_cf32_zero);
+
+  auto issue = [&](int s, int slot) {
+    const int tap = s / csteps;
+    const int c0 = (s - tap * csteps) * 32;
+    const int ti = tap / nj, tj = tap - (tap / nj) * nj;
+    const int i = ti0 + ti * tsi, j = tj0 + tj * tsj;
+    char* base = lds + slot * SB;
+    const int koff = (i * g.KW + j) * g.Cs + c0;
+#pragma unroll
+    for (int u = 0; u < WI; ++u)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(wsrc[u] + koff),
+                                       (lds_ptr)(base + (wave * WI + u) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int u = 0; u < XI; ++u) {
+      int hs, ws;
+      if constexpr (DG) {
+        hs = xh[u] + (ca + g.ph - i) / g.sh;
+        ws = xw[u] + (cb + g.pw - j) / g.sw;
+      } else {
+        hs = xh[u] + i * g.dh;
+        ws = xw[u] + j * g.dw;
+      }
+      const bool ok = xv[u] && hs >= 0 && hs < g.Hs && ws >= 0 && ws < g.Ws;
+      const int hc = ok ? hs : 0, wc = ok ? ws : 0;
+      const uint64_t ax = reinterpret_cast<uint64_t>(
+          src + ((static_cast<int64_t>(xn[u]) * g.Hs + hc) * g.Ws + wc) * g.Cs + c0 + (xc ^ xsw) * 4);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? ax : az),
+                                       (lds_ptr)(base + WB + (wave * XI + u) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[PM][4];
+#pragma unroll
+  for (int r = 0; r < PM; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < steps) issue(s0, s0);
+  for (int s = 0; s < steps; ++s) {
+    const int ahead = (steps - 1 - s) < (NS - 2) ? (steps - 1 - s) : (NS - 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
+    const char* base = lds + (s % NS) * SB;
+    bf16x8 a[4][kNP];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int row = c * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < kNP; ++i)
+        a[c][i] = *reinterpret_cast<const bf16x8*>(base + i * 4096 + row * 64 + ((fq ^ ((row >> 2) & 3)) * 16));
+    }
+#pragma unroll
+    for (int r = 0; r < PM; ++r) {
+      const int row = (wave * PM + r) * 16 + fr;
+      const int ch = (2 * fq) ^ (2 * ((row >> 1) & 3));
+      const float4 v0 = *reinterpret_cast<const float4*>(base + WB + row * 128 + ch * 16);
+      const float4 v1 = *reinterpret_cast<const float4*>(base + WB + row * 128 + ch * 16 + 16);
+      bf16x8 b[kNP];
+      split8(v0, v1, b);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = mma6(a[c], b, acc[r][c]);
+    }
+    // every wave's fragment reads of this slot retire before the barrier that lets it be refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  // D[co = 4*fq + e][pixel = fr]: four consecutive output channels of one pixel per lane
+#pragma unroll
+  for (int r = 0; r < PM; ++r) {
+    const int m = m0 + (wave * PM + r) * 16 + fr;
+    if (m >= Mc) continue;
+    const int wc = m % Wc;
+    const int t = m / Wc;
+    const int hc = t % Hc, n = t / Hc;
+    const int64_t pix = (static_cast<int64_t>(n) * g.Ho + hc * csh + ca) * g.Wo + wc * csw + cb;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t off = pix * g.Co + co0 + c * 16 + fq * 4;
+      float4 v = make_float4(acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]);
+      if constexpr (ADD) {
+        const float4 a4 = *reinterpret_cast<const float4*>(add + off);
+        v.x += a4.x;
+        v.y += a4.y;
+        v.z += a4.z;
+        v.w += a4.w;
+      }
+      *reinterpret_cast<float4*>(out + off) = v;
+    }
+  }
+}
+
+template <int PM, int NS, bool DG>
+void launch_conv_lds(const float* src, const uint16_t* w3, const ConvF32Geo& g, float* out, const float* add,
+                     hipStream_t stream) {
+  const int csh = DG ? g.sh : 1, csw = DG ? g.sw : 1;
+  const int Mc = g.N * ((g.Ho + csh - 1) / csh) * ((g.Wo + csw - 1) / csw);   // the largest class (0, 0)
+  const dim3 grid((Mc + 64 * PM - 1) / (64 * PM), g.Co / 64, csh * csw);
+  if (add) hipLaunchKernelGGL((k_cf32_conv_lds<PM, NS, DG, true>), grid, dim3(256), 0, stream, src, w3, g, out, add);
+  else hipLaunchKernelGGL((k_cf32_conv_lds<PM, NS, DG, false>), grid, dim3(256), 0, stream, src, w3, g, out, add);
+}
+
+template <int PM, bool DG>
+void launch_conv(const float* src, const uint16_t* w3, const ConvF32Geo& g, float* out, const float* add,
+                 hipStream_t stream) {
+  const int M = g.N * g.Ho * g.Wo;
+  const dim3 grid((M + 64 * PM - 1) / (64 * PM), g.Co / 64);
+  if (!DG && g.Cs % 32 != 0) {
+    if (add) hipLaunchKernelGGL((k_cf32_conv<PM, false, true, true>), grid, dim3(256), 0, stream, src, w3, g, out, add);
+    else hipLaunchKernelGGL((k_cf32_conv<PM, false, false, true>), grid, dim3(256), 0, stream, src, w3, g, out, add);
+    return;
+  }
+  if (add) hipLaunchKernelGGL((k_cf32_conv<PM, DG, true, false>), grid, dim3(256), 0, stream, src, w3, g, out, add);
+  else hipLaunchKernelGGL((k_cf32_conv<PM, DG, false, false>), grid, dim3(256), 0, stream, src, w3, g, out, add);
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-worker weight gradient
+
+constexpr int kTB = 32 * 128;          // one [32 pixel][64 channel] bf16 tile
+constexpr int kSB = 2 * kNP * kTB;     // dy pieces 0..2 | x pieces 0..2
+
+// GATHER (Cs % 64 != 0, e.g. the 3-channel CIFAR stem): k-blocks of 64 consecutive flattened
+// (tap, channel) indices (K padded to a multiple of 64, the padding never stored), the x tile gathered
+// one element at a time.
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x, const float* __restrict__ dy,
+                                                    ConvF32Geo g, int64_t rg, int64_t per_split, float* __restrict__ out,
+                                                    int64_t split_stride, int64_t group_stride) {
+  // g: the forward geometry (Hs/Ws/Cs = x's, Ho/Wo/Co = dy's)
+  __shared__ __attribute__((aligned(16))) char lds[2 * kSB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = g.KH * g.KW * g.Cs;
+  const int nkb = (K + 63) / 64;
+  const int kb = blockIdx.x % nkb, cb = blockIdx.x / nkb;
+  const int gi = blockIdx.y, sp = blockIdx.z;
+  const int k0 = kb * 64, co0 = cb * 64;
+  const int tap = k0 / g.Cs, c0 = k0 - tap * g.Cs;
+  const int ti = tap / g.KW, tj = tap - ti * g.KW;
+  const int64_t mbeg = static_cast<int64_t>(gi) * rg + static_cast<int64_t>(sp) * per_split;
+  int64_t mend = mbeg + per_split;
+  if (mend > static_cast<int64_t>(gi + 1) * rg) mend = static_cast<int64_t>(gi + 1) * rg;
+  const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
+
+  // staging: thread t owns rows (t >> 4) and (t >> 4) + 16 of the step's 32 pixels, channels 4 (t & 15) .. +3
+  const int srow = threadIdx.x >> 4, sch = threadIdx.x & 15;
+  float4 rd[2], rx[2];
+  auto load = [&](int s) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t m = mbeg + static_cast<int64_t>(s) * 32 + srow + 16 * h;
+      const bool mv = m < mend;
+      const int64_t mm = mv ? m : 0;
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 d = *reinterpret_cast<const float4*>(dy + mm * g.Co + co0 + sch * 4);
+      rd[h] = mv ? d : z;
+      const int wo = static_cast<int>(mm % g.Wo);
+      const int64_t t = mm / g.Wo;
+      const int ho = static_cast<int>(t % g.Ho);
+      const int64_t n = t / g.Ho;
+      if constexpr (GATHER) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = k0 + sch * 4 + e;
+          const int tp = k / g.Cs, ch = k - tp * g.Cs;
+          const int ki = tp / g.KW, kj = tp - ki * g.KW;
+          const int hi = ho * g.sh - g.ph + ki * g.dh, wi = wo * g.sw - g.pw + kj * g.dw;
+          const bool ok = mv && k < K && hi >= 0 && hi < g.Hs && wi >= 0 && wi < g.Ws;
+          const float a = x[((n * g.Hs + (ok ? hi : 0)) * g.Ws + (ok ? wi : 0)) * g.Cs + (ok ? ch : 0)];
+          v[e] = ok ? a : 0.f;
+        }
+        rx[h] = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        const int hi = ho * g.sh - g.ph + ti * g.dh, wi = wo * g.sw - g.pw + tj * g.dw;
+        const bool ok = mv && hi >= 0 && hi < g.Hs && wi >= 0 && wi < g.Ws;
+        const float4 v = *reinterpret_cast<const float4*>(
+            x + ((n * g.Hs + (ok ? hi : 0)) * g.Ws + (ok ? wi : 0)) * g.Cs + c0 + sch * 4);
+        rx[h] = ok ? v : z;
+      }
+    }
+  };
+  auto stage = [&](int slot) {
+    char* base = lds + slot * kSB;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int off = (srow + 16 * h) * 128 + sch * 8;
+      uint32_t p0[kNP], p1[kNP];
+      split2(rd[h].x, rd[h].y, p0);
+      split2(rd[h].z, rd[h].w, p1);
+#pragma unroll
+      for (int i = 0; i < kNP; ++i) *reinterpret_cast<uint2*>(base + i * kTB + off) = make_uint2(p0[i], p1[i]);
+      split2(rx[h].x, rx[h].y, p0);
+      split2(rx[h].z, rx[h].w, p1);
+#pragma unroll
+      for (int i = 0; i < kNP; ++i)
+        *reinterpret_cast<uint2*>(base + (kNP + i) * kTB + off) = make_uint2(p0[i], p1[i]);
+    }
+  };
+
+  const int cf0 = 2 * (wave >> 1), kf0 = 2 * (wave & 1);
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)lds));
+  const uint32_t offA = (8 * grp + q) * 128 + (16 * cf0 + 4 * p) * 2;
+  const uint32_t offB = kNP * kTB + (8 * grp + q) * 128 + (16 * kf0 + 4 * p) * 2;
+
+  if (steps > 0) load(0);
+  for (int s = 0; s < steps; ++s) {
+    // slot s & 1 was last read in step s - 2, before every wave passed step s - 1's barrier
+    stage(s & 1);
+    if (s + 1 < steps) load(s + 1);
+    __syncthreads();
+    const uint32_t sb = lds0 + (s & 1) * kSB;
+    // transposed fragments (see k_iwgrad in iconv_nhwc.hip) of one piece tile: two fragments u
+    auto tr_read = [&](uint32_t addr, bf16x8 (&f)[2]) {
+      s16x4 r[4];
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %4\n\t"
+          "ds_read_b64_tr_b16 %1, %4 offset:512\n\t"
+          "ds_read_b64_tr_b16 %2, %4 offset:32\n\t"
+          "ds_read_b64_tr_b16 %3, %4 offset:544\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+          : "v"(addr)
+          : "memory");
+      f[0] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r[0], r[1], 0, 1, 2, 3, 4, 5, 6, 7));
+      f[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r[2], r[3], 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    bf16x8 ta[kNP][2], tb[kNP][2];
+#pragma unroll
+    for (int i = 0; i < kNP; ++i) {
+      tr_read(sb + i * kTB + offA, ta[i]);
+      tr_read(sb + i * kTB + offB, tb[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const bf16x8 av[kNP] = {ta[0][u], ta[1][u], ta[2][u]};
+        const bf16x8 bv[kNP] = {tb[0][v], tb[1][v], tb[2][v]};
+        acc[u][v] = mma6(av, bv, acc[u][v]);
+      }
+  }
+
+  // D[co = 4*grp + e][k = li] of each (u, v) fragment
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + (cf0 + u) * 16 + 4 * grp + e;
+        const int k = k0 + (kf0 + v) * 16 + li;
+        const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
+                          static_cast<int64_t>(co) * K + k;
+        if (!GATHER || k < K) out[o] = acc[u][v][e];
+      }
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight split (once per step): W [R][T][C] fp32 -> W_hi, W_lo [R][T][C] and Wt_hi, Wt_lo [C][T][R]
+// bf16, 64 x 64 tiles of one tap through LDS (padded pitch)
+
+constexpr int kWJobs = 64;
+struct WJob {
+  const float* w;
+  uint16_t* pieces;    // [3][R][ld]
+  uint16_t* tpieces;   // nullable: [3][C][T][R] (no transposed copy)
+  int R, T, C;
+  int ld;              // row pitch of the pieces (elements)
+  int tile0;
+};
+struct WTable {
+  WJob j[kWJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void k_wsplit(WTable t) {
+  __shared__ uint16_t tp[kNP][64][66];   // the tile's pieces, [c][r] order
+  int ji = 0;
+  while (ji + 1 < t.n && static_cast<int>(blockIdx.x) >= t.j[ji + 1].tile0) ++ji;
+  const WJob jb = t.j[ji];
+  const int tr = (jb.R + 63) / 64, tc = (jb.C + 63) / 64;
+  const int l = blockIdx.x - jb.tile0;
+  const int tap = l / (tr * tc);
+  const int rem = l - tap * tr * tc;
+  const int r0 = (rem / tc) * 64, c0 = (rem % tc) * 64;
+  const int lc = threadIdx.x & 63, lr = threadIdx.x >> 6;
+  for (int rr = lr; rr < 64; rr += 4) {
+    const int r = r0 + rr, c = c0 + lc;
+    uint16_t pc[kNP] = {};
+    if (r < jb.R && c < jb.C) {
+      const int64_t o = (static_cast<int64_t>(r) * jb.T + tap) * jb.C + c;
+      const int64_t od = static_cast<int64_t>(r) * jb.ld + tap * jb.C + c;
+      const int64_t stride = static_cast<int64_t>(jb.R) * jb.ld;
+      float v = jb.w[o];
+#pragma unroll
+      for (int i = 0; i < kNP; ++i) {
+        pc[i] = f_to_bf16(v);
+        v -= bf16_to_f(pc[i]);
+        jb.pieces[i * stride + od] = pc[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kNP; ++i) tp[i][lc][rr] = pc[i];
+  }
+  if (jb.tpieces == nullptr) return;
+  __syncthreads();
+  const int64_t tstride = static_cast<int64_t>(jb.R) * jb.T * jb.C;
+  for (int cc = lr; cc < 64; cc += 4) {
+    const int c = c0 + cc, r = r0 + lc;
+    if (c < jb.C && r < jb.R) {
+      const int64_t o = (static_cast<int64_t>(c) * jb.T + tap) * jb.R + r;
+#pragma unroll
+      for (int i = 0; i < kNP; ++i) jb.tpieces[i * tstride + o] = tp[i][cc][lc];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// classifier and global average pool (fp32, VALU)
+
+// logits[r][o] = Σ_f x[r][f] w[o][f] + b[o]: one wave per row, O <= 64 outputs kept in registers
+constexpr int kLinMaxO = 16;
+__global__ __launch_bounds__(256) void k_f32_linear_fwd(const float* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ b, int R, int F, int O,
+                                                        float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  for (int o0 = 0; o0 < O; o0 += kLinMaxO) {
+    float acc[kLinMaxO];
+#pragma unroll
+    for (int o = 0; o < kLinMaxO; ++o) acc[o] = 0.f;
+    for (int f = lane; f < F; f += 64) {
+      const float xv = x[static_cast<int64_t>(row) * F + f];
+#pragma unroll
+      for (int o = 0; o < kLinMaxO; ++o)
+        if (o0 + o < O) acc[o] = fmaf(xv, w[static_cast<int64_t>(o0 + o) * F + f], acc[o]);
+    }
+#pragma unroll
+    for (int o = 0; o < kLinMaxO; ++o) {
+      float v = acc[o];
+#pragma unroll
+      for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s);
+      if (lane == 0 && o0 + o < O) y[static_cast<int64_t>(row) * O + o0 + o] = v + (b ? b[o0 + o] : 0.f);
+    }
+  }
+}
+
+// dx[r][f] = Σ_o dl[r][o] w[o][f]
+__global__ __launch_bounds__(256) void k_f32_linear_dgrad(const float* __restrict__ dl, const float* __restrict__ w,
+                                                          int R, int F, int O, float* __restrict__ dx) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= static_cast<int64_t>(R) * F) return;
+  const int64_t r = t / F;
+  const int f = static_cast<int>(t - r * F);
+  float a = 0.f;
+  for (int o = 0; o < O; ++o) a = fmaf(dl[r * O + o], w[static_cast<int64_t>(o) * F + f], a);
+  dx[t] = a;
+}
+
+// per worker g: dW_g[o][f] = Σ_{r in g} dl[r][o] x[r][f], db_g[o] = Σ dl[r][o]; written at
+// out + g * row_stride + off_w / off_b (the exchange rows); blockIdx.y = g, one thread per f
+__global__ __launch_bounds__(256) void k_f32_linear_wgrad(const float* __restrict__ x, const float* __restrict__ dl,
+                                                          int rg, int F, int O, float* __restrict__ out,
+                                                          int64_t row_stride, int64_t off_w, int64_t off_b) {
+  const int g = blockIdx.y;
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  const float* xg = x + static_cast<int64_t>(g) * rg * F;
+  const float* dg = dl + static_cast<int64_t>(g) * rg * O;
+  float* og = out + static_cast<int64_t>(g) * row_stride;
+  for (int o0 = 0; o0 < O; o0 += kLinMaxO) {
+    float acc[kLinMaxO];
+#pragma unroll
+    for (int o = 0; o < kLinMaxO; ++o) acc[o] = 0.f;
+    if (f < F) {
+      for (int r = 0; r < rg; ++r) {
+        const float xv = xg[static_cast<int64_t>(r) * F + f];
+#pragma unroll
+        for (int o = 0; o < kLinMaxO; ++o)
+          if (o0 + o < O) acc[o] = fmaf(dg[static_cast<int64_t>(r) * O + o0 + o], xv, acc[o]);
+      }
+#pragma unroll
+      for (int o = 0; o < kLinMaxO; ++o)
+        if (o0 + o < O) og[off_w + static_cast<int64_t>(o0 + o) * F + f] = acc[o];
+    }
+  }
+  if (off_b >= 0 && blockIdx.x == 0 && threadIdx.x < O) {
+    float s = 0.f;
+    for (int r = 0; r < rg; ++r) s += dg[static_cast<int64_t>(r) * O + threadIdx.x];
+    og[off_b + threadIdx.x] = s;
+  }
+}
+
+// pooled[n][c] = mean over HW of x[n][hw][c]
+__global__ __launch_bounds__(256) void k_f32_avgpool_fwd(const float* __restrict__ x, int N, int HW, int C,
+                                                         float* __restrict__ y) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= static_cast<int64_t>(N) * C) return;
+  const int64_t n = t / C;
+  const int c = static_cast<int>(t - n * C);
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += x[(n * HW + p) * C + c];
+  y[t] = s / static_cast<float>(HW);
+}
+
+__global__ __launch_bounds__(256) void k_f32_avgpool_bwd(const float* __restrict__ dy, int N, int HW, int C,
+                                                         float* __restrict__ dx) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= static_cast<int64_t>(N) * HW * C) return;
+  const int c = static_cast<int>(t % C);
+  const int64_t n = t / (static_cast<int64_t>(HW) * C);
+  dx[t] = dy[n * C + c] / static_cast<float>(HW);
+}
+
+unsigned blocks_for(int64_t items) { return static_cast<unsigned>((items + 255) / 256); }
+
+}  // namespace
+
+bool conv_f32_supported(const ConvF32Geo& g) { return g.Co % 64 == 0 && g.Cs > 0 && g.Co > 0; }
+
+int conv_f32_pick(const ConvF32Geo& g) {
+  const int64_t M = static_cast<int64_t>(g.N) * g.Ho * g.Wo;
+  const int64_t nco = g.Co / 64;
+  int pm = 4;
+  while (pm > 1 && ((M + 64 * pm - 1) / (64 * pm)) * nco < 512) pm /= 2;
+  return pm;
+}
+
+void conv_f32(const float* src, const uint16_t* w3, const ConvF32Geo& g, bool dgrad, float* out, const float* add,
+              int pm, hipStream_t stream) {
+  if (static_cast<int64_t>(g.N) * g.Ho * g.Wo <= 0) return;
+  if (pm <= 0) pm = conv_f32_pick(g) + 10;
+  if (pm > 10 && g.Cs % 32 == 0 && (!dgrad || (g.dh == 1 && g.dw == 1))) {   // the LDS-staged kernel
+    if (dgrad) {
+      if (pm >= 14) launch_conv_lds<4, 2, true>(src, w3, g, out, add, stream);
+      else if (pm == 12) launch_conv_lds<2, 3, true>(src, w3, g, out, add, stream);
+      else launch_conv_lds<1, 3, true>(src, w3, g, out, add, stream);
+    } else {
+      if (pm >= 14) launch_conv_lds<4, 2, false>(src, w3, g, out, add, stream);
+      else if (pm == 12) launch_conv_lds<2, 3, false>(src, w3, g, out, add, stream);
+      else launch_conv_lds<1, 3, false>(src, w3, g, out, add, stream);
+    }
+    return;
+  }
+  if (pm > 10) pm -= 10;
+  if (dgrad) {
+    if (pm >= 4) launch_conv<4, true>(src, w3, g, out, add, stream);
+    else if (pm == 2) launch_conv<2, true>(src, w3, g, out, add, stream);
+    else launch_conv<1, true>(src, w3, g, out, add, stream);
+  } else {
+    if (pm >= 4) launch_conv<4, false>(src, w3, g, out, add, stream);
+    else if (pm == 2) launch_conv<2, false>(src, w3, g, out, add, stream);
+    else launch_conv<1, false>(src, w3, g, out, add, stream);
+  }
+}
+
+bool wgrad_f32_supported(const ConvF32Geo& g) { return g.Cs > 0 && g.Co % 64 == 0; }
+
+void wgrad_f32(const float* x, const float* dy, const ConvF32Geo& g, int groups, int64_t rg, int splits, float* out,
+               int64_t split_stride, int64_t group_stride, hipStream_t stream) {
+  const int K = g.KH * g.KW * g.Cs;
+  if (splits < 1) splits = 1;
+  const int64_t per_split = (rg + splits - 1) / splits;
+  const dim3 grid(((K + 63) / 64) * (g.Co / 64), groups, splits);
+  if (g.Cs % 64 != 0)
+    hipLaunchKernelGGL(k_cf32_wgrad<true>, grid, dim3(256), 0, stream, x, dy, g, rg, per_split, out, split_stride,
+                       group_stride);
+  else
+    hipLaunchKernelGGL(k_cf32_wgrad<false>, grid, dim3(256), 0, stream, x, dy, g, rg, per_split, out, split_stride,
+                       group_stride);
+}
+
+void wsplit_multi(const WSplitJob* jobs, int count, hipStream_t stream) {
+  for (int b = 0; b < count; b += kWJobs) {
+    WTable t{};
+    int tiles = 0;
+    t.n = count - b < kWJobs ? count - b : kWJobs;
+    for (int i = 0; i < t.n; ++i) {
+      const WSplitJob& s = jobs[b + i];
+      t.j[i] = WJob{s.w, s.pieces, s.tpieces, s.R, s.T, s.C, s.ld > 0 ? s.ld : s.T * s.C, tiles};
+      tiles += s.T * ((s.R + 63) / 64) * ((s.C + 63) / 64);
+    }
+    if (tiles > 0) hipLaunchKernelGGL(k_wsplit, dim3(tiles), dim3(256), 0, stream, t);
+  }
+}
+
+void linear_f32_fwd(const float* x, const float* w, const float* b, int R, int F, int O, float* y, hipStream_t stream) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(k_f32_linear_fwd, dim3((R + 3) / 4), dim3(256), 0, stream, x, w, b, R, F, O, y);
+}
+
+void linear_f32_dgrad(const float* dl, const float* w, int R, int F, int O, float* dx, hipStream_t stream) {
+  const int64_t items = static_cast<int64_t>(R) * F;
+  if (items <= 0) return;
+  hipLaunchKernelGGL(k_f32_linear_dgrad, dim3(blocks_for(items)), dim3(256), 0, stream, dl, w, R, F, O, dx);
+}
+
+void linear_f32_wgrad(const float* x, const float* dl, int groups, int rg, int F, int O, float* out, int64_t row_stride,
+                      int64_t off_w, int64_t off_b, hipStream_t stream) {
+  if (groups <= 0 || F <= 0) return;
+  hipLaunchKernelGGL(k_f32_linear_wgrad, dim3((F + 255) / 256, groups), dim3(256), 0, stream, x, dl, rg, F, O, out,
+                     row_stride, off_w, off_b);
+}
+
+void avgpool_f32_fwd(const float* x, int N, int HW, int C, float* y, hipStream_t stream) {
+  const int64_t items = static_cast<int64_t>(N) * C;
+  if (items <= 0) return;
+  hipLaunchKernelGGL(k_f32_avgpool_fwd, dim3(blocks_for(items)), dim3(256), 0, stream, x, N, HW, C, y);
+}
+
+void avgpool_f32_bwd(const float* dy, int N, int HW, int C, float* dx, hipStream_t stream) {
+  const int64_t items = static_cast<int64_t>(N) * HW * C;
+  if (items <= 0) return;
+  hipLaunchKernelGGL(k_f32_avgpool_bwd, dim3(blocks_for(items)), dim3(256), 0, stream, dy, N, HW, C, dx);
+}
+
+}  // namespace gpu
+}  // namespace garfield

@@ -1,0 +1,52 @@
+// Host-side launchers of the fp32 (reference-precision) grouped-step kernels (conv_f32.hip):
+// NHWC convolutions on split-bf16 MFMA (three bf16 pieces per fp32 operand, the six products of
+// order <= 2, fp32 accumulation), the per-step weight split, and the classifier / average-pool
+// kernels. Asynchronous, no allocation, HIP-graph capturable.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace garfield {
+namespace gpu {
+
+// Geometry of one convolution: source activation [N][Hs][Ws][Cs], output [N][Ho][Wo][Co], and the
+// FORWARD convolution's kernel / stride / padding / dilation. For a data gradient the source is dy
+// (Hs, Ws, Cs = the forward's Ho, Wo, Cout) and the output dx (Ho, Wo, Co = the forward's H, W, Cin).
+struct ConvF32Geo {
+  int N, Hs, Ws, Cs, Ho, Wo, Co;
+  int KH, KW, sh, sw, ph, pw, dh, dw;
+};
+
+// Cs % 32 == 0, Co % 64 == 0
+bool conv_f32_supported(const ConvF32Geo& g);
+int conv_f32_pick(const ConvF32Geo& g);
+// out[m, co] (+= add, read from `add`) of the forward (w3: the pieces [3][Co][KH][KW][Cs]) or, with
+// dgrad, of the data gradient (w3: the transposed pieces [3][Co = Cin][KH][KW][Cs = Cout], any stride).
+void conv_f32(const float* src, const uint16_t* w3, const ConvF32Geo& g, bool dgrad, float* out, const float* add,
+              int pm, hipStream_t stream);
+// Cs % 64 == 0, Co % 64 == 0 (g: the forward geometry)
+bool wgrad_f32_supported(const ConvF32Geo& g);
+// out[s][grp][co][k] (fp32) = Σ over the s-th of `splits` ranges of worker grp's rg output pixels of
+// dy[m, co] · patch(x)[m, k]; element offset s * split_stride + grp * group_stride + co * K + k.
+void wgrad_f32(const float* x, const float* dy, const ConvF32Geo& g, int groups, int64_t rg, int splits, float* out,
+               int64_t split_stride, int64_t group_stride, hipStream_t stream);
+
+struct WSplitJob {
+  const float* w;      // [R][T][C] fp32 (a channels_last weight: R = Cout, T = KH*KW, C = Cin)
+  uint16_t* pieces;    // [3][R][ld] bf16: w0 = bf16(w), w1 = bf16(w - w0), w2 = bf16(w - w0 - w1)
+  uint16_t* tpieces;   // nullable: [3][C][T][R] the transposed pieces (the data gradient's weight)
+  int R, T, C;
+  int ld;              // row pitch of the pieces in elements (0: T * C; e.g. 160 for the padded stem)
+};
+void wsplit_multi(const WSplitJob* jobs, int count, hipStream_t stream);
+
+// classifier: y[R][O] = x[R][F] · w[O][F]ᵀ + b; dx = dl · w; per-worker dW / db into rows
+void linear_f32_fwd(const float* x, const float* w, const float* b, int R, int F, int O, float* y, hipStream_t stream);
+void linear_f32_dgrad(const float* dl, const float* w, int R, int F, int O, float* dx, hipStream_t stream);
+void linear_f32_wgrad(const float* x, const float* dl, int groups, int rg, int F, int O, float* out, int64_t row_stride,
+                      int64_t off_w, int64_t off_b, hipStream_t stream);
+void avgpool_f32_fwd(const float* x, int N, int HW, int C, float* y, hipStream_t stream);
+void avgpool_f32_bwd(const float* dy, int N, int HW, int C, float* dx, hipStream_t stream);
+
+}  // namespace gpu
+}  // namespace garfield

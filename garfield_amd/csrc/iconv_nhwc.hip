@@ -681,11 +681,7 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   const int M = g.N * g.Ho * g.Wo;
   if (M <= 0) return;
   if (pm <= 0) {  // measured (scripts/bench_iconv.py): the largest pixel tile that keeps ~500 workgroups
-    static const int64_t min_wg = [] {   // tuning knob: GARFIELD_ICONV_PM_WG
-      const char* e = std::getenv("GARFIELD_ICONV_PM_WG");
-      const long v = e ? std::atol(e) : 0;
-      return static_cast<int64_t>(v > 0 ? v : 500);
-    }();
+    constexpr int64_t min_wg = 500;
     const int64_t ncb = Cout / 64;
     pm = 4;
     while (pm > 1 && ((M + 64 * pm - 1) / (64 * pm)) * ncb < min_wg) pm /= 2;
@@ -854,33 +850,12 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
   }
 }
 
-// GARFIELD_IWGRAD_ROW: 0 one tap per workgroup, 1 the three taps of a kernel row (default),
-// 3 all nine taps of a 3x3 kernel
-static int iwgrad_row_mode() {
-  static const int m = [] {
-    const char* e = std::getenv("GARFIELD_IWGRAD_ROW");
-    return e ? std::atoi(e) : 1;
-  }();
-  return m;
-}
-
-// GARFIELD_IWGRAD_1X1_NT: input-channel blocks per workgroup of a 1x1 weight gradient
-// (4 / 2 / 1; a layer takes the largest that divides its C / 64)
-static int iwgrad_1x1_nt(int C) {
-  static const int m = [] {
-    const char* e = std::getenv("GARFIELD_IWGRAD_1X1_NT");
-    return e ? std::atoi(e) : 2;   // profiles/r2/iwgrad_wg_nt_sweep.log
-  }();
-  for (int nt = m; nt > 1; nt /= 2)
-    if (C % (64 * nt) == 0) return nt;
-  return 1;
-}
-
+// Taps per weight-gradient workgroup: a 3x3 kernel's row of three taps shares each staged dy tile
+// (profiles/r2/ab_iwgrad_9tap.log: all nine taps leave one wave per SIMD and lose); a 1x1
+// convolution's two 64-channel input blocks share it (profiles/r2/iwgrad_wg_nt_sweep.log).
 int iwgrad_taps_per_block(int kw, int kh, int C) {
-  if (kw == 1 && kh == 1) return iwgrad_1x1_nt(C);
-  const int m = iwgrad_row_mode();
-  if (kw != 3 || m == 0) return 1;
-  return m == 3 ? 9 : 3;
+  if (kw == 1 && kh == 1) return C % 128 == 0 ? 2 : 1;
+  return kw == 3 ? 3 : 1;
 }
 
 void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
@@ -889,38 +864,24 @@ void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cou
   if (splits < 1) splits = 1;
   const int64_t per_split = (rg + splits - 1) / splits;
   const int tpb = iwgrad_taps_per_block(g.KW, g.KH, g.C);
-  if (tpb > 1 && g.KW == 1) {
-    const dim3 grid((g.C / (64 * tpb)) * (Cout / 64), groups, splits);
-#define GARFIELD_IWG_1X1(NSV, NTV)                                                                                 \
-  if (out_bf16)                                                                                                    \
-    hipLaunchKernelGGL((k_iwgrad_1x1<NSV, true, NTV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, \
-                       out, split_stride, group_stride);                                                          \
-  else                                                                                                             \
-    hipLaunchKernelGGL((k_iwgrad_1x1<NSV, false, NTV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,\
-                       out, split_stride, group_stride)
-    static const int ns = [] {   // GARFIELD_IWGRAD_1X1_NS: pipeline stages (3 or 4)
-      const char* e = std::getenv("GARFIELD_IWGRAD_1X1_NS");
-      return e && std::atoi(e) == 4 ? 4 : 3;
-    }();
-    if (tpb == 4) { GARFIELD_IWG_1X1(3, 4); }
-    else if (ns == 4) { GARFIELD_IWG_1X1(4, 2); }
-    else { GARFIELD_IWG_1X1(3, 2); }
-#undef GARFIELD_IWG_1X1
+  if (tpb == 2 && g.KW == 1) {   // 1x1: two 64-channel input blocks per workgroup, 3 pipeline stages
+    const dim3 grid((g.C / 128) * (Cout / 64), groups, splits);
+    if (out_bf16)
+      hipLaunchKernelGGL((k_iwgrad_1x1<3, true, 2>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                         split_stride, group_stride);
+    else
+      hipLaunchKernelGGL((k_iwgrad_1x1<3, false, 2>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                         split_stride, group_stride);
     return;
   }
-  if (tpb > 1 && (tpb == 3 || g.KH == 3)) {
-    const int nr = tpb == 9 ? 3 : 1;
-    const dim3 grid((g.KH / nr) * (g.C / 64) * (Cout / 64), groups, splits);
-#define GARFIELD_IWG_ROWS(NSV, NRV)                                                                                 \
-  if (out_bf16)                                                                                                     \
-    hipLaunchKernelGGL((k_iwgrad_rows<NSV, true, NRV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,  \
-                       out, split_stride, group_stride);                                                           \
-  else                                                                                                              \
-    hipLaunchKernelGGL((k_iwgrad_rows<NSV, false, NRV>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, \
-                       out, split_stride, group_stride)
-    if (nr == 3) { GARFIELD_IWG_ROWS(2, 3); }
-    else { GARFIELD_IWG_ROWS(3, 1); }
-#undef GARFIELD_IWG_ROWS
+  if (tpb == 3) {                // the three taps of a kernel row per workgroup
+    const dim3 grid(g.KH * (g.C / 64) * (Cout / 64), groups, splits);
+    if (out_bf16)
+      hipLaunchKernelGGL((k_iwgrad_rows<3, true, 1>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                         split_stride, group_stride);
+    else
+      hipLaunchKernelGGL((k_iwgrad_rows<3, false, 1>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                         split_stride, group_stride);
     return;
   }
   const dim3 grid((K / 64) * (Cout / 64), groups, splits);

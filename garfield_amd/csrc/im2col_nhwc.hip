@@ -184,8 +184,9 @@ __global__ __launch_bounds__(kThreads) void k_col2im_scalar(const uint16_t* __re
 // windows that cover an input pixel (no scatter, no atomics, no zero fill).
 // Ties and NaN follow ATen: the first maximum in (i, j) scan order wins, a NaN
 // always wins.
-__global__ __launch_bounds__(kThreads) void k_maxpool_fwd(const uint16_t* __restrict__ x, Im2col g,
-                                                         uint16_t* __restrict__ y, uint8_t* __restrict__ idx) {
+template <int DT>
+__global__ __launch_bounds__(kThreads) void k_maxpool_fwd(const void* __restrict__ x, Im2col g,
+                                                         void* __restrict__ y, uint8_t* __restrict__ idx) {
   const int cv = g.C / 8;
   const int64_t total = static_cast<int64_t>(g.N) * g.Ho * g.Wo * cv;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_fwd(const uint16_t* __rest
         const int wi = wo * g.sw - g.pw + j * g.dw;
         if (wi < 0 || wi >= g.W) continue;
         float a[8];
-        load_vec<kBF16, 8>(x, ((static_cast<int64_t>(n) * g.H + hi) * g.W + wi) * g.C + v * 8, a);
+        load_vec<DT, 8>(x, ((static_cast<int64_t>(n) * g.H + hi) * g.W + wi) * g.C + v * 8, a);
         const int tap = i * g.KW + j;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_fwd(const uint16_t* __rest
       }
     }
     const int64_t o = static_cast<int64_t>(m) * g.C + v * 8;
-    store_vec<8>(y, kBF16, o, best);
+    store_vec<8>(y, DT, o, best);
     uint2 packed;
     packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (static_cast<uint32_t>(arg[3]) << 24);
     packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (static_cast<uint32_t>(arg[7]) << 24);
@@ -222,9 +223,10 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_fwd(const uint16_t* __rest
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_maxpool_bwd(const uint16_t* __restrict__ dy,
+template <int DT>
+__global__ __launch_bounds__(kThreads) void k_maxpool_bwd(const void* __restrict__ dy,
                                                          const uint8_t* __restrict__ idx, Im2col g,
-                                                         uint16_t* __restrict__ dx) {
+                                                         void* __restrict__ dx) {
   const int cv = g.C / 8;
   const int64_t total = static_cast<int64_t>(g.N) * g.H * g.W * cv;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_bwd(const uint16_t* __rest
         const uint2 p = *reinterpret_cast<const uint2*>(idx + o);
         const int tap = i * g.KW + j;
         float d[8];
-        load_vec<kBF16, 8>(dy, o, d);
+        load_vec<DT, 8>(dy, o, d);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint32_t word = e < 4 ? p.x : p.y;
@@ -251,7 +253,7 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_bwd(const uint16_t* __rest
         }
       }
     }
-    store_vec<8>(dx, kBF16, static_cast<int64_t>(pix) * g.C + v * 8, acc);
+    store_vec<8>(dx, DT, static_cast<int64_t>(pix) * g.C + v * 8, acc);
   }
 }
 
@@ -294,16 +296,18 @@ unsigned grid_for(int64_t items) {
 }
 }  // namespace
 
-void maxpool_fwd_nhwc(const uint16_t* x, const Im2col& g, uint16_t* y, uint8_t* idx, hipStream_t stream) {
+void maxpool_fwd_nhwc(const void* x, const Im2col& g, void* y, uint8_t* idx, hipStream_t stream, int dt) {
   const int64_t items = static_cast<int64_t>(g.N) * g.Ho * g.Wo * (g.C / 8);
   if (items <= 0) return;
-  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for(items)), dim3(kThreads), 0, stream, x, g, y, idx);
+  if (dt == kF32) hipLaunchKernelGGL(k_maxpool_fwd<kF32>, dim3(grid_for(items)), dim3(kThreads), 0, stream, x, g, y, idx);
+  else hipLaunchKernelGGL(k_maxpool_fwd<kBF16>, dim3(grid_for(items)), dim3(kThreads), 0, stream, x, g, y, idx);
 }
 
-void maxpool_bwd_nhwc(const uint16_t* dy, const uint8_t* idx, const Im2col& g, uint16_t* dx, hipStream_t stream) {
+void maxpool_bwd_nhwc(const void* dy, const uint8_t* idx, const Im2col& g, void* dx, hipStream_t stream, int dt) {
   const int64_t items = static_cast<int64_t>(g.N) * g.H * g.W * (g.C / 8);
   if (items <= 0) return;
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(items)), dim3(kThreads), 0, stream, dy, idx, g, dx);
+  if (dt == kF32) hipLaunchKernelGGL(k_maxpool_bwd<kF32>, dim3(grid_for(items)), dim3(kThreads), 0, stream, dy, idx, g, dx);
+  else hipLaunchKernelGGL(k_maxpool_bwd<kBF16>, dim3(grid_for(items)), dim3(kThreads), 0, stream, dy, idx, g, dx);
 }
 
 }  // namespace gpu

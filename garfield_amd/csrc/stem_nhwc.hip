@@ -1,11 +1,11 @@
 // The ResNet stem as an implicit-GEMM MFMA convolution (gfx950): 7x7, stride 2,
-// padding 3, over 3 input channels, NHWC bf16, for the grouped step's k workers.
+// padding 3, over 3 input channels, NHWC, for the grouped step's k workers.
 //
 // The generic path of the grouped executor runs this layer as im2col (a [pixels, 152]
 // patch matrix: 156 MB for 2000 CIFAR images, written by 8 scalar 2-byte gathers per
 // 16-byte store) + a hipBLASLt GEMM that reads it back, and keeps the matrix alive
 // for the weight gradient (~170 us forward + ~57 us weight-gradient GEMM per step,
-// profiles/r3). Here nothing but the input (12 MB) and the output (65 MB) touch HBM:
+// profiles/r3). Here nothing but the input and the output touch HBM:
 //
 // * forward: a workgroup owns 128 consecutive output pixels of one image. It stages
 //   the input rows they read (zero-padded borders) and the [64][160] weight matrix
@@ -17,8 +17,15 @@
 //   worker's images and accumulates dW[64][160] over their pixels with the
 //   pixel index as the MFMA reduction dimension: A = dyᵀ (a [64][32] LDS tile
 //   written transposed), B = the patch values of those 32 pixels, gathered from the
-//   staged input rows. The fp32 slabs of the slices are summed by the deferred
-//   split-K reduction of the exchange rows (GradSink.queue_split).
+//   staged input rows. An image is processed in BANDS of output rows whose input rows
+//   fit the LDS budget (one band for CIFAR sizes, 8 bands at 224 x 224). The fp32 slabs
+//   of the slices are summed by the deferred split-K reduction of the exchange rows
+//   (GradSink.queue_split).
+//
+// SPLIT (the reference-precision fp32 step): fp32 input / dy / output; every staged value
+// is split into three bf16 pieces (LDS holds all three), the weight comes as its three pieces, and
+// each product is the six piece products of order <= 2 on the bf16 MFMA with fp32 accumulation
+// (see conv_f32.hip).
 #include "bn_gpu.hpp"
 #include "gar_device.hpp"
 
@@ -32,11 +39,14 @@ constexpr int kK = kKH * kKW * kC;        // 147
 constexpr int kKP = 160;                   // padded to 5 k-steps of 32
 constexpr int kTile = 128;                 // output pixels per forward workgroup
 constexpr int kThreads = 256;
-constexpr int kMaxPatch = 24576;           // elements (48 KB) of staged input per workgroup
+constexpr int kMaxPatch = 24576;           // elements of staged input per workgroup (bf16)
+constexpr int kMaxPatchSplit = 16384;      // ... per piece array of the split (fp32) form
+constexpr int kNP = 3;                     // bf16 pieces per fp32 value (split form)
 
 struct StemGeo {
   int N, H, W, Ho, Wo;
   int pw;          // staged row width in pixels = W + 2P
+  int band;        // output rows per weight-gradient band
 };
 
 // patch offset (elements) of reduction index k = (ky * 7 + kx) * 3 + ci inside the
@@ -52,23 +62,28 @@ __device__ __forceinline__ int tap_offset(int k, int pw, int zero) {
 // A staged row is the image row's 3W contiguous elements between 3P zero elements on each side;
 // the (row, column) position advances without divisions, and each thread issues kStageBatch
 // independent loads before its LDS stores (one memory latency per batch, not per element).
+// SPLIT: x is fp32 and each value lands as three pieces in patch, patch + pstride, patch + 2 pstride.
 constexpr int kStageBatch = 8;
-__device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ x, const StemGeo& g, int n, int iy0, int rows,
-                                           uint16_t* patch) {
+template <bool SPLIT>
+__device__ __forceinline__ void stage_rows(const void* __restrict__ xv, const StemGeo& g, int n, int iy0, int rows,
+                                           uint16_t* patch, int pstride) {
   const int per_row = g.pw * kC, row_len = g.W * kC;
   const int total = rows * per_row;
-  const uint16_t* src = x + static_cast<int64_t>(n) * g.H * row_len - kP * kC;   // (iy, c) at src + iy*row_len + c
+  const int64_t img = static_cast<int64_t>(n) * g.H * row_len - kP * kC;   // (iy, c) at img + iy*row_len + c
   const int dr = kThreads / per_row, dc = kThreads - dr * per_row;
   int e = threadIdx.x, r = e / per_row, c = e - r * per_row;
   while (e < total) {
-    uint16_t v[kStageBatch];
+    float v[kStageBatch];
     int pos[kStageBatch];
 #pragma unroll
     for (int b = 0; b < kStageBatch; ++b) {
       const int iy = iy0 + r;
-      v[b] = 0;
-      if (e < total && iy >= 0 && iy < g.H && c >= kP * kC && c < kP * kC + row_len)
-        v[b] = src[static_cast<int64_t>(iy) * row_len + c];
+      v[b] = 0.f;
+      if (e < total && iy >= 0 && iy < g.H && c >= kP * kC && c < kP * kC + row_len) {
+        const int64_t o = img + static_cast<int64_t>(iy) * row_len + c;
+        if constexpr (SPLIT) v[b] = static_cast<const float*>(xv)[o];
+        else v[b] = bf16_to_f(static_cast<const uint16_t*>(xv)[o]);
+      }
       pos[b] = e;
       e += kThreads;
       c += dc;
@@ -80,17 +95,47 @@ __device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ x, const
     }
 #pragma unroll
     for (int b = 0; b < kStageBatch; ++b)
-      if (pos[b] < total) patch[pos[b]] = v[b];
+      if (pos[b] < total) {
+        if constexpr (SPLIT) {
+          float r = v[b];
+#pragma unroll
+          for (int i = 0; i < kNP; ++i) {
+            const uint16_t h = f_to_bf16(r);
+            patch[i * pstride + pos[b]] = h;
+            r -= bf16_to_f(h);
+          }
+        } else {
+          patch[pos[b]] = f_to_bf16(v[b]);
+        }
+      }
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_stem_fwd(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
-                                                       StemGeo g, uint16_t* __restrict__ y) {
-  // LDS (dynamic, sized by the host for this geometry): weights [64][160] | staged input rows
-  // (+1 zero); the [128][64] output tile reuses the whole area
+__device__ __forceinline__ bf16x8 u8_to_bf16x8(const uint16_t (&v)[8]) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = __builtin_bit_cast(__bf16, v[j]);
+  return r;
+}
+
+// the six piece products of order <= 2 (split form), the small terms first
+__device__ __forceinline__ f32x4 mma6(const bf16x8 (&a)[kNP], const bf16x8 (&b)[kNP], f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ x, const uint16_t* __restrict__ w,
+                                                       StemGeo g, void* __restrict__ y) {
+  // LDS (dynamic, sized by the host for this geometry): weights [64][160] (x3 split) | staged
+  // input rows (+1 zero) (x3 split); the output tile reuses the whole area
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  constexpr int NP = SPLIT ? kNP : 1;
   uint16_t* wl = lds;
-  uint16_t* patch = lds + kCout * kKP;
   const int tiles = (g.Ho * g.Wo + kTile - 1) / kTile;
   const int n = blockIdx.x / tiles;
   const int p0 = (blockIdx.x - n * tiles) * kTile;
@@ -98,13 +143,15 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const uint16_t* __restric
   const int oy0 = p0 / g.Wo, oy1 = (p0 + npix - 1) / g.Wo;
   const int iy0 = oy0 * kS - kP;
   const int rows = (oy1 - oy0) * kS + kKH;
-  // weights: the zero-padded [64][160] bf16 matrix (columns in the channels_last weight's
-  // (ky, kx, ci) order), 16-byte loads
-  for (int e = threadIdx.x; e < kCout * kKP / 8; e += kThreads)
-    reinterpret_cast<uint4*>(wl)[e] = reinterpret_cast<const uint4*>(w)[e];
-  stage_rows(x, g, n, iy0, rows, patch);
   const int zero = rows * g.pw * kC;
-  if (threadIdx.x == 0) patch[zero] = 0;
+  uint16_t* patch = lds + NP * kCout * kKP;
+  const int pstride = zero + 8;   // elements between the piece arrays of the staged rows
+  // weights: the zero-padded [64][160] bf16 matrix (columns in the channels_last weight's
+  // (ky, kx, ci) order; split: its three pieces one after the other), 16-byte loads
+  for (int e = threadIdx.x; e < NP * kCout * kKP / 8; e += kThreads)
+    reinterpret_cast<uint4*>(wl)[e] = reinterpret_cast<const uint4*>(w)[e];
+  stage_rows<SPLIT>(x, g, n, iy0, rows, patch, pstride);
+  if (threadIdx.x < NP) patch[threadIdx.x * pstride + zero] = 0;
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -129,54 +176,82 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const uint16_t* __restric
     int off[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) off[j] = tap_offset(kb + j, g.pw, zero);
-    bf16x8 bx[2];
+    bf16x8 bx[2][NP];
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint16_t v = off[j] == zero ? uint16_t(0) : patch[pbase[f] + off[j]];
-        bx[f][j] = __builtin_bit_cast(__bf16, v);
+      for (int i = 0; i < NP; ++i) {
+        uint16_t vh[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vh[j] = patch[i * pstride + (off[j] == zero ? zero : pbase[f] + off[j])];
+        bx[f][i] = u8_to_bf16x8(vh);
       }
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const bf16x8 aw = *reinterpret_cast<const bf16x8*>(wl + (c * 16 + fr) * kKP + kb);
+      bf16x8 aw[NP];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) acc[f][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx[f], acc[f][c], 0, 0, 0);
+      for (int i = 0; i < NP; ++i) aw[i] = *reinterpret_cast<const bf16x8*>(wl + i * kCout * kKP + (c * 16 + fr) * kKP + kb);
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        if constexpr (SPLIT) acc[f][c] = mma6(aw, bx[f], acc[f][c]);
+        else acc[f][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], bx[f][0], acc[f][c], 0, 0, 0);
+      }
     }
   }
   // epilogue: D lane = pixel fr of fragment f, channels 16c + 4fq .. +3 -> LDS tile [128][64] -> 16-byte rows
   __syncthreads();   // every wave's weight and patch reads are done: reuse the area
-  uint16_t* tile = lds;
+  if constexpr (SPLIT) {
+    float* tile = reinterpret_cast<float*>(lds);
 #pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const int pl = wave * 32 + f * 16 + fr;
+    for (int f = 0; f < 2; ++f) {
+      const int pl = wave * 32 + f * 16 + fr;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      uint2 o;
-      o.x = static_cast<uint32_t>(f_to_bf16(acc[f][c][0])) | (static_cast<uint32_t>(f_to_bf16(acc[f][c][1])) << 16);
-      o.y = static_cast<uint32_t>(f_to_bf16(acc[f][c][2])) | (static_cast<uint32_t>(f_to_bf16(acc[f][c][3])) << 16);
-      *reinterpret_cast<uint2*>(tile + pl * kCout + c * 16 + fq * 4) = o;
+      for (int c = 0; c < 4; ++c)
+        *reinterpret_cast<float4*>(tile + pl * kCout + c * 16 + fq * 4) =
+            make_float4(acc[f][c][0], acc[f][c][1], acc[f][c][2], acc[f][c][3]);
     }
+    __syncthreads();
+    float* out = static_cast<float*>(y) + (static_cast<int64_t>(n) * g.Ho * g.Wo + p0) * kCout;
+    for (int e = threadIdx.x; e < npix * (kCout / 4); e += kThreads)
+      *reinterpret_cast<float4*>(out + e * 4) = *reinterpret_cast<const float4*>(tile + e * 4);
+  } else {
+    uint16_t* tile = lds;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const int pl = wave * 32 + f * 16 + fr;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint2 o;
+        o.x = pack_bf16x2(acc[f][c][0], acc[f][c][1]);
+        o.y = pack_bf16x2(acc[f][c][2], acc[f][c][3]);
+        *reinterpret_cast<uint2*>(tile + pl * kCout + c * 16 + fq * 4) = o;
+      }
+    }
+    __syncthreads();
+    uint16_t* out = static_cast<uint16_t*>(y) + (static_cast<int64_t>(n) * g.Ho * g.Wo + p0) * kCout;
+    for (int e = threadIdx.x; e < npix * (kCout / 8); e += kThreads)
+      *reinterpret_cast<uint4*>(out + e * 8) = *reinterpret_cast<const uint4*>(tile + e * 8);
   }
-  __syncthreads();
-  uint16_t* out = y + (static_cast<int64_t>(n) * g.Ho * g.Wo + p0) * kCout;
-  for (int e = threadIdx.x; e < npix * (kCout / 8); e += kThreads)
-    *reinterpret_cast<uint4*>(out + e * 8) = *reinterpret_cast<const uint4*>(tile + e * 8);
 }
 
-// Weight gradient: workgroup (slice s, worker g) sums over images [i0, i1) of worker g.
-// Pixels are processed 32 at a time (one MFMA reduction step): the dy tile [32][64] is
-// written transposed into LDS ([64][32 + pad]); each of the 4 waves owns 16 output
-// channels and all 10 k-blocks of 16 (160 padded taps): acc[10] f32x4.
+// Weight gradient: workgroup (slice s, worker g) sums over images [i0, i1) of worker g, each in
+// bands of g.band output rows. Pixels are processed 32 at a time (one MFMA reduction step): the
+// dy tile [32][64] is written transposed into LDS ([64][32 + pad]); each of the 4 waves owns 16
+// output channels and all 10 k-blocks of 16 (160 padded taps): acc[10] f32x4.
 constexpr int kDyPitch = 40;   // bf16 per transposed dy row (32 + 8: 16-byte aligned, conflict-spread)
 
-__global__ __launch_bounds__(kThreads) void k_stem_wgrad(const uint16_t* __restrict__ x,
-                                                         const uint16_t* __restrict__ dy, StemGeo g, int imgs_per_worker,
-                                                         int slices, float* __restrict__ part) {
+template <bool SPLIT>
+__global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict__ x, const void* __restrict__ dy,
+                                                         StemGeo g, int imgs_per_worker, int slices,
+                                                         float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];   // dynamic: sized by the host
-  uint16_t* dyt = lds;                       // [64][kDyPitch]
-  uint16_t* patch = lds + kCout * kDyPitch;  // one image's input rows
+  constexpr int NP = SPLIT ? kNP : 1;
+  uint16_t* dyt = lds;                            // [64][kDyPitch] (x3 split: the pieces one after the other)
+  const int brows = (g.band - 1) * kS + kKH;      // input rows a band's outputs read
+  const int zero = brows * g.pw * kC;
+  uint16_t* patch = lds + NP * kCout * kDyPitch;  // one band's input rows (x3 split)
+  const int pstride = zero + 8;
   const int s = blockIdx.x, grp = blockIdx.y;
   const int per = (imgs_per_worker + slices - 1) / slices;
   const int i0 = grp * imgs_per_worker + s * per;
@@ -184,8 +259,6 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const uint16_t* __restr
   if (i1 > (grp + 1) * imgs_per_worker) i1 = (grp + 1) * imgs_per_worker;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int rows = (g.Ho - 1) * kS + kKH;    // every input row an image's outputs read
-  const int zero = rows * g.pw * kC;
   // this lane's 10 taps (k = 16 kb + fr), as staged-row offsets
   int toff[kKP / 16];
 #pragma unroll
@@ -194,58 +267,74 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const uint16_t* __restr
 #pragma unroll
   for (int kb = 0; kb < kKP / 16; ++kb) acc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int npix = g.Ho * g.Wo;
+  const int pq = threadIdx.x >> 3, cv = threadIdx.x & 7;   // this thread's 8 channels of one dy pixel
   for (int n = i0; n < i1; ++n) {
-    __syncthreads();   // the previous image's patch reads are done
-    stage_rows(x, g, n, -kP, rows, patch);
-    if (threadIdx.x == 0) patch[zero] = 0;
-    const uint16_t* dyi = dy + static_cast<int64_t>(n) * npix * kCout;
-    // this thread's 16 bytes of a dy tile: pixel q0 + pq, channels 8 cv .. +7; the next
-    // tile's load is issued before the current tile's MFMAs (one latency per image, not per tile)
-    const int pq = threadIdx.x >> 3, cv = threadIdx.x & 7;
-    auto load_dy = [&](int q0) {
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (q0 + pq < npix) v = *reinterpret_cast<const uint4*>(dyi + static_cast<int64_t>(q0 + pq) * kCout + cv * 8);
-      return v;
-    };
-    uint4 vnext = load_dy(0);
-    for (int q0 = 0; q0 < npix; q0 += 32) {
-      __syncthreads();   // previous dy tile consumed (and, first time, the patch staged)
-      {
-        const uint32_t wv[4] = {vnext.x, vnext.y, vnext.z, vnext.w};
+    for (int ob0 = 0; ob0 < g.Ho; ob0 += g.band) {
+      const int ob1 = ob0 + g.band < g.Ho ? ob0 + g.band : g.Ho;
+      const int q_lo = ob0 * g.Wo, q_hi = ob1 * g.Wo;      // the band's pixels [q_lo, q_hi)
+      __syncthreads();   // the previous band's patch reads are done
+      stage_rows<SPLIT>(x, g, n, ob0 * kS - kP, (ob1 - ob0 - 1) * kS + kKH, patch, pstride);
+      if (threadIdx.x < NP) patch[threadIdx.x * pstride + zero] = 0;
+      const int64_t dyi = static_cast<int64_t>(n) * npix * kCout;
+      // the next tile's load is issued before the current tile's MFMAs (one latency per band, not per tile)
+      auto load_dy = [&](int q0, float (&v)[8]) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          dyt[(cv * 8 + 2 * i) * kDyPitch + pq] = static_cast<uint16_t>(wv[i] & 0xffffu);
-          dyt[(cv * 8 + 2 * i + 1) * kDyPitch + pq] = static_cast<uint16_t>(wv[i] >> 16);
+        for (int i = 0; i < 8; ++i) v[i] = 0.f;
+        if (q0 + pq < q_hi) {
+          if constexpr (SPLIT) load_vec<kF32, 8>(dy, dyi + static_cast<int64_t>(q0 + pq) * kCout + cv * 8, v);
+          else load_vec<kBF16, 8>(dy, dyi + static_cast<int64_t>(q0 + pq) * kCout + cv * 8, v);
         }
-      }
-      if (q0 + 32 < npix) vnext = load_dy(q0 + 32);
-      __syncthreads();
-      // A = dyᵀ: lane holds channel (16 wave + fr), pixels q0 + 8 fq .. +7
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(dyt + (wave * 16 + fr) * kDyPitch + fq * 8);
-      // B: pixels q0 + 8 fq + j (rows of the reduction), tap k = 16 kb + fr (column)
-      // (the 8 pixels are consecutive: one division, then column steps with a row wrap)
-      int pb[8];
-      {
-        const int p = q0 + fq * 8;
-        int oy = p / g.Wo, ox = p - oy * g.Wo;
+      };
+      float vnext[8];
+      load_dy(q_lo, vnext);
+      for (int q0 = q_lo; q0 < q_hi; q0 += 32) {
+        __syncthreads();   // previous dy tile consumed (and, first time, the band staged)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pb[j] = p + j < npix ? (oy * kS * g.pw + ox * kS) * kC : -1;   // rows staged from input row -P
-          if (++ox == g.Wo) {
-            ox = 0;
-            ++oy;
+        for (int i = 0; i < 8; ++i) {
+          float r = vnext[i];
+#pragma unroll
+          for (int pc = 0; pc < NP; ++pc) {
+            const uint16_t h = f_to_bf16(r);
+            dyt[pc * kCout * kDyPitch + (cv * 8 + i) * kDyPitch + pq] = h;
+            r -= bf16_to_f(h);
           }
         }
-      }
+        if (q0 + 32 < q_hi) load_dy(q0 + 32, vnext);
+        __syncthreads();
+        // A = dyᵀ: lane holds channel (16 wave + fr), pixels q0 + 8 fq .. +7
+        bf16x8 a[NP];
 #pragma unroll
-      for (int kb = 0; kb < kKP / 16; ++kb) {
-        bf16x8 b;
+        for (int pc = 0; pc < NP; ++pc)
+          a[pc] = *reinterpret_cast<const bf16x8*>(dyt + pc * kCout * kDyPitch + (wave * 16 + fr) * kDyPitch + fq * 8);
+        // B: pixels q0 + 8 fq + j (rows of the reduction), tap k = 16 kb + fr (column)
+        // (the 8 pixels are consecutive: one division, then column steps with a row wrap)
+        int pb[8];
+        {
+          const int p = q0 + fq * 8;
+          int oy = p / g.Wo, ox = p - oy * g.Wo;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint16_t v = (pb[j] < 0 || toff[kb] == zero) ? uint16_t(0) : patch[pb[j] + toff[kb]];
-          b[j] = __builtin_bit_cast(__bf16, v);
+          for (int j = 0; j < 8; ++j) {
+            pb[j] = p + j < q_hi ? ((oy - ob0) * kS * g.pw + ox * kS) * kC : -1;   // band staged from row ob0*S - P
+            if (++ox == g.Wo) {
+              ox = 0;
+              ++oy;
+            }
+          }
         }
-        acc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[kb], 0, 0, 0);
+#pragma unroll
+        for (int kb = 0; kb < kKP / 16; ++kb) {
+          bf16x8 b[NP];
+#pragma unroll
+          for (int pc = 0; pc < NP; ++pc) {
+            uint16_t vh[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              vh[j] = patch[pc * pstride + ((pb[j] < 0 || toff[kb] == zero) ? zero : pb[j] + toff[kb])];
+            b[pc] = u8_to_bf16x8(vh);
+          }
+          if constexpr (SPLIT) acc[kb] = mma6(a, b, acc[kb]);
+          else acc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc[kb], 0, 0, 0);
+        }
       }
     }
   }
@@ -260,7 +349,7 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const uint16_t* __restr
   }
 }
 
-StemGeo geo(int N, int H, int W) {
+StemGeo geo(int N, int H, int W, bool split = false) {
   StemGeo g{};
   g.N = N;
   g.H = H;
@@ -268,33 +357,60 @@ StemGeo geo(int N, int H, int W) {
   g.Ho = (H + 2 * kP - kKH) / kS + 1;
   g.Wo = (W + 2 * kP - kKW) / kS + 1;
   g.pw = W + 2 * kP;
+  // weight-gradient bands: as many output rows as the staged input rows allow
+  const int max_rows = (split ? kMaxPatchSplit : kMaxPatch) / (g.pw * kC) - 1;
+  int band = max_rows >= kKH ? (max_rows - kKH) / kS + 1 : 0;
+  g.band = band > g.Ho ? g.Ho : band;
   return g;
 }
 
 int fwd_rows(const StemGeo& g) { return ((kTile + g.Wo - 1) / g.Wo) * kS + kKH; }   // max staged rows per tile
-int wg_rows(const StemGeo& g) { return (g.Ho - 1) * kS + kKH; }                     // every row an image reads
+
+template <class K>
+void allow_lds(K kernel, size_t bytes) {
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(bytes));
+}
 
 }  // namespace
 
 bool stem_supported(int H, int W) {
   if (H <= 0 || W <= 0) return false;
-  const StemGeo g = geo(1, H, W);
-  return fwd_rows(g) * g.pw * kC < kMaxPatch && wg_rows(g) * g.pw * kC < kMaxPatch;
+  const StemGeo g = geo(1, H, W), gs = geo(1, H, W, true);
+  return fwd_rows(g) * g.pw * kC < kMaxPatchSplit && g.band >= 1 && gs.band >= 1;
 }
 
-void stem_fwd(const uint16_t* x, const uint16_t* w, int N, int H, int W, uint16_t* y, hipStream_t stream) {
-  const StemGeo g = geo(N, H, W);
+void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream) {
+  const StemGeo g = geo(N, H, W, split);
   const int tiles = (g.Ho * g.Wo + kTile - 1) / kTile;
-  const size_t lds = (static_cast<size_t>(kCout) * kKP + static_cast<size_t>(fwd_rows(g)) * g.pw * kC + 8) * 2;
-  hipLaunchKernelGGL(k_stem_fwd, dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
+  const int np = split ? kNP : 1;
+  size_t lds = (static_cast<size_t>(np) * kCout * kKP + np * (static_cast<size_t>(fwd_rows(g)) * g.pw * kC + 8)) * 2;
+  const size_t tile = static_cast<size_t>(kTile) * kCout * (split ? 4 : 2);
+  if (lds < tile) lds = tile;
+  if (split) {
+    allow_lds(k_stem_fwd<true>, lds);
+    hipLaunchKernelGGL(k_stem_fwd<true>, dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
+  } else {
+    hipLaunchKernelGGL(k_stem_fwd<false>, dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
+  }
 }
 
-void stem_wgrad(const uint16_t* x, const uint16_t* dy, int N, int H, int W, int groups, int slices, float* part,
+void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,
                 hipStream_t stream) {
-  const StemGeo g = geo(N, H, W);
-  const size_t lds = (static_cast<size_t>(kCout) * kDyPitch + static_cast<size_t>(wg_rows(g)) * g.pw * kC + 8) * 2;
-  hipLaunchKernelGGL(k_stem_wgrad, dim3(slices, groups), dim3(kThreads), lds, stream, x, dy, g, N / groups, slices,
-                     part);
+  const StemGeo g = geo(N, H, W, split);
+  const int np = split ? kNP : 1;
+  const size_t brows = static_cast<size_t>((g.band - 1) * kS + kKH);
+  const size_t lds = (static_cast<size_t>(np) * kCout * kDyPitch + np * (brows * g.pw * kC + 8)) * 2;
+  if (split) {
+    allow_lds(k_stem_wgrad<true>, lds);
+    hipLaunchKernelGGL(k_stem_wgrad<true>, dim3(slices, groups), dim3(kThreads), lds, stream, x, dy, g, N / groups,
+                       slices, part);
+  } else {
+    allow_lds(k_stem_wgrad<false>, lds);
+    hipLaunchKernelGGL(k_stem_wgrad<false>, dim3(slices, groups), dim3(kThreads), lds, stream, x, dy, g, N / groups,
+                       slices, part);
+  }
 }
 
 }  // namespace gpu

@@ -6,7 +6,8 @@ RandomCrop(32, padding=4) + RandomHorizontalFlip + Normalize
 (uint8, NHWC) images of a dataset resident in HBM and, per step, draws the k
 logical workers' sample indices on the device and builds the whole grouped batch
 with ``data_aug.hip`` (gather + random crop + flip + normalise + bf16 cast,
-channels_last) — no host work, no per-image launches. The crop/flip of a row is a
+channels_last; fp32 when the consumer's step runs at the reference precision) — no host work, no
+per-image launches. The crop/flip of a row is a
 hash of (seed, step, row), so a step's batch is reproducible.
 
 CPU tensors take a PyTorch implementation of the same augmentation (same hash is
@@ -51,13 +52,14 @@ class DeviceBatches:
         self.gen.manual_seed(self.seed)
 
     def attach(self, buffers) -> bool:
-        """Write every batch straight into a consumer's input buffers (x [k*B, C, H, W] bf16
+        """Write every batch straight into a consumer's input buffers (x [k*B, C, H, W] bf16 or fp32
         channels_last, y [k*B] int64: ``RobustDataParallel.grouped_inputs``); False (nothing
         changed) when they do not fit."""
         if buffers is None or self.device.type != "cuda":
             return False
         x, y = buffers
-        if (tuple(x.shape) != tuple(self.out.shape) or x.dtype != torch.bfloat16 or x.device != self.device
+        if (tuple(x.shape) != tuple(self.out.shape) or x.dtype not in (torch.bfloat16, torch.float32)
+                or x.device != self.device
                 or not x.is_contiguous(memory_format=torch.channels_last) or y.dtype != torch.long
                 or tuple(y.shape) != (self.k * self.B,) or not y.is_contiguous()):
             return False

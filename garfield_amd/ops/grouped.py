@@ -36,9 +36,7 @@ test suite); on the GPU the native extension is mandatory.
 """
 from __future__ import annotations
 
-import contextlib
 import math
-import os
 
 import torch
 import torch.nn.functional as F
@@ -46,50 +44,32 @@ import torch.nn.functional as F
 from garfield_amd import _native
 from garfield_amd.utils.flat import is_dense
 
-# k x k convolutions of the grouped step on the GPU: "gemm" (HIP im2col/col2im +
-# hipBLASLt GEMMs, per-worker weight gradients in one batched GEMM) or "miopen"
-# (ATen/MIOpen convolutions, one weight-gradient call per worker). MIOpen's NHWC
-# solvers are not HIP-graph replay safe on ROCm 7 / gfx950 (non-finite weight
-# gradients from a replay on), so "miopen" is only for eager A/B runs.
-CONV_MODE = os.environ.get("GARFIELD_GROUPED_CONV", "gemm")
-# Implicit-GEMM MFMA convolutions (iconv_nhwc.hip) for the k x k layers whose
-# channel counts fit its tiles (C % 64, Cout % 64): forward, and the stride-1 data
-# gradient as a convolution with the flipped weight. "0" keeps im2col + GEMM.
-ICONV = os.environ.get("GARFIELD_ICONV", "1") != "0"
-# Their per-worker weight gradients by the implicit MFMA kernel (no im2col matrix).
-IWGRAD = os.environ.get("GARFIELD_IWGRAD", "1") != "0"
-# ... and for the 1x1 stride-1 convolutions too (else a split-K batched hipBLASLt GEMM).
-# 1x1 weight gradients on the implicit kernel too: 6.77-6.83 vs 6.82-6.88 ms/step (profiles/r2/ab_iwgrad_1x1.log)
-IWGRAD_1X1 = os.environ.get("GARFIELD_IWGRAD_1X1", "1") != "0"
-# The ResNet stem (7x7/2, 3 -> 64 channels) on its own implicit MFMA kernels (stem_nhwc.hip):
-# no im2col patch matrix in the forward or the weight gradient. "0" keeps im2col + GEMM.
-STEM = os.environ.get("GARFIELD_STEM", "1") != "0"
-_STEM_WG = int(os.environ.get("GARFIELD_STEM_WG", "1024"))   # weight-gradient workgroups to aim for
-# weight gradients on a side stream (see WgradStream): measured slower in the graphed step
-# (7.23 vs 7.07 ms: per-layer fork/join dependencies leave 8% of the window idle), so off
-WGRAD_STREAM = os.environ.get("GARFIELD_WGRAD_STREAM", "0")
-# "small": only layers with <= WGRAD_STREAM_ROWS output rows in the whole grouped batch (CIFAR
-# layer3/layer4), whose kernels are latency-bound and leave most CUs idle
-WGRAD_STREAM_ROWS = int(os.environ.get("GARFIELD_WGRAD_STREAM_ROWS", "8000"))
-XENT = os.environ.get("GARFIELD_XENT", "1") != "0"   # fused per-worker cross-entropy kernel
-# 1x1 stride-1 convolutions (forward and data gradient) on the hand-written MFMA GEMMs of
-# gemm_nt.hip instead of hipBLASLt: the weight-stationary persistent kernel for K <= 256, the
-# K-loop kernel otherwise. The forward also emits the next (large-layer) BatchNorm's
-# per-worker statistics from its registers, so that BatchNorm runs no partial-sum pass.
-# "0" keeps hipBLASLt (torch.mm / addmm_).
-GEMM_NT = os.environ.get("GARFIELD_GEMM_NT", "1") != "0"
-GEMM_NT_DGRAD = os.environ.get("GARFIELD_GEMM_NT_DGRAD", "1") != "0"
-# 3x3 / stride-1 / pad-1 convolutions on the halo-staged kernel (conv3x3_nhwc.hip) wherever its tiles
-# fit: the forward through gpu_iconv's automatic choice, the data gradient on the flipped transposed
-# weight (refresh_dgrad_weights). "0" keeps the implicit-GEMM kernel for both.
-CONV3X3 = os.environ.get("GARFIELD_CONV3X3", "1") != "0"
-# ... with the consuming BatchNorm's statistics from the forward's epilogue (bn_stats.hpp). Off by
-# default: on the ResNet-18 step the epilogue reductions (+25-100 µs per layer-1 launch) and the
-# per-wave tile merge (k_finalize_tiles) cost more than the partial-sum pass they remove
-# (profiles/r3/conv3x3/rocprof_r18_krum_f2_stats.txt).
-CONV3X3_STATS = os.environ.get("GARFIELD_CONV3X3_STATS", "0") != "0"
-# split-K weight-gradient sums of every layer deferred to one launch after the backward
-SPLIT_DEFER = os.environ.get("GARFIELD_SPLIT_DEFER", "1") != "0"
+# Kernel choices of the grouped step. Each was measured against the path it replaced (the
+# profiles cited at each switch's use); they stay module flags so tests can compare the two.
+# Implicit-GEMM MFMA convolutions (iconv_nhwc.hip) for the k x k layers whose channel counts fit its
+# tiles (C % 64, Cout % 64): forward, and the stride-1 data gradient as a convolution with the flipped
+# weight; else im2col + GEMM.
+ICONV = True
+# Their per-worker weight gradients by the implicit MFMA kernel (no im2col matrix) ...
+IWGRAD = True
+# ... and for the 1x1 stride-1 convolutions too: 6.77-6.83 vs 6.82-6.88 ms/step for the split-K batched
+# GEMM (profiles/r2/ab_iwgrad_1x1.log)
+IWGRAD_1X1 = True
+# The ResNet stem (7x7/2, 3 -> 64 channels) on its own implicit MFMA kernels (stem_nhwc.hip): no im2col
+# patch matrix in the forward or the weight gradient.
+STEM = True
+_STEM_WG = 1024   # stem weight-gradient workgroups to aim for
+XENT = True       # fused per-worker cross-entropy kernel (loss_xent.hip)
+# 1x1 stride-1 convolutions (forward and data gradient) on the hand-written MFMA GEMMs of gemm_nt.hip
+# instead of hipBLASLt: the weight-stationary persistent kernel for K <= 256, the K-loop kernel
+# otherwise. The forward also emits the next (large-layer) BatchNorm's per-worker statistics from its
+# registers, so that BatchNorm runs no partial-sum pass (profiles/r3/bench_gemm_nt.json.log).
+GEMM_NT = True
+GEMM_NT_DGRAD = True
+# 3x3 / stride-1 / pad-1 convolutions on the halo-staged kernel (conv3x3_nhwc.hip) wherever its tiles fit:
+# the forward through gpu_iconv's automatic choice, the data gradient on the flipped transposed weight
+# (refresh_dgrad_weights) (profiles/r3/conv3x3/).
+CONV3X3 = True
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -166,7 +146,7 @@ class GradSink:
     def queue_split(self, part: torch.Tensor, out: torch.Tensor) -> None:
         """Σ_s part[s] -> out, deferred to ``flush`` where every queued layer's split-K sum runs
         in ONE launch (the exchange rows are read only after the backward)."""
-        if SPLIT_DEFER and self.defer_splits and part.is_cuda:
+        if self.defer_splits and part.is_cuda:
             self._split_parts.append(part)
             self._split_outs.append(out)
         else:
@@ -360,8 +340,8 @@ class _GroupedBN(torch.autograd.Function):
         r2 = rows2d(res) if res is not None else None
         st.ensure(x.device, torch.float64 if x.dtype == torch.float64 else torch.float32)
         if x.is_cuda:
-            if x.dtype != torch.bfloat16:
-                raise TypeError("grouped BatchNorm on the GPU takes bf16 activations")
+            if x.dtype not in (torch.bfloat16, torch.float32):
+                raise TypeError("grouped BatchNorm on the GPU takes bf16 or fp32 activations")
             y = torch.empty_like(x, memory_format=torch.channels_last)
             bn = st.bn
             rg = x2.shape[0] // st.groups
@@ -450,6 +430,9 @@ class ConvSpec:
         self.dcol = False         # its data gradient runs dcol = dy · Wmat + col2im (Wmatᵀ refreshed per step)
         self.wd = None            # flipped transposed weight [Cin, Cout, 3, 3] of the halo-kernel data gradient
         self.flip = False         # its data gradient runs on the halo kernel (wd refreshed per step)
+        # fp32 step: the weight split into three bf16 pieces [3, Cout, K] and the channel-transposed
+        # pieces [3, Cin, KH, KW, Cout] of the data gradient (refresh_f32_weights, once per step)
+        self.w3 = self.wt3 = None
 
 
 def _gemm_nt_ok(a2: torch.Tensor, b2: torch.Tensor) -> bool:
@@ -463,8 +446,7 @@ def _gemm_nt_ok(a2: torch.Tensor, b2: torch.Tensor) -> bool:
 # Configuration of each gemm_nt problem, measured once: key (M, N, K, rg or 0, add) -> cfg. The
 # step's first (eager) run times every valid tile configuration on the real operands (scratch
 # outputs, 3 calls each after a warm call) and keeps the fastest; graph captures and replays
-# reuse it. GARFIELD_GEMM_TUNE=0 takes the static choice of gemm_nt_pick instead.
-GEMM_TUNE = os.environ.get("GARFIELD_GEMM_TUNE", "1") != "0"
+# reuse it (during a capture the static choice of gemm_nt_pick stands in).
 _GEMM_CFG: dict = {}
 
 
@@ -477,7 +459,7 @@ def _gemm_cfg(a2: torch.Tensor, b2: torch.Tensor, rg: int, add: torch.Tensor | N
     if cfg is not None:
         return cfg
     cfg = C_.gemm_nt_pick(M, N, K, rg)
-    if not GEMM_TUNE or cfg < 0 or torch.cuda.is_current_stream_capturing():
+    if cfg < 0 or torch.cuda.is_current_stream_capturing():
         return cfg
     cands = [c for c in range(C_.gemm_nt_num_cfg())
              if C_.gemm_nt_valid(c, N, K) and (rg == 0 or C_.gemm_nt_stats_rows(c) <= rg)]
@@ -595,31 +577,6 @@ def _flip_weight_buf(spec: "ConvSpec") -> torch.Tensor:
     return spec.wd
 
 
-def _halo_forward_stats(x: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> torch.Tensor | None:
-    """y = conv3x3(x, w) on the halo-staged kernel with the consuming (large-layer) BatchNorm's per-worker
-    statistics written by its epilogue (``spec.bn_next.tile``), so that BatchNorm runs no partial-sum
-    pass; None when the shape or the BatchNorm does not qualify."""
-    st = spec.bn_next
-    if not (CONV3X3 and CONV3X3_STATS and st is not None and x.is_cuda and x.dtype == torch.bfloat16 and spec.kernel == (3, 3)
-            and spec.stride == (1, 1) and spec.padding == (1, 1) and spec.dilation == (1, 1)):
-        return None
-    C_ = _native.native()
-    n, cin, h, wd = x.shape
-    cout = w.shape[0]
-    H = C_.conv3x3_stats_rows(n, h, wd, cin, cout)
-    M = n * h * wd
-    if H <= 0 or M % spec.groups:
-        return None
-    rg = M // spec.groups
-    if rg < H or C_.bn_small(rg):
-        return None
-    stats = torch.empty((-(-M // H) * 6 * cout,), dtype=torch.float32, device=x.device)
-    y = torch.empty((n, cout, h, wd), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-    C_.gpu_iconv(x, w, 3, 3, 1, 1, 1, 1, 1, 1, y, None, 0, False, stats, rg)
-    st.tile = (stats, H, 1)
-    return y
-
-
 def _halo_dgrad_ok(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> bool:
     """The 3x3 / stride-1 / pad-1 data gradient on the halo-staged kernel (conv3x3_nhwc.hip): a forward
     convolution of dy with the flipped transposed weight (refreshed once per step)."""
@@ -704,7 +661,7 @@ def _iconv_ok(x: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
             and -(-rows // 64) * (w.shape[0] // 64) >= _ICONV_MINWG)
 
 
-_ICONV_MINWG = int(os.environ.get("GARFIELD_ICONV_MINWG", "400"))   # tuning knob (workgroups)
+_ICONV_MINWG = 400   # workgroups (profiles/bench_iconv_r1.log)
 
 
 def _iconv(x: torch.Tensor, w: torch.Tensor, geom, out_hw, add: torch.Tensor | None = None,
@@ -746,14 +703,14 @@ def _wgrad3x3_splits(rows_per_worker: int, blocks: int) -> int:
     return S
 
 
-_WGRAD3_WG = int(os.environ.get("GARFIELD_WGRAD3X3_WG", "512"))
-_WGRAD3_MINTILES = int(os.environ.get("GARFIELD_WGRAD3X3_MINTILES", "1"))   # profiles/r3/conv3x3/bench_conv3x3_shapes.log
+_WGRAD3_WG = 512
+_WGRAD3_MINTILES = 1   # profiles/r3/conv3x3/bench_conv3x3_shapes.log
 
 
-# tuning knobs (profiles/iwgrad_split_sweep_r1.log; 512 since the 1x1 layers joined the
-# implicit kernel: profiles/r2/iwgrad_wg_nt_sweep.log)
-_IWGRAD_WG = int(os.environ.get("GARFIELD_IWGRAD_WG", "512"))
-_IWGRAD_MINPIX = int(os.environ.get("GARFIELD_IWGRAD_MINPIX", "256"))
+# profiles/iwgrad_split_sweep_r1.log; 512 since the 1x1 layers joined the implicit kernel
+# (profiles/r2/iwgrad_wg_nt_sweep.log)
+_IWGRAD_WG = 512
+_IWGRAD_MINPIX = 256
 
 
 def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int) -> None:
@@ -868,61 +825,122 @@ def _wgrad(dy2: torch.Tensor, a2: torch.Tensor, G: int, out: torch.Tensor | None
     return part.view(G, S, cout, K).float().sum(1)
 
 
-class WgradStream:
-    """Side stream for the per-worker weight gradients of the backward.
-
-    A layer's weight gradient and its data gradient are independent; the data
-    gradient feeds the next BatchNorm backward, a chain of short, latency-bound
-    kernels (few workgroups, one launch gap each) that leaves most CUs idle. The
-    weight-gradient GEMMs run on this stream, forked from the current stream at
-    each layer and joined once (``join``) before the exchange rows are read, so
-    they fill those gaps. Under HIP-graph capture the fork/join become parallel
-    graph branches. Operands are ``record_stream``-ed so the caching allocator
-    does not recycle them while the side stream still reads them."""
-
-    _streams: dict = {}
-    active: dict = {}
-
-    @classmethod
-    def fork(cls, *tensors: torch.Tensor):
-        dev = tensors[0].device
-        s = cls._streams.get(dev)
-        if s is None:
-            s = cls._streams[dev] = torch.cuda.Stream(device=dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        for t in tensors:
-            if t is not None:
-                t.record_stream(s)
-        cls.active[dev] = s
-        return torch.cuda.stream(s)
-
-    @classmethod
-    def join(cls, dev) -> None:
-        s = cls.active.pop(dev, None)
-        if s is not None:
-            torch.cuda.current_stream(dev).wait_stream(s)
+# --------------------------------------------------------------------------- #
+# fp32 (reference-precision) convolutions: conv_f32.hip / stem_nhwc.hip on split-bf16 MFMA
 
 
-def _wgrad_ctx(*tensors):
-    """Side-stream context for a weight-gradient computation (a no-op on CPU or when disabled).
-    ``tensors[-1]`` is the layer's output gradient dy (its rows decide the "small" mode)."""
-    if WGRAD_STREAM == "0" or not tensors[0].is_cuda:
-        return contextlib.nullcontext()
-    if WGRAD_STREAM == "small":
-        dy = tensors[-1]
-        rows = dy.numel() // dy.shape[1] if dy.dim() >= 2 else dy.numel()
-        if rows > WGRAD_STREAM_ROWS:
-            return contextlib.nullcontext()
-    return WgradStream.fork(*tensors)
+def _stem_shape(w: torch.Tensor, spec: "ConvSpec") -> bool:
+    return (tuple(w.shape) == (64, 3, 7, 7) and spec.stride == (2, 2) and spec.padding == (3, 3)
+            and spec.dilation == (1, 1))
+
+
+def _f32_conv_ok(x: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> bool:
+    """The fp32 step's own kernels take this convolution (raises on a GPU shape they cannot:
+    the fp32 grouped step never falls back to a library convolution)."""
+    if not (x.is_cuda and x.dtype == torch.float32):
+        return False
+    if _stem_shape(w, spec) and _native.native().stem_supported(x.shape[2], x.shape[3]):
+        return True
+    if w.shape[0] % 64 or (w.shape[1] % 64 and w.shape[1] % 32 == 0):
+        raise ValueError(f"fp32 grouped convolution: no kernel for {tuple(w.shape)} (Cout % 64; Cin % 64 or a "
+                         f"gathered Cin % 32 != 0)")
+    return True
+
+
+def _gathered(w: torch.Tensor) -> bool:
+    """Input channels the fp32 kernels gather one element at a time (e.g. a 3-channel first layer):
+    the split weight rows are the flattened (tap, channel) index padded to a multiple of 32."""
+    return w.shape[1] % 32 != 0
+
+
+def refresh_f32_weights(specs) -> None:
+    """The fp32 step's per-step weight split, ONE launch for the whole network: every convolution
+    weight W (fp32, channels_last) -> its bf16 pieces W0 = bf16(W), W1 = bf16(W - W0), W2 =
+    bf16(W - W0 - W1) [3, Cout, K] and the channel-transposed pieces [3, Cin, KH, KW, Cout] its data
+    gradient multiplies by; the stem's pieces are zero-padded [64, 160] matrices (stem_nhwc.hip)."""
+    jobs = []
+    for spec in specs:
+        w = spec.conv.weight
+        if not (w.is_cuda and w.dtype == torch.float32):
+            continue
+        if not _channels_last_weight(w):
+            raise ValueError("fp32 grouped convolution: the weight must be channels_last")
+        cout, cin, kh, kw = w.shape
+        wd = w.detach()
+        if _stem_shape(w, spec):
+            if spec.w3 is None or spec.w3.device != w.device:
+                spec.w3 = torch.zeros((3, 64, 160), dtype=torch.bfloat16, device=w.device)
+            jobs.append((wd, spec.w3, None, 64, 1, 147, 160))
+            continue
+        K = kh * kw * cin
+        if _gathered(w):   # a first layer (its data gradient is never taken): padded rows, no transposed pieces
+            kp = (K + 31) // 32 * 32
+            if spec.w3 is None or spec.w3.shape != (3, cout, kp) or spec.w3.device != w.device:
+                spec.w3 = torch.zeros((3, cout, kp), dtype=torch.bfloat16, device=w.device)
+            jobs.append((wd, spec.w3, None, cout, 1, K, kp))
+            continue
+        if spec.w3 is None or spec.w3.shape != (3, cout, K) or spec.w3.device != w.device:
+            spec.w3 = torch.empty((3, cout, K), dtype=torch.bfloat16, device=w.device)
+            spec.wt3 = torch.empty((3, cin, kh * kw * cout), dtype=torch.bfloat16, device=w.device)
+        jobs.append((wd, spec.w3, spec.wt3, cout, kh * kw, cin, 0))
+    if jobs:
+        _native.native().gpu_wsplit_multi(jobs)
+
+
+def _f32_forward(x: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> torch.Tensor:
+    if spec.w3 is None:
+        refresh_f32_weights([spec])
+    n, _, h, wd = x.shape
+    ho, wo = _out_hw(spec, h, wd)
+    y = torch.empty((n, w.shape[0], ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    if _stem_shape(w, spec):
+        _native.native().gpu_stem_fwd(x, spec.w3, y)
+    else:
+        _native.native().gpu_conv_f32(x, spec.w3, *_geom(spec), False, y)
+    return y
+
+
+def _f32_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", xshape, add: torch.Tensor | None):
+    """dx (+ add, written in place of add) of an fp32 convolution, any stride."""
+    dx = add if add is not None else torch.empty(xshape, dtype=dy.dtype, device=dy.device,
+                                                 memory_format=torch.channels_last)
+    _native.native().gpu_conv_f32(dy, spec.wt3, *_geom(spec), True, dx, add)
+    return dx
+
+
+def _f32_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> None:
+    """Per-worker fp32 weight gradients straight into the (fp32) exchange rows, or as split
+    slabs summed there by the deferred split-K reduction."""
+    C_ = _native.native()
+    w = spec.conv.weight
+    if _stem_shape(w, spec):
+        _stem_wgrad(x, dy, spec, G)
+        return
+    cout = dy.shape[1]
+    K = w.numel() // cout
+    rows = dy.shape[0] * dy.shape[2] * dy.shape[3] // G
+    S = _iwgrad_splits(rows, -(-K // 64) * (cout // 64) * G)
+    out = spec.sink.rows_view(w, (cout, K), torch.float32) if S == 1 else None
+    if out is not None:
+        C_.gpu_wgrad_f32(x, dy, *_geom(spec), G, out, 1)
+        return
+    part = torch.empty((S, G, cout, K), dtype=torch.float32, device=dy.device)
+    C_.gpu_wgrad_f32(x, dy, *_geom(spec), G, part, S)
+    rows_v = spec.sink.rows_view(w, (cout, K), spec.sink.flat.dtype)
+    if rows_v is not None:
+        spec.sink.queue_split(part, rows_v)
+    else:
+        spec.sink.put_groups(w, part.sum(0))
 
 
 class _GroupedConv(torch.autograd.Function):
     """Convolution over the grouped batch with per-worker weight gradients.
 
-    GPU, k x k kernels (``CONV_MODE == "gemm"``): im2col -> hipBLASLt GEMMs ->
+    GPU, k x k kernels: implicit-GEMM / halo-staged MFMA kernels, or im2col -> GEMMs ->
     col2im (im2col_nhwc.hip); the forward's col is kept for the weight gradient.
     1x1 stride-1 kernels are plain GEMMs on the NHWC rows. CPU (and
-    ``CONV_MODE == "miopen"``): ATen convolutions, per-worker weight gradients."""
+    shapes no kernel takes): ATen convolutions, per-worker weight gradients. fp32 activations take
+    the fp32 kernels (conv_f32.hip)."""
 
     @staticmethod
     def forward(ctx, x, w, spec: ConvSpec, join: GradJoin | None = None):
@@ -930,6 +948,10 @@ class _GroupedConv(torch.autograd.Function):
         ctx.join = join
         ctx.xshape = tuple(x.shape)
         n, _, h, wd = x.shape
+        if _f32_conv_ok(x, w, spec):
+            ctx.mode = "f32"
+            ctx.save_for_backward(x, w)
+            return _f32_forward(x, w, spec)
         if spec.gemm:
             ctx.mode = "rows"
             ctx.save_for_backward(x, w)
@@ -937,19 +959,18 @@ class _GroupedConv(torch.autograd.Function):
             if y2 is None:
                 y2 = torch.mm(rows2d(x), w.reshape(w.shape[0], -1).t())
             return from_rows(y2, n, h, wd)
-        if CONV_MODE == "gemm" and _stem_ok(x, w, spec):
+        if _stem_ok(x, w, spec):
             ctx.mode = "stem"
             ctx.save_for_backward(x, w)
             ho, wo = _out_hw(spec, h, wd)
             y = torch.empty((n, 64, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
             _native.native().gpu_stem_fwd(x, _wmat(w, 160, spec), y)
             return y
-        if CONV_MODE == "gemm" and _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
+        if _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
             ctx.mode = "iconv"
             ctx.save_for_backward(x, w)
-            y = _halo_forward_stats(x, w, spec)
-            return y if y is not None else _iconv(x, w, _geom(spec), _out_hw(spec, h, wd))
-        if x.is_cuda and CONV_MODE == "gemm" and _channels_last_weight(w):
+            return _iconv(x, w, _geom(spec), _out_hw(spec, h, wd))
+        if x.is_cuda and _channels_last_weight(w):
             ctx.mode = "col"
             col = _im2col(x, spec)
             ho, wo = _out_hw(spec, h, wd)
@@ -974,7 +995,16 @@ class _GroupedConv(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         prev = ctx.join.take() if (need_dx and ctx.join is not None) else None
         first = need_dx and ctx.join is not None and prev is None   # park dx for the other branch
-        if mode == "rows":                       # a = x
+        if mode == "f32":                        # a = x
+            if need_dx:
+                if _stem_shape(w, spec) or _gathered(w):   # a first layer: dx of the input, never wanted in training
+                    dx = _cl(_conv_bwd(dy, a, w, spec, [True, False, False])[0])
+                else:
+                    dx = _f32_dgrad(dy, w, spec, ctx.xshape, _cl(prev) if prev is not None else None)
+                    prev = None
+            if spec.sink is not None:
+                _f32_wgrad(a, dy, spec, G)
+        elif mode == "rows":                     # a = x
             if need_dx:
                 w2 = w.reshape(cout, -1)
                 if prev is not None:             # the other branch's gradient, folded into the GEMM
@@ -987,14 +1017,13 @@ class _GroupedConv(torch.autograd.Function):
                     dx = from_rows(d2 if d2 is not None else torch.mm(dy2, w2), n, h, wd)
             if spec.sink is not None:
                 K = w.numel() // cout
-                with _wgrad_ctx(a, dy):
-                    if IWGRAD_1X1 and _iwgrad_ok(a, dy):
-                        _iwgrad(a, dy, spec, G, K)
-                    else:
-                        out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype)
-                        dW = _wgrad(dy2, rows2d(a), G, out, spec.sink)
-                        if out is None:
-                            spec.sink.put_groups(spec.conv.weight, dW)
+                if IWGRAD_1X1 and _iwgrad_ok(a, dy):
+                    _iwgrad(a, dy, spec, G, K)
+                else:
+                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype)
+                    dW = _wgrad(dy2, rows2d(a), G, out, spec.sink)
+                    if out is None:
+                        spec.sink.put_groups(spec.conv.weight, dW)
         elif mode == "iconv":                    # a = x
             (kh, kw), (sh, sw), (ph, pw), (dh, dw) = spec.kernel, spec.stride, spec.padding, spec.dilation
             K = w.numel() // cout
@@ -1019,17 +1048,15 @@ class _GroupedConv(torch.autograd.Function):
                         _native.native().gpu_col2im(dcol, *_geom(spec), dx)
                 prev = None
             if use_iw:
-                with _wgrad_ctx(a, dy):
-                    _iwgrad(a, dy, spec, G, K)
+                _iwgrad(a, dy, spec, G, K)
             elif spec.sink is not None:
-                with _wgrad_ctx(col, dy):
-                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if (kp == K or dy2.is_cuda) \
-                        else None
-                    dW = _wgrad(dy2, col, G, out, spec.sink)
-                    if out is None:
-                        if kp != K:
-                            dW = dW[:, :, :K].contiguous()
-                        spec.sink.put_groups(spec.conv.weight, dW)
+                out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if (kp == K or dy2.is_cuda) \
+                    else None
+                dW = _wgrad(dy2, col, G, out, spec.sink)
+                if out is None:
+                    if kp != K:
+                        dW = dW[:, :, :K].contiguous()
+                    spec.sink.put_groups(spec.conv.weight, dW)
         elif mode == "stem":                     # a = x (the network input: dx is rarely wanted)
             if need_dx:
                 dx = _cl(_conv_bwd(dy, a, w, spec, [True, False, False])[0])
@@ -1053,14 +1080,13 @@ class _GroupedConv(torch.autograd.Function):
                 # dW_g[co, (i, j, ci)] = Σ_rows dy_g[row, co] · col_g[row, (i, j, ci)]: the
                 # weight's channels_last memory order, one batched GEMM for all workers
                 K = w.numel() // cout
-                with _wgrad_ctx(a, dy):
-                    out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if (kp == K or dy2.is_cuda) \
-                        else None
-                    dW = _wgrad(dy2, a, G, out, spec.sink)
-                    if out is None:
-                        if kp != K:
-                            dW = dW[:, :, :K].contiguous()
-                        spec.sink.put_groups(spec.conv.weight, dW)
+                out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy2.dtype) if (kp == K or dy2.is_cuda) \
+                    else None
+                dW = _wgrad(dy2, a, G, out, spec.sink)
+                if out is None:
+                    if kp != K:
+                        dW = dW[:, :, :K].contiguous()
+                    spec.sink.put_groups(spec.conv.weight, dW)
         else:                                    # a = x
             if need_dx:
                 dx = _cl(_conv_bwd(dy, a, w, spec, [True, False, False])[0])
@@ -1126,7 +1152,7 @@ class _MaxPool(torch.autograd.Function):
 
 def grouped_maxpool(x: torch.Tensor, mp: torch.nn.MaxPool2d) -> torch.Tensor:
     k, s, p, d = _pool_args(mp)
-    if (x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0 and d == 1 and not mp.ceil_mode
+    if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % 8 == 0 and d == 1 and not mp.ceil_mode
             and None not in (k, s, p) and 2 * p <= k and k * k <= 256):
         return _MaxPool.apply(_cl(x), int(k), int(s), int(p))
     y = F.max_pool2d(x, mp.kernel_size, mp.stride, mp.padding, mp.dilation, mp.ceil_mode)
@@ -1149,6 +1175,11 @@ class _GroupedLinear(torch.autograd.Function):
     def forward(ctx, x, w, b, spec: LinearSpec):
         ctx.spec = spec
         ctx.save_for_backward(x, w)
+        if x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32:   # the fp32 step's own kernel
+            y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+            _native.native().gpu_linear_f32_fwd(x.contiguous(), w.contiguous(),
+                                                b.detach() if b is not None else None, y)
+            return y
         return F.linear(x, w, b)
 
     @staticmethod
@@ -1157,6 +1188,8 @@ class _GroupedLinear(torch.autograd.Function):
         spec = ctx.spec
         G = spec.groups
         dy = dy.contiguous()
+        if dy.is_cuda and dy.dtype == torch.float32 and w.dtype == torch.float32:
+            return _linear_f32_backward(ctx, x, w, dy, spec, G)
         dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
         if spec.sink is not None:
             out, fin = dy.shape[1], x.shape[1]
@@ -1174,6 +1207,58 @@ class _GroupedLinear(torch.autograd.Function):
                 else:
                     spec.sink.put_groups(spec.lin.bias, _acc(dy3).sum(1))
         return dx, None, None, None
+
+
+def _linear_f32_backward(ctx, x, w, dy, spec: LinearSpec, G: int):
+    """fp32 classifier backward on the native kernels: dx = dy·W, and every worker's dW / db
+    written straight into its fp32 exchange row (or queued for the flatten kernel)."""
+    C_ = _native.native()
+    dx = None
+    if ctx.needs_input_grad[0]:
+        dx = torch.empty_like(x)
+        C_.gpu_linear_f32_dgrad(dy, w.contiguous(), dx)
+    sink = spec.sink
+    if sink is not None:
+        lin = spec.lin
+        if sink.flat.dtype == torch.float32 and sink.flat.is_cuda:
+            ob = sink.base + sink.offset(lin.bias) if lin.bias is not None else -1
+            C_.gpu_linear_f32_wgrad(x.contiguous(), dy, G, sink.flat, sink.row_stride, sink.base + sink.offset(lin.weight),
+                                    ob)
+        else:
+            x3 = x.contiguous().view(G, -1, x.shape[1])
+            dy3 = dy.view(G, -1, dy.shape[1])
+            sink.put_groups(lin.weight, torch.bmm(dy3.transpose(1, 2), x3))
+            if lin.bias is not None:
+                sink.put_groups(lin.bias, dy3.sum(1))
+    return dx, None, None, None
+
+
+class _AvgPoolF32(torch.autograd.Function):
+    """Global average pool of an fp32 NHWC activation on the native kernel (no ATen reduction)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        n, c, h, w = x.shape
+        y = torch.empty((n, c), dtype=x.dtype, device=x.device)
+        _native.native().gpu_avgpool_f32(x, y, False)
+        ctx.xshape = tuple(x.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        _native.native().gpu_avgpool_f32(dy.contiguous(), dx, True)
+        return dx
+
+
+def global_avgpool(x: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last -> [N, C] mean over H, W (a view when H = W = 1)."""
+    n, c, h, w = x.shape
+    if h * w == 1:
+        return x.reshape(n, c)
+    if x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last):
+        return _AvgPoolF32.apply(x)
+    return x.mean((2, 3))
 
 
 def grouped_linear(x, spec: LinearSpec):

@@ -55,9 +55,10 @@ LAYERWISE_RULES = {"krum", "bulyan", "brute", "aksel"}   # per-layer != flat onl
 # selection, one segmented combine + SGD); "0" runs the per-segment loop (the reference form).
 LW_DEVICE = os.environ.get("GARFIELD_LW_DEVICE", "1") != "0"
 LW_JOB = 32768   # coordinates per job of the segmented kernels (a multiple of 8)
-# fp32 (no autocast) worker batching on the GPU: the grouped-channel executor (parallel/grouped_fp32.py);
-# "0" keeps the per-worker path.
-FP32_GROUPED = os.environ.get("GARFIELD_FP32_GROUPED", "1") != "0"
+# fp32 (no autocast) worker batching on the GPU (the reference's precision): "1" (default) the grouped
+# NHWC executor on the fp32 kernels (conv_f32.hip, split-bf16 MFMA; bn_nhwc.hip in fp32), "channel" the
+# grouped-channel executor on ATen / hipBLASLt (parallel/grouped_fp32.py), "0" the per-worker path.
+FP32_GROUPED = os.environ.get("GARFIELD_FP32_GROUPED", "1")
 
 
 @dataclass
@@ -230,18 +231,24 @@ class RobustDataParallel:
         wb = self.cfg.worker_batching
         if wb is None:
             wb = self.device.type == "cuda"
-        self._fp32_grouped = False
+        self._fp32_grouped = False      # the grouped-channel executor (fp32, ATen)
+        self._fp32_nhwc = False         # the grouped NHWC executor in fp32 (own kernels)
         if not (wb and self._supports_grouping):
             return False
         if self.device.type == "cuda":
             # bf16 activations with bf16 working weights (the grouped kernels' contract)
             if self.cfg.lp_weights and self.cfg.autocast_dtype == torch.bfloat16:
                 return grouped.supports(model)
-            # the reference's fp32: the grouped-channel executor (ATen / MIOpen grouped convolutions)
-            if (self.cfg.autocast_dtype is None and not self.cfg.lp_weights and not self.cfg.channels_last
-                    and FP32_GROUPED and grouped_fp32.supports(model)):
-                self._fp32_grouped = True
-                return True
+            # the reference's fp32: fp32 activations and weights on the fp32 grouped kernels
+            if self.cfg.autocast_dtype is None and not self.cfg.lp_weights and FP32_GROUPED != "0":
+                if FP32_GROUPED == "channel":
+                    if not self.cfg.channels_last and grouped_fp32.supports(model):
+                        self._fp32_grouped = True
+                        return True
+                    return False
+                if grouped.supports(model):
+                    self._fp32_nhwc = True
+                    return True
             return False
         return grouped.supports(model)
 
@@ -737,19 +744,19 @@ class RobustDataParallel:
     def _ensure_gbuf(self, B: int, sample_shape: tuple, label_shape: tuple = (), label_dtype=torch.int64) -> None:
         shape = (self.k * B, *sample_shape)
         if self._gx is None or tuple(self._gx.shape) != shape:
-            fp32 = getattr(self, "_fp32_grouped", False)
+            fp32 = getattr(self, "_fp32_grouped", False) or getattr(self, "_fp32_nhwc", False)
             dt = torch.bfloat16 if (self.device.type == "cuda" and not fp32) else torch.float32
-            fmt = torch.contiguous_format if fp32 else torch.channels_last
+            fmt = torch.contiguous_format if getattr(self, "_fp32_grouped", False) else torch.channels_last
             self._gx = torch.empty(shape, dtype=dt, device=self.device, memory_format=fmt)
             self._gy = torch.empty((self.k * B, *label_shape), dtype=label_dtype, device=self.device)
             self._ggraph = None
             self._gsrc = None
 
     def grouped_inputs(self, batch: int, sample_shape, label_dtype=torch.int64):
-        """The grouped step's static input buffers ([k*batch, *sample_shape] channels_last, and
-        the labels) for a producer that writes each step's batch in place
+        """The grouped step's static input buffers ([k*batch, *sample_shape] channels_last, bf16 or
+        fp32 by the step's precision, and the labels) for a producer that writes each step's batch in place
         (``data.fresh.DeviceBatches.attach``): no staging copy. None when the step is not grouped."""
-        if self._gexec is None or getattr(self, "_fp32_grouped", False):   # the producer writes bf16 rows
+        if self._gexec is None or getattr(self, "_fp32_grouped", False):   # the producer writes NHWC rows
             return None
         self._ensure_gbuf(int(batch), tuple(sample_shape), (), label_dtype)
         return self._gx, self._gy

@@ -22,8 +22,8 @@ import torch.nn.functional as F
 from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
 from garfield_amd.parallel.signals import DeviceSignal
 from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, grouped_bn,
-                                      WgradStream, grouped_conv, grouped_cross_entropy, grouped_linear,
-                                      grouped_maxpool, refresh_dgrad_weights)
+                                      global_avgpool, grouped_conv, grouped_cross_entropy, grouped_linear,
+                                      grouped_maxpool, refresh_dgrad_weights, refresh_f32_weights)
 
 
 def supports(model: nn.Module) -> bool:
@@ -156,9 +156,7 @@ class GroupedResNet:
             for blk in getattr(m, name):
                 x = self._block(blk, x)
         self.ws.flush_running()
-        n, c, h, w = x.shape
-        pooled = x.reshape(n, c) if h * w == 1 else x.mean((2, 3))
-        return grouped_linear(pooled, self.fc)
+        return grouped_linear(global_avgpool(x), self.fc)
 
     def losses(self, logits: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         G = self.groups
@@ -173,7 +171,9 @@ class GroupedResNet:
     def run(self, x: torch.Tensor, y: torch.Tensor, loss_out: torch.Tensor | None = None) -> torch.Tensor:
         if x.shape[0] % self.groups:
             raise ValueError(f"batch of {x.shape[0]} rows is not divisible into {self.groups} workers")
-        if x.is_cuda:
+        if x.is_cuda and x.dtype == torch.float32:
+            refresh_f32_weights(self.conv.values())     # the fp32 step's split weights: one launch
+        elif x.is_cuda:
             refresh_dgrad_weights(self.conv.values())   # Wᵀ of every 1x1 layer: one launch
         per = self.losses(self.forward(x), y)
         # d(Σ_g loss_g)/d loss_g = 1: seeded directly (no sum / fill / expand kernels)
@@ -181,8 +181,6 @@ class GroupedResNet:
                 or self._seed.dtype != per.dtype:
             self._seed = torch.ones_like(per)
         per.backward(self._seed)
-        if x.is_cuda:
-            WgradStream.join(x.device)   # weight gradients computed on the side stream
         self.sink.flush()
         if self._end is not None:
             self._end.record(torch.cuda.current_stream(x.device))

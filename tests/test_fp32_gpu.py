@@ -1,0 +1,304 @@
+"""The reference-precision (fp32) grouped step on MI355X: conv_f32.hip (split-bf16 MFMA: three
+bf16 pieces per operand, the six products of order <= 2, fp32 accumulation), the fp32 forms of bn_nhwc.hip / stem_nhwc.hip /
+the max pool / the classifier, each against a float64 PyTorch reference of the same op, and a
+whole ResNet step's per-worker gradient rows against fp32 autograd of the workers run one by one
+(the reference trains in fp32: Garfield_CC/trainer.py:296-303)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from garfield_amd.models import build_model
+from garfield_amd.parallel.comm import DistContext
+from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synthetic_batches
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _split(native, w):
+    """The three bf16 pieces [3, Cout, K] and the transposed pieces [3, Cin, KH, KW, Cout] of an fp32 weight."""
+    cout, cin, kh, kw = w.shape
+    w = cl(w)
+    p = torch.empty((3, cout, kh * kw * cin), dtype=torch.bfloat16, device=w.device)
+    t = torch.empty((3, cin, kh * kw * cout), dtype=torch.bfloat16, device=w.device)
+    native.gpu_wsplit_multi([(w, p, t, cout, kh * kw, cin, 0)])
+    return p, t
+
+
+def _pieces(v):
+    out, r = [], v.clone()
+    for _ in range(3):
+        out.append(r.to(torch.bfloat16))
+        r = r - out[-1].float()
+    return torch.stack(out)
+
+
+def test_weight_split_pieces(cuda, native):
+    w = torch.randn(128, 64, 3, 3, device=cuda)
+    p, t = _split(native, w)
+    wr = cl(w).permute(0, 2, 3, 1).reshape(128, -1)
+    assert torch.equal(p, _pieces(wr))
+    assert rel(p.double().sum(0), wr) < 1e-7                 # three pieces carry fp32's 24 bits
+    wt = cl(w).permute(1, 2, 3, 0).reshape(64, -1)          # [Cin][KH][KW][Cout]
+    assert torch.equal(t, _pieces(wt))
+
+
+TOL = 1e-6   # fp32-level: the three-piece products lose ~2^-26, under fp32's own rounding of the sums
+
+SHAPES = [  # N, Cin, Cout, H, k, s, p
+    (6, 64, 64, 8, 3, 1, 1), (4, 64, 256, 8, 1, 1, 0), (5, 256, 64, 8, 1, 1, 0), (3, 128, 128, 8, 3, 2, 1),
+    (4, 256, 512, 4, 1, 2, 0), (9, 512, 512, 2, 3, 1, 1), (2, 64, 128, 7, 3, 2, 1), (3, 64, 192, 5, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("pm", [0, 2])
+@pytest.mark.parametrize("N,C,Co,H,k,s,p", SHAPES)
+def test_conv_f32_forward_dgrad_match_fp64(cuda, native, N, C, Co, H, k, s, p, pm):
+    """Forward (with and without a fused add) and the data gradient (any stride: the transposed
+    convolution, by parity class on the LDS-staged kernel) against float64 convolutions, on the
+    automatic choice (the LDS-staged kernel) and on the register kernel (pm = 2)."""
+    x = cl(torch.randn(N, C, H, H, device=cuda))
+    w = cl(torch.randn(Co, C, k, k, device=cuda) / (C * k * k) ** 0.5)
+    w3, wt3 = _split(native, w)
+    ref = F.conv2d(x.double(), w.double(), None, s, p)
+    y = cl(torch.empty(ref.shape, device=cuda))
+    native.gpu_conv_f32(x, w3, k, k, s, s, p, p, 1, 1, False, y, None, pm)
+    assert rel(y, ref) < TOL
+    add = cl(torch.randn(ref.shape, device=cuda))
+    y2 = add.clone()
+    native.gpu_conv_f32(x, w3, k, k, s, s, p, p, 1, 1, False, y2, y2, pm)
+    assert rel(y2, ref + add.double()) < TOL
+    dy = cl(torch.randn(ref.shape, device=cuda))
+    dref = torch.nn.grad.conv2d_input(x.shape, w.double(), dy.double(), s, p)
+    dx = cl(torch.empty(x.shape, device=cuda))
+    dx = cl(torch.full(x.shape, float("nan"), device=cuda))   # every pixel is written (zero-tap classes too)
+    native.gpu_conv_f32(dy, wt3, k, k, s, s, p, p, 1, 1, True, dx, None, pm)
+    assert rel(dx, dref) < TOL
+
+
+@pytest.mark.parametrize("G,B,C,Co,H,k,s,p,S", [(4, 3, 64, 64, 8, 3, 1, 1, 1), (4, 3, 64, 64, 8, 3, 1, 1, 4),
+                                                (3, 5, 128, 256, 8, 1, 1, 0, 2), (8, 2, 128, 128, 8, 3, 2, 1, 1),
+                                                (2, 7, 256, 512, 4, 1, 2, 0, 3), (8, 4, 512, 512, 1, 3, 1, 1, 1)])
+def test_wgrad_f32_matches_per_worker_fp64(cuda, native, G, B, C, Co, H, k, s, p, S):
+    x = cl(torch.randn(G * B, C, H, H, device=cuda))
+    Ho = (H + 2 * p - k) // s + 1
+    dy = cl(torch.randn(G * B, Co, Ho, Ho, device=cuda))
+    K = k * k * C
+    part = torch.full((S, G, Co, K), float("nan"), device=cuda)
+    native.gpu_wgrad_f32(x, dy, k, k, s, s, p, p, 1, 1, G, part, S)
+    for g in range(G):
+        sl = slice(g * B, (g + 1) * B)
+        dw = torch.nn.grad.conv2d_weight(x[sl].double(), (Co, C, k, k), dy[sl].double(), s, p)
+        assert rel(part[:, g].sum(0), dw.permute(0, 2, 3, 1).reshape(Co, K)) < TOL
+    if S == 1:   # straight into strided exchange rows
+        rows = torch.zeros(G, Co * K + 100, device=cuda)
+        view = rows.as_strided((G, Co, K), (Co * K + 100, K, 1), 0)
+        native.gpu_wgrad_f32(x, dy, k, k, s, s, p, p, 1, 1, G, view, 1)
+        assert torch.equal(view, part[0])
+        assert rows[:, Co * K:].abs().max() == 0
+
+
+@pytest.mark.parametrize("C,k,s,p", [(3, 3, 1, 1), (16, 3, 1, 1), (3, 5, 2, 2)])
+def test_conv_f32_gathered_first_layer(cuda, native, C, k, s, p):
+    """Cin % 32 != 0 (the CIFAR ResNet's 3-channel 3x3 first layer): forward and per-worker weight
+    gradient with the (tap, channel) index gathered element by element."""
+    from garfield_amd.ops.grouped import ConvSpec, refresh_f32_weights
+
+    G, B, H = 3, 4, 12
+    conv = torch.nn.Conv2d(C, 64, k, s, p, bias=False).to(cuda).to(memory_format=torch.channels_last)
+    spec = ConvSpec(conv, None, G)
+    refresh_f32_weights([spec])
+    x = cl(torch.randn(G * B, C, H, H, device=cuda))
+    ref = F.conv2d(x.double(), conv.weight.double(), None, s, p)
+    y = cl(torch.empty(ref.shape, device=cuda))
+    native.gpu_conv_f32(x, spec.w3, k, k, s, s, p, p, 1, 1, False, y)
+    assert rel(y, ref) < TOL
+    dy = cl(torch.randn(ref.shape, device=cuda))
+    K = k * k * C
+    part = torch.full((2, G, 64, K), float("nan"), device=cuda)
+    native.gpu_wgrad_f32(x, dy, k, k, s, s, p, p, 1, 1, G, part, 2)
+    for g in range(G):
+        sl = slice(g * B, (g + 1) * B)
+        dw = torch.nn.grad.conv2d_weight(x[sl].double(), (64, C, k, k), dy[sl].double(), s, p)
+        assert rel(part[:, g].sum(0), dw.permute(0, 2, 3, 1).reshape(64, K)) < TOL
+
+
+@pytest.mark.parametrize("G,B,H,W,S", [(2, 3, 32, 32, 1), (3, 2, 32, 32, 4), (2, 2, 33, 20, 2), (2, 1, 224, 224, 2)])
+def test_stem_f32_matches_fp64(cuda, native, G, B, H, W, S):
+    """The fp32 (split) stem: forward and per-worker weight gradient (banded at 224 x 224)."""
+    from garfield_amd.ops.grouped import ConvSpec, refresh_f32_weights
+
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(cuda).to(memory_format=torch.channels_last)
+    spec = ConvSpec(conv, None, G)
+    refresh_f32_weights([spec])
+    x = cl(torch.randn(G * B, 3, H, W, device=cuda))
+    ref = F.conv2d(x.double(), conv.weight.double(), None, 2, 3)
+    y = cl(torch.empty(ref.shape, device=cuda))
+    native.gpu_stem_fwd(x, spec.w3, y)
+    assert rel(y, ref) < TOL
+    dy = cl(torch.randn(ref.shape, device=cuda))
+    part = torch.full((S, G, 64, 147), float("nan"), device=cuda)
+    native.gpu_stem_wgrad(x, dy, G, part)
+    for g in range(G):
+        sl = slice(g * B, (g + 1) * B)
+        dw = torch.nn.grad.conv2d_weight(x[sl].double(), (64, 3, 7, 7), dy[sl].double(), 2, 3)
+        assert rel(part[:, g].sum(0), dw.permute(0, 2, 3, 1).reshape(64, 147)) < TOL
+
+
+def test_stem_bf16_imagenet_banded(cuda, native):
+    """224 x 224 crops on the bf16 stem kernels (the weight gradient stages the image in bands)."""
+    from garfield_amd.ops.grouped import _wmat
+    assert native.stem_supported(224, 224) and not native.stem_supported(32, 4000)
+    G, B = 2, 2
+    x = torch.randn(G * B, 3, 224, 224, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, device=cuda) / 12).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.float(), w.float(), None, 2, 3)
+    y = torch.empty(ref.shape, dtype=torch.bfloat16, device=cuda, memory_format=torch.channels_last)
+    native.gpu_stem_fwd(x, _wmat(w, 160).contiguous(), y)
+    assert rel(y.float(), ref) < 1e-2
+    dy = torch.randn(ref.shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    part = torch.full((3, G, 64, 147), float("nan"), device=cuda)
+    native.gpu_stem_wgrad(x, dy, G, part)
+    for g in range(G):
+        sl = slice(g * B, (g + 1) * B)
+        dw = torch.nn.grad.conv2d_weight(x[sl].float(), (64, 3, 7, 7), dy[sl].float(), 2, 3)
+        assert rel(part[:, g].sum(0), dw.permute(0, 2, 3, 1).reshape(64, 147)) < 1e-2
+
+
+@pytest.mark.parametrize("G,B,H,C,relu,res", [(8, 16, 4, 64, True, False), (4, 8, 2, 256, True, True),
+                                              (2, 9, 1, 2048, True, True), (2, 40, 8, 64, False, False)])
+def test_bn_f32_forward_backward_match_fp64(cuda, G, B, H, C, relu, res):
+    """bn_nhwc.hip in fp32 (both the small-layer and the three-pass forms) vs float64 autograd of
+    each worker's BatchNorm (+ residual) (+ ReLU), including dγ/dβ in the exchange rows."""
+    from garfield_amd.ops.grouped import BNState, GradSink, Workspace, grouped_bn
+
+    torch.manual_seed(0)
+    bn = torch.nn.BatchNorm2d(C).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    flat = torch.zeros(G * 4 * C, device=cuda)
+    sink = GradSink(flat, 4 * C, 0, {id(bn.weight): 0, id(bn.bias): C}, G)
+    st = BNState(bn, relu, sink, G)
+    x = cl(torch.randn(G * B, C, H, H, device=cuda) * 3 + 1).requires_grad_(True)
+    r = cl(torch.randn(G * B, C, H, H, device=cuda)).requires_grad_(True) if res else None
+    y = grouped_bn(x, st, Workspace(), r)
+    dy = cl(torch.randn(y.shape, device=cuda))
+    y.backward(dy)
+    for g in range(G):
+        sl = slice(g * B, (g + 1) * B)
+        xg = x[sl].detach().double().requires_grad_(True)
+        w = bn.weight.detach().double().requires_grad_(True)
+        b = bn.bias.detach().double().requires_grad_(True)
+        yr = F.batch_norm(xg, None, None, w, b, True, 0.0, bn.eps)
+        rg = None
+        if res:
+            rg = r[sl].detach().double().requires_grad_(True)
+            yr = yr + rg
+        if relu:
+            yr = yr.clamp_min(0)
+        yr.backward(dy[sl].double())
+        assert rel(y[sl], yr) < 1e-5
+        assert rel(x.grad[sl], xg.grad) < 1e-5
+        assert rel(flat[g * 4 * C: g * 4 * C + C], w.grad) < 1e-5
+        assert rel(flat[g * 4 * C + C: g * 4 * C + 2 * C], b.grad) < 1e-5
+        if res:
+            assert rel(r.grad[sl], rg.grad) < 1e-5
+
+
+def test_linear_avgpool_maxpool_f32(cuda, native):
+    G, B, C, H, O = 4, 6, 64, 5, 10
+    x = cl(torch.randn(G * B, C, H, H, device=cuda))
+    pooled = torch.empty(G * B, C, device=cuda)
+    native.gpu_avgpool_f32(x, pooled, False)
+    assert rel(pooled, x.double().mean((2, 3))) < 1e-6
+    dp = torch.randn(G * B, C, device=cuda)
+    dx = cl(torch.empty_like(x))
+    native.gpu_avgpool_f32(dp, dx, True)
+    assert rel(dx, (dp.double() / (H * H))[:, :, None, None].expand(-1, -1, H, H)) < 1e-6
+    w, b = torch.randn(O, C, device=cuda), torch.randn(O, device=cuda)
+    y = torch.empty(G * B, O, device=cuda)
+    native.gpu_linear_f32_fwd(pooled, w, b, y)
+    assert rel(y, pooled.double() @ w.double().T + b.double()) < 1e-6
+    dl = torch.randn(G * B, O, device=cuda)
+    dxp = torch.empty_like(pooled)
+    native.gpu_linear_f32_dgrad(dl, w, dxp)
+    assert rel(dxp, dl.double() @ w.double()) < 1e-6
+    stride = O * C + O + 7
+    rows = torch.zeros(G * stride, device=cuda)
+    native.gpu_linear_f32_wgrad(pooled, dl, G, rows, stride, 3, 3 + O * C)
+    for g in range(G):
+        sl = slice(g * B, (g + 1) * B)
+        assert rel(rows[g * stride + 3: g * stride + 3 + O * C], (dl[sl].double().T @ pooled[sl].double()).flatten()) < 1e-6
+        assert rel(rows[g * stride + 3 + O * C: g * stride + 3 + O * C + O], dl[sl].double().sum(0)) < 1e-6
+    mx = cl(torch.randn(3, 64, 9, 9, device=cuda))
+    from garfield_amd.ops.grouped import grouped_maxpool
+    mp = torch.nn.MaxPool2d(3, 2, 1)
+    xr = mx.clone().requires_grad_(True)
+    ym = grouped_maxpool(xr, mp)
+    ref = F.max_pool2d(mx.double().requires_grad_(True), 3, 2, 1)
+    assert torch.equal(ym.double(), ref.detach())
+    gy = cl(torch.randn(ym.shape, device=cuda))
+    ym.backward(gy)
+    xd = mx.double().requires_grad_(True)
+    F.max_pool2d(xd, 3, 2, 1).backward(gy.double())
+    assert rel(xr.grad, xd.grad) < 1e-7
+
+
+def _fp32_rows_vs_autograd(cuda, name, k, B, shape=(3, 32, 32)):
+    torch.manual_seed(0)
+    ref = build_model(name, 10).to(cuda)
+    eng = RobustDataParallel(build_model(name, 10), F.cross_entropy, DistContext(device=cuda),
+                             EngineConfig(gar="average", f=0, workers_per_rank=k, exchange_dtype=torch.float32,
+                                          autocast_dtype=None, lp_weights=False, lr=0.0, momentum=0.0,
+                                          weight_decay=0.0, cuda_graph=False, worker_batching=True))
+    assert eng._gexec is not None and eng._fp32_nhwc
+    with torch.no_grad():
+        for p, v in zip(ref.parameters(), eng.flat.params):
+            p.copy_(v)
+    b = synthetic_batches(k, B, shape, 10, cuda)
+    eng.step(b)
+    torch.cuda.synchronize()
+    ref.train()
+    errs = []
+    for j, (x, y) in enumerate(b):
+        ref.zero_grad()
+        F.cross_entropy(ref(x.float().contiguous()), y).backward()
+        g_ref = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
+        g_eng = torch.cat([v.reshape(-1) for v in eng.flat.views(eng.X[j, 0])])
+        errs.append(rel(g_eng, g_ref))
+    return errs
+
+
+@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
+def test_fp32_grouped_rows_match_fp32_autograd(cuda, name):
+    """The fp32 grouped step (own kernels, no library GEMM) gives every worker's gradient row
+    within 1e-4 relative error of fp32 autograd run worker by worker."""
+    errs = _fp32_rows_vs_autograd(cuda, name, 4, 8)
+    assert max(errs) < 1e-4, errs
+
+
+def test_fp32_grouped_graph_step_matches_eager(cuda):
+    """The fp32 grouped step captured as one HIP graph replays what the eager step computes."""
+    def run(graph):
+        torch.manual_seed(0)
+        eng = RobustDataParallel(build_model("resnet18", 10), F.cross_entropy, DistContext(device=cuda),
+                                 EngineConfig(gar="krum", f=1, workers_per_rank=5, exchange_dtype=torch.float32,
+                                              autocast_dtype=None, lp_weights=False, lr=0.05, cuda_graph=graph,
+                                              worker_batching=True))
+        b = synthetic_batches(5, 6, (3, 32, 32), 10, cuda)
+        for _ in range(4):
+            eng.step(b)
+        torch.cuda.synchronize()
+        return eng.flat_model().clone(), eng._ggraph is not None
+    a, ga = run(False)
+    c, gc = run(True)
+    assert gc and not ga
+    assert rel(c, a) < 1e-6
