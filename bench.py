@@ -83,8 +83,8 @@ def parse():
     p.add_argument("--f", type=int, default=2)
     p.add_argument("--exchange-dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
-                   help="fp32: the reference's precision end to end (no autocast, fp32 exchange rows, fp32 weights; "
-                        "per-worker HIP graphs, since the grouped NHWC kernels are bf16)")
+                   help="fp32: the reference's precision end to end (no autocast, fp32 exchange rows, fp32 weights: "
+                        "the grouped NHWC executor on the fp32 kernels)")
     p.add_argument("--channels-last", action="store_true")
     p.add_argument("--overhead", action="store_true",
                    help="also time the same job with the 'average' GAR and report the Krum overhead")
@@ -115,6 +115,9 @@ def parse():
                         "crop + flip + normalise (data_aug.hip, one launch); static: the same batches every step")
     p.add_argument("--dataset-size", type=int, default=0,
                    help="images in the synthetic dataset (default 50000 CIFAR-shape, 2000 ImageNet-shape)")
+    p.add_argument("--no-fp32", action="store_true",
+                   help="skip the companion run at the reference's precision (fp32_ms_per_step / fp32_img_per_s: "
+                        "the same job with fp32 activations, weights and exchange rows on the fp32 kernels)")
     p.add_argument("--lr", type=float, default=0.01,
                    help="0.01: the reference lr (0.2) diverges from random init on the synthetic data")
     return p.parse_args()
@@ -150,33 +153,17 @@ def timed_steps(eng, batches, steps, warmup, ctx, trend=None):
     return elapsed, float(loss)
 
 
-def main():
-    a = parse()
-    ctx = init_distributed()
-    if a.cudnn_benchmark:
-        torch.backends.cudnn.benchmark = True
-    world = ctx.world_size
-    if world != a.gpus:
-        raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {world} ranks "
-                         f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')}); refusing to report a mislabelled number")
-    if world > 1:
-        assert ctx.is_distributed and dist.get_world_size() == a.gpus, "process group not initialised"
-    shape = (3, 32, 32) if a.dataset == "cifar10" else (3, 224, 224)
-    num_classes = 10 if a.dataset == "cifar10" else 1000
-    torch.manual_seed(1234)
-    model = build_model(a.model, num_classes=num_classes)
-    d = num_parameters(model)
-    fp32 = a.precision == "fp32"
-    if fp32:
-        a.exchange_dtype, a.no_lp_weights = "fp32", True   # worker batching: the grouped NHWC executor in fp32
-    xdt = torch.bfloat16 if a.exchange_dtype == "bf16" else torch.float32
+def build_job(a, ctx, model, shape, num_classes, fp32: bool):
+    """The engine of the benchmarked job and its batch source; fp32: the reference's precision
+    (no autocast, fp32 exchange rows and weights: the grouped NHWC executor on the fp32 kernels)."""
+    exchange, lp = ("fp32", False) if fp32 else (a.exchange_dtype, not a.no_lp_weights)
+    xdt = torch.bfloat16 if exchange == "bf16" else torch.float32
     amp = {} if not fp32 else {"autocast_dtype": None}
     cfg = EngineConfig(gar=a.gar, f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
                        weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
-                       cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=not a.no_lp_weights,
+                       cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=lp,
                        worker_batching=False if a.no_worker_batching else None,
-                       shard_gar=True if a.shard_gar else (False if a.layerwise else None),
-                       layerwise=a.layerwise, **amp)
+                       shard_gar=True if a.shard_gar else None, layerwise=a.layerwise, **amp)
     if a.num_ps:
         from dataclasses import asdict
 
@@ -201,6 +188,29 @@ def main():
     else:
         batches = synthetic_batches(a.workers_per_gpu, a.batch, shape, num_classes, ctx.device,
                                     seed=1000 + ctx.rank, channels_last=a.channels_last)
+        if fp32:
+            batches = [(x.float(), y) for x, y in batches]
+    return eng, batches, xdt, amp
+
+
+def main():
+    a = parse()
+    ctx = init_distributed()
+    if a.cudnn_benchmark:
+        torch.backends.cudnn.benchmark = True
+    world = ctx.world_size
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {world} ranks "
+                         f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')}); refusing to report a mislabelled number")
+    if world > 1:
+        assert ctx.is_distributed and dist.get_world_size() == a.gpus, "process group not initialised"
+    shape = (3, 32, 32) if a.dataset == "cifar10" else (3, 224, 224)
+    num_classes = 10 if a.dataset == "cifar10" else 1000
+    torch.manual_seed(1234)
+    model = build_model(a.model, num_classes=num_classes)
+    d = num_parameters(model)
+    fp32 = a.precision == "fp32"
+    eng, batches, xdt, amp = build_job(a, ctx, model, shape, num_classes, fp32)
     if a.resume:
         from garfield_amd.utils.checkpoint import load_engine
 
@@ -253,6 +263,15 @@ def main():
         extra["ref_impl_ms_per_step"] = round(ms_ref, 3)
         extra["ref_impl_img_per_s"] = round(n * a.batch / (ms_ref / 1000.0), 2)
         extra["speedup_vs_ref_impl"] = round(ms_ref / ms, 3)
+    if not fp32 and not a.no_fp32 and not a.num_ps:
+        # the reference's precision, same job, same invocation: fp32 activations / weights / exchange rows
+        # on the fp32 kernels (conv_f32.hip: split-bf16 MFMA; bn_nhwc.hip and the rest in fp32)
+        torch.manual_seed(1234)
+        eng32, b32, _, _ = build_job(a, ctx, build_model(a.model, num_classes=num_classes), shape, num_classes, True)
+        e32, loss32 = timed_steps(eng32, b32, a.steps, a.warmup, ctx)
+        ms32 = 1000.0 * e32 / a.steps
+        extra.update({"fp32_ms_per_step": round(ms32, 3), "fp32_img_per_s": round(n * a.batch / (ms32 / 1000.0), 2),
+                      "fp32_final_loss": round(loss32, 4), "fp32_worker_batching": eng32._gexec is not None})
     if ctx.rank == 0:
         default = (a.model, a.gar, a.f, a.dataset) == ("resnet50", "krum", 2, "cifar10")
         gar_name = {"krum": "Multi-Krum"}.get(a.gar, a.gar)

@@ -130,7 +130,7 @@ def main(argv=None, results: dict | None = None):
     common = dict(gar=gar_name, f=a.fw, workers_per_rank=k, lr=a.lr, momentum=a.momentum, weight_decay=a.wd,
                   exchange_dtype=xdt, byzantine=byz, cuda_graph=a.cuda_graph)
     if a.layerwise:
-        common.update(layerwise=True, shard_gar=False)
+        common.update(layerwise=True)
     if byz_mode:
         eng = ByzantinePSDataParallel(model, loss_fn, ctx,
                                       ByzPSConfig(num_ps=a.num_ps, fps=a.fps, mar=mar, ps_attack=a.ps_attack,

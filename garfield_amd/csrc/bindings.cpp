@@ -816,6 +816,22 @@ void g_lw_combine_sgd(const RowSet& rs, const at::Tensor& jobs, const at::Tensor
                                 stream_of(rs.device));
 }
 
+void g_lw_bulyan_tail(const RowSet& rs, const at::Tensor& jobs, const at::Tensor& W, int64_t t, int64_t beta,
+                      const at::Tensor& out) {
+  check_gpu(rs);
+  TORCH_CHECK(jobs.device() == rs.device && jobs.scalar_type() == at::kLong && jobs.dim() == 2 && jobs.size(1) == 3 &&
+                  jobs.is_contiguous(), "gpu_lw_bulyan_tail: jobs must be a contiguous int64 [J, 3] tensor");
+  TORCH_CHECK(t >= 1 && t <= 64 && beta >= 1 && beta <= t, "gpu_lw_bulyan_tail: 1 <= beta <= t <= 64");
+  TORCH_CHECK(W.device() == rs.device && W.scalar_type() == at::kFloat && W.is_contiguous() &&
+                  W.numel() % (t * rs.n) == 0, "gpu_lw_bulyan_tail: W must be a contiguous fp32 [L, t, n] tensor");
+  TORCH_CHECK(out.device() == rs.device && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() >= rs.d,
+              "gpu_lw_bulyan_tail: out must be a contiguous fp32 vector of >= d elements");
+  c10::hip::HIPGuard guard(rs.device.index());
+  garfield::gpu::lw_bulyan_tail(rs.table, rs.n, rs.dt, jobs.data_ptr<int64_t>(), static_cast<int>(jobs.size(0)),
+                                fptr(W), static_cast<int>(t), static_cast<int>(beta), out.data_ptr<float>(),
+                                stream_of(rs.device));
+}
+
 // Large gradient sets: x an [n, d] GPU matrix (unit column stride, row stride ld, 16-bit or fp32).
 int large_dtype(const at::Tensor& x, const at::Tensor& out) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 && x.size(0) >= 1 &&
@@ -1526,6 +1542,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
               const at::Tensor& gram) { g_lw_gram(rows_from_list(L, true), jobs, seg_lo, slabs, gram); },
            "Per-segment MFMA Gram matrices of the rows: gram [L, np, np]; jobs [J, 3] int64 (start, end, segment) "
            "ranges inside one segment each, in segment order; seg_lo [L + 1] int32 first job per segment");
+  def_rows(m, "gpu_lw_bulyan_tail",
+           [](const at::Tensor& G, const at::Tensor& jobs, const at::Tensor& W, int64_t t, int64_t beta,
+              const at::Tensor& out) { g_lw_bulyan_tail(rows_from_2d(G, true), jobs, W, t, beta, out); },
+           [](const std::vector<at::Tensor>& L, const at::Tensor& jobs, const at::Tensor& W, int64_t t, int64_t beta,
+              const at::Tensor& out) { g_lw_bulyan_tail(rows_from_list(L, true), jobs, W, t, beta, out); },
+           "Layer-wise Bulyan's tail: out[x] = the averaged median (beta) of the t selection means of x's "
+           "segment (W [L, t, n] fp32, jobs (start, end, segment) in local coordinates)");
   def_rows(m, "gpu_lw_combine_sgd",
            [](const at::Tensor& G, const at::Tensor& jobs, const at::Tensor& seg_off, int64_t base, const at::Tensor& w,
               const at::Tensor& p, const at::Tensor& mom, const c10::optional<at::Tensor>& sh, double lr, double mo,
@@ -1540,11 +1563,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "Per-segment weighted combine of the rows (weights [L, n]) fused with the SGD update; args (rows, jobs "
            "(local coordinates), seg_off (global), base (global coordinate of local 0), weights, param, mom, "
            "shadow|None, lr, momentum, dampening, weight_decay, nesterov, first_step)");
-  m.def("gpu_bulyan_select", [](const at::Tensor& gram, int n, int f, int mm, int t, const at::Tensor& W) {
+  m.def("gpu_bulyan_select", [](const at::Tensor& gram, int n, int f, int mm, int t, const at::Tensor& W, int batch) {
     c10::hip::HIPGuard guard(gram.device().index());
-    TORCH_CHECK(W.numel() >= static_cast<int64_t>(t) * n, "W too small");
-    garfield::gpu::bulyan_select(fptr(gram), garfield::gpu::gram_padded(n), n, f, mm, t, fptr(W), stream_of(gram.device()));
-  });
+    TORCH_CHECK(batch >= 1, "batch must be >= 1");
+    const int np = garfield::gpu::gram_padded(n);
+    TORCH_CHECK(W.numel() >= static_cast<int64_t>(batch) * t * n && gram.numel() >= static_cast<int64_t>(batch) * np * np,
+                "gpu_bulyan_select: buffers too small for the batch");
+    garfield::gpu::bulyan_select(fptr(gram), np, n, f, mm, t, fptr(W), stream_of(gram.device()), batch);
+  }, py::arg("gram"), py::arg("n"), py::arg("f"), py::arg("m"), py::arg("t"), py::arg("W"), py::arg("batch") = 1,
+     "Bulyan's t selection steps on device: W [t, n]; batch > 1: gram [batch, np, np] -> W [batch, t, n]");
   m.def("gpu_brute_select", [](const at::Tensor& gram, int n, int f, const at::Tensor& best, const at::Tensor& w) {
     c10::hip::HIPGuard guard(gram.device().index());
     TORCH_CHECK(n <= 64, "brute: n must be <= 64");

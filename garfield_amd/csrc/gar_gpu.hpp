@@ -29,8 +29,9 @@ void krum_select(const float* gram, int np, int n, int f, int m, float* weights,
                  int* order, float* scores, hipStream_t stream, int batch = 1);
 
 // W[t][n]: row k = uniform weights of the (m-k) best-scoring gradients at step k
+// batch > 1: gram [batch][np][np] -> W [batch][t][n]
 void bulyan_select(const float* gram, int np, int n, int f, int m, int t, float* W,
-                   hipStream_t stream);
+                   hipStream_t stream, int batch = 1);
 // best: one uint64 (initialised here), weights[n]
 void brute_select(const float* gram, int np, int n, int f, unsigned long long* best,
                   float* weights, hipStream_t stream);
@@ -59,6 +60,10 @@ void combine_sgd(const RowTable& rows, int n, int64_t d, int dt, const float* we
 // lw_gram: gram [L][np][np] = per-segment G·Gᵀ (slabs: [njobs][gram_slab_floats(n)] workspace).
 void lw_gram(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const int* seg_lo, int L,
              float* slabs, float* gram, hipStream_t stream);
+// lw_bulyan_tail: out[x] (fp32) for every coordinate x of the jobs (LOCAL coordinates) = Bulyan's
+// tail with x's segment's W[s] [t][n]: the averaged median (beta) of the t selection means
+void lw_bulyan_tail(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const float* W, int t,
+                    int beta, float* out, hipStream_t stream);
 // lw_combine_sgd: per coordinate of segment s, g = Σ_j weights[s][j] row_j, then the SGD update
 // of param / momentum (and the shadow copy), as combine_sgd does with one weight vector.
 // jobs in LOCAL coordinates of rows / param / momentum / shadow, base = the global coordinate of

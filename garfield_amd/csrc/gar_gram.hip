@@ -266,6 +266,9 @@ __global__ __launch_bounds__(1024) void k_krum_select(const float* __restrict__ 
 __global__ __launch_bounds__(1024) void k_bulyan_select(const float* __restrict__ gram, int np, int n,
                                                         int f, int m, int t, float* __restrict__ W) {
   extern __shared__ float lds[];
+  // workgroup b selects problem b of a batch (the layer-wise GAR: one Gram per parameter segment)
+  gram += static_cast<int64_t>(blockIdx.x) * np * np;
+  W += static_cast<int64_t>(blockIdx.x) * t * n;
   float* D = lds;                    // n * (n + 1); becomes the pruned distances
   float* S = lds + n * (n + 1);      // n scores
   __shared__ int best;
@@ -497,10 +500,11 @@ void krum_select(const float* gram_in, int np, int n, int f, int m, float* weigh
                      weights, order, scores);
 }
 
-void bulyan_select(const float* gram_in, int np, int n, int f, int m, int t, float* W, hipStream_t stream) {
+void bulyan_select(const float* gram_in, int np, int n, int f, int m, int t, float* W, hipStream_t stream, int batch) {
   static bool once = (allow_big_lds(reinterpret_cast<const void*>(&k_bulyan_select)), true);
   (void)once;
-  hipLaunchKernelGGL(k_bulyan_select, dim3(1), dim3(1024), select_lds_bytes(n), stream, gram_in, np, n, f, m, t, W);
+  hipLaunchKernelGGL(k_bulyan_select, dim3(batch), dim3(1024), select_lds_bytes(n), stream, gram_in, np, n, f, m, t,
+                     W);
 }
 
 static unsigned long long host_binom(int a, int b) {

@@ -9,7 +9,10 @@
 //   lw_gram         one split-K MFMA Gram launch over a JOB table (each job a coordinate range
 //                   inside one segment) writing a partial [np, np] slab per job, then one
 //                   fixed-order segmented reduction into gram[L][np][np];
-//   krum_select     the existing one-workgroup selection, batched: workgroup s selects segment s;
+//   krum_select     the existing one-workgroup selection, batched: workgroup s selects segment s
+//                   (bulyan_select likewise: W [L][t][n]);
+//   lw_bulyan_tail  Bulyan's tail per coordinate with its segment's W [t][n] (the t selection
+//                   means, then their averaged median: the flat tail's per-coordinate code);
 //   lw_combine_sgd  one launch: job j combines its coordinates with its segment's weights and
 //                   applies the fused SGD update (the same per-element arithmetic as k_combine +
 //                   k_combine_sgd: 8-wide groups from the segment start, 4 rows per step, a scalar
@@ -17,6 +20,7 @@
 //
 // Segment boundaries are arbitrary element offsets (a BatchNorm bias of 64, a 9408-element
 // stem): 16-byte loads where a group is aligned, element loads where it is not.
+#include "gar_coord.hpp"
 #include "gar_device.hpp"
 
 namespace garfield {
@@ -277,6 +281,39 @@ __global__ __launch_bounds__(256) void k_lw_combine_sgd(RowTable rows, int n, co
   }
 }
 
+// Layer-wise Bulyan's tail: job j's coordinates get the flat tail (coord_body<kBulyanTail>: the
+// t selection means with the segment's W [t][n], read by uniform scalar loads, then the averaged
+// median of the t means, beta = t - 2f) -- the per-coordinate arithmetic of k_coordwise. Grid
+// (jobs, kLwTailSub): the kLwTailSub workgroups of a job interleave its coordinates.
+constexpr int kLwTailSub = 8;
+
+template <int DT, int NP>
+__global__ __launch_bounds__(256) void k_lw_bulyan_tail(RowTable rows, int n, const int64_t* __restrict__ jobs,
+                                                        const float* __restrict__ W, int t, int beta,
+                                                        float* __restrict__ out) {
+  const int64_t a = jobs[3 * blockIdx.x], b = jobs[3 * blockIdx.x + 1];
+  const float* Ws = W + jobs[3 * blockIdx.x + 2] * static_cast<int64_t>(t) * n;
+  for (int64_t x = a + blockIdx.y * 256 + threadIdx.x; x < b; x += 256 * kLwTailSub) {
+    float res[1];
+    coord::coord_body<DT, NP, 1, kBulyanTail>(coord::DirectLoader<DT, 1>{rows, x, false}, n, 0, beta, Ws, t, 0, 0,
+                                              x, res);
+    out[x] = res[0];
+  }
+}
+
+template <int DT> struct LwBulyan {
+  static void run(const RowTable& rows, int n, const int64_t* jobs, int njobs, const float* W, int t, int beta,
+                  float* out, hipStream_t s) {
+    const dim3 grid(njobs, kLwTailSub);
+    switch (coord::np_for(t)) {
+      case 8: hipLaunchKernelGGL((k_lw_bulyan_tail<DT, 8>), grid, dim3(256), 0, s, rows, n, jobs, W, t, beta, out); break;
+      case 16: hipLaunchKernelGGL((k_lw_bulyan_tail<DT, 16>), grid, dim3(256), 0, s, rows, n, jobs, W, t, beta, out); break;
+      case 32: hipLaunchKernelGGL((k_lw_bulyan_tail<DT, 32>), grid, dim3(256), 0, s, rows, n, jobs, W, t, beta, out); break;
+      default: hipLaunchKernelGGL((k_lw_bulyan_tail<DT, 64>), grid, dim3(256), 0, s, rows, n, jobs, W, t, beta, out); break;
+    }
+  }
+};
+
 template <int DT, int NB>
 void launch_lw_gram(const RowTable& rows, int n, const int64_t* jobs, int njobs, float* slabs, hipStream_t s) {
   hipLaunchKernelGGL((k_lw_gram_partial<DT, NB>), dim3(njobs), dim3(256), 0, s, rows, n, jobs, slabs);
@@ -309,6 +346,12 @@ void lw_gram(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs
   const int nb = gram_nb(n);
   const int E = nb * (nb + 1) / 2 * 256;
   hipLaunchKernelGGL(k_lw_gram_reduce, dim3((E + 255) / 256, L), dim3(256), 0, stream, slabs, seg_lo, nb, gram);
+}
+
+void lw_bulyan_tail(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const float* W, int t,
+                    int beta, float* out, hipStream_t stream) {
+  if (njobs <= 0 || t <= 0) return;
+  by_dtype<LwBulyan>(dt, rows, n, jobs, njobs, W, t, beta, out, stream);
 }
 
 void lw_combine_sgd(const RowTable& rows, int n, int dt, const int64_t* jobs, int njobs, const float* weights,

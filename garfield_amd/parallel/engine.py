@@ -262,12 +262,6 @@ class RobustDataParallel:
             return False
         if self.ctx.world_size > 1 and not self.ctx.is_distributed:
             raise ValueError("sharded aggregation over several ranks needs an initialised process group")
-        if self.cfg.layerwise:
-            if self.cfg.gar != "krum":      # layer-wise Krum shards: per-segment partial Grams are additive
-                if self.cfg.shard_gar:
-                    raise ValueError("sharded layer-wise aggregation supports krum (shard_gar=False for others)")
-                return False
-            return True
         if self.cfg.gar not in SUPPORTED:
             raise ValueError(f"sharded aggregation does not support {self.cfg.gar!r} (shard_gar=False)")
         return True
@@ -508,8 +502,8 @@ class RobustDataParallel:
         if cfg.m is not None and rule in ("krum", "bulyan"):
             gkw["m"] = cfg.m
         cuda = self.device.type == "cuda"
-        if cuda and LW_DEVICE and rule == "krum" and self.n <= gar.MAX_ROWS:
-            self._layerwise_device(first)
+        if cuda and LW_DEVICE and self.n <= gar.MAX_ROWS and (rule == "krum" or (rule == "bulyan" and self.n <= 64)):
+            self._layerwise_device(rule, first)
             return
         g = self._gagg if self._gagg is not None else torch.zeros(self.ld, dtype=torch.float32, device=self.device)
         self._gagg = g
@@ -534,10 +528,11 @@ class RobustDataParallel:
         """(offset, numel) of every parameter segment, by offset."""
         return sorted(zip(self.flat.offsets, self.flat.numels))
 
-    def _layerwise_device(self, first: bool) -> None:
-        """Layer-wise Krum on device: per-segment Grams (one launch over a job table + one
-        segmented reduction), every segment's selection in one batched launch, and one
-        segmented combine fused with the SGD update."""
+    def _layerwise_device(self, rule: str, first: bool) -> None:
+        """Layer-wise Krum / Bulyan on device: per-segment Grams (one launch over a job table + one
+        segmented reduction), every segment's selection in one batched launch, then Krum: one
+        segmented combine fused with the SGD update; Bulyan: one segmented tail launch (each
+        coordinate's t selection means with its segment's W, their averaged median) + the update."""
         cfg = self.cfg
         C = self._C
         lw = getattr(self, "_lw", None)
@@ -565,6 +560,21 @@ class RobustDataParallel:
         m = cfg.m if cfg.m is not None else n - f - 2
         G = self.G[:, : self.d]
         C.gpu_lw_gram(G, lw["jobs"], lw["seg_lo"], lw["slabs"], lw["gram"])
+        if rule == "bulyan":
+            t = n - 2 * f - 2
+            W = lw.get("W")
+            if W is None:
+                W = lw["W"] = torch.empty((lw["L"], t, n), dtype=torch.float32, device=self.device)
+            if self._gagg is None:
+                self._gagg = torch.zeros(self.ld, dtype=torch.float32, device=self.device)
+            g = self._gagg[: self.d]
+            C.gpu_bulyan_select(lw["gram"], n, f, m, t, W, lw["L"])
+            C.gpu_lw_bulyan_tail(G, lw["jobs"], W, t, t - 2 * f, g)
+            C.gpu_combine_sgd(g.view(1, -1), self._one, self.flat.data[: self.d], self.mom[: self.d], None,
+                              self._shadow, cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov,
+                              first)
+            self.last_weights = None
+            return
         C.gpu_krum_select(lw["gram"], n, f, m, lw["w"], lw["order"], lw["scores"], lw["L"])
         C.gpu_lw_combine_sgd(G, lw["jobs"], lw["seg_off"], 0, lw["w"], self.flat.data[: self.d], self.mom[: self.d],
                              self._shadow, cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)

@@ -60,6 +60,7 @@ from garfield_amd.parallel.rccl import direct_backend
 from garfield_amd.parallel.signals import Handoff
 
 DISTANCE_RULES = {"krum", "brute", "bulyan"}
+LAYERWISE_RULES = {"krum", "bulyan", "brute", "aksel"}
 SUPPORTED = DISTANCE_RULES | {"average", "aksel", "median", "trimmed-mean", "averaged-median", "average-nan",
                               "condense"}
 
@@ -282,7 +283,7 @@ class ShardedAggregator:
         if not self._started:
             self.start_exchange()
         self._gathers = []
-        if cfg.layerwise:
+        if cfg.layerwise and cfg.gar in LAYERWISE_RULES:   # per-tensor == flat for the coordinate rules
             self._layerwise(cfg, first)
         elif e.device.type == "cuda":
             self._gpu(cfg, first)
@@ -550,11 +551,12 @@ class ShardedAggregator:
         return W
 
     # ------------------------------------------------------------------ #
-    # Layer-wise Krum, sharded: per-parameter-segment squared distances are additive over the
+    # Layer-wise rules, sharded. Per-parameter-segment squared distances are additive over the
     # coordinate shards too, so each rank adds the partial Grams of its owned coordinates per
-    # segment ([L, n, n]), the partials are summed over ranks in rank order, every rank selects
-    # every segment (identically), and each rank combines + updates its owned coordinates with
-    # their segment's weights.
+    # segment ([L, n, n]; Aksel: the [L, n] partial distances to the coordinate-wise median), the
+    # partials are summed over ranks in rank order, every rank selects every segment
+    # (identically), and each rank aggregates + updates its owned coordinates with their
+    # segment's selection (Krum / Brute / Aksel: weights; Bulyan: W [t, n] and the tail).
 
     def _lw_plan(self):
         """Per bucket: the owned range's pieces of every parameter segment (local coordinates)."""
@@ -567,16 +569,20 @@ class ShardedAggregator:
         segs = sorted(zip(e.flat.offsets, e.flat.numels))
         offs = [o for o, _ in segs] + [segs[-1][0] + segs[-1][1]]
         L = len(segs)
-        plan = {"L": L, "offs": offs, "buckets": {}}
+        plan = {"L": L, "offs": offs, "buckets": {}, "seg_id": {}}
         for b in self.buckets:
             o0, o1 = b.own.start, b.own.stop
             jobs, seg_lo = [], [0]
+            sid = torch.full((b.S,), L, dtype=torch.int64)   # L: padding past the last segment
             for si in range(L):
                 x0, x1 = max(offs[si], o0), min(offs[si + 1], o1)
+                if x1 > x0:
+                    sid[x0 - o0:x1 - o0] = si
                 for a in range(x0, x1, LW_JOB):
                     jobs.append((a - o0, min(a + LW_JOB, x1) - o0, si))
                 seg_lo.append(len(jobs))
             plan["buckets"][b.lo] = (jobs, seg_lo)
+            plan["seg_id"][b.lo] = sid.to(e.device)
         if e.device.type == "cuda":
             C, dev, n = e._C, e.device, self.n
             np_ = C.gram_padded(n)
@@ -592,31 +598,76 @@ class ShardedAggregator:
             plan["w"] = torch.empty((L, n), dtype=torch.float32, device=dev)
             plan["order"] = torch.empty((L, n), dtype=torch.int32, device=dev)
             plan["scores"] = torch.empty((L, n), dtype=torch.float32, device=dev)
+            plan["best"] = torch.empty(1, dtype=torch.int64, device=dev)
+            plan["np"] = np_
         self._lwp = plan
         return plan
 
+    def _lw_aksel_weights(self, cfg, plan, Xs: dict) -> torch.Tensor:
+        """Layer-wise Aksel: per segment, the c rows closest (squared distance, summed over the owned
+        coordinates of every rank) to the coordinate-wise median get weight 1/c (ties by slot)."""
+        n, L = self.n, plan["L"]
+        D = torch.zeros((n, L + 1), dtype=torch.float64, device=self.e.device)
+        for b in self.buckets:
+            X = Xs[b.lo]
+            med = gar.aggregate("median", X).to(X.dtype)
+            D.index_add_(1, plan["seg_id"][b.lo], ((X - med) ** 2).double())
+        D = self._sum_over_ranks(D[:, :L].t().contiguous())
+        D = torch.where(torch.isfinite(D), D, torch.full_like(D, math.inf))
+        c = (n + 1) // 2 if dict(cfg.gar_kwargs).get("mode", "mid") == "mid" else n - cfg.f
+        idx = torch.sort(D, dim=1, stable=True).indices[:, :c]
+        return torch.zeros((L, n), dtype=torch.float32, device=D.device).scatter_(1, idx, 1.0 / c)
+
     def _layerwise(self, cfg, first: bool) -> None:
         e = self.e
+        rule = cfg.gar
         n, f = self.n, cfg.f
         m = cfg.m if cfg.m is not None else n - f - 2
+        t = n - 2 * f - 2
         plan = self._lw_plan()
         L = plan["L"]
         if e.device.type == "cuda":
             C = e._C
-            total = None
-            for b in self.buckets:          # partial per-segment Grams as the buckets land
-                self._wait(b)
-                bp = plan["buckets"][b.lo]
-                if bp["J"] == 0:
-                    continue
-                C.gpu_lw_gram(b.rows, bp["jobs"], bp["seg_lo"], bp["slabs"], bp["gram"])
-                total = bp["gram"].clone() if total is None else total.add_(bp["gram"])
-            if total is None:
-                total = torch.zeros_like(next(iter(plan["buckets"].values()))["gram"])
-            total = self._sum_over_ranks(total)
-            C.gpu_krum_select(total, n, f, m, plan["w"], plan["order"], plan["scores"], L)
-            e.last_weights = plan["w"]
             args = (cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
+            if rule == "aksel":
+                for b in self.buckets:
+                    self._wait(b)
+                w = self._lw_aksel_weights(cfg, plan, {b.lo: torch.stack(b.rows).float() for b in self.buckets})
+                plan["w"].copy_(w)
+            else:
+                total = None
+                for b in self.buckets:          # partial per-segment Grams as the buckets land
+                    self._wait(b)
+                    bp = plan["buckets"][b.lo]
+                    if bp["J"] == 0:
+                        continue
+                    C.gpu_lw_gram(b.rows, bp["jobs"], bp["seg_lo"], bp["slabs"], bp["gram"])
+                    total = bp["gram"].clone() if total is None else total.add_(bp["gram"])
+                if total is None:
+                    total = torch.zeros_like(next(iter(plan["buckets"].values()))["gram"])
+                total = self._sum_over_ranks(total)
+                if rule == "bulyan":
+                    W = plan.get("W")
+                    if W is None:
+                        W = plan["W"] = torch.empty((L, t, n), dtype=torch.float32, device=e.device)
+                    C.gpu_bulyan_select(total, n, f, m, t, W, L)
+                    e.last_weights = None
+                    for b in self._update_order():
+                        bp = plan["buckets"][b.lo]
+                        g = self._gagg(b)
+                        if bp["J"]:
+                            C.gpu_lw_bulyan_tail(b.rows, bp["jobs"][: bp["J"]], W, t, t - 2 * f, g)
+                        p, mom, sh = self._param(b)
+                        C.gpu_combine_sgd([g], self._one, p, mom, None, sh, *args)
+                        self._gather_bucket(b)
+                    return
+                if rule == "brute":
+                    np2 = plan["np"] ** 2
+                    for si in range(L):
+                        C.gpu_brute_select(total[si * np2:(si + 1) * np2], n, f, plan["best"], plan["w"][si])
+                else:
+                    C.gpu_krum_select(total, n, f, m, plan["w"], plan["order"], plan["scores"], L)
+            e.last_weights = plan["w"]
             for b in self._update_order():
                 bp = plan["buckets"][b.lo]
                 if bp["J"]:
@@ -628,27 +679,42 @@ class ShardedAggregator:
         # CPU (gloo): per-segment partial squared distances of the owned coordinates (fp64)
         for b in self.buckets:
             self._wait(b)
-        D = torch.zeros((L, n, n), dtype=torch.float64)
-        Xs = {}
-        for b in self.buckets:
-            X = torch.stack([r.double() for r in b.rows])                 # [n, S] owned shard of b
-            Xs[b.lo] = X
-            for a, z, si in plan["buckets"][b.lo][0]:
-                Y = X[:, a:z]
-                sq = (Y * Y).sum(1)
-                D[si] += sq[:, None] + sq[None, :] - 2.0 * (Y @ Y.T)
-        D = self._sum_over_ranks(D)
-        W = torch.zeros((L, n), dtype=torch.float32)
-        for si in range(L):
-            Ds = D[si].clamp_min(0)
-            Ds.fill_diagonal_(math.inf)
-            W[si] = ref.krum_weights(Ds, f, m).float()
-        e.last_weights = W
+        Xs = {b.lo: torch.stack([r.float() for r in b.rows]) for b in self.buckets}   # [n, S] owned shards
+        Cn = _native.require_for(torch.empty(0))
+        if rule == "aksel":
+            W = self._lw_aksel_weights(cfg, plan, Xs)
+        else:
+            D = torch.zeros((L, n, n), dtype=torch.float64)
+            for b in self.buckets:
+                X = Xs[b.lo].double()
+                for a, z, si in plan["buckets"][b.lo][0]:
+                    Y = X[:, a:z]
+                    sq = (Y * Y).sum(1)
+                    D[si] += sq[:, None] + sq[None, :] - 2.0 * (Y @ Y.T)
+            D = self._sum_over_ranks(D)
+            W = torch.zeros((L, t, n) if rule == "bulyan" else (L, n), dtype=torch.float32)
+            for si in range(L):
+                Ds = D[si].clamp_min(0)
+                Ds.fill_diagonal_(math.inf)
+                if rule == "krum":
+                    W[si] = ref.krum_weights(Ds, f, m).float()
+                elif rule == "brute":
+                    W[si] = (Cn.cpu_brute_weights(Ds, f) if Cn is not None else ref.brute_weights(Ds, f)).float()
+                else:
+                    W[si] = (Cn.cpu_bulyan_weights(Ds, f, m, t) if Cn is not None
+                             else ref.bulyan_weights(Ds, f, m)).float().view(t, n)
+        e.last_weights = None if rule == "bulyan" else W
         for b in self._update_order():
-            X = Xs[b.lo].float()
+            X = Xs[b.lo]
             g = torch.zeros(b.S, dtype=torch.float32)
             for a, z, si in plan["buckets"][b.lo][0]:
-                g[a:z] = (W[si][:, None] * X[:, a:z]).sum(0)
+                if rule != "bulyan":
+                    g[a:z] = (W[si][:, None] * X[:, a:z]).sum(0)
+                elif Cn is not None:
+                    g[a:z] = Cn.cpu_coordwise(X[:, a:z], gar._MODE["bulyan-tail"], f, t - 2 * f, W[si].reshape(-1), t,
+                                              0, 1.0).float()
+                else:
+                    g[a:z] = gar._torch_closest_mean(W[si] @ X[:, a:z], t - 2 * f).float()
             self._sgd_cpu(b, g, first)
             self._gather_bucket(b)
 

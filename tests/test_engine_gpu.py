@@ -301,24 +301,55 @@ def test_fp32_grouped_channel_path_matches_per_worker_engine(cuda, graph):
 
 
 @pytest.mark.gpu
-def test_sharded_layerwise_krum_matches_unsharded_on_gpu(cuda):
-    """Layer-wise Krum through the sharded aggregator (one rank: per-bucket segment Grams over the
-    owned ranges, batched selection, per-bucket segmented combine with the bucket's base offset)
-    equals the unsharded device path: same per-segment weights, parameters to fp32 rounding."""
+@pytest.mark.parametrize("rule,f", [("krum", 2), ("bulyan", 1), ("brute", 2), ("aksel", 2)])
+def test_sharded_layerwise_matches_unsharded_on_gpu(cuda, rule, f):
+    """Layer-wise rules through the sharded aggregator (one rank: per-bucket segment Grams over the
+    owned ranges -- Aksel: per-segment distances to the median --, batched selection, per-bucket
+    segmented combine / Bulyan tail) equal the unsharded path: same per-segment weights,
+    parameters to fp32 rounding."""
     outs = []
     for shard in (False, True):
         torch.manual_seed(0)
-        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, byzantine={3: "reverse"}, lr=0.05, momentum=0.9,
+        cfg = EngineConfig(gar=rule, f=f, workers_per_rank=8, byzantine={3: "reverse"}, lr=0.05, momentum=0.9,
                            weight_decay=5e-4, layerwise=True, shard_gar=shard, cuda_graph=False)
         eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
         assert (eng._shard is not None) == shard
         eng.step(synthetic_batches(8, 4, (3, 32, 32), 10, cuda, seed=3))
         torch.cuda.synchronize()
-        outs.append((eng.flat.reference_vector().clone(), eng.last_weights.clone()))
+        w = eng.last_weights
+        outs.append((eng.flat.reference_vector().clone(), w.clone() if w is not None else None))
     (p0, w0), (p1, w1) = outs
-    assert torch.equal(w0, w1)
+    if rule != "bulyan":
+        assert w0.shape == w1.shape and torch.equal(w0.float(), w1.float())
     rel = ((p1 - p0).norm() / p0.norm()).item()
     assert rel < 1e-6, rel
+
+
+@pytest.mark.gpu
+def test_layerwise_bulyan_device_matches_per_segment_rule(cuda):
+    """Layer-wise Bulyan on device (segmented Gram, the t selections of every segment in one
+    batched launch, one segmented tail launch) == per segment: the HIP Bulyan selection W of the
+    segment's rows, V = W · rows in fp32, the averaged median of V (beta = t - 2f)."""
+    from garfield_amd.ops import gar
+
+    torch.manual_seed(0)
+    n, f = 16, 3
+    cfg = EngineConfig(gar="bulyan", f=f, workers_per_rank=n, byzantine={3: "reverse", 9: "reverse"}, lr=0.1,
+                       momentum=0.0, weight_decay=0.0, layerwise=True, cuda_graph=False)
+    eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+    b = synthetic_batches(n, 4, (3, 32, 32), 10, cuda)
+    before = eng.flat.data[: eng.d].clone()
+    eng.step(b)
+    torch.cuda.synchronize()
+    t = n - 2 * f - 2
+    expect = torch.empty(eng.d, dtype=torch.float32, device=cuda)
+    for off, numel in zip(eng.flat.offsets, eng.flat.numels):
+        seg = eng.G[:, off:off + numel]
+        W = gar.bulyan_weights(seg, f).float()
+        assert float(W[:, 3].abs().max()) == 0.0 and float(W[:, 9].abs().max()) == 0.0
+        expect[off:off + numel] = gar._torch_closest_mean(W @ seg.float(), t - 2 * f).float()
+    got = (before - eng.flat.data[: eng.d]) / 0.1
+    assert ((got - expect).norm() / expect.norm()).item() < 1e-5
 
 
 @pytest.mark.gpu

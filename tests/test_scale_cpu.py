@@ -26,6 +26,7 @@ from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synth
 
 RULES = [("krum", 2), ("bulyan", 2), ("median", 2), ("trimmed-mean", 2), ("brute", 2), ("aksel", 2)]
 BYZ = {3: "lie", 12: "reverse"}
+LW_RULES = [("bulyan", 2), ("krum", 2), ("brute", 2), ("aksel", 2), ("median", 2)]
 
 
 def free_port():
@@ -63,25 +64,27 @@ def _direct(mode):
     return made
 
 
-def _rules_worker(rank, world, port, outdir, mode):
+def _rules_worker(rank, world, port, outdir, mode, layerwise=False):
     from garfield_amd.parallel.comm import shutdown
 
     ctx = _init(rank, world, port)
     made = _direct(mode)
     out = {}
-    for rule, f in RULES:
+    for rule, f in (LW_RULES if layerwise else RULES):
         torch.manual_seed(0)
         eng = RobustDataParallel(build_model("mlp"), F.nll_loss, ctx,
                                  EngineConfig(gar=rule, f=f, workers_per_rank=2, byzantine=BYZ, shard_gar=mode > 0,
-                                              lr=0.05, collusion="all", shadow_cpu=mode == 2))
+                                              lr=0.05, collusion="all", shadow_cpu=mode == 2, layerwise=layerwise))
         assert (eng._shard is not None) == (mode > 0)
         if mode == 2:
             assert eng._shard._rccl is made[-1] and eng._shadow is not None
         b = synthetic_batches(2, 8, (1, 28, 28), 10, "cpu", seed=rank)
         for _ in range(2):
             eng.step(b)
+        w = eng.last_weights
         out[rule] = {"flat": eng.flat_model().clone(), "sum": eng.replica_checksum(),
-                     "calls": dict(made[-1].calls) if mode == 2 else {}}
+                     "calls": dict(made[-1].calls) if mode == 2 else {},
+                     "w": w.clone().float() if w is not None else torch.zeros(0)}
     torch.save(out, os.path.join(outdir, f"{mode}r{rank}.pt"))
     shutdown(ctx)
 
@@ -105,6 +108,29 @@ def test_eight_rank_sharded_equals_redundant_bitwise():
             calls = res[(2, 0)][rule]["calls"]
             assert calls["all_to_all"] == 2 and calls["all_gather_inplace"] == 2, (rule, calls)
             assert "all_reduce" not in calls, (rule, calls)   # every MLP parameter is a shadow view
+
+
+def test_eight_rank_sharded_layerwise_equals_redundant_bitwise():
+    """Garfield_CC's per-layer aggregation (--layerwise) sharded over 8 ranks (per-segment partial
+    distances summed over ranks, per-segment selections, each rank's owned coordinates
+    aggregated with their segment's selection), through the direct-RCCL contract (2), == the
+    redundant per-segment loop (0), BITWISE, for Bulyan, Krum, Brute, Aksel (and a coordinate
+    rule, where per-layer == flat); the reversed attacker never selected by Krum."""
+    world = 8
+    with tempfile.TemporaryDirectory() as d:
+        for mode in (0, 2):
+            mp.spawn(_rules_worker, args=(world, free_port(), d, mode, True), nprocs=world, join=True)
+        res = {(s, r): torch.load(os.path.join(d, f"{s}r{r}.pt"), weights_only=True)
+               for s in (0, 2) for r in range(world)}
+        for rule, _ in LW_RULES:
+            ref = res[(0, 0)][rule]
+            for s in (0, 2):
+                for r in range(world):
+                    got = res[(s, r)][rule]
+                    assert got["sum"] == ref["sum"], (rule, s, r)
+                    assert torch.equal(got["flat"], ref["flat"]), (rule, s, r)
+        wk = res[(2, 0)]["krum"]["w"]
+        assert wk.dim() == 2 and wk.shape[0] >= 2 and float(wk[:, 12].abs().max()) == 0.0
 
 
 def _grouped_worker(rank, world, port, outdir, mode, k):
