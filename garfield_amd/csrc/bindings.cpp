@@ -863,6 +863,23 @@ void g_large_coord(const at::Tensor& x, int64_t mode, int64_t f, int64_t beta, c
                              static_cast<int>(f), static_cast<int>(beta), out.data_ptr(), stream_of(x.device()));
 }
 
+void g_large_select(const at::Tensor& gram, int64_t f, int64_t m, int64_t rounds, bool shrink, const at::Tensor& W) {
+  TORCH_CHECK(gram.is_cuda() && gram.scalar_type() == at::kFloat && gram.dim() == 2 && gram.size(0) == gram.size(1) &&
+                  gram.stride(1) == 1 && gram.size(0) <= garfield::kLargeRows,
+              "gpu_large_select: gram must be an fp32 [n, n] GPU matrix (unit column stride), n <= ", garfield::kLargeRows);
+  const int64_t n = gram.size(0);
+  TORCH_CHECK(f >= 0 && n - f - 2 >= 1 && m >= 1 && m <= n && rounds >= 1 && rounds <= n,
+              "gpu_large_select: needs n - f - 2 >= 1, 1 <= m <= n, 1 <= rounds <= n");
+  TORCH_CHECK(W.device() == gram.device() && W.scalar_type() == at::kFloat && W.is_contiguous() &&
+                  W.numel() == rounds * n, "gpu_large_select: W must be a contiguous fp32 [rounds, n] tensor");
+  c10::hip::HIPGuard guard(gram.device().index());
+  auto dopt = gram.options().dtype(at::kDouble);
+  at::Tensor tv = at::empty({n}, dopt), ns = at::empty({n}, dopt), ti = at::empty({n}, gram.options().dtype(at::kInt));
+  garfield::gpu::large_select(gram.data_ptr<float>(), gram.stride(0), static_cast<int>(n), static_cast<int>(f),
+                              static_cast<int>(m), static_cast<int>(rounds), shrink, tv.data_ptr<double>(),
+                              ti.data_ptr<int>(), ns.data_ptr<double>(), W.data_ptr<float>(), stream_of(gram.device()));
+}
+
 // Split-K slabs -> strided per-group output: part fp32 [S, G, ...] and out [G, ...] (fp32 / bf16 /
 // fp16) may have any slab / group strides and one row pitch each (the last dim contiguous, the
 // dims between it and the group dim dense), e.g. a padded GEMM result cropped into exchange rows.
@@ -1677,6 +1694,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("LARGE_ROWS") = garfield::kLargeRows;
   m.def("gpu_large_combine", &g_large_combine,
         "out = w · x for an [n, d] gradient matrix with n <= LARGE_ROWS (fp32 accumulation); args (x, w, out)");
+  m.def("gpu_large_select", &g_large_select, py::arg("gram"), py::arg("f"), py::arg("m"), py::arg("rounds"),
+        py::arg("shrink"), py::arg("W"),
+        "Multi-Krum (rounds=1, shrink=False) / Bulyan (rounds=t, shrink=True) selection weights W [rounds, n] "
+        "from an fp32 Gram of n <= LARGE_ROWS rows, on device (fp64 distances)");
   m.def("gpu_large_coord", &g_large_coord,
         "Coordinate-wise rule on an [n, d] gradient matrix with n <= LARGE_ROWS by LDS radix select; "
         "args (x, mode 0 median | 1 trimmed-mean | 2 averaged-median, f, beta, out)");

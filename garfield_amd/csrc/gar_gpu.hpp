@@ -82,6 +82,11 @@ int coordwise_max_rows();
 // ---- Large gradient sets (kMaxRows < n <= kLargeRows), one [n, ld] matrix (gar_large.hip) ----
 // out[j] = Σ_i w[i] x[i, j] (out in x's dtype); mode 0 median, 1 trimmed-mean(f), 2 averaged-median(beta).
 void large_combine(const void* x, int dt, int n, int64_t d, int64_t ld, const float* w, void* out, hipStream_t stream);
+// Multi-Krum (rounds 1, W [1][n] = 1/m on the m best scores) / Bulyan (rounds t, shrink: W [t][n] with
+// 1/max(m - k, 1) in round k) selection from an fp32 Gram [n][ld] (n <= kLargeRows, 1 <= n - f - 2);
+// thr_val / thr_idx / nearsum: [n] workspaces.
+void large_select(const float* gram, int64_t ld, int n, int f, int m, int rounds, bool shrink, double* thr_val,
+                  int* thr_idx, double* nearsum, float* W, hipStream_t stream);
 void large_coord(const void* x, int dt, int n, int64_t d, int64_t ld, int mode, int f, int beta, void* out,
                  hipStream_t stream);
 

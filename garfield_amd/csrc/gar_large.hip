@@ -19,6 +19,18 @@
 //                     +inf), ties in value order: a select on |x - med| keys computed
 //                     on the fly, then one scan.
 //   Semantics are those of ops/gar.py's vectorised PyTorch versions (_torch_coord).
+// * k_large_near + k_large_select: Multi-Krum / Bulyan SELECTION from the fp32 Gram [n, n], on
+//   device (no host round trip; reference semantics of ops/reference.py krum_weights /
+//   bulyan_weights, distances in fp64):
+//     k_large_near    one workgroup per row i: D[i, j] = g_ii + g_jj - 2 g_ij (fp64; +inf on the
+//                     diagonal and where non-finite, else clamped at 0), bitonic-sorted as
+//                     (value, index) pairs in LDS; the q-th pair is row i's neighbourhood
+//                     threshold (j near i iff (D_ij, j) <= it) and Σ_j near D_ij its Krum score;
+//     k_large_select  one workgroup: `rounds` selection rounds on the scores held in LDS; each
+//                     round ranks every row by (score, index) (NaN as +inf) in one O(n) pass per
+//                     lane, writes W[k] = 1/mk on the mk best, removes the best (score = FLT_MAX)
+//                     and subtracts its distance from the rows it is near (Bulyan's P column).
+#include <cfloat>
 #include "gar_device.hpp"
 #include "gar_gpu.hpp"
 
@@ -234,7 +246,119 @@ void launch_coord(const void* x, int n, int64_t d, int64_t ld, int mode, int f, 
   else hipLaunchKernelGGL((k_large_coord<DT, MODE_AVGMED>), grid, dim3(kLT), 0, stream, x, n, d, ld, f, beta, out);
 }
 
+constexpr int kSelThreads = 1024;   // = kLargeRows: one lane per row
+
+__device__ __forceinline__ double lg_dist(const float* __restrict__ g, int64_t ld, int i, int j) {
+  if (i == j) return INFINITY;
+  const double d = static_cast<double>(g[i * ld + i]) + static_cast<double>(g[j * ld + j]) -
+                   2.0 * static_cast<double>(g[i * ld + j]);
+  return isfinite(d) ? fmax(d, 0.0) : INFINITY;
+}
+
+__device__ __forceinline__ bool pair_less(double a, int ia, double b, int ib) {
+  return a < b || (a == b && ia < ib);
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_large_near(const float* __restrict__ g, int64_t ld, int n, int q,
+                                                            double* __restrict__ thr_val, int* __restrict__ thr_idx,
+                                                            double* __restrict__ nearsum) {
+  __shared__ double val[kSelThreads];
+  __shared__ double row[kSelThreads];
+  __shared__ int idx[kSelThreads];
+  const int i = blockIdx.x, t = threadIdx.x;
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  if (t < np2) {
+    const double d = t < n ? lg_dist(g, ld, i, t) : INFINITY;
+    val[t] = d;
+    idx[t] = t;   // padding sorts after every real entry (index >= n)
+    row[t] = d;
+  }
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (t < np2) {
+        const int p = t ^ j;
+        if (p > t) {
+          const bool up = (t & k) == 0;
+          const bool sw = up ? pair_less(val[p], idx[p], val[t], idx[t]) : pair_less(val[t], idx[t], val[p], idx[p]);
+          if (sw) {
+            const double tv = val[t];
+            val[t] = val[p];
+            val[p] = tv;
+            const int ti = idx[t];
+            idx[t] = idx[p];
+            idx[p] = ti;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (t == 0) {
+    const double tv = val[q - 1];
+    const int ti = idx[q - 1];
+    double s = 0.0;
+    for (int j = 0; j < n; ++j)
+      if (!pair_less(tv, ti, row[j], j)) s += row[j];   // (D_ij, j) <= threshold: j is near i
+    thr_val[i] = tv;
+    thr_idx[i] = ti;
+    nearsum[i] = s;
+  }
+}
+
+__global__ __launch_bounds__(kSelThreads) void k_large_select(const float* __restrict__ g, int64_t ld, int n, int m,
+                                                              int rounds, int shrink,
+                                                              const double* __restrict__ thr_val,
+                                                              const int* __restrict__ thr_idx,
+                                                              const double* __restrict__ nearsum,
+                                                              float* __restrict__ W) {
+  __shared__ double sc[kSelThreads];
+  __shared__ int best;
+  const int i = threadIdx.x;
+  const bool mine = i < n;
+  double tv = 0.0;
+  int ti = 0;
+  if (mine) {
+    sc[i] = nearsum[i];
+    tv = thr_val[i];
+    ti = thr_idx[i];
+  }
+  for (int k = 0; k < rounds; ++k) {
+    __syncthreads();
+    const int mk = shrink ? (m - k > 1 ? m - k : 1) : m;
+    if (mine) {
+      const double vi = isnan(sc[i]) ? INFINITY : sc[i];
+      int r = 0;
+      for (int j = 0; j < n; ++j) {
+        const double vj = isnan(sc[j]) ? INFINITY : sc[j];
+        r += pair_less(vj, j, vi, i);
+      }
+      W[static_cast<int64_t>(k) * n + i] = r < mk ? 1.0f / static_cast<float>(mk) : 0.0f;
+      if (r == 0) best = i;
+    }
+    __syncthreads();
+    const int b = best;
+    if (mine) {
+      if (i == b) {
+        sc[i] = static_cast<double>(FLT_MAX);
+      } else {
+        const double dib = lg_dist(g, ld, i, b);
+        if (!pair_less(tv, ti, dib, b)) sc[i] -= dib;   // b is among row i's q nearest: P[i, b]
+      }
+    }
+  }
+}
+
 }  // namespace
+
+void large_select(const float* gram, int64_t ld, int n, int f, int m, int rounds, bool shrink, double* thr_val,
+                  int* thr_idx, double* nearsum, float* W, hipStream_t stream) {
+  const int q = n - f - 2;
+  hipLaunchKernelGGL(k_large_near, dim3(n), dim3(kSelThreads), 0, stream, gram, ld, n, q, thr_val, thr_idx, nearsum);
+  hipLaunchKernelGGL(k_large_select, dim3(1), dim3(kSelThreads), 0, stream, gram, ld, n, m, rounds, shrink ? 1 : 0,
+                     thr_val, thr_idx, nearsum, W);
+}
 
 void large_combine(const void* x, int dt, int n, int64_t d, int64_t ld, const float* w, void* out, hipStream_t stream) {
   if (d <= 0) return;

@@ -365,6 +365,8 @@ def _bulyan_W(rows: Rows, f: int, m: int) -> torch.Tensor:
         W = ws.get("bulyan_W", t * rows.n)
         C.gpu_bulyan_select(g, rows.n, f, m, t, W)
         return W.view(t, rows.n)
+    if rows.device.type == "cuda" and rows.n > MAX_ROWS:
+        return large_select(_large_gram(rows), f, m, bulyan=True)
     D = pairwise_distances(rows.obj) if C is not None else ref.pairwise_sqdist(rows.stacked())
     if rows.n > MAX_ROWS:
         return _large_bulyan_weights(D, f, m).float().to(rows.device)
@@ -531,7 +533,21 @@ def _large_gram(rows: Rows) -> torch.Tensor:
 
 
 def _large_krum_weights(rows: Rows, f: int, m: int) -> torch.Tensor:
-    return krum_weights_from_gram(_large_gram(rows), f, m)
+    g = _large_gram(rows)
+    if g.is_cuda:
+        return large_select(g, f, m)
+    return krum_weights_from_gram(g, f, m)
+
+
+def large_select(g: torch.Tensor, f: int, m: int, bulyan: bool = False) -> torch.Tensor:
+    """Multi-Krum weights [n] (or Bulyan's W [t, n]) from a GPU fp32 Gram of up to LARGE_ROWS rows, on
+    device (gar_large.hip: per-row neighbourhoods by an LDS bitonic sort, the selection rounds in one
+    workgroup; fp64 distances): no host round trip."""
+    n = g.shape[0]
+    rounds = n - 2 * f - 2 if bulyan else 1
+    W = torch.empty((rounds, n), dtype=torch.float32, device=g.device)
+    _native.native().gpu_large_select(g.float().contiguous(), f, m, rounds, bulyan, W)
+    return W if bulyan else W[0]
 
 
 def distances_from_gram(g: torch.Tensor) -> torch.Tensor:

@@ -467,7 +467,9 @@ class ShardedAggregator:
         for b in self.buckets:
             self._wait(b)
             mats[b.lo] = self._matrix(b)
-        if rule in ("krum", "bulyan", "brute"):
+        if rule == "brute":   # C(n, f) subsets of n > 128 rows: the device search takes n <= 64
+            raise ValueError(f"brute: n must be <= 64 on the GPU (n = {n})")
+        if rule in ("krum", "bulyan"):
             total = None
             for b in self.buckets:
                 X = mats[b.lo]
@@ -476,12 +478,9 @@ class ShardedAggregator:
             gs = self._sum_over_ranks(total)[perm][:, perm]          # slot order on every rank
             m = cfg.m if cfg.m is not None else n - f - 2
             if rule == "krum":
-                ws = gar.krum_weights_from_gram(gs, f, m)
-            elif rule == "brute":
-                from garfield_amd.ops import reference as _ref
-                ws = _ref.brute_weights(gar.distances_from_gram(gs.double()).cpu(), f).float().to(e.device)
+                ws = gar.large_select(gs, f, m)
             else:
-                W = gar._large_bulyan_weights(gar.distances_from_gram(gs.double()), f, m).float().to(e.device)
+                W = gar.large_select(gs, f, m, bulyan=True)
                 Wm = torch.empty_like(W)
                 Wm[:, perm] = W
                 t, beta = n - 2 * f - 2, n - 4 * f - 2

@@ -69,3 +69,63 @@ def test_large_krum_and_bulyan_selections(cuda):
     _close(gar.krum(Xg, f), wref @ X, 1e-5)
     out = gar.bulyan(Xg, f)
     _close(out, ref.bulyan(X, f, n - f - 2), 1e-4)
+
+
+@pytest.mark.parametrize("n,f", [(256, 20), (1024, 50), (129, 1)])
+def test_large_select_on_device_matches_fp64_reference(cuda, n, f):
+    """gar_large.hip's device selection (per-row neighbourhoods by LDS bitonic sort, the rounds in one
+    workgroup) == the fp64 reference selection from the same Gram (ops/reference.py semantics),
+    Multi-Krum weights and every Bulyan round's W row."""
+    g = torch.Generator().manual_seed(n)
+    X = torch.randn(n, 2000, generator=g, dtype=torch.float64)
+    X[:f] *= 30.0
+    G = (X.float().to(cuda) @ X.float().to(cuda).T).contiguous()
+    D = gar.distances_from_gram(G.double()).cpu()
+    m = n - f - 2
+    w = gar.large_select(G, f, m)
+    assert torch.equal(w.cpu(), ref.krum_weights(D, f, m).float())
+    W = gar.large_select(G, f, m, bulyan=True)
+    assert W.shape == (n - 2 * f - 2, n)
+    assert torch.equal(W.cpu(), gar._large_bulyan_weights(D, f, m).float())
+
+
+@pytest.mark.parametrize("rule", ["bulyan", "krum"])
+def test_engine_n256_on_device(cuda, monkeypatch, rule):
+    """n = 256 logical workers on one GPU (what 8 GPUs x 32 workers aggregate): the redundant
+    (_large_update) and sharded (_gpu_large) paths select on device -- a host copy of any GPU tensor
+    during the aggregation fails the test --; redundant == the fp64 reference rule on the same rows,
+    sharded == redundant."""
+    import torch.nn.functional as F
+
+    from garfield_amd.models import build_model
+    from garfield_amd.parallel.comm import DistContext
+    from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synthetic_batches
+
+    n, f = 256, 20
+    real_cpu = torch.Tensor.cpu
+
+    def no_host_copy(t, *a, **k):
+        if t.is_cuda:
+            raise AssertionError("host copy in the n > 128 aggregation")
+        return real_cpu(t, *a, **k)
+
+    deltas = []
+    for shard in (False, True):
+        torch.manual_seed(0)
+        eng = RobustDataParallel(build_model("mlp"), F.nll_loss, DistContext(device=cuda),
+                                 EngineConfig(gar=rule, f=f, workers_per_rank=n, byzantine={5: "reverse", 77: "reverse"},
+                                              lr=0.1, momentum=0.0, weight_decay=0.0, exchange_dtype=torch.float32,
+                                              shard_gar=shard, cuda_graph=False))
+        assert (eng._shard is not None) == shard
+        eng.compute_local(synthetic_batches(n, 4, (1, 28, 28), 10, cuda))
+        before = eng.flat.data[: eng.d].clone()
+        G = None if shard else eng.G[:, : eng.d].double().cpu()
+        monkeypatch.setattr(torch.Tensor, "cpu", no_host_copy)
+        eng.aggregate_and_update()
+        torch.cuda.synchronize()
+        monkeypatch.setattr(torch.Tensor, "cpu", real_cpu)
+        deltas.append(((before - eng.flat.data[: eng.d]) / 0.1).double().cpu())
+        if G is not None:
+            want = ref.bulyan(G, f, n - f - 2) if rule == "bulyan" else ref.krum(G, f, n - f - 2)
+            assert ((deltas[-1] - want).norm() / want.norm()).item() < 1e-5
+    assert ((deltas[1] - deltas[0]).norm() / deltas[0].norm()).item() < 1e-6
