@@ -1019,7 +1019,7 @@ int64_t conv_out(int64_t in, int64_t k, int64_t s, int64_t p, int64_t d) { retur
 // geometry (dgrad: src = dy, out = dx, w = Wt [Co = Cin][kh][kw][Cs = Cout] split); (+ add)
 void g_conv_f32(const at::Tensor& src, const at::Tensor& w3, int64_t kh, int64_t kw, int64_t sh, int64_t sw,
                 int64_t ph, int64_t pw, int64_t dh, int64_t dw, bool dgrad, const at::Tensor& out,
-                const c10::optional<at::Tensor>& add, int64_t pm) {
+                const c10::optional<at::Tensor>& add, int64_t pm, int64_t ksplit) {
   const auto dev = src.device();
   check_f32_cl(src, dev, "src");
   check_f32_cl(out, dev, "out");
@@ -1060,8 +1060,14 @@ void g_conv_f32(const at::Tensor& src, const at::Tensor& w3, int64_t kh, int64_t
     ap = add->data_ptr<float>();
   }
   c10::hip::HIPGuard guard(dev.index());
+  // split-K: automatic with the automatic kernel choice (pm <= 0, ksplit 0), or forced (ksplit > 1)
+  int S = ksplit > 0 ? static_cast<int>(ksplit) : (pm <= 0 ? garfield::gpu::conv_f32_ksplit(g, dgrad) : 1);
+  if (g.Cs % 32 != 0 || (dgrad && (g.dh != 1 || g.dw != 1))) S = 1;
+  at::Tensor part;
+  if (S > 1) part = at::empty({S * out.numel()}, out.options().memory_format(at::MemoryFormat::Contiguous));
   garfield::gpu::conv_f32(src.data_ptr<float>(), reinterpret_cast<const uint16_t*>(w3.data_ptr()), g, dgrad,
-                          out.data_ptr<float>(), ap, static_cast<int>(pm), stream_of(dev));
+                          out.data_ptr<float>(), ap, static_cast<int>(pm), stream_of(dev), S,
+                          S > 1 ? part.data_ptr<float>() : nullptr);
 }
 
 // per-worker weight gradients of a convolution (forward geometry from x, dy): out fp32
@@ -1769,10 +1775,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "split s of worker g of dyᵀ · patches(x); args (x, dy, kh, kw, sh, sw, ph, pw, dh, dw, groups, out, splits)");
   m.def("gpu_conv_f32", &g_conv_f32, py::arg("src"), py::arg("w"), py::arg("kh"), py::arg("kw"),
         py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("dgrad"),
-        py::arg("out"), py::arg("add") = py::none(), py::arg("pm") = 0,
+        py::arg("out"), py::arg("add") = py::none(), py::arg("pm") = 0, py::arg("ksplit") = 0,
         "fp32 NHWC implicit-GEMM convolution (forward, or with dgrad the data gradient of a convolution of this "
         "geometry, any stride) on split-bf16 MFMA (three bf16 pieces per operand, the six products of order <= 2, "
-        "fp32 accumulation); w: the weight's pieces [3, Co, K]");
+        "fp32 accumulation); w: the weight's pieces [3, Co, K]; pm 0: automatic kernel choice (split-K included "
+        "unless ksplit is given), ksplit > 1: that many k-splits summed by a second pass");
   m.def("conv_f32_supported", [](int64_t cs, int64_t co) {
     garfield::gpu::ConvF32Geo g{};
     g.Cs = static_cast<int>(cs);

@@ -228,10 +228,13 @@ __global__ __launch_bounds__(256) void k_cf32_conv(const float* __restrict__ src
 
 __device__ __attribute__((aligned(16))) float g_cf32_zero[8];   // 32 zero bytes: source of padded taps
 
+// Split-K (ksplit > 1: layers with few output tiles and a long reduction, e.g. 256 channels of 3x3
+// at 2x2 pixels): blockIdx.z = class * ksplit + kz, split kz runs k-steps [kz·chunk, (kz+1)·chunk) and
+// writes its fp32 partial tile into slab kz of `out` (k_cf32_ksum then adds the slabs, + add).
 template <int PM, int NS, bool DG, bool ADD>
 __global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__ src, const uint16_t* __restrict__ w3,
                                                        ConvF32Geo g, float* __restrict__ out,
-                                                       const float* __restrict__ add) {
+                                                       const float* __restrict__ add, int ksplit) {
   constexpr int BM = 64 * PM;
   constexpr int WB = kNP * 64 * 64;     // weight pieces per stage (bytes): 3 x 64 rows x 64 B
   constexpr int XB = BM * 128;          // activation tile per stage (bytes): BM rows x 128 B
@@ -245,7 +248,8 @@ __global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__
   const int K = g.KH * g.KW * g.Cs;
   // parity class of this workgroup's output pixels (data gradient of a strided convolution)
   const int csh = DG ? g.sh : 1, csw = DG ? g.sw : 1;
-  const int ca = DG ? static_cast<int>(blockIdx.z) / g.sw : 0, cb = DG ? static_cast<int>(blockIdx.z) % g.sw : 0;
+  const int cls = static_cast<int>(blockIdx.z) / ksplit, kz = static_cast<int>(blockIdx.z) - cls * ksplit;
+  const int ca = DG ? cls / g.sw : 0, cb = DG ? cls % g.sw : 0;
   const int Hc = (g.Ho - ca + csh - 1) / csh, Wc = (g.Wo - cb + csw - 1) / csw;
   const int Mc = g.N * Hc * Wc;
   const int m0 = blockIdx.x * BM;
@@ -262,7 +266,11 @@ __global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__
   const int ni = ti0 < g.KH ? (g.KH - ti0 + tsi - 1) / tsi : 0;
   const int nj = tj0 < g.KW ? (g.KW - tj0 + tsj - 1) / tsj : 0;
   const int csteps = g.Cs / 32;
-  const int steps = ni * nj * csteps;
+  const int all_steps = ni * nj * csteps;
+  const int chunk = (all_steps + ksplit - 1) / ksplit;
+  const int sbeg = kz * chunk < all_steps ? kz * chunk : all_steps;
+  const int steps = (sbeg + chunk < all_steps ? sbeg + chunk : all_steps) - sbeg;
+  if (ksplit > 1) out += static_cast<int64_t>(kz) * g.N * g.Ho * g.Wo * g.Co;   // this split's slab
 
   // this lane's activation rows: rows (wave * XI + u) * 8 + lane / 8 of the tile, chunk lane % 8
   const int xr = lane >> 3, xc = lane & 7;
@@ -299,7 +307,8 @@ __global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__
   }
   const uint64_t az = reinterpret_cast<uint64_t>(g_cf32_zero);
 
-  auto issue = [&](int s, int slot) {
+  auto issue = [&](int sl, int slot) {
+    const int s = sbeg + sl;
     const int tap = s / csteps;
     const int c0 = (s - tap * csteps) * 32;
     const int ti = tap / nj, tj = tap - (tap / nj) * nj;
@@ -397,12 +406,33 @@ __global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__
 
 template <int PM, int NS, bool DG>
 void launch_conv_lds(const float* src, const uint16_t* w3, const ConvF32Geo& g, float* out, const float* add,
-                     hipStream_t stream) {
+                     int ksplit, hipStream_t stream) {
   const int csh = DG ? g.sh : 1, csw = DG ? g.sw : 1;
   const int Mc = g.N * ((g.Ho + csh - 1) / csh) * ((g.Wo + csw - 1) / csw);   // the largest class (0, 0)
-  const dim3 grid((Mc + 64 * PM - 1) / (64 * PM), g.Co / 64, csh * csw);
-  if (add) hipLaunchKernelGGL((k_cf32_conv_lds<PM, NS, DG, true>), grid, dim3(256), 0, stream, src, w3, g, out, add);
-  else hipLaunchKernelGGL((k_cf32_conv_lds<PM, NS, DG, false>), grid, dim3(256), 0, stream, src, w3, g, out, add);
+  const dim3 grid((Mc + 64 * PM - 1) / (64 * PM), g.Co / 64, csh * csw * ksplit);
+  if (add && ksplit == 1)
+    hipLaunchKernelGGL((k_cf32_conv_lds<PM, NS, DG, true>), grid, dim3(256), 0, stream, src, w3, g, out, add, 1);
+  else
+    hipLaunchKernelGGL((k_cf32_conv_lds<PM, NS, DG, false>), grid, dim3(256), 0, stream, src, w3, g, out, nullptr,
+                       ksplit);
+}
+
+// out[i] = Σ_s part[s][i] (+ add[i]), float4 lanes (the slab is a multiple of 64 floats)
+__global__ __launch_bounds__(256) void k_cf32_ksum(const float* __restrict__ part, int S, int64_t slab,
+                                                   float* __restrict__ out, const float* __restrict__ add) {
+  const int64_t n4 = slab / 4;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n4;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    float4 acc = add ? reinterpret_cast<const float4*>(add)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < S; ++s) {
+      const float4 v = reinterpret_cast<const float4*>(part + s * slab)[i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = acc;
+  }
 }
 
 template <int PM, bool DG>
@@ -564,6 +594,145 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x,
         const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
                           static_cast<int64_t>(co) * K + k;
         if (!GATHER || k < K) out[o] = acc[u][v][e];
+      }
+}
+
+// The 128 co x 128 k form (Cs % 128 == 0, Co % 128 == 0): each wave computes 4 x 4 fragments (64 co x
+// 64 k) instead of 2 x 2, halving the LDS fragment bytes per MFMA (the 64 x 64 form reads 512 B of
+// LDS per MFMA and is LDS-bound). Each operand's [32 pixel][128 channel] step tile is kept as two
+// [32][64] sub-tiles (128-byte pitch: the bank pattern of the 64 x 64 form).
+constexpr int kTB2 = 2 * kTB;              // one operand piece: two [32][64] sub-tiles
+constexpr int kSB2 = 2 * kNP * kTB2;       // dy pieces 0..2 | x pieces 0..2
+
+__global__ __launch_bounds__(256) void k_cf32_wgrad2(const float* __restrict__ x, const float* __restrict__ dy,
+                                                     ConvF32Geo g, int64_t rg, int64_t per_split,
+                                                     float* __restrict__ out, int64_t split_stride,
+                                                     int64_t group_stride) {
+  extern __shared__ __attribute__((aligned(16))) char dlds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = g.KH * g.KW * g.Cs;
+  const int nkb = K / 128;
+  const int kb = blockIdx.x % nkb, cb = blockIdx.x / nkb;
+  const int gi = blockIdx.y, sp = blockIdx.z;
+  const int k0 = kb * 128, co0 = cb * 128;
+  const int tap = k0 / g.Cs, c0 = k0 - tap * g.Cs;
+  const int ti = tap / g.KW, tj = tap - ti * g.KW;
+  const int64_t mbeg = static_cast<int64_t>(gi) * rg + static_cast<int64_t>(sp) * per_split;
+  int64_t mend = mbeg + per_split;
+  if (mend > static_cast<int64_t>(gi + 1) * rg) mend = static_cast<int64_t>(gi + 1) * rg;
+  const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
+
+  // staging: thread t owns rows (t >> 4) and (t >> 4) + 16, channels 4 (t & 15) .. +3 of both sub-tiles
+  const int srow = threadIdx.x >> 4, sch = threadIdx.x & 15;
+  float4 rd[2][2], rx[2][2];   // [row half][sub-tile]
+  auto load = [&](int s) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t m = mbeg + static_cast<int64_t>(s) * 32 + srow + 16 * h;
+      const bool mv = m < mend;
+      const int64_t mm = mv ? m : 0;
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int wo = static_cast<int>(mm % g.Wo);
+      const int64_t t = mm / g.Wo;
+      const int ho = static_cast<int>(t % g.Ho);
+      const int64_t n = t / g.Ho;
+      const int hi = ho * g.sh - g.ph + ti * g.dh, wi = wo * g.sw - g.pw + tj * g.dw;
+      const bool ok = mv && hi >= 0 && hi < g.Hs && wi >= 0 && wi < g.Ws;
+      const float* xp = x + ((n * g.Hs + (ok ? hi : 0)) * g.Ws + (ok ? wi : 0)) * g.Cs + c0 + sch * 4;
+      const float* dp = dy + mm * g.Co + co0 + sch * 4;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float4 d = *reinterpret_cast<const float4*>(dp + 64 * b);
+        const float4 v = *reinterpret_cast<const float4*>(xp + 64 * b);
+        rd[h][b] = mv ? d : z;
+        rx[h][b] = ok ? v : z;
+      }
+    }
+  };
+  auto stage = [&](int slot) {
+    char* base = dlds + slot * kSB2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int off = b * kTB + (srow + 16 * h) * 128 + sch * 8;
+        uint32_t p0[kNP], p1[kNP];
+        split2(rd[h][b].x, rd[h][b].y, p0);
+        split2(rd[h][b].z, rd[h][b].w, p1);
+#pragma unroll
+        for (int i = 0; i < kNP; ++i) *reinterpret_cast<uint2*>(base + i * kTB2 + off) = make_uint2(p0[i], p1[i]);
+        split2(rx[h][b].x, rx[h][b].y, p0);
+        split2(rx[h][b].z, rx[h][b].w, p1);
+#pragma unroll
+        for (int i = 0; i < kNP; ++i)
+          *reinterpret_cast<uint2*>(base + (kNP + i) * kTB2 + off) = make_uint2(p0[i], p1[i]);
+      }
+  };
+
+  // wave (a, b): co sub-tile a = wave >> 1 (fragments 4a .. 4a + 3), k sub-tile b = wave & 1
+  const int sa = wave >> 1, sbk = wave & 1;
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)dlds));
+  const uint32_t offA = sa * kTB + (8 * grp + q) * 128 + (4 * p) * 2;
+  const uint32_t offB = kNP * kTB2 + sbk * kTB + (8 * grp + q) * 128 + (4 * p) * 2;
+
+  if (steps > 0) load(0);
+  for (int s = 0; s < steps; ++s) {
+    stage(s & 1);
+    if (s + 1 < steps) load(s + 1);
+    __syncthreads();
+    const uint32_t sb = lds0 + (s & 1) * kSB2;
+    auto tr_read = [&](uint32_t addr, bf16x8 (&f)[2]) {
+      s16x4 r[4];
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %4\n\t"
+          "ds_read_b64_tr_b16 %1, %4 offset:512\n\t"
+          "ds_read_b64_tr_b16 %2, %4 offset:32\n\t"
+          "ds_read_b64_tr_b16 %3, %4 offset:544\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+          : "v"(addr)
+          : "memory");
+      f[0] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r[0], r[1], 0, 1, 2, 3, 4, 5, 6, 7));
+      f[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r[2], r[3], 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    bf16x8 ta[kNP][4], tb[kNP][4];
+#pragma unroll
+    for (int i = 0; i < kNP; ++i) {
+      bf16x8 t0[2], t1[2];
+      tr_read(sb + i * kTB2 + offA, t0);
+      tr_read(sb + i * kTB2 + offA + 64, t1);   // fragments 2, 3: 32 columns on
+      ta[i][0] = t0[0]; ta[i][1] = t0[1]; ta[i][2] = t1[0]; ta[i][3] = t1[1];
+      tr_read(sb + i * kTB2 + offB, t0);
+      tr_read(sb + i * kTB2 + offB + 64, t1);
+      tb[i][0] = t0[0]; tb[i][1] = t0[1]; tb[i][2] = t1[0]; tb[i][3] = t1[1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const bf16x8 av[kNP] = {ta[0][u], ta[1][u], ta[2][u]};
+        const bf16x8 bv[kNP] = {tb[0][v], tb[1][v], tb[2][v]};
+        acc[u][v] = mma6(av, bv, acc[u][v]);
+      }
+  }
+
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + (4 * sa + u) * 16 + 4 * grp + e;
+        const int k = k0 + (4 * sbk + v) * 16 + li;
+        const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
+                          static_cast<int64_t>(co) * K + k;
+        out[o] = acc[u][v][e];
       }
 }
 
@@ -730,27 +899,53 @@ unsigned blocks_for(int64_t items) { return static_cast<unsigned>((items + 255) 
 
 bool conv_f32_supported(const ConvF32Geo& g) { return g.Co % 64 == 0 && g.Cs > 0 && g.Co > 0; }
 
-int conv_f32_pick(const ConvF32Geo& g) {
-  const int64_t M = static_cast<int64_t>(g.N) * g.Ho * g.Wo;
-  const int64_t nco = g.Co / 64;
-  int pm = 4;
-  while (pm > 1 && ((M + 64 * pm - 1) / (64 * pm)) * nco < 512) pm /= 2;
-  return pm;
+int conv_f32_ksplit(const ConvF32Geo& g, bool dgrad) {
+  // PM = 4 tiles (the best LDS-read / MFMA ratio) and, below 200 of them, split-K up to 200+
+  // workgroups, each split at least 8 k-steps; the slabs cost 2 x S x M x Co x 4 bytes of traffic.
+  // Measured on the ResNet-50 CIFAR shapes (scripts/bench_conv_f32.py, profiles/r4): e.g. 256 ch 3x3
+  // at 2x2 px (128 tiles) 0.158 -> 0.095 ms with S = 2; 512 ch at 1x1 px (64 tiles) 0.32 -> 0.094 ms
+  // with S = 4; 500 tiles and more run best unsplit.
+  const int csh = dgrad ? g.sh : 1, csw = dgrad ? g.sw : 1;
+  const int64_t Mc = static_cast<int64_t>(g.N) * ((g.Ho + csh - 1) / csh) * ((g.Wo + csw - 1) / csw);
+  const int64_t tiles = ((Mc + 255) / 256) * (g.Co / 64) * csh * csw;
+  const int taps = dgrad ? ((g.KH + csh - 1) / csh) * ((g.KW + csw - 1) / csw) : g.KH * g.KW;
+  const int steps = taps * (g.Cs / 32);
+  int S = 1;
+  while (S < 8 && tiles * S < 200 && steps / (2 * S) >= 8) S *= 2;
+  return S;
 }
 
 void conv_f32(const float* src, const uint16_t* w3, const ConvF32Geo& g, bool dgrad, float* out, const float* add,
-              int pm, hipStream_t stream) {
+              int pm, hipStream_t stream, int ksplit, float* part) {
   if (static_cast<int64_t>(g.N) * g.Ho * g.Wo <= 0) return;
-  if (pm <= 0) pm = conv_f32_pick(g) + 10;
+  if (ksplit > 1 && part != nullptr && g.Cs % 32 == 0 && (!dgrad || (g.dh == 1 && g.dw == 1))) {
+    // PM = 4 tiles, split-K into the slabs of `part`, then one summing pass (+ add)
+    if (pm <= 0 || pm == 15) {
+      if (dgrad) launch_conv_lds<4, 3, true>(src, w3, g, part, nullptr, ksplit, stream);
+      else launch_conv_lds<4, 3, false>(src, w3, g, part, nullptr, ksplit, stream);
+    } else {
+      if (dgrad) launch_conv_lds<4, 2, true>(src, w3, g, part, nullptr, ksplit, stream);
+      else launch_conv_lds<4, 2, false>(src, w3, g, part, nullptr, ksplit, stream);
+    }
+    const int64_t slab = static_cast<int64_t>(g.N) * g.Ho * g.Wo * g.Co;
+    int64_t blocks = (slab / 4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_cf32_ksum, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, part, ksplit, slab, out,
+                       add);
+    return;
+  }
+  if (pm <= 0) pm = 15;   // PM = 4, a 3-deep ring: the fastest or within 5 % on every measured shape
   if (pm > 10 && g.Cs % 32 == 0 && (!dgrad || (g.dh == 1 && g.dw == 1))) {   // the LDS-staged kernel
     if (dgrad) {
-      if (pm >= 14) launch_conv_lds<4, 2, true>(src, w3, g, out, add, stream);
-      else if (pm == 12) launch_conv_lds<2, 3, true>(src, w3, g, out, add, stream);
-      else launch_conv_lds<1, 3, true>(src, w3, g, out, add, stream);
+      if (pm == 15) launch_conv_lds<4, 3, true>(src, w3, g, out, add, 1, stream);
+      else if (pm >= 14) launch_conv_lds<4, 2, true>(src, w3, g, out, add, 1, stream);
+      else if (pm == 12) launch_conv_lds<2, 3, true>(src, w3, g, out, add, 1, stream);
+      else launch_conv_lds<1, 3, true>(src, w3, g, out, add, 1, stream);
     } else {
-      if (pm >= 14) launch_conv_lds<4, 2, false>(src, w3, g, out, add, stream);
-      else if (pm == 12) launch_conv_lds<2, 3, false>(src, w3, g, out, add, stream);
-      else launch_conv_lds<1, 3, false>(src, w3, g, out, add, stream);
+      if (pm == 15) launch_conv_lds<4, 3, false>(src, w3, g, out, add, 1, stream);
+      else if (pm >= 14) launch_conv_lds<4, 2, false>(src, w3, g, out, add, 1, stream);
+      else if (pm == 12) launch_conv_lds<2, 3, false>(src, w3, g, out, add, 1, stream);
+      else launch_conv_lds<1, 3, false>(src, w3, g, out, add, 1, stream);
     }
     return;
   }
@@ -767,12 +962,23 @@ void conv_f32(const float* src, const uint16_t* w3, const ConvF32Geo& g, bool dg
 }
 
 bool wgrad_f32_supported(const ConvF32Geo& g) { return g.Cs > 0 && g.Co % 64 == 0; }
+bool wgrad_f32_wide(const ConvF32Geo& g) { return g.Cs % 128 == 0 && g.Co % 128 == 0; }
 
 void wgrad_f32(const float* x, const float* dy, const ConvF32Geo& g, int groups, int64_t rg, int splits, float* out,
                int64_t split_stride, int64_t group_stride, hipStream_t stream) {
   const int K = g.KH * g.KW * g.Cs;
   if (splits < 1) splits = 1;
   const int64_t per_split = (rg + splits - 1) / splits;
+  if (wgrad_f32_wide(g)) {
+    static bool once = (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cf32_wgrad2),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kSB2),
+                        true);
+    (void)once;
+    const dim3 grid2((K / 128) * (g.Co / 128), groups, splits);
+    hipLaunchKernelGGL(k_cf32_wgrad2, grid2, dim3(256), 2 * kSB2, stream, x, dy, g, rg, per_split, out, split_stride,
+                       group_stride);
+    return;
+  }
   const dim3 grid(((K + 63) / 64) * (g.Co / 64), groups, splits);
   if (g.Cs % 64 != 0)
     hipLaunchKernelGGL(k_cf32_wgrad<true>, grid, dim3(256), 0, stream, x, dy, g, rg, per_split, out, split_stride,

@@ -19,13 +19,17 @@ struct ConvF32Geo {
 
 // Cs % 32 == 0, Co % 64 == 0
 bool conv_f32_supported(const ConvF32Geo& g);
-int conv_f32_pick(const ConvF32Geo& g);
+// split-K factor of the automatic choice (1: none); ksplit > 1 needs a `part` workspace of
+// ksplit x N x Ho x Wo x Co floats
+int conv_f32_ksplit(const ConvF32Geo& g, bool dgrad);
 // out[m, co] (+= add, read from `add`) of the forward (w3: the pieces [3][Co][KH][KW][Cs]) or, with
 // dgrad, of the data gradient (w3: the transposed pieces [3][Co = Cin][KH][KW][Cs = Cout], any stride).
 void conv_f32(const float* src, const uint16_t* w3, const ConvF32Geo& g, bool dgrad, float* out, const float* add,
-              int pm, hipStream_t stream);
+              int pm, hipStream_t stream, int ksplit = 1, float* part = nullptr);
 // Cs % 64 == 0, Co % 64 == 0 (g: the forward geometry)
 bool wgrad_f32_supported(const ConvF32Geo& g);
+// the 128 x 128-tile weight gradient takes this layer (Cs % 128 == 0, Co % 128 == 0): 4x fewer tiles
+bool wgrad_f32_wide(const ConvF32Geo& g);
 // out[s][grp][co][k] (fp32) = Σ over the s-th of `splits` ranges of worker grp's rg output pixels of
 // dy[m, co] · patch(x)[m, k]; element offset s * split_stride + grp * group_stride + co * K + k.
 void wgrad_f32(const float* x, const float* dy, const ConvF32Geo& g, int groups, int64_t rg, int splits, float* out,

@@ -919,7 +919,8 @@ def _f32_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> N
     cout = dy.shape[1]
     K = w.numel() // cout
     rows = dy.shape[0] * dy.shape[2] * dy.shape[3] // G
-    S = _iwgrad_splits(rows, -(-K // 64) * (cout // 64) * G)
+    tile = 128 if (x.shape[1] % 128 == 0 and cout % 128 == 0) else 64   # conv_f32.hip: the wide form
+    S = _iwgrad_splits(rows, -(-K // tile) * (cout // tile) * G)
     out = spec.sink.rows_view(w, (cout, K), torch.float32) if S == 1 else None
     if out is not None:
         C_.gpu_wgrad_f32(x, dy, *_geom(spec), G, out, 1)

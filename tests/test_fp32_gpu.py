@@ -58,29 +58,33 @@ SHAPES = [  # N, Cin, Cout, H, k, s, p
     (4, 256, 512, 4, 1, 2, 0), (9, 512, 512, 2, 3, 1, 1), (2, 64, 128, 7, 3, 2, 1), (3, 64, 192, 5, 3, 1, 1)]
 
 
-@pytest.mark.parametrize("pm", [0, 2])
+@pytest.mark.parametrize("pm,ks", [(0, 0), (2, 0), (0, 3), (0, 8)])
 @pytest.mark.parametrize("N,C,Co,H,k,s,p", SHAPES)
-def test_conv_f32_forward_dgrad_match_fp64(cuda, native, N, C, Co, H, k, s, p, pm):
+def test_conv_f32_forward_dgrad_match_fp64(cuda, native, N, C, Co, H, k, s, p, pm, ks):
     """Forward (with and without a fused add) and the data gradient (any stride: the transposed
-    convolution, by parity class on the LDS-staged kernel) against float64 convolutions, on the
-    automatic choice (the LDS-staged kernel) and on the register kernel (pm = 2)."""
+    convolution, by parity class on the LDS-staged kernel; with and without the add) against float64
+    convolutions, on the automatic choice (the LDS-staged kernel, split-K where it picks it), on the
+    register kernel (pm = 2) and with a forced split-K (ks = 3, 8: uneven and empty splits)."""
     x = cl(torch.randn(N, C, H, H, device=cuda))
     w = cl(torch.randn(Co, C, k, k, device=cuda) / (C * k * k) ** 0.5)
     w3, wt3 = _split(native, w)
     ref = F.conv2d(x.double(), w.double(), None, s, p)
-    y = cl(torch.empty(ref.shape, device=cuda))
-    native.gpu_conv_f32(x, w3, k, k, s, s, p, p, 1, 1, False, y, None, pm)
+    y = cl(torch.full(ref.shape, float("nan"), device=cuda))
+    native.gpu_conv_f32(x, w3, k, k, s, s, p, p, 1, 1, False, y, None, pm, ks)
     assert rel(y, ref) < TOL
     add = cl(torch.randn(ref.shape, device=cuda))
     y2 = add.clone()
-    native.gpu_conv_f32(x, w3, k, k, s, s, p, p, 1, 1, False, y2, y2, pm)
+    native.gpu_conv_f32(x, w3, k, k, s, s, p, p, 1, 1, False, y2, y2, pm, ks)
     assert rel(y2, ref + add.double()) < TOL
     dy = cl(torch.randn(ref.shape, device=cuda))
     dref = torch.nn.grad.conv2d_input(x.shape, w.double(), dy.double(), s, p)
-    dx = cl(torch.empty(x.shape, device=cuda))
     dx = cl(torch.full(x.shape, float("nan"), device=cuda))   # every pixel is written (zero-tap classes too)
-    native.gpu_conv_f32(dy, wt3, k, k, s, s, p, p, 1, 1, True, dx, None, pm)
+    native.gpu_conv_f32(dy, wt3, k, k, s, s, p, p, 1, 1, True, dx, None, pm, ks)
     assert rel(dx, dref) < TOL
+    addx = cl(torch.randn(x.shape, device=cuda))
+    dx2 = addx.clone()
+    native.gpu_conv_f32(dy, wt3, k, k, s, s, p, p, 1, 1, True, dx2, dx2, pm, ks)
+    assert rel(dx2, dref + addx.double()) < TOL
 
 
 @pytest.mark.parametrize("G,B,C,Co,H,k,s,p,S", [(4, 3, 64, 64, 8, 3, 1, 1, 1), (4, 3, 64, 64, 8, 3, 1, 1, 4),
@@ -260,7 +264,8 @@ def _cpu_grads(model, x, y) -> torch.Tensor:
 
 def _fp32_rows_vs_references(cuda, name, k, B, bn_bias=None, shape=(3, 32, 32)):
     """Per worker: (ours vs float64 CPU autograd, PyTorch fp32 CPU autograd vs float64, ours vs fp32
-    GPU autograd). bn_bias: every BatchNorm shift set to this value first."""
+    CPU autograd, ours vs fp32 GPU autograd, fp32 GPU autograd vs float64). bn_bias: every
+    BatchNorm shift set to this value first."""
     torch.manual_seed(0)
     ref = build_model(name, 10).to(cuda)
     eng = RobustDataParallel(build_model(name, 10), F.cross_entropy, DistContext(device=cuda),
@@ -290,7 +295,8 @@ def _fp32_rows_vs_references(cuda, name, k, B, bn_bias=None, shape=(3, 32, 32)):
         g_eng = torch.cat([v.reshape(-1) for v in eng.flat.views(eng.X[j, 0])])
         xc, yc = x.float().cpu(), y.cpu()
         g64 = _cpu_grads(m64, xc.double(), yc)
-        out.append((rel(g_eng, g64), rel(_cpu_grads(m32, xc, yc), g64), rel(g_eng, g_gpu32)))
+        g32 = _cpu_grads(m32, xc, yc)
+        out.append((rel(g_eng, g64), rel(g32, g64), rel(g_eng, g32), rel(g_eng, g_gpu32), rel(g_gpu32, g64)))
     return out
 
 
@@ -300,11 +306,14 @@ def test_fp32_grouped_rows_match_fp32_autograd(cuda, name):
     of fp32 autograd run worker by worker AND of float64 autograd, at the CIFAR shape (k = 4 workers
     of 8 images), in the ReLU-kink-free regime: every BatchNorm shift = 6, so no pre-activation lies
     within rounding distance of a ReLU's kink (see the next test for why that matters); PyTorch's
-    own fp32 CPU autograd is then within 3e-7 (ResNet-18) / 1.2e-5 (ResNet-50) of float64."""
+    own fp32 CPU autograd is then within 3e-7 (ResNet-18) / 1.2e-5 (ResNet-50) of float64. (fp32 GPU
+    autograd -- MIOpen -- is itself ~1e-4 from float64 on ResNet-50: printed, not asserted.)"""
     res = _fp32_rows_vs_references(cuda, name, 4, 8, bn_bias=6.0)
-    print(name, [tuple(f"{v:.2e}" for v in r) for r in res])
-    for ours64, _, ours32 in res:
+    print(name, "(ours-fp64, torch32cpu-fp64, ours-torch32cpu, ours-torch32gpu, torch32gpu-fp64):",
+          [tuple(f"{v:.2e}" for v in r) for r in res])
+    for ours64, cpu64, ours32, _, _ in res:
         assert ours64 < 1e-4 and ours32 < 1e-4, res
+        assert ours64 < 3 * cpu64 + 1e-6, res     # as close to float64 as PyTorch's fp32
 
 
 @pytest.mark.parametrize("name,floor", [("resnet18", 2e-2), ("resnet50", 2.5e-1)])
@@ -317,7 +326,7 @@ def test_fp32_grouped_rows_at_init_within_the_kink_floor(cuda, name, floor):
     gradient as far (scripts/diag_fp32_rows.py). So here: every worker within that floor of float64
     (no gross error anywhere); the per-worker errors are printed next to PyTorch fp32's."""
     res = _fp32_rows_vs_references(cuda, name, 4, 8)
-    print(name, "(ours vs fp64, PyTorch fp32 CPU vs fp64, ours vs fp32 GPU):",
+    print(name, "(ours-fp64, torch32cpu-fp64, ours-torch32cpu, ours-torch32gpu, torch32gpu-fp64):",
           [tuple(f"{v:.2e}" for v in r) for r in res])
     assert max(r[0] for r in res) < floor, res
 
