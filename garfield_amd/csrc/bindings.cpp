@@ -1062,7 +1062,7 @@ void g_conv_f32(const at::Tensor& src, const at::Tensor& w3, int64_t kh, int64_t
   c10::hip::HIPGuard guard(dev.index());
   // split-K: automatic with the automatic kernel choice (pm <= 0, ksplit 0), or forced (ksplit > 1)
   int S = ksplit > 0 ? static_cast<int>(ksplit) : (pm <= 0 ? garfield::gpu::conv_f32_ksplit(g, dgrad) : 1);
-  if (g.Cs % 32 != 0 || (dgrad && (g.dh != 1 || g.dw != 1))) S = 1;
+  if (!garfield::gpu::conv_f32_lds_ok(g, dgrad)) S = 1;
   at::Tensor part;
   if (S > 1) part = at::empty({S * out.numel()}, out.options().memory_format(at::MemoryFormat::Contiguous));
   garfield::gpu::conv_f32(src.data_ptr<float>(), reinterpret_cast<const uint16_t*>(w3.data_ptr()), g, dgrad,
@@ -1092,6 +1092,7 @@ void g_wgrad_f32(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t 
   TORCH_CHECK(dy.size(0) == g.N && conv_out(g.Hs, kh, sh, ph, dh) == g.Ho && conv_out(g.Ws, kw, sw, pw, dw) == g.Wo,
               "gpu_wgrad_f32: dy is not the forward output of x");
   TORCH_CHECK(garfield::gpu::wgrad_f32_supported(g), "gpu_wgrad_f32: needs Cout % 64 == 0");
+  TORCH_CHECK(dy.numel() / g.Co < (int64_t{1} << 31), "gpu_wgrad_f32: more than 2^31 output pixels");
   const int64_t M = static_cast<int64_t>(g.N) * g.Ho * g.Wo;
   TORCH_CHECK(groups >= 1 && M % groups == 0, "gpu_wgrad_f32: ", M, " output pixels do not split into ", groups,
               " workers");

@@ -272,29 +272,42 @@ __global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__
   const int steps = (sbeg + chunk < all_steps ? sbeg + chunk : all_steps) - sbeg;
   if (ksplit > 1) out += static_cast<int64_t>(kz) * g.N * g.Ho * g.Wo * g.Co;   // this split's slab
 
-  // this lane's activation rows: rows (wave * XI + u) * 8 + lane / 8 of the tile, chunk lane % 8
+  // taps of the class in k-step order t = ti * nj + tj: source offset (di, dj) of tap t relative to
+  // the row's base pixel -- forward (i·dh, j·dw); data gradient (dI0 - ti, dJ0 - tj) with
+  // dI0 = (ca + ph - ti0) / sh (exact in this class)
+  const int dI0 = DG ? (ca + g.ph - ti0) / g.sh : 0, dJ0 = DG ? (cb + g.pw - tj0) / g.sw : 0;
+  auto tap_di = [&](int ti) { return DG ? dI0 - ti : (ti0 + ti * tsi) * g.dh; };
+  auto tap_dj = [&](int tj) { return DG ? dJ0 - tj : (tj0 + tj * tsj) * g.dw; };
+
+  // this lane's activation rows: rows (wave * XI + u) * 8 + lane / 8 of the tile, chunk lane % 8. Per
+  // row: its base element offset (with the lane's swizzled chunk) and the bit mask of the taps whose
+  // source pixel is inside the image (KH * KW <= 32), so a k-step costs a shift, an add and a select.
   const int xr = lane >> 3, xc = lane & 7;
-  int xh[XI], xw[XI], xn[XI];
-  bool xv[XI];
+  int xoff[XI];
+  uint32_t xmask[XI];
 #pragma unroll
   for (int u = 0; u < XI; ++u) {
     const int row = (wave * XI + u) * 8 + xr;
     const int m = m0 + row;
-    xv[u] = m < Mc;
-    const int mm = xv[u] ? m : 0;
+    const int mm = m < Mc ? m : 0;
     const int wc = mm % Wc;
     const int t = mm / Wc;
-    const int hc = t % Hc;
-    xn[u] = t / Hc;
-    if constexpr (DG) {   // source dy row of tap i: hc + (ca + ph - i) / sh (exact in this class)
-      xh[u] = hc;
-      xw[u] = wc;
-    } else {
-      xh[u] = hc * g.sh - g.ph;
-      xw[u] = wc * g.sw - g.pw;
-    }
+    const int hc = t % Hc, n = t / Hc;
+    const int hb = DG ? hc : hc * g.sh - g.ph, wb = DG ? wc : wc * g.sw - g.pw;
+    uint32_t mask = 0;
+    if (m < Mc)
+      for (int ti = 0; ti < ni; ++ti) {
+        const int hs = hb + tap_di(ti);
+        if (hs < 0 || hs >= g.Hs) continue;
+        for (int tj = 0; tj < nj; ++tj) {
+          const int ws = wb + tap_dj(tj);
+          if (ws >= 0 && ws < g.Ws) mask |= 1u << (ti * nj + tj);
+        }
+      }
+    xmask[u] = mask;
+    const int swz = (row >> 1) & 7;   // chunk swizzle: 16 consecutive rows of one fragment read hit 16 bank groups
+    xoff[u] = ((n * g.Hs + hb) * g.Ws + wb) * g.Cs + (xc ^ swz) * 4;
   }
-  const int xsw = 2 * ((xr >> 1) & 3);          // chunk swizzle of the activation rows (even: pairs stay adjacent)
   // weight rows: glds block q covers rows 16 q .. 16 q + 15 of one piece, lane -> row lane / 4, chunk lane % 4
   const int wr = lane >> 2, wcn = lane & 3;
   const int64_t piece = static_cast<int64_t>(g.Co) * K;
@@ -307,34 +320,38 @@ __global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__
   }
   const uint64_t az = reinterpret_cast<uint64_t>(g_cf32_zero);
 
-  auto issue = [&](int sl, int slot) {
-    const int s = sbeg + sl;
-    const int tap = s / csteps;
-    const int c0 = (s - tap * csteps) * 32;
-    const int ti = tap / nj, tj = tap - (tap / nj) * nj;
-    const int i = ti0 + ti * tsi, j = tj0 + tj * tsj;
+  // k-step walk (issue order): tap (ti, tj), channel block c0 -- no divisions in the loop
+  int it_ti, it_tj, it_c0;
+  {
+    const int tap = sbeg / csteps;
+    it_c0 = (sbeg - tap * csteps) * 32;
+    it_ti = nj ? tap / nj : 0;
+    it_tj = tap - it_ti * nj;
+  }
+  auto issue = [&](int slot) {
+    const int i = ti0 + it_ti * tsi, j = tj0 + it_tj * tsj;
+    const int tbit = it_ti * nj + it_tj;
     char* base = lds + slot * SB;
-    const int koff = (i * g.KW + j) * g.Cs + c0;
+    const int koff = (i * g.KW + j) * g.Cs + it_c0;
 #pragma unroll
     for (int u = 0; u < WI; ++u)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(wsrc[u] + koff),
                                        (lds_ptr)(base + (wave * WI + u) * 1024), 16, 0, 0);
+    const int toff = (tap_di(it_ti) * g.Ws + tap_dj(it_tj)) * g.Cs + it_c0;
 #pragma unroll
     for (int u = 0; u < XI; ++u) {
-      int hs, ws;
-      if constexpr (DG) {
-        hs = xh[u] + (ca + g.ph - i) / g.sh;
-        ws = xw[u] + (cb + g.pw - j) / g.sw;
-      } else {
-        hs = xh[u] + i * g.dh;
-        ws = xw[u] + j * g.dw;
-      }
-      const bool ok = xv[u] && hs >= 0 && hs < g.Hs && ws >= 0 && ws < g.Ws;
-      const int hc = ok ? hs : 0, wc = ok ? ws : 0;
-      const uint64_t ax = reinterpret_cast<uint64_t>(
-          src + ((static_cast<int64_t>(xn[u]) * g.Hs + hc) * g.Ws + wc) * g.Cs + c0 + (xc ^ xsw) * 4);
+      const bool ok = (xmask[u] >> tbit) & 1u;
+      const uint64_t ax = reinterpret_cast<uint64_t>(src + (xoff[u] + toff));
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? ax : az),
                                        (lds_ptr)(base + WB + (wave * XI + u) * 1024), 16, 0, 0);
+    }
+    it_c0 += 32;
+    if (it_c0 == g.Cs) {
+      it_c0 = 0;
+      if (++it_tj == nj) {
+        it_tj = 0;
+        ++it_ti;
+      }
     }
   };
 
@@ -347,14 +364,14 @@ __global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int s0 = 0; s0 < NS - 1; ++s0)
-    if (s0 < steps) issue(s0, s0);
+    if (s0 < steps) issue(s0);
   for (int s = 0; s < steps; ++s) {
     const int ahead = (steps - 1 - s) < (NS - 2) ? (steps - 1 - s) : (NS - 2);
     if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
+    if (s + NS - 1 < steps) issue((s + NS - 1) % NS);
     const char* base = lds + (s % NS) * SB;
     bf16x8 a[4][kNP];
 #pragma unroll
@@ -367,9 +384,9 @@ __global__ __launch_bounds__(256) void k_cf32_conv_lds(const float* __restrict__
 #pragma unroll
     for (int r = 0; r < PM; ++r) {
       const int row = (wave * PM + r) * 16 + fr;
-      const int ch = (2 * fq) ^ (2 * ((row >> 1) & 3));
-      const float4 v0 = *reinterpret_cast<const float4*>(base + WB + row * 128 + ch * 16);
-      const float4 v1 = *reinterpret_cast<const float4*>(base + WB + row * 128 + ch * 16 + 16);
+      const int swz = (row >> 1) & 7;
+      const float4 v0 = *reinterpret_cast<const float4*>(base + WB + row * 128 + ((2 * fq) ^ swz) * 16);
+      const float4 v1 = *reinterpret_cast<const float4*>(base + WB + row * 128 + ((2 * fq + 1) ^ swz) * 16);
       bf16x8 b[kNP];
       split8(v0, v1, b);
 #pragma unroll
@@ -452,6 +469,13 @@ void launch_conv(const float* src, const uint16_t* w3, const ConvF32Geo& g, floa
 // ---------------------------------------------------------------------------------------------
 // per-worker weight gradient
 
+// transposed fragment read through the compiler builtin (the compiler tracks the returned registers,
+// so a step's reads are all in flight before the first wait)
+__device__ __forceinline__ s16x4 tr16(uint32_t lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      reinterpret_cast<__attribute__((address_space(3))) s16x4*>(static_cast<uintptr_t>(lds_addr)));
+}
+
 constexpr int kTB = 32 * 128;          // one [32 pixel][64 channel] bf16 tile
 constexpr int kSB = 2 * kNP * kTB;     // dy pieces 0..2 | x pieces 0..2
 
@@ -476,6 +500,7 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x,
   int64_t mend = mbeg + per_split;
   if (mend > static_cast<int64_t>(gi + 1) * rg) mend = static_cast<int64_t>(gi + 1) * rg;
   const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
+  const FastDiv fWo = make_fastdiv(g.Wo), fHo = make_fastdiv(g.Ho);
 
   // staging: thread t owns rows (t >> 4) and (t >> 4) + 16 of the step's 32 pixels, channels 4 (t & 15) .. +3
   const int srow = threadIdx.x >> 4, sch = threadIdx.x & 15;
@@ -489,10 +514,11 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x,
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 d = *reinterpret_cast<const float4*>(dy + mm * g.Co + co0 + sch * 4);
       rd[h] = mv ? d : z;
-      const int wo = static_cast<int>(mm % g.Wo);
-      const int64_t t = mm / g.Wo;
-      const int ho = static_cast<int>(t % g.Ho);
-      const int64_t n = t / g.Ho;
+      uint32_t t, uwo, un, uho;   // m < 2^31 (checked by the host)
+      fdivmod(static_cast<uint32_t>(mm), fWo, t, uwo);
+      fdivmod(t, fHo, un, uho);
+      const int wo = static_cast<int>(uwo), ho = static_cast<int>(uho);
+      const int64_t n = un;
       if constexpr (GATHER) {
         float v[4];
 #pragma unroll
@@ -553,18 +579,9 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x,
     const uint32_t sb = lds0 + (s & 1) * kSB;
     // transposed fragments (see k_iwgrad in iconv_nhwc.hip) of one piece tile: two fragments u
     auto tr_read = [&](uint32_t addr, bf16x8 (&f)[2]) {
-      s16x4 r[4];
-      asm volatile(
-          "ds_read_b64_tr_b16 %0, %4\n\t"
-          "ds_read_b64_tr_b16 %1, %4 offset:512\n\t"
-          "ds_read_b64_tr_b16 %2, %4 offset:32\n\t"
-          "ds_read_b64_tr_b16 %3, %4 offset:544\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
-          : "v"(addr)
-          : "memory");
-      f[0] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r[0], r[1], 0, 1, 2, 3, 4, 5, 6, 7));
-      f[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r[2], r[3], 0, 1, 2, 3, 4, 5, 6, 7));
+      const s16x4 r0 = tr16(addr), r1 = tr16(addr + 512), r2 = tr16(addr + 32), r3 = tr16(addr + 544);
+      f[0] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+      f[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7));
     };
     bf16x8 ta[kNP][2], tb[kNP][2];
 #pragma unroll
@@ -601,6 +618,10 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x,
 // 64 k) instead of 2 x 2, halving the LDS fragment bytes per MFMA (the 64 x 64 form reads 512 B of
 // LDS per MFMA and is LDS-bound). Each operand's [32 pixel][128 channel] step tile is kept as two
 // [32][64] sub-tiles (128-byte pitch: the bank pattern of the 64 x 64 form).
+// LDS swizzle of the transposed-read tiles: 8-byte unit u of pixel row r is stored at u ^ 4 tr_swz(r),
+// so the 32 (row, unit) pairs one half-wave's ds_read_b64_tr_b16 touches (rows {0..3, 8..11} + 16 j,
+// four units) fall on distinct bank pairs (unswizzled: 4-way conflicts, 60 % of the LDS cycles)
+__device__ __forceinline__ int tr_swz(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 1); }
 constexpr int kTB2 = 2 * kTB;              // one operand piece: two [32][64] sub-tiles
 constexpr int kSB2 = 2 * kNP * kTB2;       // dy pieces 0..2 | x pieces 0..2
 
@@ -621,6 +642,7 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad2(const float* __restrict__ x
   int64_t mend = mbeg + per_split;
   if (mend > static_cast<int64_t>(gi + 1) * rg) mend = static_cast<int64_t>(gi + 1) * rg;
   const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
+  const FastDiv fWo = make_fastdiv(g.Wo), fHo = make_fastdiv(g.Ho);
 
   // staging: thread t owns rows (t >> 4) and (t >> 4) + 16, channels 4 (t & 15) .. +3 of both sub-tiles
   const int srow = threadIdx.x >> 4, sch = threadIdx.x & 15;
@@ -632,10 +654,11 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad2(const float* __restrict__ x
       const bool mv = m < mend;
       const int64_t mm = mv ? m : 0;
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      const int wo = static_cast<int>(mm % g.Wo);
-      const int64_t t = mm / g.Wo;
-      const int ho = static_cast<int>(t % g.Ho);
-      const int64_t n = t / g.Ho;
+      uint32_t t, uwo, un, uho;   // m < 2^31 (checked by the host)
+      fdivmod(static_cast<uint32_t>(mm), fWo, t, uwo);
+      fdivmod(t, fHo, un, uho);
+      const int wo = static_cast<int>(uwo), ho = static_cast<int>(uho);
+      const int64_t n = un;
       const int hi = ho * g.sh - g.ph + ti * g.dh, wi = wo * g.sw - g.pw + tj * g.dw;
       const bool ok = mv && hi >= 0 && hi < g.Hs && wi >= 0 && wi < g.Ws;
       const float* xp = x + ((n * g.Hs + (ok ? hi : 0)) * g.Ws + (ok ? wi : 0)) * g.Cs + c0 + sch * 4;
@@ -655,7 +678,8 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad2(const float* __restrict__ x
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        const int off = b * kTB + (srow + 16 * h) * 128 + sch * 8;
+        const int row = srow + 16 * h;
+        const int off = b * kTB + row * 128 + ((sch ^ (4 * tr_swz(row))) * 8);
         uint32_t p0[kNP], p1[kNP];
         split2(rd[h][b].x, rd[h][b].y, p0);
         split2(rd[h][b].z, rd[h][b].w, p1);
@@ -678,8 +702,15 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad2(const float* __restrict__ x
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)dlds));
-  const uint32_t offA = sa * kTB + (8 * grp + q) * 128 + (4 * p) * 2;
-  const uint32_t offB = kNP * kTB2 + sbk * kTB + (8 * grp + q) * 128 + (4 * p) * 2;
+  // fragment k (columns 16 k .. 16 k + 15) of a sub-tile: 8-byte unit 4 k + p of row 8 grp + q, stored
+  // at unit (4 k + p) ^ 4 tr_swz(row) (rows + 4 share the swizzle)
+  const int trow = 8 * grp + q, tsw = tr_swz(trow);
+  uint32_t offA[4], offB[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    offA[k] = sa * kTB + trow * 128 + ((4 * (k ^ tsw) + p) * 8);
+    offB[k] = kNP * kTB2 + sbk * kTB + trow * 128 + ((4 * (k ^ tsw) + p) * 8);
+  }
 
   if (steps > 0) load(0);
   for (int s = 0; s < steps; ++s) {
@@ -687,29 +718,23 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad2(const float* __restrict__ x
     if (s + 1 < steps) load(s + 1);
     __syncthreads();
     const uint32_t sb = lds0 + (s & 1) * kSB2;
-    auto tr_read = [&](uint32_t addr, bf16x8 (&f)[2]) {
-      s16x4 r[4];
-      asm volatile(
-          "ds_read_b64_tr_b16 %0, %4\n\t"
-          "ds_read_b64_tr_b16 %1, %4 offset:512\n\t"
-          "ds_read_b64_tr_b16 %2, %4 offset:32\n\t"
-          "ds_read_b64_tr_b16 %3, %4 offset:544\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
-          : "v"(addr)
-          : "memory");
-      f[0] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r[0], r[1], 0, 1, 2, 3, 4, 5, 6, 7));
-      f[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r[2], r[3], 0, 1, 2, 3, 4, 5, 6, 7));
+    // fragments at a0, a1 (rows r and r + 4 each): the compiler builtin, so the 24 reads of a step are
+    // in flight together (no LDS-DMA runs in this kernel: the waits it places cost nothing)
+    auto tr_read = [&](uint32_t a0, uint32_t a1, bf16x8 (&f)[2]) {
+      const s16x4 r0 = tr16(a0), r1 = tr16(a0 + 512), r2 = tr16(a1), r3 = tr16(a1 + 512);
+      f[0] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+      f[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7));
     };
     bf16x8 ta[kNP][4], tb[kNP][4];
 #pragma unroll
     for (int i = 0; i < kNP; ++i) {
+      const uint32_t pb = sb + i * kTB2;
       bf16x8 t0[2], t1[2];
-      tr_read(sb + i * kTB2 + offA, t0);
-      tr_read(sb + i * kTB2 + offA + 64, t1);   // fragments 2, 3: 32 columns on
+      tr_read(pb + offA[0], pb + offA[1], t0);
+      tr_read(pb + offA[2], pb + offA[3], t1);
       ta[i][0] = t0[0]; ta[i][1] = t0[1]; ta[i][2] = t1[0]; ta[i][3] = t1[1];
-      tr_read(sb + i * kTB2 + offB, t0);
-      tr_read(sb + i * kTB2 + offB + 64, t1);
+      tr_read(pb + offB[0], pb + offB[1], t0);
+      tr_read(pb + offB[2], pb + offB[3], t1);
       tb[i][0] = t0[0]; tb[i][1] = t0[1]; tb[i][2] = t1[0]; tb[i][3] = t1[1];
     }
 #pragma unroll
@@ -899,6 +924,13 @@ unsigned blocks_for(int64_t items) { return static_cast<unsigned>((items + 255) 
 
 bool conv_f32_supported(const ConvF32Geo& g) { return g.Co % 64 == 0 && g.Cs > 0 && g.Co > 0; }
 
+// the LDS-staged kernel's preconditions: 32-channel k-steps, a tap mask of <= 32 bits, 32-bit element
+// offsets into the source, unit dilation for the transposed (data-gradient) form
+bool conv_f32_lds_ok(const ConvF32Geo& g, bool dgrad) {
+  return g.Cs % 32 == 0 && g.KH * g.KW <= 32 && (!dgrad || (g.dh == 1 && g.dw == 1)) &&
+         static_cast<int64_t>(g.N) * g.Hs * g.Ws * g.Cs < (int64_t{1} << 31);
+}
+
 int conv_f32_ksplit(const ConvF32Geo& g, bool dgrad) {
   // PM = 4 tiles (the best LDS-read / MFMA ratio) and, below 200 of them, split-K up to 200+
   // workgroups, each split at least 8 k-steps; the slabs cost 2 x S x M x Co x 4 bytes of traffic.
@@ -918,7 +950,7 @@ int conv_f32_ksplit(const ConvF32Geo& g, bool dgrad) {
 void conv_f32(const float* src, const uint16_t* w3, const ConvF32Geo& g, bool dgrad, float* out, const float* add,
               int pm, hipStream_t stream, int ksplit, float* part) {
   if (static_cast<int64_t>(g.N) * g.Ho * g.Wo <= 0) return;
-  if (ksplit > 1 && part != nullptr && g.Cs % 32 == 0 && (!dgrad || (g.dh == 1 && g.dw == 1))) {
+  if (ksplit > 1 && part != nullptr && conv_f32_lds_ok(g, dgrad)) {
     // PM = 4 tiles, split-K into the slabs of `part`, then one summing pass (+ add)
     if (pm <= 0 || pm == 15) {
       if (dgrad) launch_conv_lds<4, 3, true>(src, w3, g, part, nullptr, ksplit, stream);
@@ -935,7 +967,7 @@ void conv_f32(const float* src, const uint16_t* w3, const ConvF32Geo& g, bool dg
     return;
   }
   if (pm <= 0) pm = 15;   // PM = 4, a 3-deep ring: the fastest or within 5 % on every measured shape
-  if (pm > 10 && g.Cs % 32 == 0 && (!dgrad || (g.dh == 1 && g.dw == 1))) {   // the LDS-staged kernel
+  if (pm > 10 && conv_f32_lds_ok(g, dgrad)) {   // the LDS-staged kernel
     if (dgrad) {
       if (pm == 15) launch_conv_lds<4, 3, true>(src, w3, g, out, add, 1, stream);
       else if (pm >= 14) launch_conv_lds<4, 2, true>(src, w3, g, out, add, 1, stream);

@@ -19,6 +19,7 @@ struct ConvF32Geo {
 
 // Cs % 32 == 0, Co % 64 == 0
 bool conv_f32_supported(const ConvF32Geo& g);
+bool conv_f32_lds_ok(const ConvF32Geo& g, bool dgrad);
 // split-K factor of the automatic choice (1: none); ksplit > 1 needs a `part` workspace of
 // ksplit x N x Ho x Wo x Co floats
 int conv_f32_ksplit(const ConvF32Geo& g, bool dgrad);

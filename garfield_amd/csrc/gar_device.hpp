@@ -279,6 +279,25 @@ void by_dtype(int dt, A&&... a) {
 }
 
 
+// Division by a run-time constant d >= 1 without the ~30-instruction integer division sequence
+// (Granlund-Montgomery with a 33-bit multiplier): q = (umulhi(n, m) + n) >> l, exact for n < 2^31.
+// Pixel decompositions in the k-loops of the implicit-GEMM kernels (m -> n, h, w) use it.
+struct FastDiv {
+  uint32_t d, m, l;
+};
+__host__ __device__ inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = ((1ull << (32 + l)) / d) - (1ull << 32) + 1;
+  return FastDiv{d, static_cast<uint32_t>(m), l};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.l; }
+// q = n / d, r = n - q d
+__device__ __forceinline__ void fdivmod(uint32_t n, const FastDiv& f, uint32_t& q, uint32_t& r) {
+  q = fdiv(n, f);
+  r = n - q * f.d;
+}
+
 }  // namespace dev
 }  // namespace gpu
 }  // namespace garfield
