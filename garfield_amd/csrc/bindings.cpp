@@ -1073,7 +1073,8 @@ void g_conv_f32(const at::Tensor& src, const at::Tensor& w3, int64_t kh, int64_t
 // per-worker weight gradients of a convolution (forward geometry from x, dy): out fp32
 // [splits, groups, Cout, K] contiguous, or (splits == 1) a [groups, Cout, K] view with contiguous rows
 void g_wgrad_f32(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
-                 int64_t pw, int64_t dh, int64_t dw, int64_t groups, const at::Tensor& out, int64_t splits) {
+                 int64_t pw, int64_t dh, int64_t dw, int64_t groups, const at::Tensor& out, int64_t splits,
+                 int64_t variant) {
   const auto dev = x.device();
   check_f32_cl(x, dev, "x");
   check_f32_cl(dy, dev, "dy");
@@ -1113,8 +1114,11 @@ void g_wgrad_f32(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t 
     gs = out.stride(0);
   }
   c10::hip::HIPGuard guard(dev.index());
+  TORCH_CHECK(variant >= 0 && variant <= 3 && ((variant != 1 && variant != 2) || garfield::gpu::wgrad_f32_wide(g)),
+              "gpu_wgrad_f32: variant 0 auto, 1/2 the 128x128 form (Cin, Cout % 128 == 0), 3 the 64x64 form");
   garfield::gpu::wgrad_f32(x.data_ptr<float>(), dy.data_ptr<float>(), g, static_cast<int>(groups), M / groups,
-                           static_cast<int>(splits), out.data_ptr<float>(), ss, gs, stream_of(dev));
+                           static_cast<int>(splits), out.data_ptr<float>(), ss, gs, stream_of(dev),
+                           static_cast<int>(variant));
 }
 
 // jobs: (w fp32 [R, T, C] memory order, pieces bf16 [3, R, ld], tpieces [3, C, T, R] or None, R, T, C, ld)
@@ -1787,8 +1791,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     g.Co = static_cast<int>(co);
     return garfield::gpu::conv_f32_supported(g);
   }, py::arg("cs"), py::arg("co"));
-  m.def("gpu_wgrad_f32", &g_wgrad_f32, "Per-worker fp32 weight gradient on split-bf16 MFMA; args (x, dy, kh, kw, "
-        "sh, sw, ph, pw, dh, dw, groups, out, splits)");
+  m.def("gpu_wgrad_f32", &g_wgrad_f32, py::arg("x"), py::arg("dy"), py::arg("kh"), py::arg("kw"), py::arg("sh"),
+        py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("groups"), py::arg("out"),
+        py::arg("splits"), py::arg("variant") = 0,
+        "Per-worker fp32 weight gradient on split-bf16 MFMA (variant: 0 auto, 1 / 2 the 128x128 tile double- / "
+        "single-buffered, 3 the 64x64 tile)");
   m.def("gpu_wsplit_multi", &g_wsplit_multi, "Per-step weight split of many fp32 weights: W -> its three bf16 "
         "pieces (row pitch ld) and, optionally, the channel-transposed pieces of the data gradient");
   m.def("gpu_linear_f32_fwd", [](const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& b,

@@ -6,7 +6,8 @@
 // one-stage-ahead ring of its 256-pixel variant leaves the load latency exposed. Measured on the
 // CIFAR ResNet-18 step this is 26 % of the bf16 MFMA peak (profiles/r3/configs/rocprof_r18_krum_f2.txt).
 //
-// Here a workgroup's output tile is TR WHOLE image rows (BM = 64 * PMF pixels, W | BM), and its
+// Here a workgroup's output tile is TR WHOLE image rows (TP = TR * W <= BM = 64 * PMF pixels; any
+// width: 224 of 256 pixels at W = 56, so the ImageNet widths 56 / 28 / 14 / 7 run here too), and its
 // input is staged ONCE per 64-channel block as a zero-padded halo: per image segment of the tile,
 // (rows + 2) x (W + 2) pixels (a 32-wide image: 10 x 34 pixels for 256 outputs, 1.33x instead of
 // 9x). The nine taps then read their B fragments from the halo at a uniform shift (i * (W + 2) + j),
@@ -41,14 +42,13 @@ using lds_ptr = __attribute__((address_space(3))) void*;
 __device__ __attribute__((aligned(16))) uint4 g_c3_zero[8];   // 128 zero bytes: padded pixels
 
 struct Halo {
-  int TR;    // output rows per tile (BM / W)
+  int TR;    // output rows per tile: the most whole rows with TR * W <= BM that tile the images evenly
+  int TP;    // output pixels per tile: TR * W (= BM for power-of-two widths; 224 of 256 at W = 56)
   int TRI;   // output rows per image segment: min(TR, H)
   int SW;    // staged columns: W + 2
   int SEGP;  // staged pixels per segment: (TRI + 2) * SW
   int NPIX;  // staged pixels per tile: (TR / TRI) * SEGP
   int nu;    // halo glds instructions per wave: ceil(NPIX / 32) <= NU
-  int lw;    // log2 W (W divides the power-of-two tile, so W and TRI are powers of two)
-  int lt;    // log2 TRI
 };
 
 constexpr int EPI_PLAIN = 0, EPI_ADD = 1, EPI_STATS = 2;
@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
   const int M = g.N * g.Ho * g.Wo;
   const int st = g.sh;                 // 1, or 2 (a downsampling convolution)
   const int R0 = blockIdx.x * hp.TR;   // first output (global) row of the tile
-  const int m0 = blockIdx.x * BM;
+  const int m0 = blockIdx.x * hp.TP;
+  const int mlim = m0 + hp.TP < M ? m0 + hp.TP : M;   // pixels past TP (a non-power-of-two width) are idle
   const int co0 = blockIdx.y * 64;
   const int lc = lane & 7;             // this lane's 16-byte slot of a staged row
 
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
     const int ml = (wave * PMF + r) * 16 + fr;
     const int t = ml / g.Wo, col = ml - (ml / g.Wo) * g.Wo;
     const int seg = t / hp.TRI;
-    sp0[r] = seg * hp.SEGP + (t - seg * hp.TRI) * st * hp.SW + col * st;
+    sp0[r] = ml < hp.TP ? seg * hp.SEGP + (t - seg * hp.TRI) * st * hp.SW + col * st : 0;
   }
 
   f32x4 acc[PMF][4];
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
     }
   }
 
-  conv_epilogue<PMF, EPI>(acc, m0 + wave * PMF * 16, M, Cout, co0, y, add, stats, rg);
+  conv_epilogue<PMF, EPI>(acc, m0 + wave * PMF * 16, mlim, Cout, co0, y, add, stats, rg);
 }
 
 // 64 input channels (one halo block per tile: ResNet layer1-type layers). The one-shot kernel above
@@ -302,9 +303,9 @@ __global__ __launch_bounds__(256) void k_conv3x3_res(const uint16_t* __restrict_
 #pragma unroll
   for (int r = 0; r < PMF; ++r) {
     const int ml = (wave * PMF + r) * 16 + fr;
-    const int t = ml >> hp.lw, col = ml & (g.W - 1);
-    const int seg = t >> hp.lt;
-    sp0[r] = seg * hp.SEGP + (t & (hp.TRI - 1)) * hp.SW + col;
+    const int t = ml / g.W, col = ml - t * g.W;
+    const int seg = t / hp.TRI;
+    sp0[r] = ml < hp.TP ? seg * hp.SEGP + (t - seg * hp.TRI) * hp.SW + col : 0;
   }
 
   int tile = blockIdx.x;
@@ -354,12 +355,14 @@ __global__ __launch_bounds__(256) void k_conv3x3_res(const uint16_t* __restrict_
       if (st + 2 < 18) frags(st + 2, a0, b0);
       mma(a1, b1);
     }
-    conv_epilogue<PMF, EPI>(acc, tile * BM + wave * PMF * 16, M, Cout, co0, y, add, stats, rg);
+    const int mt = tile * hp.TP;
+    conv_epilogue<PMF, EPI>(acc, mt + wave * PMF * 16, mt + hp.TP < M ? mt + hp.TP : M, Cout, co0, y, add, stats,
+                            rg);
     // the next halo has landed and every wave is done with this one before it is refilled. The
     // epilogue's 16 output stores (PMF x 4 global_store_dwordx2, issued after the halo loads) may stay
-    // in flight: waiting for them too exposed the store latency once per tile. A ragged last tile
-    // may branch around stores, so it drains everything.
-    if (tile * BM + BM <= M) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+    // in flight: waiting for them too exposed the store latency once per tile. A ragged tile (the
+    // last one, or every tile of a TP < BM width) may branch around stores, so it drains everything.
+    if (hp.TP == BM && mt + BM <= M) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
@@ -371,19 +374,20 @@ bool plan(const Im2col& g, int pmf, int nu_max, Halo& hp) {
   // ((Wo - 1) * st + 3) input columns per image segment
   const int st = g.sh;
   const int BM = 64 * pmf;
-  if (g.Wo > BM || BM % g.Wo) return false;
-  hp.TR = BM / g.Wo;
+  if (g.Wo > BM) return false;
+  // the most whole output rows per tile that still tile the images evenly (TR | Ho, or Ho | TR for tiles
+  // of several small images): W = 32 -> 8 rows (256 px), 56 -> 4 (224), 28 -> 7 (196), 7 -> 35 (245)
+  hp.TR = 0;
+  for (int tr = BM / g.Wo; tr >= 1 && hp.TR == 0; --tr)
+    if ((tr <= g.Ho && g.Ho % tr == 0) || (tr > g.Ho && tr % g.Ho == 0)) hp.TR = tr;
+  if (hp.TR == 0) return false;
+  hp.TP = hp.TR * g.Wo;
+  if (4 * hp.TP < 3 * BM) return false;   // under 75 % of the tile's MFMA work would be used
   hp.TRI = hp.TR < g.Ho ? hp.TR : g.Ho;
-  if ((hp.TR <= g.Ho && g.Ho % hp.TR) || (hp.TR > g.Ho && hp.TR % g.Ho)) return false;
   hp.SW = (g.Wo - 1) * st + 3;
   hp.SEGP = ((hp.TRI - 1) * st + 3) * hp.SW;
   hp.NPIX = (hp.TR / hp.TRI) * hp.SEGP;
   hp.nu = (hp.NPIX + 31) / 32;
-  hp.lw = 0;
-  while ((1 << hp.lw) < g.Wo) ++hp.lw;
-  hp.lt = 0;
-  while ((1 << hp.lt) < hp.TRI) ++hp.lt;
-  if ((1 << hp.lw) != g.Wo || (1 << hp.lt) != hp.TRI) return false;
   return hp.nu <= nu_max;
 }
 
@@ -435,8 +439,8 @@ template <int NU, bool OUT_BF16>
 __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                   Im2col g, Halo hp, int Cout, int64_t rg, int tiles_per_split,
                                                   void* out, int64_t split_stride, int64_t group_stride) {
-  constexpr int TP = 128;               // output pixels per tile
-  constexpr int DB = TP * 128;          // dy tile bytes
+  constexpr int TPC = 128;              // output pixels per tile at most (hp.TP: whole rows)
+  constexpr int DB = TPC * 128;         // dy tile bytes
   __shared__ __attribute__((aligned(16))) char lds[DB + NU * 4096];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -448,7 +452,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
   const int rows = g.N * g.H;
   const int64_t pbeg = static_cast<int64_t>(gi) * rg;       // the worker's first pixel (an image start)
   const int64_t pend = pbeg + rg;
-  const int ntiles = static_cast<int>((rg + TP - 1) / TP);
+  const int ntiles = static_cast<int>((rg + hp.TP - 1) / hp.TP);
+  const FastDiv fW = make_fastdiv(g.W);
   const int t0 = sp * tiles_per_split;
   const int t1 = t0 + tiles_per_split < ntiles ? t0 + tiles_per_split : ntiles;
   const int lc = lane & 7;
@@ -482,16 +487,17 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
       for (int b = 0; b < 2; ++b) acc[t][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int tile = t0; tile < t1; ++tile) {
-    const int64_t P0 = pbeg + static_cast<int64_t>(tile) * TP;   // first pixel of the tile
+    const int64_t P0 = pbeg + static_cast<int64_t>(tile) * hp.TP;   // first pixel of the tile
+    const int64_t Pend = P0 + hp.TP < pend ? P0 + hp.TP : pend;
     const int R0 = static_cast<int>(P0 / g.W);
     const int h0 = R0 % g.H;
-    // dy tile: 128 pixels x 8 chunks, 4 glds per lane
+    // dy tile: 128 pixels x 8 chunks, 4 glds per lane (pixels past TP: zero rows)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int m = (u * 4 + wave) * 8 + (lane >> 3);
       const int64_t P = P0 + m;
       const uint64_t a = reinterpret_cast<uint64_t>(dy + P * Cout + co0 + ((lc ^ tr_swz(m)) * 8));
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(P < pend ? a : az),
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(P < Pend ? a : az),
                                        (lds_ptr)(lds + (u * 4 + wave) * 1024), 16, 0, 0);
     }
 #pragma unroll
@@ -515,9 +521,11 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int m = 32 * c + 8 * grp + 4 * h + q;
-        const int t = m >> hp.lw, col = m & (g.W - 1);
-        const int seg = t >> hp.lt;
-        hp0[h] = seg * hp.SEGP + (t & (hp.TRI - 1)) * hp.SW + col;
+        uint32_t t, col;
+        fdivmod(static_cast<uint32_t>(m), fW, t, col);
+        const int seg = static_cast<int>(t) / hp.TRI;
+        // a pixel past TP has a zero dy row; it reads halo pixel 0 (finite) so 0 x stale LDS cannot be NaN
+        hp0[h] = m < hp.TP ? seg * hp.SEGP + (static_cast<int>(t) - seg * hp.TRI) * hp.SW + static_cast<int>(col) : 0;
       }
       // A = dyᵀ fragments of co fragments cf0, cf0 + 1: dy rows 32c + 8grp + 4h + q
       s16x4 ra[4];
@@ -590,7 +598,7 @@ bool wgrad3x3_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int C
                    hipStream_t stream) {
   Halo hp;
   if (!wgrad3x3_fits(g, Cout, rg) || !plan(g, 2, kNuWgrad, hp)) return false;
-  const int ntiles = static_cast<int>((rg + 127) / 128);
+  const int ntiles = static_cast<int>((rg + hp.TP - 1) / hp.TP);
   if (splits < 1) splits = 1;
   const int per = (ntiles + splits - 1) / splits;
   const dim3 grid((g.C / 64) * (Cout / 64), groups, splits);
@@ -634,9 +642,11 @@ bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cou
   if (pmf <= 0) pmf = conv3x3_pick(g, Cout);
   if (stats && (add || rg < 16 * pmf)) return false;
   Halo hp;
+  // the statistics epilogue indexes its tiles by 16 * PMF-pixel wave ranges: whole tiles only
+  if (stats && !(plan(g, pmf, pmf == 4 ? kNuBig : kNuSmall, hp) && hp.TP == 64 * pmf)) return false;
   if (pmf == 4 && g.C == 64 && conv3x3_pick(g, Cout) == 4 && plan(g, 4, kNuRes, hp)) {
     const int tiles = (g.N * g.H + hp.TR - 1) / hp.TR;
-    int gx = cu_count() / (Cout / 64);
+    int gx = cu_count() / (Cout / 64);   // (the tile rows above are re-planned for the resident halo)
     gx = gx < 1 ? 1 : (gx > tiles ? tiles : gx);
     const dim3 grid(gx, Cout / 64);
     if (add)

@@ -625,7 +625,10 @@ __device__ __forceinline__ int tr_swz(int row) { return ((row >> 1) & 1) | (((ro
 constexpr int kTB2 = 2 * kTB;              // one operand piece: two [32][64] sub-tiles
 constexpr int kSB2 = 2 * kNP * kTB2;       // dy pieces 0..2 | x pieces 0..2
 
-__global__ __launch_bounds__(256) void k_cf32_wgrad2(const float* __restrict__ x, const float* __restrict__ dy,
+// NB = 2: double-buffered tiles (96 KB, one workgroup per CU, one barrier per step); NB = 1: one tile
+// (48 KB, two workgroups per CU hide each other's staging and barriers; two barriers per step)
+template <int NB>
+__global__ __launch_bounds__(256, NB == 1 ? 2 : 1) void k_cf32_wgrad2(const float* __restrict__ x, const float* __restrict__ dy,
                                                      ConvF32Geo g, int64_t rg, int64_t per_split,
                                                      float* __restrict__ out, int64_t split_stride,
                                                      int64_t group_stride) {
@@ -714,10 +717,11 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad2(const float* __restrict__ x
 
   if (steps > 0) load(0);
   for (int s = 0; s < steps; ++s) {
-    stage(s & 1);
+    if (NB == 1 && s > 0) __syncthreads();   // every wave has read step s - 1's tile
+    stage(NB == 1 ? 0 : (s & 1));
     if (s + 1 < steps) load(s + 1);
     __syncthreads();
-    const uint32_t sb = lds0 + (s & 1) * kSB2;
+    const uint32_t sb = lds0 + (NB == 1 ? 0 : (s & 1)) * kSB2;
     // fragments at a0, a1 (rows r and r + 4 each): the compiler builtin, so the 24 reads of a step are
     // in flight together (no LDS-DMA runs in this kernel: the waits it places cost nothing)
     auto tr_read = [&](uint32_t a0, uint32_t a1, bf16x8 (&f)[2]) {
@@ -997,18 +1001,27 @@ bool wgrad_f32_supported(const ConvF32Geo& g) { return g.Cs > 0 && g.Co % 64 == 
 bool wgrad_f32_wide(const ConvF32Geo& g) { return g.Cs % 128 == 0 && g.Co % 128 == 0; }
 
 void wgrad_f32(const float* x, const float* dy, const ConvF32Geo& g, int groups, int64_t rg, int splits, float* out,
-               int64_t split_stride, int64_t group_stride, hipStream_t stream) {
+               int64_t split_stride, int64_t group_stride, hipStream_t stream, int variant) {
   const int K = g.KH * g.KW * g.Cs;
   if (splits < 1) splits = 1;
   const int64_t per_split = (rg + splits - 1) / splits;
-  if (wgrad_f32_wide(g)) {
-    static bool once = (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cf32_wgrad2),
+  // automatic: the single-buffered 128 x 128 form (two workgroups per CU) wherever it applies -- 25-30 %
+  // under the double-buffered one on every ResNet-50 CIFAR shape (profiles/r4/bench_conv_f32.log)
+  if (variant == 0) variant = wgrad_f32_wide(g) ? 2 : 3;
+  if (variant == 1 || variant == 2) {
+    static bool once = (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cf32_wgrad2<2>),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kSB2),
+                        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_cf32_wgrad2<1>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, kSB2),
                         true);
     (void)once;
     const dim3 grid2((K / 128) * (g.Co / 128), groups, splits);
-    hipLaunchKernelGGL(k_cf32_wgrad2, grid2, dim3(256), 2 * kSB2, stream, x, dy, g, rg, per_split, out, split_stride,
-                       group_stride);
+    if (variant == 1)
+      hipLaunchKernelGGL(k_cf32_wgrad2<2>, grid2, dim3(256), 2 * kSB2, stream, x, dy, g, rg, per_split, out,
+                         split_stride, group_stride);
+    else
+      hipLaunchKernelGGL(k_cf32_wgrad2<1>, grid2, dim3(256), kSB2, stream, x, dy, g, rg, per_split, out,
+                         split_stride, group_stride);
     return;
   }
   const dim3 grid(((K + 63) / 64) * (g.Co / 64), groups, splits);

@@ -33,8 +33,10 @@ bool wgrad_f32_supported(const ConvF32Geo& g);
 bool wgrad_f32_wide(const ConvF32Geo& g);
 // out[s][grp][co][k] (fp32) = Σ over the s-th of `splits` ranges of worker grp's rg output pixels of
 // dy[m, co] · patch(x)[m, k]; element offset s * split_stride + grp * group_stride + co * K + k.
+// variant: 0 automatic, 1 / 2 the 128 x 128 form double- / single-buffered (wgrad_f32_wide shapes), 3 the
+// 64 x 64 form
 void wgrad_f32(const float* x, const float* dy, const ConvF32Geo& g, int groups, int64_t rg, int splits, float* out,
-               int64_t split_stride, int64_t group_stride, hipStream_t stream);
+               int64_t split_stride, int64_t group_stride, hipStream_t stream, int variant = 0);
 
 struct WSplitJob {
   const float* w;      // [R][T][C] fp32 (a channels_last weight: R = Cout, T = KH*KW, C = Cin)

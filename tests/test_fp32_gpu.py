@@ -95,12 +95,14 @@ def test_wgrad_f32_matches_per_worker_fp64(cuda, native, G, B, C, Co, H, k, s, p
     Ho = (H + 2 * p - k) // s + 1
     dy = cl(torch.randn(G * B, Co, Ho, Ho, device=cuda))
     K = k * k * C
-    part = torch.full((S, G, Co, K), float("nan"), device=cuda)
-    native.gpu_wgrad_f32(x, dy, k, k, s, s, p, p, 1, 1, G, part, S)
-    for g in range(G):
-        sl = slice(g * B, (g + 1) * B)
-        dw = torch.nn.grad.conv2d_weight(x[sl].double(), (Co, C, k, k), dy[sl].double(), s, p)
-        assert rel(part[:, g].sum(0), dw.permute(0, 2, 3, 1).reshape(Co, K)) < TOL
+    variants = (0, 1, 2, 3) if C % 128 == 0 and Co % 128 == 0 else (0, 3)
+    for var in variants:   # automatic, 128x128 double- / single-buffered, 64x64
+        part = torch.full((S, G, Co, K), float("nan"), device=cuda)
+        native.gpu_wgrad_f32(x, dy, k, k, s, s, p, p, 1, 1, G, part, S, var)
+        for g in range(G):
+            sl = slice(g * B, (g + 1) * B)
+            dw = torch.nn.grad.conv2d_weight(x[sl].double(), (Co, C, k, k), dy[sl].double(), s, p)
+            assert rel(part[:, g].sum(0), dw.permute(0, 2, 3, 1).reshape(Co, K)) < TOL, var
     if S == 1:   # straight into strided exchange rows
         rows = torch.zeros(G, Co * K + 100, device=cuda)
         view = rows.as_strided((G, Co, K), (Co * K + 100, K, 1), 0)

@@ -211,11 +211,15 @@ def test_stem_unsupported_sizes(native):
                                          (33, 512, 512, 4, 22), (6, 64, 64, 16, 0), (13, 192, 256, 8, 0),
                                          # 64 input channels: the weight-resident persistent kernel (more
                                          # tiles than workgroups: 280 / 272 tiles)
-                                         (70, 64, 64, 32, 24), (4, 64, 128, 32, 24), (17, 64, 64, 16, 0)])
+                                         (70, 64, 64, 32, 24), (4, 64, 128, 32, 24), (17, 64, 64, 16, 0),
+                                         # ImageNet widths (tiles of TR whole rows, TR * W < 256 pixels):
+                                         # 56 (4 rows, resident 64-channel kernel), 28 (7), 14 (14), 7 (5 images)
+                                         (2, 64, 64, 56, 0), (3, 64, 128, 56, 24), (2, 128, 128, 28, 0),
+                                         (3, 256, 256, 14, 24), (6, 512, 512, 7, 0), (5, 256, 128, 7, 22)])
 def test_conv3x3_halo_matches_conv2d(cuda, native, N, C, Co, H, pm):
     """Halo-staged 3x3 kernel (conv3x3_nhwc.hip) vs an fp32 conv2d of the same bf16 operands: tiles
     inside one image (32x32, 16x16), tiles of several padded images (8x8, 4x4), a ragged last tile,
-    several 64-channel halo refills, and the fused add."""
+    several 64-channel halo refills, the fused add, and the non-power-of-two ImageNet widths."""
     assert native.conv3x3_pick(N, H, H, C, Co) in (2, 4)
     x = torch.randn(N, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(Co, C, 3, 3, device=cuda) / (C * 9) ** 0.5).to(torch.bfloat16)
@@ -233,7 +237,10 @@ def test_conv3x3_halo_matches_conv2d(cuda, native, N, C, Co, H, pm):
 
 @pytest.mark.parametrize("G,B,C,Co,H,S", [(8, 8, 512, 512, 4, 1), (8, 8, 256, 256, 8, 1), (8, 8, 128, 128, 16, 4),
                                           (8, 8, 64, 64, 32, 16), (3, 5, 64, 128, 8, 2), (2, 7, 128, 64, 4, 3),
-                                          (4, 3, 192, 64, 16, 64)])
+                                          (4, 3, 192, 64, 16, 64),
+                                          # ImageNet widths: 112- / 112- / 98- / 126-pixel tiles of whole rows
+                                          (2, 2, 64, 64, 56, 2), (2, 3, 128, 128, 28, 1), (3, 2, 256, 64, 14, 4),
+                                          (2, 5, 512, 512, 7, 1)])
 def test_wgrad3x3_halo_matches_conv_weight_grad(cuda, native, G, B, C, Co, H, S):
     """Halo-staged per-worker 3x3 weight gradient (conv3x3_nhwc.hip) vs fp32 conv2d_weight of each
     worker's images: ragged last tiles, empty splits (zero slabs), NaN-prefilled outputs, both the
@@ -276,7 +283,8 @@ def test_iconv_stride2_matches_conv2d(cuda, native, N, C, Co, H):
 
 def test_conv3x3_halo_refuses_unfit_shapes(native):
     assert native.conv3x3_pick(4, 2, 2, 256, 256) == 0      # 2x2 images: the halo exceeds the LDS budget
-    assert native.conv3x3_pick(4, 7, 7, 64, 64) == 0        # 7 does not divide a pixel tile
+    assert native.conv3x3_pick(4, 150, 150, 64, 64) == 0    # one 150-pixel row uses < 75 % of a tile
+    assert native.conv3x3_pick(4, 7, 7, 64, 64) == 4        # 5 images of 7 rows: 245 of 256 pixels
     assert native.conv3x3_pick(4, 32, 32, 32, 64) == 0      # C % 64
 
 
