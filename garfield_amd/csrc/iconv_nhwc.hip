@@ -155,6 +155,12 @@ __device__ __attribute__((aligned(16))) uint4 g_iconv_zero[8];  // 128 zero byte
 using lds_ptr = __attribute__((address_space(3))) void*;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
+// Bank swizzle of the transposed-read tiles of the weight gradients: a half-wave's ds_read_b64_tr_b16
+// touches pixel rows {0..3, 8..11} (+ 16) at one chunk pair; with plain 128-byte rows rows 0, 2, 8, 10
+// share banks (4-way conflicts). Row r's 16-byte chunks are stored XOR 2 tr_g(r) (the global side of
+// the LDS-DMA picks the chunk), which spreads those rows over distinct banks.
+__device__ __forceinline__ int tr_g(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 1); }
+
 // TW: w is the FORWARD weight of a stride-1 convolution and this launch computes its data
 // gradient (x = dy, C = the forward's output channels, Cout = its input channels, padding
 // KH-1-ph): A[o][(i', j', c)] = Wf[c][KH-1-i'][KW-1-j'][o]. The W tile is staged as plain
@@ -391,6 +397,7 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
   const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
 
   const int lrow = wave * 8 + (lane >> 3), lchunk = lane & 7;   // this lane's glds row / 16-byte chunk
+  const int lsw = lchunk ^ (2 * tr_g(lrow));                      // the global chunk it stages (swizzle)
   const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
   const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
 
@@ -399,7 +406,7 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
     const bool mv = m < static_cast<int>(mend);
     const int mm = mv ? m : 0;
     char* base = lds + slot * SB;
-    const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lchunk * 8);
+    const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lsw * 8);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? ady : az), (lds_ptr)(base + wave * 1024), 16,
                                      0, 0);
     const int wo = mm % g.Wo;
@@ -409,7 +416,7 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
     const int hi = ho * g.sh - g.ph + ti * g.dh, wi = wo * g.sw - g.pw + tj * g.dw;
     const bool ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
     const uint64_t ax = reinterpret_cast<uint64_t>(
-        x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 + lchunk * 8);
+        x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 + lsw * 8);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? ax : az),
                                      (lds_ptr)(base + TB + wave * 1024), 16, 0, 0);
   };
@@ -429,8 +436,12 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
   // puts a vmcnt(0) in front of them (it cannot tell them from the in-flight LDS-DMA ring
   // stages), which serialises the ring.
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)lds));
-  const uint32_t offA = (8 * grp + q) * 128 + (16 * cf0 + 4 * p) * 2;
-  const uint32_t offB = TB + (8 * grp + q) * 128 + (16 * kf0 + 4 * p) * 2;
+  // staged rows carry their 16-byte chunks XOR-swizzled by 2 tr_g(row) (see the staging): fragment f of
+  // row r sits at chunk pair f ^ tr_g(r); the second fragment of a pair is dtr = +-32 bytes away
+  const int tg = tr_g(8 * grp + q);
+  const uint32_t offA = (8 * grp + q) * 128 + 32 * (cf0 ^ tg) + 8 * p;
+  const uint32_t offB = TB + (8 * grp + q) * 128 + 32 * (kf0 ^ tg) + 8 * p;
+  const uint32_t dtr = (tg & 1) ? static_cast<uint32_t>(-32) : 32u;
 
 #pragma unroll
   for (int s0 = 0; s0 < NS - 1; ++s0)
@@ -446,15 +457,15 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
     asm volatile(
         "ds_read_b64_tr_b16 %0, %8\n\t"
         "ds_read_b64_tr_b16 %1, %8 offset:512\n\t"
-        "ds_read_b64_tr_b16 %2, %8 offset:32\n\t"
-        "ds_read_b64_tr_b16 %3, %8 offset:544\n\t"
+        "ds_read_b64_tr_b16 %2, %10\n\t"
+        "ds_read_b64_tr_b16 %3, %10 offset:512\n\t"
         "ds_read_b64_tr_b16 %4, %9\n\t"
         "ds_read_b64_tr_b16 %5, %9 offset:512\n\t"
-        "ds_read_b64_tr_b16 %6, %9 offset:32\n\t"
-        "ds_read_b64_tr_b16 %7, %9 offset:544\n\t"
+        "ds_read_b64_tr_b16 %6, %11\n\t"
+        "ds_read_b64_tr_b16 %7, %11 offset:512\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
-        : "v"(sb + offA), "v"(sb + offB)
+        : "v"(sb + offA), "v"(sb + offB), "v"(sb + offA + dtr), "v"(sb + offB + dtr)
         : "memory");
     // every wave's reads of this slot are done (waited above) before the next barrier lets it be refilled
     if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
@@ -519,6 +530,7 @@ __global__ __launch_bounds__(256) void k_iwgrad_rows(const uint16_t* __restrict_
   const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
 
   const int lrow = wave * 8 + (lane >> 3), lchunk = lane & 7;
+  const int lsw = lchunk ^ (2 * tr_g(lrow));   // the global chunk this lane stages (bank swizzle)
   const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
   const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
 
@@ -527,7 +539,7 @@ __global__ __launch_bounds__(256) void k_iwgrad_rows(const uint16_t* __restrict_
     const bool mv = m < static_cast<int>(mend);
     const int mm = mv ? m : 0;
     char* base = lds + slot * SB;
-    const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lchunk * 8);
+    const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lsw * 8);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? ady : az), (lds_ptr)(base + wave * 1024), 16,
                                      0, 0);
     const int wo = mm % g.Wo;
@@ -543,7 +555,7 @@ __global__ __launch_bounds__(256) void k_iwgrad_rows(const uint16_t* __restrict_
         const int wi = wo * g.sw - g.pw + j * g.dw;
         const bool ok = rok && wi >= 0 && wi < g.W;
         const uint64_t ax = reinterpret_cast<uint64_t>(
-            x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 + lchunk * 8);
+            x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 + lsw * 8);
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? ax : az),
                                          (lds_ptr)(base + TB * (1 + r * NT + j) + wave * 1024), 16, 0, 0);
       }
@@ -561,8 +573,12 @@ __global__ __launch_bounds__(256) void k_iwgrad_rows(const uint16_t* __restrict_
       for (int b = 0; b < 2; ++b) acc[j][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)lds));
-  const uint32_t offA = (8 * grp + q) * 128 + (16 * cf0 + 4 * p) * 2;
-  const uint32_t offB = TB + (8 * grp + q) * 128 + (16 * kf0 + 4 * p) * 2;
+  // staged rows carry their 16-byte chunks XOR-swizzled by 2 tr_g(row) (see the staging): fragment f of
+  // row r sits at chunk pair f ^ tr_g(r); the second fragment of a pair is dtr = +-32 bytes away
+  const int tg = tr_g(8 * grp + q);
+  const uint32_t offA = (8 * grp + q) * 128 + 32 * (cf0 ^ tg) + 8 * p;
+  const uint32_t offB = TB + (8 * grp + q) * 128 + 32 * (kf0 ^ tg) + 8 * p;
+  const uint32_t dtr = (tg & 1) ? static_cast<uint32_t>(-32) : 32u;
 
 #pragma unroll
   for (int s0 = 0; s0 < NS - 1; ++s0)
@@ -579,25 +595,25 @@ __global__ __launch_bounds__(256) void k_iwgrad_rows(const uint16_t* __restrict_
     asm volatile(
         "ds_read_b64_tr_b16 %0, %16\n\t"
         "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
-        "ds_read_b64_tr_b16 %2, %16 offset:32\n\t"
-        "ds_read_b64_tr_b16 %3, %16 offset:544\n\t"
+        "ds_read_b64_tr_b16 %2, %20\n\t"
+        "ds_read_b64_tr_b16 %3, %20 offset:512\n\t"
         "ds_read_b64_tr_b16 %4, %17\n\t"
         "ds_read_b64_tr_b16 %5, %17 offset:512\n\t"
-        "ds_read_b64_tr_b16 %6, %17 offset:32\n\t"
-        "ds_read_b64_tr_b16 %7, %17 offset:544\n\t"
+        "ds_read_b64_tr_b16 %6, %21\n\t"
+        "ds_read_b64_tr_b16 %7, %21 offset:512\n\t"
         "ds_read_b64_tr_b16 %8, %18\n\t"
         "ds_read_b64_tr_b16 %9, %18 offset:512\n\t"
-        "ds_read_b64_tr_b16 %10, %18 offset:32\n\t"
-        "ds_read_b64_tr_b16 %11, %18 offset:544\n\t"
+        "ds_read_b64_tr_b16 %10, %22\n\t"
+        "ds_read_b64_tr_b16 %11, %22 offset:512\n\t"
         "ds_read_b64_tr_b16 %12, %19\n\t"
         "ds_read_b64_tr_b16 %13, %19 offset:512\n\t"
-        "ds_read_b64_tr_b16 %14, %19 offset:32\n\t"
-        "ds_read_b64_tr_b16 %15, %19 offset:544\n\t"
+        "ds_read_b64_tr_b16 %14, %23\n\t"
+        "ds_read_b64_tr_b16 %15, %23 offset:512\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(ra[0]), "=&v"(ra[1]), "=&v"(ra[2]), "=&v"(ra[3]), "=&v"(rb[0][0]), "=&v"(rb[0][1]), "=&v"(rb[0][2]),
           "=&v"(rb[0][3]), "=&v"(rb[0][4]), "=&v"(rb[0][5]), "=&v"(rb[0][6]), "=&v"(rb[0][7]), "=&v"(rb[0][8]),
           "=&v"(rb[0][9]), "=&v"(rb[0][10]), "=&v"(rb[0][11])
-        : "v"(sb + offA), "v"(sb + offB), "v"(sb + offB + TB), "v"(sb + offB + 2 * TB)
+        : "v"(sb + offA), "v"(sb + offB), "v"(sb + offB + TB), "v"(sb + offB + 2 * TB), "v"(sb + offA + dtr), "v"(sb + offB + dtr), "v"(sb + offB + TB + dtr), "v"(sb + offB + 2 * TB + dtr)
         : "memory");
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
@@ -605,21 +621,21 @@ __global__ __launch_bounds__(256) void k_iwgrad_rows(const uint16_t* __restrict_
       asm volatile(
           "ds_read_b64_tr_b16 %0, %12\n\t"
           "ds_read_b64_tr_b16 %1, %12 offset:512\n\t"
-          "ds_read_b64_tr_b16 %2, %12 offset:32\n\t"
-          "ds_read_b64_tr_b16 %3, %12 offset:544\n\t"
+          "ds_read_b64_tr_b16 %2, %15\n\t"
+          "ds_read_b64_tr_b16 %3, %15 offset:512\n\t"
           "ds_read_b64_tr_b16 %4, %13\n\t"
           "ds_read_b64_tr_b16 %5, %13 offset:512\n\t"
-          "ds_read_b64_tr_b16 %6, %13 offset:32\n\t"
-          "ds_read_b64_tr_b16 %7, %13 offset:544\n\t"
+          "ds_read_b64_tr_b16 %6, %16\n\t"
+          "ds_read_b64_tr_b16 %7, %16 offset:512\n\t"
           "ds_read_b64_tr_b16 %8, %14\n\t"
           "ds_read_b64_tr_b16 %9, %14 offset:512\n\t"
-          "ds_read_b64_tr_b16 %10, %14 offset:32\n\t"
-          "ds_read_b64_tr_b16 %11, %14 offset:544\n\t"
+          "ds_read_b64_tr_b16 %10, %17\n\t"
+          "ds_read_b64_tr_b16 %11, %17 offset:512\n\t"
           "s_waitcnt lgkmcnt(0)"
           : "=&v"(rb[r][0]), "=&v"(rb[r][1]), "=&v"(rb[r][2]), "=&v"(rb[r][3]), "=&v"(rb[r][4]), "=&v"(rb[r][5]),
             "=&v"(rb[r][6]), "=&v"(rb[r][7]), "=&v"(rb[r][8]), "=&v"(rb[r][9]), "=&v"(rb[r][10]), "=&v"(rb[r][11])
-          : "v"(ob), "v"(ob + TB), "v"(ob + 2 * TB)
-          : "memory");
+          : "v"(ob), "v"(ob + TB), "v"(ob + 2 * TB), "v"(ob + dtr), "v"(ob + TB + dtr), "v"(ob + 2 * TB + dtr)
+        : "memory");
     }
     if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
     bf16x8 a[2];
@@ -729,6 +745,7 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
   const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 31) / 32) : 0;
 
   const int lrow = wave * 8 + (lane >> 3), lchunk = lane & 7;
+  const int lsw = lchunk ^ (2 * tr_g(lrow));   // the global chunk this lane stages (bank swizzle)
   const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
   const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
 
@@ -737,7 +754,7 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
     const bool mv = m < static_cast<int>(mend);
     const int mm = mv ? m : 0;
     char* base = lds + slot * SB;
-    const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lchunk * 8);
+    const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lsw * 8);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? ady : az), (lds_ptr)(base + wave * 1024), 16,
                                      0, 0);
     const int wo = mm % g.Wo;
@@ -747,7 +764,7 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
     const int hi = ho * g.sh - g.ph, wi = wo * g.sw - g.pw;
     const bool ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
     const uint16_t* xr = x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 +
-                         lchunk * 8;
+                         lsw * 8;
 #pragma unroll
     for (int j = 0; j < NT; ++j)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? reinterpret_cast<uint64_t>(xr + j * 64) : az),
@@ -765,8 +782,12 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
       for (int b = 0; b < 2; ++b) acc[j][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)lds));
-  const uint32_t offA = (8 * grp + q) * 128 + (16 * cf0 + 4 * p) * 2;
-  const uint32_t offB = TB + (8 * grp + q) * 128 + (16 * kf0 + 4 * p) * 2;
+  // staged rows carry their 16-byte chunks XOR-swizzled by 2 tr_g(row) (see the staging): fragment f of
+  // row r sits at chunk pair f ^ tr_g(r); the second fragment of a pair is dtr = +-32 bytes away
+  const int tg = tr_g(8 * grp + q);
+  const uint32_t offA = (8 * grp + q) * 128 + 32 * (cf0 ^ tg) + 8 * p;
+  const uint32_t offB = TB + (8 * grp + q) * 128 + 32 * (kf0 ^ tg) + 8 * p;
+  const uint32_t dtr = (tg & 1) ? static_cast<uint32_t>(-32) : 32u;
 
 #pragma unroll
   for (int s0 = 0; s0 < NS - 1; ++s0)
@@ -784,36 +805,36 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
     asm volatile(
         "ds_read_b64_tr_b16 %0, %12\n\t"
         "ds_read_b64_tr_b16 %1, %12 offset:512\n\t"
-        "ds_read_b64_tr_b16 %2, %12 offset:32\n\t"
-        "ds_read_b64_tr_b16 %3, %12 offset:544\n\t"
+        "ds_read_b64_tr_b16 %2, %15\n\t"
+        "ds_read_b64_tr_b16 %3, %15 offset:512\n\t"
         "ds_read_b64_tr_b16 %4, %13\n\t"
         "ds_read_b64_tr_b16 %5, %13 offset:512\n\t"
-        "ds_read_b64_tr_b16 %6, %13 offset:32\n\t"
-        "ds_read_b64_tr_b16 %7, %13 offset:544\n\t"
+        "ds_read_b64_tr_b16 %6, %16\n\t"
+        "ds_read_b64_tr_b16 %7, %16 offset:512\n\t"
         "ds_read_b64_tr_b16 %8, %14\n\t"
         "ds_read_b64_tr_b16 %9, %14 offset:512\n\t"
-        "ds_read_b64_tr_b16 %10, %14 offset:32\n\t"
-        "ds_read_b64_tr_b16 %11, %14 offset:544\n\t"
+        "ds_read_b64_tr_b16 %10, %17\n\t"
+        "ds_read_b64_tr_b16 %11, %17 offset:512\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(ra[0]), "=&v"(ra[1]), "=&v"(ra[2]), "=&v"(ra[3]), "=&v"(rb[0][0]), "=&v"(rb[0][1]), "=&v"(rb[0][2]),
           "=&v"(rb[0][3]), "=&v"(rb[1][0]), "=&v"(rb[1][1]), "=&v"(rb[1][2]), "=&v"(rb[1][3])
-        : "v"(sb + offA), "v"(sb + offB), "v"(sb + offB + TB)
+        : "v"(sb + offA), "v"(sb + offB), "v"(sb + offB + TB), "v"(sb + offA + dtr), "v"(sb + offB + dtr), "v"(sb + offB + TB + dtr)
         : "memory");
     if constexpr (NT == 4) {
       asm volatile(
           "ds_read_b64_tr_b16 %0, %8\n\t"
           "ds_read_b64_tr_b16 %1, %8 offset:512\n\t"
-          "ds_read_b64_tr_b16 %2, %8 offset:32\n\t"
-          "ds_read_b64_tr_b16 %3, %8 offset:544\n\t"
+          "ds_read_b64_tr_b16 %2, %10\n\t"
+          "ds_read_b64_tr_b16 %3, %10 offset:512\n\t"
           "ds_read_b64_tr_b16 %4, %9\n\t"
           "ds_read_b64_tr_b16 %5, %9 offset:512\n\t"
-          "ds_read_b64_tr_b16 %6, %9 offset:32\n\t"
-          "ds_read_b64_tr_b16 %7, %9 offset:544\n\t"
+          "ds_read_b64_tr_b16 %6, %11\n\t"
+          "ds_read_b64_tr_b16 %7, %11 offset:512\n\t"
           "s_waitcnt lgkmcnt(0)"
           : "=&v"(rb[2][0]), "=&v"(rb[2][1]), "=&v"(rb[2][2]), "=&v"(rb[2][3]), "=&v"(rb[3][0]), "=&v"(rb[3][1]),
             "=&v"(rb[3][2]), "=&v"(rb[3][3])
-          : "v"(sb + offB + 2 * TB), "v"(sb + offB + 3 * TB)
-          : "memory");
+          : "v"(sb + offB + 2 * TB), "v"(sb + offB + 3 * TB), "v"(sb + offB + 2 * TB + dtr), "v"(sb + offB + 3 * TB + dtr)
+        : "memory");
     }
     // the refilled slot was read in the previous k-step, before every wave passed this barrier
     if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
