@@ -115,6 +115,9 @@ def parse():
                         "crop + flip + normalise (data_aug.hip, one launch); static: the same batches every step")
     p.add_argument("--dataset-size", type=int, default=0,
                    help="images in the synthetic dataset (default 50000 CIFAR-shape, 2000 ImageNet-shape)")
+    p.add_argument("--attack", default="",
+                   help="comma-separated attacks of the Byzantine logical workers (e.g. reverse,lie): worker slot i "
+                        "(global slot order) runs attack i; the JSON reports the GAR weight they received")
     p.add_argument("--no-fp32", action="store_true",
                    help="skip the companion run at the reference's precision (fp32_ms_per_step / fp32_img_per_s: "
                         "the same job with fp32 activations, weights and exchange rows on the fp32 kernels)")
@@ -163,7 +166,8 @@ def build_job(a, ctx, model, shape, num_classes, fp32: bool):
                        weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
                        cuda_graph=not a.no_graph, profile_phases=a.phases, lp_weights=lp,
                        worker_batching=False if a.no_worker_batching else None,
-                       shard_gar=True if a.shard_gar else None, layerwise=a.layerwise, **amp)
+                       shard_gar=True if a.shard_gar else None, layerwise=a.layerwise,
+                       byzantine={i: name for i, name in enumerate(x for x in a.attack.split(",") if x)}, **amp)
     if a.num_ps:
         from dataclasses import asdict
 
@@ -263,6 +267,14 @@ def main():
         extra["ref_impl_ms_per_step"] = round(ms_ref, 3)
         extra["ref_impl_img_per_s"] = round(n * a.batch / (ms_ref / 1000.0), 2)
         extra["speedup_vs_ref_impl"] = round(ms_ref / ms, 3)
+    if a.attack:
+        byz = dict(eng.cfg.byzantine)
+        w = getattr(eng, "last_weights", None)
+        extra["byzantine_workers"] = {str(k): v for k, v in byz.items()}
+        if w is not None and w.dim() == 1:   # the last step's selection weights, global slot order
+            wc = w.float().cpu()
+            extra["byzantine_weight_max"] = float(wc[list(byz)].abs().max())
+            extra["honest_weight_sum"] = round(float(wc.sum() - wc[list(byz)].sum()), 6)
     if not fp32 and not a.no_fp32 and not a.num_ps:
         # the reference's precision, same job, same invocation: fp32 activations / weights / exchange rows
         # on the fp32 kernels (conv_f32.hip: split-bf16 MFMA; bn_nhwc.hip and the rest in fp32)

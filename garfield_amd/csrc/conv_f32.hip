@@ -936,18 +936,17 @@ bool conv_f32_lds_ok(const ConvF32Geo& g, bool dgrad) {
 }
 
 int conv_f32_ksplit(const ConvF32Geo& g, bool dgrad) {
-  // PM = 4 tiles (the best LDS-read / MFMA ratio) and, below 200 of them, split-K up to 200+
-  // workgroups, each split at least 8 k-steps; the slabs cost 2 x S x M x Co x 4 bytes of traffic.
-  // Measured on the ResNet-50 CIFAR shapes (scripts/bench_conv_f32.py, profiles/r4): e.g. 256 ch 3x3
-  // at 2x2 px (128 tiles) 0.158 -> 0.095 ms with S = 2; 512 ch at 1x1 px (64 tiles) 0.32 -> 0.094 ms
+  // below 400 PM = 2 tiles (two workgroups per CU: ~512 slots), split-K up to 400+ workgroups, each split
+  // at least 8 k-steps; the slabs cost 2 x S x M x Co x 4 bytes of traffic. Measured on the ResNet-50
+  // CIFAR shapes (scripts/bench_conv_f32.py, profiles/r4): e.g. 512 ch 3x3 at 1x1 px 0.32 -> 0.08 ms
   // with S = 4; 500 tiles and more run best unsplit.
   const int csh = dgrad ? g.sh : 1, csw = dgrad ? g.sw : 1;
   const int64_t Mc = static_cast<int64_t>(g.N) * ((g.Ho + csh - 1) / csh) * ((g.Wo + csw - 1) / csw);
-  const int64_t tiles = ((Mc + 255) / 256) * (g.Co / 64) * csh * csw;
+  const int64_t tiles = ((Mc + 127) / 128) * (g.Co / 64) * csh * csw;   // PM = 2 tiles
   const int taps = dgrad ? ((g.KH + csh - 1) / csh) * ((g.KW + csw - 1) / csw) : g.KH * g.KW;
   const int steps = taps * (g.Cs / 32);
   int S = 1;
-  while (S < 8 && tiles * S < 200 && steps / (2 * S) >= 8) S *= 2;
+  while (S < 8 && tiles * S < 400 && steps / (2 * S) >= 8) S *= 2;
   return S;
 }
 
@@ -956,7 +955,10 @@ void conv_f32(const float* src, const uint16_t* w3, const ConvF32Geo& g, bool dg
   if (static_cast<int64_t>(g.N) * g.Ho * g.Wo <= 0) return;
   if (ksplit > 1 && part != nullptr && conv_f32_lds_ok(g, dgrad)) {
     // PM = 4 tiles, split-K into the slabs of `part`, then one summing pass (+ add)
-    if (pm <= 0 || pm == 15) {
+    if (pm <= 0 || pm == 13) {
+      if (dgrad) launch_conv_lds<2, 2, true>(src, w3, g, part, nullptr, ksplit, stream);
+      else launch_conv_lds<2, 2, false>(src, w3, g, part, nullptr, ksplit, stream);
+    } else if (pm == 15) {
       if (dgrad) launch_conv_lds<4, 3, true>(src, w3, g, part, nullptr, ksplit, stream);
       else launch_conv_lds<4, 3, false>(src, w3, g, part, nullptr, ksplit, stream);
     } else {
@@ -970,17 +972,22 @@ void conv_f32(const float* src, const uint16_t* w3, const ConvF32Geo& g, bool dg
                        add);
     return;
   }
-  if (pm <= 0) pm = 15;   // PM = 4, a 3-deep ring: the fastest or within 5 % on every measured shape
+  // automatic: PM = 2 with a 2-deep ring (57 KB of LDS: two workgroups per CU hide each other's barriers
+  // and load waits) -- 10-25 % under PM = 4 / one workgroup per CU on the larger ResNet-50 layers
+  // (profiles/r4/bench_conv_f32.log); the few-tile layers take it with split-K (conv_f32_ksplit)
+  if (pm <= 0) pm = 13;
   if (pm > 10 && conv_f32_lds_ok(g, dgrad)) {   // the LDS-staged kernel
     if (dgrad) {
       if (pm == 15) launch_conv_lds<4, 3, true>(src, w3, g, out, add, 1, stream);
       else if (pm >= 14) launch_conv_lds<4, 2, true>(src, w3, g, out, add, 1, stream);
       else if (pm == 12) launch_conv_lds<2, 3, true>(src, w3, g, out, add, 1, stream);
+      else if (pm == 13) launch_conv_lds<2, 2, true>(src, w3, g, out, add, 1, stream);
       else launch_conv_lds<1, 3, true>(src, w3, g, out, add, 1, stream);
     } else {
       if (pm == 15) launch_conv_lds<4, 3, false>(src, w3, g, out, add, 1, stream);
       else if (pm >= 14) launch_conv_lds<4, 2, false>(src, w3, g, out, add, 1, stream);
       else if (pm == 12) launch_conv_lds<2, 3, false>(src, w3, g, out, add, 1, stream);
+      else if (pm == 13) launch_conv_lds<2, 2, false>(src, w3, g, out, add, 1, stream);
       else launch_conv_lds<1, 3, false>(src, w3, g, out, add, 1, stream);
     }
     return;

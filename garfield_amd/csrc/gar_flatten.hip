@@ -171,6 +171,7 @@ namespace {
 struct SplitTable {
   SplitJob job[kMaxSplitJobs];
   int32_t blk0[kMaxSplitJobs + 1];
+  dev::FastDiv fper[kMaxSplitJobs], fcv[kMaxSplitJobs];   // the element decomposition without divisions
   int count;
 };
 
@@ -179,14 +180,13 @@ __global__ __launch_bounds__(256) void k_split_reduce_multi(SplitTable t) {
   while (j + 1 < t.count && static_cast<int>(blockIdx.x) >= t.blk0[j + 1]) ++j;
   const SplitJob& J = t.job[j];
   const int V = J.vec ? 4 : 1;
-  const int64_t cv = (J.Cc + V - 1) / V;
-  const int64_t per = J.R * cv;
-  const int64_t tid = static_cast<int64_t>(blockIdx.x - t.blk0[j]) * blockDim.x + threadIdx.x;
-  if (tid >= per * J.G) return;
-  const int g = static_cast<int>(tid / per);
-  const int64_t rem = tid - static_cast<int64_t>(g) * per;
-  const int64_t r = rem / cv;
-  const int64_t c = (rem - r * cv) * V;
+  const uint32_t cv = t.fcv[j].d, per = t.fper[j].d;   // (Cc / V) per row, R rows per group: < 2^31 (host)
+  const uint32_t tid = (blockIdx.x - t.blk0[j]) * blockDim.x + threadIdx.x;
+  if (tid >= per * static_cast<uint32_t>(J.G)) return;
+  const uint32_t g = dev::fdiv(tid, t.fper[j]);
+  const uint32_t rem = tid - g * per;
+  const uint32_t r = dev::fdiv(rem, t.fcv[j]);
+  const int64_t c = static_cast<int64_t>(rem - r * cv) * V;
   const float* p = J.part + static_cast<int64_t>(g) * J.gs + r * J.ipitch + c;
   const int64_t o = static_cast<int64_t>(g) * J.ostride + r * J.opitch + c;
   if (J.vec) {
@@ -223,6 +223,9 @@ void split_reduce_multi(const SplitJob* jobs, int count, hipStream_t stream) {
                reinterpret_cast<uintptr_t>(J.part) % 16 == 0) ? 1 : 0;
       t.job[i] = J;
       t.blk0[i] = blocks;
+      const int64_t cvh = J.vec ? J.Cc / 4 : J.Cc;
+      t.fcv[i] = dev::make_fastdiv(static_cast<uint32_t>(cvh));
+      t.fper[i] = dev::make_fastdiv(static_cast<uint32_t>(cvh * J.R));
       const int64_t work = (J.vec ? J.Cc / 4 : J.Cc) * J.R * J.G;
       blocks += static_cast<int32_t>((work + 255) / 256);
     }

@@ -1,6 +1,7 @@
 """Micro-benchmark: the fp32 (split-bf16) convolution kernels of conv_f32.hip on the grouped
 ResNet-50 CIFAR step's shapes (8 workers x 250 images): forward / data gradient per kernel variant
-(pm 11 / 12 / 14 / 15 = LDS-staged PM 1 / 2 / 4 / 4 with a 3-deep ring; ks = split-K) and the
+(pm 11 / 12 / 13 / 14 / 15 = LDS-staged PM 1 / 2 (3-deep ring) / 2 (2-deep: two workgroups per CU) / 4 /
+4 with a 3-deep ring; ks = split-K) and the
 per-worker weight gradient, in ms and TFLOP/s of fp32 work."""
 import sys
 
@@ -28,7 +29,7 @@ def timeit(fn, reps=10):
     return a.elapsed_time(b) / reps
 
 
-variants = [(0, 0), (11, 1), (15, 1), (15, 2), (15, 4)]
+variants = [(0, 0), (13, 1), (13, 2), (13, 4), (15, 2), (15, 4)]
 for cin, cout, H, k, s in SHAPES:
     p = k // 2
     Ho = (H + 2 * p - k) // s + 1
@@ -47,8 +48,8 @@ for cin, cout, H, k, s in SHAPES:
         td = timeit(lambda: C.gpu_conv_f32(y, wt3, k, k, s, s, p, p, 1, 1, True, dx, None, pm, ks))
         line += f" | pm{pm}/ks{ks} f {tf:.3f} d {td:.3f}"
     rows = N * Ho * Ho // G
-    for var in ((1, 2, 3) if cin % 128 == 0 and cout % 128 == 0 else (3,)):
-        for S in (1, 2, 4, 8):
+    for var in ((2,) if cin % 128 == 0 and cout % 128 == 0 else (3,)):
+        for S in (1, 2, 4, 8, 16):
             part = torch.empty((S, G, cout, K), device=dev)
             tw = timeit(lambda: C.gpu_wgrad_f32(x, y, k, k, s, s, p, p, 1, 1, G, part, S, var))
             line += f" | wg v{var} S{S} {tw:.3f} ({fl / tw * 1e3:.0f})"
