@@ -830,21 +830,37 @@ __global__ __launch_bounds__(256) void k_wsplit(WTable t) {
 
 // logits[r][o] = Σ_f x[r][f] w[o][f] + b[o]: one wave per row, O <= 64 outputs kept in registers
 constexpr int kLinMaxO = 16;
+// y[row][o]: one wave per row, the lanes over f, 8 f-columns per lane in flight (x and w loads issue
+// back to back instead of one dependent round trip per column)
 __global__ __launch_bounds__(256) void k_f32_linear_fwd(const float* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ b, int R, int F, int O,
                                                         float* __restrict__ y) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
+  const float* xr = x + static_cast<int64_t>(row) * F;
   for (int o0 = 0; o0 < O; o0 += kLinMaxO) {
     float acc[kLinMaxO];
 #pragma unroll
     for (int o = 0; o < kLinMaxO; ++o) acc[o] = 0.f;
-    for (int f = lane; f < F; f += 64) {
-      const float xv = x[static_cast<int64_t>(row) * F + f];
+    for (int f0 = 0; f0 < F; f0 += 512) {
+      float xv[8];
 #pragma unroll
-      for (int o = 0; o < kLinMaxO; ++o)
-        if (o0 + o < O) acc[o] = fmaf(xv, w[static_cast<int64_t>(o0 + o) * F + f], acc[o]);
+      for (int u = 0; u < 8; ++u) {
+        const int f = f0 + u * 64 + lane;
+        xv[u] = f < F ? xr[f] : 0.f;
+      }
+#pragma unroll
+      for (int o = 0; o < kLinMaxO; ++o) {
+        if (o0 + o < O) {
+          const float* wr = w + static_cast<int64_t>(o0 + o) * F;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int f = f0 + u * 64 + lane;
+            acc[o] = fmaf(xv[u], f < F ? wr[f] : 0.f, acc[o]);
+          }
+        }
+      }
     }
 #pragma unroll
     for (int o = 0; o < kLinMaxO; ++o) {
@@ -869,12 +885,15 @@ __global__ __launch_bounds__(256) void k_f32_linear_dgrad(const float* __restric
 }
 
 // per worker g: dW_g[o][f] = Σ_{r in g} dl[r][o] x[r][f], db_g[o] = Σ dl[r][o]; written at
-// out + g * row_stride + off_w / off_b (the exchange rows); blockIdx.y = g, one thread per f
+// out + g * row_stride + off_w / off_b (the exchange rows). Block (64 f-columns, worker g): its four waves
+// take every fourth row, then the four partial sums are added in LDS in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void k_f32_linear_wgrad(const float* __restrict__ x, const float* __restrict__ dl,
                                                           int rg, int F, int O, float* __restrict__ out,
                                                           int64_t row_stride, int64_t off_w, int64_t off_b) {
+  __shared__ float red[3][kLinMaxO][64];
   const int g = blockIdx.y;
-  const int f = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + lane;
   const float* xg = x + static_cast<int64_t>(g) * rg * F;
   const float* dg = dl + static_cast<int64_t>(g) * rg * O;
   float* og = out + static_cast<int64_t>(g) * row_stride;
@@ -883,16 +902,26 @@ __global__ __launch_bounds__(256) void k_f32_linear_wgrad(const float* __restric
 #pragma unroll
     for (int o = 0; o < kLinMaxO; ++o) acc[o] = 0.f;
     if (f < F) {
-      for (int r = 0; r < rg; ++r) {
+#pragma unroll 4
+      for (int r = q; r < rg; r += 4) {
         const float xv = xg[static_cast<int64_t>(r) * F + f];
 #pragma unroll
         for (int o = 0; o < kLinMaxO; ++o)
           if (o0 + o < O) acc[o] = fmaf(dg[static_cast<int64_t>(r) * O + o0 + o], xv, acc[o]);
       }
+    }
+    if (q > 0) {
+#pragma unroll
+      for (int o = 0; o < kLinMaxO; ++o) red[q - 1][o][lane] = acc[o];
+    }
+    __syncthreads();
+    if (q == 0 && f < F) {
 #pragma unroll
       for (int o = 0; o < kLinMaxO; ++o)
-        if (o0 + o < O) og[off_w + static_cast<int64_t>(o0 + o) * F + f] = acc[o];
+        if (o0 + o < O)
+          og[off_w + static_cast<int64_t>(o0 + o) * F + f] = ((acc[o] + red[0][o][lane]) + red[1][o][lane]) + red[2][o][lane];
     }
+    __syncthreads();
   }
   if (off_b >= 0 && blockIdx.x == 0 && threadIdx.x < O) {
     float s = 0.f;
@@ -1068,7 +1097,7 @@ void linear_f32_dgrad(const float* dl, const float* w, int R, int F, int O, floa
 void linear_f32_wgrad(const float* x, const float* dl, int groups, int rg, int F, int O, float* out, int64_t row_stride,
                       int64_t off_w, int64_t off_b, hipStream_t stream) {
   if (groups <= 0 || F <= 0) return;
-  hipLaunchKernelGGL(k_f32_linear_wgrad, dim3((F + 255) / 256, groups), dim3(256), 0, stream, x, dl, rg, F, O, out,
+  hipLaunchKernelGGL(k_f32_linear_wgrad, dim3((F + 63) / 64, groups), dim3(256), 0, stream, x, dl, rg, F, O, out,
                      row_stride, off_w, off_b);
 }
 

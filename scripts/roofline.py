@@ -24,6 +24,10 @@ MFMA_PEAK = 2.5e15
 CLASSES = [
     ("BatchNorm (partial / finalize / apply / small)", r"k_partial|k_fwd_apply|k_bwd_apply|k_bn_|finalize|bn_running"),
     ("hipBLASLt GEMM (1x1 conv, stem, layer4, classifier)", r"^Cijk_"),
+    ("hand-written 1x1 / im2col GEMMs (gemm_nt.hip)", r"k_gemm_nt|k_gemm_ws"),
+    ("halo-staged 3x3 conv / weight gradient (conv3x3_nhwc.hip)", r"k_conv3x3|k_wgrad3x3"),
+    ("stem 7x7 (stem_nhwc.hip)", r"k_stem"),
+    ("fp32 split-bf16 convolutions / weight gradients (conv_f32.hip)", r"k_cf32|k_wsplit|k_f32_"),
     ("implicit-GEMM conv fwd/dgrad (k_iconv_lds)", r"k_iconv"),
     ("implicit weight gradients (k_iwgrad)", r"k_iwgrad"),
     ("im2col / col2im", r"im2col|col2im"),
