@@ -476,6 +476,10 @@ __device__ __forceinline__ s16x4 tr16(uint32_t lds_addr) {
       reinterpret_cast<__attribute__((address_space(3))) s16x4*>(static_cast<uintptr_t>(lds_addr)));
 }
 
+// LDS swizzle of the transposed-read tiles: 8-byte unit u of pixel row r is stored at u ^ 4 tr_swz(r),
+// so the 32 (row, unit) pairs one half-wave's ds_read_b64_tr_b16 touches (rows {0..3, 8..11} + 16 j,
+// four units) fall on distinct bank pairs (unswizzled: 4-way conflicts, 60 % of the LDS cycles)
+__device__ __forceinline__ int tr_swz(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 1); }
 constexpr int kTB = 32 * 128;          // one [32 pixel][64 channel] bf16 tile
 constexpr int kSB = 2 * kNP * kTB;     // dy pieces 0..2 | x pieces 0..2
 
@@ -545,7 +549,8 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x,
     char* base = lds + slot * kSB;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int off = (srow + 16 * h) * 128 + sch * 8;
+      const int row = srow + 16 * h;
+      const int off = row * 128 + ((sch ^ (4 * tr_swz(row))) * 8);   // bank swizzle (see tr_swz)
       uint32_t p0[kNP], p1[kNP];
       split2(rd[h].x, rd[h].y, p0);
       split2(rd[h].z, rd[h].w, p1);
@@ -567,8 +572,11 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x,
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)lds));
-  const uint32_t offA = (8 * grp + q) * 128 + (16 * cf0 + 4 * p) * 2;
-  const uint32_t offB = kNP * kTB + (8 * grp + q) * 128 + (16 * kf0 + 4 * p) * 2;
+  // fragment k of a tile: 8-byte unit 4 k + p of row 8 grp + q, stored at unit (4 k + p) ^ 4 tr_swz(row)
+  const int trow = 8 * grp + q, tsw = tr_swz(trow);
+  const uint32_t offA0 = trow * 128 + (4 * (cf0 ^ tsw) + p) * 8, offA1 = trow * 128 + (4 * ((cf0 + 1) ^ tsw) + p) * 8;
+  const uint32_t offB0 = kNP * kTB + trow * 128 + (4 * (kf0 ^ tsw) + p) * 8;
+  const uint32_t offB1 = kNP * kTB + trow * 128 + (4 * ((kf0 + 1) ^ tsw) + p) * 8;
 
   if (steps > 0) load(0);
   for (int s = 0; s < steps; ++s) {
@@ -578,16 +586,16 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x,
     __syncthreads();
     const uint32_t sb = lds0 + (s & 1) * kSB;
     // transposed fragments (see k_iwgrad in iconv_nhwc.hip) of one piece tile: two fragments u
-    auto tr_read = [&](uint32_t addr, bf16x8 (&f)[2]) {
-      const s16x4 r0 = tr16(addr), r1 = tr16(addr + 512), r2 = tr16(addr + 32), r3 = tr16(addr + 544);
+    auto tr_read = [&](uint32_t a0, uint32_t a1, bf16x8 (&f)[2]) {   // fragments at a0, a1 (rows r, r + 4)
+      const s16x4 r0 = tr16(a0), r1 = tr16(a0 + 512), r2 = tr16(a1), r3 = tr16(a1 + 512);
       f[0] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
       f[1] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r2, r3, 0, 1, 2, 3, 4, 5, 6, 7));
     };
     bf16x8 ta[kNP][2], tb[kNP][2];
 #pragma unroll
     for (int i = 0; i < kNP; ++i) {
-      tr_read(sb + i * kTB + offA, ta[i]);
-      tr_read(sb + i * kTB + offB, tb[i]);
+      tr_read(sb + i * kTB + offA0, sb + i * kTB + offA1, ta[i]);
+      tr_read(sb + i * kTB + offB0, sb + i * kTB + offB1, tb[i]);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -618,10 +626,6 @@ __global__ __launch_bounds__(256) void k_cf32_wgrad(const float* __restrict__ x,
 // 64 k) instead of 2 x 2, halving the LDS fragment bytes per MFMA (the 64 x 64 form reads 512 B of
 // LDS per MFMA and is LDS-bound). Each operand's [32 pixel][128 channel] step tile is kept as two
 // [32][64] sub-tiles (128-byte pitch: the bank pattern of the 64 x 64 form).
-// LDS swizzle of the transposed-read tiles: 8-byte unit u of pixel row r is stored at u ^ 4 tr_swz(r),
-// so the 32 (row, unit) pairs one half-wave's ds_read_b64_tr_b16 touches (rows {0..3, 8..11} + 16 j,
-// four units) fall on distinct bank pairs (unswizzled: 4-way conflicts, 60 % of the LDS cycles)
-__device__ __forceinline__ int tr_swz(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 1); }
 constexpr int kTB2 = 2 * kTB;              // one operand piece: two [32][64] sub-tiles
 constexpr int kSB2 = 2 * kNP * kTB2;       // dy pieces 0..2 | x pieces 0..2
 

@@ -198,10 +198,14 @@ __global__ __launch_bounds__(256) void k_split_reduce_multi(SplitTable t) {
       const float4 a = *reinterpret_cast<const float4*>(p + static_cast<int64_t>(s) * J.ss);
       acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
     }
-    dev::store_one(J.out, J.odt, o, acc.x);
-    dev::store_one(J.out, J.odt, o + 1, acc.y);
-    dev::store_one(J.out, J.odt, o + 2, acc.z);
-    dev::store_one(J.out, J.odt, o + 3, acc.w);
+    if (J.vec == 2) {   // fp32 rows, 16-byte aligned: one vector store
+      *reinterpret_cast<float4*>(static_cast<float*>(J.out) + o) = acc;
+    } else {
+      dev::store_one(J.out, J.odt, o, acc.x);
+      dev::store_one(J.out, J.odt, o + 1, acc.y);
+      dev::store_one(J.out, J.odt, o + 2, acc.z);
+      dev::store_one(J.out, J.odt, o + 3, acc.w);
+    }
   } else {
     float acc = 0.f;
 #pragma unroll 8
@@ -221,6 +225,9 @@ void split_reduce_multi(const SplitJob* jobs, int count, hipStream_t stream) {
       SplitJob J = jobs[base + i];
       J.vec = (J.Cc % 4 == 0 && J.ipitch % 4 == 0 && J.ss % 4 == 0 && J.gs % 4 == 0 &&
                reinterpret_cast<uintptr_t>(J.part) % 16 == 0) ? 1 : 0;
+      if (J.vec && J.odt == kF32 && J.opitch % 4 == 0 && J.ostride % 4 == 0 &&
+          reinterpret_cast<uintptr_t>(J.out) % 16 == 0)
+        J.vec = 2;
       t.job[i] = J;
       t.blk0[i] = blocks;
       const int64_t cvh = J.vec ? J.Cc / 4 : J.Cc;
