@@ -1713,11 +1713,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "Coordinate-wise rule on an [n, d] gradient matrix with n <= LARGE_ROWS by LDS radix select; "
         "args (x, mode 0 median | 1 trimmed-mean | 2 averaged-median, f, beta, out)");
   m.def("iwgrad_taps_per_block",
-        [](int64_t kw, int64_t kh, int64_t c) {
-          return garfield::gpu::iwgrad_taps_per_block(static_cast<int>(kw), static_cast<int>(kh), static_cast<int>(c));
+        [](int64_t kw, int64_t kh, int64_t c, int64_t cout) {
+          return garfield::gpu::iwgrad_taps_per_block(static_cast<int>(kw), static_cast<int>(kh), static_cast<int>(c),
+                                                      static_cast<int>(cout));
         },
-        py::arg("kw"), py::arg("kh") = 3, py::arg("c") = 0,
-        "Taps (1x1: input-channel blocks) per workgroup gpu_iwgrad uses for a kh x kw kernel over c input channels");
+        py::arg("kw"), py::arg("kh") = 3, py::arg("c") = 0, py::arg("cout") = 0,
+        "Taps (1x1: 64-channel input blocks x 64-channel output blocks / 64x64 tiles) per workgroup gpu_iwgrad uses "
+        "for a kh x kw kernel over c input and cout output channels");
   m.def("gpu_split_reduce_multi", &g_split_reduce_multi,
         "gpu_split_reduce for many (part, out) pairs in one launch; args (parts, outs)");
   m.def("gpu_split_reduce", &g_split_reduce,

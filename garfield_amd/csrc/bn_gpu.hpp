@@ -149,7 +149,7 @@ void maxpool_bwd_nhwc(const void* dy, const uint8_t* idx, const Im2col& g, void*
 // Taps per workgroup of iwgrad_nhwc for a kh x kw kernel over C input channels (3x3: the three
 // taps of a kernel row share each staged dy tile, GARFIELD_IWGRAD_ROW; 1x1: up to four 64-channel
 // input blocks share it, GARFIELD_IWGRAD_1X1_NT).
-int iwgrad_taps_per_block(int kw, int kh = 3, int C = 0);
+int iwgrad_taps_per_block(int kw, int kh = 3, int C = 0, int Cout = 0);
 void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
                  int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream);
 // accumulate: dx += col2im(dcol) instead of dx = col2im(dcol).

@@ -871,11 +871,152 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
   }
 }
 
+// 1x1 weight gradient with 128 output channels x 128 input channels per workgroup (Cout, C % 128 == 0):
+// each wave computes 4 x 4 fragments (64 x 64) -- four times the MFMAs per staged byte and per barrier of
+// the 2 x 2-fragment kernel above, which is latency-bound (one 32-pixel step = 8 MFMAs per wave between
+// barriers). A stage is 64 pixels (two 32-deep MFMA steps): dy [64 px][128 co] and x [64 px][128 ci] as
+// four [64][64] bf16 sub-tiles of 128-byte rows, staged by LDS-DMA with the bank swizzle (tr_g), read
+// transposed; 3-deep ring (96 KB: one workgroup per CU).
+constexpr int kW1Stage = 4 * 64 * 128;   // bytes per stage: dy0 | dy1 | x0 | x1
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(256) void k_iwgrad_1x1_wide(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                         Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
+                                                         int64_t split_stride, int64_t group_stride) {
+  constexpr int NS = 3;
+  constexpr int SUB = 64 * 128;          // one [64 px][64 ch] sub-tile
+  extern __shared__ __attribute__((aligned(16))) char wlds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = g.C;
+  const int nq = g.C / 128;
+  const int qb = blockIdx.x % nq, cb = blockIdx.x / nq;
+  const int c0 = qb * 128, co0 = cb * 128;
+  const int gi = blockIdx.y, sp = blockIdx.z;
+  const int64_t mbeg = static_cast<int64_t>(gi) * rg + static_cast<int64_t>(sp) * per_split;
+  int64_t mend = mbeg + per_split;
+  if (mend > static_cast<int64_t>(gi + 1) * rg) mend = static_cast<int64_t>(gi + 1) * rg;
+  const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 63) / 64) : 0;
+  const FastDiv fWo = make_fastdiv(g.Wo), fHo = make_fastdiv(g.Ho);
+
+  // staging: instruction u (0..7) of this wave covers sub-tile u / 2, rows 8 ((u & 1) * 4 + wave) + lane / 8
+  const int lchunk = lane & 7;
+  const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
+  const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
+  auto issue = [&](int s, int slot) {
+    char* base = wlds + slot * kW1Stage;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      const int row = 8 * (hb * 4 + wave) + (lane >> 3);
+      const int lsw = lchunk ^ (2 * tr_g(row));
+      const int m = static_cast<int>(mbeg) + s * 64 + row;   // < 2^31: checked by the host wrapper
+      const bool mv = m < static_cast<int>(mend);
+      const int mm = mv ? m : 0;
+      uint32_t t, wo, n, ho;
+      fdivmod(static_cast<uint32_t>(mm), fWo, t, wo);
+      fdivmod(t, fHo, n, ho);
+      const int hi = static_cast<int>(ho) * g.sh - g.ph, wi = static_cast<int>(wo) * g.sw - g.pw;
+      const bool ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+      const uint16_t* dr = dy + static_cast<int64_t>(mm) * Cout + co0 + lsw * 8;
+      const uint16_t* xr = x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 +
+                           lsw * 8;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? reinterpret_cast<uint64_t>(dr + 64 * b) : az),
+                                         (lds_ptr)(base + b * SUB + (hb * 4 + wave) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? reinterpret_cast<uint64_t>(xr + 64 * b) : az),
+                                         (lds_ptr)(base + (2 + b) * SUB + (hb * 4 + wave) * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  // wave (sa, sb): co sub-tile sa = wave >> 1 (fragments 4 sa ..), ci sub-tile sb = wave & 1
+  const int sa = wave >> 1, sbk = wave & 1;
+  const int grp = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int trow = 8 * grp + q, tg = tr_g(trow);
+  uint32_t offA[4], offB[4];   // fragment k: chunk pair k ^ tg of row trow (+ 4 rows at offset 512)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    offA[k] = sa * SUB + trow * 128 + 32 * (k ^ tg) + 8 * p;
+    offB[k] = (2 + sbk) * SUB + trow * 128 + 32 * (k ^ tg) + 8 * p;
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)wlds));
+
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < steps) issue(s0, s0);
+  for (int s = 0; s < steps; ++s) {
+    const int ahead = (steps - 1 - s) < (NS - 2) ? (steps - 1 - s) : (NS - 2);
+    if (ahead >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // the next stage's 8 glds may stay in flight
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
+    const uint32_t sbase = lds0 + (s % NS) * kW1Stage;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {   // pixel rows 32 ks .. 32 ks + 31
+      const uint32_t b0 = sbase + ks * 4096;
+      s16x4 ra[8], rb[8];
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %16\n\t"
+          "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
+          "ds_read_b64_tr_b16 %2, %17\n\t"
+          "ds_read_b64_tr_b16 %3, %17 offset:512\n\t"
+          "ds_read_b64_tr_b16 %4, %18\n\t"
+          "ds_read_b64_tr_b16 %5, %18 offset:512\n\t"
+          "ds_read_b64_tr_b16 %6, %19\n\t"
+          "ds_read_b64_tr_b16 %7, %19 offset:512\n\t"
+          "ds_read_b64_tr_b16 %8, %20\n\t"
+          "ds_read_b64_tr_b16 %9, %20 offset:512\n\t"
+          "ds_read_b64_tr_b16 %10, %21\n\t"
+          "ds_read_b64_tr_b16 %11, %21 offset:512\n\t"
+          "ds_read_b64_tr_b16 %12, %22\n\t"
+          "ds_read_b64_tr_b16 %13, %22 offset:512\n\t"
+          "ds_read_b64_tr_b16 %14, %23\n\t"
+          "ds_read_b64_tr_b16 %15, %23 offset:512\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(ra[0]), "=&v"(ra[1]), "=&v"(ra[2]), "=&v"(ra[3]), "=&v"(ra[4]), "=&v"(ra[5]), "=&v"(ra[6]),
+            "=&v"(ra[7]), "=&v"(rb[0]), "=&v"(rb[1]), "=&v"(rb[2]), "=&v"(rb[3]), "=&v"(rb[4]), "=&v"(rb[5]),
+            "=&v"(rb[6]), "=&v"(rb[7])
+          : "v"(b0 + offA[0]), "v"(b0 + offA[1]), "v"(b0 + offA[2]), "v"(b0 + offA[3]), "v"(b0 + offB[0]),
+            "v"(b0 + offB[1]), "v"(b0 + offB[2]), "v"(b0 + offB[3])
+          : "memory");
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ra[2 * k], ra[2 * k + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+        b[k] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(rb[2 * k], rb[2 * k + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b[v], acc[u][v], 0, 0, 0);
+    }
+  }
+
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + (4 * sa + u) * 16 + 4 * grp + e;
+        const int k = c0 + (4 * sbk + v) * 16 + li;
+        const int64_t o = static_cast<int64_t>(sp) * split_stride + static_cast<int64_t>(gi) * group_stride +
+                          static_cast<int64_t>(co) * K + k;
+        if constexpr (OUT_BF16) static_cast<uint16_t*>(out)[o] = f_to_bf16(acc[u][v][e]);
+        else static_cast<float*>(out)[o] = acc[u][v][e];
+      }
+}
+
 // Taps per weight-gradient workgroup: a 3x3 kernel's row of three taps shares each staged dy tile
 // (profiles/r2/ab_iwgrad_9tap.log: all nine taps leave one wave per SIMD and lose); a 1x1
 // convolution's two 64-channel input blocks share it (profiles/r2/iwgrad_wg_nt_sweep.log).
-int iwgrad_taps_per_block(int kw, int kh, int C) {
-  if (kw == 1 && kh == 1) return C % 128 == 0 ? 2 : 1;
+int iwgrad_taps_per_block(int kw, int kh, int C, int Cout) {
+  if (kw == 1 && kh == 1) return C % 128 == 0 ? (Cout % 128 == 0 ? 4 : 2) : 1;   // 4: the 128 x 128 tile
   return kw == 3 ? 3 : 1;
 }
 
@@ -884,7 +1025,23 @@ void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cou
   const int K = g.KH * g.KW * g.C;
   if (splits < 1) splits = 1;
   const int64_t per_split = (rg + splits - 1) / splits;
-  const int tpb = iwgrad_taps_per_block(g.KW, g.KH, g.C);
+  const int tpb = iwgrad_taps_per_block(g.KW, g.KH, g.C, Cout);
+  if (tpb == 4 && g.KW == 1) {   // 1x1, C and Cout % 128: the 128 x 128-tile kernel
+    static bool once = (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iwgrad_1x1_wide<true>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kW1Stage),
+                        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iwgrad_1x1_wide<false>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kW1Stage),
+                        true);
+    (void)once;
+    const dim3 grid((g.C / 128) * (Cout / 128), groups, splits);
+    if (out_bf16)
+      hipLaunchKernelGGL(k_iwgrad_1x1_wide<true>, grid, dim3(256), 3 * kW1Stage, stream, x, dy, g, Cout, rg, per_split,
+                         out, split_stride, group_stride);
+    else
+      hipLaunchKernelGGL(k_iwgrad_1x1_wide<false>, grid, dim3(256), 3 * kW1Stage, stream, x, dy, g, Cout, rg, per_split,
+                         out, split_stride, group_stride);
+    return;
+  }
   if (tpb == 2 && g.KW == 1) {   // 1x1: two 64-channel input blocks per workgroup, 3 pipeline stages
     const dim3 grid((g.C / 128) * (Cout / 64), groups, splits);
     if (out_bf16)

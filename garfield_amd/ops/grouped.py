@@ -725,7 +725,7 @@ def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int)
         S = _wgrad3x3_splits(rows, (x.shape[1] // 64) * (cout // 64) * G)
     else:
         S = _iwgrad_splits(rows, (K // 64) * (cout // 64) * G //
-                          C_.iwgrad_taps_per_block(spec.kernel[1], spec.kernel[0], x.shape[1]))
+                          C_.iwgrad_taps_per_block(spec.kernel[1], spec.kernel[0], x.shape[1], cout))
     out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy.dtype) if S == 1 else None
     if out is not None:
         C_.gpu_iwgrad(x, dy, *_geom(spec), G, out, 1)
