@@ -1445,6 +1445,8 @@ bool load(const std::string& path);
 void all_to_all(int64_t comm, const void* send, void* recv, size_t count, int dtype, hipStream_t stream);
 void all_gather(int64_t comm, const void* send, void* recv, size_t count, int dtype, hipStream_t stream);
 void all_reduce_sum(int64_t comm, const void* send, void* recv, size_t count, int dtype, hipStream_t stream);
+void exchange(int64_t comm, const int64_t* ptr, const int64_t* count, const int64_t* peer, int64_t nsend,
+              int64_t nops, int dtype, hipStream_t stream);
 }  // namespace rccl
 }  // namespace garfield
 
@@ -1496,6 +1498,29 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     garfield::rccl::all_reduce_sum(comm, send.data_ptr(), recv.data_ptr(), static_cast<size_t>(send.numel()),
                                    nccl_dtype(send), reinterpret_cast<hipStream_t>(stream));
   }, py::arg("comm"), py::arg("send"), py::arg("recv"), py::arg("stream"), "ncclAllReduce(sum) on `stream`");
+  m.def("rccl_exchange", [](int64_t comm, const std::vector<at::Tensor>& sends, const std::vector<int64_t>& to,
+                            const std::vector<at::Tensor>& recvs, const std::vector<int64_t>& from, int64_t world,
+                            int64_t stream) {
+    TORCH_CHECK(sends.size() == to.size() && recvs.size() == from.size(), "garfield rccl: one peer per buffer");
+    TORCH_CHECK(!sends.empty() || !recvs.empty(), "garfield rccl: empty exchange");
+    const at::Tensor& ref = sends.empty() ? recvs[0] : sends[0];
+    std::vector<int64_t> ptr, cnt, peer;
+    auto add = [&](const at::Tensor& t, int64_t p) {
+      TORCH_CHECK(t.is_cuda() && t.device() == ref.device() && t.is_contiguous() && t.scalar_type() == ref.scalar_type(),
+                  "garfield rccl: contiguous GPU buffers of one dtype on one device");
+      TORCH_CHECK(p >= 0 && p < world, "garfield rccl: peer ", p, " outside the world of ", world);
+      ptr.push_back(reinterpret_cast<int64_t>(t.data_ptr()));
+      cnt.push_back(t.numel());
+      peer.push_back(p);
+    };
+    for (size_t i = 0; i < sends.size(); ++i) add(sends[i], to[i]);
+    for (size_t i = 0; i < recvs.size(); ++i) add(recvs[i], from[i]);
+    garfield::rccl::exchange(comm, ptr.data(), cnt.data(), peer.data(), static_cast<int64_t>(sends.size()),
+                             static_cast<int64_t>(ptr.size()), nccl_dtype(ref), reinterpret_cast<hipStream_t>(stream));
+  }, py::arg("comm"), py::arg("sends"), py::arg("to"), py::arg("recvs"), py::arg("from_"), py::arg("world"),
+     py::arg("stream"),
+     "One ncclGroup of ncclSend(sends[i] -> to[i]) and ncclRecv(recvs[i] <- from_[i]) on `stream`; transfers "
+     "between one pair of ranks match in issue order");
   m.def("event_create", &event_create, py::arg("scope") = 1,
         "HIP event (no timing); scope 0: system-scope release on record (HIP default), 1: device-scope "
         "release (enough for other streams of this device), 2: no system fence");

@@ -83,6 +83,29 @@ void all_to_all(int64_t comm, const void* send, void* recv, size_t count, int dt
   check(api().all_to_all(send, recv, count, dtype, reinterpret_cast<Comm>(comm), stream), "ncclAllToAll");
 }
 
+// One group of point-to-point transfers: ops[i] = (ptr, count, peer), the first nsend are
+// sends. Sends to one peer are matched with that peer's receives in issue order, so a
+// bucket's rows leave straight from the exchange rows (one contiguous shard per worker
+// row and destination) with no packing copy, and this rank's own shard never moves.
+void exchange(int64_t comm, const int64_t* ptr, const int64_t* count, const int64_t* peer, int64_t nsend,
+              int64_t nops, int dtype, hipStream_t stream) {
+  const Api& a = api();
+  Comm c = reinterpret_cast<Comm>(comm);
+  check(a.group_start(), "ncclGroupStart");
+  for (int64_t i = 0; i < nops; ++i) {
+    Res r = i < nsend
+        ? a.send(reinterpret_cast<const void*>(ptr[i]), static_cast<size_t>(count[i]), dtype,
+                 static_cast<int>(peer[i]), c, stream)
+        : a.recv(reinterpret_cast<void*>(ptr[i]), static_cast<size_t>(count[i]), dtype,
+                 static_cast<int>(peer[i]), c, stream);
+    if (r != 0) {
+      a.group_end();
+      check(r, i < nsend ? "ncclSend" : "ncclRecv");
+    }
+  }
+  check(a.group_end(), "ncclGroupEnd");
+}
+
 void all_gather(int64_t comm, const void* send, void* recv, size_t count, int dtype, hipStream_t stream) {
   check(api().all_gather(send, recv, count, dtype, reinterpret_cast<Comm>(comm), stream), "ncclAllGather");
 }

@@ -57,6 +57,11 @@ class DirectRCCL:
     def all_to_all(self, send: torch.Tensor, recv: torch.Tensor, stream) -> None:
         self._C.rccl_all_to_all(self.comm, send, recv, self.world, stream.cuda_stream)
 
+    def exchange(self, sends: list, to: list, recvs: list, frm: list, stream) -> None:
+        """One group of ncclSend(sends[i] -> rank to[i]) / ncclRecv(recvs[i] <- rank frm[i]);
+        transfers between one pair of ranks match in issue order."""
+        self._C.rccl_exchange(self.comm, sends, to, recvs, frm, self.world, stream.cuda_stream)
+
     def all_gather(self, send: torch.Tensor, recv: torch.Tensor, stream) -> None:
         """recv = [world, *send.shape] flat; in place when send is recv's own rank block."""
         self._C.rccl_all_gather(self.comm, send, recv, self.world, stream.cuda_stream)
@@ -78,7 +83,11 @@ class GlooDirect:
       rank r, chunk r of ``recv`` comes from rank r (``ncclAllToAll``);
     * ``all_gather(send, recv)``: ``recv`` = world x ``send``; when ``send`` overlaps ``recv`` it
       must be EXACTLY recv's own rank block (RCCL's in-place form), anything else is refused;
-    * ``all_reduce_sum(t)``: in place.
+    * ``all_reduce_sum(t)``: in place;
+    * ``exchange(sends, to, recvs, frm)``: one group of point-to-point transfers; every buffer
+      flat and contiguous, no transfer to or from this rank itself, no receive buffer
+      overlapping another buffer, and the sends to a peer pair up in order with that peer's
+      receives (sizes checked against the peer's actual receives).
 
     ``calls`` counts the collectives by kind (the tests assert the per-step pattern)."""
 
@@ -126,6 +135,31 @@ class GlooDirect:
             raise ValueError("direct all_reduce: contiguous buffer")
         self.calls["all_reduce"] += 1
         dist.all_reduce(t)
+
+    def exchange(self, sends: list, to: list, recvs: list, frm: list, stream=None) -> None:
+        if len(sends) != len(to) or len(recvs) != len(frm):
+            raise ValueError("direct exchange: one peer per buffer")
+        for t, p in [*zip(sends, to), *zip(recvs, frm)]:
+            if not (t.is_contiguous() and t.dim() == 1):
+                raise ValueError("direct exchange: flat contiguous buffers")
+            if not 0 <= p < self.world or p == self.rank:
+                raise ValueError(f"direct exchange: peer {p} (the own shard never moves)")
+        for i, r in enumerate(recvs):
+            for t in [*sends, *recvs[:i]]:
+                if self._overlap(r, t):
+                    raise ValueError("direct exchange: a receive buffer overlaps another buffer")
+        # the sizes each peer will send, checked against the receives posted for it (in order)
+        mine = {p: [int(t.numel()) for t, q in zip(sends, to) if q == p] for p in range(self.world)}
+        table = [None] * self.world
+        dist.all_gather_object(table, mine)
+        for p in range(self.world):
+            if p != self.rank and table[p][self.rank] != [int(t.numel()) for t, q in zip(recvs, frm) if q == p]:
+                raise ValueError(f"direct exchange: rank {p}'s sends do not match the receives posted for it")
+        self.calls["exchange"] += 1
+        ops = [dist.P2POp(dist.isend, t, p) for t, p in zip(sends, to)]
+        ops += [dist.P2POp(dist.irecv, t, p) for t, p in zip(recvs, frm)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
 
 
 _OVERRIDE = None

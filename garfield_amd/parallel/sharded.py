@@ -17,9 +17,11 @@ squared distances, and squared distances are additive over coordinate blocks:
 2. a bucket is exchanged as soon as the backward has written it: the grouped
    executor's captured graph bumps a device-side counter when its backward crosses
    the bucket boundary (``parallel/signals.py``), a comm stream waits for it ON THE
-   DEVICE, applies the simulated attacks to that slice, packs the k local rows as
-   ``[dst, worker, shard]`` and sends the whole bucket in ONE ``all_to_all_single``
-   -- so most of the exchange runs under the rest of the backward (every collective
+   DEVICE, applies the simulated attacks to that slice and sends the whole bucket in
+   ONE group of RCCL point-to-point transfers straight from the exchange rows (each
+   local row's shard ``dst`` is contiguous; this rank's own shard is read in place and
+   never moves; through torch.distributed: a ``[dst, worker, shard]`` pack and one
+   ``all_to_all_single``) -- so most of the exchange runs under the rest of the backward (every collective
    of the step is issued from the comm stream: a HIP event dependency on the main
    stream would slow the next graph replay, see signals.py);
 3. distance-based rules (Krum/Multi-Krum, Bulyan's selection, Brute): each rank
@@ -89,12 +91,13 @@ class _Bucket:
     leaves in ONE ``all_to_all_single``), ``recv[src, j]`` = shard ``rank`` of source
     rank src's local worker j (the row of global slot j * world + src)."""
 
-    def __init__(self, lo: int, hi: int, world: int, rank: int, k: int, dev, dt):
+    def __init__(self, lo: int, hi: int, world: int, rank: int, k: int, dev, dt, pack: bool):
         self.lo, self.hi = lo, hi
         self.S = (hi - lo) // world
         self.own = slice(lo + rank * self.S, lo + (rank + 1) * self.S)
-        self.send = torch.empty((world, k, self.S), dtype=dt, device=dev) if world > 1 else None
+        self.send = torch.empty((world, k, self.S), dtype=dt, device=dev) if world > 1 and pack else None
         self.recv = torch.empty((world, k, self.S), dtype=dt, device=dev) if world > 1 else None
+        self.p2p = None        # the direct exchange's (sends, to, recvs, from) lists
         self.moff = 0          # offset of this bucket's shard in the momentum buffer
         self.works: list = []
         self.rows: list = []
@@ -116,22 +119,6 @@ class ShardedAggregator:
         cuts = sorted({min(e.ld, ((int(b) + align - 1) // align) * align) for b in boundaries} - {0, e.ld})
         edges = [0, *cuts, e.ld]
         dev, dt = e.device, e.X.dtype
-        # ready order of the backward: highest coordinates (last layers) first
-        self.buckets = [_Bucket(edges[i], edges[i + 1], self.world, self.rank, self.k, dev, dt)
-                        for i in reversed(range(len(edges) - 1))]
-        off = 0
-        for b in sorted(self.buckets, key=lambda b: b.lo):
-            b.moff = off
-            off += b.S
-        self.S = off                                   # owned coordinates = ld / world
-        for b in self.buckets:
-            b.rows = self._rows_of(b)
-        self._one = torch.ones(1, dtype=torch.float32, device=dev)
-        self._avg = torch.full((self.n,), 1.0 / self.n, dtype=torch.float32, device=dev)
-        self._ws = {}
-        self._started = False
-        self._gathers: list = []
-        self.master_stale = False
         # every collective of the step is issued from the comm stream (so RCCL's internal
         # stream depends on it, never on the main stream: parallel/signals.py), which
         # follows the main stream through device-side hand-offs
@@ -143,17 +130,57 @@ class ShardedAggregator:
         self._handoff = Handoff(dev) if side else None
         # RCCL kernels straight onto the comm stream (rccl.py); None: torch.distributed
         self._rccl = direct_backend(self.world, self.rank, side)
+        # ready order of the backward: highest coordinates (last layers) first
+        self.buckets = [_Bucket(edges[i], edges[i + 1], self.world, self.rank, self.k, dev, dt, self._rccl is None)
+                        for i in reversed(range(len(edges) - 1))]
+        off = 0
+        for b in sorted(self.buckets, key=lambda b: b.lo):
+            b.moff = off
+            off += b.S
+        self.S = off                                   # owned coordinates = ld / world
+        for b in self.buckets:
+            b.rows = self._rows_of(b)
+            if self._rccl is not None:
+                b.p2p = self._p2p_of(b)
+        self._one = torch.ones(1, dtype=torch.float32, device=dev)
+        self._avg = torch.full((self.n,), 1.0 / self.n, dtype=torch.float32, device=dev)
+        self._ws = {}
+        self._started = False
+        self._gathers: list = []
+        self.master_stale = False
         self._init_fp32_sync()
 
     # ------------------------------------------------------------------ #
     # layout
 
     def _rows_of(self, b: _Bucket) -> list:
-        """Row (global slot j * world + src) -> its shard of bucket b, in slot order."""
+        """Row (global slot j * world + src) -> its shard of bucket b, in slot order. On the
+        direct exchange this rank's own workers' rows are read in place from the exchange
+        rows (the own shard never moves); the packed all_to_all receives them in recv[rank]."""
         e = self.e
         if self.world == 1:
             return [e.X[j, 0, b.lo:b.hi] for j in range(self.k)]
-        return [b.recv[s % self.world, s // self.world] for s in range(self.n)]
+        rows = []
+        for s in range(self.n):
+            src, j = s % self.world, s // self.world
+            rows.append(e.X[j, 0, b.own] if src == self.rank and self._rccl is not None else b.recv[src, j])
+        return rows
+
+    def _p2p_of(self, b: _Bucket):
+        """The direct exchange of bucket b as point-to-point transfers with no packing copy:
+        local worker j's shard dst (contiguous in its exchange row) goes to rank dst, and
+        source rank src's worker j lands in recv[src, j]; pairs match in issue order."""
+        e, W = self.e, self.world
+        sends, to, recvs, frm = [], [], [], []
+        for d in range(1, W):
+            dst = (self.rank + d) % W            # staggered peers: every rank starts on a different link
+            src = (self.rank - d) % W
+            for j in range(self.k):
+                sends.append(e.X[j, 0, b.lo + dst * b.S:b.lo + (dst + 1) * b.S])
+                to.append(dst)
+                recvs.append(b.recv[src, j])
+                frm.append(src)
+        return sends, to, recvs, frm
 
     def _init_fp32_sync(self) -> None:
         """fp32 parameters the forward reads directly (not mirrored by the bf16 working
@@ -197,11 +224,14 @@ class ShardedAggregator:
 
     def start_exchange(self, events=None) -> None:
         """Issue every bucket's exchange, in ready order: the simulated attacks on the
-        bucket's slice of the local rows, one pack of the k rows into ``send[dst, j]``
-        and ONE ``all_to_all_single`` per bucket (3 collectives per step for the
-        ResNets). ``events[i]`` (optional) marks the point of the backward where bucket
-        i's rows are complete; the comm stream waits on it, so the exchange overlaps
-        the rest of the backward."""
+        bucket's slice of the local rows, then ONE group of transfers per bucket (3 per
+        step for the ResNets). On the direct RCCL path that group is the point-to-point
+        sends of each local row's shards straight from the exchange rows (no packing copy:
+        on a memory-bound backward the copy alone cost as much HBM time as the transfer)
+        and this rank's own shard stays where it is; through torch.distributed it is a pack
+        into ``send[dst, j]`` and one ``all_to_all_single``. ``events[i]`` (optional) marks
+        the point of the backward where bucket i's rows are complete; the comm stream
+        waits on it, so the exchange overlaps the rest of the backward."""
         e = self.e
         side = self._comm_stream is not None
         use_events = (side and events is not None and overlap_enabled(self.world)
@@ -219,18 +249,12 @@ class ShardedAggregator:
             with ctx:
                 e._attack_rows(b.lo, b.hi)
                 b.works = []
-                local = e.X[:, 0, b.lo:b.hi].view(self.k, self.world, b.S).transpose(0, 1)   # [dst, j, S]
-                if self.world > 1:
+                if self.world > 1 and self._rccl is not None:   # straight from the exchange rows
+                    self._rccl.exchange(*b.p2p, self._comm_stream)
+                elif self.world > 1:
+                    local = e.X[:, 0, b.lo:b.hi].view(self.k, self.world, b.S).transpose(0, 1)   # [dst, j, S]
                     b.send.copy_(local)
-                    if self._rccl is not None:
-                        self._rccl.all_to_all(b.send.view(-1), b.recv.view(-1), self._comm_stream)
-                    else:
-                        b.works.append(dist.all_to_all_single(b.recv.view(-1), b.send.view(-1), async_op=True))
-                elif side and loopback_enabled():   # world 1: emulate the transfer (traces / tests)
-                    if b.recv is None:
-                        b.recv = torch.empty((1, self.k, b.S), dtype=e.X.dtype, device=e.device)
-                        b.rows = [b.recv[0, j] for j in range(self.k)]
-                    b.recv.copy_(local)
+                    b.works.append(dist.all_to_all_single(b.recv.view(-1), b.send.view(-1), async_op=True))
                 if side:
                     b.done = torch.cuda.Event(enable_timing=_TIMING)
                     b.done.record(s)
@@ -450,7 +474,9 @@ class ShardedAggregator:
         """Bucket b's received shards as ONE [n, S] matrix (row src * k + j: the receive
         buffer as it lands, no copy); ``self._perm[s]`` is the matrix row of global slot s."""
         if self.world == 1:
-            return torch.stack(b.rows) if b.recv is None else b.recv.view(self.n, b.S)
+            return torch.stack(b.rows)
+        if self._rccl is not None:   # the own shard was read in place: bring it into the matrix
+            b.recv[self.rank].copy_(self.e.X[:, 0, b.own])
         return b.recv.view(self.n, b.S)
 
     def _gpu_large(self, cfg, first: bool) -> None:
@@ -827,6 +853,7 @@ _TIMING = os.environ.get("GARFIELD_EXCHANGE_TIMING", "0") == "1"
 
 
 def loopback_enabled() -> bool:
-    """GARFIELD_LOOPBACK_EXCHANGE=1 at world 1: copy every bucket into a receive buffer
-    on the side stream, as the all-to-all would (rocprof traces of the overlap, tests)."""
+    """GARFIELD_LOOPBACK_EXCHANGE=1 at world 1: run the exchange machinery of a multi-rank
+    step (comm stream, in-graph bucket signals, device-side hand-offs, per-bucket events)
+    with nothing to move, since a rank's own shard is read in place (traces, tests)."""
     return os.environ.get("GARFIELD_LOOPBACK_EXCHANGE", "0") == "1"

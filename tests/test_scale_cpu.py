@@ -9,8 +9,10 @@ MI355X (one process per device), with CPU tensors.
   buckets and the n = 64 Krum selection of the flagship configuration;
 * the exchange leaves in ONE ``all_to_all_single`` per bucket;
 * the same runs through ``GlooDirect`` (``parallel/rccl.py``): the direct-RCCL branch of the
-  exchange that 8 GPUs take, with its call contract checked (flat all-to-all, in-place
-  all-gather of this rank's block), bitwise equal to the torch.distributed branch.
+  exchange that 8 GPUs take, with its call contract checked (one group of point-to-point
+  transfers per bucket straight from the exchange rows, sizes matched against the peers'
+  receives, the own shard never sent; in-place all-gather of this rank's block), bitwise
+  equal to the torch.distributed branch.
 """
 import os
 import socket
@@ -106,7 +108,7 @@ def test_eight_rank_sharded_equals_redundant_bitwise():
                     assert got["sum"] == ref["sum"], (rule, s, r)
                     assert torch.equal(got["flat"], ref["flat"]), (rule, s, r)
             calls = res[(2, 0)][rule]["calls"]
-            assert calls["all_to_all"] == 2 and calls["all_gather_inplace"] == 2, (rule, calls)
+            assert calls["exchange"] == 2 and calls["all_gather_inplace"] == 2, (rule, calls)
             assert "all_reduce" not in calls, (rule, calls)   # every MLP parameter is a shadow view
 
 
@@ -177,7 +179,7 @@ def test_grouped_sharded_flagship_path(world, k):
     """ResNet worker batching + sharded bucketed Krum at 4 x 4 (n = 16) and 8 x 8 (n = 64)
     ranks x workers: replicas identical, sharded == redundant, 3 all_to_all per step; the
     direct-RCCL contract (mode 2) bitwise equal to the torch.distributed branch, with the exact
-    collective pattern of a GPU step: 3 all_to_all + 1 Gram all-gather + 3 in-place weight
+    collective pattern of a GPU step: 3 point-to-point exchange groups + 1 Gram all-gather + 3 in-place weight
     all-gathers + 1 all-reduce of the BatchNorm affine parameters."""
     with tempfile.TemporaryDirectory() as d:
         for mode in (0, 1, 2):
@@ -198,7 +200,7 @@ def test_grouped_sharded_flagship_path(world, k):
         assert torch.equal(res[(2, 0)]["flat"], res[(1, 0)]["flat"])     # direct contract == dist branch
         for r in range(world):
             for calls in res[(2, r)]["per_step"]:
-                assert calls == {"all_to_all": 3, "all_gather": 1, "all_gather_inplace": 3, "all_reduce": 1}, calls
+                assert calls == {"exchange": 3, "all_gather": 1, "all_gather_inplace": 3, "all_reduce": 1}, calls
 
 
 def _byzps_worker(rank, world, port, outdir, num_ps):
