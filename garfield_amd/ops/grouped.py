@@ -684,8 +684,8 @@ def _iwgrad_ok(x: torch.Tensor, dy: torch.Tensor) -> bool:
 
 
 def _iwgrad_splits(rows_per_worker: int, tiles: int) -> int:
-    """Pixel splits of the implicit weight gradient: enough workgroups (~1024) to fill the
-    chip, each split at least 256 pixels."""
+    """Pixel splits of the implicit weight gradient: about ``_IWGRAD_WG`` workgroups to fill the
+    chip, each split at least ``_IWGRAD_MINPIX`` pixels."""
     S = 1
     while S < 16 and tiles * S < _IWGRAD_WG and rows_per_worker // (2 * S) >= _IWGRAD_MINPIX:
         S *= 2
@@ -694,8 +694,7 @@ def _iwgrad_splits(rows_per_worker: int, tiles: int) -> int:
 
 def _wgrad3x3_splits(rows_per_worker: int, blocks: int) -> int:
     """Pixel splits of the halo-staged 3x3 weight gradient (one workgroup per (64 co, 64 ci) block,
-    worker and split, all nine taps): enough workgroups to fill the chip twice over (two per CU),
-    each split at least ``_WGRAD3_MINTILES`` 128-pixel tiles."""
+    worker and split, all nine taps): about one workgroup per CU, each split at least ``_WGRAD3_MINTILES`` 128-pixel tiles."""
     tiles = -(-rows_per_worker // 128)
     S = 1
     while S < 64 and blocks * S < _WGRAD3_WG and tiles // (2 * S) >= _WGRAD3_MINTILES:
@@ -703,14 +702,18 @@ def _wgrad3x3_splits(rows_per_worker: int, blocks: int) -> int:
     return S
 
 
-_WGRAD3_WG = 512
+# fewer, larger pixel splits since the split slabs are summed in one deferred pass: the
+# slab traffic (each split writes a [G, cout, K] fp32 slab, read back by the sum) weighs
+# more than the extra workgroups (profiles/r4/splits/: 6.17-6.20 -> 6.11-6.13 ms/step
+# with _IWGRAD_MINPIX 256 -> 512)
+_WGRAD3_WG = 256
 _WGRAD3_MINTILES = 1   # profiles/r3/conv3x3/bench_conv3x3_shapes.log
 
 
 # profiles/iwgrad_split_sweep_r1.log; 512 since the 1x1 layers joined the implicit kernel
 # (profiles/r2/iwgrad_wg_nt_sweep.log)
 _IWGRAD_WG = 512
-_IWGRAD_MINPIX = 256
+_IWGRAD_MINPIX = 512
 
 
 def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int) -> None:
