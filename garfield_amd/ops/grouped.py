@@ -911,6 +911,13 @@ def _f32_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", xshape, add:
     return dx
 
 
+# pixel splits of the fp32 weight gradients: up to ~1024 workgroups (two per CU), each split
+# >= 250 pixels: the measured optimum on the ResNet-50 CIFAR shapes (scripts/bench_conv_f32.py,
+# profiles/r4/bench_conv_f32.log)
+_F32_WGRAD_WG = 1024
+_F32_WGRAD_MINPIX = 250
+
+
 def _f32_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> None:
     """Per-worker fp32 weight gradients straight into the (fp32) exchange rows, or as split
     slabs summed there by the deferred split-K reduction."""
@@ -923,11 +930,9 @@ def _f32_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> N
     K = w.numel() // cout
     rows = dy.shape[0] * dy.shape[2] * dy.shape[3] // G
     tile = 128 if (x.shape[1] % 128 == 0 and cout % 128 == 0) else 64   # conv_f32.hip: the wide form
-    # pixel splits up to ~1024 workgroups (two per CU), each split >= 250 pixels: the measured optimum on
-    # the ResNet-50 CIFAR shapes (scripts/bench_conv_f32.py, profiles/r4/bench_conv_f32.log)
     tiles = -(-K // tile) * (cout // tile) * G
     S = 1
-    while S < 16 and tiles * S < 1024 and rows // (2 * S) >= 250:
+    while S < 16 and tiles * S < _F32_WGRAD_WG and rows // (2 * S) >= _F32_WGRAD_MINPIX:
         S *= 2
     out = spec.sink.rows_view(w, (cout, K), torch.float32) if S == 1 else None
     if out is not None:
