@@ -702,12 +702,13 @@ def _wgrad3x3_splits(rows_per_worker: int, blocks: int) -> int:
     return S
 
 
-# fewer, larger pixel splits since the split slabs are summed in one deferred pass: the
-# slab traffic (each split writes a [G, cout, K] fp32 slab, read back by the sum) weighs
-# more than the extra workgroups (profiles/r4/splits/: 6.17-6.20 -> 6.11-6.13 ms/step
-# with _IWGRAD_MINPIX 256 -> 512)
-_WGRAD3_WG = 256
-_WGRAD3_MINTILES = 1   # profiles/r3/conv3x3/bench_conv3x3_shapes.log
+# at least three 128-pixel tiles per split: on ResNet-50's small 3x3 layers (8x8 and 4x4, 125 and
+# 32 tiles per worker) the slab traffic (each split writes a [G, cout, K] fp32 slab, read back by
+# the deferred sum) weighs more than the extra workgroups; ResNet-18's larger layers keep their
+# splits (profiles/r4/splits/: ResNet-50 6.17-6.20 -> 6.11-6.13 ms/step together with
+# _IWGRAD_MINPIX 256 -> 512; ResNet-18 unchanged, while a 256-workgroup target costs it 0.8 ms)
+_WGRAD3_WG = 512
+_WGRAD3_MINTILES = 3
 
 
 # profiles/iwgrad_split_sweep_r1.log; 512 since the 1x1 layers joined the implicit kernel

@@ -685,6 +685,7 @@ class RobustDataParallel:
                 self._shadow[: self.d].copy_(p)
 
     def _eager_step(self, batches) -> torch.Tensor:
+        self._join()
         with self.timer.phase("compute+exchange"):
             losses = self.compute_local(batches)
         with self.timer.phase("gar_update"):
@@ -724,6 +725,7 @@ class RobustDataParallel:
             self._capture(batches)
             if self._graph is None:
                 return self._eager_step(batches)
+        self._join()
         works = []
         issue = _SlotIssuer(self)
         with self.timer.phase("compute"):
@@ -800,11 +802,34 @@ class RobustDataParallel:
         if (self.device.type == "cuda" and self.cfg.cuda_graph and not self._graph_failed and self.step_count >= 1
                 and self._ggraph is None and getattr(self._gexec, "graph_safe", True)):
             self._capture_grouped()
-        if self._ggraph is not None:
+        if self._shard is not None:   # this step's updates may run beside the next forward's stages
+            self._shard.staged = isinstance(self._ggraph, list)
+        if isinstance(self._ggraph, list):   # staged: each stage waits for the buckets it reads
+            waits = self._shard.stage_waits(self._gexec.stage_ends(self.ld))
+            main = torch.cuda.current_stream(self.device)
+            for g, ev in zip(self._ggraph, waits):
+                if ev is not None:
+                    main.wait_event(ev)
+                g.replay()
+            self._gexec.replayed()
+        elif self._ggraph is not None:
+            self._join()
             self._ggraph.replay()
             self._gexec.replayed()   # the bucket signals captured in the graph fired once more
         else:
+            self._join()
             self._gexec.run(self._gx, self._gy, self._gloss)
+
+    def _staging(self) -> bool:
+        """Whether the grouped step is captured as stages cut at the bucket boundaries (the
+        sharded exchange with its comm stream and stream-ordered collectives, bf16)."""
+        return (self._shard is not None and self._shard.staging_ok() and hasattr(self._gexec, "run_stages")
+                and self._gexec.stageable(self._gx))
+
+    def _join(self) -> None:
+        """The main stream waits for the previous step's buckets still in flight on the comm stream."""
+        if self._shard is not None:
+            self._shard.join()
 
     def _grouped_step(self, batches) -> torch.Tensor:
         self._stage_grouped(batches)
@@ -886,12 +911,26 @@ class RobustDataParallel:
             with torch.cuda.stream(s):  # warm-up on the capture stream (per-stream library state)
                 self._gexec.run(self._gx, self._gy, self._gloss)
             s.synchronize()
-            g = torch.cuda.CUDAGraph()
             mode = "thread_local" if self.world > 1 else "global"
-            with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
-                self._gexec.run(self._gx, self._gy, self._gloss)
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            self._ggraph = g
+            if self._staging():
+                # one graph per stage (shared memory pool), cut at the bucket boundaries of the
+                # forward: the next step's early layers need not wait for the late buckets' updates
+                graphs, pool, stages = [], None, self._gexec.run_stages(self._gx, self._gy, self._gloss)
+                done = False
+                while not done:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode=mode):
+                        done = next(stages, None) is None
+                    graphs.append(g)
+                    pool = g.pool()
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                self._ggraph = graphs
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
+                    self._gexec.run(self._gx, self._gy, self._gloss)
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                self._ggraph = g
         except Exception as e:  # capture unsupported: stay eager
             warning(f"HIP graph capture of the grouped step failed, running eagerly: {e!r}")
             self._graph_failed = True
@@ -984,6 +1023,7 @@ class RobustDataParallel:
 
     @torch.no_grad()
     def evaluate(self, batches, binary: bool = False) -> float:
+        self._join()
         self.model.eval()
         correct = total = 0
         amp = (torch.autocast("cuda", dtype=self.cfg.autocast_dtype)

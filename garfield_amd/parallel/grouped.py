@@ -143,6 +143,14 @@ class GroupedResNet:
         return self._conv_bn(out, last_conv, last_bn, True, res=sc)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        out = []
+        for _ in self._forward_stages(x, out):
+            pass
+        return out[0]
+
+    def _forward_stages(self, x: torch.Tensor, out: list):
+        """The forward, yielding before each marked layer (a bucket boundary): the stage
+        that follows reads that bucket's weights first. The logits land in ``out``."""
         m = self.model
         # small layers' running statistics: one batched launch after the last BatchNorm
         self.ws.defer_running = x.is_cuda
@@ -153,10 +161,31 @@ class GroupedResNet:
         for name in ("layer1", "layer2", "layer3", "layer4"):
             if self._events is not None and name in self._events:
                 x = _BucketMark.apply(x, self._events[name], self.sink)
+            if name in self.marks:
+                yield name
             for blk in getattr(m, name):
                 x = self._block(blk, x)
         self.ws.flush_running()
-        return grouped_linear(global_avgpool(x), self.fc)
+        out.append(grouped_linear(global_avgpool(x), self.fc))
+
+    def stage_ends(self, ld: int) -> list:
+        """Flat offset where the parameters each stage of ``run_stages`` reads end: the
+        stages cut at the marked layers, in forward order; the last one (the rest of the
+        forward and the whole backward, which writes every gradient row) ends at ``ld``."""
+        offs = []
+        for name in ("layer1", "layer2", "layer3", "layer4"):
+            if name in self.marks:
+                layer = getattr(self.model, name)
+                o = [self._offsets[id(p)] for p in layer.parameters() if id(p) in self._offsets]
+                if o:
+                    offs.append(min(o))
+        return [*offs, ld]
+
+    def stageable(self, x: torch.Tensor) -> bool:
+        """Whether ``run_stages``' stages read only their own bucket's weights: the bf16 step
+        (its backward's transposed 1x1 weights are refreshed after the forward); the fp32
+        step splits every weight into bf16 pieces before the forward."""
+        return bool(self.marks) and x.is_cuda and x.dtype != torch.float32
 
     def losses(self, logits: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         G = self.groups
@@ -169,13 +198,24 @@ class GroupedResNet:
         return torch.stack([self.loss_fn(lg[g], yg[g]) for g in range(G)])
 
     def run(self, x: torch.Tensor, y: torch.Tensor, loss_out: torch.Tensor | None = None) -> torch.Tensor:
+        for _ in self.run_stages(x, y, loss_out):
+            pass
+        return self._per
+
+    def run_stages(self, x: torch.Tensor, y: torch.Tensor, loss_out: torch.Tensor | None = None):
+        """``run`` cut into stages at the marked layers (a generator: it yields between stages).
+        The engine captures each stage as its own HIP graph, so the next step's stem-to-layer2
+        forward can start while the later buckets' updates and weight all-gathers still run
+        on the comm stream (each later stage waits for its bucket's event)."""
         if x.shape[0] % self.groups:
             raise ValueError(f"batch of {x.shape[0]} rows is not divisible into {self.groups} workers")
         if x.is_cuda and x.dtype == torch.float32:
             refresh_f32_weights(self.conv.values())     # the fp32 step's split weights: one launch
-        elif x.is_cuda:
-            refresh_dgrad_weights(self.conv.values())   # Wᵀ of every 1x1 layer: one launch
-        per = self.losses(self.forward(x), y)
+        out = []
+        yield from self._forward_stages(x, out)
+        if x.is_cuda and x.dtype != torch.float32:
+            refresh_dgrad_weights(self.conv.values())   # the backward's Wᵀ of every 1x1 layer: one launch
+        per = self.losses(out[0], y)
         # d(Σ_g loss_g)/d loss_g = 1: seeded directly (no sum / fill / expand kernels)
         if self._seed is None or self._seed.shape != per.shape or self._seed.device != per.device \
                 or self._seed.dtype != per.dtype:
@@ -187,7 +227,7 @@ class GroupedResNet:
         per = per.detach()
         if loss_out is not None:
             loss_out.copy_(per)
-        return per
+        self._per = per
 
 
 class _BucketMark(torch.autograd.Function):

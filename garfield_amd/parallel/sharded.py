@@ -147,6 +147,9 @@ class ShardedAggregator:
         self._ws = {}
         self._started = False
         self._gathers: list = []
+        self._scatters: list = []
+        self._ready: list = []      # (bucket lo, event) of buckets finished on the comm stream
+        self.staged = False         # the engine replays the next forward in bucket stages
         self.master_stale = False
         self._init_fp32_sync()
 
@@ -184,9 +187,11 @@ class ShardedAggregator:
 
     def _init_fp32_sync(self) -> None:
         """fp32 parameters the forward reads directly (not mirrored by the bf16 working
-        weights): their owned values travel in one all-reduce of a compact vector."""
+        weights): per bucket, their owned values travel in one all-reduce of a compact
+        vector right after the bucket's weight all-gather."""
         e = self.e
-        self._np_idx = None
+        for b in self.buckets:
+            b.np = None
         if e._shadow is None or self.world == 1:
             return
         lp = e.shadow_param_ids()
@@ -200,10 +205,12 @@ class ShardedAggregator:
         own = torch.zeros(e.ld, dtype=torch.bool)
         for b in self.buckets:
             own[b.own] = True
-        self._np_idx = gidx.to(e.device)
-        self._np_own_pos = torch.nonzero(own[gidx]).flatten().to(e.device)
-        self._np_own_idx = gidx[own[gidx]].to(e.device)
-        self._np_buf = torch.zeros(gidx.numel(), dtype=torch.float32, device=e.device)
+        for b in self.buckets:
+            bidx = gidx[(gidx >= b.lo) & (gidx < b.hi)]
+            if bidx.numel() == 0:
+                continue
+            b.np = (bidx.to(e.device), torch.nonzero(own[bidx]).flatten().to(e.device),
+                    bidx[own[bidx]].to(e.device), torch.zeros(bidx.numel(), dtype=torch.float32, device=e.device))
 
     # ------------------------------------------------------------------ #
     # exchange
@@ -316,55 +323,119 @@ class ShardedAggregator:
         self._started = False
         self._finish_gathers()
 
-    def _gather_bucket(self, b: _Bucket) -> None:
+    def _gather_bucket(self, b: _Bucket, handoff: bool = True) -> None:
         """Start the all-gather of bucket b's updated parameters (the bf16 working weights
         when the forward reads those, else the fp32 master) as soon as its update is
-        queued: on RCCL it runs beside the remaining buckets' updates."""
+        queued, then the compact all-reduce of the bucket's fp32 parameters the forward
+        reads directly (BatchNorm affine): on RCCL it runs beside the remaining buckets'
+        updates. ``handoff=False``: the update was issued on the comm stream itself."""
         e = self.e
         if self.world == 1:
             return
         buf = e._shadow if e._shadow is not None else e.flat.data
         full, mine = buf[b.lo:b.hi], buf[b.own]
-        with self._on_comm():
+        ctx = self._on_comm() if handoff else torch.cuda.stream(self._comm_stream)
+        with ctx:
             if self._rccl is not None:   # in place: this rank's block is its own shard
                 self._rccl.all_gather(mine, full, self._comm_stream)
             else:
                 if gloo_backend():
                     mine = mine.clone()  # gloo rejects an input aliasing the output
                 self._gathers.append(dist.all_gather_into_tensor(full, mine, async_op=True))
+            if b.np is not None:
+                idx, own_pos, own_idx, nb = b.np
+                nb.zero_()
+                nb[own_pos] = e.flat.data[own_idx]
+                if self._rccl is not None:   # stream-ordered: scattered back on the comm stream
+                    self._rccl.all_reduce_sum(nb, self._comm_stream)
+                    e.flat.data[idx] = nb
+                else:
+                    self._gathers.append(dist.all_reduce(nb, async_op=True))
+                    self._scatters.append(b)
 
     def _finish_gathers(self) -> None:
-        """Wait (stream-ordered on RCCL) for the weight all-gathers, then exchange the compact
-        fp32 parameters the forward reads directly (BatchNorm affine) in one all-reduce."""
+        """Wait for the weight all-gathers and compact all-reduces: stream-ordered on RCCL
+        (the main stream waits for the comm stream, or, with the next forward staged, each
+        stage waits for its buckets' events: ``stage_waits``), host-side for torch.distributed."""
         e = self.e
         if self.world == 1:
             if e._shadow is not None and e.device.type != "cuda":
                 with torch.no_grad():
                     e._shadow.copy_(e.flat.data)
             return
-        if e._shadow is not None and self._np_idx is not None:
-            nb = self._np_buf
-            nb.zero_()
-            nb[self._np_own_pos] = e.flat.data[self._np_own_idx]
-            with self._on_comm():
-                if self._rccl is not None:
-                    self._rccl.all_reduce_sum(nb, self._comm_stream)
-                else:
-                    self._gathers.append(dist.all_reduce(nb, async_op=True))
         for w in self._gathers:
             w.wait()
         self._gathers = []
-        self._back_to_main()
+        for b in self._scatters:
+            idx, _, _, nb = b.np
+            e.flat.data[idx] = nb
+        self._scatters = []
+        if not self._ready:
+            self._back_to_main()
         if e._shadow is not None:
             self.master_stale = True
-            if self._np_idx is not None:
-                e.flat.data[self._np_idx] = self._np_buf
+
+    # ------------------------------------------------------------------ #
+    # the next step's forward, staged at the bucket boundaries
+
+    def staging_ok(self) -> bool:
+        """Whether the updates can run beside the next forward: a comm stream, and every
+        collective stream-ordered on it (the direct RCCL path, or nothing to exchange)."""
+        return self._comm_stream is not None and (self.world == 1 or self._rccl is not None)
+
+    def _update_buckets(self, fn) -> None:
+        """``fn(b)`` issues bucket b's update; buckets in update order (low coordinates first).
+        With the next forward staged (``self.staged``), the first bucket's update stays on the
+        main stream and the others run on the comm stream (one device-side hand-off), each
+        bucket followed by its weight all-gather and an event (``self._ready``) that the next
+        forward's stage reading it waits on: the stem-to-layer2 forward runs while the
+        layer3/layer4 updates and all-gathers are still in flight."""
+        order = self._update_order()
+        staged = self.staged and self.staging_ok()
+        for i, b in enumerate(order):
+            if staged and i > 0:
+                if i == 1:
+                    self._handoff.to_comm(torch.cuda.current_stream(self.e.device), self._comm_stream)
+                with torch.cuda.stream(self._comm_stream):
+                    fn(b)
+                self._gather_bucket(b, handoff=False)
+            else:
+                fn(b)
+                self._gather_bucket(b)
+            if staged and (i > 0 or self.world > 1):
+                ev = torch.cuda.Event(enable_timing=_TIMING)
+                ev.record(self._comm_stream)
+                self._ready.append((b.lo, ev))
+
+    def stage_waits(self, ends: list) -> list:
+        """For each stage of the next forward (``ends[i]``: where the parameters it reads end),
+        the event it must wait on (None: nothing pending): the last comm-stream bucket that
+        starts below that end (the comm stream finishes buckets in coordinate order)."""
+        out = []
+        for hi in ends:
+            ev = None
+            for lo, e in self._ready:
+                if lo < hi:
+                    ev = e
+            out.append(ev)
+        self._ready = []
+        return out
+
+    def join(self) -> None:
+        """The main stream waits for every pending bucket (a step that is not staged, or any
+        reader of the parameters)."""
+        if self._ready:
+            main = torch.cuda.current_stream(self.e.device)
+            for _, ev in self._ready:
+                main.wait_event(ev)
+            self._ready = []
 
     def quiesce(self) -> None:
         """Order torch.distributed collectives issued next after this aggregator's direct
         ones (same communicator): the main stream waits for the comm stream."""
         if self._comm_stream is not None:
             torch.cuda.current_stream(self.e.device).wait_stream(self._comm_stream)
+        self._ready = []
 
     def sync_master(self) -> None:
         """Collective: refresh the fp32 master outside this rank's shards (checkpoints,
@@ -432,26 +503,26 @@ class ShardedAggregator:
                 w = self._select(C, total, rule, f, cfg)
             if rule != "bulyan":
                 e.last_weights = w
-                for b in self._update_order():
+
+                def combine(b):
                     p, mom, sh = self._param(b)
                     C.gpu_combine_sgd(b.rows, w, p, mom, None, sh, *args)
-                    self._gather_bucket(b)
+                self._update_buckets(combine)
                 return
             t = n - 2 * f - 2
-            for b in self._update_order():
+
+            def tail(b):
                 g = self._gagg(b)
                 C.gpu_coordwise(b.rows, modes["bulyan-tail"], f, t - 2 * f, w, t, 0, 1.0, g)
                 p, mom, sh = self._param(b)
                 C.gpu_combine_sgd([g], self._one, p, mom, None, sh, *args)
-                self._gather_bucket(b)
+            self._update_buckets(tail)
             return
-        for b in self.buckets:
+        if rule == "average":
+            e.last_weights = self._avg
+        for b in self.buckets:   # coordinate-wise aggregation as the buckets land
             self._wait(b)
-            p, mom, sh = self._param(b)
             if rule == "average":
-                e.last_weights = self._avg
-                C.gpu_combine_sgd(b.rows, self._avg, p, mom, None, sh, *args)
-                self._gather_bucket(b)
                 continue
             g = self._gagg(b)
             if rule == "median":
@@ -467,8 +538,14 @@ class ShardedAggregator:
                                 float(kw.get("p", 0.9)), g)
             else:
                 raise ValueError(f"sharded aggregation does not support {rule!r}")
-            C.gpu_combine_sgd([g], self._one, p, mom, None, sh, *args)
-            self._gather_bucket(b)
+
+        def update(b):
+            p, mom, sh = self._param(b)
+            if rule == "average":
+                C.gpu_combine_sgd(b.rows, self._avg, p, mom, None, sh, *args)
+            else:
+                C.gpu_combine_sgd([self._gagg(b)], self._one, p, mom, None, sh, *args)
+        self._update_buckets(update)
 
     def _matrix(self, b: _Bucket) -> torch.Tensor:
         """Bucket b's received shards as ONE [n, S] matrix (row src * k + j: the receive
@@ -834,6 +911,7 @@ class ShardedAggregator:
         return out
 
     def load_momentum(self, full: torch.Tensor) -> None:
+        self.quiesce()
         e = self.e
         for b in self.buckets:
             e.mom[b.moff:b.moff + b.S].copy_(full[b.own])

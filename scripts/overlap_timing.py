@@ -6,7 +6,9 @@ Runs the bench configuration with ``--shard-gar`` on one GPU and the loopback ex
 all-to-all would move it), and reads HIP timing events: the step start, the end of the
 grouped forward/backward graph (main stream) and the moment each bucket's exchange
 finished on the comm stream. A bucket whose exchange finished before the graph ended
-ran under the backward.
+ran under the backward. With the forward staged at the bucket boundaries (the default
+with a comm stream), it also reports when the previous step's layer3 / layer4+fc updates
+ended relative to this step's forward start: positive = they ran beside the forward.
 
     GARFIELD_OVERLAP=1 python scripts/overlap_timing.py [--steps 5]
 """
@@ -51,6 +53,8 @@ def main():
     def timed_compute():
         s0 = torch.cuda.Event(enable_timing=True)
         s1 = torch.cuda.Event(enable_timing=True)
+        # the previous step's buckets still in flight on the comm stream (staged forward)
+        marks["prev_ready"] = list(eng._shard._ready) if eng._shard is not None else []
         s0.record()
         inner()
         s1.record()
@@ -72,6 +76,10 @@ def main():
         if eng._shard is not None:
             rec["bucket_done_ms"] = [round(t0.elapsed_time(b.done), 3) for b in eng._shard.buckets]
             rec["bucket_params"] = [b.hi - b.lo for b in eng._shard.buckets]
+            # > 0: the previous step's update of that bucket ended AFTER this step's forward started
+            rec["prev_update_end_vs_forward_start_ms"] = {lo: round(t0.elapsed_time(ev), 3)
+                                                          for lo, ev in marks["prev_ready"]}
+            rec["staged_graphs"] = len(eng._ggraph) if isinstance(eng._ggraph, list) else 0
         out.append(rec)
     print(json.dumps({"overlap_env": os.environ.get("GARFIELD_OVERLAP", ""), "steps": out}), flush=True)
 

@@ -165,11 +165,14 @@ def test_cuda_graph_never_writes_loader_tensors(cuda):
 @pytest.mark.parametrize("rule,f,overlap", [("krum", 2, "1"), ("median", 1, "1"), ("bulyan", 1, "1"),
                                             ("krum", 2, "0")])
 def test_bucketed_exchange_overlap_loopback(cuda, rule, f, overlap, monkeypatch):
-    """Sharded aggregation with layer buckets on one rank, the exchange emulated by
-    copies on the side stream (GARFIELD_LOOPBACK_EXCHANGE=1) that start when the
-    HIP-graph backward records each bucket's event: fresh inputs every step, so a
-    copy that ran before its bucket was written would read the previous step's
-    gradients. Must equal the redundant (unsharded) path."""
+    """Sharded aggregation with layer buckets on one rank and the exchange machinery of a
+    multi-rank step (GARFIELD_LOOPBACK_EXCHANGE=1: comm stream, bucket signals recorded by
+    the HIP-graph backward, per-bucket events), with the next forward replayed as three
+    graphs cut at the bucket boundaries: the layer3/layer4 updates run on the comm stream
+    beside the next step's stem-to-layer2 stage, and each later stage waits for its bucket.
+    Fresh inputs every step, so a stage that ran before its weights were updated, or an
+    update that read rows the next backward had already overwritten, would change the
+    result. Must equal the redundant (unsharded) path."""
     monkeypatch.setenv("GARFIELD_LOOPBACK_EXCHANGE", "1")
     monkeypatch.setenv("GARFIELD_OVERLAP", overlap)     # in-graph bucket signals, or after the backward
     outs = []
@@ -186,7 +189,7 @@ def test_bucketed_exchange_overlap_loopback(cuda, rule, f, overlap, monkeypatch)
             eng.step(b)
         torch.cuda.synchronize()
         if shard:
-            assert eng._ggraph is not None
+            assert isinstance(eng._ggraph, list) and len(eng._ggraph) == 3 and eng._shard.staged
         outs.append(eng.flat.reference_vector().clone())
     rel = ((outs[1] - outs[0]).norm() / outs[0].norm()).item()
     assert rel < 1e-5, rel

@@ -180,7 +180,7 @@ def test_grouped_sharded_flagship_path(world, k):
     ranks x workers: replicas identical, sharded == redundant, 3 all_to_all per step; the
     direct-RCCL contract (mode 2) bitwise equal to the torch.distributed branch, with the exact
     collective pattern of a GPU step: 3 point-to-point exchange groups + 1 Gram all-gather + 3 in-place weight
-    all-gathers + 1 all-reduce of the BatchNorm affine parameters."""
+    all-gathers + 1 all-reduce per bucket of its BatchNorm affine parameters."""
     with tempfile.TemporaryDirectory() as d:
         for mode in (0, 1, 2):
             mp.spawn(_grouped_worker, args=(world, free_port(), d, mode, k), nprocs=world, join=True)
@@ -200,7 +200,7 @@ def test_grouped_sharded_flagship_path(world, k):
         assert torch.equal(res[(2, 0)]["flat"], res[(1, 0)]["flat"])     # direct contract == dist branch
         for r in range(world):
             for calls in res[(2, r)]["per_step"]:
-                assert calls == {"exchange": 3, "all_gather": 1, "all_gather_inplace": 3, "all_reduce": 1}, calls
+                assert calls == {"exchange": 3, "all_gather": 1, "all_gather_inplace": 3, "all_reduce": 3}, calls
 
 
 def _byzps_worker(rank, world, port, outdir, num_ps):
