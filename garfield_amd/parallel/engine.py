@@ -59,6 +59,9 @@ LW_JOB = 32768   # coordinates per job of the segmented kernels (a multiple of 8
 # NHWC executor on the fp32 kernels (conv_f32.hip, split-bf16 MFMA; bn_nhwc.hip in fp32), "channel" the
 # grouped-channel executor on ATen / hipBLASLt (parallel/grouped_fp32.py), "0" the per-worker path.
 FP32_GROUPED = os.environ.get("GARFIELD_FP32_GROUPED", "1")
+# sharded steps with a comm stream: the grouped step captured as stages cut at the bucket boundaries,
+# so the next forward's early layers run beside the late buckets' updates / all-gathers ("0": one graph)
+STAGE_FORWARD = os.environ.get("GARFIELD_STAGE_FORWARD", "1") != "0"
 
 
 @dataclass
@@ -823,8 +826,8 @@ class RobustDataParallel:
     def _staging(self) -> bool:
         """Whether the grouped step is captured as stages cut at the bucket boundaries (the
         sharded exchange with its comm stream and stream-ordered collectives, bf16)."""
-        return (self._shard is not None and self._shard.staging_ok() and hasattr(self._gexec, "run_stages")
-                and self._gexec.stageable(self._gx))
+        return (STAGE_FORWARD and self._shard is not None and self._shard.staging_ok()
+                and hasattr(self._gexec, "run_stages") and self._gexec.stageable(self._gx))
 
     def _join(self) -> None:
         """The main stream waits for the previous step's buckets still in flight on the comm stream."""

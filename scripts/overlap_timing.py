@@ -64,21 +64,28 @@ def main():
     for _ in range(4):
         eng.step(feed.next())
     torch.cuda.synchronize()
-    out = []
+    # a.steps steps back to back (no host sync in between, as in training), events kept per step
+    rounds = []
     for _ in range(a.steps):
         eng.step(feed.next())
         end = torch.cuda.Event(enable_timing=True)
         end.record()
-        torch.cuda.synchronize()
-        t0 = marks["start"]
-        rec = {"graph_end_ms": round(t0.elapsed_time(marks["graph_end"]), 3),
+        rounds.append((dict(marks), end, [b.done for b in eng._shard.buckets] if eng._shard is not None else []))
+        if eng._shard is not None:   # the bucket events are re-created every step: keep this step's
+            for b in eng._shard.buckets:
+                b.done = None
+    torch.cuda.synchronize()
+    out = []
+    for mk, end, dones in rounds:
+        t0 = mk["start"]
+        rec = {"graph_end_ms": round(t0.elapsed_time(mk["graph_end"]), 3),
                "step_end_ms": round(t0.elapsed_time(end), 3)}
         if eng._shard is not None:
-            rec["bucket_done_ms"] = [round(t0.elapsed_time(b.done), 3) for b in eng._shard.buckets]
+            rec["bucket_done_ms"] = [round(t0.elapsed_time(d), 3) for d in dones if d is not None]
             rec["bucket_params"] = [b.hi - b.lo for b in eng._shard.buckets]
             # > 0: the previous step's update of that bucket ended AFTER this step's forward started
             rec["prev_update_end_vs_forward_start_ms"] = {lo: round(t0.elapsed_time(ev), 3)
-                                                          for lo, ev in marks["prev_ready"]}
+                                                          for lo, ev in mk["prev_ready"]}
             rec["staged_graphs"] = len(eng._ggraph) if isinstance(eng._ggraph, list) else 0
         out.append(rec)
     print(json.dumps({"overlap_env": os.environ.get("GARFIELD_OVERLAP", ""), "steps": out}), flush=True)
