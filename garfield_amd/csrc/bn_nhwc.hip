@@ -313,6 +313,11 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
   if (tr >= rp) return;
   const int nv = C / 8;
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * rp * kApplyIters;
+  // one channel group per thread (C <= 8 * tch): its scale / shift are loaded once per worker
+  // instead of once per row (they were 4x the row's own bytes in load instructions)
+  const bool fixed = nv <= tch;
+  int gl = -1;
+  float sc[8], sf[8];
 #pragma unroll
   for (int it = 0; it < kApplyIters; ++it) {
     const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
@@ -321,10 +326,13 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
     for (int v = threadIdx.x % tch; v < nv; v += tch) {
       const int c = v * 8;
       const int64_t off = row * C + c;
-      float a[8], sc[8], sf[8];
+      float a[8];
       load8<DT>(x, off, a);
-      load8f(scale + static_cast<int64_t>(g) * C + c, sc);
-      load8f(shift + static_cast<int64_t>(g) * C + c, sf);
+      if (!fixed || g != gl) {
+        load8f(scale + static_cast<int64_t>(g) * C + c, sc);
+        load8f(shift + static_cast<int64_t>(g) * C + c, sf);
+        gl = g;
+      }
       float o[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = a[i] * sc[i] + sf[i];
@@ -389,6 +397,9 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const void* __restrict__
   if (tr >= rp) return;
   const int nv = C / 8;
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * rp * kApplyIters;
+  const bool fixed = nv <= tch;   // one channel group per thread: coefficients once per worker
+  int gl = -1;
+  float mu[8], ca[8], cb[8], cc[8];
 #pragma unroll
   for (int it = 0; it < kApplyIters; ++it) {
     const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
@@ -398,7 +409,7 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const void* __restrict__
     for (int v = threadIdx.x % tch; v < nv; v += tch) {
       const int c = v * 8;
       const int64_t off = row * C + c;
-      float a[8], d[8], mu[8], ca[8], cb[8], cc[8];
+      float a[8], d[8];
       load8<DT>(x, off, a);
       load8<DT>(dy, off, d);
       if constexpr (RM == 1) {
@@ -411,10 +422,13 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const void* __restrict__
 #pragma unroll
         for (int i = 0; i < 8; ++i) d[i] = (mb >> i) & 1u ? d[i] : 0.f;
       }
-      load8f(mean + static_cast<int64_t>(g) * C + c, mu);
-      load8f(cg + c, ca);
-      load8f(cg + C + c, cb);
-      load8f(cg + 2 * C + c, cc);
+      if (!fixed || g != gl) {
+        load8f(mean + static_cast<int64_t>(g) * C + c, mu);
+        load8f(cg + c, ca);
+        load8f(cg + C + c, cb);
+        load8f(cg + 2 * C + c, cc);
+        gl = g;
+      }
       float o[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = ca[i] * (d[i] - cb[i] - (a[i] - mu[i]) * cc[i]);
