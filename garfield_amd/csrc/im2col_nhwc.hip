@@ -189,10 +189,11 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_fwd(const void* __restrict
                                                          void* __restrict__ y, uint8_t* __restrict__ idx) {
   const int cv = g.C / 8;
   const int64_t total = static_cast<int64_t>(g.N) * g.Ho * g.Wo * cv;
+  const bool narrow = total <= 0x7fffffff;   // 32-bit index math (the 64-bit divisions dominated)
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
        t += static_cast<int64_t>(gridDim.x) * kThreads) {
-    const int v = static_cast<int>(t % cv);
-    const int m = static_cast<int>(t / cv);
+    const int v = narrow ? static_cast<int>(t) % cv : static_cast<int>(t % cv);
+    const int m = narrow ? static_cast<int>(t) / cv : static_cast<int>(t / cv);
     const int wo = m % g.Wo;
     const int ho = (m / g.Wo) % g.Ho;
     const int n = m / (g.Wo * g.Ho);
@@ -229,29 +230,46 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_bwd(const void* __restrict
                                                          void* __restrict__ dx) {
   const int cv = g.C / 8;
   const int64_t total = static_cast<int64_t>(g.N) * g.H * g.W * cv;
+  const bool narrow = total <= 0x7fffffff;
+  // undilated windows: only the output rows / columns whose window covers (hi, wi) are visited
+  // (1-4 of the 9 taps of a 3x3 / 2 pool), in the generic loop's (i, j) order
+  const bool unit = g.dh == 1 && g.dw == 1;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
        t += static_cast<int64_t>(gridDim.x) * kThreads) {
-    const int v = static_cast<int>(t % cv);
-    const int pix = static_cast<int>(t / cv);
+    const int v = narrow ? static_cast<int>(t) % cv : static_cast<int>(t % cv);
+    const int pix = narrow ? static_cast<int>(t) / cv : static_cast<int>(t / cv);
     const int wi = pix % g.W;
     const int hi = (pix / g.W) % g.H;
     const int n = pix / (g.W * g.H);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < g.KH; ++i) {
-      for (int j = 0; j < g.KW; ++j) {
-        const int m = tap_row(g, n, hi, wi, i, j);
-        if (m < 0) continue;
-        const int64_t o = static_cast<int64_t>(m) * g.C + v * 8;
-        const uint2 p = *reinterpret_cast<const uint2*>(idx + o);
-        const int tap = i * g.KW + j;
-        float d[8];
-        load_vec<DT, 8>(dy, o, d);
+    auto take = [&](int m, int tap) {
+      const int64_t o = static_cast<int64_t>(m) * g.C + v * 8;
+      const uint2 p = *reinterpret_cast<const uint2*>(idx + o);
+      float d[8];
+      load_vec<DT, 8>(dy, o, d);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t word = e < 4 ? p.x : p.y;
-          if (static_cast<int>((word >> (8 * (e & 3))) & 0xffu) == tap) acc[e] += d[e];
-        }
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t word = e < 4 ? p.x : p.y;
+        if (static_cast<int>((word >> (8 * (e & 3))) & 0xffu) == tap) acc[e] += d[e];
       }
+    };
+    if (unit) {
+      // window (ho, wo) covers hi iff i = hi + ph - ho*sh lies in [0, KH)
+      const int ah = hi + g.ph, aw = wi + g.pw;
+      int ho1 = ah / g.sh, wo1 = aw / g.sw;
+      if (ho1 > g.Ho - 1) ho1 = g.Ho - 1;
+      if (wo1 > g.Wo - 1) wo1 = g.Wo - 1;
+      const int lh = ah - g.KH + 1, lw = aw - g.KW + 1;
+      const int ho0 = lh <= 0 ? 0 : (lh + g.sh - 1) / g.sh, wo0 = lw <= 0 ? 0 : (lw + g.sw - 1) / g.sw;
+      for (int ho = ho1; ho >= ho0; --ho)          // i ascending
+        for (int wo = wo1; wo >= wo0; --wo)        // j ascending
+          take((n * g.Ho + ho) * g.Wo + wo, (ah - ho * g.sh) * g.KW + (aw - wo * g.sw));
+    } else {
+      for (int i = 0; i < g.KH; ++i)
+        for (int j = 0; j < g.KW; ++j) {
+          const int m = tap_row(g, n, hi, wi, i, j);
+          if (m >= 0) take(m, i * g.KW + j);
+        }
     }
     store_vec<8>(dx, DT, static_cast<int64_t>(pix) * g.C + v * 8, acc);
   }

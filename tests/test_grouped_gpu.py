@@ -330,7 +330,8 @@ def test_iconv_dgrad_matches_autograd(cuda, native):
         assert rel(add.float(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("N,C,H,k,s,p", [(4, 64, 16, 3, 2, 1), (3, 8, 7, 2, 2, 0), (2, 16, 9, 3, 1, 1)])
+@pytest.mark.parametrize("N,C,H,k,s,p", [(4, 64, 16, 3, 2, 1), (3, 8, 7, 2, 2, 0), (2, 16, 9, 3, 1, 1), (2, 64, 112, 3, 2, 1),
+                                          (2, 8, 15, 3, 2, 1)])
 def test_maxpool_matches_aten(cuda, N, C, H, k, s, p):
     from garfield_amd.ops.grouped import grouped_maxpool
 
