@@ -7,7 +7,7 @@
 // for the weight gradient (~170 us forward + ~57 us weight-gradient GEMM per step,
 // profiles/r3). Here nothing but the input and the output touch HBM:
 //
-// * forward: a workgroup owns 128 consecutive output pixels of one image. It stages
+// * forward: a workgroup owns 256 (bf16; split: 128) consecutive output pixels of one image. It stages
 //   the input rows they read (zero-padded borders) and the [64][160] weight matrix
 //   (K = 7*7*3 = 147 padded to 5 k-steps of 32) in LDS; v_mfma_f32_16x16x32_bf16
 //   with the WEIGHT as the A operand (D's lane = 4 consecutive output channels of
@@ -37,7 +37,10 @@ namespace {
 constexpr int kC = 3, kKH = 7, kKW = 7, kS = 2, kP = 3, kCout = 64;
 constexpr int kK = kKH * kKW * kC;        // 147
 constexpr int kKP = 160;                   // padded to 5 k-steps of 32
-constexpr int kTile = 128;                 // output pixels per forward workgroup
+// output pixels per forward workgroup: 64 * F (F 16-pixel fragments per wave); bf16 takes F = 4
+// (a 256-pixel tile stages its input rows and the weights once per ~2.3 ImageNet output rows:
+// 3.38 -> 2.52 ms per ImageNet step), the split form F = 2 (three pieces of every operand in registers)
+constexpr int kFwdFragBf16 = 4, kFwdFragSplit = 2;
 constexpr int kThreads = 256;
 constexpr int kMaxPatch = 24576;           // elements of staged input per workgroup (bf16)
 constexpr int kMaxPatchSplit = 16384;      // ... per piece array of the split (fp32) form
@@ -128,7 +131,7 @@ __device__ __forceinline__ f32x4 mma6(const bf16x8 (&a)[kNP], const bf16x8 (&b)[
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
 }
 
-template <bool SPLIT>
+template <bool SPLIT, int F>
 __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ x, const uint16_t* __restrict__ w,
                                                        StemGeo g, void* __restrict__ y) {
   // LDS (dynamic, sized by the host for this geometry): weights [64][160] (x3 split) | staged
@@ -136,6 +139,7 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   constexpr int NP = SPLIT ? kNP : 1;
   uint16_t* wl = lds;
+  constexpr int kTile = 64 * F;
   const int tiles = (g.Ho * g.Wo + kTile - 1) / kTile;
   const int n = blockIdx.x / tiles;
   const int p0 = (blockIdx.x - n * tiles) * kTile;
@@ -156,18 +160,18 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  // this wave's pixels: [wave * 32, wave * 32 + 32) of the tile, two 16-pixel fragments
-  int pbase[2];
+  // this wave's pixels: [wave * 16F, wave * 16F + 16F) of the tile, F 16-pixel fragments
+  int pbase[F];
 #pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    int p = p0 + wave * 32 + f * 16 + fr;
+  for (int f = 0; f < F; ++f) {
+    int p = p0 + wave * 16 * F + f * 16 + fr;
     if (p > p0 + npix - 1) p = p0 + npix - 1;   // clamp: computed, never stored
     const int oy = p / g.Wo, ox = p - oy * g.Wo;
     pbase[f] = ((oy * kS - kP - iy0) * g.pw + ox * kS) * kC;
   }
-  f32x4 acc[2][4];
+  f32x4 acc[F][4];
 #pragma unroll
-  for (int f = 0; f < 2; ++f)
+  for (int f = 0; f < F; ++f)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[f][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -176,9 +180,9 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
     int off[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) off[j] = tap_offset(kb + j, g.pw, zero);
-    bf16x8 bx[2][NP];
+    bf16x8 bx[F][NP];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < F; ++f) {
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         uint16_t vh[8];
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
 #pragma unroll
       for (int i = 0; i < NP; ++i) aw[i] = *reinterpret_cast<const bf16x8*>(wl + i * kCout * kKP + (c * 16 + fr) * kKP + kb);
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
+      for (int f = 0; f < F; ++f) {
         if constexpr (SPLIT) acc[f][c] = mma6(aw, bx[f], acc[f][c]);
         else acc[f][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], bx[f][0], acc[f][c], 0, 0, 0);
       }
@@ -204,8 +208,8 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
   if constexpr (SPLIT) {
     float* tile = reinterpret_cast<float*>(lds);
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const int pl = wave * 32 + f * 16 + fr;
+    for (int f = 0; f < F; ++f) {
+      const int pl = wave * 16 * F + f * 16 + fr;
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         *reinterpret_cast<float4*>(tile + pl * kCout + c * 16 + fq * 4) =
@@ -218,8 +222,8 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
   } else {
     uint16_t* tile = lds;
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const int pl = wave * 32 + f * 16 + fr;
+    for (int f = 0; f < F; ++f) {
+      const int pl = wave * 16 * F + f * 16 + fr;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         uint2 o;
@@ -364,7 +368,7 @@ StemGeo geo(int N, int H, int W, bool split = false) {
   return g;
 }
 
-int fwd_rows(const StemGeo& g) { return ((kTile + g.Wo - 1) / g.Wo) * kS + kKH; }   // max staged rows per tile
+int fwd_rows(const StemGeo& g, int tile) { return ((tile + g.Wo - 1) / g.Wo) * kS + kKH; }   // max staged rows per tile
 
 template <class K>
 void allow_lds(K kernel, size_t bytes) {
@@ -378,21 +382,24 @@ void allow_lds(K kernel, size_t bytes) {
 bool stem_supported(int H, int W) {
   if (H <= 0 || W <= 0) return false;
   const StemGeo g = geo(1, H, W), gs = geo(1, H, W, true);
-  return fwd_rows(g) * g.pw * kC < kMaxPatchSplit && g.band >= 1 && gs.band >= 1;
+  return fwd_rows(g, 64 * kFwdFragBf16) * g.pw * kC < kMaxPatch && fwd_rows(g, 64 * kFwdFragSplit) * g.pw * kC < kMaxPatchSplit &&
+         g.band >= 1 && gs.band >= 1;
 }
 
 void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream) {
   const StemGeo g = geo(N, H, W, split);
-  const int tiles = (g.Ho * g.Wo + kTile - 1) / kTile;
+  const int T = 64 * (split ? kFwdFragSplit : kFwdFragBf16);
+  const int tiles = (g.Ho * g.Wo + T - 1) / T;
   const int np = split ? kNP : 1;
-  size_t lds = (static_cast<size_t>(np) * kCout * kKP + np * (static_cast<size_t>(fwd_rows(g)) * g.pw * kC + 8)) * 2;
-  const size_t tile = static_cast<size_t>(kTile) * kCout * (split ? 4 : 2);
+  size_t lds = (static_cast<size_t>(np) * kCout * kKP + np * (static_cast<size_t>(fwd_rows(g, T)) * g.pw * kC + 8)) * 2;
+  const size_t tile = static_cast<size_t>(T) * kCout * (split ? 4 : 2);
   if (lds < tile) lds = tile;
   if (split) {
-    allow_lds(k_stem_fwd<true>, lds);
-    hipLaunchKernelGGL(k_stem_fwd<true>, dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
+    allow_lds(k_stem_fwd<true, kFwdFragSplit>, lds);
+    hipLaunchKernelGGL((k_stem_fwd<true, kFwdFragSplit>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
   } else {
-    hipLaunchKernelGGL(k_stem_fwd<false>, dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
+    allow_lds(k_stem_fwd<false, kFwdFragBf16>, lds);
+    hipLaunchKernelGGL((k_stem_fwd<false, kFwdFragBf16>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
   }
 }
 
