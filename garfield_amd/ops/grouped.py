@@ -687,7 +687,7 @@ def _iwgrad_splits(rows_per_worker: int, tiles: int) -> int:
     """Pixel splits of the implicit weight gradient: about ``_IWGRAD_WG`` workgroups to fill the
     chip, each split at least ``_IWGRAD_MINPIX`` pixels."""
     S = 1
-    while S < 16 and tiles * S < _IWGRAD_WG and rows_per_worker // (2 * S) >= _IWGRAD_MINPIX:
+    while S < _IWGRAD_MAXS and tiles * S < _IWGRAD_WG and rows_per_worker // (2 * S) >= _IWGRAD_MINPIX:
         S *= 2
     return S
 
@@ -715,6 +715,7 @@ _WGRAD3_MINTILES = 3
 # (profiles/r2/iwgrad_wg_nt_sweep.log)
 _IWGRAD_WG = 512
 _IWGRAD_MINPIX = 512
+_IWGRAD_MAXS = 64   # ImageNet-size rows: more than 16 splits fill the chip (profiles/r4/splits/in_*: 177.8 -> 177.1 ms)
 
 
 def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int) -> None:
