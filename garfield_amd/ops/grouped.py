@@ -758,7 +758,11 @@ def _stem_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> 
     """Per-worker stem weight gradients (``gpu_stem_wgrad``): fp32 slabs of image slices,
     summed into the exchange rows by the deferred split-K reduction."""
     per = x.shape[0] // G
-    S = max(1, min(per, -(-_STEM_WG // G)))
+    # large images (ImageNet crops: 12544 output pixels each) take twice the workgroups: one image
+    # per slice still amortises the band staging (profiles/r4/splits/inst_*: 179.6 -> 178.7 ms),
+    # while CIFAR-size images keep ~2 images per slice (splits/stc_*: 2048 costs 0.03 ms there)
+    wg = _STEM_WG * (2 if dy.shape[2] * dy.shape[3] > 4096 else 1)
+    S = max(1, min(per, -(-wg // G)))
     part = torch.empty((S, G, 64, 147), dtype=torch.float32, device=dy.device)
     _native.native().gpu_stem_wgrad(x, dy, G, part)
     rows = spec.sink.rows_view(spec.conv.weight, (64, 147), spec.sink.flat.dtype)
