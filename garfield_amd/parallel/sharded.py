@@ -87,8 +87,8 @@ def overlap_enabled(world: int = 1) -> bool:
 class _Bucket:
     """One layer bucket [lo, hi) of the flat vector, cut into ``world`` shards of S.
 
-    ``send[dst, j]`` = local worker j's shard ``dst`` (packed so the whole bucket
-    leaves in ONE ``all_to_all_single``), ``recv[src, j]`` = shard ``rank`` of source
+    ``send[dst, j]`` = local worker j's shard ``dst`` (torch.distributed path only: packed so
+    the whole bucket leaves in ONE ``all_to_all_single``), ``recv[src, j]`` = shard ``rank`` of source
     rank src's local worker j (the row of global slot j * world + src)."""
 
     def __init__(self, lo: int, hi: int, world: int, rank: int, k: int, dev, dt, pack: bool):
