@@ -85,6 +85,9 @@ def save_engine(path: str, engine, meta: dict | None = None, write: bool = True)
 
 def load_engine(path: str, engine) -> dict:
     state = load(path)
+    shard = getattr(engine, "_shard", None)
+    if shard is not None and hasattr(shard, "quiesce"):
+        shard.quiesce()   # a previous step's updates may still run on the exchange stream
     engine.flat.load_reference_vector(state["flat"].to(engine.flat.data.device))
     saved = state.get("buffers", {})
     with torch.no_grad():
