@@ -204,23 +204,31 @@ __global__ __launch_bounds__(kThreads) void k_partial(const void* __restrict__ x
   }
 }
 
-// Finalize workgroups: 64 channels x 4 chunk lanes for ONE group (blockIdx.y),
+// Finalize workgroups: FC channels x 256 / FC chunk lanes for ONE group (blockIdx.y),
 // every chunk load issued before it is consumed (the chunk sums are a
 // latency-bound gather otherwise), lanes reduced through LDS in a fixed order.
-constexpr int kFinCh = 64;
-constexpr int kFinLanes = kThreads / kFinCh;  // 4
+// Finalize: 16 channels x 16 chunk lanes per workgroup: a chunk lane's loads (<= 8 per array for up to
+// 128 chunks) are one batch, so the pass costs one memory latency instead of four with 64 x 4
+// (bf16 ResNet-50 step -0.02 ms, fp32 -0.05 ms: profiles/r4/bn_fin/)
+constexpr int kFin = 16;
 
+template <int FC>
+struct Fin {
+  static constexpr int Ch = FC, Lanes = kThreads / FC;
+};
+
+template <int FC>
 __device__ __forceinline__ void chunk_sums(const float* __restrict__ part, const Geo& geo, int g, int c, float* sred,
                                            float* qred, float& S, float& Q) {
-  const int tc = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
+  const int tc = threadIdx.x % Fin<FC>::Ch, lane = threadIdx.x / Fin<FC>::Ch;
   const int C = geo.C;
   float s = 0.f, q = 0.f;
   if (c < C) {
-    for (int ch0 = lane; ch0 < geo.chunks; ch0 += kFinLanes * 8) {
+    for (int ch0 = lane; ch0 < geo.chunks; ch0 += Fin<FC>::Lanes * 8) {
       float a[8], b[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int ch = ch0 + kFinLanes * u;
+        const int ch = ch0 + Fin<FC>::Lanes * u;
         const int64_t o = (static_cast<int64_t>(g) * geo.chunks + ch) * 2 * C;
         a[u] = ch < geo.chunks ? part[o + c] : 0.f;
         b[u] = ch < geo.chunks ? part[o + C + c] : 0.f;
@@ -229,17 +237,17 @@ __device__ __forceinline__ void chunk_sums(const float* __restrict__ part, const
       for (int u = 0; u < 8; ++u) { s += a[u]; q += b[u]; }
     }
   }
-  sred[lane * kFinCh + tc] = s;
-  qred[lane * kFinCh + tc] = q;
+  sred[lane * Fin<FC>::Ch + tc] = s;
+  qred[lane * Fin<FC>::Ch + tc] = q;
   __syncthreads();
   S = 0.f;
   Q = 0.f;
 #pragma unroll
-  for (int l = 0; l < kFinLanes; ++l) { S += sred[l * kFinCh + tc]; Q += qred[l * kFinCh + tc]; }
+  for (int l = 0; l < Fin<FC>::Lanes; ++l) { S += sred[l * Fin<FC>::Ch + tc]; Q += qred[l * Fin<FC>::Ch + tc]; }
 }
 
 // Forward finalize of one (group, 64-channel block): mean, 1/std, scale, shift.
-template <int DT>
+template <int DT, int FC>
 __global__ __launch_bounds__(kThreads) void k_fwd_finalize(const float* __restrict__ part, const void* __restrict__ x,
                                                           Geo geo, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps,
@@ -248,10 +256,10 @@ __global__ __launch_bounds__(kThreads) void k_fwd_finalize(const float* __restri
   __shared__ float sred[kThreads], qred[kThreads];
   const int C = geo.C;
   const int g = blockIdx.y;
-  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  const int c = blockIdx.x * FC + threadIdx.x % FC;
   float S, Q;
-  chunk_sums(part, geo, g, c, sred, qred, S, Q);
-  if (threadIdx.x >= kFinCh || c >= C) return;
+  chunk_sums<FC>(part, geo, g, c, sred, qred, S, Q);
+  if (threadIdx.x >= FC || c >= C) return;
   const float M = static_cast<float>(geo.rg);
   const float sh = load_one<DT>(x, static_cast<int64_t>(g) * geo.rg * C + c);
   const float m1 = S / M;
@@ -359,6 +367,7 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
 
 // Backward finalize of one (group, 64-channel block): dγ, dβ -> exchange rows;
 // apply coefficients.
+template <int FC>
 __global__ __launch_bounds__(kThreads) void k_bwd_finalize(const float* __restrict__ part, Geo geo,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ istd,
@@ -367,10 +376,10 @@ __global__ __launch_bounds__(kThreads) void k_bwd_finalize(const float* __restri
   __shared__ float sred[kThreads], qred[kThreads];
   const int C = geo.C;
   const int g = blockIdx.y;
-  const int c = blockIdx.x * kFinCh + threadIdx.x % kFinCh;
+  const int c = blockIdx.x * FC + threadIdx.x % FC;
   float A, B;
-  chunk_sums(part, geo, g, c, sred, qred, A, B);
-  if (threadIdx.x >= kFinCh || c >= C) return;
+  chunk_sums<FC>(part, geo, g, c, sred, qred, A, B);
+  if (threadIdx.x >= FC || c >= C) return;
   const float M = static_cast<float>(geo.rg);
   const int64_t gc = static_cast<int64_t>(g) * C + c;
   const float is = istd[gc];
@@ -827,9 +836,8 @@ void forward_dt(const void* x, const void* res, int64_t rg, int groups, int C, c
     const int ncb = (C + g.cb - 1) / g.cb;
     hipLaunchKernelGGL((k_partial<false, 0, DT>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
                        nullptr, nullptr, nullptr, g, part);
-    const dim3 fgrid((C + kFinCh - 1) / kFinCh, groups);
-    hipLaunchKernelGGL((k_fwd_finalize<DT>), fgrid, dim3(kThreads), 0, stream, part, x, g, gamma, beta, eps, mean, istd,
-                       scale, shift);
+    hipLaunchKernelGGL((k_fwd_finalize<DT, kFin>), dim3((C + kFin - 1) / kFin, groups), dim3(kThreads), 0, stream, part,
+                       x, g, gamma, beta, eps, mean, istd, scale, shift);
   }
   const RunStats rs{mean, istd, run_mean, run_var, eps, momentum, groups};
   int tch, rp;
@@ -861,7 +869,7 @@ void backward_dt(const void* x, const void* dy, const void* y, const uint8_t* ma
   if (rm == 2) hipLaunchKernelGGL((k_partial<true, 2, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
   else if (rm == 1) hipLaunchKernelGGL((k_partial<true, 1, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
   else hipLaunchKernelGGL((k_partial<true, 0, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
-  hipLaunchKernelGGL(k_bwd_finalize, dim3((C + kFinCh - 1) / kFinCh, groups), dim3(kThreads), 0, stream, part, g,
+  hipLaunchKernelGGL(k_bwd_finalize<kFin>, dim3((C + kFin - 1) / kFin, groups), dim3(kThreads), 0, stream, part, g,
                      gamma, istd, coef, grow, grow_dt, row_stride, off_gamma, off_beta);
   int tch, rp;
   apply_geometry(C, &tch, &rp);
