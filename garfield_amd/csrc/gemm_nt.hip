@@ -473,18 +473,19 @@ __global__ __launch_bounds__(kMergeCh * kMergeLanes) void k_finalize_tiles(
   const int g = blockIdx.y;
   const int64_t g0 = static_cast<int64_t>(g) * rg, g1 = g0 + rg < M ? g0 + rg : M;
   const int64_t t_lo = g0 / H, t_hi = (g1 - 1) / H;
-  const int64_t nent = (t_hi - t_lo + 1) * E;          // (tile, entry) pairs of this worker
+  const int nent = static_cast<int>((t_hi - t_lo + 1) * E);   // (tile, entry) pairs of this worker
   float n = 0.f, mu = 0.f, m2 = 0.f;
   if (c < C) {
-    for (int64_t i0 = lane; i0 < nent; i0 += kMergeLanes * 4) {
+    for (int i0 = lane; i0 < nent; i0 += kMergeLanes * 4) {   // 32-bit index math (no 64-bit divisions)
       float sv[4], qv[4], nv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int64_t i = i0 + static_cast<int64_t>(u) * kMergeLanes;
+        const int i = i0 + u * kMergeLanes;
         nv[u] = 0.f;
         sv[u] = qv[u] = 0.f;
         if (i < nent) {
-          const int64_t t = t_lo + i / E, e = i - (i / E) * E;
+          const int q = i / E;
+          const int64_t t = t_lo + q, e = i - q * E;
           const int slot = t * H < g0 ? 1 : 0;          // the tile started in the previous worker
           const float* p = stats + ((t * E + e) * 2 + slot) * 3 * C + c;
           nv[u] = p[0];
