@@ -1869,11 +1869,87 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                     rows.data_ptr<float>(), row_stride, off_w, off_b, stream_of(dev));
   }, py::arg("x"), py::arg("dl"), py::arg("groups"), py::arg("rows"), py::arg("row_stride"), py::arg("off_w"),
      py::arg("off_b"), "Per-worker fp32 classifier dW / db written into the exchange rows");
+  auto check_bf16_mat = [](const at::Tensor& t, const at::Device& dev, int64_t r, int64_t c, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.device() == dev && t.scalar_type() == at::kBFloat16 && t.is_contiguous() &&
+                    t.numel() == r * c,
+                "garfield linear_bf16: ", what, " must be a contiguous bf16 [", r, ", ", c, "] tensor on ", dev);
+  };
+  m.def("gpu_linear_bf16_fwd", [check_bf16_mat](const at::Tensor& x, const at::Tensor& w,
+                                                const c10::optional<at::Tensor>& b, const at::Tensor& y) {
+    const auto dev = x.device();
+    const int64_t R = x.size(0), F = x.size(1), O = w.size(0);
+    check_bf16_mat(x, dev, R, F, "x");
+    check_bf16_mat(w, dev, O, F, "w");
+    check_bf16_mat(y, dev, R, O, "y");
+    const uint16_t* bp = nullptr;
+    if (b.has_value() && b->defined()) {
+      check_bf16_mat(*b, dev, 1, O, "b");
+      bp = reinterpret_cast<const uint16_t*>(b->data_ptr());
+    }
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::linear_bf16_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                   reinterpret_cast<const uint16_t*>(w.data_ptr()), bp, static_cast<int>(R),
+                                   static_cast<int>(F), static_cast<int>(O), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                   stream_of(dev));
+  }, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"),
+     "bf16 classifier forward y = x wᵀ + b (fp32 accumulation, one rounding)");
+  m.def("gpu_linear_bf16_dgrad", [check_bf16_mat](const at::Tensor& dl, const at::Tensor& w, const at::Tensor& dx) {
+    const auto dev = dl.device();
+    const int64_t R = dl.size(0), O = dl.size(1), F = w.size(1);
+    check_bf16_mat(dl, dev, R, O, "dl");
+    check_bf16_mat(w, dev, O, F, "w");
+    check_bf16_mat(dx, dev, R, F, "dx");
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::linear_bf16_dgrad(reinterpret_cast<const uint16_t*>(dl.data_ptr()),
+                                     reinterpret_cast<const uint16_t*>(w.data_ptr()), static_cast<int>(R),
+                                     static_cast<int>(F), static_cast<int>(O), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                                     stream_of(dev));
+  }, py::arg("dl"), py::arg("w"), py::arg("dx"), "bf16 classifier data gradient dx = dl w");
+  m.def("gpu_linear_bf16_wgrad", [check_bf16_mat](const at::Tensor& x, const at::Tensor& dl, int64_t groups,
+                                                  const at::Tensor& rows, int64_t row_stride, int64_t off_w,
+                                                  int64_t off_b) {
+    const auto dev = x.device();
+    const int64_t R = x.size(0), F = x.size(1), O = dl.size(1);
+    check_bf16_mat(x, dev, R, F, "x");
+    check_bf16_mat(dl, dev, R, O, "dl");
+    TORCH_CHECK(groups >= 1 && R % groups == 0, "gpu_linear_bf16_wgrad: rows do not split into groups");
+    TORCH_CHECK(rows.is_cuda() && rows.device() == dev && rows.is_contiguous() &&
+                    (rows.scalar_type() == at::kFloat || rows.scalar_type() == at::kBFloat16 ||
+                     rows.scalar_type() == at::kHalf),
+                "gpu_linear_bf16_wgrad: rows must be a contiguous fp32 / bf16 / fp16 exchange buffer");
+    TORCH_CHECK(off_w >= 0 && row_stride >= 0 && (groups - 1) * row_stride + off_w + O * F <= rows.numel() &&
+                    (off_b < 0 || (groups - 1) * row_stride + off_b + O <= rows.numel()),
+                "gpu_linear_bf16_wgrad: row offsets out of bounds");
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::linear_bf16_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                     reinterpret_cast<const uint16_t*>(dl.data_ptr()), static_cast<int>(groups),
+                                     static_cast<int>(R / groups), static_cast<int>(F), static_cast<int>(O),
+                                     rows.data_ptr(), dtype_code(rows), row_stride, off_w, off_b, stream_of(dev));
+  }, py::arg("x"), py::arg("dl"), py::arg("groups"), py::arg("rows"), py::arg("row_stride"), py::arg("off_w"),
+     py::arg("off_b"), "Per-worker bf16 classifier dW / db (fp32 sums, one rounding) written into the exchange rows");
   m.def("gpu_avgpool_f32", [](const at::Tensor& x, const at::Tensor& y, bool backward) {
     // forward: x [N, C, H, W] channels_last -> y [N, C]; backward: x = dy [N, C] -> y = dx [N, C, H, W]
     const at::Tensor& big = backward ? y : x;
     const at::Tensor& small = backward ? x : y;
     const auto dev = big.device();
+    if (big.scalar_type() == at::kBFloat16) {   // the bf16 step
+      TORCH_CHECK(big.is_cuda() && big.dim() == 4 && big.is_contiguous(at::MemoryFormat::ChannelsLast),
+                  "gpu_avgpool: the activation must be a channels_last 4-D tensor");
+      const int64_t N = big.size(0), C = big.size(1), HW = big.size(2) * big.size(3);
+      TORCH_CHECK(small.is_cuda() && small.device() == dev && small.scalar_type() == at::kBFloat16 &&
+                      small.is_contiguous() && small.numel() == N * C,
+                  "gpu_avgpool: the pooled tensor must be a contiguous bf16 [N, C] tensor");
+      c10::hip::HIPGuard guard(dev.index());
+      auto xp = reinterpret_cast<const uint16_t*>(x.data_ptr());
+      auto yp = reinterpret_cast<uint16_t*>(y.data_ptr());
+      if (backward)
+        garfield::gpu::avgpool_bf16_bwd(xp, static_cast<int>(N), static_cast<int>(HW), static_cast<int>(C), yp,
+                                        stream_of(dev));
+      else
+        garfield::gpu::avgpool_bf16_fwd(xp, static_cast<int>(N), static_cast<int>(HW), static_cast<int>(C), yp,
+                                        stream_of(dev));
+      return;
+    }
     check_f32_cl(big, dev, "activation");
     const int64_t N = big.size(0), C = big.size(1), HW = big.size(2) * big.size(3);
     check_f32_mat(small, dev, N, C, "pooled");
@@ -1884,7 +1960,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     else
       garfield::gpu::avgpool_f32_fwd(x.data_ptr<float>(), static_cast<int>(N), static_cast<int>(HW),
                                      static_cast<int>(C), y.data_ptr<float>(), stream_of(dev));
-  }, py::arg("x"), py::arg("y"), py::arg("backward"), "fp32 NHWC global average pool (forward / backward)");
+  }, py::arg("x"), py::arg("y"), py::arg("backward"), "fp32 / bf16 NHWC global average pool (forward / backward)");
   m.def("stem_supported", &garfield::gpu::stem_supported, py::arg("h"), py::arg("w"),
         "True when the implicit stem kernels (7x7/2, 3 -> 64 channels) handle H x W images");
   m.def("gpu_stem_fwd", [](const at::Tensor& x, const at::Tensor& w160, const at::Tensor& y) {
@@ -1892,10 +1968,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     TORCH_CHECK(x.is_cuda() && (split || x.scalar_type() == at::kBFloat16) && x.dim() == 4 && x.size(1) == 3 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "gpu_stem_fwd: x must be a channels_last bf16 or fp32 [N, 3, H, W] tensor");
-    TORCH_CHECK(w160.device() == x.device() && w160.scalar_type() == at::kBFloat16 && w160.is_contiguous() &&
-                    w160.numel() == (split ? 3 : 1) * 64 * 160,
-                "gpu_stem_fwd: w must be the contiguous zero-padded [64, 160] bf16 matrix (fp32 x: its pieces "
-                "[3, 64, 160])");
+    const bool raw = !split && w160.numel() == 64 * 147;   // the channels_last weight itself (padded in LDS)
+    TORCH_CHECK(w160.device() == x.device() && w160.scalar_type() == at::kBFloat16 &&
+                    (raw ? (w160.dim() == 4 && w160.is_contiguous(at::MemoryFormat::ChannelsLast)) : w160.is_contiguous()) &&
+                    (raw || w160.numel() == (split ? 3 : 1) * 64 * 160),
+                "gpu_stem_fwd: w must be the contiguous zero-padded [64, 160] bf16 matrix, the channels_last bf16 "
+                "[64, 3, 7, 7] weight (bf16 x), or (fp32 x) the pieces [3, 64, 160]");
     const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
     TORCH_CHECK(garfield::gpu::stem_supported(static_cast<int>(H), static_cast<int>(W)), "gpu_stem_fwd: unsupported size");
     const int64_t Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
@@ -1906,7 +1984,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     c10::hip::HIPGuard guard(x.device().index());
     garfield::gpu::stem_fwd(x.data_ptr(), reinterpret_cast<const uint16_t*>(w160.data_ptr()), split,
                             static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), y.data_ptr(),
-                            stream_of(x.device()));
+                            stream_of(x.device()), raw ? 147 : 160);
   }, py::arg("x"), py::arg("w"), py::arg("y"),
      "Implicit-GEMM ResNet stem forward (7x7/2, pad 3, 3 -> 64); fp32 x: split-bf16 MFMA on the weight's pieces");
   m.def("gpu_stem_wgrad", [](const at::Tensor& x, const at::Tensor& dy, int64_t groups, const at::Tensor& part) {

@@ -62,7 +62,10 @@ void augment_gather(const uint8_t* src, int64_t nsrc, const int64_t* idx, const 
 // images into 64 channels on MFMA, without a patch matrix. w: zero-padded [64][160] bf16.
 // split: the fp32 form — x / y fp32, w = the weight's three bf16 pieces [3][64][160].
 bool stem_supported(int H, int W);
-void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream);
+// w: the zero-padded [64][160] matrix (split: its three pieces), or (wpitch = 147, bf16 only) the
+// channels_last [64][7][7][3] weight itself
+void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream,
+              int wpitch = 160);
 // per-worker weight gradients: part fp32 [slices][groups][64][147] (sum over slices = dW of the worker);
 // split: x / dy fp32
 void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,

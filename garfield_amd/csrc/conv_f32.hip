@@ -830,19 +830,26 @@ __global__ __launch_bounds__(256) void k_wsplit(WTable t) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// classifier and global average pool (fp32, VALU)
+// classifier (fp32 or bf16 operands, fp32 accumulation, one rounding) and global average pool
+// (fp32), VALU: the classifier is ~0.1 GFLOP per step, far below a GEMM tile's worth of work
+
+// element loads / stores of the classifier's operand type (float, or bf16 as uint16_t)
+__device__ __forceinline__ float lin_ld(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float lin_ld(const uint16_t* p, int64_t i) { return bf16_to_f(p[i]); }
+__device__ __forceinline__ void lin_st(float* p, int64_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void lin_st(uint16_t* p, int64_t i, float v) { p[i] = f_to_bf16(v); }
 
 // logits[r][o] = Σ_f x[r][f] w[o][f] + b[o]: one wave per row, O <= 64 outputs kept in registers
 constexpr int kLinMaxO = 16;
 // y[row][o]: one wave per row, the lanes over f, 8 f-columns per lane in flight (x and w loads issue
 // back to back instead of one dependent round trip per column)
-__global__ __launch_bounds__(256) void k_f32_linear_fwd(const float* __restrict__ x, const float* __restrict__ w,
-                                                        const float* __restrict__ b, int R, int F, int O,
-                                                        float* __restrict__ y) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_linear_fwd(const T* __restrict__ x, const T* __restrict__ w,
+                                                    const T* __restrict__ b, int R, int F, int O, T* __restrict__ y) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
-  const float* xr = x + static_cast<int64_t>(row) * F;
+  const T* xr = x + static_cast<int64_t>(row) * F;
   for (int o0 = 0; o0 < O; o0 += kLinMaxO) {
     float acc[kLinMaxO];
 #pragma unroll
@@ -852,16 +859,16 @@ __global__ __launch_bounds__(256) void k_f32_linear_fwd(const float* __restrict_
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int f = f0 + u * 64 + lane;
-        xv[u] = f < F ? xr[f] : 0.f;
+        xv[u] = f < F ? lin_ld(xr, f) : 0.f;
       }
 #pragma unroll
       for (int o = 0; o < kLinMaxO; ++o) {
         if (o0 + o < O) {
-          const float* wr = w + static_cast<int64_t>(o0 + o) * F;
+          const T* wr = w + static_cast<int64_t>(o0 + o) * F;
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const int f = f0 + u * 64 + lane;
-            acc[o] = fmaf(xv[u], f < F ? wr[f] : 0.f, acc[o]);
+            acc[o] = fmaf(xv[u], f < F ? lin_ld(wr, f) : 0.f, acc[o]);
           }
         }
       }
@@ -871,36 +878,34 @@ __global__ __launch_bounds__(256) void k_f32_linear_fwd(const float* __restrict_
       float v = acc[o];
 #pragma unroll
       for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s);
-      if (lane == 0 && o0 + o < O) y[static_cast<int64_t>(row) * O + o0 + o] = v + (b ? b[o0 + o] : 0.f);
+      if (lane == 0 && o0 + o < O) lin_st(y, static_cast<int64_t>(row) * O + o0 + o, v + (b ? lin_ld(b, o0 + o) : 0.f));
     }
   }
 }
-
-// dx[r][f] = Σ_o dl[r][o] w[o][f]
-__global__ __launch_bounds__(256) void k_f32_linear_dgrad(const float* __restrict__ dl, const float* __restrict__ w,
-                                                          int R, int F, int O, float* __restrict__ dx) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_linear_dgrad(const T* __restrict__ dl, const T* __restrict__ w, int R, int F,
+                                                      int O, T* __restrict__ dx) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (t >= static_cast<int64_t>(R) * F) return;
   const int64_t r = t / F;
   const int f = static_cast<int>(t - r * F);
   float a = 0.f;
-  for (int o = 0; o < O; ++o) a = fmaf(dl[r * O + o], w[static_cast<int64_t>(o) * F + f], a);
-  dx[t] = a;
+  for (int o = 0; o < O; ++o) a = fmaf(lin_ld(dl, r * O + o), lin_ld(w, static_cast<int64_t>(o) * F + f), a);
+  lin_st(dx, t, a);
 }
-
-// per worker g: dW_g[o][f] = Σ_{r in g} dl[r][o] x[r][f], db_g[o] = Σ dl[r][o]; written at
-// out + g * row_stride + off_w / off_b (the exchange rows). Block (64 f-columns, worker g): its four waves
-// take every fourth row, then the four partial sums are added in LDS in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void k_f32_linear_wgrad(const float* __restrict__ x, const float* __restrict__ dl,
-                                                          int rg, int F, int O, float* __restrict__ out,
-                                                          int64_t row_stride, int64_t off_w, int64_t off_b) {
+// per-worker dW_g[o][f] = Σ_{r in g} dl[r][o] x[r][f] and db_g[o] = Σ_{r in g} dl[r][o], written straight
+// into worker g's exchange row (element type ODT: fp32 / bf16 / fp16)
+template <typename T>
+__global__ __launch_bounds__(256) void k_linear_wgrad(const T* __restrict__ x, const T* __restrict__ dl, int rg, int F,
+                                                      int O, void* __restrict__ out, int odt, int64_t row_stride,
+                                                      int64_t off_w, int64_t off_b) {
   __shared__ float red[3][kLinMaxO][64];
   const int g = blockIdx.y;
   const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int f = blockIdx.x * 64 + lane;
-  const float* xg = x + static_cast<int64_t>(g) * rg * F;
-  const float* dg = dl + static_cast<int64_t>(g) * rg * O;
-  float* og = out + static_cast<int64_t>(g) * row_stride;
+  const T* xg = x + static_cast<int64_t>(g) * rg * F;
+  const T* dg = dl + static_cast<int64_t>(g) * rg * O;
+  const int64_t og = static_cast<int64_t>(g) * row_stride;
   for (int o0 = 0; o0 < O; o0 += kLinMaxO) {
     float acc[kLinMaxO];
 #pragma unroll
@@ -908,10 +913,10 @@ __global__ __launch_bounds__(256) void k_f32_linear_wgrad(const float* __restric
     if (f < F) {
 #pragma unroll 4
       for (int r = q; r < rg; r += 4) {
-        const float xv = xg[static_cast<int64_t>(r) * F + f];
+        const float xv = lin_ld(xg, static_cast<int64_t>(r) * F + f);
 #pragma unroll
         for (int o = 0; o < kLinMaxO; ++o)
-          if (o0 + o < O) acc[o] = fmaf(dg[static_cast<int64_t>(r) * O + o0 + o], xv, acc[o]);
+          if (o0 + o < O) acc[o] = fmaf(lin_ld(dg, static_cast<int64_t>(r) * O + o0 + o), xv, acc[o]);
       }
     }
     if (q > 0) {
@@ -923,36 +928,224 @@ __global__ __launch_bounds__(256) void k_f32_linear_wgrad(const float* __restric
 #pragma unroll
       for (int o = 0; o < kLinMaxO; ++o)
         if (o0 + o < O)
-          og[off_w + static_cast<int64_t>(o0 + o) * F + f] = ((acc[o] + red[0][o][lane]) + red[1][o][lane]) + red[2][o][lane];
+          store_one(out, odt, og + off_w + static_cast<int64_t>(o0 + o) * F + f,
+                    ((acc[o] + red[0][o][lane]) + red[1][o][lane]) + red[2][o][lane]);
     }
     __syncthreads();
   }
   if (off_b >= 0 && blockIdx.x == 0 && threadIdx.x < O) {
     float s = 0.f;
-    for (int r = 0; r < rg; ++r) s += dg[static_cast<int64_t>(r) * O + threadIdx.x];
-    og[off_b + threadIdx.x] = s;
+    for (int r = 0; r < rg; ++r) s += lin_ld(dg, static_cast<int64_t>(r) * O + threadIdx.x);
+    store_one(out, odt, og + off_b + threadIdx.x, s);
+  }
+}
+// ---- bf16 classifier with 16-byte operand loads (F % 8 == 0, O <= kLinV) ------------------------
+// The step's classifier is [2000 x 2048] x [2048 x 10]: ~0.1 GFLOP and 8 MB of activations, so it is
+// an HBM stream, not a GEMM: each lane holds 8 consecutive features of a row (one 16-byte load), the
+// weight rows are staged in LDS once per workgroup, and the O dot products are reduced across the wave.
+constexpr int kLinV = 16;        // outputs per launch pass (O <= kLinV)
+constexpr int kLinRows = 8;      // rows per workgroup (2 per wave)
+
+__device__ __forceinline__ void unpack_bf16x8(const uint4 u, float (&v)[8]) {
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+
+// y[r][o] = Σ_f x[r][f] w[o][f] + b[o]; LDS: w [O][F] bf16 (<= 16 x 4096 x 2 = 128 KB). Each wave's two
+// rows are loaded (4 x 16 B per lane and row per 2048 features) before the weight staging barrier, so the
+// HBM latency of x overlaps the weight's L2 reads.
+__global__ __launch_bounds__(256) void k_linear_fwd_v(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                      const uint16_t* __restrict__ b, int R, int F, int O,
+                                                      uint16_t* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t wl[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fv = F / 8;
+  const int r0 = blockIdx.x * kLinRows + wave * 2;
+  float acc[2][kLinV];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int o = 0; o < kLinV; ++o) acc[i][o] = 0.f;
+  for (int c0 = 0; c0 < fv; c0 += 256) {
+    uint4 xr[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = c0 + u * 64 + lane;
+        xr[i][u] = (r0 + i < R && c < fv) ? reinterpret_cast<const uint4*>(x + static_cast<int64_t>(r0 + i) * F)[c]
+                                          : make_uint4(0u, 0u, 0u, 0u);
+      }
+    if (c0 == 0) {   // uniform over the workgroup
+      const int nv = O * fv;
+      for (int e = threadIdx.x; e < nv; e += 256)
+        reinterpret_cast<uint4*>(wl)[e] = reinterpret_cast<const uint4*>(w)[e];
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u * 64 + lane;
+      if (c >= fv) break;
+      float xv[2][8];
+      unpack_bf16x8(xr[0][u], xv[0]);
+      unpack_bf16x8(xr[1][u], xv[1]);
+#pragma unroll
+      for (int o = 0; o < kLinV; ++o) {
+        if (o < O) {
+          float wv[8];
+          unpack_bf16x8(reinterpret_cast<const uint4*>(wl + o * F)[c], wv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            acc[0][o] = fmaf(xv[0][k], wv[k], acc[0][o]);
+            acc[1][o] = fmaf(xv[1][k], wv[k], acc[1][o]);
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int o = 0; o < kLinV; ++o) {
+      if (o < O) {
+        float v = acc[i][o];
+#pragma unroll
+        for (int s2 = 32; s2 >= 1; s2 >>= 1) v += __shfl_xor(v, s2);
+        if (lane == o && r0 + i < R) y[static_cast<int64_t>(r0 + i) * O + o] = f_to_bf16(v + (b ? bf16_to_f(b[o]) : 0.f));
+      }
+    }
+}
+
+// dx[r][f .. f + 8] = Σ_o dl[r][o] w[o][f .. f + 8]: one 16-byte output per thread
+__global__ __launch_bounds__(256) void k_linear_dgrad_v(const uint16_t* __restrict__ dl, const uint16_t* __restrict__ w,
+                                                        int R, int F, int O, uint16_t* __restrict__ dx) {
+  const int fv = F / 8;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= static_cast<int64_t>(R) * fv) return;
+  const int64_t r = t / fv;
+  const int c = static_cast<int>(t - r * fv);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int o = 0; o < O; ++o) {
+    const float d = bf16_to_f(dl[r * O + o]);
+    float wv[8];
+    unpack_bf16x8(reinterpret_cast<const uint4*>(w + static_cast<int64_t>(o) * F)[c], wv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = fmaf(d, wv[k], a[k]);
+  }
+  reinterpret_cast<uint4*>(dx)[t] = make_uint4(pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]),
+                                               pack_bf16x2(a[4], a[5]), pack_bf16x2(a[6], a[7]));
+}
+
+// per-worker dW_g[o][f] = Σ_{r in g} dl[r][o] x[r][f], db_g[o] = Σ_{r in g} dl[r][o] into worker g's exchange
+// row. Workgroup (64 features, worker g): lane = feature chunk (8 x 8 features) + 8 x row lane (8 per wave, 32
+// in all), four rows' loads in flight per lane; dl of the worker staged in LDS as fp32; the row lanes
+// reduced by shuffles inside the wave, then across the 4 waves through LDS.
+constexpr int kWgF = 64;
+__global__ __launch_bounds__(256) void k_linear_wgrad_v(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dl,
+                                                        int rg, int F, int O, void* __restrict__ out, int odt,
+                                                        int64_t row_stride, int64_t off_w, int64_t off_b) {
+  extern __shared__ __attribute__((aligned(16))) float dls[];   // [rg][O] then [4][kLinV][8][8] partials
+  const int g = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ch = lane & 7, rl = wave * 8 + (lane >> 3);          // feature chunk, row lane (0..31)
+  const int f0 = blockIdx.x * kWgF + ch * 8;
+  const uint16_t* dg = dl + static_cast<int64_t>(g) * rg * O;
+  const uint16_t* xg = x + static_cast<int64_t>(g) * rg * F + f0;
+  const bool fok = f0 < F;
+  uint4 xr[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {   // the first four rows' loads before the staging barrier
+    const int r = rl + 32 * u;
+    xr[u] = (fok && r < rg) ? *reinterpret_cast<const uint4*>(xg + static_cast<int64_t>(r) * F) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  for (int e = threadIdx.x; e < rg * O; e += 256) dls[e] = bf16_to_f(dg[e]);
+  __syncthreads();
+  float acc[kLinV][8];
+#pragma unroll
+  for (int o = 0; o < kLinV; ++o)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[o][k] = 0.f;
+  for (int r0 = 0; r0 < rg; r0 += 128) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + rl + 32 * u;
+      if (r < rg) {
+        float xv[8];
+        unpack_bf16x8(xr[u], xv);
+#pragma unroll
+        for (int o = 0; o < kLinV; ++o) {
+          if (o < O) {
+            const float d = dls[r * O + o];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[o][k] = fmaf(d, xv[k], acc[o][k]);
+          }
+        }
+      }
+    }
+    if (r0 + 128 < rg) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + 128 + rl + 32 * u;
+        xr[u] = (fok && r < rg) ? *reinterpret_cast<const uint4*>(xg + static_cast<int64_t>(r) * F)
+                                : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  }
+  float* red = dls + rg * O;
+#pragma unroll
+  for (int o = 0; o < kLinV; ++o)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = acc[o][k];
+      v += __shfl_xor(v, 8);
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      acc[o][k] = v;
+    }
+  if ((lane >> 3) == 0) {
+#pragma unroll
+    for (int o = 0; o < kLinV; ++o)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[((wave * kLinV + o) * 8 + ch) * 8 + k] = acc[o][k];
+  }
+  __syncthreads();
+  const int64_t og = static_cast<int64_t>(g) * row_stride;
+  for (int e = threadIdx.x; e < O * kWgF; e += 256) {
+    const int o = e / kWgF, q = e - o * kWgF, c2 = q / 8, k = q - c2 * 8;
+    const int f = blockIdx.x * kWgF + q;
+    if (f < F) {
+      float v = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < 4; ++w2) v += red[((w2 * kLinV + o) * 8 + c2) * 8 + k];
+      store_one(out, odt, og + off_w + static_cast<int64_t>(o) * F + f, v);
+    }
+  }
+  if (off_b >= 0 && blockIdx.x == 0 && threadIdx.x < O) {
+    float sb = 0.f;
+    for (int r = 0; r < rg; ++r) sb += dls[r * O + threadIdx.x];
+    store_one(out, odt, og + off_b + threadIdx.x, sb);
   }
 }
 
-// pooled[n][c] = mean over HW of x[n][hw][c]
-__global__ __launch_bounds__(256) void k_f32_avgpool_fwd(const float* __restrict__ x, int N, int HW, int C,
-                                                         float* __restrict__ y) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_avgpool_fwd(const T* __restrict__ x, int N, int HW, int C, T* __restrict__ y) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (t >= static_cast<int64_t>(N) * C) return;
   const int64_t n = t / C;
   const int c = static_cast<int>(t - n * C);
   float s = 0.f;
-  for (int p = 0; p < HW; ++p) s += x[(n * HW + p) * C + c];
-  y[t] = s / static_cast<float>(HW);
+  for (int p = 0; p < HW; ++p) s += lin_ld(x, (n * HW + p) * C + c);
+  lin_st(y, t, s / static_cast<float>(HW));
 }
-
-__global__ __launch_bounds__(256) void k_f32_avgpool_bwd(const float* __restrict__ dy, int N, int HW, int C,
-                                                         float* __restrict__ dx) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_avgpool_bwd(const T* __restrict__ dy, int N, int HW, int C, T* __restrict__ dx) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (t >= static_cast<int64_t>(N) * HW * C) return;
   const int c = static_cast<int>(t % C);
   const int64_t n = t / (static_cast<int64_t>(HW) * C);
-  dx[t] = dy[n * C + c] / static_cast<float>(HW);
+  lin_st(dx, t, lin_ld(dy, n * C + c) / static_cast<float>(HW));
 }
 
 unsigned blocks_for(int64_t items) { return static_cast<unsigned>((items + 255) / 256); }
@@ -1089,32 +1282,95 @@ void wsplit_multi(const WSplitJob* jobs, int count, hipStream_t stream) {
 
 void linear_f32_fwd(const float* x, const float* w, const float* b, int R, int F, int O, float* y, hipStream_t stream) {
   if (R <= 0) return;
-  hipLaunchKernelGGL(k_f32_linear_fwd, dim3((R + 3) / 4), dim3(256), 0, stream, x, w, b, R, F, O, y);
+  hipLaunchKernelGGL(k_linear_fwd<float>, dim3((R + 3) / 4), dim3(256), 0, stream, x, w, b, R, F, O, y);
 }
 
 void linear_f32_dgrad(const float* dl, const float* w, int R, int F, int O, float* dx, hipStream_t stream) {
   const int64_t items = static_cast<int64_t>(R) * F;
   if (items <= 0) return;
-  hipLaunchKernelGGL(k_f32_linear_dgrad, dim3(blocks_for(items)), dim3(256), 0, stream, dl, w, R, F, O, dx);
+  hipLaunchKernelGGL(k_linear_dgrad<float>, dim3(blocks_for(items)), dim3(256), 0, stream, dl, w, R, F, O, dx);
 }
 
 void linear_f32_wgrad(const float* x, const float* dl, int groups, int rg, int F, int O, float* out, int64_t row_stride,
                       int64_t off_w, int64_t off_b, hipStream_t stream) {
   if (groups <= 0 || F <= 0) return;
-  hipLaunchKernelGGL(k_f32_linear_wgrad, dim3((F + 63) / 64, groups), dim3(256), 0, stream, x, dl, rg, F, O, out,
-                     row_stride, off_w, off_b);
+  hipLaunchKernelGGL(k_linear_wgrad<float>, dim3((F + 63) / 64, groups), dim3(256), 0, stream, x, dl, rg, F, O,
+                     static_cast<void*>(out), static_cast<int>(kF32), row_stride, off_w, off_b);
+}
+
+// the vectorised kernels' limits: F % 8, O <= kLinV, the staged weight / gradient rows in LDS
+bool linear_bf16_vec(int R, int F, int O, int rg) {
+  (void)R;
+  return F % 8 == 0 && O >= 1 && O <= kLinV && static_cast<int64_t>(O) * F * 2 <= 128 * 1024 &&
+         (rg <= 0 || (static_cast<int64_t>(rg) * O + 4 * kLinV * kWgF) * 4 <= 128 * 1024);
+}
+
+namespace {
+template <typename K>
+void allow_lin_lds(K* k, size_t bytes) {
+  if (bytes > 64 * 1024) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bytes));
+}
+}  // namespace
+
+void linear_bf16_fwd(const uint16_t* x, const uint16_t* w, const uint16_t* b, int R, int F, int O, uint16_t* y,
+                     hipStream_t stream) {
+  if (R <= 0) return;
+  if (linear_bf16_vec(R, F, O, 0)) {
+    const size_t lds = static_cast<size_t>(O) * F * 2;
+    allow_lin_lds(k_linear_fwd_v, lds);
+    hipLaunchKernelGGL(k_linear_fwd_v, dim3((R + kLinRows - 1) / kLinRows), dim3(256), lds, stream, x, w, b, R, F, O, y);
+    return;
+  }
+  hipLaunchKernelGGL(k_linear_fwd<uint16_t>, dim3((R + 3) / 4), dim3(256), 0, stream, x, w, b, R, F, O, y);
+}
+
+void linear_bf16_dgrad(const uint16_t* dl, const uint16_t* w, int R, int F, int O, uint16_t* dx, hipStream_t stream) {
+  const int64_t items = static_cast<int64_t>(R) * F;
+  if (items <= 0) return;
+  if (F % 8 == 0) {
+    hipLaunchKernelGGL(k_linear_dgrad_v, dim3(blocks_for(items / 8)), dim3(256), 0, stream, dl, w, R, F, O, dx);
+    return;
+  }
+  hipLaunchKernelGGL(k_linear_dgrad<uint16_t>, dim3(blocks_for(items)), dim3(256), 0, stream, dl, w, R, F, O, dx);
+}
+
+void linear_bf16_wgrad(const uint16_t* x, const uint16_t* dl, int groups, int rg, int F, int O, void* out, int odt,
+                       int64_t row_stride, int64_t off_w, int64_t off_b, hipStream_t stream) {
+  if (groups <= 0 || F <= 0) return;
+  if (linear_bf16_vec(rg * groups, F, O, rg)) {
+    const size_t lds = (static_cast<size_t>(rg) * O + 4 * kLinV * kWgF) * 4;
+    allow_lin_lds(k_linear_wgrad_v, lds);
+    hipLaunchKernelGGL(k_linear_wgrad_v, dim3((F + kWgF - 1) / kWgF, groups), dim3(256), lds, stream, x, dl, rg, F, O, out,
+                       odt, row_stride, off_w, off_b);
+    return;
+  }
+  hipLaunchKernelGGL(k_linear_wgrad<uint16_t>, dim3((F + 63) / 64, groups), dim3(256), 0, stream, x, dl, rg, F, O, out,
+                     odt, row_stride, off_w, off_b);
 }
 
 void avgpool_f32_fwd(const float* x, int N, int HW, int C, float* y, hipStream_t stream) {
   const int64_t items = static_cast<int64_t>(N) * C;
   if (items <= 0) return;
-  hipLaunchKernelGGL(k_f32_avgpool_fwd, dim3(blocks_for(items)), dim3(256), 0, stream, x, N, HW, C, y);
+  hipLaunchKernelGGL(k_avgpool_fwd<float>, dim3(blocks_for(items)), dim3(256), 0, stream, x, N, HW, C, y);
 }
 
 void avgpool_f32_bwd(const float* dy, int N, int HW, int C, float* dx, hipStream_t stream) {
   const int64_t items = static_cast<int64_t>(N) * HW * C;
   if (items <= 0) return;
-  hipLaunchKernelGGL(k_f32_avgpool_bwd, dim3(blocks_for(items)), dim3(256), 0, stream, dy, N, HW, C, dx);
+  hipLaunchKernelGGL(k_avgpool_bwd<float>, dim3(blocks_for(items)), dim3(256), 0, stream, dy, N, HW, C, dx);
+}
+
+void avgpool_bf16_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t stream) {
+  const int64_t items = static_cast<int64_t>(N) * C;
+  if (items <= 0) return;
+  hipLaunchKernelGGL(k_avgpool_fwd<uint16_t>, dim3(blocks_for(items)), dim3(256), 0, stream, x, N, HW, C, y);
+}
+
+void avgpool_bf16_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t stream) {
+  const int64_t items = static_cast<int64_t>(N) * HW * C;
+  if (items <= 0) return;
+  hipLaunchKernelGGL(k_avgpool_bwd<uint16_t>, dim3(blocks_for(items)), dim3(256), 0, stream, dy, N, HW, C, dx);
 }
 
 }  // namespace gpu

@@ -52,6 +52,15 @@ void linear_f32_fwd(const float* x, const float* w, const float* b, int R, int F
 void linear_f32_dgrad(const float* dl, const float* w, int R, int F, int O, float* dx, hipStream_t stream);
 void linear_f32_wgrad(const float* x, const float* dl, int groups, int rg, int F, int O, float* out, int64_t row_stride,
                       int64_t off_w, int64_t off_b, hipStream_t stream);
+// bf16 classifier (fp32 accumulation, one rounding); the weight gradient is written in the exchange
+// rows' element type odt (gar_device.hpp dtype codes)
+void linear_bf16_fwd(const uint16_t* x, const uint16_t* w, const uint16_t* b, int R, int F, int O, uint16_t* y,
+                     hipStream_t stream);
+void linear_bf16_dgrad(const uint16_t* dl, const uint16_t* w, int R, int F, int O, uint16_t* dx, hipStream_t stream);
+void linear_bf16_wgrad(const uint16_t* x, const uint16_t* dl, int groups, int rg, int F, int O, void* out, int odt,
+                       int64_t row_stride, int64_t off_w, int64_t off_b, hipStream_t stream);
+void avgpool_bf16_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t stream);
+void avgpool_bf16_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t stream);
 void avgpool_f32_fwd(const float* x, int N, int HW, int C, float* y, hipStream_t stream);
 void avgpool_f32_bwd(const float* dy, int N, int HW, int C, float* dx, hipStream_t stream);
 

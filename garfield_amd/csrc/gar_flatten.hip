@@ -6,6 +6,7 @@
 // garfieldpp/worker.py:93-94 (one concat kernel + a D2H copy per worker per step).
 // Here the row stays on the device, the cast is fused, and no intermediate fp32
 // flat vector is materialised.
+#include <vector>
 #include "gar_device.hpp"
 
 namespace garfield {
@@ -217,10 +218,24 @@ __global__ __launch_bounds__(256) void k_split_reduce_multi(SplitTable t) {
 }  // namespace
 
 void split_reduce_multi(const SplitJob* jobs, int count, hipStream_t stream) {
+  // the batched kernel decomposes its element index in 32 bits: a job of 2^31 or more vector
+  // elements (or a launch of 2^31 threads) runs alone on the 64-bit kernel instead
+  constexpr int64_t kLim = (int64_t{1} << 31) - 256;
+  std::vector<SplitJob> small;
+  small.reserve(count);
+  for (int i = 0; i < count; ++i) {
+    const SplitJob& J = jobs[i];
+    const int64_t work = J.Cc * J.R * J.G;     // >= the vector-element count
+    if (work >= kLim - 512) split_reduce(J.part, J.S, J.G, J.R, J.Cc, J.ipitch, J.opitch, J.ss, J.gs, J.out, J.odt,
+                                   J.ostride, stream);
+    else small.push_back(J);
+  }
+  jobs = small.data();
+  count = static_cast<int>(small.size());
   for (int base = 0; base < count; base += kMaxSplitJobs) {
     SplitTable t{};
     t.count = count - base < kMaxSplitJobs ? count - base : kMaxSplitJobs;
-    int32_t blocks = 0;
+    int64_t blocks = 0;
     for (int i = 0; i < t.count; ++i) {
       SplitJob J = jobs[base + i];
       J.vec = (J.Cc % 4 == 0 && J.ipitch % 4 == 0 && J.ss % 4 == 0 && J.gs % 4 == 0 &&
@@ -229,15 +244,21 @@ void split_reduce_multi(const SplitJob* jobs, int count, hipStream_t stream) {
           reinterpret_cast<uintptr_t>(J.out) % 16 == 0)
         J.vec = 2;
       t.job[i] = J;
-      t.blk0[i] = blocks;
       const int64_t cvh = J.vec ? J.Cc / 4 : J.Cc;
+      const int64_t nb = (cvh * J.R * J.G + 255) / 256;
+      if ((blocks + nb) * 256 >= kLim) {     // this job starts the next launch
+        t.count = i;
+        break;
+      }
+      t.blk0[i] = static_cast<int32_t>(blocks);
       t.fcv[i] = dev::make_fastdiv(static_cast<uint32_t>(cvh));
       t.fper[i] = dev::make_fastdiv(static_cast<uint32_t>(cvh * J.R));
-      const int64_t work = (J.vec ? J.Cc / 4 : J.Cc) * J.R * J.G;
-      blocks += static_cast<int32_t>((work + 255) / 256);
+      blocks += nb;
     }
-    t.blk0[t.count] = blocks;
-    if (blocks > 0) hipLaunchKernelGGL(k_split_reduce_multi, dim3(blocks), dim3(256), 0, stream, t);
+    if (t.count == 0) continue;   // unreachable: every job alone is below the limit
+    t.blk0[t.count] = static_cast<int32_t>(blocks);
+    if (blocks > 0) hipLaunchKernelGGL(k_split_reduce_multi, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, t);
+    base -= kMaxSplitJobs - t.count;   // resume after the last job launched
   }
 }
 

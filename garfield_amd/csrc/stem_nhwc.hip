@@ -133,7 +133,7 @@ __device__ __forceinline__ f32x4 mma6(const bf16x8 (&a)[kNP], const bf16x8 (&b)[
 
 template <bool SPLIT, int F>
 __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ x, const uint16_t* __restrict__ w,
-                                                       StemGeo g, void* __restrict__ y) {
+                                                       StemGeo g, void* __restrict__ y, int wpitch) {
   // LDS (dynamic, sized by the host for this geometry): weights [64][160] (x3 split) | staged
   // input rows (+1 zero) (x3 split); the output tile reuses the whole area
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
@@ -151,9 +151,27 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
   uint16_t* patch = lds + NP * kCout * kKP;
   const int pstride = zero + 8;   // elements between the piece arrays of the staged rows
   // weights: the zero-padded [64][160] bf16 matrix (columns in the channels_last weight's
-  // (ky, kx, ci) order; split: its three pieces one after the other), 16-byte loads
-  for (int e = threadIdx.x; e < NP * kCout * kKP / 8; e += kThreads)
-    reinterpret_cast<uint4*>(wl)[e] = reinterpret_cast<const uint4*>(w)[e];
+  // (ky, kx, ci) order; split: its three pieces one after the other), 16-byte loads; or
+  // (wpitch = 147) the channels_last bf16 weight itself, padded while it is staged (no per-step
+  // padding copy)
+  if (wpitch == kKP) {
+    for (int e = threadIdx.x; e < NP * kCout * kKP / 8; e += kThreads)
+      reinterpret_cast<uint4*>(wl)[e] = reinterpret_cast<const uint4*>(w)[e];
+  } else {   // 64 x 147 contiguous bf16 (18816 bytes, 16-byte aligned): 16-byte loads, scattered into rows
+    for (int e = threadIdx.x; e < kCout * kK / 8; e += kThreads) {
+      const uint4 v = reinterpret_cast<const uint4*>(w)[e];
+      const uint32_t h[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int q = e * 8 + i, r = q / kK, c = q - (q / kK) * kK;
+        wl[r * kKP + c] = static_cast<uint16_t>((i & 1) ? (h[i >> 1] >> 16) : (h[i >> 1] & 0xffffu));
+      }
+    }
+    for (int e = threadIdx.x; e < kCout * (kKP - kK); e += kThreads) {
+      const int r = e / (kKP - kK);
+      wl[r * kKP + kK + (e - r * (kKP - kK))] = 0;
+    }
+  }
   stage_rows<SPLIT>(x, g, n, iy0, rows, patch, pstride);
   if (threadIdx.x < NP) patch[threadIdx.x * pstride + zero] = 0;
   __syncthreads();
@@ -386,7 +404,8 @@ bool stem_supported(int H, int W) {
          g.band >= 1 && gs.band >= 1;
 }
 
-void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream) {
+void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream,
+              int wpitch) {
   const StemGeo g = geo(N, H, W, split);
   const int T = 64 * (split ? kFwdFragSplit : kFwdFragBf16);
   const int tiles = (g.Ho * g.Wo + T - 1) / T;
@@ -396,10 +415,12 @@ void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W,
   if (lds < tile) lds = tile;
   if (split) {
     allow_lds(k_stem_fwd<true, kFwdFragSplit>, lds);
-    hipLaunchKernelGGL((k_stem_fwd<true, kFwdFragSplit>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
+    hipLaunchKernelGGL((k_stem_fwd<true, kFwdFragSplit>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y,
+                       kKP);
   } else {
     allow_lds(k_stem_fwd<false, kFwdFragBf16>, lds);
-    hipLaunchKernelGGL((k_stem_fwd<false, kFwdFragBf16>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y);
+    hipLaunchKernelGGL((k_stem_fwd<false, kFwdFragBf16>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y,
+                       wpitch == kK ? kK : kKP);
   }
 }
 

@@ -984,7 +984,7 @@ class _GroupedConv(torch.autograd.Function):
             ctx.save_for_backward(x, w)
             ho, wo = _out_hw(spec, h, wd)
             y = torch.empty((n, 64, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-            _native.native().gpu_stem_fwd(x, _wmat(w, 160, spec), y)
+            _native.native().gpu_stem_fwd(x, w, y)   # the weight is padded while the kernel stages it
             return y
         if _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
             ctx.mode = "iconv"
@@ -1190,15 +1190,35 @@ class LinearSpec:
         self.groups = groups
 
 
+# outputs up to which the bf16 classifier runs on its own streaming kernels (conv_f32.hip: the CIFAR
+# 10-class head is an 8 MB HBM stream, not a GEMM); a 1000-class ImageNet head is a real GEMM
+# (8 GFLOP) and stays on hipBLASLt
+_LINEAR_BF16_MAX_O = 16
+
+
+def _native_linear(x: torch.Tensor, w: torch.Tensor) -> str | None:
+    """The classifier's own kernels (conv_f32.hip: fp32 accumulation, one rounding): "f32" / "bf16"
+    for matching GPU operands, None for the CPU path (and the wide bf16 head, see above)."""
+    if not x.is_cuda:
+        return None
+    if x.dtype == torch.float32 and w.dtype == torch.float32:
+        return "f32"
+    if x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+        return "bf16" if w.shape[0] <= _LINEAR_BF16_MAX_O and x.shape[1] % 8 == 0 else None
+    raise TypeError(f"grouped linear on the GPU: fp32 or bf16 operands, got {x.dtype} x {w.dtype}")
+
+
 class _GroupedLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, spec: LinearSpec):
         ctx.spec = spec
         ctx.save_for_backward(x, w)
-        if x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32:   # the fp32 step's own kernel
+        kind = _native_linear(x, w)
+        if kind is not None:   # no library GEMM: the classifier's own kernel
             y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
-            _native.native().gpu_linear_f32_fwd(x.contiguous(), w.contiguous(),
-                                                b.detach() if b is not None else None, y)
+            bb = b.detach().to(x.dtype).contiguous() if b is not None else None
+            fwd = _native.native().gpu_linear_f32_fwd if kind == "f32" else _native.native().gpu_linear_bf16_fwd
+            fwd(x.contiguous(), w.contiguous(), bb, y)
             return y
         return F.linear(x, w, b)
 
@@ -1208,8 +1228,11 @@ class _GroupedLinear(torch.autograd.Function):
         spec = ctx.spec
         G = spec.groups
         dy = dy.contiguous()
-        if dy.is_cuda and dy.dtype == torch.float32 and w.dtype == torch.float32:
+        kind = _native_linear(x, w) if dy.is_cuda else None
+        if kind == "f32":
             return _linear_f32_backward(ctx, x, w, dy, spec, G)
+        if kind == "bf16":
+            return _linear_bf16_backward(ctx, x, w, dy.to(torch.bfloat16), spec, G)
         dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
         if spec.sink is not None:
             out, fin = dy.shape[1], x.shape[1]
@@ -1253,8 +1276,33 @@ def _linear_f32_backward(ctx, x, w, dy, spec: LinearSpec, G: int):
     return dx, None, None, None
 
 
+def _linear_bf16_backward(ctx, x, w, dy, spec: LinearSpec, G: int):
+    """bf16 classifier backward on the native kernels: dx = dy·W, and every worker's dW / db (fp32
+    sums, one rounding) written straight into its exchange row (any exchange dtype)."""
+    C_ = _native.native()
+    dx = None
+    if ctx.needs_input_grad[0]:
+        dx = torch.empty_like(x)
+        C_.gpu_linear_bf16_dgrad(dy, w.contiguous(), dx)
+    sink = spec.sink
+    if sink is not None:
+        lin = spec.lin
+        if sink.flat.is_cuda and sink.flat.dtype in (torch.float32, torch.bfloat16, torch.float16):
+            ob = sink.base + sink.offset(lin.bias) if lin.bias is not None else -1
+            C_.gpu_linear_bf16_wgrad(x.contiguous(), dy, G, sink.flat, sink.row_stride,
+                                     sink.base + sink.offset(lin.weight), ob)
+        else:
+            x3 = x.contiguous().view(G, -1, x.shape[1]).float()
+            dy3 = dy.view(G, -1, dy.shape[1]).float()
+            sink.put_groups(lin.weight, torch.bmm(dy3.transpose(1, 2), x3))
+            if lin.bias is not None:
+                sink.put_groups(lin.bias, dy3.sum(1))
+    return dx, None, None, None
+
+
 class _AvgPoolF32(torch.autograd.Function):
-    """Global average pool of an fp32 NHWC activation on the native kernel (no ATen reduction)."""
+    """Global average pool of an fp32 or bf16 NHWC activation on the native kernel (no ATen
+    reduction)."""
 
     @staticmethod
     def forward(ctx, x):
@@ -1276,7 +1324,7 @@ def global_avgpool(x: torch.Tensor) -> torch.Tensor:
     n, c, h, w = x.shape
     if h * w == 1:
         return x.reshape(n, c)
-    if x.is_cuda and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last):
+    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.is_contiguous(memory_format=torch.channels_last):
         return _AvgPoolF32.apply(x)
     return x.mean((2, 3))
 

@@ -75,6 +75,16 @@ def init_distributed(backend: str | None = None, device: str | None = None, time
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
         ctx.initialized_here = True
+    elif world == 1 and use_cuda and os.environ.get("GARFIELD_DIRECT_RCCL_WORLD1") == "1" and not dist.is_initialized():
+        # a one-rank RCCL communicator for the direct path's world-1 run (parallel/sharded.py)
+        import socket
+
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+        ctx.initialized_here = True
     return ctx
 
 

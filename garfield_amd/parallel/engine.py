@@ -56,8 +56,8 @@ LAYERWISE_RULES = {"krum", "bulyan", "brute", "aksel"}   # per-layer != flat onl
 LW_DEVICE = os.environ.get("GARFIELD_LW_DEVICE", "1") != "0"
 LW_JOB = 32768   # coordinates per job of the segmented kernels (a multiple of 8)
 # fp32 (no autocast) worker batching on the GPU (the reference's precision): "1" (default) the grouped
-# NHWC executor on the fp32 kernels (conv_f32.hip, split-bf16 MFMA; bn_nhwc.hip in fp32), "channel" the
-# grouped-channel executor on ATen / hipBLASLt (parallel/grouped_fp32.py), "0" the per-worker path.
+# NHWC executor on the fp32 kernels (conv_f32.hip, split-bf16 MFMA; bn_nhwc.hip in fp32), "0" the
+# per-worker path.
 FP32_GROUPED = os.environ.get("GARFIELD_FP32_GROUPED", "1")
 # sharded steps with a comm stream: the grouped step captured as stages cut at the bucket boundaries,
 # so the next forward's early layers run beside the late buckets' updates / all-gathers ("0": one graph)
@@ -180,6 +180,7 @@ class RobustDataParallel:
         if ctx.is_distributed:
             dist.broadcast(self.flat.data, src=0)
         self.d, self.ld = self.flat.d, self.flat.ld
+        self.flat.before_read = self.synchronize    # readers of the weights join a staged step first
         self.work_params = list(self.flat.params)   # what forward/backward sees (see _install_shadow)
         self._shadow = None
         self._install_shadow()
@@ -229,12 +230,9 @@ class RobustDataParallel:
     def _want_grouping(self, model: nn.Module) -> bool:
         from garfield_amd.parallel import grouped
 
-        from garfield_amd.parallel import grouped_fp32
-
         wb = self.cfg.worker_batching
         if wb is None:
             wb = self.device.type == "cuda"
-        self._fp32_grouped = False      # the grouped-channel executor (fp32, ATen)
         self._fp32_nhwc = False         # the grouped NHWC executor in fp32 (own kernels)
         if not (wb and self._supports_grouping):
             return False
@@ -244,11 +242,6 @@ class RobustDataParallel:
                 return grouped.supports(model)
             # the reference's fp32: fp32 activations and weights on the fp32 grouped kernels
             if self.cfg.autocast_dtype is None and not self.cfg.lp_weights and FP32_GROUPED != "0":
-                if FP32_GROUPED == "channel":
-                    if not self.cfg.channels_last and grouped_fp32.supports(model):
-                        self._fp32_grouped = True
-                        return True
-                    return False
                 if grouped.supports(model):
                     self._fp32_nhwc = True
                     return True
@@ -256,7 +249,7 @@ class RobustDataParallel:
         return grouped.supports(model)
 
     def _want_sharded(self) -> bool:
-        from garfield_amd.parallel.sharded import SUPPORTED
+        from garfield_amd.parallel.sharded import SUPPORTED, layerwise_device_ok
 
         sg = self.cfg.shard_gar
         if sg is None:   # default: on for multi-rank jobs
@@ -267,6 +260,10 @@ class RobustDataParallel:
             raise ValueError("sharded aggregation over several ranks needs an initialised process group")
         if self.cfg.gar not in SUPPORTED:
             raise ValueError(f"sharded aggregation does not support {self.cfg.gar!r} (shard_gar=False)")
+        if (self.cfg.layerwise and self.cfg.gar in LAYERWISE_RULES and self.device.type == "cuda"
+                and not layerwise_device_ok(self.cfg.gar, self.cfg.workers_per_rank * self.ctx.world_size,
+                                            self.cfg.f)):
+            return False   # beyond the segmented device kernels: the unsharded per-segment loop
         return True
 
     def _gather_slot(self, j: int):
@@ -274,6 +271,16 @@ class RobustDataParallel:
         if self.world == 1 or self._sharded:
             return None
         return all_gather_rows(self.X[j], self.rank, async_op=True)
+
+    def synchronize(self) -> None:
+        """Make the current stream wait for every update, weight all-gather and BatchNorm-affine
+        scatter of the last step still in flight on the comm stream. A staged sharded step
+        returns before its layer3/layer4 buckets are updated (the next step's forward stages wait
+        on them on the device); any other reader of ``model.parameters()`` / ``flat.data`` calls
+        this first. The flat-vector readers (``flat.vector``, ``flat.reference_vector``,
+        checkpoints) and ``evaluate`` do so themselves."""
+        if getattr(self, "_shard", None) is not None:
+            self._shard.join()
 
     def set_lr(self, lr: float) -> None:
         """Learning rate of the next updates (a scheduler hook): the fused combine + SGD
@@ -296,13 +303,8 @@ class RobustDataParallel:
         from garfield_amd.parallel.sharded import overlap_enabled
 
         buckets = ("layer4", "layer3") if self._sharded else ()
-        if getattr(self, "_fp32_grouped", False):
-            from garfield_amd.parallel.grouped_fp32 import GroupedChannelResNet
-
-            self._gexec = GroupedChannelResNet(self.model, self.k, sink, loss_fn, offsets=offsets)
-        else:
-            self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn, marks=buckets, offsets=offsets,
-                                        signals=overlap_enabled(self.ctx.world_size))
+        self._gexec = GroupedResNet(self.model, self.k, sink, loss_fn, marks=buckets, offsets=offsets,
+                                    signals=overlap_enabled(self.ctx.world_size))
         self._gx = self._gy = None
         self._gsrc = None
         self._gsrc_refs = None
@@ -759,10 +761,9 @@ class RobustDataParallel:
     def _ensure_gbuf(self, B: int, sample_shape: tuple, label_shape: tuple = (), label_dtype=torch.int64) -> None:
         shape = (self.k * B, *sample_shape)
         if self._gx is None or tuple(self._gx.shape) != shape:
-            fp32 = getattr(self, "_fp32_grouped", False) or getattr(self, "_fp32_nhwc", False)
+            fp32 = getattr(self, "_fp32_nhwc", False)
             dt = torch.bfloat16 if (self.device.type == "cuda" and not fp32) else torch.float32
-            fmt = torch.contiguous_format if getattr(self, "_fp32_grouped", False) else torch.channels_last
-            self._gx = torch.empty(shape, dtype=dt, device=self.device, memory_format=fmt)
+            self._gx = torch.empty(shape, dtype=dt, device=self.device, memory_format=torch.channels_last)
             self._gy = torch.empty((self.k * B, *label_shape), dtype=label_dtype, device=self.device)
             self._ggraph = None
             self._gsrc = None
@@ -771,7 +772,7 @@ class RobustDataParallel:
         """The grouped step's static input buffers ([k*batch, *sample_shape] channels_last, bf16 or
         fp32 by the step's precision, and the labels) for a producer that writes each step's batch in place
         (``data.fresh.DeviceBatches.attach``): no staging copy. None when the step is not grouped."""
-        if self._gexec is None or getattr(self, "_fp32_grouped", False):   # the producer writes NHWC rows
+        if self._gexec is None:
             return None
         self._ensure_gbuf(int(batch), tuple(sample_shape), (), label_dtype)
         return self._gx, self._gy

@@ -35,8 +35,14 @@ class DirectRCCL:
     @classmethod
     def create(cls, group=None) -> "DirectRCCL | None":
         """The direct path for the default (or given) NCCL process group, or None (another
-        backend, ``GARFIELD_DIRECT_RCCL=0``, or the library / communicator unavailable)."""
-        if os.environ.get("GARFIELD_DIRECT_RCCL", "1") == "0" or not dist.is_initialized():
+        backend, not enabled, or the library / communicator unavailable).
+
+        Opt-in (``GARFIELD_DIRECT_RCCL=1``): the point-to-point exchange straight from the
+        exchange rows and the staged next forward it enables have run on one GPU only (the
+        one-rank test ``tests/test_rccl_gpu.py`` and the gloo contract rehearsals), never over
+        xGMI between GPUs, so multi-rank jobs default to torch.distributed's packed
+        ``all_to_all_single`` and the one-graph step."""
+        if not direct_enabled() or not dist.is_initialized():
             return None
         pg = group or dist.distributed_c10d._get_default_group()
         if dist.get_backend(pg) != "nccl":
@@ -60,6 +66,8 @@ class DirectRCCL:
     def exchange(self, sends: list, to: list, recvs: list, frm: list, stream) -> None:
         """One group of ncclSend(sends[i] -> rank to[i]) / ncclRecv(recvs[i] <- rank frm[i]);
         transfers between one pair of ranks match in issue order."""
+        if not sends and not recvs:   # one rank: nothing leaves
+            return
         self._C.rccl_exchange(self.comm, sends, to, recvs, frm, self.world, stream.cuda_stream)
 
     def all_gather(self, send: torch.Tensor, recv: torch.Tensor, stream) -> None:
@@ -165,6 +173,10 @@ class GlooDirect:
 _OVERRIDE = None
 
 
+def direct_enabled() -> bool:
+    return os.environ.get("GARFIELD_DIRECT_RCCL", "0") == "1"
+
+
 def set_direct_backend(factory) -> None:
     """``factory(world, rank)`` -> the direct backend every ``ShardedAggregator`` built next
     uses at world > 1 (e.g. ``GlooDirect`` in the CPU rehearsals); None restores the default
@@ -173,10 +185,11 @@ def set_direct_backend(factory) -> None:
     _OVERRIDE = factory
 
 
-def direct_backend(world: int, rank: int, side: bool):
+def direct_backend(world: int, rank: int, side: bool, world1: bool = False):
     """The direct backend of a sharded exchange: the override when set, else DirectRCCL when the
-    exchange has its own comm stream and several ranks."""
-    if world <= 1:
+    exchange has its own comm stream and several ranks (``world1``: also on one rank, the
+    test/trace run of the multi-rank call sequence)."""
+    if world <= 1 and not world1:
         return None
     if _OVERRIDE is not None:
         return _OVERRIDE(world, rank)

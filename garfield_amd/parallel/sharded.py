@@ -67,6 +67,20 @@ SUPPORTED = DISTANCE_RULES | {"average", "aksel", "median", "trimmed-mean", "ave
                               "condense"}
 
 
+def layerwise_device_ok(rule: str, n: int, f: int) -> bool:
+    """Whether the sharded GPU layer-wise path's device kernels take this configuration:
+    the segmented Gram (``gpu_lw_gram``) and the batched selections need n <= MAX_ROWS, the
+    layer-wise Bulyan tail t = n - 2f - 2 <= 64 selected rows, Brute's subset search n <= 64.
+    Other configurations keep the unsharded engine's per-segment loop."""
+    if n > gar.MAX_ROWS:
+        return False
+    if rule == "bulyan":
+        return n - 2 * f - 2 <= 64
+    if rule == "brute":
+        return n <= 64
+    return True
+
+
 def shard_pad(world: int, base: int = 64) -> int:
     """Row padding such that every shard is a whole number of 64-element (16-byte aligned) blocks."""
     return base * world
@@ -125,11 +139,16 @@ class ShardedAggregator:
         # (world 1 without the loopback exchange: nothing to overlap, and a second active
         # queue alone costs the main stream's graph ~4-5 % (profiles/r3/probe_cross_stream.log):
         # everything stays on the main stream)
-        side = dev.type == "cuda" and (self.world > 1 or loopback_enabled() or overlap_enabled(self.world))
+        forced = dev.type == "cuda" and self.world == 1 and direct_world1()
+        side = dev.type == "cuda" and (self.world > 1 or loopback_enabled() or overlap_enabled(self.world) or forced)
         self._comm_stream = torch.cuda.Stream(dev) if side else None
         self._handoff = Handoff(dev) if side else None
         # RCCL kernels straight onto the comm stream (rccl.py); None: torch.distributed
-        self._rccl = direct_backend(self.world, self.rank, side)
+        self._rccl = direct_backend(self.world, self.rank, side, forced)
+        # whether the step issues its collectives: several ranks, or the one-rank run of the
+        # direct RCCL path (GARFIELD_DIRECT_RCCL_WORLD1=1, tests and traces: real RCCL calls on a
+        # one-rank communicator beside the staged graphs, no shortcut taken for world 1)
+        self._coll = self.world > 1 or self._rccl is not None
         # ready order of the backward: highest coordinates (last layers) first
         self.buckets = [_Bucket(edges[i], edges[i + 1], self.world, self.rank, self.k, dev, dt, self._rccl is None)
                         for i in reversed(range(len(edges) - 1))]
@@ -192,7 +211,7 @@ class ShardedAggregator:
         e = self.e
         for b in self.buckets:
             b.np = None
-        if e._shadow is None or self.world == 1:
+        if e._shadow is None or not self._coll:
             return
         lp = e.shadow_param_ids()
         idx = []
@@ -256,7 +275,7 @@ class ShardedAggregator:
             with ctx:
                 e._attack_rows(b.lo, b.hi)
                 b.works = []
-                if self.world > 1 and self._rccl is not None:   # straight from the exchange rows
+                if self._coll and self._rccl is not None:   # straight from the exchange rows
                     self._rccl.exchange(*b.p2p, self._comm_stream)
                 elif self.world > 1:
                     local = e.X[:, 0, b.lo:b.hi].view(self.k, self.world, b.S).transpose(0, 1)   # [dst, j, S]
@@ -277,12 +296,12 @@ class ShardedAggregator:
 
     def _sum_over_ranks(self, t: torch.Tensor) -> torch.Tensor:
         """Every rank's ``t`` summed in rank order (identical result on every rank)."""
-        if self.world == 1:
+        if not self._coll:
             return t.clone()
         return self._gather_ranks(t).sum(0)
 
     def _concat_ranks(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if not self._coll:
             return t
         return self._gather_ranks(t).view(-1, *t.shape[1:])
 
@@ -330,7 +349,7 @@ class ShardedAggregator:
         reads directly (BatchNorm affine): on RCCL it runs beside the remaining buckets'
         updates. ``handoff=False``: the update was issued on the comm stream itself."""
         e = self.e
-        if self.world == 1:
+        if not self._coll:
             return
         buf = e._shadow if e._shadow is not None else e.flat.data
         full, mine = buf[b.lo:b.hi], buf[b.own]
@@ -358,7 +377,7 @@ class ShardedAggregator:
         (the main stream waits for the comm stream, or, with the next forward staged, each
         stage waits for its buckets' events: ``stage_waits``), host-side for torch.distributed."""
         e = self.e
-        if self.world == 1:
+        if not self._coll:
             if e._shadow is not None and e.device.type != "cuda":
                 with torch.no_grad():
                     e._shadow.copy_(e.flat.data)
@@ -402,7 +421,7 @@ class ShardedAggregator:
             else:
                 fn(b)
                 self._gather_bucket(b)
-            if staged and (i > 0 or self.world > 1):
+            if staged and (i > 0 or self._coll):
                 ev = torch.cuda.Event(enable_timing=_TIMING)
                 ev.record(self._comm_stream)
                 self._ready.append((b.lo, ev))
@@ -705,15 +724,29 @@ class ShardedAggregator:
         self._lwp = plan
         return plan
 
-    def _lw_aksel_weights(self, cfg, plan, Xs: dict) -> torch.Tensor:
+    _AKSEL_CHUNK = 1 << 20   # coordinates per distance chunk: n x 1M x 8 B of transient memory
+
+    def _lw_aksel_weights(self, cfg, plan, buckets) -> torch.Tensor:
         """Layer-wise Aksel: per segment, the c rows closest (squared distance, summed over the owned
-        coordinates of every rank) to the coordinate-wise median get weight 1/c (ties by slot)."""
+        coordinates of every rank) to the coordinate-wise median get weight 1/c (ties by slot).
+        ``buckets`` yields (bucket lo, its [n] owned row shards) one bucket at a time (on the GPU as
+        each lands); the distances are accumulated per coordinate chunk, so the transient memory is
+        one chunk of the rows, not fp32/fp64 copies of every bucket."""
         n, L = self.n, plan["L"]
-        D = torch.zeros((n, L + 1), dtype=torch.float64, device=self.e.device)
-        for b in self.buckets:
-            X = Xs[b.lo]
-            med = gar.aggregate("median", X).to(X.dtype)
-            D.index_add_(1, plan["seg_id"][b.lo], ((X - med) ** 2).double())
+        e = self.e
+        D = torch.zeros((n, L + 1), dtype=torch.float64, device=e.device)
+        for lo, rows in buckets:
+            S = rows[0].numel()
+            if e.device.type == "cuda":
+                med = self._ws_any().get("lw_aksel_med", S)[:S]
+                e._C.gpu_coordwise(rows, gar._MODE["median"], 0, 0, None, 0, 0, 1.0, med)
+            else:
+                med = gar.aggregate("median", torch.stack([r.float() for r in rows])).float()
+            sid = plan["seg_id"][lo]
+            for a in range(0, S, self._AKSEL_CHUNK):
+                z = min(S, a + self._AKSEL_CHUNK)
+                X = torch.stack([r[a:z] for r in rows]).float()
+                D.index_add_(1, sid[a:z], ((X - med[a:z]) ** 2).double())
         D = self._sum_over_ranks(D[:, :L].t().contiguous())
         D = torch.where(torch.isfinite(D), D, torch.full_like(D, math.inf))
         c = (n + 1) // 2 if dict(cfg.gar_kwargs).get("mode", "mid") == "mid" else n - cfg.f
@@ -732,10 +765,11 @@ class ShardedAggregator:
             C = e._C
             args = (cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
             if rule == "aksel":
-                for b in self.buckets:
-                    self._wait(b)
-                w = self._lw_aksel_weights(cfg, plan, {b.lo: torch.stack(b.rows).float() for b in self.buckets})
-                plan["w"].copy_(w)
+                def landed():
+                    for b in self.buckets:
+                        self._wait(b)
+                        yield b.lo, b.rows
+                plan["w"].copy_(self._lw_aksel_weights(cfg, plan, landed()))
             else:
                 total = None
                 for b in self.buckets:          # partial per-segment Grams as the buckets land
@@ -784,7 +818,7 @@ class ShardedAggregator:
         Xs = {b.lo: torch.stack([r.float() for r in b.rows]) for b in self.buckets}   # [n, S] owned shards
         Cn = _native.require_for(torch.empty(0))
         if rule == "aksel":
-            W = self._lw_aksel_weights(cfg, plan, Xs)
+            W = self._lw_aksel_weights(cfg, plan, ((b.lo, list(Xs[b.lo])) for b in self.buckets))
         else:
             D = torch.zeros((L, n, n), dtype=torch.float64)
             for b in self.buckets:
@@ -928,6 +962,14 @@ class _nullctx:
 # GARFIELD_EXCHANGE_TIMING=1: the per-bucket "exchange issued" events are timing events
 # (scripts/overlap_timing.py reads them against the step's start and its backward's end)
 _TIMING = os.environ.get("GARFIELD_EXCHANGE_TIMING", "0") == "1"
+
+
+def direct_world1() -> bool:
+    """GARFIELD_DIRECT_RCCL_WORLD1=1 (with GARFIELD_DIRECT_RCCL=1, on a one-rank NCCL process
+    group): the sharded step at world 1 issues every collective of the multi-rank step through
+    the direct RCCL path on the comm stream, instead of taking the world-1 shortcuts (tests,
+    traces)."""
+    return os.environ.get("GARFIELD_DIRECT_RCCL_WORLD1", "0") == "1"
 
 
 def loopback_enabled() -> bool:

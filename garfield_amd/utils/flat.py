@@ -122,6 +122,13 @@ class FlatParams:
         if with_grad:
             self.grad = torch.zeros(self.ld, dtype=dtype, device=device)
             self.attach_grads(self.grad)
+        # called before the readers below: an engine whose updates may still be in flight on a
+        # side stream (a staged sharded step) installs its ``synchronize`` here
+        self.before_read = None
+
+    def _sync(self) -> None:
+        if self.before_read is not None:
+            self.before_read()
 
     def views(self, flat: torch.Tensor):
         """Per-parameter views (parameter strides) of a flat buffer laid out like ``data``;
@@ -136,6 +143,7 @@ class FlatParams:
             p.grad = v
 
     def vector(self) -> torch.Tensor:
+        self._sync()
         return self.data[: self.d]
 
     def grad_vector(self) -> torch.Tensor:
@@ -143,9 +151,11 @@ class FlatParams:
 
     def reference_vector(self) -> torch.Tensor:
         """Reference interchange layout: cat of p.view(-1) (logical order)."""
+        self._sync()
         return flatten(p.detach() for p in self.params)
 
     def load_reference_vector(self, flat: torch.Tensor) -> None:
+        self._sync()
         with torch.no_grad():
             pos = 0
             for p, n in zip(self.params, self.numels):
@@ -155,6 +165,7 @@ class FlatParams:
     def to_reference(self, buf: torch.Tensor) -> torch.Tensor:
         """A buffer laid out like ``data`` (memory order, e.g. the momentum) in the
         reference layout (logical ``p.view(-1)`` order per parameter)."""
+        self._sync()
         return flatten(v.detach() for v in self.views(buf))
 
     def from_reference(self, flat: torch.Tensor, buf: torch.Tensor) -> torch.Tensor:

@@ -259,3 +259,18 @@ def test_two_rank_sharded_layerwise_krum_matches_redundant():
         assert rel < 1e-5, rel
         m0, m1 = r["0r0"]["mom"], r["1r0"]["mom"]
         assert ((m1 - m0).norm() / m0.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("rule,n,f,ok", [
+    ("krum", 64, 2, True), ("krum", 256, 2, False),
+    ("bulyan", 64, 3, True), ("bulyan", 72, 1, False), ("bulyan", 128, 31, True), ("bulyan", 128, 30, False),
+    ("brute", 64, 1, True), ("brute", 72, 1, False),
+    ("aksel", 128, 2, True), ("aksel", 256, 2, False),
+])
+def test_sharded_layerwise_routing_respects_device_limits(rule, n, f, ok):
+    """Multi-rank layer-wise runs take the sharded device path only inside its kernels' limits
+    (segmented Gram n <= 128, Bulyan tail t <= 64, Brute n <= 64); beyond them the engine keeps
+    the unsharded per-segment loop instead of failing after the exchange."""
+    from garfield_amd.parallel.sharded import layerwise_device_ok
+
+    assert layerwise_device_ok(rule, n, f) == ok

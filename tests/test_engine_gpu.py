@@ -273,13 +273,13 @@ def test_layerwise_krum_device_equals_segment_loop_bitwise(cuda, monkeypatch, mo
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("graph", [False, True])
-def test_fp32_grouped_channel_path_matches_per_worker_engine(cuda, graph):
-    """fp32 (the reference's precision) with worker batching: the grouped-channel executor
-    (MIOpen grouped convolutions, per-(worker, channel) BatchNorm) against the per-worker fp32
+def test_fp32_grouped_path_matches_per_worker_engine(cuda, graph):
+    """fp32 (the reference's precision) with worker batching: the grouped NHWC executor on the
+    fp32 kernels (conv_f32.hip split-bf16 MFMA, bn_nhwc.hip in fp32) against the per-worker fp32
     engine. The two run different convolution algorithms (fp32 rounding differs by ~1e-3 of a
     gradient), so: the first update within 2e-2 and the parameters within 2e-3 after 3 averaged
-    steps (reference layout), HIP-graph replays included. The exact math
-    is checked in fp64 on the CPU (tests/test_grouped_fp32_cpu.py)."""
+    steps (reference layout), HIP-graph replays included. The exact grouped math is checked in
+    fp64 on the CPU (tests/test_grouped_cpu.py)."""
     outs, deltas = [], []
     for wb in (False, True):
         torch.manual_seed(0)

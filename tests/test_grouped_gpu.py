@@ -499,3 +499,50 @@ def test_headline_path_trains_like_fp32(cuda):
     print(f"last-10 mean loss: grouped bf16 {lb:.4f}, fp32 {lf:.4f}; first {bf[0]:.4f} / {fp[0]:.4f}")
     assert lb < 0.6 * math.log(10), (lb, bf[::10])
     assert abs(lb - lf) <= 0.05 + 0.05 * lf, (lb, lf)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,B,F_,O,xdt", [(8, 250, 2048, 10, torch.bfloat16), (3, 7, 512, 16, torch.float32),
+                                          (2, 5, 96, 10, torch.bfloat16), (3, 7, 512, 37, torch.float32)])
+def test_grouped_linear_bf16_matches_fp32_reference(cuda, native, G, B, F_, O, xdt):
+    """The bf16 classifier on its own kernels (no hipBLASLt / ATen): forward, data gradient and every
+    worker's dW / db written into its exchange row (bf16 or fp32 rows), against an fp32 PyTorch
+    reference of the same op on the same bf16 operands (fp32 accumulation, one rounding)."""
+    from garfield_amd.ops.grouped import LinearSpec, grouped_linear
+
+    torch.manual_seed(0)
+    lin = nn.Linear(F_, O).to(cuda).to(torch.bfloat16)
+    R = G * B
+    x = torch.randn(R, F_, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    d = sum(p.numel() for p in lin.parameters())
+    flat = torch.zeros(G, d + 64, dtype=xdt, device=cuda)
+    offsets = {id(lin.weight): 0, id(lin.bias): O * F_}
+    sink = GradSink(flat.view(-1), d + 64, 0, offsets, G)
+    y = grouped_linear(x, LinearSpec(lin, sink, G))
+    dy = torch.randn(R, O, device=cuda).to(torch.bfloat16)
+    y.backward(dy)
+    sink.flush()
+    xf, wf, bf, dyf = x.detach().float(), lin.weight.detach().float(), lin.bias.detach().float(), dy.float()
+    assert rel(y.float(), xf @ wf.t() + bf) < 1e-2
+    assert rel(x.grad.float(), dyf @ wf) < 1e-2
+    for g in range(G):
+        sl = slice(g * B, (g + 1) * B)
+        dw = dyf[sl].t() @ xf[sl]
+        db = dyf[sl].sum(0)
+        assert rel(flat[g, :O * F_].float().view(O, F_), dw) < 1e-2
+        assert rel(flat[g, O * F_:O * F_ + O].float(), db) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,C,H", [(16, 2048, 7), (5, 64, 3)])
+def test_global_avgpool_bf16_matches_mean(cuda, N, C, H):
+    from garfield_amd.ops.grouped import global_avgpool
+
+    x = torch.randn(N, C, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = global_avgpool(x)
+    dy = torch.randn(N, C, device=cuda).to(torch.bfloat16)
+    y.backward(dy)
+    assert rel(y.float(), x.detach().float().mean((2, 3))) < 1e-2
+    ref = (dy.float() / (H * H))[:, :, None, None].expand(N, C, H, H)
+    assert rel(x.grad.float(), ref) < 1e-2

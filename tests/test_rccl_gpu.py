@@ -31,9 +31,10 @@ def one_rank_nccl():
         dist.destroy_process_group()
 
 
-def test_direct_rccl_calls_on_one_rank(one_rank_nccl):
+def test_direct_rccl_calls_on_one_rank(one_rank_nccl, monkeypatch):
     from garfield_amd.parallel.rccl import DirectRCCL
 
+    monkeypatch.setenv("GARFIELD_DIRECT_RCCL", "1")
     dev = one_rank_nccl
     d = DirectRCCL.create()
     assert d is not None, "the direct RCCL path must bind on a GPU box"
@@ -63,3 +64,36 @@ def test_direct_rccl_calls_on_one_rank(one_rank_nccl):
         d.all_gather(out, out, s)
     s.synchronize()
     assert torch.equal(out, blk)
+
+
+def test_sharded_step_on_direct_rccl_one_rank_equals_loopback(one_rank_nccl, monkeypatch):
+    """The full sharded grouped step with its collectives issued through the direct RCCL path on
+    a one-rank communicator (GARFIELD_DIRECT_RCCL_WORLD1=1): the partial-Gram all-gather, the
+    in-place bf16 weight all-gathers and the BatchNorm-affine all-reduce run as real RCCL calls on
+    the comm stream, beside the next step's staged three-graph forward, with the in-graph bucket
+    signals on. Ten steps with fresh inputs must be bitwise equal to the same step without the
+    collectives (the world-1 loopback run of the same machinery)."""
+    import torch.nn.functional as F
+
+    from garfield_amd.models import build_model
+    from garfield_amd.parallel.comm import DistContext
+    from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synthetic_batches
+
+    dev = one_rank_nccl
+    monkeypatch.setenv("GARFIELD_LOOPBACK_EXCHANGE", "1")
+    monkeypatch.setenv("GARFIELD_OVERLAP", "1")
+    outs = []
+    for direct in ("0", "1"):
+        monkeypatch.setenv("GARFIELD_DIRECT_RCCL", direct)
+        monkeypatch.setenv("GARFIELD_DIRECT_RCCL_WORLD1", direct)
+        torch.manual_seed(0)
+        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, shard_gar=True, lr=0.01, cuda_graph=True)
+        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=dev), cfg)
+        assert (eng._shard._rccl is not None) == (direct == "1")
+        for it in range(10):
+            eng.step(synthetic_batches(8, 8, (3, 32, 32), 10, dev, seed=300 + it))
+        eng.synchronize()
+        torch.cuda.synchronize()
+        assert isinstance(eng._ggraph, list) and len(eng._ggraph) == 3 and eng._shard.staged
+        outs.append((eng.flat.reference_vector().clone(), eng.momentum_vector().clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
