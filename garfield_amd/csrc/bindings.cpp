@@ -365,15 +365,21 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
                   const c10::optional<at::Tensor>& gamma, const c10::optional<at::Tensor>& beta, double eps,
                   double momentum, const c10::optional<at::Tensor>& run_mean,
                   const c10::optional<at::Tensor>& run_var, const at::Tensor& part, const at::Tensor& mean,
-                  const at::Tensor& istd, const at::Tensor& scale, const at::Tensor& shift, const at::Tensor& y,
-                  bool relu, const c10::optional<at::Tensor>& mask, bool defer_running,
+                  const at::Tensor& istd, const at::Tensor& scale, const at::Tensor& shift,
+                  const c10::optional<at::Tensor>& y, bool relu, const c10::optional<at::Tensor>& mask,
+                  bool defer_running,
                   const c10::optional<at::Tensor>& tile_stats, int64_t tile_m, int64_t tile_e) {
   const auto dev = x.device();
   const int dt = check_act_rows(x, dev, "x");
-  check_act_rows(y, dev, "y", dt);
-  TORCH_CHECK(y.sizes() == x.sizes(), "garfield bn: y must have x's shape");
+  void* yp = nullptr;
+  if (y.has_value() && y->defined()) {
+    check_act_rows(*y, dev, "y", dt);
+    TORCH_CHECK(y->sizes() == x.sizes(), "garfield bn: y must have x's shape");
+    yp = y->data_ptr();
+  }
   uint8_t* mp = nullptr;
   if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(yp != nullptr, "garfield bn: a ReLU mask comes with the apply pass (y)");
     TORCH_CHECK(relu, "garfield bn: a ReLU mask needs relu=True");
     check_relu_mask(*mask, x);
     mp = static_cast<uint8_t*>(mask->data_ptr());
@@ -406,7 +412,7 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
   }
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::bn_forward(x.data_ptr(), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
-                            static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, y.data_ptr(), relu, mp,
+                            static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, yp, relu, mp,
                             defer_running, stream_of(dev), ts, tile_m, static_cast<int>(tile_e), dt);
 }
 
@@ -486,7 +492,8 @@ void g_bn_backward(const at::Tensor& x, const at::Tensor& dy, const c10::optiona
                    const c10::optional<at::Tensor>& gamma, const at::Tensor& mean, const at::Tensor& istd,
                    const at::Tensor& part, const at::Tensor& coef, const at::Tensor& dx,
                    const c10::optional<at::Tensor>& dres, const c10::optional<at::Tensor>& grow, int64_t row_stride,
-                   int64_t off_gamma, int64_t off_beta) {
+                   int64_t off_gamma, int64_t off_beta, const c10::optional<at::Tensor>& rscale,
+                   const c10::optional<at::Tensor>& rshift) {
   const auto dev = x.device();
   const int dt = check_act_rows(x, dev, "x");
   check_act_rows(dy, dev, "dy", dt);
@@ -531,9 +538,14 @@ void g_bn_backward(const at::Tensor& x, const at::Tensor& dy, const c10::optiona
                     " + ", groups, " rows of stride ", row_stride, " is out of bounds (", grow->numel(), ")");
     gp = grow->data_ptr();
   }
+  const float* rs = opt_vec(rscale, groups * C, dev, "relu scale");
+  const float* rf = opt_vec(rshift, groups * C, dev, "relu shift");
+  TORCH_CHECK((rs == nullptr) == (rf == nullptr), "garfield bn: pass both the ReLU scale and shift or neither");
+  TORCH_CHECK(rs == nullptr || (yp == nullptr && mp == nullptr),
+              "garfield bn: the ReLU test from (scale, shift) replaces y / the mask");
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::bn_backward(x.data_ptr(), dy.data_ptr(), yp, mp, rg, G, static_cast<int>(C), g, m, is, pw, cw,
-                             dx.data_ptr(), dr, gp, gdt, row_stride, off_gamma, off_beta, stream_of(dev), dt);
+                             dx.data_ptr(), dr, gp, gdt, row_stride, off_gamma, off_beta, stream_of(dev), dt, rs, rf);
 }
 
 garfield::gpu::Im2col conv_geometry(const at::Tensor& x, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
@@ -686,7 +698,9 @@ int64_t g_conv3x3_pick(int64_t n, int64_t h, int64_t w, int64_t c, int64_t cout)
 // Row-major NT GEMM (gemm_nt.hip): c = a · bᵀ (+ add); a [M, K], b [N, K], c/add [M, N], all contiguous
 // bf16 rows; stats (fp32, [ceil(M / BM)][2][2][N]): fused per-worker (rg rows) BatchNorm statistics.
 void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, const c10::optional<at::Tensor>& add,
-               const c10::optional<at::Tensor>& stats, int64_t rg, int64_t cfg) {
+               const c10::optional<at::Tensor>& stats, int64_t rg, int64_t cfg,
+               const c10::optional<at::Tensor>& pro_scale, const c10::optional<at::Tensor>& pro_shift,
+               int64_t pro_groups) {
   const auto dev = a.device();
   auto chk = [&](const at::Tensor& t, const char* what) {
     TORCH_CHECK(t.is_cuda() && t.device() == dev && t.scalar_type() == at::kBFloat16 && t.dim() == 2 &&
@@ -724,9 +738,28 @@ void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, co
     garfield::gpu::gemm_nt_stats_geometry(static_cast<int>(cfg), M, static_cast<int>(N), static_cast<int>(K), rg, &H, &E);
     sp = ws_vec(*stats, ((M + H - 1) / H) * E * 6 * N, dev, "stats");
   }
+  const float* psc = nullptr;
+  const float* psh = nullptr;
+  int64_t prg = 0;
+  if (pro_scale.has_value() && pro_scale->defined()) {
+    TORCH_CHECK(ap == nullptr, "gpu_gemm_nt: the BatchNorm prologue and add are exclusive");
+    TORCH_CHECK(pro_groups >= 1 && M % pro_groups == 0, "gpu_gemm_nt: the prologue needs M to split into ",
+                pro_groups, " workers");
+    prg = M / pro_groups;
+    psc = opt_vec(pro_scale, pro_groups * K, dev, "pro_scale");
+    psh = opt_vec(pro_shift, pro_groups * K, dev, "pro_shift");
+    TORCH_CHECK(psh != nullptr, "gpu_gemm_nt: pro_shift missing");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(psc) % 16 == 0 && reinterpret_cast<uintptr_t>(psh) % 16 == 0,
+                "gpu_gemm_nt: pro_scale / pro_shift must be 16-byte aligned");
+    TORCH_CHECK(garfield::gpu::gemm_nt_pro_ok(static_cast<int>(cfg), static_cast<int>(K), prg,
+                                              static_cast<int>(pro_groups)),
+                "gpu_gemm_nt: configuration ", cfg, " has no BatchNorm-prologue form for K = ", K, ", ", prg,
+                " rows per worker");
+  }
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::gemm_nt(u16(a), u16(b), static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), u16_mut(c),
-                         ap, sp, rg, static_cast<int>(cfg), stream_of(dev));
+                         ap, sp, rg, static_cast<int>(cfg), stream_of(dev), psc, psh, prg,
+                         static_cast<int>(pro_groups));
 }
 
 // Transposes of many bf16 matrices in one launch: dsts[i] = srcs[i]ᵀ (2-D, contiguous, 16-B aligned,
@@ -1163,7 +1196,8 @@ void check_f32_mat(const at::Tensor& t, const at::Device& dev, int64_t r, int64_
 }
 
 void g_iwgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
-              int64_t pw, int64_t dh, int64_t dw, int64_t groups, const at::Tensor& out, int64_t splits) {
+              int64_t pw, int64_t dh, int64_t dw, int64_t groups, const at::Tensor& out, int64_t splits,
+              const c10::optional<at::Tensor>& pro_scale, const c10::optional<at::Tensor>& pro_shift) {
   auto g = conv_geometry(x, kh, kw, sh, sw, ph, pw, dh, dw);
   TORCH_CHECK(g.C % 64 == 0, "gpu_iwgrad: input channels must be a multiple of 64 (got ", g.C, ")");
   TORCH_CHECK(dy.is_cuda() && dy.device() == x.device() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
@@ -1198,7 +1232,17 @@ void g_iwgrad(const at::Tensor& x, const at::Tensor& dy, int64_t kh, int64_t kw,
     bf16 = true;
     gs = out.stride(0);
   }
+  const float* psc = opt_vec(pro_scale, groups * g.C, x.device(), "pro_scale");
+  const float* psh = opt_vec(pro_shift, groups * g.C, x.device(), "pro_shift");
+  TORCH_CHECK((psc == nullptr) == (psh == nullptr), "gpu_iwgrad: pass both pro_scale and pro_shift or neither");
   c10::hip::HIPGuard guard(x.device().index());
+  if (psc) {   // the BatchNorm prologue: 1x1 / stride 1 / no padding (no padding pixel to keep at zero)
+    TORCH_CHECK(kh == 1 && kw == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0,
+                "gpu_iwgrad: the BatchNorm prologue takes 1x1 stride-1 unpadded convolutions only");
+    garfield::gpu::iwgrad_nhwc(u16(x), u16(dy), g, static_cast<int>(cout), static_cast<int>(groups), M / groups,
+                               static_cast<int>(splits), out.data_ptr(), bf16, ss, gs, stream_of(x.device()), psc, psh);
+    return;
+  }
   // the halo-staged 3x3 kernel whenever it fits
   if (garfield::gpu::wgrad3x3_nhwc(u16(x), u16(dy), g, static_cast<int>(cout), static_cast<int>(groups),
                                          M / groups, static_cast<int>(splits), out.data_ptr(), bf16, ss, gs,
@@ -1719,7 +1763,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_bn_backward", &g_bn_backward,
         "Per-worker BatchNorm backward; writes dγ/dβ of worker g to grow[g*row_stride + off_(gamma|beta) + c]; "
         "args (x, dy, y|mask|None, groups, gamma, mean, istd, part, coef, dx, dres|None, grow|None, row_stride, "
-        "off_gamma, off_beta); the ReLU test reads y > 0 (bf16) or the forward's uint8 bit mask");
+        "off_gamma, off_beta, relu_scale=None, relu_shift=None); the ReLU test reads y > 0 (bf16), "
+        "the forward's uint8 bit mask, or recomputes bf16(x * relu_scale + relu_shift) > 0",
+        py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("groups"), py::arg("gamma"), py::arg("mean"),
+        py::arg("istd"), py::arg("part"), py::arg("coef"), py::arg("dx"), py::arg("dres"), py::arg("grow"),
+        py::arg("row_stride"), py::arg("off_gamma"), py::arg("off_beta"), py::arg("relu_scale") = py::none(),
+        py::arg("relu_shift") = py::none());
   m.def("gpu_im2col", &g_im2col, "NHWC im2col of a channels_last bf16 tensor into col [N*Ho*Wo, ldc >= KH*KW*C] "
         "(pad columns zeroed); args (x, kh, kw, sh, sw, ph, pw, dh, dw, col)");
   m.def("gpu_col2im", &g_col2im, "Adjoint of gpu_im2col (gather, deterministic): dx = col2im(dcol); args "
@@ -1760,9 +1809,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_gemm_nt", &g_gemm_nt,
         "Row-major NT GEMM on MFMA: c = a · bᵀ (+ add); args (a [M,K], b [N,K], c [M,N], add=None, stats=None, "
         "rg=0, cfg=-1); stats: fp32 per-worker BatchNorm statistics of c, laid out as gemm_nt_stats_geometry "
-        "says (gpu_bn_forward's tile_stats / tile_m / tile_e)",
+        "says (gpu_bn_forward's tile_stats / tile_m / tile_e); pro_scale / pro_shift [pro_groups, K] fp32: a is a "
+        "pre-BatchNorm activation used as bf16(max(a * scale + shift, 0)) of its row's worker (the BatchNorm + ReLU "
+        "fused into the staging of a)",
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("add") = py::none(), py::arg("stats") = py::none(),
-        py::arg("rg") = 0, py::arg("cfg") = -1);
+        py::arg("rg") = 0, py::arg("cfg") = -1, py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none(),
+        py::arg("pro_groups") = 0);
+  m.def("gemm_nt_pro_ok", [](int64_t cfg, int64_t K, int64_t prg, int64_t groups) {
+    return garfield::gpu::gemm_nt_pro_ok(static_cast<int>(cfg), static_cast<int>(K), prg, static_cast<int>(groups));
+  }, py::arg("cfg"), py::arg("K"), py::arg("rows_per_worker"), py::arg("groups"),
+     "Whether gpu_gemm_nt configuration cfg has a BatchNorm-prologue form for this shape");
   m.def("gemm_nt_pick", [](int64_t M, int64_t N, int64_t K, int64_t rg_limit) {
     return garfield::gpu::gemm_nt_pick(M, static_cast<int>(N), static_cast<int>(K), rg_limit);
   }, "Tile configuration gpu_gemm_nt picks for M x N x K (rg_limit > 0: stats rows <= rg_limit); -1 if none");
@@ -1804,7 +1860,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad3x3_fits", &g_wgrad3x3_fits, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("c"), py::arg("cout"),
         py::arg("groups"), "True when gpu_iwgrad of this 3x3 / stride-1 / pad-1 shape runs the halo-staged kernel");
   m.def("gpu_iwgrad", &g_iwgrad, "Per-worker implicit-GEMM weight gradient on MFMA: out[s, g] = Σ over pixel "
-        "split s of worker g of dyᵀ · patches(x); args (x, dy, kh, kw, sh, sw, ph, pw, dh, dw, groups, out, splits)");
+        "split s of worker g of dyᵀ · patches(x); args (x, dy, kh, kw, sh, sw, ph, pw, dh, dw, groups, out, splits, "
+        "pro_scale=None, pro_shift=None); pro_*: [groups, C] BatchNorm prologue of x (1x1 only)",
+        py::arg("x"), py::arg("dy"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
+        py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("groups"), py::arg("out"), py::arg("splits"),
+        py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none());
   m.def("gpu_conv_f32", &g_conv_f32, py::arg("src"), py::arg("w"), py::arg("kh"), py::arg("kw"),
         py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("dgrad"),
         py::arg("out"), py::arg("add") = py::none(), py::arg("pm") = 0, py::arg("ksplit") = 0,

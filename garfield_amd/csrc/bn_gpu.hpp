@@ -37,8 +37,9 @@ void bn_running_update(const RunJobs& jobs, hipStream_t stream);
 // True when a layer of rg rows per worker takes the single-kernel small-layer path.
 bool bn_small(int64_t rg);
 
-// defer_running (small-layer path only): skip the running-statistics replay; the caller
-// batches it with bn_running_update.
+// defer_running (small-layer path, and any layer with y null): skip the running-statistics replay; the
+// caller batches it with bn_running_update. y null: statistics and scale / shift only, no apply pass (the
+// consumer applies the BatchNorm + ReLU while staging its input: gemm_nt / iwgrad prologues).
 // dt: the activations' dtype (kBF16, or kF32 for the reference-precision step)
 void bn_forward(const void* x, const void* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
@@ -76,8 +77,13 @@ void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, 
 // BatchNorm statistics of C, [ceil(M / SR)][2][2][N] floats (SR = gemm_nt_stats_rows(cfg)), merged by
 // bn_finalize_tiles. Configurations 0..8 stream K through an LDS ring; 9..14 keep the weight slice
 // resident in LDS and stream row tiles through a persistent workgroup (K <= 256).
+// pro_scale / pro_shift [pro_groups][K] (nullable, no `add`): the BatchNorm prologue -- A is the
+// pre-BatchNorm activation (pro_rg rows per worker) and each element is used as
+// bf16(max(a * scale + shift, 0)) (gemm_nt_pro_ok(cfg, ...) must hold)
 void gemm_nt(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
-             float* stats, int64_t rg, int cfg, hipStream_t stream);
+             float* stats, int64_t rg, int cfg, hipStream_t stream, const float* pro_scale = nullptr,
+             const float* pro_shift = nullptr, int64_t pro_rg = 0, int pro_groups = 0);
+bool gemm_nt_pro_ok(int cfg, int K, int64_t prg, int groups);
 // Configuration for an M x N x K problem (-1: none fits); rg_limit > 0: stats tiles <= rg_limit rows.
 int gemm_nt_pick(int64_t M, int N, int K, int64_t rg_limit);
 int gemm_nt_num_cfg();
@@ -106,7 +112,9 @@ void bn_backward(const void* x, const void* dy, const void* y, const uint8_t* ma
                  int C,
                  const float* gamma, const float* mean, const float* istd, float* part, float* coef, void* dx,
                  void* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
-                 hipStream_t stream, int dt = 1);
+                 hipStream_t stream, int dt = 1, const float* rsc = nullptr, const float* rsh = nullptr);
+// (rsc / rsh [groups, C], nullable: the ReLU test of a BatchNorm whose normalised output was never
+// written -- its consumer applied it while staging its input -- recomputes it as bf16(x * rsc + rsh) > 0.)
 
 // NHWC im2col (bf16): col[(n*Ho + ho)*Wo + wo][(i*KW + j)*C + c] = x[n][ho*sh - ph + i*dh][wo*sw - pw + j*dw][c]
 // (0 outside the image). col: [N*Ho*Wo, ldc] with ldc >= KH*KW*C; columns past KH*KW*C are zeroed
@@ -153,8 +161,11 @@ void maxpool_bwd_nhwc(const void* dy, const uint8_t* idx, const Im2col& g, void*
 // taps of a kernel row share each staged dy tile, GARFIELD_IWGRAD_ROW; 1x1: up to four 64-channel
 // input blocks share it, GARFIELD_IWGRAD_1X1_NT).
 int iwgrad_taps_per_block(int kw, int kh = 3, int C = 0, int Cout = 0);
+// pro_scale / pro_shift [groups][C] (nullable; 1x1 / stride 1 / no padding only): x is a pre-BatchNorm
+// activation used as bf16(max(x * scale + shift, 0)) of the workgroup's worker
 void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
-                 int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream);
+                 int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream,
+                 const float* pro_scale = nullptr, const float* pro_shift = nullptr);
 // accumulate: dx += col2im(dcol) instead of dx = col2im(dcol).
 void col2im_nhwc(const uint16_t* dcol, const Im2col& g, uint16_t* dx, bool accumulate, hipStream_t stream);
 

@@ -88,6 +88,26 @@ __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
+// dz = dy masked by the forward ReLU. RM: 0 none, 1 y > 0, 2 the bit mask, 3 the stored value of
+// bf16(x * scale + shift) > 0 (a BatchNorm whose normalised output was never written)
+template <int RM, int DT>
+__device__ __forceinline__ void relu_mask8(float (&d)[8], const float (&a)[8], const void* y, const uint8_t* mask,
+                                           int64_t off, const float (&sc)[8], const float (&sf)[8]) {
+  if constexpr (RM == 1) {
+    float yy[8];
+    load8<DT>(y, off, yy);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = yy[i] > 0.f ? d[i] : 0.f;
+  } else if constexpr (RM == 2) {
+    const uint32_t mb = mask[off >> 3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = (mb >> i) & 1u ? d[i] : 0.f;
+  } else if constexpr (RM == 3) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = stored_pos<DT>(fmaxf(fmaf(a[i], sc[i], sf[i]), 0.f)) ? d[i] : 0.f;
+  }
+}
+
 // Partial per-(group, channel) sums over one row chunk.
 //   forward : s = Σ (x - shift), q = Σ (x - shift)^2  with shift = x[first row of the group]
 //             (shifted sums: no catastrophic cancellation when |mean| >> std)
@@ -98,7 +118,8 @@ template <bool BWD, int RM, int DT>
 __global__ __launch_bounds__(kThreads) void k_partial(const void* __restrict__ x, const void* __restrict__ dy,
                                                      const void* __restrict__ y, const uint8_t* __restrict__ mask,
                                                      const float* __restrict__ mean, Geo geo,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part, const float* __restrict__ rsc,
+                                                     const float* __restrict__ rsh) {
   __shared__ __attribute__((aligned(16))) float red[2][kThreads * 8];
   const int C = geo.C;
   const int tc = threadIdx.x % geo.tch;
@@ -113,12 +134,16 @@ __global__ __launch_bounds__(kThreads) void k_partial(const void* __restrict__ x
   const int64_t r0 = static_cast<int64_t>(chunk) * geo.rows_per_chunk;
   int64_t r1 = r0 + geo.rows_per_chunk;
   if (r1 > geo.rg) r1 = geo.rg;
-  float s[8], q[8], sh[8];
+  float s[8], q[8], sh[8], rs[8] = {}, rf[8] = {};
 #pragma unroll
   for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; sh[i] = 0.f; }
   if (active) {
     if constexpr (BWD) load8f(mean + static_cast<int64_t>(g) * C + c0, sh);
     else load8<DT>(x, base * C + c0, sh);
+    if constexpr (RM == 3) {
+      load8f(rsc + static_cast<int64_t>(g) * C + c0, rs);
+      load8f(rsh + static_cast<int64_t>(g) * C + c0, rf);
+    }
     int64_t r = r0 + tr;
     // two rows in flight per lane
     for (; r + geo.rp < r1; r += 2 * geo.rp) {
@@ -130,20 +155,8 @@ __global__ __launch_bounds__(kThreads) void k_partial(const void* __restrict__ x
         float d0[8], d1[8];
         load8<DT>(dy, o0, d0);
         load8<DT>(dy, o1, d1);
-        if constexpr (RM == 1) {
-          float y0[8], y1[8];
-          load8<DT>(y, o0, y0);
-          load8<DT>(y, o1, y1);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) { d0[i] = y0[i] > 0.f ? d0[i] : 0.f; d1[i] = y1[i] > 0.f ? d1[i] : 0.f; }
-        } else if constexpr (RM == 2) {
-          const uint32_t m0 = mask[o0 >> 3], m1 = mask[o1 >> 3];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            d0[i] = (m0 >> i) & 1u ? d0[i] : 0.f;
-            d1[i] = (m1 >> i) & 1u ? d1[i] : 0.f;
-          }
-        }
+        relu_mask8<RM, DT>(d0, a0, y, mask, o0, rs, rf);
+        relu_mask8<RM, DT>(d1, a1, y, mask, o1, rs, rf);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           s[i] += d0[i] + d1[i];
@@ -165,16 +178,7 @@ __global__ __launch_bounds__(kThreads) void k_partial(const void* __restrict__ x
       if constexpr (BWD) {
         float d0[8];
         load8<DT>(dy, o0, d0);
-        if constexpr (RM == 1) {
-          float y0[8];
-          load8<DT>(y, o0, y0);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) d0[i] = y0[i] > 0.f ? d0[i] : 0.f;
-        } else if constexpr (RM == 2) {
-          const uint32_t m0 = mask[o0 >> 3];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) d0[i] = (m0 >> i) & 1u ? d0[i] : 0.f;
-        }
+        relu_mask8<RM, DT>(d0, a0, y, mask, o0, rs, rf);
 #pragma unroll
         for (int i = 0; i < 8; ++i) { s[i] += d0[i]; q[i] += d0[i] * (a0[i] - sh[i]); }
       } else {
@@ -401,14 +405,15 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const void* __restrict__
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ coef, int64_t rg, int64_t R, int C,
                                                        int tch, int rp, void* __restrict__ dx,
-                                                       void* __restrict__ dres) {
+                                                       void* __restrict__ dres, const float* __restrict__ rsc,
+                                                       const float* __restrict__ rsh) {
   const int tr = threadIdx.x / tch;
   if (tr >= rp) return;
   const int nv = C / 8;
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * rp * kApplyIters;
   const bool fixed = nv <= tch;   // one channel group per thread: coefficients once per worker
   int gl = -1;
-  float mu[8], ca[8], cb[8], cc[8];
+  float mu[8], ca[8], cb[8], cc[8], rs[8] = {}, rf[8] = {};
 #pragma unroll
   for (int it = 0; it < kApplyIters; ++it) {
     const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
@@ -421,23 +426,18 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const void* __restrict__
       float a[8], d[8];
       load8<DT>(x, off, a);
       load8<DT>(dy, off, d);
-      if constexpr (RM == 1) {
-        float yy[8];
-        load8<DT>(y, off, yy);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d[i] = yy[i] > 0.f ? d[i] : 0.f;
-      } else if constexpr (RM == 2) {
-        const uint32_t mb = mask[off >> 3];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d[i] = (mb >> i) & 1u ? d[i] : 0.f;
-      }
       if (!fixed || g != gl) {
         load8f(mean + static_cast<int64_t>(g) * C + c, mu);
         load8f(cg + c, ca);
         load8f(cg + C + c, cb);
         load8f(cg + 2 * C + c, cc);
+        if constexpr (RM == 3) {
+          load8f(rsc + static_cast<int64_t>(g) * C + c, rs);
+          load8f(rsh + static_cast<int64_t>(g) * C + c, rf);
+        }
         gl = g;
       }
+      relu_mask8<RM, DT>(d, a, y, mask, off, rs, rf);
       float o[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = ca[i] * (d[i] - cb[i] - (a[i] - mu[i]) * cc[i]);
@@ -575,6 +575,27 @@ __device__ __forceinline__ F8 keep_bits(F8 d, uint32_t mb) {
   return d;
 }
 
+// RM 3: dz = dy where the never-written normalised value bf16(x * scale + shift) is > 0
+template <int DT>
+__device__ __forceinline__ Raw8<DT> keep_affine(Raw8<DT> d, const Raw8<DT>& xr, const float (&sc)[8],
+                                                const float (&sf)[8]) {
+  float a[8];
+  unpack8(xr, a);
+  if constexpr (DT == kF32) {
+    float dd[8];
+    unpack8(d, dd);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dd[i] = stored_pos<DT>(fmaxf(fmaf(a[i], sc[i], sf[i]), 0.f)) ? dd[i] : 0.f;
+    return F8{make_float4(dd[0], dd[1], dd[2], dd[3]), make_float4(dd[4], dd[5], dd[6], dd[7])};
+  } else {
+    uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (!stored_pos<DT>(fmaxf(fmaf(a[i], sc[i], sf[i]), 0.f))) w[i >> 1] &= (i & 1) ? 0x0000ffffu : 0xffff0000u;
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // Each thread keeps its (<= kSmallIt) rows of 8 channels in registers as stored (packed
 // bf16 or fp32), so the apply pass does not re-read x (or dy) from memory.
 template <int CH, bool RES, bool RELU, int DT>
@@ -642,7 +663,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const void* __re
     lsh[threadIdx.x] = sf;
   }
   __syncthreads();
-  if (!act) return;
+  if (!act || y == nullptr) return;   // y null: statistics only (the consumer applies scale / shift itself)
   float sc[8], sf[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { sc[i] = lsc[tc * 8 + i]; sf[i] = lsh[tc * 8 + i]; }
@@ -680,7 +701,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
     const void* __restrict__ x, const void* __restrict__ dy, const void* __restrict__ y,
     const uint8_t* __restrict__ mask, int64_t rg, int C, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ istd, void* __restrict__ dx,
-    void* __restrict__ dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta) {
+    void* __restrict__ dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
+    const float* __restrict__ rsc, const float* __restrict__ rsh) {
   constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH>::Vec, kSmallLanes = SmallGeo<CH>::Lanes,
                 kSmallIt = SmallGeo<CH>::It;
   __shared__ float red[2][kSmallLanes][kSmallCh];
@@ -692,11 +714,15 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
   const int64_t base = static_cast<int64_t>(g) * rg;
   // dz = dy masked by the forward ReLU, kept as stored in registers with x
   Raw8<DT> xr[kSmallIt], dr[kSmallIt];
-  float A[8], B[8], mu[8];
+  float A[8], B[8], mu[8], rs[8] = {}, rf[8] = {};
 #pragma unroll
   for (int i = 0; i < 8; ++i) { A[i] = 0.f; B[i] = 0.f; mu[i] = 0.f; }
   if (act) {
     load8f(mean + static_cast<int64_t>(g) * C + c0, mu);
+    if constexpr (RM == 3) {
+      load8f(rsc + static_cast<int64_t>(g) * C + c0, rs);
+      load8f(rsh + static_cast<int64_t>(g) * C + c0, rf);
+    }
 #pragma unroll
     for (int it = 0; it < kSmallIt; ++it) {
       const int64_t r = tr + it * kSmallLanes;
@@ -706,6 +732,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
         Raw8<DT> d = ld_raw8<DT>(dy, off);
         if constexpr (RM == 1) d = keep_pos(d, ld_raw8<DT>(y, off));
         else if constexpr (RM == 2) d = keep_bits(d, mask[off >> 3]);
+        else if constexpr (RM == 3) d = keep_affine<DT>(d, xr[it], rs, rf);
         dr[it] = d;
       }
     }
@@ -801,12 +828,13 @@ template <int CH, int DT>
 void launch_bwd_small(const void* x, const void* dy, const void* y, const uint8_t* mask, int64_t rg,
                       int groups, int C, const float* gamma, const float* mean, const float* istd, void* dx,
                       void* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
-                      int rm, hipStream_t stream) {
+                      int rm, hipStream_t stream, const float* rsc, const float* rsh) {
   const dim3 sgrid((C + CH - 1) / CH, groups);
 #define GARFIELD_BWD_SMALL(RMV, RESV)                                                                           \
   hipLaunchKernelGGL((k_bn_bwd_small<CH, RMV, RESV, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, dy, y, mask, rg, C, \
-                     gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta)
-  if (rm == 2) { if (dres) GARFIELD_BWD_SMALL(2, true); else GARFIELD_BWD_SMALL(2, false); }
+                     gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rsc, rsh)
+  if (rm == 3) { if (dres) GARFIELD_BWD_SMALL(3, true); else GARFIELD_BWD_SMALL(3, false); }
+  else if (rm == 2) { if (dres) GARFIELD_BWD_SMALL(2, true); else GARFIELD_BWD_SMALL(2, false); }
   else if (rm == 1) { if (dres) GARFIELD_BWD_SMALL(1, true); else GARFIELD_BWD_SMALL(1, false); }
   else { if (dres) GARFIELD_BWD_SMALL(0, true); else GARFIELD_BWD_SMALL(0, false); }
 #undef GARFIELD_BWD_SMALL
@@ -835,9 +863,18 @@ void forward_dt(const void* x, const void* res, int64_t rg, int groups, int C, c
     const Geo g = geometry(rg, groups, C);
     const int ncb = (C + g.cb - 1) / g.cb;
     hipLaunchKernelGGL((k_partial<false, 0, DT>), dim3(g.chunks, ncb, groups), dim3(kThreads), 0, stream, x, nullptr,
-                       nullptr, nullptr, nullptr, g, part);
+                       nullptr, nullptr, nullptr, g, part, nullptr, nullptr);
     hipLaunchKernelGGL((k_fwd_finalize<DT, kFin>), dim3((C + kFin - 1) / kFin, groups), dim3(kThreads), 0, stream, part,
                        x, g, gamma, beta, eps, mean, istd, scale, shift);
+  }
+  if (y == nullptr) {   // statistics only: the running statistics without the apply pass's first workgroup
+    if (run_mean && !defer_running) {
+      RunJobs jobs{};
+      jobs.j[0] = RunJob{mean, istd, run_mean, run_var, rg, C, groups, eps, momentum};
+      jobs.n = 1;
+      bn_running_update(jobs, stream);
+    }
+    return;
   }
   const RunStats rs{mean, istd, run_mean, run_var, eps, momentum, groups};
   int tch, rp;
@@ -857,18 +894,23 @@ template <int DT>
 void backward_dt(const void* x, const void* dy, const void* y, const uint8_t* mask, int64_t rg, int groups,
                  int C, const float* gamma, const float* mean, const float* istd, float* part, float* coef, void* dx,
                  void* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
-                 hipStream_t stream) {
-  const int rm = mask ? 2 : (y ? 1 : 0);
+                 hipStream_t stream, const float* rsc, const float* rsh) {
+  const int rm = mask ? 2 : (y ? 1 : (rsc ? 3 : 0));
   if (rg <= kSmallRows) {
-    launch_bwd_small<32, DT>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream);
+    launch_bwd_small<32, DT>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride,
+                             off_gamma, off_beta, rm, stream, rsc, rsh);
     return;
   }
   const Geo g = geometry(rg, groups, C);
   const int ncb = (C + g.cb - 1) / g.cb;
   const dim3 pgrid(g.chunks, ncb, groups);
-  if (rm == 2) hipLaunchKernelGGL((k_partial<true, 2, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
-  else if (rm == 1) hipLaunchKernelGGL((k_partial<true, 1, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
-  else hipLaunchKernelGGL((k_partial<true, 0, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part);
+#define GARFIELD_PARTIAL(RMV) \
+  hipLaunchKernelGGL((k_partial<true, RMV, DT>), pgrid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, g, part, rsc, rsh)
+  if (rm == 3) GARFIELD_PARTIAL(3);
+  else if (rm == 2) GARFIELD_PARTIAL(2);
+  else if (rm == 1) GARFIELD_PARTIAL(1);
+  else GARFIELD_PARTIAL(0);
+#undef GARFIELD_PARTIAL
   hipLaunchKernelGGL(k_bwd_finalize<kFin>, dim3((C + kFin - 1) / kFin, groups), dim3(kThreads), 0, stream, part, g,
                      gamma, istd, coef, grow, grow_dt, row_stride, off_gamma, off_beta);
   int tch, rp;
@@ -876,8 +918,9 @@ void backward_dt(const void* x, const void* dy, const void* y, const uint8_t* ma
   const int64_t R = rg * groups;
   const dim3 grid = apply_grid(R, rp);
 #define GARFIELD_BWD_APPLY(RMV, RESV) \
-  hipLaunchKernelGGL((k_bwd_apply<RMV, RESV, DT>), grid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, coef, rg, R, C, tch, rp, dx, dres)
-  if (rm == 2) { if (dres) GARFIELD_BWD_APPLY(2, true); else GARFIELD_BWD_APPLY(2, false); }
+  hipLaunchKernelGGL((k_bwd_apply<RMV, RESV, DT>), grid, dim3(kThreads), 0, stream, x, dy, y, mask, mean, coef, rg, R, C, tch, rp, dx, dres, rsc, rsh)
+  if (rm == 3) { if (dres) GARFIELD_BWD_APPLY(3, true); else GARFIELD_BWD_APPLY(3, false); }
+  else if (rm == 2) { if (dres) GARFIELD_BWD_APPLY(2, true); else GARFIELD_BWD_APPLY(2, false); }
   else if (rm == 1) { if (dres) GARFIELD_BWD_APPLY(1, true); else GARFIELD_BWD_APPLY(1, false); }
   else { if (dres) GARFIELD_BWD_APPLY(0, true); else GARFIELD_BWD_APPLY(0, false); }
 #undef GARFIELD_BWD_APPLY
@@ -906,13 +949,13 @@ void bn_forward(const void* x, const void* res, int64_t rg, int groups, int C, c
 void bn_backward(const void* x, const void* dy, const void* y, const uint8_t* mask, int64_t rg, int groups,
                  int C, const float* gamma, const float* mean, const float* istd, float* part, float* coef, void* dx,
                  void* dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
-                 hipStream_t stream, int dt) {
+                 hipStream_t stream, int dt, const float* rsc, const float* rsh) {
   if (dt == kF32)
     backward_dt<kF32>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, part, coef, dx, dres, grow, grow_dt, row_stride,
-                      off_gamma, off_beta, stream);
+                      off_gamma, off_beta, stream, rsc, rsh);
   else
     backward_dt<kBF16>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, part, coef, dx, dres, grow, grow_dt,
-                       row_stride, off_gamma, off_beta, stream);
+                       row_stride, off_gamma, off_beta, stream, rsc, rsh);
 }
 
 void bn_running_update(const RunJobs& jobs, hipStream_t stream) {

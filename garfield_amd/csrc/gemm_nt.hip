@@ -46,18 +46,48 @@ using namespace dev;
 namespace {
 
 using lds_ptr = __attribute__((address_space(3))) void*;
-__device__ __attribute__((aligned(16))) uint4 g_gemm_zero[8];  // 128 zero bytes: source of padded rows
+__device__ __attribute__((aligned(16))) uint4 g_gemm_zero[8];
+
+struct GemmPro {         // BatchNorm prologue of A (see pro_chunk); sc == nullptr: none
+  const float* sc;       // [G][K] scale
+  const float* sh;       // [G][K] shift
+  FastDiv frg;           // rows per worker
+  int G;
+};  // 128 zero bytes: source of padded rows
 
 constexpr int EPI_PLAIN = 0, EPI_ADD = 1, EPI_STATS = 2;
+
+// BatchNorm prologue (PRO): A holds the PRE-BatchNorm activation of the layer before; each staged
+// 16-byte chunk (8 channels of one row) becomes bf16(max(x * scale[g][c] + shift[g][c], 0)) in LDS
+// before any wave reads it, g = row / rg (the row's worker). The lane that staged a chunk by
+// LDS-DMA transforms exactly that chunk (its own completed load), then one barrier publishes the
+// tile: the normalised activation is never written to HBM. Scale / shift come from an LDS table
+// filled once per workgroup (dynamic LDS).
+__device__ __forceinline__ void pro_chunk(char* p, const float* sc, const float* sh) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  const float4 s0 = *reinterpret_cast<const float4*>(sc), s1 = *reinterpret_cast<const float4*>(sc + 4);
+  const float4 h0 = *reinterpret_cast<const float4*>(sh), h1 = *reinterpret_cast<const float4*>(sh + 4);
+  const float a[8] = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                      __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u),
+                      __uint_as_float(v.z << 16), __uint_as_float(v.z & 0xffff0000u),
+                      __uint_as_float(v.w << 16), __uint_as_float(v.w & 0xffff0000u)};
+  const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+  float y[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) y[i] = fmaxf(fmaf(a[i], sv[i], hv[i]), 0.f);
+  *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]),
+                                            pack_bf16x2(y[4], y[5]), pack_bf16x2(y[6], y[7]));
+}
 
 // ---------------------------------------------------------------------------------------------
 // K-loop kernel
 
-template <int WPM, int WPN, int WM, int WN, int NS, int EPI>
+template <int WPM, int WPN, int WM, int WN, int NS, int EPI, bool PRO>
 __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                  int M, int N, int K, uint16_t* __restrict__ C,
                                                  const uint16_t* __restrict__ add, float* __restrict__ stats,
-                                                 int64_t rg) {
+                                                 int64_t rg, GemmPro pro) {
   static_assert(WM * WN == 4, "4 waves per workgroup");
   constexpr int BM = 16 * WPM * WM, BN = 16 * WPN * WN;
   constexpr int AB = BM * 128, BB = BN * 128, SB = AB + BB;
@@ -95,6 +125,21 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
   const uint64_t az = reinterpret_cast<uint64_t>(reinterpret_cast<const uint16_t*>(g_gemm_zero) + lchunk * 8);
   const int steps = K / 64;
 
+  // PRO: the [2][K] scale and shift of the tile's (at most two) workers: rows of worker g0 use entry 0
+  extern __shared__ __attribute__((aligned(16))) float ptab[];
+  uint32_t pg0 = 0;
+  if constexpr (PRO) {
+    pg0 = fdiv(static_cast<uint32_t>(m0), pro.frg);
+    const uint32_t pg1 = pg0 + 1 < static_cast<uint32_t>(pro.G) ? pg0 + 1 : pg0;
+    for (int i = threadIdx.x; i < K; i += 256) {
+      ptab[i] = pro.sc[static_cast<int64_t>(pg0) * K + i];
+      ptab[K + i] = pro.sc[static_cast<int64_t>(pg1) * K + i];
+      ptab[2 * K + i] = pro.sh[static_cast<int64_t>(pg0) * K + i];
+      ptab[3 * K + i] = pro.sh[static_cast<int64_t>(pg1) * K + i];
+    }
+    __syncthreads();   // the table is read by every lane's transforms
+  }
+
   auto issue = [&](int s, int slot) {
     char* base = lds + slot * SB;
     const int k0 = s * 64;
@@ -121,12 +166,37 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
   for (int s0 = 0; s0 < NS - 1; ++s0)
     if (s0 < steps) issue(s0, s0);
 
-  for (int s = 0; s < steps; ++s) {
-    // stage s has landed when at most (stages issued after it) x PER loads are outstanding
-    const int ahead = (steps - 1 - s) < (NS - 2) ? (steps - 1 - s) : (NS - 2);
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+  // stage st has landed (for this lane) when at most (stages issued after it) x PER loads are outstanding
+  auto wait_landed = [&](int st, int issued) {
+    const int after = issued - 1 - st;
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // PRO: this lane's own landed chunks of stage st (published by the barrier at the top of its k-step)
+  auto pro_stage = [&](int st) {
+    char* sb = lds + (st % NS) * SB;
+#pragma unroll
+    for (int u = 0; u < AI; ++u) {
+      const int row = (wave * AI + u) * 8 + lrow;
+      if (av[u]) {
+        const int sel = fdiv(static_cast<uint32_t>(m0 + row), pro.frg) != pg0 ? 1 : 0;
+        const int ch = st * 64 + (lchunk ^ lrow) * 8;
+        pro_chunk(sb + (wave * AI + u) * 1024 + lane * 16, ptab + sel * K + ch, ptab + (2 + sel) * K + ch);
+      }
+    }
+  };
+  if constexpr (PRO) {
+    if (steps > 0) {
+      wait_landed(0, steps < NS - 1 ? steps : NS - 1);
+      pro_stage(0);
+    }
+  }
+
+  for (int s = 0; s < steps; ++s) {
+    const int issued = s + NS - 1 < steps ? s + NS - 1 : steps;   // stages issued before this k-step
+    if constexpr (PRO) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // stage s was transformed last k-step
+    else wait_landed(s, issued);
     __builtin_amdgcn_s_barrier();
     if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
     const char* base = lds + (s % NS) * SB;
@@ -148,6 +218,12 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
     }
     // every wave's fragment reads of this slot retire before the barrier that lets it be refilled
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (PRO) {   // the next stage, while the other waves still multiply this one
+      if (s + 1 < steps) {
+        wait_landed(s + 1, s + NS < steps ? s + NS : steps);
+        pro_stage(s + 1);
+      }
+    }
   }
 
   // ---- epilogue. The fragments hold 4 channels of one pixel per lane; the tile goes through
@@ -214,11 +290,11 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
 // of its stored bf16 values per channel in registers (s: the wave's first stored row of the
 // chunk), and reduces them over the 16 lanes of a DPP row only when the chunk (or the worker)
 // ends: one statistics tile per chunk (H = per * BM rows), one entry per wave row (E = WM).
-template <int BN, int RW, int KB, int EPI>
+template <int BN, int RW, int KB, int EPI, bool PRO>
 __global__ __launch_bounds__(256) void k_gemm_ws(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                  int M, int N, uint16_t* __restrict__ C,
                                                  const uint16_t* __restrict__ add, float* __restrict__ stats,
-                                                 int64_t rg, int tiles_m, int P, int per, int nchunks) {
+                                                 int64_t rg, int tiles_m, int P, int per, int nchunks, GemmPro pro) {
   constexpr int WN = BN / 64, WM = 4 / WN, BM = WM * RW, WPM = RW / 16, K = KB * 64;
   static_assert(WN * WM == 4 && RW % 16 == 0 && BM % 32 == 0, "4 waves of RW x 64");
   constexpr int BB = BN * K * 2, AB = BM * K * 2, EB = RW * 128;
@@ -234,6 +310,16 @@ __global__ __launch_bounds__(256) void k_gemm_ws(const uint16_t* __restrict__ A,
   const int n0 = tn * BN;
   const int lrow = lane >> 3, lchunk = lane & 7;
   char* const el = lds + BB + 2 * AB + wave * EB;
+  // PRO: every worker's scale and shift ([2][G][K], dynamic LDS), filled before the first barrier
+  extern __shared__ __attribute__((aligned(16))) float ptab[];
+  if constexpr (PRO) {
+    const int n = pro.G * K;
+    for (int i = threadIdx.x; i < n; i += 256) {
+      ptab[i] = pro.sc[i];
+      ptab[n + i] = pro.sh[i];
+    }
+    __syncthreads();   // the table is read by every lane's transforms
+  }
 
 #pragma unroll
   for (int u = 0; u < BI; ++u) {
@@ -321,9 +407,29 @@ __global__ __launch_bounds__(256) void k_gemm_ws(const uint16_t* __restrict__ A,
     }
   };
 
+  // PRO: this lane's own landed chunks of tile t in slot sl (published by the next loop-top barrier)
+  auto pro_tile = [&](int t, int sl) {
+#pragma unroll
+    for (int u = 0; u < AI; ++u) {
+      const int q = wave * AI + u, kb = q / (BM / 8), rb = q - kb * (BM / 8);
+      const int row = t * BM + rb * 8 + lrow;
+      if (row < M) {
+        const int g = static_cast<int>(fdiv(static_cast<uint32_t>(row), pro.frg));
+        const int ch = kb * 64 + (lchunk ^ lrow) * 8;
+        pro_chunk(lds + BB + sl * AB + kb * BM * 128 + rb * 1024 + lane * 16, ptab + g * K + ch,
+                  ptab + pro.G * K + g * K + ch);
+      }
+    }
+  };
+
   int T = p, tm = p * per;
   issue(tm, 0);
   int slot = 0;
+  if constexpr (PRO) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pro_tile(tm, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   if constexpr (EPI == EPI_STATS) {
     reset();
     const int64_t c0 = static_cast<int64_t>(T) * per * BM;
@@ -443,6 +549,11 @@ __global__ __launch_bounds__(256) void k_gemm_ws(const uint16_t* __restrict__ A,
       }
     }
     if (!more) break;
+    if constexpr (PRO) {   // the next tile, while the other waves still finish this one
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pro_tile(tm2, slot ^ 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     T = T2;
     tm = tm2;
     slot ^= 1;
@@ -527,18 +638,28 @@ __global__ __launch_bounds__(kMergeCh * kMergeLanes) void k_finalize_tiles(
 
 template <int WPM, int WPN, int WM, int WN, int NS>
 void launch_cfg(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
-                float* stats, int64_t rg, hipStream_t stream) {
+                float* stats, int64_t rg, hipStream_t stream, const GemmPro& pro) {
   constexpr int BM = 16 * WPM * WM, BN = 16 * WPN * WN;
   const dim3 grid(((M + BM - 1) / BM) * (N / BN));
+  if (pro.sc) {   // forward of a 1x1 convolution over a pre-BatchNorm input (plain or statistics epilogue)
+    const size_t tab = static_cast<size_t>(4) * K * sizeof(float);
+    if (stats)
+      hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_STATS, true>), grid, dim3(256), tab, stream, A, B, M, N,
+                         K, C, add, stats, rg, pro);
+    else
+      hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_PLAIN, true>), grid, dim3(256), tab, stream, A, B, M, N,
+                         K, C, add, stats, rg, pro);
+    return;
+  }
   if (stats)
-    hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_STATS>), grid, dim3(256), 0, stream, A, B, M, N, K, C,
-                       add, stats, rg);
+    hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_STATS, false>), grid, dim3(256), 0, stream, A, B, M, N, K,
+                       C, add, stats, rg, pro);
   else if (add)
-    hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_ADD>), grid, dim3(256), 0, stream, A, B, M, N, K, C,
-                       add, stats, rg);
+    hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_ADD, false>), grid, dim3(256), 0, stream, A, B, M, N, K, C,
+                       add, stats, rg, pro);
   else
-    hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_PLAIN>), grid, dim3(256), 0, stream, A, B, M, N, K, C,
-                       add, stats, rg);
+    hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_PLAIN, false>), grid, dim3(256), 0, stream, A, B, M, N, K,
+                       C, add, stats, rg, pro);
 }
 
 constexpr int ws_bm(int BN, int RW) { return (4 / (BN / 64)) * RW; }
@@ -570,29 +691,40 @@ WsPlan ws_plan(int BN, int RW, int KB, int64_t M, int N, int64_t rg) {
 
 template <int BN, int RW, int KB>
 void launch_ws(const uint16_t* A, const uint16_t* B, int M, int N, uint16_t* C, const uint16_t* add, float* stats,
-               int64_t rg, hipStream_t stream) {
+               int64_t rg, hipStream_t stream, const GemmPro& pro) {
   static_assert(ws_lds(BN, RW, KB) <= 160 * 1024, "LDS");
   const WsPlan w = ws_plan(BN, RW, KB, M, N, stats ? rg : 0);
   const dim3 grid(w.P * (N / BN));
+  if (pro.sc) {
+    const size_t tab = static_cast<size_t>(2) * pro.G * KB * 64 * sizeof(float);
+    if (stats)
+      hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_STATS, true>), grid, dim3(256), tab, stream, A, B, M, N, C, add,
+                         stats, rg, w.tiles_m, w.P, w.per, w.nchunks, pro);
+    else
+      hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_PLAIN, true>), grid, dim3(256), tab, stream, A, B, M, N, C, add,
+                         stats, rg, w.tiles_m, w.P, w.per, w.nchunks, pro);
+    return;
+  }
   if (stats)
-    hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_STATS>), grid, dim3(256), 0, stream, A, B, M, N, C, add, stats, rg,
-                       w.tiles_m, w.P, w.per, w.nchunks);
+    hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_STATS, false>), grid, dim3(256), 0, stream, A, B, M, N, C, add, stats,
+                       rg, w.tiles_m, w.P, w.per, w.nchunks, pro);
   else if (add)
-    hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_ADD>), grid, dim3(256), 0, stream, A, B, M, N, C, add, stats, rg,
-                       w.tiles_m, w.P, w.per, w.nchunks);
+    hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_ADD, false>), grid, dim3(256), 0, stream, A, B, M, N, C, add, stats,
+                       rg, w.tiles_m, w.P, w.per, w.nchunks, pro);
   else
-    hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_PLAIN>), grid, dim3(256), 0, stream, A, B, M, N, C, add, stats, rg,
-                       w.tiles_m, w.P, w.per, w.nchunks);
+    hipLaunchKernelGGL((k_gemm_ws<BN, RW, KB, EPI_PLAIN, false>), grid, dim3(256), 0, stream, A, B, M, N, C, add, stats,
+                       rg, w.tiles_m, w.P, w.per, w.nchunks, pro);
 }
 
 template <int BN, int RW>
 void launch_ws_k(int K, const uint16_t* A, const uint16_t* B, int M, int N, uint16_t* C, const uint16_t* add,
-                 float* stats, int64_t rg, hipStream_t stream) {
+                 float* stats, int64_t rg, hipStream_t stream, const GemmPro& pro) {
   switch (K) {
-    case 64: launch_ws<BN, RW, 1>(A, B, M, N, C, add, stats, rg, stream); break;
-    case 128: launch_ws<BN, RW, 2>(A, B, M, N, C, add, stats, rg, stream); break;
+    case 64: launch_ws<BN, RW, 1>(A, B, M, N, C, add, stats, rg, stream, pro); break;
+    case 128: launch_ws<BN, RW, 2>(A, B, M, N, C, add, stats, rg, stream, pro); break;
     default:
-      if constexpr (BN <= 128 && ws_lds(BN, RW, 4) <= 160 * 1024) launch_ws<BN, RW, 4>(A, B, M, N, C, add, stats, rg, stream);
+      if constexpr (BN <= 128 && ws_lds(BN, RW, 4) <= 160 * 1024)
+        launch_ws<BN, RW, 4>(A, B, M, N, C, add, stats, rg, stream, pro);
       break;
   }
 }
@@ -692,6 +824,16 @@ void transpose_multi(const uint16_t* const* srcs, uint16_t* const* dsts, const i
 
 int gemm_nt_num_cfg() { return kNumCfg; }
 
+// The BatchNorm-prologue form of configuration cfg: its LDS (ring + scale / shift table) fits, and a
+// K-loop tile spans at most two workers (BM <= rows per worker)
+bool gemm_nt_pro_ok(int cfg, int K, int64_t prg, int groups) {
+  if (cfg < 0 || cfg >= kNumCfg || prg <= 0 || prg >= (int64_t{1} << 31)) return false;
+  if (cfg < kNumNt) return kCfgBM[cfg] <= prg && static_cast<int64_t>(4) * K * 4 <= 32 * 1024;
+  const int i = cfg - kNumNt;
+  const int64_t tab = static_cast<int64_t>(2) * groups * K * 4;   // dynamic LDS: <= 64 KB without an attribute
+  return ws_fits(i, K) && tab <= 64 * 1024 && ws_lds(kWsBN[i], kWsRW[i], K / 64) + tab <= 160 * 1024;
+}
+
 bool gemm_nt_valid(int cfg, int N, int K) {
   if (cfg < 0 || cfg >= kNumCfg || K % 64 || K <= 0) return false;
   if (cfg < kNumNt) return N % kCfgBN[cfg] == 0;
@@ -759,24 +901,32 @@ int gemm_nt_pick(int64_t M, int N, int K, int64_t rg_limit) {
 }
 
 void gemm_nt(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
-             float* stats, int64_t rg, int cfg, hipStream_t stream) {
+             float* stats, int64_t rg, int cfg, hipStream_t stream, const float* pro_scale, const float* pro_shift,
+             int64_t pro_rg, int pro_groups) {
   if (M <= 0) return;
+  GemmPro pro{};
+  if (pro_scale) {
+    pro.sc = pro_scale;
+    pro.sh = pro_shift;
+    pro.frg = make_fastdiv(static_cast<uint32_t>(pro_rg));
+    pro.G = pro_groups;
+  }
   switch (cfg) {
-    case 0: launch_cfg<4, 4, 2, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    case 6: launch_cfg<4, 4, 2, 2, 3>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    case 7: launch_cfg<2, 2, 2, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    case 8: launch_cfg<2, 4, 1, 4, 2>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    case 1: launch_cfg<4, 4, 4, 1, 2>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    case 2: launch_cfg<2, 4, 2, 2, 3>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    case 3: launch_cfg<4, 4, 1, 4, 2>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    case 4: launch_cfg<2, 2, 2, 2, 4>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    case 5: launch_cfg<4, 8, 2, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream); break;
-    case 9: launch_ws_k<256, 32>(K, A, B, M, N, C, add, stats, rg, stream); break;
-    case 10: launch_ws_k<256, 64>(K, A, B, M, N, C, add, stats, rg, stream); break;
-    case 11: launch_ws_k<128, 16>(K, A, B, M, N, C, add, stats, rg, stream); break;
-    case 12: launch_ws_k<128, 32>(K, A, B, M, N, C, add, stats, rg, stream); break;
-    case 13: launch_ws_k<64, 16>(K, A, B, M, N, C, add, stats, rg, stream); break;
-    default: launch_ws_k<64, 32>(K, A, B, M, N, C, add, stats, rg, stream); break;
+    case 0: launch_cfg<4, 4, 2, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream, pro); break;
+    case 6: launch_cfg<4, 4, 2, 2, 3>(A, B, M, N, K, C, add, stats, rg, stream, pro); break;
+    case 7: launch_cfg<2, 2, 2, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream, pro); break;
+    case 8: launch_cfg<2, 4, 1, 4, 2>(A, B, M, N, K, C, add, stats, rg, stream, pro); break;
+    case 1: launch_cfg<4, 4, 4, 1, 2>(A, B, M, N, K, C, add, stats, rg, stream, pro); break;
+    case 2: launch_cfg<2, 4, 2, 2, 3>(A, B, M, N, K, C, add, stats, rg, stream, pro); break;
+    case 3: launch_cfg<4, 4, 1, 4, 2>(A, B, M, N, K, C, add, stats, rg, stream, pro); break;
+    case 4: launch_cfg<2, 2, 2, 2, 4>(A, B, M, N, K, C, add, stats, rg, stream, pro); break;
+    case 5: launch_cfg<4, 8, 2, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream, pro); break;
+    case 9: launch_ws_k<256, 32>(K, A, B, M, N, C, add, stats, rg, stream, pro); break;
+    case 10: launch_ws_k<256, 64>(K, A, B, M, N, C, add, stats, rg, stream, pro); break;
+    case 11: launch_ws_k<128, 16>(K, A, B, M, N, C, add, stats, rg, stream, pro); break;
+    case 12: launch_ws_k<128, 32>(K, A, B, M, N, C, add, stats, rg, stream, pro); break;
+    case 13: launch_ws_k<64, 16>(K, A, B, M, N, C, add, stats, rg, stream, pro); break;
+    default: launch_ws_k<64, 32>(K, A, B, M, N, C, add, stats, rg, stream, pro); break;
   }
 }
 

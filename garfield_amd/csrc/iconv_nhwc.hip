@@ -36,6 +36,23 @@ namespace {
 
 constexpr int kWaves = 4;
 
+// BatchNorm prologue of a weight gradient's input fragment (the 1x1 consumers of a BatchNorm + ReLU whose
+// output was never written): 8 pixels of one channel of one worker, bf16(max(x * sc + sh, 0)). A 1x1
+// stride-1 unpadded convolution has no padding pixels; rows past the worker's end are zeros whose dy
+// rows are zeros too.
+__device__ __forceinline__ bf16x8 pro_frag(bf16x8 b, float sc, float sh) {
+  const uint4 u = __builtin_bit_cast(uint4, b);
+  const float x[8] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                      __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u),
+                      __uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
+                      __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u)};
+  float y[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) y[i] = fmaxf(fmaf(x[i], sc, sh), 0.f);
+  return __builtin_bit_cast(bf16x8, make_uint4(pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]),
+                                               pack_bf16x2(y[4], y[5]), pack_bf16x2(y[6], y[7])));
+}
+
 template <int PM>
 struct Frags {
   bf16x8 a[4];
@@ -375,10 +392,11 @@ void launch_lds(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
 // afterwards) when the tile grid alone cannot fill the chip.
 
 
-template <int NS, bool OUT_BF16>
+template <int NS, bool OUT_BF16, bool PRO>
 __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                 Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
-                                                int64_t split_stride, int64_t group_stride) {
+                                                int64_t split_stride, int64_t group_stride,
+                                                const float* __restrict__ psc, const float* __restrict__ psh) {
   constexpr int TB = 32 * 128;  // one 32-pixel x 64-channel tile
   constexpr int SB = 2 * TB;    // dy tile + x tile per stage
   __shared__ __attribute__((aligned(16))) char lds[NS * SB];
@@ -442,6 +460,15 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
   const uint32_t offA = (8 * grp + q) * 128 + 32 * (cf0 ^ tg) + 8 * p;
   const uint32_t offB = TB + (8 * grp + q) * 128 + 32 * (kf0 ^ tg) + 8 * p;
   const uint32_t dtr = (tg & 1) ? static_cast<uint32_t>(-32) : 32u;
+  float psv[2] = {0.f, 0.f}, phv[2] = {0.f, 0.f};   // PRO: this lane's two input channels (1x1: k = channel)
+  if constexpr (PRO) {
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int64_t o = static_cast<int64_t>(gi) * g.C + c0 + (kf0 + v) * 16 + li;
+      psv[v] = psc[o];
+      phv[v] = psh[o];
+    }
+  }
 
 #pragma unroll
   for (int s0 = 0; s0 < NS - 1; ++s0)
@@ -478,6 +505,7 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
                            r[5 + 2 * u][0], r[5 + 2 * u][1], r[5 + 2 * u][2], r[5 + 2 * u][3]};
       a[u] = __builtin_bit_cast(bf16x8, va);   // dy tile: A[co][m]
       b[u] = __builtin_bit_cast(bf16x8, vb);   // x tile:  B[m][k]
+      if constexpr (PRO) b[u] = pro_frag(b[u], psv[u], phv[u]);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -725,10 +753,11 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
 // Weight gradient of a 1x1 convolution with NT 64-channel input blocks per workgroup: the
 // k-step's 32-pixel dy tile is staged once for NT x tiles (the per-tap kernel re-reads it for
 // every input-channel block). NT = 2 or 4.
-template <int NS, bool OUT_BF16, int NT>
+template <int NS, bool OUT_BF16, int NT, bool PRO>
 __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                     Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
-                                                    int64_t split_stride, int64_t group_stride) {
+                                                    int64_t split_stride, int64_t group_stride,
+                                                    const float* __restrict__ psc, const float* __restrict__ psh) {
   constexpr int TB = 32 * 128;
   constexpr int SB = (1 + NT) * TB;
   __shared__ __attribute__((aligned(16))) char lds[NS * SB];
@@ -788,6 +817,17 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
   const uint32_t offA = (8 * grp + q) * 128 + 32 * (cf0 ^ tg) + 8 * p;
   const uint32_t offB = TB + (8 * grp + q) * 128 + 32 * (kf0 ^ tg) + 8 * p;
   const uint32_t dtr = (tg & 1) ? static_cast<uint32_t>(-32) : 32u;
+  float psv[NT][2] = {}, phv[NT][2] = {};   // PRO: this lane's input channels
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const int64_t o = static_cast<int64_t>(gi) * g.C + c0 + j * 64 + (kf0 + v) * 16 + li;
+        psv[j][v] = psc[o];
+        phv[j][v] = psh[o];
+      }
+  }
 
 #pragma unroll
   for (int s0 = 0; s0 < NS - 1; ++s0)
@@ -845,8 +885,9 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int v = 0; v < 2; ++v) {
-        const bf16x8 bx =
+        bf16x8 bx =
             __builtin_bit_cast(bf16x8, __builtin_shufflevector(rb[j][2 * v], rb[j][2 * v + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+        if constexpr (PRO) bx = pro_frag(bx, psv[j][v], phv[j][v]);
 #pragma unroll
         for (int u = 0; u < 2; ++u)
           acc[j][u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], bx, acc[j][u][v], 0, 0, 0);
@@ -879,10 +920,11 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
 // transposed; 3-deep ring (96 KB: one workgroup per CU).
 constexpr int kW1Stage = 4 * 64 * 128;   // bytes per stage: dy0 | dy1 | x0 | x1
 
-template <bool OUT_BF16>
+template <bool OUT_BF16, bool PRO>
 __global__ __launch_bounds__(256) void k_iwgrad_1x1_wide(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                          Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
-                                                         int64_t split_stride, int64_t group_stride) {
+                                                         int64_t split_stride, int64_t group_stride,
+                                                         const float* __restrict__ psc, const float* __restrict__ psh) {
   constexpr int NS = 3;
   constexpr int SUB = 64 * 128;          // one [64 px][64 ch] sub-tile
   extern __shared__ __attribute__((aligned(16))) char wlds[];
@@ -945,6 +987,15 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1_wide(const uint16_t* __restr
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)wlds));
+  float psv[4] = {}, phv[4] = {};   // PRO: this lane's four input channels
+  if constexpr (PRO) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int64_t o = static_cast<int64_t>(gi) * g.C + c0 + (4 * sbk + v) * 16 + li;
+      psv[v] = psc[o];
+      phv[v] = psh[o];
+    }
+  }
 
 #pragma unroll
   for (int s0 = 0; s0 < NS - 1; ++s0)
@@ -989,6 +1040,7 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1_wide(const uint16_t* __restr
       for (int k = 0; k < 4; ++k) {
         a[k] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ra[2 * k], ra[2 * k + 1], 0, 1, 2, 3, 4, 5, 6, 7));
         b[k] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(rb[2 * k], rb[2 * k + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+        if constexpr (PRO) b[k] = pro_frag(b[k], psv[k], phv[k]);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -1020,55 +1072,70 @@ int iwgrad_taps_per_block(int kw, int kh, int C, int Cout) {
   return kw == 3 ? 3 : 1;
 }
 
-void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
-                 int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream) {
+template <bool PRO>
+void iwgrad_launch(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
+                   int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream,
+                   const float* psc, const float* psh) {
   const int K = g.KH * g.KW * g.C;
   if (splits < 1) splits = 1;
   const int64_t per_split = (rg + splits - 1) / splits;
   const int tpb = iwgrad_taps_per_block(g.KW, g.KH, g.C, Cout);
   if (tpb == 4 && g.KW == 1) {   // 1x1, C and Cout % 128: the 128 x 128-tile kernel
-    static bool once = (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iwgrad_1x1_wide<true>),
+    static bool once = (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iwgrad_1x1_wide<true, PRO>),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kW1Stage),
-                        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iwgrad_1x1_wide<false>),
+                        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iwgrad_1x1_wide<false, PRO>),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kW1Stage),
                         true);
     (void)once;
     const dim3 grid((g.C / 128) * (Cout / 128), groups, splits);
     if (out_bf16)
-      hipLaunchKernelGGL(k_iwgrad_1x1_wide<true>, grid, dim3(256), 3 * kW1Stage, stream, x, dy, g, Cout, rg, per_split,
-                         out, split_stride, group_stride);
+      hipLaunchKernelGGL((k_iwgrad_1x1_wide<true, PRO>), grid, dim3(256), 3 * kW1Stage, stream, x, dy, g, Cout, rg,
+                         per_split, out, split_stride, group_stride, psc, psh);
     else
-      hipLaunchKernelGGL(k_iwgrad_1x1_wide<false>, grid, dim3(256), 3 * kW1Stage, stream, x, dy, g, Cout, rg, per_split,
-                         out, split_stride, group_stride);
+      hipLaunchKernelGGL((k_iwgrad_1x1_wide<false, PRO>), grid, dim3(256), 3 * kW1Stage, stream, x, dy, g, Cout, rg,
+                         per_split, out, split_stride, group_stride, psc, psh);
     return;
   }
   if (tpb == 2 && g.KW == 1) {   // 1x1: two 64-channel input blocks per workgroup, 3 pipeline stages
     const dim3 grid((g.C / 128) * (Cout / 64), groups, splits);
     if (out_bf16)
-      hipLaunchKernelGGL((k_iwgrad_1x1<3, true, 2>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
-                         split_stride, group_stride);
+      hipLaunchKernelGGL((k_iwgrad_1x1<3, true, 2, PRO>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,
+                         out, split_stride, group_stride, psc, psh);
     else
-      hipLaunchKernelGGL((k_iwgrad_1x1<3, false, 2>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
-                         split_stride, group_stride);
+      hipLaunchKernelGGL((k_iwgrad_1x1<3, false, 2, PRO>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split,
+                         out, split_stride, group_stride, psc, psh);
     return;
   }
-  if (tpb == 3) {                // the three taps of a kernel row per workgroup
-    const dim3 grid(g.KH * (g.C / 64) * (Cout / 64), groups, splits);
-    if (out_bf16)
-      hipLaunchKernelGGL((k_iwgrad_rows<3, true, 1>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
-                         split_stride, group_stride);
-    else
-      hipLaunchKernelGGL((k_iwgrad_rows<3, false, 1>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
-                         split_stride, group_stride);
-    return;
+  if constexpr (!PRO) {
+    if (tpb == 3) {                // the three taps of a kernel row per workgroup
+      const dim3 grid(g.KH * (g.C / 64) * (Cout / 64), groups, splits);
+      if (out_bf16)
+        hipLaunchKernelGGL((k_iwgrad_rows<3, true, 1>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                           split_stride, group_stride);
+      else
+        hipLaunchKernelGGL((k_iwgrad_rows<3, false, 1>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                           split_stride, group_stride);
+      return;
+    }
   }
   const dim3 grid((K / 64) * (Cout / 64), groups, splits);
   if (out_bf16)
-    hipLaunchKernelGGL((k_iwgrad<3, true>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
-                       split_stride, group_stride);
+    hipLaunchKernelGGL((k_iwgrad<3, true, PRO>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                       split_stride, group_stride, psc, psh);
   else
-    hipLaunchKernelGGL((k_iwgrad<3, false>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
-                       split_stride, group_stride);
+    hipLaunchKernelGGL((k_iwgrad<3, false, PRO>), grid, dim3(256), 0, stream, x, dy, g, Cout, rg, per_split, out,
+                       split_stride, group_stride, psc, psh);
+}
+
+void iwgrad_nhwc(const uint16_t* x, const uint16_t* dy, const Im2col& g, int Cout, int groups, int64_t rg,
+                 int splits, void* out, bool out_bf16, int64_t split_stride, int64_t group_stride, hipStream_t stream,
+                 const float* pro_scale, const float* pro_shift) {
+  if (pro_scale)   // 1x1 / stride 1 / no padding only (host-checked): the kernels' input has no padding pixel
+    iwgrad_launch<true>(x, dy, g, Cout, groups, rg, splits, out, out_bf16, split_stride, group_stride, stream,
+                        pro_scale, pro_shift);
+  else
+    iwgrad_launch<false>(x, dy, g, Cout, groups, rg, splits, out, out_bf16, split_stride, group_stride, stream, nullptr,
+                         nullptr);
 }
 
 }  // namespace gpu

@@ -37,6 +37,7 @@ test suite); on the GPU the native extension is mandatory.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -70,6 +71,9 @@ GEMM_NT_DGRAD = True
 # the forward through gpu_iconv's automatic choice, the data gradient on the flipped transposed weight
 # (refresh_dgrad_weights) (profiles/r3/conv3x3/).
 CONV3X3 = True
+# A bottleneck's bn2 + ReLU applied inside its 1x1 conv3 (GEMM prologue, weight-gradient prologue, ReLU test
+# recomputed in the BatchNorm backward): the normalised activation is never written (_GroupedBNConv).
+BN_PROLOGUE = os.environ.get("GARFIELD_BN_PROLOGUE", "0") == "1"
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -450,29 +454,38 @@ def _gemm_nt_ok(a2: torch.Tensor, b2: torch.Tensor) -> bool:
 _GEMM_CFG: dict = {}
 
 
-def _gemm_cfg(a2: torch.Tensor, b2: torch.Tensor, rg: int, add: torch.Tensor | None) -> int:
+def _gemm_cfg(a2: torch.Tensor, b2: torch.Tensor, rg: int, add: torch.Tensor | None, pro=None) -> int:
+    """``pro``: (scale, shift, groups) of a BatchNorm prologue on a2 (only configurations with a
+    prologue form are candidates)."""
     C_ = _native.native()
     M, K = a2.shape
     N = b2.shape[0]
-    key = (M, N, K, rg, add is not None)
+    key = (M, N, K, rg, add is not None, pro is not None)
     cfg = _GEMM_CFG.get(key)
     if cfg is not None:
         return cfg
+
+    def pro_ok(c):
+        return pro is None or C_.gemm_nt_pro_ok(c, K, M // pro[2], pro[2])
+
+    cands = [c for c in range(C_.gemm_nt_num_cfg())
+             if C_.gemm_nt_valid(c, N, K) and (rg == 0 or C_.gemm_nt_stats_rows(c) <= rg) and pro_ok(c)]
     cfg = C_.gemm_nt_pick(M, N, K, rg)
+    if cfg >= 0 and not pro_ok(cfg):
+        cfg = cands[0] if cands else -1
     if cfg < 0 or torch.cuda.is_current_stream_capturing():
         return cfg
-    cands = [c for c in range(C_.gemm_nt_num_cfg())
-             if C_.gemm_nt_valid(c, N, K) and (rg == 0 or C_.gemm_nt_stats_rows(c) <= rg)]
     out = torch.empty((M, N), dtype=a2.dtype, device=a2.device)
     addc = add.clone() if add is not None else None
+    pkw = {} if pro is None else {"pro_scale": pro[0], "pro_shift": pro[1], "pro_groups": pro[2]}
     best, best_t = cfg, float("inf")
     for c in cands:
         st = torch.empty(C_.gemm_nt_stats_geometry(c, M, N, K, rg)[2], device=a2.device) if rg else None
-        C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c)   # warm
+        C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c, **pkw)   # warm
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0.record()
         for _ in range(3):
-            C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c)
+            C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c, **pkw)
         t1.record()
         t1.synchronize()
         t = t0.elapsed_time(t1)
@@ -482,10 +495,11 @@ def _gemm_cfg(a2: torch.Tensor, b2: torch.Tensor, rg: int, add: torch.Tensor | N
     return best
 
 
-def _gemm_nt_forward(x2: torch.Tensor, w2: torch.Tensor, spec: ConvSpec):
+def _gemm_nt_forward(x2: torch.Tensor, w2: torch.Tensor, spec: ConvSpec, pro=None):
     """y = x2 · w2ᵀ on gemm_nt.hip; with ``spec.bn_next`` (the BatchNorm that consumes y, a
-    large-layer one) the kernel also writes that BatchNorm's per-worker tile statistics.
-    None: use hipBLASLt."""
+    large-layer one) the kernel also writes that BatchNorm's per-worker tile statistics. ``pro``
+    ((scale, shift, groups)): x2 is a pre-BatchNorm activation, normalised + ReLU'd by the kernel as
+    it stages it. None: use hipBLASLt (never with ``pro``)."""
     if not (GEMM_NT and _gemm_nt_ok(x2, w2)):
         return None
     C_ = _native.native()
@@ -494,10 +508,10 @@ def _gemm_nt_forward(x2: torch.Tensor, w2: torch.Tensor, spec: ConvSpec):
     st = spec.bn_next
     rg = M // spec.groups
     stats_rg = rg if (st is not None and M % spec.groups == 0 and not C_.bn_small(rg)) else 0
-    cfg = _gemm_cfg(x2, w2, stats_rg, None) if stats_rg else -1
+    cfg = _gemm_cfg(x2, w2, stats_rg, None, pro) if stats_rg else -1
     if cfg < 0:
         stats_rg = 0
-        cfg = _gemm_cfg(x2, w2, 0, None)
+        cfg = _gemm_cfg(x2, w2, 0, None, pro)
     if cfg < 0:
         return None
     y2 = torch.empty((M, N), dtype=x2.dtype, device=x2.device)
@@ -505,7 +519,8 @@ def _gemm_nt_forward(x2: torch.Tensor, w2: torch.Tensor, spec: ConvSpec):
     if stats_rg:
         geo = C_.gemm_nt_stats_geometry(cfg, M, N, K, stats_rg)
         stats = torch.empty(geo[2], dtype=torch.float32, device=x2.device)
-    C_.gpu_gemm_nt(x2, w2, y2, None, stats, stats_rg, cfg)
+    pkw = {} if pro is None else {"pro_scale": pro[0], "pro_shift": pro[1], "pro_groups": pro[2]}
+    C_.gpu_gemm_nt(x2, w2, y2, None, stats, stats_rg, cfg, **pkw)
     if stats is not None:
         st.tile = (stats, geo[0], geo[1])
     return y2
@@ -718,10 +733,12 @@ _IWGRAD_MINPIX = 512
 _IWGRAD_MAXS = 64   # ImageNet-size rows: more than 16 splits fill the chip (profiles/r4/splits/in_*: 177.8 -> 177.1 ms)
 
 
-def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int) -> None:
+def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int, pro=None) -> None:
     """Per-worker weight gradients of an iconv-mode convolution without an im2col matrix
     (``gpu_iwgrad``): written straight into the exchange rows when one pass covers every
-    worker's pixels, else as fp32 split slabs summed into the sink."""
+    worker's pixels, else as fp32 split slabs summed into the sink. ``pro`` ((scale, shift), 1x1
+    only): x is a pre-BatchNorm activation normalised + ReLU'd in the kernel."""
+    pkw = {} if pro is None else {"pro_scale": pro[0], "pro_shift": pro[1]}
     cout = dy.shape[1]
     rows = dy.shape[0] * dy.shape[2] * dy.shape[3] // G
     C_ = _native.native()
@@ -733,10 +750,10 @@ def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int)
                           C_.iwgrad_taps_per_block(spec.kernel[1], spec.kernel[0], x.shape[1], cout))
     out = spec.sink.rows_view(spec.conv.weight, (cout, K), dy.dtype) if S == 1 else None
     if out is not None:
-        C_.gpu_iwgrad(x, dy, *_geom(spec), G, out, 1)
+        C_.gpu_iwgrad(x, dy, *_geom(spec), G, out, 1, **pkw)
         return
     part = torch.empty((S, G, cout, K), dtype=torch.float32, device=dy.device)
-    C_.gpu_iwgrad(x, dy, *_geom(spec), G, part, S)
+    C_.gpu_iwgrad(x, dy, *_geom(spec), G, part, S, **pkw)
     rows = spec.sink.rows_view(spec.conv.weight, (cout, K), spec.sink.flat.dtype)
     if rows is not None:     # the S slabs summed straight into the exchange rows (deferred, batched)
         spec.sink.queue_split(part, rows)
@@ -1128,6 +1145,106 @@ def grouped_conv(x, spec: ConvSpec, join: GradJoin | None = None):
     """Convolution with per-worker weight gradients; ``join``: x's other gradient
     branch (see ``GradJoin``)."""
     return _GroupedConv.apply(_cl(x), spec.conv.weight, spec, join)
+
+
+# --------------------------------------------------------------------------- #
+# BatchNorm + ReLU fused into the following 1x1 convolution (the bottleneck's bn2 -> conv3)
+
+
+class _GroupedBNConv(torch.autograd.Function):
+    """conv(relu(BN_per_worker(x))) for a 1x1 stride-1 convolution, without ever writing the
+    normalised activation.
+
+    Forward: the BatchNorm's statistics and per-worker scale / shift only (no apply pass); the
+    convolution's GEMM applies bf16(max(x * scale + shift, 0)) to each A chunk as it lands in LDS
+    (gemm_nt.hip's prologue). Backward: the data gradient is the plain GEMM (it never reads the
+    input); the weight gradient applies the same prologue to its input fragments (iconv_nhwc.hip);
+    the BatchNorm backward recomputes its ReLU test from x, scale and shift (no mask). Saves the
+    apply pass's read + write and the mask of every such BatchNorm, and the next layer reads the
+    pre-BatchNorm tensor it would have read anyway."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, w, st: BNState, ws: Workspace, spec: ConvSpec):
+        n, C, h, wd = x.shape
+        x2 = rows2d(x)
+        st.ensure(x.device)
+        bn, G = st.bn, st.groups
+        rg = x2.shape[0] // G
+        C_ = _native.native()
+        part = ws.get("bn_part", C_.bn_part_floats(rg, G, C), x.device)
+        track = bn.track_running_stats and bn.running_mean is not None
+        tile, st.tile = st.tile, None
+        defer = bool(track and ws.defer_running)
+        C_.gpu_bn_forward(x2, None, G, bn.weight, bn.bias, float(bn.eps), float(bn.momentum),
+                          bn.running_mean if track else None, bn.running_var if track else None,
+                          part, st.mean, st.istd, st.scale, st.shift, None, True, None, defer,
+                          tile_stats=tile[0] if tile is not None else None,
+                          tile_m=tile[1] if tile is not None else 0, tile_e=tile[2] if tile is not None else 1)
+        if defer:
+            ws.running_jobs.append((st.mean, st.istd, bn.running_mean, bn.running_var, rg, float(bn.eps),
+                                    float(bn.momentum)))
+        y2 = _gemm_nt_forward(x2, w.reshape(w.shape[0], -1), spec, pro=(st.scale, st.shift, G))
+        if y2 is None:
+            raise RuntimeError("fused BatchNorm -> 1x1 convolution: no gemm_nt configuration (bn_conv_ok)")
+        ctx.st, ctx.ws, ctx.spec = st, ws, spec
+        ctx.save_for_backward(x, w)
+        return from_rows(y2, n, h, wd)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        st, ws, spec = ctx.st, ctx.ws, ctx.spec
+        dy = _cl(dy)
+        dy2 = rows2d(dy)
+        G = spec.groups
+        cout = dy.shape[1]
+        n, C, h, wd = x.shape
+        w2 = w.reshape(cout, -1)
+        da2 = _gemm_nt_dgrad(dy2, w2, None, spec)          # d(normalised input): never reads x
+        if da2 is None:
+            da2 = torch.mm(dy2, w2)
+        if spec.sink is not None:
+            _iwgrad(x, dy, spec, G, C, pro=(st.scale, st.shift))
+        x2 = rows2d(x)
+        rg = x2.shape[0] // G
+        C_ = _native.native()
+        bn, sink = st.bn, st.sink
+        part = ws.get("bn_part", C_.bn_part_floats(rg, G, C), x.device)
+        coef = ws.get("bn_coef", 3 * G * C, x.device)
+        grow, stride, og, ob = None, 0, -1, -1
+        if sink is not None:
+            grow, stride = sink.flat, sink.row_stride
+            og = sink.base + sink.offset(bn.weight) if bn.weight is not None else -1
+            ob = sink.base + sink.offset(bn.bias) if bn.bias is not None else -1
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        C_.gpu_bn_backward(x2, da2, None, G, bn.weight, st.mean, st.istd, part, coef, rows2d(dx), None, grow, stride,
+                           og, ob, relu_scale=st.scale, relu_shift=st.shift)
+        return dx, None, None, None, None, None, None
+
+
+def bn_conv_ok(x: torch.Tensor, st: BNState, spec: ConvSpec) -> bool:
+    """Whether BatchNorm st (with ReLU) fuses into the 1x1 convolution spec that consumes it: bf16
+    on the GPU, a 1x1 stride-1 GEMM with its weight gradient on the implicit kernels, channel
+    counts the MFMA tiles take, and a gemm_nt configuration with a prologue form."""
+    if not (BN_PROLOGUE and GEMM_NT and IWGRAD_1X1 and IWGRAD and x.is_cuda and x.dtype == torch.bfloat16
+            and spec.gemm and st.relu and spec.sink is not None):
+        return False
+    w = spec.conv.weight
+    if w.dtype != torch.bfloat16 or w.shape[1] % 64 or w.shape[0] % 64 or x.shape[1] % 64:
+        return False
+    M = x.shape[0] * x.shape[2] * x.shape[3]
+    if M % spec.groups:
+        return False
+    C_ = _native.native()
+    K, N, prg = x.shape[1], w.shape[0], M // spec.groups
+    return any(C_.gemm_nt_valid(c, N, K) and C_.gemm_nt_pro_ok(c, K, prg, spec.groups)
+               for c in range(C_.gemm_nt_num_cfg()))
+
+
+def grouped_bn_conv(x, st: BNState, ws: Workspace, spec: ConvSpec):
+    """conv(relu(BN(x))) with the BatchNorm folded into the convolution (see _GroupedBNConv); the
+    caller checks ``bn_conv_ok``."""
+    return _GroupedBNConv.apply(_cl(x), st.bn.weight, st.bn.bias, spec.conv.weight, st, ws, spec)
 
 
 # --------------------------------------------------------------------------- #

@@ -21,9 +21,10 @@ import torch.nn.functional as F
 
 from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
 from garfield_amd.parallel.signals import DeviceSignal
-from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, grouped_bn,
-                                      global_avgpool, grouped_conv, grouped_cross_entropy, grouped_linear,
-                                      grouped_maxpool, refresh_dgrad_weights, refresh_f32_weights)
+from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, bn_conv_ok,
+                                      global_avgpool, grouped_bn, grouped_bn_conv, grouped_conv,
+                                      grouped_cross_entropy, grouped_linear, grouped_maxpool, refresh_dgrad_weights,
+                                      refresh_f32_weights)
 
 
 def supports(model: nn.Module) -> bool:
@@ -133,7 +134,27 @@ class GroupedResNet:
         join = GradJoin() if self.join_residuals else None
         out = self._conv_bn(x, blk.conv1, blk.bn1, True, join)
         if isinstance(blk, Bottleneck):
-            out = self._conv_bn(out, blk.conv2, blk.bn2, True)
+            st2 = self._state(blk.bn2, True)
+            spec2 = self.conv[blk.conv2]
+            spec2.bn_next = st2
+            try:
+                x2 = grouped_conv(out, spec2)            # pre-bn2 (with bn2's statistics when the conv has them)
+            finally:
+                spec2.bn_next = None
+            spec3 = self.conv[blk.conv3]
+            if bn_conv_ok(x2, st2, spec3):
+                # bn2 + ReLU applied by conv3's kernels: the normalised activation is never written
+                st3 = self._state(blk.bn3, True)
+                spec3.bn_next = st3
+                try:
+                    y3 = grouped_bn_conv(x2, st2, self.ws, spec3)
+                finally:
+                    spec3.bn_next = None
+                if blk.downsample is None:
+                    return grouped_bn(y3, st3, self.ws, x, join)
+                sc = self._conv_bn(x, blk.downsample[0], blk.downsample[1], False, join)
+                return grouped_bn(y3, st3, self.ws, sc)
+            out = grouped_bn(x2, st2, self.ws)
             last_conv, last_bn = blk.conv3, blk.bn3
         else:
             last_conv, last_bn = blk.conv2, blk.bn2

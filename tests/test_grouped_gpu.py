@@ -31,9 +31,13 @@ def _bn_ref_group(xg, gamma, beta, eps, rg, relu):
 
 @pytest.mark.parametrize("G,B,H,C,relu,res", [(8, 16, 4, 64, True, False), (3, 5, 3, 96, False, False),
                                               (4, 8, 2, 256, True, True), (2, 9, 1, 2048, True, True),
-                                              (8, 2, 8, 520, True, False), (1, 64, 8, 128, False, True)])
+                                              (8, 2, 8, 520, True, False), (1, 64, 8, 128, False, True),
+                                              (4, 32, 8, 64, True, True), (2, 20, 10, 192, True, False),
+                                              (3, 17, 9, 520, True, True)])
 @pytest.mark.parametrize("defer", [False, True])
 def test_bn_kernels_match_fp32_reference(cuda, G, B, H, C, relu, res, defer):
+    """Grouped BatchNorm forward + backward against an fp32 autograd reference per worker, on the
+    single-kernel small path (<= 1024 rows per worker) and the large path."""
     torch.manual_seed(C + G)
     N = G * B
     x = (torch.randn(N, C, H, H, device=cuda) * 2 + 0.5).to(torch.bfloat16)
@@ -546,3 +550,76 @@ def test_global_avgpool_bf16_matches_mean(cuda, N, C, H):
     assert rel(y.float(), x.detach().float().mean((2, 3))) < 1e-2
     ref = (dy.float() / (H * H))[:, :, None, None].expand(N, C, H, H)
     assert rel(x.grad.float(), ref) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,B,H,C,Co", [(8, 16, 8, 64, 256), (4, 32, 8, 128, 512), (2, 5, 4, 512, 2048),
+                                        (8, 250, 1, 512, 2048), (3, 40, 8, 256, 1024)])
+def test_bn_prologue_conv_matches_fp32_reference(cuda, G, B, H, C, Co, monkeypatch):
+    """BatchNorm + ReLU folded into the following 1x1 convolution (_GroupedBNConv: statistics-only
+    BatchNorm forward, gemm_nt prologue, weight-gradient prologue, ReLU test recomputed in the
+    BatchNorm backward) against an fp32 autograd reference of BN -> ReLU -> conv per worker on the same
+    bf16 operands: the output, dx, and every worker's dW / dγ / dβ in its exchange row."""
+    import garfield_amd.ops.grouped as grouped_ops
+    from garfield_amd.ops.grouped import ConvSpec, bn_conv_ok, grouped_bn_conv
+
+    monkeypatch.setattr(grouped_ops, "BN_PROLOGUE", True)
+    torch.manual_seed(G * C + H)
+    N = G * B
+    x = (torch.randn(N, C, H, H, device=cuda) * 1.5 + 0.3).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(C).to(cuda)
+    conv = nn.Conv2d(C, Co, 1, bias=False).to(cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    ld = Co * C + 2 * C + 64
+    X = torch.zeros(G, ld, dtype=torch.bfloat16, device=cuda)
+    offs = {id(conv.weight): 0, id(bn.weight): Co * C, id(bn.bias): Co * C + C}
+    sink = GradSink(X.view(-1), ld, 0, offs, G)
+    st = BNState(bn, True, sink, G)
+    spec = ConvSpec(conv, sink, G)
+    ws = Workspace()
+    xin = x.clone().requires_grad_(True)
+    assert bn_conv_ok(xin, st, spec)
+    y = grouped_bn_conv(xin, st, ws, spec)
+    dy = torch.randn_like(y).contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    spec.sink.flush()
+    rows = B * H * H
+    x2, dy2 = rows2d(x).float(), rows2d(dy).float()
+    w2 = conv.weight.detach().float().reshape(Co, C)
+    for g in range(G):
+        sl = slice(g * rows, (g + 1) * rows)
+        xg = x2[sl].clone().requires_grad_(True)
+        gam = bn.weight.detach().clone().requires_grad_(True)
+        bet = bn.bias.detach().clone().requires_grad_(True)
+        wg = w2.clone().requires_grad_(True)
+        a = _bn_ref_group(xg, gam, bet, bn.eps, None, True)
+        yg = a @ wg.t()
+        yg.backward(dy2[sl])
+        assert rel(rows2d(y)[sl], yg.detach()) < 2e-2
+        assert rel(rows2d(xin.grad)[sl], xg.grad) < 3e-2
+        assert rel(X[g, :Co * C].view(Co, C), wg.grad) < 2e-2
+        assert rel(X[g, Co * C:Co * C + C], gam.grad) < 3e-2
+        assert rel(X[g, Co * C + C:Co * C + 2 * C], bet.grad) < 3e-2
+
+
+@pytest.mark.gpu
+def test_bn_prologue_step_matches_materialised_step(cuda, monkeypatch):
+    """The grouped ResNet-50 step with bn2 folded into conv3 (BN_PROLOGUE) against the same step with
+    bn2 materialised: the exchange rows of 8 workers agree to bf16 rounding (the normalised activation
+    is rounded once either way; only summation orders differ)."""
+    import garfield_amd.ops.grouped as grouped_ops
+
+    rows = []
+    for on in (False, True):
+        monkeypatch.setattr(grouped_ops, "BN_PROLOGUE", on)
+        torch.manual_seed(0)
+        cfg = EngineConfig(gar="average", f=0, workers_per_rank=8, lr=0.01, cuda_graph=False)
+        eng = RobustDataParallel(build_model("resnet50"), F.cross_entropy, DistContext(device=cuda), cfg)
+        b = synthetic_batches(8, 16, (3, 32, 32), 10, cuda, seed=5)
+        eng.step(b)
+        torch.cuda.synchronize()
+        rows.append(eng.X.float().clone())
+    assert rel(rows[1], rows[0]) < 2e-2
