@@ -108,6 +108,8 @@ def parse():
     p.add_argument("--fps", type=int, default=0, help="Byzantine servers tolerated by the model aggregation")
     p.add_argument("--mar", default="median", help="model aggregation rule of the Byzantine-server mode")
     p.add_argument("--ps-workers", action="store_true", help="server ranks also host logical workers")
+    p.add_argument("--ps-attack", default="", help="attack of the simulated Byzantine servers (ranks < fps), "
+                                                   "e.g. reverse: the Byzantine-server mode's resilience check")
     p.add_argument("--checkpoint", default="", help="save a checkpoint here after the timed steps (untimed)")
     p.add_argument("--resume", default="", help="restore this checkpoint file before the warm-up")
     p.add_argument("--data", default="fresh", choices=["fresh", "static"],
@@ -175,7 +177,7 @@ def build_job(a, ctx, model, shape, num_classes, fp32: bool):
 
         eng = ByzantinePSDataParallel(model, F.cross_entropy, ctx,
                                       ByzPSConfig(**asdict(cfg), num_ps=a.num_ps, fps=a.fps, mar=a.mar,
-                                                  ps_workers=a.ps_workers))
+                                                  ps_workers=a.ps_workers, ps_attack=a.ps_attack))
     else:
         eng = RobustDataParallel(model, F.cross_entropy, ctx, cfg)
     if a.data == "fresh":
@@ -226,7 +228,7 @@ def main():
 
         save_engine(a.checkpoint, eng, meta={"bench": vars(a)}, write=ctx.rank == 0)
     checksums = None
-    if world > 1 and not a.num_ps:   # untimed: the replicas must be bit-identical
+    if world > 1:   # untimed: the replicas must be bit-identical (Byzantine-server mode: every rank, attacker included)
         mine = torch.tensor([eng.replica_checksum()], dtype=torch.float64, device=ctx.device)
         allc = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allc, mine)
@@ -310,7 +312,8 @@ def main():
                 "image_shape": list(shape),
                 "parallelism": f"dp{world} (robust DP, {a.workers_per_gpu} logical workers/GPU, n={n})"
                                + (f", {a.num_ps} Byzantine-resilient server replicas (fps={a.fps}, mar={a.mar}"
-                                  f"{', servers host workers' if a.ps_workers else ''})" if a.num_ps else ""),
+                                  f"{', servers host workers' if a.ps_workers else ''}"
+                                  f"{', server attack ' + a.ps_attack if a.ps_attack else ''})" if a.num_ps else ""),
                 "process_group": {"backend": ctx.backend,
                                   "world_size": dist.get_world_size() if ctx.is_distributed else 1},
                 "gar": a.gar + (" (layer-wise: per parameter tensor)" if a.layerwise else ""),

@@ -885,6 +885,38 @@ void g_large_combine(const at::Tensor& x, const at::Tensor& w, const at::Tensor&
                                w.data_ptr<float>(), out.data_ptr(), stream_of(x.device()));
 }
 
+void g_large_gram(const at::Tensor& x, const at::Tensor& slabs, const at::Tensor& gram) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1 && x.size(0) <= garfield::kLargeRows,
+              "gpu_large_gram: x must be a GPU [n, d] matrix with unit column stride, n <= ", garfield::kLargeRows);
+  const int dt = dtype_code(x);
+  TORCH_CHECK(dt != garfield::kF64, "gpu_large_gram: x must be fp32, bf16 or fp16");
+  const int64_t n = x.size(0), d = x.size(1);
+  const int esz = dt == garfield::kF32 ? 4 : 2;
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && (x.stride(0) * esz) % 16 == 0,
+              "gpu_large_gram: rows must be 16-byte aligned");
+  TORCH_CHECK(gram.device() == x.device() && gram.scalar_type() == at::kFloat && gram.is_contiguous() &&
+                  gram.numel() == n * n, "gpu_large_gram: gram must be a contiguous fp32 [n, n] tensor");
+  ws_vec(slabs, garfield::gpu::large_gram_slab_floats(static_cast<int>(n), d, dt), x.device(), "slabs");
+  c10::hip::HIPGuard guard(x.device().index());
+  garfield::gpu::large_gram(x.data_ptr(), dt, static_cast<int>(n), d, x.stride(0), slabs.data_ptr<float>(),
+                            gram.data_ptr<float>(), stream_of(x.device()));
+}
+
+void g_large_wx(const at::Tensor& W, const at::Tensor& x, const at::Tensor& V) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2 && x.stride(1) == 1, "gpu_large_wx: x must be a GPU [n, d] matrix");
+  const int dt = dtype_code(x);
+  TORCH_CHECK(dt != garfield::kF64, "gpu_large_wx: x must be fp32, bf16 or fp16");
+  const int64_t n = x.size(0), d = x.size(1);
+  TORCH_CHECK(W.device() == x.device() && W.scalar_type() == at::kFloat && W.is_contiguous() && W.dim() == 2 &&
+                  W.size(1) == n, "gpu_large_wx: W must be a contiguous fp32 [t, n] tensor");
+  const int64_t t = W.size(0);
+  TORCH_CHECK(V.device() == x.device() && V.scalar_type() == at::kFloat && V.dim() == 2 && V.size(0) == t &&
+                  V.size(1) == d && V.stride(1) == 1, "gpu_large_wx: V must be an fp32 [t, d] matrix (unit column stride)");
+  c10::hip::HIPGuard guard(x.device().index());
+  garfield::gpu::large_wx(W.data_ptr<float>(), static_cast<int>(t), static_cast<int>(n), x.data_ptr(), dt, d,
+                          x.stride(0), V.data_ptr<float>(), V.stride(0), stream_of(x.device()));
+}
+
 void g_large_coord(const at::Tensor& x, int64_t mode, int64_t f, int64_t beta, const at::Tensor& out) {
   const int dt = large_dtype(x, out);
   const int64_t n = x.size(0);
@@ -1777,6 +1809,25 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dh"), py::arg("dw"), py::arg("dx"), py::arg("accumulate") = false);
 
   m.attr("LARGE_ROWS") = garfield::kLargeRows;
+  m.def("large_gram_slab_floats", [](int64_t n, int64_t d, const at::Tensor& like) {
+    return garfield::gpu::large_gram_slab_floats(static_cast<int>(n), d, dtype_code(like));
+  }, py::arg("n"), py::arg("d"), py::arg("like"), "Workspace floats gpu_large_gram needs for n rows of d elements "
+     "of like's dtype");
+  m.def("gpu_large_gram", &g_large_gram, py::arg("x"), py::arg("slabs"), py::arg("gram"),
+        "fp32 Gram [n, n] of the [n, d] rows x (n <= LARGE_ROWS) on MFMA: split-K 64 x 64 tiles, fixed-order sums");
+  m.def("gpu_large_wx", &g_large_wx, py::arg("W"), py::arg("x"), py::arg("V"),
+        "V [t, d] = W [t, n] fp32 · x [n, d] on fp32 MFMA (Bulyan's selection means)");
+  m.def("gpu_collude", [](const std::vector<at::Tensor>& rows, int64_t peers, bool empire, double param) {
+    RowSet rs = rows_from_list(rows, true);
+    TORCH_CHECK(rs.device.is_cuda(), "gpu_collude: GPU rows");
+    TORCH_CHECK(peers >= 0 && peers < rs.n, "gpu_collude: 0 <= peers < number of rows");
+    TORCH_CHECK(rs.dt != garfield::kF64, "gpu_collude: fp32, bf16 or fp16 rows");
+    c10::hip::HIPGuard guard(rs.device.index());
+    garfield::gpu::collude(rs.table, static_cast<int>(peers), rs.n - static_cast<int>(peers), rs.d, rs.dt, empire,
+                           static_cast<float>(param), stream_of(rs.device));
+  }, py::arg("rows"), py::arg("peers"), py::arg("empire"), py::arg("param"),
+     "Colluding attacks in place on exchanged rows: rows[:peers] are the estimates, rows[peers:] the Byzantine rows "
+     "(their honest gradient in, mean + z * std (lie) or -eps * mean (empire) of {own row} + estimates out)");
   m.def("gpu_large_combine", &g_large_combine,
         "out = w · x for an [n, d] gradient matrix with n <= LARGE_ROWS (fp32 accumulation); args (x, w, out)");
   m.def("gpu_large_select", &g_large_select, py::arg("gram"), py::arg("f"), py::arg("m"), py::arg("rounds"),

@@ -76,6 +76,79 @@ __global__ __launch_bounds__(256) void k_combine(RowTable rows, int n, int64_t d
       store_one(out, out_dt, x, gather_weighted_one<DT>(rows, sel, wsel, cnt, x));
 }
 
+// ---------------------------------------------------------------------------
+// Colluding attacks on the exchanged rows (lie / empire, runtime/attacks.py semantics): rows 0..P-1
+// of the table are the colluders' honest estimates, rows P..P+T-1 the Byzantine rows, which still hold
+// their own honest gradient g_t. With E_t = {g_t} + the P estimates (k = P + 1 rows):
+//   lie    g_t <- mean(E_t) + z * std_unbiased(E_t)
+//   empire g_t <- -eps * mean(E_t)
+// One pass reads the estimates once for every target (per coordinate: their sum, then the sum of
+// squared deviations from their mean in a second pass over the same L2-resident lines), so the
+// estimates are never materialised in fp32 (the ATen form stacked k fp32 copies of every row).
+// var(E_t) = (Q + P (m_p - m_t)^2 + (g_t - m_t)^2) / (k - 1), Q = Σ_p (v_p - m_p)^2.
+template <int DT>
+__global__ __launch_bounds__(256) void k_collude(RowTable rows, int P, int T, int64_t d, int empire, float param) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x * 8;
+  const float k = static_cast<float>(P + 1);
+  for (int64_t x = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 8; x < d; x += stride) {
+    const int nv = d - x >= 8 ? 8 : static_cast<int>(d - x);
+    float s1[8], q[8], mp[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) { s1[c] = 0.f; q[c] = 0.f; }
+    for (int j = 0; j < P; ++j) {
+      float v[8];
+      if (nv == 8) load_vec<DT, 8>(rows.p[j], x, v);
+      else
+        for (int c = 0; c < 8; ++c) v[c] = c < nv ? load_one<DT>(rows.p[j], x + c) : 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) s1[c] += v[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) mp[c] = P > 0 ? s1[c] / static_cast<float>(P) : 0.f;
+    if (!empire) {
+      for (int j = 0; j < P; ++j) {
+        float v[8];
+        if (nv == 8) load_vec<DT, 8>(rows.p[j], x, v);
+        else
+          for (int c = 0; c < 8; ++c) v[c] = c < nv ? load_one<DT>(rows.p[j], x + c) : 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { const float e = v[c] - mp[c]; q[c] = fmaf(e, e, q[c]); }
+      }
+    }
+    for (int t = 0; t < T; ++t) {
+      void* row = const_cast<void*>(rows.p[P + t]);
+      float g[8], o[8];
+      if (nv == 8) load_vec<DT, 8>(row, x, g);
+      else
+        for (int c = 0; c < 8; ++c) g[c] = c < nv ? load_one<DT>(row, x + c) : 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float m = (s1[c] + g[c]) / k;
+        if (empire) {
+          o[c] = -param * m;
+        } else {
+          const float dm = mp[c] - m, dg = g[c] - m;
+          const float var = P > 0 ? (q[c] + static_cast<float>(P) * dm * dm + dg * dg) / (k - 1.f) : 0.f;
+          o[c] = m + param * sqrtf(var > 0.f ? var : 0.f);
+        }
+      }
+      if (nv == 8) store_vec<8>(row, DT, x, o);
+      else
+        for (int c = 0; c < nv; ++c) store_one(row, DT, x + c, o[c]);
+    }
+  }
+}
+
+template <int DT> struct Collude {
+  static void run(const RowTable& rows, int P, int T, int64_t d, int empire, float param, hipStream_t s) {
+    int64_t blocks = (d / 8 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((k_collude<DT>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s, rows, P, T, d, empire,
+                       param);
+  }
+};
+
 __device__ __forceinline__ float sgd_apply(float g, float& p, float& buf, const SgdArgs& a) {
   if (a.weight_decay != 0.f) g += a.weight_decay * p;
   if (a.momentum != 0.f) {
@@ -266,6 +339,11 @@ template <int DT> struct Sqdist {
 void sqdist_partial(const RowTable& rows, int n, int64_t d, int dt, const float* center, float* slabs, int grid,
                     hipStream_t stream) {
   by_dtype<Sqdist>(dt, rows, n, d, center, slabs, grid, stream);
+}
+
+void collude(const RowTable& rows, int P, int T, int64_t d, int dt, bool empire, float param, hipStream_t stream) {
+  if (T <= 0 || d <= 0) return;
+  by_dtype<Collude>(dt, rows, P, T, d, empire ? 1 : 0, param, stream);
 }
 
 void aksel_select(const float* slabs, int grid, int n, int c, float* weights, float* dists, hipStream_t stream) {

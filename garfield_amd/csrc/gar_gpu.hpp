@@ -82,6 +82,13 @@ int coordwise_max_rows();
 // ---- Large gradient sets (kMaxRows < n <= kLargeRows), one [n, ld] matrix (gar_large.hip) ----
 // out[j] = Σ_i w[i] x[i, j] (out in x's dtype); mode 0 median, 1 trimmed-mean(f), 2 averaged-median(beta).
 void large_combine(const void* x, int dt, int n, int64_t d, int64_t ld, const float* w, void* out, hipStream_t stream);
+// fp32 Gram [n, n] of the [n, d] rows x (row stride ld) on MFMA: split-K 64 x 64 tiles into
+// large_gram_slab_floats(n, d, dt) floats of slabs, then a fixed-order reduction (n <= kLargeRows)
+int64_t large_gram_slab_floats(int n, int64_t d, int dt);
+void large_gram(const void* x, int dt, int n, int64_t d, int64_t ld, float* slabs, float* gram, hipStream_t stream);
+// V [t, d] (row stride ldv) = W [t, n] fp32 · x [n, d] (row stride ld) on fp32 MFMA
+void large_wx(const float* W, int t, int n, const void* x, int dt, int64_t d, int64_t ld, float* V, int64_t ldv,
+              hipStream_t stream);
 // Multi-Krum (rounds 1, W [1][n] = 1/m on the m best scores) / Bulyan (rounds t, shrink: W [t][n] with
 // 1/max(m - k, 1) in round k) selection from an fp32 Gram [n][ld] (n <= kLargeRows, 1 <= n - f - 2);
 // thr_val / thr_idx / nearsum: [n] workspaces.
@@ -94,6 +101,10 @@ void large_coord(const void* x, int dt, int n, int64_t d, int64_t ld, int mode, 
 int sqdist_grid(int64_t d);
 void sqdist_partial(const RowTable& rows, int n, int64_t d, int dt, const float* center,
                     float* slabs, int grid, hipStream_t stream);
+// Colluding attacks (runtime/attacks.py lie / empire) in place on the exchanged rows: rows 0..P-1 the
+// colluders' estimates, rows P..P+T-1 the Byzantine rows (holding their honest gradient); param = z
+// (lie) or eps (empire)
+void collude(const RowTable& rows, int P, int T, int64_t d, int dt, bool empire, float param, hipStream_t stream);
 void aksel_select(const float* slabs, int grid, int n, int c, float* weights, float* dists,
                   hipStream_t stream);
 

@@ -350,6 +350,211 @@ __global__ __launch_bounds__(kSelThreads) void k_large_select(const float* __res
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Gram matrix of a large set on MFMA (the selections' distances): G = X Xᵀ for n <= kLargeRows
+// rows. The n x n output is cut into 64 x 64 tiles (4 x 4 blocks of 16 rows); workgroup
+// (split s, tile pair (I, J), I <= J) multiplies rows I*64.. by rows J*64.. over the coordinate
+// chunk of split s, each lane holding the same 64-byte slices of its A and B rows as MFMA operands
+// (a common k permutation of both operands is free for a dot product, as in gar_gram.hip's n <= 128
+// kernel), 4 waves over the chunk, combined in LDS. The split partials are summed in a fixed order
+// by k_large_gram_reduce, which writes both triangles.
+constexpr int kGT = 64;                  // tile rows
+constexpr int kGTB = kGT / 16;           // 16-row blocks per tile side
+
+__device__ __forceinline__ void tri_pair(int p, int T, int& I, int& J) {
+  I = 0;
+  while (p >= T - I) { p -= T - I; ++I; }
+  J = I + p;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void k_large_gram_tile(const void* __restrict__ x, int n, int64_t d, int64_t ld,
+                                                         int T, int64_t chunk, float* __restrict__ slabs) {
+  constexpr int ESZ = (DT == kF32) ? 4 : 2;
+  constexpr int KSPAN = 256 / ESZ;   // elements per row per wave step
+  constexpr int QSPAN = KSPAN / 4;   // elements per lane per wave step
+  __shared__ float red[kGTB * kGTB * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int split = blockIdx.x;
+  int I, J;
+  tri_pair(static_cast<int>(blockIdx.y), T, I, J);
+  const int64_t d_main = (d / KSPAN) * KSPAN;
+  const int64_t start = static_cast<int64_t>(split) * chunk;
+  int64_t end = start + chunk;
+  if (end > d_main) end = d_main;
+  const char* base = static_cast<const char*>(x);
+  const char* ap[kGTB];
+  const char* bp[kGTB];
+  bool av[kGTB], bv[kGTB];
+#pragma unroll
+  for (int a = 0; a < kGTB; ++a) {
+    const int ra = I * kGT + a * 16 + r16, rb = J * kGT + a * 16 + r16;
+    av[a] = ra < n;
+    bv[a] = rb < n;
+    ap[a] = base + static_cast<int64_t>(av[a] ? ra : 0) * ld * ESZ;
+    bp[a] = base + static_cast<int64_t>(bv[a] ? rb : 0) * ld * ESZ;
+  }
+  f32x4 acc[kGTB][kGTB];
+#pragma unroll
+  for (int a = 0; a < kGTB; ++a)
+#pragma unroll
+    for (int b = 0; b < kGTB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t k = start + static_cast<int64_t>(wave) * KSPAN; k < end; k += 4 * KSPAN) {
+    const int64_t off = (k + static_cast<int64_t>(q) * QSPAN) * ESZ;
+    uint4 ua[kGTB][4], ub[kGTB][4];
+#pragma unroll
+    for (int a = 0; a < kGTB; ++a)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        ua[a][s4] = av[a] ? *reinterpret_cast<const uint4*>(ap[a] + off + 16 * s4) : make_uint4(0u, 0u, 0u, 0u);
+        ub[a][s4] = bv[a] ? *reinterpret_cast<const uint4*>(bp[a] + off + 16 * s4) : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+    for (int a = 0; a < kGTB; ++a)
+#pragma unroll
+      for (int b = 0; b < kGTB; ++b)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          if constexpr (DT == kBF16) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ua[a][s4]),
+                                                                __builtin_bit_cast(bf16x8, ub[b][s4]), acc[a][b], 0, 0, 0);
+          } else if constexpr (DT == kF16) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ua[a][s4]),
+                                                               __builtin_bit_cast(f16x8, ub[b][s4]), acc[a][b], 0, 0, 0);
+          } else {
+            const float4 xa = __builtin_bit_cast(float4, ua[a][s4]);
+            const float4 xb = __builtin_bit_cast(float4, ub[b][s4]);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.x, xb.x, acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.y, xb.y, acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.z, xb.z, acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa.w, xb.w, acc[a][b], 0, 0, 0);
+          }
+        }
+  }
+  // 4 waves combined in LDS in a fixed order; C/D map: row = 4 (lane >> 4) + reg, column = lane & 15
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int a = 0; a < kGTB; ++a)
+#pragma unroll
+        for (int b = 0; b < kGTB; ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int idx = (a * 16 + q * 4 + r) * kGT + b * 16 + r16;
+            red[idx] = (w == 0 ? 0.f : red[idx]) + acc[a][b][r];
+          }
+    }
+    __syncthreads();
+  }
+  if (split == 0 && d_main < d) {   // the < KSPAN trailing coordinates
+    for (int e = threadIdx.x; e < kGT * kGT; e += 256) {
+      const int i = I * kGT + e / kGT, j = J * kGT + e % kGT;
+      if (i < n && j < n) {
+        float sum = 0.f;
+        for (int64_t c = d_main; c < d; ++c)
+          sum += load1<DT>(x, static_cast<int64_t>(i) * ld + c) * load1<DT>(x, static_cast<int64_t>(j) * ld + c);
+        red[e] += sum;
+      }
+    }
+    __syncthreads();
+  }
+  float* slab = slabs + (static_cast<int64_t>(blockIdx.y) * gridDim.x + split) * (kGT * kGT);
+  for (int e = threadIdx.x; e < kGT * kGT; e += 256) slab[e] = red[e];
+}
+
+// Σ over the splits (fixed order) of tile pair blockIdx.y, written to both triangles of gram [n, n].
+__global__ __launch_bounds__(256) void k_large_gram_reduce(const float* __restrict__ slabs, int splits, int T, int n,
+                                                           float* __restrict__ gram) {
+  int I, J;
+  tri_pair(static_cast<int>(blockIdx.y), T, I, J);
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= kGT * kGT) return;
+  const float* sp = slabs + static_cast<int64_t>(blockIdx.y) * splits * (kGT * kGT) + e;
+  float sum = 0.f;
+  for (int s2 = 0; s2 < splits; ++s2) sum += sp[static_cast<int64_t>(s2) * (kGT * kGT)];
+  const int i = I * kGT + e / kGT, j = J * kGT + e % kGT;
+  if (i < n && j < n) {
+    gram[static_cast<int64_t>(i) * n + j] = sum;
+    gram[static_cast<int64_t>(j) * n + i] = sum;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// V = W · X on MFMA (Bulyan's t selection means of every coordinate): W [t, n] fp32 (rows of weights
+// 1/mk), X [n, d] (row stride ld, bf16 / fp16 / fp32), V [t, d] fp32 (row stride ldv). fp32 MFMA
+// (v_mfma_f32_16x16x4_f32) on X widened exactly to fp32, so V is the fp32 product of the reference.
+// Workgroup tile: 64 rows of W x 256 coordinates, 16-deep k-steps staged in LDS (X widened to fp32
+// on the way in); wave w owns coordinates [64 w, 64 w + 64) as 4 x 4 16x16 fragments.
+constexpr int kWxT = 64, kWxC = 256, kWxK = 16, kWxXP = kWxC + 8, kWxWP = kWxK + 1;
+
+template <int DT>
+__global__ __launch_bounds__(256) void k_large_wx(const float* __restrict__ W, int t, int n, const void* __restrict__ x,
+                                                  int64_t d, int64_t ld, float* __restrict__ V, int64_t ldv) {
+  __shared__ float xs[kWxK * kWxXP];
+  __shared__ float wsm[kWxT * kWxWP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * kWxC;
+  const int t0 = blockIdx.y * kWxT;
+  // staging roles: X row xr = tid / 16, 16 coordinates from xc = (tid % 16) * 16; W row wr = tid / 4, 4 k
+  const int xr = threadIdx.x >> 4, xc = (threadIdx.x & 15) * 16;
+  const int wr = threadIdx.x >> 2, wk = (threadIdx.x & 3) * 4;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < n; k0 += kWxK) {
+    {   // X tile [16 rows][256 coordinates] -> fp32 LDS
+      const int row = k0 + xr;
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t c = c0 + xc + i;
+        v[i] = (row < n && c < d) ? load1<DT>(x, static_cast<int64_t>(row) * ld + c) : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; i += 4)
+        *reinterpret_cast<float4*>(&xs[xr * kWxXP + xc + i]) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+    }
+    {   // W tile [64 rows][16 k]
+      const int row = t0 + wr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + wk + i;
+        wsm[wr * kWxWP + wk + i] = (row < t && k < n) ? W[static_cast<int64_t>(row) * n + k] : 0.f;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < kWxK; kk += 4) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) av[a] = wsm[(a * 16 + r16) * kWxWP + kk + kq];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) bv[b] = xs[(kk + kq) * kWxXP + wave * 64 + b * 16 + r16];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = t0 + a * 16 + kq * 4 + r;
+        const int64_t c = c0 + wave * 64 + b * 16 + r16;
+        if (row < t && c < d) V[static_cast<int64_t>(row) * ldv + c] = acc[a][b][r];
+      }
+}
+
 }  // namespace
 
 void large_select(const float* gram, int64_t ld, int n, int f, int m, int rounds, bool shrink, double* thr_val,
@@ -378,5 +583,58 @@ void large_coord(const void* x, int dt, int n, int64_t d, int64_t ld, int mode, 
   else launch_coord<kF16>(x, n, d, ld, mode, f, beta, out, stream);
 }
 
+
+int large_gram_tiles(int n) { const int T = (n + kGT - 1) / kGT; return T * (T + 1) / 2; }
+
+int large_gram_splits(int n, int64_t d, int dt) {
+  const int64_t kspan = 256 / (dt == kF32 ? 4 : 2);
+  const int64_t steps = d / kspan;
+  const int pairs = large_gram_tiles(n);
+  int64_t s = (1024 + pairs - 1) / pairs;   // ~1024 workgroups in all
+  const int64_t maxs = steps / 32;          // >= 8 steps per wave
+  if (s > maxs) s = maxs;
+  if (s < 1) s = 1;
+  return static_cast<int>(s);
+}
+
+int64_t large_gram_slab_floats(int n, int64_t d, int dt) {
+  return static_cast<int64_t>(large_gram_tiles(n)) * large_gram_splits(n, d, dt) * kGT * kGT;
+}
+
+namespace {
+template <int DT> struct GramTiles {
+  static void run(const void* x, int n, int64_t d, int64_t ld, float* slabs, float* gram, hipStream_t stream) {
+    constexpr int64_t kspan = 256 / (DT == kF32 ? 4 : 2);
+    const int T = (n + kGT - 1) / kGT;
+    const int pairs = T * (T + 1) / 2;
+    const int splits = large_gram_splits(n, d, DT);
+    const int64_t steps = d / kspan;
+    const int64_t per = (steps + splits - 1) / splits;
+    const int64_t chunk = (per < 1 ? 1 : per) * kspan;
+    hipLaunchKernelGGL((k_large_gram_tile<DT>), dim3(splits, pairs), dim3(256), 0, stream, x, n, d, ld, T, chunk,
+                       slabs);
+    hipLaunchKernelGGL(k_large_gram_reduce, dim3((kGT * kGT + 255) / 256, pairs), dim3(256), 0, stream, slabs, splits,
+                       T, n, gram);
+  }
+};
+template <int DT> struct Wx {
+  static void run(const float* W, int t, int n, const void* x, int64_t d, int64_t ld, float* V, int64_t ldv,
+                  hipStream_t stream) {
+    const dim3 grid(static_cast<unsigned>((d + kWxC - 1) / kWxC), (t + kWxT - 1) / kWxT);
+    hipLaunchKernelGGL((k_large_wx<DT>), grid, dim3(256), 0, stream, W, t, n, x, d, ld, V, ldv);
+  }
+};
+}  // namespace
+
+void large_gram(const void* x, int dt, int n, int64_t d, int64_t ld, float* slabs, float* gram, hipStream_t stream) {
+  if (n <= 0) return;
+  by_dtype<GramTiles>(dt, x, n, d, ld, slabs, gram, stream);
+}
+
+void large_wx(const float* W, int t, int n, const void* x, int dt, int64_t d, int64_t ld, float* V, int64_t ldv,
+              hipStream_t stream) {
+  if (t <= 0 || d <= 0) return;
+  by_dtype<Wx>(dt, W, t, n, x, d, ld, V, ldv, stream);
+}
 }  // namespace gpu
 }  // namespace garfield

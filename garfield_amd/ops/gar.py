@@ -20,7 +20,8 @@ CPU path: the C++ thread-pool implementations in the same extension.
 More than ``MAX_ROWS`` (128) gradients (the reference's gar_bench sweeps n to 512): on
 the GPU, up to ``LARGE_ROWS`` (1024) rows run on ``gar_large.hip`` as one [n, d] matrix
 (combine with fp32 accumulation; median / trimmed-mean / averaged-median and the Bulyan
-tail by LDS radix select; the Krum/Bulyan Gram as one hipBLASLt GEMM with fp32 output);
+tail by LDS radix select; the Krum/Bulyan Gram as a split-K MFMA kernel with fp32 output and
+Bulyan's W·X on fp32 MFMA);
 everything else, and the CPU, uses a vectorised PyTorch implementation.
 """
 from __future__ import annotations
@@ -385,9 +386,11 @@ def bulyan(gradients, f: int, m: int | None = None, **_) -> torch.Tensor:
         X, Wd = _matrix(rows), W.to(rows.device, torch.float32)
         out = torch.empty(rows.d, dtype=torch.float32, device=rows.device)
         step = max(1, (1 << 28) // (4 * max(rows.n, t)))
+        Vbuf = torch.empty((t, min(step, rows.d)), dtype=torch.float32, device=rows.device)
         for c0 in range(0, rows.d, step):
-            V = torch.mm(Wd, X[:, c0:c0 + step].float())
-            _native.native().gpu_large_coord(V, 2, 0, beta, out[c0:c0 + step])
+            w = min(step, rows.d - c0)
+            V = large_wx(Wd, X[:, c0:c0 + w], Vbuf[:, :w])
+            _native.native().gpu_large_coord(V, 2, 0, beta, out[c0:c0 + w])
         return _finish(out, rows)
     if rows.n > MAX_ROWS:
         V = W.to(rows.device) @ rows.stacked().float()
@@ -523,12 +526,35 @@ def aksel(gradients, f: int, mode: str = "mid", **_) -> torch.Tensor:
 # Vectorised PyTorch implementations for n > MAX_ROWS (same semantics).
 
 
+def large_gram(X: torch.Tensor) -> torch.Tensor:
+    """fp32 Gram matrix [n, n] of a GPU [n, d] matrix of up to LARGE_ROWS rows on the MFMA kernel of
+    gar_large.hip (split-K 64 x 64 tiles, fixed-order sums; no library GEMM)."""
+    C = _native.native()
+    if X.stride(1) != 1 or (X.stride(0) * X.element_size()) % 16 or X.data_ptr() % 16:
+        X = X.contiguous()
+        if (X.shape[1] * X.element_size()) % 16:   # pad the rows to 16 bytes (zeros add nothing)
+            X = torch.nn.functional.pad(X, (0, (-X.shape[1]) % (16 // X.element_size())))
+    n, d = X.shape
+    slabs = torch.empty(max(C.large_gram_slab_floats(n, d, X), 1), dtype=torch.float32, device=X.device)
+    g = torch.empty((n, n), dtype=torch.float32, device=X.device)
+    C.gpu_large_gram(X, slabs, g)
+    return g
+
+
+def large_wx(W: torch.Tensor, X: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """V [t, d] = W [t, n] · X [n, d] in fp32 on the MFMA kernel of gar_large.hip."""
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    V = out if out is not None else torch.empty((W.shape[0], X.shape[1]), dtype=torch.float32, device=X.device)
+    _native.native().gpu_large_wx(W.contiguous(), X, V)
+    return V
+
+
 def _large_gram(rows: Rows) -> torch.Tensor:
-    """fp32 Gram matrix of a large set: one hipBLASLt GEMM with fp32 output on 16-bit GPU rows."""
-    X = rows.stacked()
-    if X.is_cuda and X.dtype in (torch.bfloat16, torch.float16):
-        return torch.mm(X, X.T, out_dtype=torch.float32)
-    X = X.float()
+    """fp32 Gram matrix of a large set: the MFMA kernel on the GPU, fp32 matmul on the CPU."""
+    if rows.device.type == "cuda":
+        return large_gram(_matrix(rows))
+    X = rows.stacked().float()
     return X @ X.T
 
 

@@ -24,8 +24,10 @@ things couple samples, and both are kept per worker:
 
 Activation gradients (dgrad) and forward convolutions run once on the whole
 batch: implicit-GEMM MFMA convolutions (``k_iconv_lds``, no im2col matrix) for the
-k x k layers with enough workgroups, hipBLASLt GEMMs on the NHWC rows for 1x1
-stride-1 layers, im2col + GEMM (+ col2im) otherwise. The two gradient branches of
+k x k layers with enough workgroups (the halo-staged conv3x3_nhwc.hip kernels for 3x3 stride-1),
+the hand-written MFMA GEMMs of gemm_nt.hip on the NHWC rows for 1x1 stride-1 layers, im2col +
+gemm_nt (+ col2im) otherwise. Library GEMMs remain only as fallbacks for shapes no kernel takes
+(e.g. channel counts that are not multiples of 64) and for a 1000-class ImageNet classifier. The two gradient branches of
 a residual block's input are summed inside the second branch's kernel
 (``GradJoin``). The custom autograd functions take the real
 parameters as inputs (so the graph reaches them) but return ``None`` for them:

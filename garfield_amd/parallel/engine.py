@@ -480,7 +480,7 @@ class RobustDataParallel:
     def _large_update(self, rule: str, kw: dict, first: bool) -> None:
         """More than MAX_ROWS (128) rows on the GPU (up to LARGE_ROWS = 1024, e.g. Bulyan with
         32 workers per GPU on 8 GPUs): the [n, d] set as one matrix on ``gar_large.hip``
-        (compacted-weight combine, radix-select coordinate rules, hipBLASLt Gram for the
+        (compacted-weight combine, radix-select coordinate rules, split-K MFMA Gram for the
         selections), the aggregate rounded to the exchange dtype, then the fused update."""
         cfg = self.cfg
         if rule in WEIGHTED_RULES:
@@ -896,6 +896,17 @@ class RobustDataParallel:
         honest = [i for i, s in enumerate(slots) if s not in byz]
         fw = sum(1 for s in slots if s in byz)
         peers = honest if self.cfg.collusion == "all" else honest[: max(fw - 1, 0)]
+        if rows[0].is_cuda and rows[0].dtype in (torch.bfloat16, torch.float16, torch.float32) \
+                and len(peers) + len(targets) <= gar.MAX_ROWS:
+            # one fused pass per attack kind (gar_combine.hip k_collude): every Byzantine row from the
+            # estimates read once, in the exchange dtype, no fp32 copies
+            from garfield_amd.runtime.attacks import EMPIRE_EPS, LIE_Z
+
+            for kind, param in (("lie", LIE_Z), ("empire", EMPIRE_EPS)):
+                tg = [rows[i] for i, a in targets if a == kind]
+                if tg:
+                    self._C.gpu_collude([rows[i] for i in peers] + tg, len(peers), kind == "empire", param)
+            return
         ests = [rows[i].float() for i in peers]
         for i, attack in targets:
             g = rows[i].float()

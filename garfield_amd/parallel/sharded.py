@@ -577,8 +577,8 @@ class ShardedAggregator:
 
     def _gpu_large(self, cfg, first: bool) -> None:
         """More than MAX_ROWS rows (e.g. 8 GPUs x 32 workers): each bucket's shards as one
-        matrix on the gar_large.hip kernels (Gram by hipBLASLt with fp32 output, compacted
-        combine, radix-select coordinate rules). Selections are made in slot order (the
+        matrix on the gar_large.hip kernels (split-K MFMA Gram and W·X with fp32 output,
+        compacted combine, radix-select coordinate rules). Selections are made in slot order (the
         partial Grams permuted once), then mapped back to the matrix's row order."""
         e, C = self.e, self.e._C
         rule, f, kw = cfg.gar, cfg.f, dict(cfg.gar_kwargs)
@@ -594,8 +594,7 @@ class ShardedAggregator:
         if rule in ("krum", "bulyan"):
             total = None
             for b in self.buckets:
-                X = mats[b.lo]
-                g = torch.mm(X, X.T, out_dtype=torch.float32) if X.dtype != torch.float32 else X @ X.T
+                g = gar.large_gram(mats[b.lo])                  # MFMA, fp32 (gar_large.hip)
                 total = g if total is None else total.add_(g)
             gs = self._sum_over_ranks(total)[perm][:, perm]          # slot order on every rank
             m = cfg.m if cfg.m is not None else n - f - 2
@@ -608,7 +607,7 @@ class ShardedAggregator:
                 t, beta = n - 2 * f - 2, n - 4 * f - 2
                 e.last_weights = None
                 for b in self._update_order():
-                    V = torch.mm(Wm, mats[b.lo].float())          # [t, S] fp32 (bounded: one shard)
+                    V = gar.large_wx(Wm, mats[b.lo])               # [t, S] fp32 on MFMA (bounded: one shard)
                     g = self._gagg(b)
                     C.gpu_large_coord(V, 2, 0, beta, g)
                     p, mom, sh = self._param(b)

@@ -438,3 +438,28 @@ def test_grouped_resume_after_capture_is_exact(cuda, tmp_path):
         eng.step(batches)
     assert eng._ggraph is not None
     assert torch.equal(eng.flat_model(), straight)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,T,d,dtype", [(3, 2, 100003, torch.bfloat16), (0, 1, 4096, torch.bfloat16),
+                                         (7, 1, 5000, torch.float32), (1, 3, 777, torch.float16)])
+def test_fused_collude_kernel_matches_attack_functions(cuda, native, P, T, d, dtype):
+    """gar_combine.hip k_collude (lie / empire in place on the exchanged rows, estimates read once)
+    against runtime/attacks.py's lie_attack / empire_attack on the same rows (fp32 statistics, one
+    rounding to the exchange dtype)."""
+    from garfield_amd.runtime.attacks import EMPIRE_EPS, LIE_Z, empire_attack, lie_attack
+
+    g = torch.Generator(device="cpu").manual_seed(P * 31 + T)
+    for empire in (False, True):
+        X = (torch.randn(P + T, d, generator=g) * 0.01 + 0.003).to(dtype).to(cuda)
+        ests = [X[i].float() for i in range(P)]
+        want = []
+        for t in range(T):
+            gt = X[P + t].float()
+            E = torch.stack([gt, *ests])
+            want.append((empire_attack if empire else lie_attack)(gt, E).to(dtype))
+        native.gpu_collude([X[i] for i in range(P + T)], P, empire, EMPIRE_EPS if empire else LIE_Z)
+        for t in range(T):
+            got, w = X[P + t].float(), want[t].float()
+            err = ((got - w).abs() / (w.abs() + 1e-3)).max().item()
+            assert err < 1e-2, (empire, t, err)

@@ -129,3 +129,35 @@ def test_engine_n256_on_device(cuda, monkeypatch, rule):
             want = ref.bulyan(G, f, n - f - 2) if rule == "bulyan" else ref.krum(G, f, n - f - 2)
             assert ((deltas[-1] - want).norm() / want.norm()).item() < 1e-5
     assert ((deltas[1] - deltas[0]).norm() / deltas[0].norm()).item() < 1e-6
+
+
+@pytest.mark.parametrize("n,d,dtype", [(129, 5000, torch.bfloat16), (256, 100000, torch.bfloat16),
+                                       (1024, 20000, torch.bfloat16), (300, 7777, torch.float32),
+                                       (512, 3001, torch.float16)])
+def test_large_gram_mfma_matches_fp64(cuda, n, d, dtype):
+    """gar_large.hip's split-K MFMA Gram (64 x 64 tiles, fixed-order slab sums; rows not a multiple of
+    64, d not a multiple of the k-step) against the fp64 Gram of the same (rounded) rows."""
+    g = torch.Generator().manual_seed(n + d)
+    X = torch.randn(n, d, generator=g, dtype=torch.float64).to(dtype)
+    G = gar.large_gram(X.to(cuda))
+    ref_g = X.double() @ X.double().T
+    assert G.shape == (n, n)
+    err = ((G.double().cpu() - ref_g).abs() / (ref_g.abs() + d ** 0.5)).max().item()
+    assert err < 1e-4, err
+    assert torch.equal(G.cpu(), G.cpu().T)
+
+
+@pytest.mark.parametrize("t,n,d,dtype", [(252, 256, 40000, torch.bfloat16), (70, 129, 1000, torch.float32),
+                                         (1000, 1024, 3000, torch.bfloat16)])
+def test_large_wx_mfma_matches_fp64(cuda, t, n, d, dtype):
+    """V = W · X on fp32 MFMA (Bulyan's selection means) against fp64, W with 1/mk weights."""
+    g = torch.Generator().manual_seed(t + n)
+    X = torch.randn(n, d, generator=g, dtype=torch.float64).to(dtype)
+    W = torch.zeros(t, n, dtype=torch.float64)
+    for k in range(t):
+        mk = max(n // 2 - k, 1)
+        W[k, torch.randperm(n, generator=g)[:mk]] = 1.0 / mk
+    V = gar.large_wx(W.float().to(cuda), X.to(cuda))
+    ref_v = W.float().double() @ X.double()
+    err = ((V.double().cpu() - ref_v).abs() / (ref_v.abs() + 1.0)).max().item()
+    assert err < 1e-5, err

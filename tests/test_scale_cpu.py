@@ -257,3 +257,35 @@ def test_byzantine_server_model_exchange_moves_only_server_rows(num_ps):
         assert 0 < r["bytes"] <= num_ps * r["ld"] * 4, (r["bytes"], num_ps * r["ld"] * 4)
     honest = res[1:] if num_ps > 2 else res   # rank 0 is the Byzantine server when fps = 1
     assert all(torch.equal(r["flat"], honest[-1]["flat"]) for r in honest)
+
+
+def _byzps_cfg5_worker(rank, world, port, outdir, ps_attack):
+    from garfield_amd.parallel.byzps import ByzantinePSDataParallel, ByzPSConfig
+    from garfield_amd.parallel.comm import shutdown
+
+    ctx = _init(rank, world, port)
+    torch.manual_seed(0)
+    eng = ByzantinePSDataParallel(build_model("mlp"), F.nll_loss, ctx,
+                                  ByzPSConfig(gar="trimmed-mean", f=1, workers_per_rank=1, num_ps=3, fps=1,
+                                              mar="median", ps_attack=ps_attack, lr=0.05))
+    assert eng.n_w == 5 and eng.is_ps == (rank < 3)
+    for it in range(3):
+        eng.step(synthetic_batches(1, 8, (1, 28, 28), 10, "cpu", seed=10 * it + rank))
+    torch.save({"flat": eng.flat_model().clone()}, os.path.join(outdir, f"{ps_attack or 'none'}_{rank}.pt"))
+    shutdown(ctx)
+
+
+def test_byzantine_server_config5_attacked_server_is_rejected():
+    """BASELINE config 5's pattern: 3 server replicas + 5 worker ranks, f_ps = 1, f_w = 1, Trimmed-Mean
+    over the workers, coordinate-wise median as the model aggregation. Server rank 0 is Byzantine and
+    replaces its model by -100 x its update (``ps_attack=reverse``) every step: every rank -- the
+    attacker included, which adopts the aggregate too -- ends bit-identical to the attack-free run (the
+    median of three models, two of them the honest servers' identical ones, is the honest model)."""
+    world = 8
+    with tempfile.TemporaryDirectory() as d:
+        for attack in ("", "reverse"):
+            mp.spawn(_byzps_cfg5_worker, args=(world, free_port(), d, attack), nprocs=world, join=True)
+        clean = [torch.load(os.path.join(d, f"none_{r}.pt"), weights_only=True)["flat"] for r in range(world)]
+        hit = [torch.load(os.path.join(d, f"reverse_{r}.pt"), weights_only=True)["flat"] for r in range(world)]
+    assert all(torch.equal(c, clean[0]) for c in clean)
+    assert all(torch.equal(h, clean[0]) for h in hit)
