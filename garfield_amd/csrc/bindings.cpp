@@ -604,6 +604,123 @@ void g_col2im(const at::Tensor& dcol, int64_t kh, int64_t kw, int64_t sh, int64_
   garfield::gpu::col2im_nhwc(u16(dcol), g, u16_mut(dx), accumulate, stream_of(dx.device()));
 }
 
+// Small-image 3x3 convolutions as dense GEMMs (sconv_nhwc.hip): the per-step weight expansion of every
+// such layer (one launch) and the fold of a dense weight gradient onto the nine taps.
+void g_sc_expand(const std::vector<at::Tensor>& ws, const std::vector<int64_t>& hs, const std::vector<int64_t>& wds,
+                 const std::vector<at::Tensor>& bigs, const std::vector<at::Tensor>& bigTs) {
+  const size_t n = ws.size();
+  TORCH_CHECK(hs.size() == n && wds.size() == n && bigs.size() == n && bigTs.size() == n,
+              "gpu_sc_expand: one H, W, Wbig and Wbigᵀ per weight");
+  if (n == 0) return;
+  c10::hip::HIPGuard guard(ws[0].device().index());
+  garfield::gpu::ScExpandJobs jobs{};
+  auto flush = [&]() {
+    if (jobs.count) garfield::gpu::sc_expand(jobs, stream_of(ws[0].device()));
+    jobs = garfield::gpu::ScExpandJobs{};
+  };
+  for (size_t k = 0; k < n; ++k) {
+    const auto& w = ws[k];
+    const int64_t H = hs[k], W = wds[k];
+    TORCH_CHECK(w.is_cuda() && w.device() == ws[0].device() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 &&
+                    w.size(2) == 3 && w.size(3) == 3 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_sc_expand: weights must be channels_last bf16 [Cout, Cin, 3, 3] on one device");
+    const int64_t co = w.size(0), ci = w.size(1), P = H * W;
+    TORCH_CHECK(H >= 1 && H <= 2 && W >= 1 && W <= 2 && ci % 8 == 0, "gpu_sc_expand: H, W in {1, 2}, Cin % 8 == 0");
+    for (const auto* t : {&bigs[k], &bigTs[k]})
+      TORCH_CHECK(t->device() == w.device() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
+                      t->numel() == P * co * P * ci,
+                  "gpu_sc_expand: Wbig / Wbigᵀ must be contiguous bf16 of ", P * co, " x ", P * ci, " elements");
+    TORCH_CHECK(bigs[k].dim() == 2 && bigs[k].size(0) == P * co && bigTs[k].dim() == 2 && bigTs[k].size(0) == P * ci,
+                "gpu_sc_expand: Wbig is [P*Cout, P*Cin], Wbigᵀ [P*Cin, P*Cout]");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(bigs[k].data_ptr()) % 16 == 0,
+                "gpu_sc_expand: 16-byte aligned weight and Wbig");
+    if (jobs.count == garfield::gpu::kScMaxJobs) flush();
+    auto& J = jobs.job[jobs.count];
+    J.w = u16(w);
+    J.big = u16_mut(bigs[k]);
+    J.bigT = u16_mut(bigTs[k]);
+    J.cout = static_cast<int>(co);
+    J.cin = static_cast<int>(ci);
+    J.H = static_cast<int>(H);
+    J.W = static_cast<int>(W);
+    jobs.start[jobs.count + 1] = jobs.start[jobs.count] + P * co * P * ci / 8;
+    ++jobs.count;
+  }
+  flush();
+}
+
+void g_sc_fold(const at::Tensor& slab, int64_t H, int64_t W, const at::Tensor& out) {
+  TORCH_CHECK(slab.is_cuda() && slab.scalar_type() == at::kFloat && slab.dim() == 4 && slab.is_contiguous(),
+              "gpu_sc_fold: slab must be a contiguous fp32 [S, G, P*Cout, P*Cin] device tensor");
+  TORCH_CHECK(out.device() == slab.device() && (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat) &&
+                  out.dim() == 3 && out.stride(2) == 1 && out.stride(1) == out.size(2),
+              "gpu_sc_fold: out must be a bf16 / fp32 [G, Cout, 9*Cin] view with dense rows");
+  const int64_t P = H * W, S = slab.size(0), G = slab.size(1), co = out.size(1), ci = out.size(2) / 9;
+  TORCH_CHECK(H >= 1 && H <= 2 && W >= 1 && W <= 2 && out.size(2) == 9 * ci && ci % 8 == 0 && out.size(0) == G &&
+                  slab.size(2) == P * co && slab.size(3) == P * ci,
+              "gpu_sc_fold: shapes do not match (slab [S, G, P*Cout, P*Cin], out [G, Cout, 9*Cin])");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && (out.stride(0) * out.element_size()) % 16 == 0,
+              "gpu_sc_fold: out rows must be 16-byte aligned");
+  c10::hip::HIPGuard guard(slab.device().index());
+  garfield::gpu::sc_fold(slab.data_ptr<float>(), static_cast<int>(S), static_cast<int>(G), static_cast<int>(H),
+                         static_cast<int>(W), static_cast<int>(co), static_cast<int>(ci), out.data_ptr(),
+                         out.scalar_type() == at::kBFloat16, out.stride(0), stream_of(slab.device()));
+}
+
+// Data gradient of a stride-2 convolution on the parity-class kernel (iconv_nhwc.hip):
+// dx (+)= conv_transpose(dy, w); dy/dx/add channels_last bf16, w the channels_last forward weight.
+garfield::gpu::Im2col s2_geometry(const at::Tensor& dy, const at::Tensor& dx, int64_t kh, int64_t kw, int64_t ph,
+                                  int64_t pw) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dx.is_cuda() && dx.device() == dy.device() &&
+                  dx.scalar_type() == at::kBFloat16 && dx.dim() == 4 && dx.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dx.size(0) == dy.size(0),
+              "gpu_dgrad_s2: dy and dx must be channels_last bf16 device tensors of one batch");
+  garfield::gpu::Im2col g{};
+  g.N = static_cast<int>(dy.size(0));
+  g.C = static_cast<int>(dy.size(1));
+  g.H = static_cast<int>(dy.size(2));
+  g.W = static_cast<int>(dy.size(3));
+  g.Ho = static_cast<int>(dx.size(2));
+  g.Wo = static_cast<int>(dx.size(3));
+  g.KH = static_cast<int>(kh); g.KW = static_cast<int>(kw);
+  g.sh = g.sw = 2;
+  g.ph = static_cast<int>(ph); g.pw = static_cast<int>(pw);
+  g.dh = g.dw = 1;
+  return g;
+}
+
+bool g_dgrad_s2_ok(const at::Tensor& dy, const at::Tensor& dx, int64_t kh, int64_t kw, int64_t ph, int64_t pw) {
+  return garfield::gpu::dgrad_s2_ok(s2_geometry(dy, dx, kh, kw, ph, pw), static_cast<int>(dx.size(1)));
+}
+
+void g_dgrad_s2(const at::Tensor& dy, const at::Tensor& w, int64_t kh, int64_t kw, int64_t ph, int64_t pw,
+                const at::Tensor& dx, const c10::optional<at::Tensor>& add, int64_t pm) {
+  auto g = s2_geometry(dy, dx, kh, kw, ph, pw);
+  const int64_t cout = dx.size(1);
+  TORCH_CHECK(garfield::gpu::dgrad_s2_ok(g, static_cast<int>(cout)),
+              "gpu_dgrad_s2: needs a stride-2 geometry with even dx sides, C % 64 == 0, Cout % 64 == 0, k <= 3, pad <= 1");
+  TORCH_CHECK(w.device() == dy.device() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == g.C &&
+                  w.size(1) == cout && w.size(2) == kh && w.size(3) == kw && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "gpu_dgrad_s2: w must be the channels_last bf16 forward weight [", g.C, ", ", cout, ", ", kh, ", ", kw, "]");
+  const uint16_t* ap = nullptr;
+  if (add.has_value()) {
+    const auto& a = *add;
+    TORCH_CHECK(a.device() == dx.device() && a.scalar_type() == at::kBFloat16 && a.sizes() == dx.sizes() &&
+                    a.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "gpu_dgrad_s2: add must be a channels_last bf16 tensor shaped like dx");
+    ap = u16(a);
+  }
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(dx.data_ptr()) % 8 == 0 &&
+                  (ap == nullptr || reinterpret_cast<uintptr_t>(ap) % 8 == 0),
+              "gpu_dgrad_s2: dy and w must be 16-byte aligned, dx and add 8-byte aligned");
+  TORCH_CHECK(dy.numel() < INT32_MAX && static_cast<int64_t>(g.N) * g.Ho * g.Wo < INT32_MAX, "gpu_dgrad_s2: tensor too large");
+  c10::hip::HIPGuard guard(dy.device().index());
+  garfield::gpu::dgrad_s2_nhwc(u16(dy), u16(w), g, static_cast<int>(cout), u16_mut(dx), ap, static_cast<int>(pm),
+                               stream_of(dy.device()));
+}
+
 // Implicit-GEMM convolution: y = conv(x, w) (+ add); x/y/add channels_last bf16, w the
 // [Cout, KH, KW, C]-ordered weight (a channels_last 4-D weight or its [Cout, K] matrix).
 void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
@@ -1906,6 +2023,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "Rows per statistics tile of the halo-staged 3x3 kernel's BatchNorm-statistics epilogue (0: no fit); "
         "the stats buffer holds ceil(M / rows) * 6 * Cout floats (E = 1)");
 
+  m.def("gpu_sc_expand", &g_sc_expand, py::arg("weights"), py::arg("hs"), py::arg("ws"), py::arg("bigs"),
+        py::arg("bigTs"), "Per-step expansion of 3x3 weights for images of at most 2x2 pixels: Wbig[(p', co), (p, ci)] "
+        "= W[co, h - h' + 1, w - w' + 1, ci] (0 off the kernel) and its transpose, every layer in one launch");
+  m.def("gpu_sc_fold", &g_sc_fold, py::arg("slab"), py::arg("h"), py::arg("w"), py::arg("out"),
+        "Fold a dense small-image weight gradient (fp32 [S, G, P*Cout, P*Cin]) onto the nine taps: out[g, co, "
+        "(i, j, ci)] = Σ_s Σ over the pixel pairs of tap (i, j)");
+  m.def("gpu_dgrad_s2", &g_dgrad_s2, "Data gradient of a stride-2 convolution on MFMA without a dcol matrix: dx = "
+        "conv_transpose(dy, w) (+ add, in place of add when given; dx may be add); args (dy, w, kh, kw, ph, pw, dx, "
+        "add=None, pm=0); w the channels_last forward weight [C, Cout, KH, KW]", py::arg("dy"), py::arg("w"),
+        py::arg("kh"), py::arg("kw"), py::arg("ph"), py::arg("pw"), py::arg("dx"), py::arg("add") = py::none(),
+        py::arg("pm") = 0);
+  m.def("dgrad_s2_ok", &g_dgrad_s2_ok, py::arg("dy"), py::arg("dx"), py::arg("kh"), py::arg("kw"), py::arg("ph"),
+        py::arg("pw"), "True when gpu_dgrad_s2 takes this geometry");
   m.def("conv3x3_pick", &g_conv3x3_pick, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("c"), py::arg("cout"),
         "Pixel fragments per wave the halo-staged 3x3 kernel uses for this NHWC shape (0: it does not fit)");
   m.def("wgrad3x3_fits", &g_wgrad3x3_fits, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("c"), py::arg("cout"),

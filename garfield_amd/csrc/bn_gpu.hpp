@@ -138,6 +138,32 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
 // the pixel fragments per wave (4 or 2) it would use, 0 when the shape does not fit; conv3x3_nhwc
 // returns false (and launches nothing) in that case. pmf <= 0: auto.
 int conv3x3_pick(const Im2col& g, int Cout);
+// 3x3 / stride-1 / pad-1 convolutions on images of at most 2x2 pixels as dense GEMMs (sconv_nhwc.hip):
+// per step, every such layer's W [Cout, 3, 3, Cin] -> Wbig [P*Cout, P*Cin] and Wbigᵀ in one launch
+// (P = H * W), and the fold of the dense weight gradient [S, G, P*Cout, P*Cin] (fp32) onto the taps.
+struct ScExpandJob {
+  const uint16_t* w;
+  uint16_t* big;
+  uint16_t* bigT;
+  int cout, cin, H, W;
+};
+constexpr int kScMaxJobs = 32;
+struct ScExpandJobs {
+  ScExpandJob job[kScMaxJobs];
+  int64_t start[kScMaxJobs + 1];   // prefix sums of the 8-element units of each job's Wbig
+  int count;
+};
+void sc_expand(const ScExpandJobs& jobs, hipStream_t stream);
+void sc_fold(const float* slab, int S, int G, int H, int W, int cout, int cin, void* out, bool out_bf16,
+             int64_t gstride, hipStream_t stream);
+
+// Data gradient of a stride-2 convolution (iconv_nhwc.hip, k_iconv_lds S2): four parity classes of
+// dx, each a stride-1 correlation of dy with its sub-kernel; no dcol matrix, no col2im. g: the
+// forward geometry seen from dy (H, W, C = dy's; Ho, Wo = dx's, even; sh = sw = 2); w: the forward
+// channels_last weight [C, Cout, KH, KW]; add: folded into dx.
+bool dgrad_s2_ok(const Im2col& g, int Cout);
+void dgrad_s2_nhwc(const uint16_t* dy, const uint16_t* w, const Im2col& g, int Cout, uint16_t* dx, const uint16_t* add,
+                   int pm, hipStream_t stream);
 // stats (nullable, no add): per-worker (rg pixels) BatchNorm statistics of y for bn_finalize_tiles, one
 // statistics tile of 16 * pmf pixels per wave (H = 16 * pmf, E = 1: ceil(M / H) * 6 * Cout floats).
 bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,

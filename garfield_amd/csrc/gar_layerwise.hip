@@ -20,6 +20,8 @@
 //
 // Segment boundaries are arbitrary element offsets (a BatchNorm bias of 64, a 9408-element
 // stem): 16-byte loads where a group is aligned, element loads where it is not.
+#include <cstdlib>
+
 #include "gar_coord.hpp"
 #include "gar_device.hpp"
 
@@ -27,6 +29,15 @@ namespace garfield {
 namespace gpu {
 using namespace dev;
 namespace {
+
+// GARFIELD_LW_TAIL_MFMA=0: the scalar per-coordinate tail (A/B switch)
+bool lw_tail_mfma_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("GARFIELD_LW_TAIL_MFMA");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Segmented Gram partials: the k_gram_partial scheme (gar_gram.hip) over [start, end) of one
@@ -301,9 +312,238 @@ __global__ __launch_bounds__(256) void k_lw_bulyan_tail(RowTable rows, int n, co
   }
 }
 
+// The same tail on MFMA (coord::k_bulyan_tail_mfma's scheme, per job): a workgroup builds its job's
+// segment set tables, then each wave takes whole 64-coordinate groups of the job ([64 q, 64 q + 64)
+// inside [a, b): v_mfma_f32_32x32x16 set sums, register-sorted window mean); groups with a
+// non-finite sum and the job's partial head / tail groups (a group that a segment boundary cuts)
+// take the exact per-set sums. Job boundaries are segment boundaries or multiples of 64 (the
+// engines split jobs at global multiples of LW_JOB, shards are whole 64-blocks), so which
+// coordinates take the MFMA sums does not depend on how the vector is sharded.
+template <int DT, int NP, int KS>
+__global__ __launch_bounds__(256, 2) void k_lw_bulyan_tail_mfma(RowTable rows, int n, const int64_t* __restrict__ jobs,
+                                                                const float* __restrict__ Wall, int t, int beta,
+                                                                float* __restrict__ out) {
+  using namespace coord;
+  constexpr int MB = NP > 32 ? 2 : 1;
+  constexpr int KR = 16 * KS;
+  constexpr int KRP = KR + 8;
+  constexpr int P0 = wm_p0(NP);
+  constexpr int WAVE_LDS = KR * kMfmaTailPitch > (NP - P0) * 256 ? KR * kMfmaTailPitch : (NP - P0) * 256;
+  __shared__ __align__(16) unsigned char tiles[4][WAVE_LDS];
+  __shared__ __align__(16) uint16_t sA[32 * MB * KRP];
+  __shared__ const void* sptr[KR];
+  __shared__ uint64_t smask[NP];
+  __shared__ __align__(16) float sscale[NP];
+  __shared__ __align__(16) float spad[NP];
+  __shared__ int64_t sbad[4][kTailBadSlots];
+  __shared__ int sbadn[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t a = jobs[3 * blockIdx.x], b = jobs[3 * blockIdx.x + 1];
+  const float* W = Wall + jobs[3 * blockIdx.x + 2] * static_cast<int64_t>(t) * n;
+  // a workgroup with no whole group of the job and no partial range to do leaves before the tables
+  if ((a + 63) / 64 + static_cast<int64_t>(blockIdx.y) * 4 >= b / 64 && (blockIdx.y != 0 || (a % 64 == 0 && b % 64 == 0)))
+    return;
+  {
+    const uint16_t one = DT == kBF16 ? 0x3F80 : 0x3C00;
+    for (int k = wave; k < 32 * MB; k += 4) {
+      const float w = (k < t && lane < n) ? W[k * n + lane] : 0.f;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(w != 0.f);
+      if (lane < KR) sA[k * KRP + lane] = w != 0.f ? one : 0;
+      if (k < NP) {
+        const int first = m ? __builtin_ctzll(m) : 0;
+        const float sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), first));
+        if (lane == 0) {
+          smask[k] = m;
+          sscale[k] = m ? sc : 0.f;
+          spad[k] = k < t ? 0.f : kInf;
+        }
+      }
+    }
+  }
+  for (int j = threadIdx.x; j < KR; j += blockDim.x) sptr[j] = rows.p[j < n ? j : 0];
+  if (threadIdx.x < 4) sbadn[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned char* tile = tiles[wave];
+  float* ks = reinterpret_cast<float*>(tile);
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int tr_off = (8 * (g >> 1) + q) * kMfmaTailPitch + (16 * (g & 1) + 4 * p) * 2;
+  const int a_off = (lane & 31) * KRP + 8 * (lane >> 5);
+  const float inv_beta = 1.f / static_cast<float>(beta);
+  bool overflow = false;
+  const int64_t q0 = (a + 63) / 64, q1 = b / 64;      // whole groups [q0, q1)
+  const int64_t gstep = static_cast<int64_t>(gridDim.y) * 4;
+  const int64_t gfirst = q0 + static_cast<int64_t>(blockIdx.y) * 4 + wave;
+  TileRegs<KR> pre;
+  if (gfirst < q1) tile_load<KR>(pre, sptr, gfirst * 64, lane, n);
+  for (int64_t gi = gfirst; gi < q1; gi += gstep) {
+    asm volatile("" ::: "memory");
+    const int64_t x0 = gi * 64;
+    const int nn = opaque_uniform(n), tt = opaque_uniform(t), bb = opaque_uniform(beta);
+    tile_store<KR>(tile, pre, nn, lane);
+    if (gi + gstep < q1) tile_load<KR>(pre, sptr, (gi + gstep) * 64, lane, nn);
+    f32x16_t acc[MB][2];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[mb][nb][i] = 0.f;
+#pragma unroll
+    for (int ks_ = 0; ks_ < KS; ++ks_) {
+      s16x8_t afrag[MB];
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        afrag[mb] = *reinterpret_cast<const s16x8_t*>(&sA[a_off + 32 * mb * KRP + 16 * ks_]);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+        const unsigned char* base = tile + ks_ * 16 * kMfmaTailPitch + nb * 64 + tr_off;
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * kMfmaTailPitch));
+        const s16x8_t bfrag = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) acc[mb][nb] = mfma32x32x16<DT>(afrag[mb], bfrag, acc[mb][nb]);
+      }
+    }
+    float v[NP];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int k0 = 32 * mb + (i & 3) + 8 * (i >> 2);
+        if (k0 < NP) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[mb][0][i]),
+                                                           __float_as_uint(acc[mb][1][i]), false, false);
+          v[k0] = __uint_as_float(sw[0]);
+          v[k0 + 4] = __uint_as_float(sw[1]);
+        }
+      }
+    float chk = 0.f;
+#pragma unroll
+    for (int k = 0; k < NP; k += 4) {
+      if (k % 8 == 0) asm volatile("" ::: "memory");
+      const f32x4_t sc = *reinterpret_cast<const f32x4_t*>(&sscale[k]);
+      const f32x4_t pd = *reinterpret_cast<const f32x4_t*>(&spad[k]);
+      const float scv[4] = {sc[0], sc[1], sc[2], sc[3]}, pdv[4] = {pd[0], pd[1], pd[2], pd[3]};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        chk = __builtin_fmaf(v[k + c], 0.f, chk);
+        v[k + c] = __builtin_fmaf(v[k + c], scv[c], pdv[c]);
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(chk != 0.f)) {
+      const int slot = sbadn[wave];
+      if (slot < kTailBadSlots) {
+        if (lane == 0) sbad[wave][slot] = gi;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) sbadn[wave] = slot + 1;
+      } else {
+        overflow = true;
+      }
+    }
+    out[x0 + lane] = window_mean<NP, false>(v, tt, bb, inv_beta, ks, lane);
+  }
+  // exact pass: listed groups (every group of this wave after a list overflow), then the job's
+  // partial groups: [a, 64 q0) and [64 q1, b), or [a, b) inside one group (block y 0, waves 0 / 1)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int nbad = overflow ? 0 : sbadn[wave];
+  int64_t ps = 0, pe = 0;   // this wave's partial range
+  if (blockIdx.y == 0) {
+    if (q0 > q1) {
+      if (wave == 0) { ps = a; pe = b; }
+    } else if (wave == 0 && a < q0 * 64) {
+      ps = a; pe = q0 * 64;
+    } else if (wave == 1 && q1 * 64 < b) {
+      ps = q1 * 64; pe = b;
+    }
+  }
+  bool partial_pending = pe > ps;
+  int64_t gi = overflow ? gfirst : 0;
+  for (int bi = 0;; ++bi) {
+    int64_t xs;
+    int width = 64;
+    if (overflow ? gi < q1 : bi < nbad) {
+      xs = (overflow ? gi : sbad[wave][bi]) * 64;
+      if (overflow) gi += gstep;
+    } else if (partial_pending) {
+      xs = ps;
+      width = static_cast<int>(pe - ps);
+      partial_pending = false;
+    } else {
+      break;
+    }
+    const int nn = opaque_uniform(n), tt = opaque_uniform(t), bb = opaque_uniform(beta);
+    if (width == 64 && (xs & 63) == 0) {
+      stage_tile<DT, KR>(tile, sptr, nn, xs, lane);
+    } else {   // per-column loads; columns >= width repeat the first
+      const int64_t xl = xs + (lane < width ? lane : 0);
+      for (int j = 0; j < KR; ++j)
+        reinterpret_cast<uint16_t*>(tile)[j * (kMfmaTailPitch / 2) + lane] =
+            j < nn ? static_cast<const uint16_t*>(sptr[j])[xl] : 0;
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    const uint16_t* col = reinterpret_cast<const uint16_t*>(tile) + lane;
+    float v[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      v[k] = kInf;
+      if (k < tt) {
+        uint64_t m = uniform64(lds_volatile(smask[k]));
+        float sm = 0.f;
+#pragma clang loop unroll(disable)
+        while (m) {
+          sm += cvt16<DT>(col[__builtin_ctzll(m) * (kMfmaTailPitch / 2)]);
+          m &= m - 1;
+        }
+        v[k] = sanitize_inf(sm * lds_volatile(sscale[k]));
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const float r = window_mean<NP, true>(v, tt, bb, inv_beta, ks, lane);
+    if (lane < width) out[xs + lane] = r;
+  }
+}
+
+// the MFMA tail's limits (coord::launch_bulyan_tail_mfma): bf16 / fp16, n <= 64, t - beta <= 16,
+// window_mean's register positions
+inline bool lw_tail_mfma_ok(int dt, int n, int t, int beta) {
+  if (dt == kF32 || n > 64 || t > 64 || t < 1 || beta < 1 || t - beta > coord::kTailMaxExcluded) return false;
+  const int np = coord::np_for(t);
+  return t / 2 >= coord::wm_p0(np) && beta >= coord::wm_p0(np);
+}
+
+constexpr int kLwTailMfmaSub = 16;   // workgroups per job (a 32768-coordinate job = 512 groups)
+
+template <int DT, int NP>
+void launch_lw_tail_mfma(int ks, const RowTable& rows, int n, const int64_t* jobs, int njobs, const float* W, int t,
+                         int beta, float* out, hipStream_t s) {
+  const dim3 grid(njobs, kLwTailMfmaSub);
+#define GARFIELD_LW_TAIL(KS) \
+  hipLaunchKernelGGL((k_lw_bulyan_tail_mfma<DT, NP, KS>), grid, dim3(256), 0, s, rows, n, jobs, W, t, beta, out)
+  switch (ks) {
+    case 1: GARFIELD_LW_TAIL(1); break;
+    case 2: GARFIELD_LW_TAIL(2); break;
+    case 3: GARFIELD_LW_TAIL(3); break;
+    default: GARFIELD_LW_TAIL(4); break;
+  }
+#undef GARFIELD_LW_TAIL
+}
+
 template <int DT> struct LwBulyan {
   static void run(const RowTable& rows, int n, const int64_t* jobs, int njobs, const float* W, int t, int beta,
                   float* out, hipStream_t s) {
+    if constexpr (DT != kF32) {
+      if (lw_tail_mfma_ok(DT, n, t, beta) && lw_tail_mfma_enabled()) {
+        const int ks = (n + 15) / 16;
+        switch (coord::np_for(t)) {
+          case 8: launch_lw_tail_mfma<DT, 8>(ks, rows, n, jobs, njobs, W, t, beta, out, s); break;
+          case 16: launch_lw_tail_mfma<DT, 16>(ks, rows, n, jobs, njobs, W, t, beta, out, s); break;
+          case 32: launch_lw_tail_mfma<DT, 32>(ks, rows, n, jobs, njobs, W, t, beta, out, s); break;
+          default: launch_lw_tail_mfma<DT, 64>(ks, rows, n, jobs, njobs, W, t, beta, out, s); break;
+        }
+        return;
+      }
+    }
     const dim3 grid(njobs, kLwTailSub);
     switch (coord::np_for(t)) {
       case 8: hipLaunchKernelGGL((k_lw_bulyan_tail<DT, 8>), grid, dim3(256), 0, s, rows, n, jobs, W, t, beta, out); break;

@@ -183,9 +183,17 @@ __device__ __forceinline__ int tr_g(int row) { return ((row >> 1) & 1) | (((row 
 // KH-1-ph): A[o][(i', j', c)] = Wf[c][KH-1-i'][KW-1-j'][o]. The W tile is staged as plain
 // [c][o] rows and its fragments are read transposed (ds_read_b64_tr_b16), so no flipped /
 // transposed weight copy is made.
-template <int PM, int NS, bool ADD, bool TW>
+// S2 (with TW): the data gradient of a STRIDE-2 convolution, without a dcol matrix or col2im. The
+// output pixels split by parity into four classes (blockIdx.z = 2p + q: dx rows 2u + p, columns
+// 2v + q); class (p, q) is a stride-1 correlation of dy with the sub-kernel of the forward taps
+// i = i0 + 2a (i0 = (p + ph) & 1), which read dy row u + (p + ph - i) / 2 (and likewise for the
+// columns): 1 / 2 / 2 / 4 taps for a 3x3 pad-1 kernel, 1 / 0 / 0 / 0 for a 1x1 pad-0 one (a class
+// with no tap writes zeros, or add). Here g is the forward geometry seen from dy: H, W = dy's
+// spatial size, C = dy's channels, Ho, Wo = dx's (even), sh = sw = 2.
+template <int PM, int NS, bool ADD, bool TW, bool S2>
 __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                    Im2col g, int Cout, uint16_t* y, const uint16_t* add) {
+  static_assert(!S2 || TW, "the stride-2 data gradient reads the forward weight transposed");
   constexpr int BM = 64 * PM;          // pixels per workgroup
   constexpr int XB = BM * 128;         // X tile bytes per stage
   constexpr int WB = 64 * 128;         // W tile bytes per stage
@@ -196,7 +204,14 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int M = g.N * g.Ho * g.Wo;
+  // S2: this class's output grid (HoC x WoC) and its taps along each axis (count, first forward
+  // tap, dy offset of the first tap; tap a: forward index i0 + 2a, dy offset d0 - a)
+  const int cp = S2 ? static_cast<int>(blockIdx.z >> 1) : 0, cq = S2 ? static_cast<int>(blockIdx.z & 1) : 0;
+  const int HoC = S2 ? g.Ho >> 1 : g.Ho, WoC = S2 ? g.Wo >> 1 : g.Wo;
+  const int i0h = (cp + g.ph) & 1, i0w = (cq + g.pw) & 1;
+  const int nth = S2 ? (g.KH - i0h + 1) >> 1 : g.KH, ntw = S2 ? (g.KW - i0w + 1) >> 1 : g.KW;
+  const int d0h = (cp + g.ph - i0h) >> 1, d0w = (cq + g.pw - i0w) >> 1;
+  const int M = g.N * HoC * WoC;
   const int K = g.KH * g.KW * g.C;
   const int m0 = blockIdx.x * BM;
   const int co0 = blockIdx.y * 64;
@@ -211,11 +226,16 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
     const int m = m0 + px;
     xv[u] = m < M;
     const int mm = xv[u] ? m : 0;
-    const int wo = mm % g.Wo;
-    const int t = mm / g.Wo;
-    xh[u] = (t % g.Ho) * g.sh - g.ph;
-    xw[u] = wo * g.sw - g.pw;
-    xn[u] = t / g.Ho;
+    const int wo = mm % WoC;
+    const int t = mm / WoC;
+    if constexpr (S2) {   // class pixel (u, v): dy rows u + offset
+      xh[u] = t % HoC;
+      xw[u] = wo;
+    } else {
+      xh[u] = (t % g.Ho) * g.sh - g.ph;
+      xw[u] = wo * g.sw - g.pw;
+    }
+    xn[u] = t / HoC;
     xq[u] = lchunk ^ (px & 7);
   }
   const uint16_t* wsrc[WI];
@@ -229,22 +249,31 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
   const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
 
   const int csteps = g.C / 64;
-  const int steps = g.KH * g.KW * csteps;
+  const int steps = nth * ntw * csteps;
 
   auto issue = [&](int s, int slot) {
     const int tap = s / csteps;
     const int c0 = (s - tap * csteps) * 64;
-    const int i = tap / g.KW, j = tap - (tap / g.KW) * g.KW;
+    const int a = tap / ntw, b = tap - (tap / ntw) * ntw;
     char* base = lds + slot * SB;
     int64_t woff;
-    if constexpr (TW) woff = static_cast<int64_t>(c0) * KF + ((g.KH - 1 - i) * g.KW + (g.KW - 1 - j)) * Cout;
-    else woff = tap * g.C + c0;
+    int oh, ow;   // dy offsets of this tap
+    if constexpr (S2) {
+      woff = static_cast<int64_t>(c0) * KF + ((i0h + 2 * a) * g.KW + (i0w + 2 * b)) * Cout;
+      oh = d0h - a;
+      ow = d0w - b;
+    } else {
+      if constexpr (TW) woff = static_cast<int64_t>(c0) * KF + ((g.KH - 1 - a) * g.KW + (g.KW - 1 - b)) * Cout;
+      else woff = tap * g.C + c0;
+      oh = a * g.dh;
+      ow = b * g.dw;
+    }
 #pragma unroll
     for (int u = 0; u < WI; ++u)
       __builtin_amdgcn_global_load_lds(wsrc[u] + woff, (lds_ptr)(base + XB + (wave * WI + u) * 1024), 16, 0, 0);
 #pragma unroll
     for (int u = 0; u < XI; ++u) {
-      const int hi = xh[u] + i * g.dh, wi = xw[u] + j * g.dw;
+      const int hi = xh[u] + oh, wi = xw[u] + ow;
       const bool ok = xv[u] && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
       // both addresses computed, then one select (a conditional address expression
       // becomes a branch around each load)
@@ -343,7 +372,12 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
   for (int r = 0; r < PM; ++r) {
     const int m = m0 + (wave * PM + r) * 16 + fr;
     if (m >= M) continue;
-    const int64_t rowoff = static_cast<int64_t>(m) * Cout;
+    int64_t orow = m;
+    if constexpr (S2) {   // class pixel -> dx pixel (n, 2u + p, 2v + q)
+      const int v = m % WoC, t = m / WoC;
+      orow = (static_cast<int64_t>(t / HoC) * g.Ho + 2 * (t % HoC) + cp) * g.Wo + 2 * v + cq;
+    }
+    const int64_t rowoff = orow * Cout;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int64_t off = rowoff + co0 + c * 16 + fq * 4;
@@ -369,12 +403,21 @@ void launch_lds(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   const int M = g.N * g.Ho * g.Wo;
   const dim3 grid((M + 64 * PM - 1) / (64 * PM), Cout / 64);
   if (tw) {
-    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, true>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
-    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, true>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, true, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, true, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
   } else {
-    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
-    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, false, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, false, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
   }
+}
+
+template <int PM, int NS>
+void launch_s2(const uint16_t* dy, const uint16_t* w, const Im2col& g, int Cout, uint16_t* dx, const uint16_t* add,
+               hipStream_t stream) {
+  const int M = g.N * (g.Ho >> 1) * (g.Wo >> 1);
+  const dim3 grid((M + 64 * PM - 1) / (64 * PM), Cout / 64, 4);
+  if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, true, true>), grid, dim3(256), 0, stream, dy, w, g, Cout, dx, add);
+  else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, true, true>), grid, dim3(256), 0, stream, dy, w, g, Cout, dx, add);
 }
 
 // ---------------------------------------------------------------------------
@@ -748,6 +791,25 @@ void iconv_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
   if (pm >= 4) launch<4>(x, w, g, Cout, y, add, stream);
   else if (pm == 2) launch<2>(x, w, g, Cout, y, add, stream);
   else launch<1>(x, w, g, Cout, y, add, stream);
+}
+
+bool dgrad_s2_ok(const Im2col& g, int Cout) {
+  return g.sh == 2 && g.sw == 2 && g.dh == 1 && g.dw == 1 && g.C % 64 == 0 && Cout % 64 == 0 && g.KH <= 3 &&
+         g.KW <= 3 && g.ph <= 1 && g.pw <= 1 && g.Ho % 2 == 0 && g.Wo % 2 == 0 &&
+         g.H == (g.Ho + 2 * g.ph - g.KH) / 2 + 1 && g.W == (g.Wo + 2 * g.pw - g.KW) / 2 + 1;
+}
+
+void dgrad_s2_nhwc(const uint16_t* dy, const uint16_t* w, const Im2col& g, int Cout, uint16_t* dx, const uint16_t* add,
+                   int pm, hipStream_t stream) {
+  const int64_t M = static_cast<int64_t>(g.N) * (g.Ho >> 1) * (g.Wo >> 1);
+  if (M <= 0) return;
+  if (pm <= 0) {   // the iconv rule over all four classes: the largest pixel tile keeping ~500 workgroups
+    pm = 4;
+    while (pm > 1 && ((M + 64 * pm - 1) / (64 * pm)) * (Cout / 64) * 4 < 500) pm /= 2;
+  }
+  if (pm >= 4) launch_s2<4, 2>(dy, w, g, Cout, dx, add, stream);
+  else if (pm == 2) launch_s2<2, 3>(dy, w, g, Cout, dx, add, stream);
+  else launch_s2<1, 4>(dy, w, g, Cout, dx, add, stream);
 }
 
 // Weight gradient of a 1x1 convolution with NT 64-channel input blocks per workgroup: the

@@ -76,6 +76,17 @@ CONV3X3 = True
 # A bottleneck's bn2 + ReLU applied inside its 1x1 conv3 (GEMM prologue, weight-gradient prologue, ReLU test
 # recomputed in the BatchNorm backward): the normalised activation is never written (_GroupedBNConv).
 BN_PROLOGUE = os.environ.get("GARFIELD_BN_PROLOGUE", "0") == "1"
+# Data gradients of the stride-2 convolutions (3x3 downsampling, 1x1 projection shortcut) on the parity-class
+# MFMA kernel (iconv_nhwc.hip S2) instead of a dcol GEMM + col2im, per layer where the first (eager) step
+# measured it faster (ResNet-18 CIFAR: 15.20 -> 14.93 ms/step; ResNet-50 CIFAR / ImageNet layers keep the
+# GEMM: profiles/r5/s2_dgrad/).
+S2_DGRAD = os.environ.get("GARFIELD_S2_DGRAD", "1") == "1"
+_S2_CHOICE: dict = {}   # (dy shape, w shape, dx shape, kernel, padding) -> use the parity-class kernel
+S2_FORCE = False        # tests: take the parity-class kernel wherever it fits, unmeasured
+# 3x3 / stride-1 / pad-1 convolutions on images of at most 2x2 pixels (ResNet-50 CIFAR layer3 / layer4) as
+# dense GEMMs over [N, P * C] rows with the per-step expanded weight (sconv_nhwc.hip): no out-of-image
+# taps computed (2.25x / 9x of the useful MFMA work on the implicit-GEMM / im2col paths).
+SMALL_CONV = os.environ.get("GARFIELD_SMALL_CONV", "1") == "1"
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -439,6 +450,10 @@ class ConvSpec:
         # fp32 step: the weight split into three bf16 pieces [3, Cout, K] and the channel-transposed
         # pieces [3, Cin, KH, KW, Cout] of the data gradient (refresh_f32_weights, once per step)
         self.w3 = self.wt3 = None
+        # small-image dense form (SMALL_CONV): (H, W) of its input once chosen, and the per-step expanded
+        # weight Wbig [P*Cout, P*Cin] and its transpose (refresh_sc_weights)
+        self.sc = None
+        self.wbig = self.wbigT = None
 
 
 def _gemm_nt_ok(a2: torch.Tensor, b2: torch.Tensor) -> bool:
@@ -625,6 +640,126 @@ def _gemm_nt_dgrad(dy2: torch.Tensor, w2: torch.Tensor, add: torch.Tensor | None
     out = add if add is not None else torch.empty((dy2.shape[0], wt.shape[0]), dtype=dy2.dtype, device=dy2.device)
     C_.gpu_gemm_nt(dy2, wt, out, add, None, 0, cfg)
     return out
+
+
+def _dcol_dx(dy2: torch.Tensor, w: torch.Tensor, kp: int, spec: "ConvSpec", xshape, add: torch.Tensor | None):
+    """dx (+ add, in place of add) = col2im(dy2 · Wmat): the k x k data gradient of any stride."""
+    dcol = _dcol(dy2, w, kp, spec)
+    if add is not None:
+        _native.native().gpu_col2im(dcol, *_geom(spec), add, True)
+        return add
+    dx = torch.empty(xshape, dtype=dy2.dtype, device=dy2.device, memory_format=torch.channels_last)
+    _native.native().gpu_col2im(dcol, *_geom(spec), dx)
+    return dx
+
+
+def _timed(fn, reps: int = 3) -> float:
+    fn()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(reps):
+        fn()
+    t1.record()
+    t1.synchronize()
+    return t0.elapsed_time(t1)
+
+
+def _s2_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", xshape, add: torch.Tensor | None, kp: int):
+    """dx (+ add, in place of add) of a stride-2 convolution on ``gpu_dgrad_s2``: dx's four parity
+    classes, each a stride-1 correlation of dy with its taps of the forward weight. None when the
+    kernel does not take the geometry, or when the first (eager) call of this shape measured the
+    dcol GEMM + col2im faster (then that path runs)."""
+    if not (S2_DGRAD and dy.is_cuda and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and spec.stride == (2, 2) and spec.dilation == (1, 1) and _channels_last_weight(w)
+            and xshape[2] % 2 == 0 and xshape[3] % 2 == 0 and dy.shape[1] % 64 == 0 and xshape[1] % 64 == 0):
+        return None
+    C_ = _native.native()
+    key = (tuple(dy.shape), tuple(w.shape), tuple(xshape), spec.kernel, spec.padding)
+    use = _S2_CHOICE.get(key)
+    if use is None:
+        probe = torch.empty(xshape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        use = bool(C_.dgrad_s2_ok(dy, probe, *spec.kernel, *spec.padding))
+        if use and not S2_FORCE and not torch.cuda.is_current_stream_capturing():
+            dflag = spec.dcol
+            t_s2 = _timed(lambda: C_.gpu_dgrad_s2(dy, w, *spec.kernel, *spec.padding, probe))
+            t_col = _timed(lambda: _dcol_dx(rows2d(dy), w, kp, spec, xshape, None))
+            use = t_s2 < t_col
+            spec.dcol = dflag or not use
+        _S2_CHOICE[key] = use
+    if not use:
+        return None
+    dx = add if add is not None else torch.empty(xshape, dtype=dy.dtype, device=dy.device,
+                                                 memory_format=torch.channels_last)
+    C_.gpu_dgrad_s2(dy, w, *spec.kernel, *spec.padding, dx, add)
+    return dx
+
+
+def _sc_ok(x: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> bool:
+    return (SMALL_CONV and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and spec.kernel == (3, 3) and spec.stride == (1, 1) and spec.padding == (1, 1) and spec.dilation == (1, 1)
+            and x.shape[2] <= 2 and x.shape[3] <= 2 and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
+            and _channels_last_weight(w) and GEMM_NT)
+
+
+def _sc_buffers(spec: "ConvSpec", h: int, wd: int) -> None:
+    w = spec.conv.weight
+    P = h * wd
+    shape = (P * w.shape[0], P * w.shape[1])
+    if spec.wbig is None or tuple(spec.wbig.shape) != shape or spec.wbig.device != w.device:
+        spec.wbig = torch.empty(shape, dtype=w.dtype, device=w.device)
+        spec.wbigT = torch.empty((shape[1], shape[0]), dtype=w.dtype, device=w.device)
+    spec.sc = (h, wd)
+
+
+def refresh_sc_weights(specs) -> None:
+    """Wbig and Wbigᵀ of every small-image layer (``spec.sc``) from this step's weights: ONE launch."""
+    ws, hs, wds, bigs, bigTs = [], [], [], [], []
+    for spec in specs:
+        if spec.sc is None:
+            continue
+        ws.append(spec.conv.weight.detach())
+        hs.append(spec.sc[0])
+        wds.append(spec.sc[1])
+        bigs.append(spec.wbig)
+        bigTs.append(spec.wbigT)
+    if ws:
+        _native.native().gpu_sc_expand(ws, hs, wds, bigs, bigTs)
+
+
+def _sc_rows(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels_last -> its [N, H*W*C] row matrix (a view)."""
+    return t.permute(0, 2, 3, 1).reshape(t.shape[0], -1)
+
+
+def _sc_gemm(a2: torch.Tensor, b2: torch.Tensor, add: torch.Tensor | None) -> torch.Tensor:
+    C_ = _native.native()
+    cfg = _gemm_cfg(a2, b2, 0, add)
+    if cfg < 0:
+        raise RuntimeError(f"gemm_nt has no configuration for the small-image GEMM {tuple(a2.shape)} x {tuple(b2.shape)}")
+    out = add if add is not None else torch.empty((a2.shape[0], b2.shape[0]), dtype=a2.dtype, device=a2.device)
+    C_.gpu_gemm_nt(a2, b2, out, add, None, 0, cfg)
+    return out
+
+
+def _sc_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> None:
+    """Per-worker dWbig on the 1x1 implicit weight-gradient kernel (rows = images), folded onto the nine taps
+    straight into the exchange rows."""
+    n, cin, h, wd = x.shape
+    cout = dy.shape[1]
+    P = h * wd
+    xv = _sc_rows(x).view(n, 1, 1, P * cin).permute(0, 3, 1, 2)
+    dv = _sc_rows(dy).view(n, 1, 1, P * cout).permute(0, 3, 1, 2)
+    C_ = _native.native()
+    S = _iwgrad_splits(n // G, (P * cin // 64) * (P * cout // 64) * G // C_.iwgrad_taps_per_block(1, 1, P * cin, P * cout))
+    slab = torch.empty((S, G, P * cout, P * cin), dtype=torch.float32, device=dy.device)
+    C_.gpu_iwgrad(xv, dv, 1, 1, 1, 1, 0, 0, 1, 1, G, slab, S)
+    out = spec.sink.rows_view(spec.conv.weight, (cout, 9 * cin), spec.sink.flat.dtype)
+    if out is not None and spec.sink.flat.dtype in (torch.bfloat16, torch.float32):
+        C_.gpu_sc_fold(slab, h, wd, out)
+        return
+    tmp = torch.empty((G, cout, 9 * cin), dtype=torch.float32, device=dy.device)
+    C_.gpu_sc_fold(slab, h, wd, tmp)
+    spec.sink.put_groups(spec.conv.weight, tmp)
 
 
 def _conv_bwd(dy, x, w, spec: ConvSpec, mask):
@@ -998,6 +1133,14 @@ class _GroupedConv(torch.autograd.Function):
             if y2 is None:
                 y2 = torch.mm(rows2d(x), w.reshape(w.shape[0], -1).t())
             return from_rows(y2, n, h, wd)
+        if _sc_ok(x, w, spec):
+            ctx.mode = "sc"
+            ctx.save_for_backward(x, w)
+            if spec.sc != (h, wd) or spec.wbig is None:   # first use (eager): expand now; later steps refresh
+                _sc_buffers(spec, h, wd)
+                refresh_sc_weights([spec])
+            y2 = _sc_gemm(_sc_rows(x), spec.wbig, None)
+            return y2.view(n, h, wd, -1).permute(0, 3, 1, 2)
         if _stem_ok(x, w, spec):
             ctx.mode = "stem"
             ctx.save_for_backward(x, w)
@@ -1076,15 +1219,11 @@ class _GroupedConv(torch.autograd.Function):
                         and _iconv_ok(dy, _dgrad_weight_shape(w), dy2.shape[0])):
                     dx = _iconv(dy, w, (kh, kw, 1, 1, kh - 1 - ph, kw - 1 - pw, 1, 1), (h, wd),
                                 _cl(prev) if prev is not None else None, transpose_w=True)
+                elif (d_s2 := _s2_dgrad(dy, w, spec, ctx.xshape, _cl(prev) if prev is not None else None,
+                                        kp)) is not None:
+                    dx = d_s2
                 else:
-                    dcol = _dcol(dy2, w, kp, spec)
-                    if prev is not None:
-                        dx = _cl(prev)
-                        _native.native().gpu_col2im(dcol, *_geom(spec), dx, True)
-                    else:
-                        dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device,
-                                         memory_format=torch.channels_last)
-                        _native.native().gpu_col2im(dcol, *_geom(spec), dx)
+                    dx = _dcol_dx(dy2, w, kp, spec, ctx.xshape, _cl(prev) if prev is not None else None)
                 prev = None
             if use_iw:
                 _iwgrad(a, dy, spec, G, K)
@@ -1096,6 +1235,13 @@ class _GroupedConv(torch.autograd.Function):
                     if kp != K:
                         dW = dW[:, :, :K].contiguous()
                     spec.sink.put_groups(spec.conv.weight, dW)
+        elif mode == "sc":                       # a = x, H, W <= 2: dense GEMMs on the expanded weight
+            if need_dx:
+                add = _sc_rows(_cl(prev)) if prev is not None else None
+                dx = _sc_gemm(_sc_rows(dy), spec.wbigT, add).view(n, h, wd, cin).permute(0, 3, 1, 2)
+                prev = None
+            if spec.sink is not None:
+                _sc_wgrad(a, dy, spec, G)
         elif mode == "stem":                     # a = x (the network input: dx is rarely wanted)
             if need_dx:
                 dx = _cl(_conv_bwd(dy, a, w, spec, [True, False, False])[0])
@@ -1104,14 +1250,11 @@ class _GroupedConv(torch.autograd.Function):
         elif mode == "col":                      # a = col [N*Ho*Wo, Kp]
             kp = a.shape[1]
             if need_dx:
-                dcol = _dcol(dy2, w, kp, spec)
-                if prev is not None:
-                    dx = _cl(prev)
-                    _native.native().gpu_col2im(dcol, *_geom(spec), dx, True)
-                    prev = None
-                else:
-                    dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
-                    _native.native().gpu_col2im(dcol, *_geom(spec), dx)
+                add = _cl(prev) if prev is not None else None
+                dx = _s2_dgrad(dy, w, spec, ctx.xshape, add, kp)
+                if dx is None:
+                    dx = _dcol_dx(dy2, w, kp, spec, ctx.xshape, add)
+                prev = None
             if spec.sink is not None and getattr(ctx, "x", None) is not None:
                 _iwgrad(ctx.x, dy, spec, G, w.numel() // cout)    # no patch matrix, no batched GEMM
                 ctx.x = None

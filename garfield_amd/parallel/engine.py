@@ -54,7 +54,19 @@ LAYERWISE_RULES = {"krum", "bulyan", "brute", "aksel"}   # per-layer != flat onl
 # Layer-wise Krum as device operations (gar_layerwise.hip: one segmented Gram launch, a batched
 # selection, one segmented combine + SGD); "0" runs the per-segment loop (the reference form).
 LW_DEVICE = os.environ.get("GARFIELD_LW_DEVICE", "1") != "0"
-LW_JOB = 32768   # coordinates per job of the segmented kernels (a multiple of 8)
+LW_JOB = 32768   # coordinates per job of the segmented kernels (a multiple of 64)
+
+
+def lw_job_ranges(x0: int, x1: int, origin: int = 0) -> list:
+    """[x0, x1) cut at the multiples of LW_JOB of the global coordinate (``origin``: the global
+    coordinate of local 0): every job boundary inside a segment is then a multiple of 64 whatever the
+    sharding, so the layer-wise tail's MFMA / exact split of the coordinates is sharding-invariant."""
+    out, a = [], x0
+    while a < x1:
+        e = min(((a + origin) // LW_JOB + 1) * LW_JOB - origin, x1)
+        out.append((a, e))
+        a = e
+    return out
 # fp32 (no autocast) worker batching on the GPU (the reference's precision): "1" (default) the grouped
 # NHWC executor on the fp32 kernels (conv_f32.hip, split-bf16 MFMA; bn_nhwc.hip in fp32), "0" the
 # per-worker path.
@@ -545,8 +557,7 @@ class RobustDataParallel:
             segs = self._segments()
             jobs, seg_lo = [], [0]
             for s, (off, numel) in enumerate(segs):
-                for a in range(off, off + numel, LW_JOB):
-                    jobs.append((a, min(a + LW_JOB, off + numel), s))
+                jobs.extend((a, e, s) for a, e in lw_job_ranges(off, off + numel))
                 seg_lo.append(len(jobs))
             offs = [o for o, _ in segs] + [segs[-1][0] + segs[-1][1]]
             L, n = len(segs), self.n

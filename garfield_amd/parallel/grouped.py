@@ -24,7 +24,7 @@ from garfield_amd.parallel.signals import DeviceSignal
 from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, bn_conv_ok,
                                       global_avgpool, grouped_bn, grouped_bn_conv, grouped_conv,
                                       grouped_cross_entropy, grouped_linear, grouped_maxpool, refresh_dgrad_weights,
-                                      refresh_f32_weights)
+                                      refresh_f32_weights, refresh_sc_weights)
 
 
 def supports(model: nn.Module) -> bool:
@@ -184,6 +184,10 @@ class GroupedResNet:
                 x = _BucketMark.apply(x, self._events[name], self.sink)
             if name in self.marks:
                 yield name
+            if x.is_cuda and x.dtype != torch.float32:
+                # this layer's small-image convolutions (2x2 / 1x1 inputs): expanded weights, one launch, after
+                # the stage boundary (the staged step updates this bucket's weights up to its event)
+                refresh_sc_weights([self.conv[c] for c in getattr(m, name).modules() if isinstance(c, nn.Conv2d)])
             for blk in getattr(m, name):
                 x = self._block(blk, x)
         self.ws.flush_running()

@@ -684,7 +684,7 @@ class ShardedAggregator:
         if plan is not None:
             return plan
         e = self.e
-        from garfield_amd.parallel.engine import LW_JOB
+        from garfield_amd.parallel.engine import lw_job_ranges
 
         segs = sorted(zip(e.flat.offsets, e.flat.numels))
         offs = [o for o, _ in segs] + [segs[-1][0] + segs[-1][1]]
@@ -698,8 +698,7 @@ class ShardedAggregator:
                 x0, x1 = max(offs[si], o0), min(offs[si + 1], o1)
                 if x1 > x0:
                     sid[x0 - o0:x1 - o0] = si
-                for a in range(x0, x1, LW_JOB):
-                    jobs.append((a - o0, min(a + LW_JOB, x1) - o0, si))
+                jobs.extend((a - o0, e - o0, si) for a, e in lw_job_ranges(x0, x1))
                 seg_lo.append(len(jobs))
             plan["buckets"][b.lo] = (jobs, seg_lo)
             plan["seg_id"][b.lo] = sid.to(e.device)

@@ -451,7 +451,9 @@ def test_fused_collude_kernel_matches_attack_functions(cuda, native, P, T, d, dt
 
     g = torch.Generator(device="cpu").manual_seed(P * 31 + T)
     for empire in (False, True):
-        X = (torch.randn(P + T, d, generator=g) * 0.01 + 0.003).to(dtype).to(cuda)
+        ld = (d + 7) // 8 * 8   # rows 16-byte aligned, as the exchange buffer's padded rows are
+        X = torch.zeros(P + T, ld, dtype=dtype, device=cuda)[:, :d]
+        X.copy_((torch.randn(P + T, d, generator=g) * 0.01 + 0.003).to(dtype))
         ests = [X[i].float() for i in range(P)]
         want = []
         for t in range(T):

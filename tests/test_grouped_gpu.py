@@ -334,6 +334,38 @@ def test_iconv_dgrad_matches_autograd(cuda, native):
         assert rel(add.float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,Cin,Co,H,k,p", [(4, 64, 128, 16, 3, 1), (3, 128, 256, 8, 3, 1), (2, 256, 512, 14, 1, 0),
+                                           (5, 64, 64, 4, 3, 1), (2, 512, 1024, 28, 1, 0), (2, 128, 128, 56, 3, 1)])
+@pytest.mark.parametrize("pm", [0, 1, 2, 4])
+def test_dgrad_stride2_matches_autograd(cuda, native, N, Cin, Co, H, k, p, pm):
+    """The stride-2 data gradient on the parity-class kernel (gpu_dgrad_s2) against fp32 autograd of
+    the same bf16-rounded operands; with add folded in place (the residual branch's gradient)."""
+    x = torch.randn(N, Cin, H, H, device=cuda, requires_grad=True)
+    w = (torch.randn(Co, Cin, k, k, device=cuda) / (Cin * k * k) ** 0.5).to(torch.bfloat16).float()
+    y = F.conv2d(x, w, None, 2, p)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    dyb = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wb = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dx = torch.full((N, Cin, H, H), float("nan"), dtype=torch.bfloat16, device=cuda).contiguous(
+        memory_format=torch.channels_last)
+    assert native.dgrad_s2_ok(dyb, dx, k, k, p, p)
+    native.gpu_dgrad_s2(dyb, wb, k, k, p, p, dx, None, pm)
+    assert rel(dx.float(), x.grad) < 1e-2
+    if k == 1:   # odd rows / columns have no tap: exact zeros
+        assert dx[:, :, 1::2].float().abs().max().item() == 0 and dx[:, :, :, 1::2].float().abs().max().item() == 0
+    add = torch.randn_like(dx)
+    ref = add.float() + x.grad
+    native.gpu_dgrad_s2(dyb, wb, k, k, p, p, add, add, pm)
+    assert rel(add.float(), ref) < 1e-2
+
+
+def test_dgrad_stride2_refuses_odd_sizes(cuda, native):
+    dy = torch.zeros(2, 64, 4, 4, dtype=torch.bfloat16, device=cuda).contiguous(memory_format=torch.channels_last)
+    dx = torch.zeros(2, 64, 7, 7, dtype=torch.bfloat16, device=cuda).contiguous(memory_format=torch.channels_last)
+    assert not native.dgrad_s2_ok(dy, dx, 3, 3, 1, 1)
+
+
 @pytest.mark.parametrize("N,C,H,k,s,p", [(4, 64, 16, 3, 2, 1), (3, 8, 7, 2, 2, 0), (2, 16, 9, 3, 1, 1), (2, 64, 112, 3, 2, 1),
                                           (2, 8, 15, 3, 2, 1)])
 def test_maxpool_matches_aten(cuda, N, C, H, k, s, p):
@@ -427,6 +459,64 @@ def test_implicit_1x1_weight_gradients_match_gemm_path(cuda, monkeypatch):
     b = _grouped_rows(cuda, "resnet50", 4, 16)
     for j in range(4):
         assert rel(b[j], a[j]) < 1e-2, (j, rel(b[j], a[j]))
+
+
+@pytest.mark.parametrize("flag", ["SMALL_CONV", "S2_DGRAD"])
+def test_dense_small_image_and_stride2_paths_match_implicit_path(cuda, monkeypatch, flag):
+    """SMALL_CONV (2x2 / 1x1-image 3x3 layers as dense GEMMs + folded weight gradients) and S2_DGRAD
+    (stride-2 data gradients on the parity-class kernel): a ResNet-50 step's exchange rows are as close
+    to fp32 autograd as the implicit-GEMM / im2col path's (the two bf16 paths round differently, and a
+    random-init BatchNorm net amplifies any rounding difference to ~1 % of a row), and within bf16
+    noise of them."""
+    import garfield_amd.ops.grouped as grouped
+
+    monkeypatch.setattr(grouped, "S2_FORCE", True)
+    monkeypatch.setattr(grouped, "_S2_CHOICE", {})
+    monkeypatch.setattr(grouped, flag, False)
+    a = _grouped_rows(cuda, "resnet50", 4, 16)
+    err_off = _rows_vs_fp32(cuda, "resnet50", 4, 16, True)
+    monkeypatch.setattr(grouped, flag, True)
+    b = _grouped_rows(cuda, "resnet50", 4, 16)
+    err_on = _rows_vs_fp32(cuda, "resnet50", 4, 16, True)
+    for j in range(4):
+        assert err_on[j] < 1.1 * err_off[j] + 0.01, (j, err_on, err_off)
+        assert rel(b[j], a[j]) < 5e-2, (j, rel(b[j], a[j]))
+
+
+@pytest.mark.parametrize("H", [1, 2])
+@pytest.mark.parametrize("Cin,Co", [(256, 256), (512, 512), (64, 128)])
+def test_small_image_conv_expand_and_fold(cuda, native, H, Cin, Co):
+    """sconv_nhwc.hip: x · Wbigᵀ / dy · Wbig are the convolution and its data gradient (fp32 matmuls of the
+    expanded bf16 weight against F.conv2d autograd), and the fold of the dense per-worker weight gradient
+    equals conv2d_weight per worker."""
+    G, B = 4, 8
+    N, P = G * B, H * H
+    cl = torch.channels_last
+    x = torch.randn(N, Cin, H, H, device=cuda).to(torch.bfloat16).float()
+    w = (torch.randn(Co, Cin, 3, 3, device=cuda) / (9 * Cin) ** 0.5).to(torch.bfloat16).float()
+    xr = x.clone().requires_grad_()
+    y = F.conv2d(xr, w, None, 1, 1)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    wb = w.to(torch.bfloat16).contiguous(memory_format=cl)
+    big = torch.full((P * Co, P * Cin), float("nan"), dtype=torch.bfloat16, device=cuda)
+    bigT = torch.full((P * Cin, P * Co), float("nan"), dtype=torch.bfloat16, device=cuda)
+    native.gpu_sc_expand([wb], [H], [H], [big], [bigT])
+    assert torch.equal(bigT, big.t())
+    x2 = x.permute(0, 2, 3, 1).reshape(N, -1)
+    d2 = dy.permute(0, 2, 3, 1).reshape(N, -1)
+    y2 = x2 @ big.float().t()
+    assert rel(y2.view(N, H, H, Co).permute(0, 3, 1, 2), y) < 1e-4
+    dx2 = d2 @ bigT.float().t()
+    assert rel(dx2.view(N, H, H, Cin).permute(0, 3, 1, 2), xr.grad) < 1e-4
+    slab = torch.einsum("gbo,gbk->gok", d2.view(G, B, -1), x2.view(G, B, -1))
+    slab = torch.stack([slab * 0.25, slab * 0.75]).contiguous()   # two pixel splits summed by the fold
+    ref = torch.stack([torch.nn.grad.conv2d_weight(x[g * B:(g + 1) * B], w.shape, dy[g * B:(g + 1) * B], 1, 1)
+                       for g in range(G)]).permute(0, 1, 3, 4, 2).reshape(G, Co, 9 * Cin)
+    for dt in (torch.float32, torch.bfloat16):
+        out = torch.full((G, Co + 1, 9 * Cin), float("nan"), dtype=dt, device=cuda)[:, :Co]   # a strided rows view
+        native.gpu_sc_fold(slab, H, H, out)
+        assert rel(out.float(), ref) < (1e-4 if dt == torch.float32 else 1e-2)
 
 
 def test_grouped_engine_graph_matches_eager_and_excludes_attacker(cuda):
