@@ -2202,55 +2202,71 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       garfield::gpu::avgpool_f32_fwd(x.data_ptr<float>(), static_cast<int>(N), static_cast<int>(HW),
                                      static_cast<int>(C), y.data_ptr<float>(), stream_of(dev));
   }, py::arg("x"), py::arg("y"), py::arg("backward"), "fp32 / bf16 NHWC global average pool (forward / backward)");
-  m.def("stem_supported", &garfield::gpu::stem_supported, py::arg("h"), py::arg("w"),
-        "True when the implicit stem kernels (7x7/2, 3 -> 64 channels) handle H x W images");
-  m.def("gpu_stem_fwd", [](const at::Tensor& x, const at::Tensor& w160, const at::Tensor& y) {
+  m.def("stem_supported", [](int64_t h, int64_t w, int64_t kind) {
+          return garfield::gpu::stem_supported(static_cast<int>(h), static_cast<int>(w), static_cast<int>(kind));
+        }, py::arg("h"), py::arg("w"), py::arg("kind") = 0,
+        "True when the implicit stem kernels (3 -> 64 channels; kind 0: 7x7/2 pad 3, 1: 3x3/1 pad 1) handle H x W images");
+  m.def("stem_k", &garfield::gpu::stem_k, py::arg("kind") = 0, "taps x channels of the stem kind (147 / 27)");
+  m.def("stem_kp", &garfield::gpu::stem_kp, py::arg("kind") = 0, "K padded to whole 32-wide k-steps (160 / 32)");
+  m.def("gpu_stem_fwd", [](const at::Tensor& x, const at::Tensor& wm, const at::Tensor& y, int64_t kind) {
     const bool split = x.scalar_type() == at::kFloat;
+    const int kd = static_cast<int>(kind);
+    const int K = garfield::gpu::stem_k(kd), KP = garfield::gpu::stem_kp(kd);
+    const int64_t kh = kd == garfield::gpu::kStem3x3 ? 3 : 7, st = kd == garfield::gpu::kStem3x3 ? 1 : 2,
+                  pd = kd == garfield::gpu::kStem3x3 ? 1 : 3;
     TORCH_CHECK(x.is_cuda() && (split || x.scalar_type() == at::kBFloat16) && x.dim() == 4 && x.size(1) == 3 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "gpu_stem_fwd: x must be a channels_last bf16 or fp32 [N, 3, H, W] tensor");
-    const bool raw = !split && w160.numel() == 64 * 147;   // the channels_last weight itself (padded in LDS)
-    TORCH_CHECK(w160.device() == x.device() && w160.scalar_type() == at::kBFloat16 &&
-                    (raw ? (w160.dim() == 4 && w160.is_contiguous(at::MemoryFormat::ChannelsLast)) : w160.is_contiguous()) &&
-                    (raw || w160.numel() == (split ? 3 : 1) * 64 * 160),
-                "gpu_stem_fwd: w must be the contiguous zero-padded [64, 160] bf16 matrix, the channels_last bf16 "
-                "[64, 3, 7, 7] weight (bf16 x), or (fp32 x) the pieces [3, 64, 160]");
+    const bool raw = !split && wm.numel() == 64 * K;   // the channels_last weight itself (padded in LDS)
+    TORCH_CHECK(wm.device() == x.device() && wm.scalar_type() == at::kBFloat16 &&
+                    (raw ? (wm.dim() == 4 && wm.size(2) == kh && wm.is_contiguous(at::MemoryFormat::ChannelsLast))
+                         : wm.is_contiguous()) &&
+                    (raw || wm.numel() == (split ? 3 : 1) * 64 * KP),
+                "gpu_stem_fwd: w must be the contiguous zero-padded [64, ", KP, "] bf16 matrix, the channels_last bf16 "
+                "[64, 3, ", kh, ", ", kh, "] weight (bf16 x), or (fp32 x) the pieces [3, 64, ", KP, "]");
     const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
-    TORCH_CHECK(garfield::gpu::stem_supported(static_cast<int>(H), static_cast<int>(W)), "gpu_stem_fwd: unsupported size");
-    const int64_t Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
+    TORCH_CHECK(garfield::gpu::stem_supported(static_cast<int>(H), static_cast<int>(W), kd), "gpu_stem_fwd: unsupported size");
+    const int64_t Ho = (H + 2 * pd - kh) / st + 1, Wo = (W + 2 * pd - kh) / st + 1;
     TORCH_CHECK(y.device() == x.device() && y.scalar_type() == x.scalar_type() && y.dim() == 4 && y.size(0) == N &&
                     y.size(1) == 64 && y.size(2) == Ho && y.size(3) == Wo &&
                     y.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "gpu_stem_fwd: y must be a channels_last [N, 64, Ho, Wo] tensor of x's dtype");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(wm.data_ptr()) % 16 == 0, "gpu_stem_fwd: w must be 16-byte aligned");
     c10::hip::HIPGuard guard(x.device().index());
-    garfield::gpu::stem_fwd(x.data_ptr(), reinterpret_cast<const uint16_t*>(w160.data_ptr()), split,
+    garfield::gpu::stem_fwd(x.data_ptr(), reinterpret_cast<const uint16_t*>(wm.data_ptr()), split,
                             static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), y.data_ptr(),
-                            stream_of(x.device()), raw ? 147 : 160);
-  }, py::arg("x"), py::arg("w"), py::arg("y"),
-     "Implicit-GEMM ResNet stem forward (7x7/2, pad 3, 3 -> 64); fp32 x: split-bf16 MFMA on the weight's pieces");
-  m.def("gpu_stem_wgrad", [](const at::Tensor& x, const at::Tensor& dy, int64_t groups, const at::Tensor& part) {
+                            stream_of(x.device()), raw ? K : KP, kd);
+  }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("kind") = 0,
+     "Implicit-GEMM ResNet stem forward (3 -> 64; kind 0: 7x7/2 pad 3, 1: 3x3/1 pad 1); fp32 x: split-bf16 MFMA on "
+     "the weight's pieces");
+  m.def("gpu_stem_wgrad", [](const at::Tensor& x, const at::Tensor& dy, int64_t groups, const at::Tensor& part,
+                             int64_t kind) {
     const bool split = x.scalar_type() == at::kFloat;
+    const int kd = static_cast<int>(kind);
+    const int K = garfield::gpu::stem_k(kd);
+    const int64_t kh = kd == garfield::gpu::kStem3x3 ? 3 : 7, st = kd == garfield::gpu::kStem3x3 ? 1 : 2,
+                  pd = kd == garfield::gpu::kStem3x3 ? 1 : 3;
     TORCH_CHECK(x.is_cuda() && (split || x.scalar_type() == at::kBFloat16) && x.dim() == 4 && x.size(1) == 3 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "gpu_stem_wgrad: x must be a channels_last bf16 or fp32 [N, 3, H, W] tensor");
     const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
-    const int64_t Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
+    const int64_t Ho = (H + 2 * pd - kh) / st + 1, Wo = (W + 2 * pd - kh) / st + 1;
     TORCH_CHECK(dy.device() == x.device() && dy.scalar_type() == x.scalar_type() && dy.dim() == 4 && dy.size(0) == N &&
                     dy.size(1) == 64 && dy.size(2) == Ho && dy.size(3) == Wo &&
                     dy.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "gpu_stem_wgrad: dy must be a channels_last [N, 64, Ho, Wo] tensor of x's dtype");
     TORCH_CHECK(groups >= 1 && N % groups == 0, "gpu_stem_wgrad: images not divisible into groups");
     TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 4 &&
-                    part.size(1) == groups && part.size(2) == 64 && part.size(3) == 147,
-                "gpu_stem_wgrad: part must be a contiguous fp32 [slices, groups, 64, 147] tensor");
-    TORCH_CHECK(garfield::gpu::stem_supported(static_cast<int>(H), static_cast<int>(W)), "gpu_stem_wgrad: unsupported size");
+                    part.size(1) == groups && part.size(2) == 64 && part.size(3) == K,
+                "gpu_stem_wgrad: part must be a contiguous fp32 [slices, groups, 64, ", K, "] tensor");
+    TORCH_CHECK(garfield::gpu::stem_supported(static_cast<int>(H), static_cast<int>(W), kd), "gpu_stem_wgrad: unsupported size");
     c10::hip::HIPGuard guard(x.device().index());
     garfield::gpu::stem_wgrad(x.data_ptr(), dy.data_ptr(), static_cast<int>(N), static_cast<int>(H),
                               static_cast<int>(W), static_cast<int>(groups), static_cast<int>(part.size(0)),
-                              part.data_ptr<float>(), split, stream_of(x.device()));
-  }, py::arg("x"), py::arg("dy"), py::arg("groups"), py::arg("part"),
-     "Implicit ResNet-stem weight gradient per worker: part[s, g] = slice s of worker g's dW [64, 147] (bf16 or "
-     "fp32 x / dy)");
+                              part.data_ptr<float>(), split, stream_of(x.device()), kd);
+  }, py::arg("x"), py::arg("dy"), py::arg("groups"), py::arg("part"), py::arg("kind") = 0,
+     "Implicit ResNet-stem weight gradient per worker: part[s, g] = slice s of worker g's dW [64, K] (bf16 or "
+     "fp32 x / dy; kind as gpu_stem_fwd)");
   m.def("gpu_maxpool_fwd", &g_maxpool_fwd, "NHWC bf16 max pooling (k x k, stride s, padding p) keeping the "
         "argmax tap per element; args (x, k, s, p, y, idx)");
   m.def("gpu_maxpool_bwd", &g_maxpool_bwd, "Max-pooling backward as a gather; args (dy, idx, k, s, p, dx)");

@@ -59,18 +59,22 @@ void augment_gather(const uint8_t* src, int64_t nsrc, const int64_t* idx, const 
                     int64_t R, int H, int W, int C, int pad, bool flip,
                     uint64_t seed, uint64_t step, const AugNorm& nrm, void* out, hipStream_t stream, int out_dt = 1);
 
-// ResNet stem (stem_nhwc.hip): 7x7 / stride 2 / padding 3 convolution of 3-channel NHWC
-// images into 64 channels on MFMA, without a patch matrix. w: zero-padded [64][160] bf16.
-// split: the fp32 form — x / y fp32, w = the weight's three bf16 pieces [3][64][160].
-bool stem_supported(int H, int W);
-// w: the zero-padded [64][160] matrix (split: its three pieces), or (wpitch = 147, bf16 only) the
-// channels_last [64][7][7][3] weight itself
+// ResNet stem (stem_nhwc.hip): the convolution of 3-channel NHWC images into 64 channels on MFMA,
+// without a patch matrix; kind kStem7x7: 7x7 / stride 2 / padding 3 (K = 147 taps x channels, padded
+// KP = 160), kStem3x3: the CIFAR ResNet-18 3x3 / stride 1 / padding 1 (K = 27, KP = 32).
+// split: the fp32 form — x / y fp32, w = the weight's three bf16 pieces [3][64][KP].
+constexpr int kStem7x7 = 0, kStem3x3 = 1;
+int stem_k(int kind);
+int stem_kp(int kind);
+bool stem_supported(int H, int W, int kind = kStem7x7);
+// w: the zero-padded [64][KP] matrix (split: its three pieces), or (wpitch = K, bf16 only) the
+// channels_last [64][KH][KW][3] weight itself
 void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream,
-              int wpitch = 160);
-// per-worker weight gradients: part fp32 [slices][groups][64][147] (sum over slices = dW of the worker);
+              int wpitch = 160, int kind = kStem7x7);
+// per-worker weight gradients: part fp32 [slices][groups][64][K] (sum over slices = dW of the worker);
 // split: x / dy fp32
 void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,
-                hipStream_t stream);
+                hipStream_t stream, int kind = kStem7x7);
 
 // Row-major NT GEMM on MFMA (gemm_nt.hip): C[M, N] = A[M, K] · B[N, K]ᵀ (+ add), bf16; K % 64 == 0,
 // N a multiple of the configuration's tile width. stats (nullable): per-stats-tile, per-worker (rg rows)

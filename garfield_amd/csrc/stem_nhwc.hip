@@ -34,9 +34,18 @@ namespace gpu {
 using namespace dev;
 namespace {
 
-constexpr int kC = 3, kKH = 7, kKW = 7, kS = 2, kP = 3, kCout = 64;
-constexpr int kK = kKH * kKW * kC;        // 147
-constexpr int kKP = 160;                   // padded to 5 k-steps of 32
+constexpr int kC = 3, kCout = 64;
+// Geometry of the stem: the ResNet-50 / ImageNet 7x7 / stride 2 / pad 3, or the CIFAR ResNet-18
+// 3x3 / stride 1 / pad 1 (its 27-deep reduction is one 32-wide k-step). K: taps x channels, KP: K
+// padded to whole 32-wide k-steps.
+template <int KH_, int S_, int P_>
+struct StemShape {
+  static constexpr int KH = KH_, KW = KH_, S = S_, P = P_;
+  static constexpr int K = KH * KW * kC;
+  static constexpr int KP = (K + 31) / 32 * 32;
+};
+using Stem7 = StemShape<7, 2, 3>;   // K 147, KP 160
+using Stem3 = StemShape<3, 1, 1>;   // K 27, KP 32
 // output pixels per forward workgroup: 64 * F (F 16-pixel fragments per wave); bf16 takes F = 4
 // (a 256-pixel tile stages its input rows and the weights once per ~2.3 ImageNet output rows:
 // 3.38 -> 2.52 ms per ImageNet step), the split form F = 2 (three pieces of every operand in registers)
@@ -54,9 +63,10 @@ struct StemGeo {
 
 // patch offset (elements) of reduction index k = (ky * 7 + kx) * 3 + ci inside the
 // staged rows (row width pw pixels); k >= 147 maps to `zero` (a 0 element)
+template <class SH>
 __device__ __forceinline__ int tap_offset(int k, int pw, int zero) {
-  if (k >= kK) return zero;
-  const int ky = k / (kKW * kC), r = k - ky * (kKW * kC);
+  if (k >= SH::K) return zero;
+  const int ky = k / (SH::KW * kC), r = k - ky * (SH::KW * kC);
   const int kx = r / kC, ci = r - kx * kC;
   return (ky * pw + kx) * kC + ci;
 }
@@ -67,12 +77,12 @@ __device__ __forceinline__ int tap_offset(int k, int pw, int zero) {
 // independent loads before its LDS stores (one memory latency per batch, not per element).
 // SPLIT: x is fp32 and each value lands as three pieces in patch, patch + pstride, patch + 2 pstride.
 constexpr int kStageBatch = 8;
-template <bool SPLIT>
+template <class SH, bool SPLIT>
 __device__ __forceinline__ void stage_rows(const void* __restrict__ xv, const StemGeo& g, int n, int iy0, int rows,
                                            uint16_t* patch, int pstride) {
   const int per_row = g.pw * kC, row_len = g.W * kC;
   const int total = rows * per_row;
-  const int64_t img = static_cast<int64_t>(n) * g.H * row_len - kP * kC;   // (iy, c) at img + iy*row_len + c
+  const int64_t img = static_cast<int64_t>(n) * g.H * row_len - SH::P * kC;   // (iy, c) at img + iy*row_len + c
   const int dr = kThreads / per_row, dc = kThreads - dr * per_row;
   int e = threadIdx.x, r = e / per_row, c = e - r * per_row;
   while (e < total) {
@@ -82,7 +92,7 @@ __device__ __forceinline__ void stage_rows(const void* __restrict__ xv, const St
     for (int b = 0; b < kStageBatch; ++b) {
       const int iy = iy0 + r;
       v[b] = 0.f;
-      if (e < total && iy >= 0 && iy < g.H && c >= kP * kC && c < kP * kC + row_len) {
+      if (e < total && iy >= 0 && iy < g.H && c >= SH::P * kC && c < SH::P * kC + row_len) {
         const int64_t o = img + static_cast<int64_t>(iy) * row_len + c;
         if constexpr (SPLIT) v[b] = static_cast<const float*>(xv)[o];
         else v[b] = bf16_to_f(static_cast<const uint16_t*>(xv)[o]);
@@ -131,7 +141,7 @@ __device__ __forceinline__ f32x4 mma6(const bf16x8 (&a)[kNP], const bf16x8 (&b)[
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
 }
 
-template <bool SPLIT, int F>
+template <class SH, bool SPLIT, int F>
 __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ x, const uint16_t* __restrict__ w,
                                                        StemGeo g, void* __restrict__ y, int wpitch) {
   // LDS (dynamic, sized by the host for this geometry): weights [64][160] (x3 split) | staged
@@ -145,34 +155,34 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
   const int p0 = (blockIdx.x - n * tiles) * kTile;
   const int npix = g.Ho * g.Wo - p0 < kTile ? g.Ho * g.Wo - p0 : kTile;
   const int oy0 = p0 / g.Wo, oy1 = (p0 + npix - 1) / g.Wo;
-  const int iy0 = oy0 * kS - kP;
-  const int rows = (oy1 - oy0) * kS + kKH;
+  const int iy0 = oy0 * SH::S - SH::P;
+  const int rows = (oy1 - oy0) * SH::S + SH::KH;
   const int zero = rows * g.pw * kC;
-  uint16_t* patch = lds + NP * kCout * kKP;
+  uint16_t* patch = lds + NP * kCout * SH::KP;
   const int pstride = zero + 8;   // elements between the piece arrays of the staged rows
   // weights: the zero-padded [64][160] bf16 matrix (columns in the channels_last weight's
   // (ky, kx, ci) order; split: its three pieces one after the other), 16-byte loads; or
   // (wpitch = 147) the channels_last bf16 weight itself, padded while it is staged (no per-step
   // padding copy)
-  if (wpitch == kKP) {
-    for (int e = threadIdx.x; e < NP * kCout * kKP / 8; e += kThreads)
+  if (wpitch == SH::KP) {
+    for (int e = threadIdx.x; e < NP * kCout * SH::KP / 8; e += kThreads)
       reinterpret_cast<uint4*>(wl)[e] = reinterpret_cast<const uint4*>(w)[e];
   } else {   // 64 x 147 contiguous bf16 (18816 bytes, 16-byte aligned): 16-byte loads, scattered into rows
-    for (int e = threadIdx.x; e < kCout * kK / 8; e += kThreads) {
+    for (int e = threadIdx.x; e < kCout * SH::K / 8; e += kThreads) {
       const uint4 v = reinterpret_cast<const uint4*>(w)[e];
       const uint32_t h[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int q = e * 8 + i, r = q / kK, c = q - (q / kK) * kK;
-        wl[r * kKP + c] = static_cast<uint16_t>((i & 1) ? (h[i >> 1] >> 16) : (h[i >> 1] & 0xffffu));
+        const int q = e * 8 + i, r = q / SH::K, c = q - (q / SH::K) * SH::K;
+        wl[r * SH::KP + c] = static_cast<uint16_t>((i & 1) ? (h[i >> 1] >> 16) : (h[i >> 1] & 0xffffu));
       }
     }
-    for (int e = threadIdx.x; e < kCout * (kKP - kK); e += kThreads) {
-      const int r = e / (kKP - kK);
-      wl[r * kKP + kK + (e - r * (kKP - kK))] = 0;
+    for (int e = threadIdx.x; e < kCout * (SH::KP - SH::K); e += kThreads) {
+      const int r = e / (SH::KP - SH::K);
+      wl[r * SH::KP + SH::K + (e - r * (SH::KP - SH::K))] = 0;
     }
   }
-  stage_rows<SPLIT>(x, g, n, iy0, rows, patch, pstride);
+  stage_rows<SH, SPLIT>(x, g, n, iy0, rows, patch, pstride);
   if (threadIdx.x < NP) patch[threadIdx.x * pstride + zero] = 0;
   __syncthreads();
 
@@ -185,7 +195,7 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
     int p = p0 + wave * 16 * F + f * 16 + fr;
     if (p > p0 + npix - 1) p = p0 + npix - 1;   // clamp: computed, never stored
     const int oy = p / g.Wo, ox = p - oy * g.Wo;
-    pbase[f] = ((oy * kS - kP - iy0) * g.pw + ox * kS) * kC;
+    pbase[f] = ((oy * SH::S - SH::P - iy0) * g.pw + ox * SH::S) * kC;
   }
   f32x4 acc[F][4];
 #pragma unroll
@@ -193,11 +203,11 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[f][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int s = 0; s < kKP / 32; ++s) {
+  for (int s = 0; s < SH::KP / 32; ++s) {
     const int kb = s * 32 + fq * 8;
     int off[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) off[j] = tap_offset(kb + j, g.pw, zero);
+    for (int j = 0; j < 8; ++j) off[j] = tap_offset<SH>(kb + j, g.pw, zero);
     bf16x8 bx[F][NP];
 #pragma unroll
     for (int f = 0; f < F; ++f) {
@@ -213,7 +223,8 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
     for (int c = 0; c < 4; ++c) {
       bf16x8 aw[NP];
 #pragma unroll
-      for (int i = 0; i < NP; ++i) aw[i] = *reinterpret_cast<const bf16x8*>(wl + i * kCout * kKP + (c * 16 + fr) * kKP + kb);
+      for (int i = 0; i < NP; ++i)
+        aw[i] = *reinterpret_cast<const bf16x8*>(wl + i * kCout * SH::KP + (c * 16 + fr) * SH::KP + kb);
 #pragma unroll
       for (int f = 0; f < F; ++f) {
         if constexpr (SPLIT) acc[f][c] = mma6(aw, bx[f], acc[f][c]);
@@ -263,14 +274,14 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
 // output channels and all 10 k-blocks of 16 (160 padded taps): acc[10] f32x4.
 constexpr int kDyPitch = 40;   // bf16 per transposed dy row (32 + 8: 16-byte aligned, conflict-spread)
 
-template <bool SPLIT>
+template <class SH, bool SPLIT>
 __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict__ x, const void* __restrict__ dy,
                                                          StemGeo g, int imgs_per_worker, int slices,
                                                          float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];   // dynamic: sized by the host
   constexpr int NP = SPLIT ? kNP : 1;
   uint16_t* dyt = lds;                            // [64][kDyPitch] (x3 split: the pieces one after the other)
-  const int brows = (g.band - 1) * kS + kKH;      // input rows a band's outputs read
+  const int brows = (g.band - 1) * SH::S + SH::KH;   // input rows a band's outputs read
   const int zero = brows * g.pw * kC;
   uint16_t* patch = lds + NP * kCout * kDyPitch;  // one band's input rows (x3 split)
   const int pstride = zero + 8;
@@ -282,12 +293,12 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   // this lane's 10 taps (k = 16 kb + fr), as staged-row offsets
-  int toff[kKP / 16];
+  int toff[SH::KP / 16];
 #pragma unroll
-  for (int kb = 0; kb < kKP / 16; ++kb) toff[kb] = tap_offset(kb * 16 + fr, g.pw, zero);
-  f32x4 acc[kKP / 16];
+  for (int kb = 0; kb < SH::KP / 16; ++kb) toff[kb] = tap_offset<SH>(kb * 16 + fr, g.pw, zero);
+  f32x4 acc[SH::KP / 16];
 #pragma unroll
-  for (int kb = 0; kb < kKP / 16; ++kb) acc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kb = 0; kb < SH::KP / 16; ++kb) acc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int npix = g.Ho * g.Wo;
   const int pq = threadIdx.x >> 3, cv = threadIdx.x & 7;   // this thread's 8 channels of one dy pixel
   for (int n = i0; n < i1; ++n) {
@@ -295,7 +306,7 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
       const int ob1 = ob0 + g.band < g.Ho ? ob0 + g.band : g.Ho;
       const int q_lo = ob0 * g.Wo, q_hi = ob1 * g.Wo;      // the band's pixels [q_lo, q_hi)
       __syncthreads();   // the previous band's patch reads are done
-      stage_rows<SPLIT>(x, g, n, ob0 * kS - kP, (ob1 - ob0 - 1) * kS + kKH, patch, pstride);
+      stage_rows<SH, SPLIT>(x, g, n, ob0 * SH::S - SH::P, (ob1 - ob0 - 1) * SH::S + SH::KH, patch, pstride);
       if (threadIdx.x < NP) patch[threadIdx.x * pstride + zero] = 0;
       const int64_t dyi = static_cast<int64_t>(n) * npix * kCout;
       // the next tile's load is issued before the current tile's MFMAs (one latency per band, not per tile)
@@ -336,7 +347,7 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
           int oy = p / g.Wo, ox = p - oy * g.Wo;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            pb[j] = p + j < q_hi ? ((oy - ob0) * kS * g.pw + ox * kS) * kC : -1;   // band staged from row ob0*S - P
+            pb[j] = p + j < q_hi ? ((oy - ob0) * SH::S * g.pw + ox * SH::S) * kC : -1;   // band staged from row ob0*S - P
             if (++ox == g.Wo) {
               ox = 0;
               ++oy;
@@ -344,7 +355,7 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
           }
         }
 #pragma unroll
-        for (int kb = 0; kb < kKP / 16; ++kb) {
+        for (int kb = 0; kb < SH::KP / 16; ++kb) {
           bf16x8 b[NP];
 #pragma unroll
           for (int pc = 0; pc < NP; ++pc) {
@@ -360,33 +371,35 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
       }
     }
   }
-  // D[co][k]: col = k = 16 kb + fr, rows co = 16 wave + 4 fq + r; slab [slices][G][64][147]
-  float* o = part + (static_cast<int64_t>(s) * gridDim.y + grp) * kCout * kK;
+  // D[co][k]: col = k = 16 kb + fr, rows co = 16 wave + 4 fq + r; slab [slices][G][64][K]
+  float* o = part + (static_cast<int64_t>(s) * gridDim.y + grp) * kCout * SH::K;
 #pragma unroll
-  for (int kb = 0; kb < kKP / 16; ++kb) {
+  for (int kb = 0; kb < SH::KP / 16; ++kb) {
     const int k = kb * 16 + fr;
-    if (k >= kK) continue;
+    if (k >= SH::K) continue;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) o[(wave * 16 + fq * 4 + r) * kK + k] = acc[kb][r];
+    for (int r = 0; r < 4; ++r) o[(wave * 16 + fq * 4 + r) * SH::K + k] = acc[kb][r];
   }
 }
 
+template <class SH>
 StemGeo geo(int N, int H, int W, bool split = false) {
   StemGeo g{};
   g.N = N;
   g.H = H;
   g.W = W;
-  g.Ho = (H + 2 * kP - kKH) / kS + 1;
-  g.Wo = (W + 2 * kP - kKW) / kS + 1;
-  g.pw = W + 2 * kP;
+  g.Ho = (H + 2 * SH::P - SH::KH) / SH::S + 1;
+  g.Wo = (W + 2 * SH::P - SH::KW) / SH::S + 1;
+  g.pw = W + 2 * SH::P;
   // weight-gradient bands: as many output rows as the staged input rows allow
   const int max_rows = (split ? kMaxPatchSplit : kMaxPatch) / (g.pw * kC) - 1;
-  int band = max_rows >= kKH ? (max_rows - kKH) / kS + 1 : 0;
+  int band = max_rows >= SH::KH ? (max_rows - SH::KH) / SH::S + 1 : 0;
   g.band = band > g.Ho ? g.Ho : band;
   return g;
 }
 
-int fwd_rows(const StemGeo& g, int tile) { return ((tile + g.Wo - 1) / g.Wo) * kS + kKH; }   // max staged rows per tile
+template <class SH>
+int fwd_rows(const StemGeo& g, int tile) { return ((tile + g.Wo - 1) / g.Wo) * SH::S + SH::KH; }   // max staged rows per tile
 
 template <class K>
 void allow_lds(K kernel, size_t bytes) {
@@ -395,50 +408,72 @@ void allow_lds(K kernel, size_t bytes) {
                               static_cast<int>(bytes));
 }
 
-}  // namespace
-
-bool stem_supported(int H, int W) {
+template <class SH>
+bool supported_t(int H, int W) {
   if (H <= 0 || W <= 0) return false;
-  const StemGeo g = geo(1, H, W), gs = geo(1, H, W, true);
-  return fwd_rows(g, 64 * kFwdFragBf16) * g.pw * kC < kMaxPatch && fwd_rows(g, 64 * kFwdFragSplit) * g.pw * kC < kMaxPatchSplit &&
-         g.band >= 1 && gs.band >= 1;
+  const StemGeo g = geo<SH>(1, H, W), gs = geo<SH>(1, H, W, true);
+  return fwd_rows<SH>(g, 64 * kFwdFragBf16) * g.pw * kC < kMaxPatch &&
+         fwd_rows<SH>(g, 64 * kFwdFragSplit) * g.pw * kC < kMaxPatchSplit && g.band >= 1 && gs.band >= 1;
 }
 
-void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream,
-              int wpitch) {
-  const StemGeo g = geo(N, H, W, split);
+template <class SH>
+void fwd_t(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream, int wpitch) {
+  const StemGeo g = geo<SH>(N, H, W, split);
   const int T = 64 * (split ? kFwdFragSplit : kFwdFragBf16);
   const int tiles = (g.Ho * g.Wo + T - 1) / T;
   const int np = split ? kNP : 1;
-  size_t lds = (static_cast<size_t>(np) * kCout * kKP + np * (static_cast<size_t>(fwd_rows(g, T)) * g.pw * kC + 8)) * 2;
+  size_t lds = (static_cast<size_t>(np) * kCout * SH::KP +
+                np * (static_cast<size_t>(fwd_rows<SH>(g, T)) * g.pw * kC + 8)) * 2;
   const size_t tile = static_cast<size_t>(T) * kCout * (split ? 4 : 2);
   if (lds < tile) lds = tile;
   if (split) {
-    allow_lds(k_stem_fwd<true, kFwdFragSplit>, lds);
-    hipLaunchKernelGGL((k_stem_fwd<true, kFwdFragSplit>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y,
-                       kKP);
+    allow_lds(k_stem_fwd<SH, true, kFwdFragSplit>, lds);
+    hipLaunchKernelGGL((k_stem_fwd<SH, true, kFwdFragSplit>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y,
+                       SH::KP);
   } else {
-    allow_lds(k_stem_fwd<false, kFwdFragBf16>, lds);
-    hipLaunchKernelGGL((k_stem_fwd<false, kFwdFragBf16>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y,
-                       wpitch == kK ? kK : kKP);
+    allow_lds(k_stem_fwd<SH, false, kFwdFragBf16>, lds);
+    hipLaunchKernelGGL((k_stem_fwd<SH, false, kFwdFragBf16>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y,
+                       wpitch == SH::K ? SH::K : SH::KP);
   }
 }
 
-void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,
-                hipStream_t stream) {
-  const StemGeo g = geo(N, H, W, split);
+template <class SH>
+void wgrad_t(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,
+             hipStream_t stream) {
+  const StemGeo g = geo<SH>(N, H, W, split);
   const int np = split ? kNP : 1;
-  const size_t brows = static_cast<size_t>((g.band - 1) * kS + kKH);
+  const size_t brows = static_cast<size_t>((g.band - 1) * SH::S + SH::KH);
   const size_t lds = (static_cast<size_t>(np) * kCout * kDyPitch + np * (brows * g.pw * kC + 8)) * 2;
   if (split) {
-    allow_lds(k_stem_wgrad<true>, lds);
-    hipLaunchKernelGGL(k_stem_wgrad<true>, dim3(slices, groups), dim3(kThreads), lds, stream, x, dy, g, N / groups,
-                       slices, part);
+    allow_lds(k_stem_wgrad<SH, true>, lds);
+    hipLaunchKernelGGL((k_stem_wgrad<SH, true>), dim3(slices, groups), dim3(kThreads), lds, stream, x, dy, g,
+                       N / groups, slices, part);
   } else {
-    allow_lds(k_stem_wgrad<false>, lds);
-    hipLaunchKernelGGL(k_stem_wgrad<false>, dim3(slices, groups), dim3(kThreads), lds, stream, x, dy, g, N / groups,
-                       slices, part);
+    allow_lds(k_stem_wgrad<SH, false>, lds);
+    hipLaunchKernelGGL((k_stem_wgrad<SH, false>), dim3(slices, groups), dim3(kThreads), lds, stream, x, dy, g,
+                       N / groups, slices, part);
   }
+}
+
+}  // namespace
+
+int stem_k(int kind) { return kind == kStem3x3 ? Stem3::K : Stem7::K; }
+int stem_kp(int kind) { return kind == kStem3x3 ? Stem3::KP : Stem7::KP; }
+
+bool stem_supported(int H, int W, int kind) {
+  return kind == kStem3x3 ? supported_t<Stem3>(H, W) : supported_t<Stem7>(H, W);
+}
+
+void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream,
+              int wpitch, int kind) {
+  if (kind == kStem3x3) fwd_t<Stem3>(x, w, split, N, H, W, y, stream, wpitch);
+  else fwd_t<Stem7>(x, w, split, N, H, W, y, stream, wpitch);
+}
+
+void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,
+                hipStream_t stream, int kind) {
+  if (kind == kStem3x3) wgrad_t<Stem3>(x, dy, N, H, W, groups, slices, part, split, stream);
+  else wgrad_t<Stem7>(x, dy, N, H, W, groups, slices, part, split, stream);
 }
 
 }  // namespace gpu

@@ -898,14 +898,25 @@ def _iwgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, K: int,
         spec.sink.put_groups(spec.conv.weight, part.sum(0) if S > 1 else part[0])
 
 
+def _stem_kind(w: torch.Tensor, spec: "ConvSpec") -> int | None:
+    """stem_nhwc.hip's geometry of a 3 -> 64-channel first layer: 0 the 7x7/2/pad-3 ResNet stem, 1 the
+    CIFAR ResNet-18 3x3/1/pad-1 one; None for anything else."""
+    if spec.dilation != (1, 1):
+        return None
+    if tuple(w.shape) == (64, 3, 7, 7) and spec.stride == (2, 2) and spec.padding == (3, 3):
+        return 0
+    if tuple(w.shape) == (64, 3, 3, 3) and spec.stride == (1, 1) and spec.padding == (1, 1):
+        return 1
+    return None
+
+
 def _stem_ok(x: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> bool:
-    """The 3-channel 7x7/2/pad-3 stem into 64 channels, bf16 channels_last, on sizes whose
-    staged input rows fit the kernels' LDS (every CIFAR/ImageNet-crop size up to 64 px)."""
-    return (STEM and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and tuple(w.shape) == (64, 3, 7, 7) and _channels_last_weight(w)
-            and x.is_contiguous(memory_format=torch.channels_last)
-            and spec.stride == (2, 2) and spec.padding == (3, 3) and spec.dilation == (1, 1)
-            and _native.native().stem_supported(x.shape[2], x.shape[3]))
+    """A 3-channel stem into 64 channels (``_stem_kind``), bf16 channels_last, on sizes whose staged
+    input rows fit the kernels' LDS (every CIFAR/ImageNet-crop size)."""
+    kind = _stem_kind(w, spec)
+    return (STEM and kind is not None and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and _channels_last_weight(w) and x.is_contiguous(memory_format=torch.channels_last)
+            and _native.native().stem_supported(x.shape[2], x.shape[3], kind))
 
 
 def _stem_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> None:
@@ -917,9 +928,12 @@ def _stem_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> 
     # while CIFAR-size images keep ~2 images per slice (splits/stc_*: 2048 costs 0.03 ms there)
     wg = _STEM_WG * (2 if dy.shape[2] * dy.shape[3] > 4096 else 1)
     S = max(1, min(per, -(-wg // G)))
-    part = torch.empty((S, G, 64, 147), dtype=torch.float32, device=dy.device)
-    _native.native().gpu_stem_wgrad(x, dy, G, part)
-    rows = spec.sink.rows_view(spec.conv.weight, (64, 147), spec.sink.flat.dtype)
+    C_ = _native.native()
+    kind = _stem_kind(spec.conv.weight, spec) or 0
+    K = C_.stem_k(kind)
+    part = torch.empty((S, G, 64, K), dtype=torch.float32, device=dy.device)
+    C_.gpu_stem_wgrad(x, dy, G, part, kind)
+    rows = spec.sink.rows_view(spec.conv.weight, (64, K), spec.sink.flat.dtype)
     if rows is not None:
         spec.sink.queue_split(part, rows)
     else:
@@ -1146,7 +1160,7 @@ class _GroupedConv(torch.autograd.Function):
             ctx.save_for_backward(x, w)
             ho, wo = _out_hw(spec, h, wd)
             y = torch.empty((n, 64, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-            _native.native().gpu_stem_fwd(x, w, y)   # the weight is padded while the kernel stages it
+            _native.native().gpu_stem_fwd(x, w, y, _stem_kind(w, spec))   # the weight is padded while staged
             return y
         if _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
             ctx.mode = "iconv"

@@ -208,6 +208,29 @@ def test_stem_kernels_match_fp32_conv(cuda, native, G, B, H, W, splits):
         assert rel(part[:, gi].sum(0), dw.permute(0, 2, 3, 1).reshape(64, 147)) < 1e-2
 
 
+@pytest.mark.parametrize("G,B,H,W,splits,raw", [(2, 3, 32, 32, 1, True), (3, 2, 32, 32, 4, False),
+                                                (2, 2, 33, 20, 2, True), (4, 1, 17, 9, 1, False)])
+def test_stem3x3_kernels_match_fp32_conv(cuda, native, G, B, H, W, splits, raw):
+    """stem_nhwc.hip kind 1 (the CIFAR ResNet-18 3x3/1/pad 1 stem, 3 -> 64, K = 27 in one k-step): forward
+    from the padded [64, 32] matrix or the raw channels_last weight vs fp32 conv2d, per-worker weight
+    gradient vs fp32 conv2d_weight."""
+    from garfield_amd.ops.grouped import _wmat
+    assert native.stem_supported(H, W, 1) and native.stem_k(1) == 27 and native.stem_kp(1) == 32
+    x = torch.randn(G * B, 3, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 3, 3, device=cuda) / 5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.float(), w.float(), None, 1, 1)
+    y = torch.full(ref.shape, float("nan"), dtype=torch.bfloat16, device=cuda).contiguous(memory_format=torch.channels_last)
+    native.gpu_stem_fwd(x, w if raw else _wmat(w, 32).contiguous(), y, 1)
+    assert rel(y.float(), ref) < 1e-2
+    dy = torch.randn(ref.shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    part = torch.full((splits, G, 64, 27), float("nan"), device=cuda)
+    native.gpu_stem_wgrad(x, dy, G, part, 1)
+    for gi in range(G):
+        sl = slice(gi * B, (gi + 1) * B)
+        dw = torch.nn.grad.conv2d_weight(x[sl].float(), (64, 3, 3, 3), dy[sl].float(), 1, 1)
+        assert rel(part[:, gi].sum(0), dw.permute(0, 2, 3, 1).reshape(64, 27)) < 1e-2
+
+
 def test_stem_unsupported_sizes(native):
     assert native.stem_supported(224, 224)         # ImageNet crops: the weight gradient runs in row bands
     assert native.stem_supported(32, 32)
