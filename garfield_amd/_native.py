@@ -27,6 +27,7 @@ def _try_import():
         import torch  # noqa: F401  (libc10 / libtorch symbols must be loaded first)
         _C = importlib.import_module("garfield_amd._C")
         _ERR = None
+        _check_manifest()
     except Exception as e:  # pragma: no cover - depends on the build state
         _ERR = e
         if os.environ.get("GARFIELD_AUTOBUILD", "0") == "1":
@@ -36,6 +37,22 @@ def _try_import():
             _C = importlib.import_module("garfield_amd._C")
             _ERR = None
     return _C
+
+
+def _check_manifest() -> None:
+    """Warn when the loaded extension was built from other sources than the ones in the tree
+    (``_C.build.json``, written by every build)."""
+    try:
+        import json
+
+        from garfield_amd.csrc import build as _b
+
+        man = _b.manifest_path()
+        if man.exists() and json.loads(man.read_text()).get("sources_sha256") != _b.sources_digest():
+            warnings.warn("garfield_amd: the native extension was built from different sources than the tree's "
+                          "garfield_amd/csrc (rebuild: python -m garfield_amd.csrc.build)", RuntimeWarning, stacklevel=3)
+    except Exception:   # the check is advisory
+        pass
 
 
 def available() -> bool:

@@ -89,8 +89,25 @@ def _run(cmd, verbose):
     return r
 
 
+def sources_digest() -> str:
+    """sha256 over every native source and header (name + bytes), the identity of a build."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted([*CSRC.glob("*.hip"), *CSRC.glob("*.cpp"), *CSRC.glob("*.hpp")]):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def manifest_path() -> Path:
+    return PKG / "_C.build.json"
+
+
 def build(verbose: bool = False, force: bool = False) -> Path:
-    """Compile every source (parallel, incremental) and link ``_C``. Returns the .so path."""
+    """Compile every source (parallel, incremental) and link ``_C``. Returns the .so path.
+    Writes ``_C.build.json`` next to it: the sources' digest, how many translation units this
+    call compiled, the target and the compiler, so a shipped .so can be matched to its sources."""
     incs, defs, libdir = _torch_flags()
     BUILD.mkdir(parents=True, exist_ok=True)
     opt = _opt_flags()
@@ -126,6 +143,15 @@ def build(verbose: bool = False, force: bool = False) -> Path:
                 f"-L{ROCM / 'lib'}", "-lamdhip64", "-pthread", "-ldl",
                 f"-Wl,-rpath,{libdir}", f"-Wl,-rpath,{ROCM / 'lib'}"]
         _run(link, verbose)
+    import json
+    import time
+
+    ver = subprocess.run([HIPCC, "--version"], capture_output=True, text=True).stdout.splitlines()
+    manifest = {"sources_sha256": sources_digest(), "units": len(jobs), "compiled_this_call": len(todo),
+                "linked_this_call": bool(force or todo) or not out.exists(), "arch": ARCH, "opt": opt,
+                "compiler": next((v for v in ver if "version" in v.lower()), ""),
+                "so_bytes": out.stat().st_size, "time": time.strftime("%Y-%m-%dT%H:%M:%S")}
+    manifest_path().write_text(json.dumps(manifest, indent=1) + "\n")
     return out
 
 

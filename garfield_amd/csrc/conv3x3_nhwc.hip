@@ -49,6 +49,9 @@ struct Halo {
   int SEGP;  // staged pixels per segment: (TRI + 2) * SW
   int NPIX;  // staged pixels per tile: (TR / TRI) * SEGP
   int nu;    // halo glds instructions per wave: ceil(NPIX / 32) <= NU
+  // magic-number divisors of the per-tile index arithmetic (a runtime integer division is ~20 VALU
+  // instructions, a 64-bit one far more; the prologue of a 256-pixel tile did ~40 of them)
+  FastDiv fSEGP, fSW, fTRI, fWo, fHo, fW, fH;
 };
 
 constexpr int EPI_PLAIN = 0, EPI_ADD = 1, EPI_STATS = 2;
@@ -123,11 +126,11 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int p = (u * 4 + wave) * 8 + (lane >> 3);
-    const int seg = p / hp.SEGP;
+    const int seg = static_cast<int>(fdiv(static_cast<uint32_t>(p), hp.fSEGP));
     const int rem = p - seg * hp.SEGP;
-    const int r = rem / hp.SW, c = rem - (rem / hp.SW) * hp.SW;
+    const int r = static_cast<int>(fdiv(static_cast<uint32_t>(rem), hp.fSW)), c = rem - r * hp.SW;
     const int orow = R0 + seg * hp.TRI;                            // the segment's first output row
-    const int n = orow / g.Ho;
+    const int n = static_cast<int>(fdiv(static_cast<uint32_t>(orow), hp.fHo));
     const int hl = (orow - n * g.Ho) * st - 1 + r;                 // input row inside the image
     const bool ok = p < hp.NPIX && n < g.N && hl >= 0 && hl < g.H && c >= 1 && c <= g.W;
     soff[u] = ok ? ((n * g.H + hl) * g.W + c - 1) * g.C + (lc ^ (p & 7)) * 8 : -1;
@@ -168,8 +171,8 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
 #pragma unroll
   for (int r = 0; r < PMF; ++r) {
     const int ml = (wave * PMF + r) * 16 + fr;
-    const int t = ml / g.Wo, col = ml - (ml / g.Wo) * g.Wo;
-    const int seg = t / hp.TRI;
+    const int t = static_cast<int>(fdiv(static_cast<uint32_t>(ml), hp.fWo)), col = ml - t * g.Wo;
+    const int seg = static_cast<int>(fdiv(static_cast<uint32_t>(t), hp.fTRI));
     sp0[r] = ml < hp.TP ? seg * hp.SEGP + (t - seg * hp.TRI) * st * hp.SW + col * st : 0;
   }
 
@@ -273,9 +276,9 @@ __global__ __launch_bounds__(256) void k_conv3x3_res(const uint16_t* __restrict_
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int p = (u * 4 + wave) * 8 + (lane >> 3);
-    const int seg = p / hp.SEGP;
+    const int seg = static_cast<int>(fdiv(static_cast<uint32_t>(p), hp.fSEGP));
     const int rem = p - seg * hp.SEGP;
-    const int r = rem / hp.SW;
+    const int r = static_cast<int>(fdiv(static_cast<uint32_t>(rem), hp.fSW));
     const int c = rem - r * hp.SW;
     const bool ok = u < hp.nu && p < hp.NPIX && c >= 1 && c <= g.W;
     hrow[u] = ok ? (seg * hp.TRI + r - 1) : -(1 << 28);
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_res(const uint16_t* __restrict_
   }
   auto issue_halo = [&](int tile, int buf) {
     const int R0 = tile * hp.TR;
-    const int h0 = R0 % g.H;
+    const int h0 = R0 - static_cast<int>(fdiv(static_cast<uint32_t>(R0), hp.fH)) * g.H;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       if (u < hp.nu) {
@@ -303,8 +306,8 @@ __global__ __launch_bounds__(256) void k_conv3x3_res(const uint16_t* __restrict_
 #pragma unroll
   for (int r = 0; r < PMF; ++r) {
     const int ml = (wave * PMF + r) * 16 + fr;
-    const int t = ml / g.W, col = ml - t * g.W;
-    const int seg = t / hp.TRI;
+    const int t = static_cast<int>(fdiv(static_cast<uint32_t>(ml), hp.fW)), col = ml - t * g.W;
+    const int seg = static_cast<int>(fdiv(static_cast<uint32_t>(t), hp.fTRI));
     sp0[r] = ml < hp.TP ? seg * hp.SEGP + (t - seg * hp.TRI) * hp.SW + col : 0;
   }
 
@@ -388,7 +391,14 @@ bool plan(const Im2col& g, int pmf, int nu_max, Halo& hp) {
   hp.SEGP = ((hp.TRI - 1) * st + 3) * hp.SW;
   hp.NPIX = (hp.TR / hp.TRI) * hp.SEGP;
   hp.nu = (hp.NPIX + 31) / 32;
-  return hp.nu <= nu_max;
+  hp.fSEGP = make_fastdiv(static_cast<uint32_t>(hp.SEGP));
+  hp.fSW = make_fastdiv(static_cast<uint32_t>(hp.SW));
+  hp.fTRI = make_fastdiv(static_cast<uint32_t>(hp.TRI));
+  hp.fWo = make_fastdiv(static_cast<uint32_t>(g.Wo));
+  hp.fHo = make_fastdiv(static_cast<uint32_t>(g.Ho));
+  hp.fW = make_fastdiv(static_cast<uint32_t>(g.W));
+  hp.fH = make_fastdiv(static_cast<uint32_t>(g.H));
+  return hp.nu <= nu_max && static_cast<int64_t>(g.N) * g.H * g.W < (int64_t{1} << 31);
 }
 
 template <int PMF, int NU>
@@ -453,7 +463,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
   const int64_t pbeg = static_cast<int64_t>(gi) * rg;       // the worker's first pixel (an image start)
   const int64_t pend = pbeg + rg;
   const int ntiles = static_cast<int>((rg + hp.TP - 1) / hp.TP);
-  const FastDiv fW = make_fastdiv(g.W);
+  const FastDiv fW = hp.fW;
   const int t0 = sp * tiles_per_split;
   const int t1 = t0 + tiles_per_split < ntiles ? t0 + tiles_per_split : ntiles;
   const int lc = lane & 7;
@@ -464,9 +474,9 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int p = (u * 4 + wave) * 8 + (lane >> 3);
-    const int seg = p / hp.SEGP;
+    const int seg = static_cast<int>(fdiv(static_cast<uint32_t>(p), hp.fSEGP));
     const int rem = p - seg * hp.SEGP;
-    const int r = rem / hp.SW;
+    const int r = static_cast<int>(fdiv(static_cast<uint32_t>(rem), hp.fSW));
     const int c = rem - r * hp.SW;
     const bool ok = u < hp.nu && p < hp.NPIX && c >= 1 && c <= g.W;
     hrow[u] = ok ? (seg * hp.TRI + r - 1) : -(1 << 28);   // input row relative to the tile's first row
@@ -489,8 +499,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
   for (int tile = t0; tile < t1; ++tile) {
     const int64_t P0 = pbeg + static_cast<int64_t>(tile) * hp.TP;   // first pixel of the tile
     const int64_t Pend = P0 + hp.TP < pend ? P0 + hp.TP : pend;
-    const int R0 = static_cast<int>(P0 / g.W);
-    const int h0 = R0 % g.H;
+    const int R0 = static_cast<int>(fdiv(static_cast<uint32_t>(P0), hp.fW));   // P0 < 2^31 (host check)
+    const int h0 = R0 - static_cast<int>(fdiv(static_cast<uint32_t>(R0), hp.fH)) * g.H;
     // dy tile: 128 pixels x 8 chunks, 4 glds per lane (pixels past TP: zero rows)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -523,7 +533,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
         const int m = 32 * c + 8 * grp + 4 * h + q;
         uint32_t t, col;
         fdivmod(static_cast<uint32_t>(m), fW, t, col);
-        const int seg = static_cast<int>(t) / hp.TRI;
+        const int seg = static_cast<int>(fdiv(t, hp.fTRI));
         // a pixel past TP has a zero dy row; it reads halo pixel 0 (finite) so 0 x stale LDS cannot be NaN
         hp0[h] = m < hp.TP ? seg * hp.SEGP + (static_cast<int>(t) - seg * hp.TRI) * hp.SW + static_cast<int>(col) : 0;
       }

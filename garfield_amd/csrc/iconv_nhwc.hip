@@ -190,9 +190,14 @@ __device__ __forceinline__ int tr_g(int row) { return ((row >> 1) & 1) | (((row 
 // columns): 1 / 2 / 2 / 4 taps for a 3x3 pad-1 kernel, 1 / 0 / 0 / 0 for a 1x1 pad-0 one (a class
 // with no tap writes zeros, or add). Here g is the forward geometry seen from dy: H, W = dy's
 // spatial size, C = dy's channels, Ho, Wo = dx's (even), sh = sw = 2.
+// magic divisors of the output-pixel decomposition (the class grid's for S2): m -> (n, row, column)
+struct PixDiv {
+  FastDiv fw, fh;
+};
+
 template <int PM, int NS, bool ADD, bool TW, bool S2>
 __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
-                                                   Im2col g, int Cout, uint16_t* y, const uint16_t* add) {
+                                                   Im2col g, int Cout, uint16_t* y, const uint16_t* add, PixDiv pd) {
   static_assert(!S2 || TW, "the stride-2 data gradient reads the forward weight transposed");
   constexpr int BM = 64 * PM;          // pixels per workgroup
   constexpr int XB = BM * 128;         // X tile bytes per stage
@@ -226,16 +231,18 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
     const int m = m0 + px;
     xv[u] = m < M;
     const int mm = xv[u] ? m : 0;
-    const int wo = mm % WoC;
-    const int t = mm / WoC;
+    const int t = static_cast<int>(fdiv(static_cast<uint32_t>(mm), pd.fw));
+    const int wo = mm - t * WoC;
+    const int tn = static_cast<int>(fdiv(static_cast<uint32_t>(t), pd.fh));
+    const int ho = t - tn * HoC;
     if constexpr (S2) {   // class pixel (u, v): dy rows u + offset
-      xh[u] = t % HoC;
+      xh[u] = ho;
       xw[u] = wo;
     } else {
-      xh[u] = (t % g.Ho) * g.sh - g.ph;
+      xh[u] = ho * g.sh - g.ph;
       xw[u] = wo * g.sw - g.pw;
     }
-    xn[u] = t / HoC;
+    xn[u] = tn;
     xq[u] = lchunk ^ (px & 7);
   }
   const uint16_t* wsrc[WI];
@@ -374,8 +381,9 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
     if (m >= M) continue;
     int64_t orow = m;
     if constexpr (S2) {   // class pixel -> dx pixel (n, 2u + p, 2v + q)
-      const int v = m % WoC, t = m / WoC;
-      orow = (static_cast<int64_t>(t / HoC) * g.Ho + 2 * (t % HoC) + cp) * g.Wo + 2 * v + cq;
+      const int t = static_cast<int>(fdiv(static_cast<uint32_t>(m), pd.fw)), v = m - t * WoC;
+      const int tn = static_cast<int>(fdiv(static_cast<uint32_t>(t), pd.fh));
+      orow = (static_cast<int64_t>(tn) * g.Ho + 2 * (t - tn * HoC) + cp) * g.Wo + 2 * v + cq;
     }
     const int64_t rowoff = orow * Cout;
 #pragma unroll
@@ -402,12 +410,13 @@ void launch_lds(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout,
                 bool tw, hipStream_t stream) {
   const int M = g.N * g.Ho * g.Wo;
   const dim3 grid((M + 64 * PM - 1) / (64 * PM), Cout / 64);
+  const PixDiv pd{make_fastdiv(static_cast<uint32_t>(g.Wo)), make_fastdiv(static_cast<uint32_t>(g.Ho))};
   if (tw) {
-    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, true, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
-    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, true, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, true, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add, pd);
+    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, true, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add, pd);
   } else {
-    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, false, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
-    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, false, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add);
+    if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, false, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add, pd);
+    else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, false, false>), grid, dim3(256), 0, stream, x, w, g, Cout, y, add, pd);
   }
 }
 
@@ -416,8 +425,9 @@ void launch_s2(const uint16_t* dy, const uint16_t* w, const Im2col& g, int Cout,
                hipStream_t stream) {
   const int M = g.N * (g.Ho >> 1) * (g.Wo >> 1);
   const dim3 grid((M + 64 * PM - 1) / (64 * PM), Cout / 64, 4);
-  if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, true, true>), grid, dim3(256), 0, stream, dy, w, g, Cout, dx, add);
-  else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, true, true>), grid, dim3(256), 0, stream, dy, w, g, Cout, dx, add);
+  const PixDiv pd{make_fastdiv(static_cast<uint32_t>(g.Wo >> 1)), make_fastdiv(static_cast<uint32_t>(g.Ho >> 1))};
+  if (add) hipLaunchKernelGGL((k_iconv_lds<PM, NS, true, true, true>), grid, dim3(256), 0, stream, dy, w, g, Cout, dx, add, pd);
+  else hipLaunchKernelGGL((k_iconv_lds<PM, NS, false, true, true>), grid, dim3(256), 0, stream, dy, w, g, Cout, dx, add, pd);
 }
 
 // ---------------------------------------------------------------------------
@@ -462,6 +472,7 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
   const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
   const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
 
+  const FastDiv fWo = make_fastdiv(g.Wo), fHo = make_fastdiv(g.Ho);
   auto issue = [&](int s, int slot) {
     const int m = static_cast<int>(mbeg) + s * 32 + lrow;   // < 2^31: checked by the host wrapper
     const bool mv = m < static_cast<int>(mend);
@@ -470,10 +481,10 @@ __global__ __launch_bounds__(256) void k_iwgrad(const uint16_t* __restrict__ x, 
     const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lsw * 8);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? ady : az), (lds_ptr)(base + wave * 1024), 16,
                                      0, 0);
-    const int wo = mm % g.Wo;
-    const int t = mm / g.Wo;
-    const int ho = t % g.Ho;
-    const int n = t / g.Ho;
+    uint32_t t_, wo_, n_, ho_;
+    fdivmod(static_cast<uint32_t>(mm), fWo, t_, wo_);
+    fdivmod(t_, fHo, n_, ho_);
+    const int wo = static_cast<int>(wo_), ho = static_cast<int>(ho_), n = static_cast<int>(n_);
     const int hi = ho * g.sh - g.ph + ti * g.dh, wi = wo * g.sw - g.pw + tj * g.dw;
     const bool ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
     const uint64_t ax = reinterpret_cast<uint64_t>(
@@ -605,6 +616,7 @@ __global__ __launch_bounds__(256) void k_iwgrad_rows(const uint16_t* __restrict_
   const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
   const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
 
+  const FastDiv fWo = make_fastdiv(g.Wo), fHo = make_fastdiv(g.Ho);
   auto issue = [&](int s, int slot) {
     const int m = static_cast<int>(mbeg) + s * 32 + lrow;
     const bool mv = m < static_cast<int>(mend);
@@ -613,10 +625,10 @@ __global__ __launch_bounds__(256) void k_iwgrad_rows(const uint16_t* __restrict_
     const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lsw * 8);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? ady : az), (lds_ptr)(base + wave * 1024), 16,
                                      0, 0);
-    const int wo = mm % g.Wo;
-    const int t = mm / g.Wo;
-    const int ho = t % g.Ho;
-    const int n = t / g.Ho;
+    uint32_t t_, wo_, n_, ho_;
+    fdivmod(static_cast<uint32_t>(mm), fWo, t_, wo_);
+    fdivmod(t_, fHo, n_, ho_);
+    const int wo = static_cast<int>(wo_), ho = static_cast<int>(ho_), n = static_cast<int>(n_);
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       const int hi = ho * g.sh - g.ph + (ti0 + r) * g.dh;
@@ -840,6 +852,8 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
   const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
   const uint64_t az = reinterpret_cast<uint64_t>(zsrc);
 
+  const FastDiv fWo = make_fastdiv(g.Wo), fHo = make_fastdiv(g.Ho);
+  const bool ident = g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 && g.H == g.Ho && g.W == g.Wo;
   auto issue = [&](int s, int slot) {
     const int m = static_cast<int>(mbeg) + s * 32 + lrow;
     const bool mv = m < static_cast<int>(mend);
@@ -848,14 +862,17 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
     const uint64_t ady = reinterpret_cast<uint64_t>(dy + static_cast<int64_t>(mm) * Cout + co0 + lsw * 8);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? ady : az), (lds_ptr)(base + wave * 1024), 16,
                                      0, 0);
-    const int wo = mm % g.Wo;
-    const int t = mm / g.Wo;
-    const int ho = t % g.Ho;
-    const int n = t / g.Ho;
-    const int hi = ho * g.sh - g.ph, wi = wo * g.sw - g.pw;
-    const bool ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
-    const uint16_t* xr = x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 +
-                         lsw * 8;
+    bool ok = mv;
+    int64_t xo = mm;   // a stride-1 unpadded 1x1 convolution reads the output pixel's own input row
+    if (!ident) {
+      uint32_t t_, wo_, n_, ho_;
+      fdivmod(static_cast<uint32_t>(mm), fWo, t_, wo_);
+      fdivmod(t_, fHo, n_, ho_);
+      const int hi = static_cast<int>(ho_) * g.sh - g.ph, wi = static_cast<int>(wo_) * g.sw - g.pw;
+      ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+      xo = (static_cast<int64_t>(n_) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0);
+    }
+    const uint16_t* xr = x + xo * g.C + c0 + lsw * 8;
 #pragma unroll
     for (int j = 0; j < NT; ++j)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(ok ? reinterpret_cast<uint64_t>(xr + j * 64) : az),
@@ -1001,6 +1018,7 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1_wide(const uint16_t* __restr
   if (mend > static_cast<int64_t>(gi + 1) * rg) mend = static_cast<int64_t>(gi + 1) * rg;
   const int steps = mend > mbeg ? static_cast<int>((mend - mbeg + 63) / 64) : 0;
   const FastDiv fWo = make_fastdiv(g.Wo), fHo = make_fastdiv(g.Ho);
+  const bool ident = g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0 && g.H == g.Ho && g.W == g.Wo;
 
   // staging: instruction u (0..7) of this wave covers sub-tile u / 2, rows 8 ((u & 1) * 4 + wave) + lane / 8
   const int lchunk = lane & 7;
@@ -1015,14 +1033,18 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1_wide(const uint16_t* __restr
       const int m = static_cast<int>(mbeg) + s * 64 + row;   // < 2^31: checked by the host wrapper
       const bool mv = m < static_cast<int>(mend);
       const int mm = mv ? m : 0;
-      uint32_t t, wo, n, ho;
-      fdivmod(static_cast<uint32_t>(mm), fWo, t, wo);
-      fdivmod(t, fHo, n, ho);
-      const int hi = static_cast<int>(ho) * g.sh - g.ph, wi = static_cast<int>(wo) * g.sw - g.pw;
-      const bool ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+      bool ok = mv;
+      int64_t xo = mm;   // a stride-1 unpadded 1x1 convolution reads the output pixel's own input row
+      if (!ident) {
+        uint32_t t, wo, n, ho;
+        fdivmod(static_cast<uint32_t>(mm), fWo, t, wo);
+        fdivmod(t, fHo, n, ho);
+        const int hi = static_cast<int>(ho) * g.sh - g.ph, wi = static_cast<int>(wo) * g.sw - g.pw;
+        ok = mv && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+        xo = (static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0);
+      }
       const uint16_t* dr = dy + static_cast<int64_t>(mm) * Cout + co0 + lsw * 8;
-      const uint16_t* xr = x + ((static_cast<int64_t>(n) * g.H + (ok ? hi : 0)) * g.W + (ok ? wi : 0)) * g.C + c0 +
-                           lsw * 8;
+      const uint16_t* xr = x + xo * g.C + c0 + lsw * 8;
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(mv ? reinterpret_cast<uint64_t>(dr + 64 * b) : az),

@@ -741,9 +741,53 @@ def _sc_gemm(a2: torch.Tensor, b2: torch.Tensor, add: torch.Tensor | None) -> to
     return out
 
 
+_SC_WG_CHOICE: dict = {}   # (x shape, dy shape, G) -> the dense form (else the implicit 3x3 kernel)
+SC_DENSE_WGRAD = None      # tests: True / False force the dense / implicit form (None: measured)
+
+
 def _sc_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> None:
-    """Per-worker dWbig on the 1x1 implicit weight-gradient kernel (rows = images), folded onto the nine taps
-    straight into the exchange rows."""
+    """Per-worker weight gradient of a small-image layer: the dense dWbig (1x1 implicit kernel over the
+    [N, P*C] rows, folded onto the taps) or the implicit 3x3 kernel, whichever the first eager call of the
+    shape measured faster (the dense form writes P^2 blocks of fp32 slabs; the implicit one computes the
+    out-of-image taps)."""
+    key = (tuple(x.shape), tuple(dy.shape), G)
+    dense = _SC_WG_CHOICE.get(key) if SC_DENSE_WGRAD is None else SC_DENSE_WGRAD
+    if dense is None:
+        dense = True
+        if not torch.cuda.is_current_stream_capturing() and _iwgrad_ok(x, dy):
+            sink = spec.sink
+            spec.sink = _NullSink(sink, G)
+            try:
+                t_dense = _timed(lambda: _sc_wgrad_dense(x, dy, spec, G))
+                t_imp = _timed(lambda: _iwgrad(x, dy, spec, G, 9 * x.shape[1]))
+            finally:
+                spec.sink = sink
+            dense = t_dense <= t_imp
+        _SC_WG_CHOICE[key] = dense
+    if dense:
+        _sc_wgrad_dense(x, dy, spec, G)
+    else:
+        _iwgrad(x, dy, spec, G, 9 * x.shape[1])
+
+
+class _NullSink:
+    """A GradSink stand-in for timing runs: rows views and queued sums land in scratch tensors."""
+
+    def __init__(self, sink, groups: int):
+        self.flat = sink.flat
+        self.groups = groups
+
+    def rows_view(self, p, shape, dtype):
+        return torch.empty((self.groups, *shape), dtype=dtype, device=p.device)
+
+    def queue_split(self, part, out):
+        _native.native().gpu_split_reduce(part, out)
+
+    def put_groups(self, p, grads):
+        pass
+
+
+def _sc_wgrad_dense(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> None:
     n, cin, h, wd = x.shape
     cout = dy.shape[1]
     P = h * wd

@@ -495,6 +495,7 @@ def test_dense_small_image_and_stride2_paths_match_implicit_path(cuda, monkeypat
 
     monkeypatch.setattr(grouped, "S2_FORCE", True)
     monkeypatch.setattr(grouped, "_S2_CHOICE", {})
+    monkeypatch.setattr(grouped, "SC_DENSE_WGRAD", True)
     monkeypatch.setattr(grouped, flag, False)
     a = _grouped_rows(cuda, "resnet50", 4, 16)
     err_off = _rows_vs_fp32(cuda, "resnet50", 4, 16, True)
