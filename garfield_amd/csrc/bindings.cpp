@@ -873,10 +873,16 @@ void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, co
                 "gpu_gemm_nt: configuration ", cfg, " has no BatchNorm-prologue form for K = ", K, ", ", prg,
                 " rows per worker");
   }
+  const int S = garfield::gpu::gemm_nt_splits(static_cast<int>(cfg));
+  at::Tensor slabs;
+  if (S > 1) {   // split-K: fp32 slabs from the caching allocator (graph-capture safe), summed into c
+    TORCH_CHECK(!want_stats && psc == nullptr, "gpu_gemm_nt: split-K configurations have no statistics / prologue");
+    slabs = at::empty({S, M, N}, a.options().dtype(at::kFloat));
+  }
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::gemm_nt(u16(a), u16(b), static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), u16_mut(c),
                          ap, sp, rg, static_cast<int>(cfg), stream_of(dev), psc, psh, prg,
-                         static_cast<int>(pro_groups));
+                         static_cast<int>(pro_groups), S > 1 ? slabs.data_ptr<float>() : nullptr);
 }
 
 // Transposes of many bf16 matrices in one launch: dsts[i] = srcs[i]ᵀ (2-D, contiguous, 16-B aligned,
@@ -1998,6 +2004,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "dsts[i] = srcs[i]ᵀ for 2-D bf16 matrices (dims multiples of 8), one launch per 40 matrices",
         py::arg("srcs"), py::arg("dsts"));
   m.def("gemm_nt_num_cfg", &garfield::gpu::gemm_nt_num_cfg, "Number of gpu_gemm_nt tile configurations");
+  m.def("gemm_nt_splits", &garfield::gpu::gemm_nt_splits, py::arg("cfg"),
+        "Split-K factor of a gpu_gemm_nt configuration (1: none)");
   m.def("gemm_nt_valid", [](int64_t cfg, int64_t N, int64_t K) {
     return garfield::gpu::gemm_nt_valid(static_cast<int>(cfg), static_cast<int>(N), static_cast<int>(K));
   }, "Whether configuration cfg runs an N x K weight");

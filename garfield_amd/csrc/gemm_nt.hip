@@ -56,6 +56,11 @@ struct GemmPro {         // BatchNorm prologue of A (see pro_chunk); sc == nullp
 };  // 128 zero bytes: source of padded rows
 
 constexpr int EPI_PLAIN = 0, EPI_ADD = 1, EPI_STATS = 2;
+// EPI_SPLIT: split-K (blockIdx.y = split ky of gridDim.y): the workgroup reduces K range
+// [ky K / S, (ky + 1) K / S) and stores its fp32 accumulators to ws[ky][M][N]; k_split_sum adds the
+// S slabs (+ add) into C. For the latency-bound small-M x N, long-K problems (ResNet-50 CIFAR
+// layer3 / layer4 1x1 and small-image GEMMs: 250-250 workgroups walking 16-32 k-steps each).
+constexpr int EPI_SPLIT = 3;
 
 // BatchNorm prologue (PRO): A holds the PRE-BatchNorm activation of the layer before; each staged
 // 16-byte chunk (8 channels of one row) becomes bf16(max(x * scale[g][c] + shift[g][c], 0)) in LDS
@@ -108,22 +113,25 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
   const int m0 = tm * BM, n0 = tn * BN;
   const int lrow = lane >> 3, lchunk = lane & 7;
 
+  // split-K: this workgroup's K range
+  const int KS = EPI == EPI_SPLIT ? K / static_cast<int>(gridDim.y) : K;
+  const int kbase = EPI == EPI_SPLIT ? static_cast<int>(blockIdx.y) * KS : 0;
   const uint16_t* asrc[AI];
   bool av[AI];
 #pragma unroll
   for (int u = 0; u < AI; ++u) {
     const int row = (wave * AI + u) * 8 + lrow;
     av[u] = m0 + row < M;
-    asrc[u] = A + static_cast<int64_t>(av[u] ? m0 + row : 0) * K + (lchunk ^ lrow) * 8;
+    asrc[u] = A + static_cast<int64_t>(av[u] ? m0 + row : 0) * K + kbase + (lchunk ^ lrow) * 8;
   }
   const uint16_t* bsrc[BI];
 #pragma unroll
   for (int u = 0; u < BI; ++u) {
     const int row = (wave * BI + u) * 8 + lrow;
-    bsrc[u] = B + static_cast<int64_t>(n0 + row) * K + (lchunk ^ lrow) * 8;
+    bsrc[u] = B + static_cast<int64_t>(n0 + row) * K + kbase + (lchunk ^ lrow) * 8;
   }
   const uint64_t az = reinterpret_cast<uint64_t>(reinterpret_cast<const uint16_t*>(g_gemm_zero) + lchunk * 8);
-  const int steps = K / 64;
+  const int steps = KS / 64;
 
   // PRO: the [2][K] scale and shift of the tile's (at most two) workers: rows of worker g0 use entry 0
   extern __shared__ __attribute__((aligned(16))) float ptab[];
@@ -226,6 +234,18 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
     }
   }
 
+  if constexpr (EPI == EPI_SPLIT) {   // fp32 partial sums straight from the registers (C is the slab array)
+    float* ws = reinterpret_cast<float*>(C) + static_cast<int64_t>(blockIdx.y) * M * N;
+#pragma unroll
+    for (int r = 0; r < WPM; ++r) {
+      const int m = m0 + (wm * WPM + r) * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int c = 0; c < WPN; ++c)
+        *reinterpret_cast<f32x4*>(ws + static_cast<int64_t>(m) * N + n0 + (wn * WPN + c) * 16 + 4 * fq) = acc[r][c];
+    }
+    return;
+  }
   // ---- epilogue. The fragments hold 4 channels of one pixel per lane; the tile goes through
   // LDS (bf16, padded row pitch) and leaves as 16-byte-per-lane row segments (whole 128-B
   // lines per 8 lanes). Statistics come from the registers (wave_stats).
@@ -636,6 +656,43 @@ __global__ __launch_bounds__(kMergeCh * kMergeLanes) void k_finalize_tiles(
   shift[gc] = (beta ? beta[c] : 0.f) - MU * sc;
 }
 
+// C[i] = bf16(Σ_s ws[s][i] (+ add[i])), 8 elements per thread
+template <bool ADD>
+__global__ __launch_bounds__(256) void k_split_sum(const float* __restrict__ ws, int S, int64_t n8,
+                                                   uint16_t* __restrict__ C, const uint16_t* __restrict__ add) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n8) return;
+  float v[8];
+  const float4 a0 = reinterpret_cast<const float4*>(ws)[2 * i], a1 = reinterpret_cast<const float4*>(ws)[2 * i + 1];
+  v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+  for (int s = 1; s < S; ++s) {
+    const float4* p = reinterpret_cast<const float4*>(ws + static_cast<int64_t>(s) * n8 * 8) + 2 * i;
+    const float4 b0 = p[0], b1 = p[1];
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  if constexpr (ADD) {
+    const uint4 u = reinterpret_cast<const uint4*>(add)[i];
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += bf16_to_f((e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xffffu));
+  }
+  reinterpret_cast<uint4*>(C)[i] = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                              pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+}
+
+template <int WPM, int WPN, int WM, int WN, int NS>
+void launch_split(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
+                  float* ws, int S, hipStream_t stream) {
+  constexpr int BM = 16 * WPM * WM, BN = 16 * WPN * WN;
+  const dim3 grid(((M + BM - 1) / BM) * (N / BN), S);
+  hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_SPLIT, false>), grid, dim3(256), 0, stream, A, B, M, N, K,
+                     reinterpret_cast<uint16_t*>(ws), nullptr, nullptr, int64_t{0}, GemmPro{});
+  const int64_t n8 = static_cast<int64_t>(M) * N / 8;
+  const dim3 g2(static_cast<unsigned>((n8 + 255) / 256));
+  if (add) hipLaunchKernelGGL((k_split_sum<true>), g2, dim3(256), 0, stream, ws, S, n8, C, add);
+  else hipLaunchKernelGGL((k_split_sum<false>), g2, dim3(256), 0, stream, ws, S, n8, C, add);
+}
+
 template <int WPM, int WPN, int WM, int WN, int NS>
 void launch_cfg(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
                 float* stats, int64_t rg, hipStream_t stream, const GemmPro& pro) {
@@ -736,7 +793,12 @@ constexpr int kCfgBN[] = {128, 64, 128, 256, 64, 256, 128, 64, 256};
 constexpr int kCfgSR[] = {64, 64, 32, 64, 32, 64, 64, 32, 32};
 constexpr int kWsBN[] = {256, 256, 128, 128, 64, 64};
 constexpr int kWsRW[] = {32, 64, 16, 32, 16, 32};
-constexpr int kNumCfg = kNumNt + 6;
+constexpr int kNumBase = kNumNt + 6;
+constexpr int kSplits[] = {2, 4};                       // split-K variants of the K-loop configurations
+constexpr int kNumCfg = kNumBase + 2 * kNumNt;
+// configuration -> (K-loop configuration, splits); splits 1 for the base configurations
+inline int split_of(int cfg) { return cfg >= kNumBase ? kSplits[(cfg - kNumBase) / kNumNt] : 1; }
+inline int base_of(int cfg) { return cfg >= kNumBase ? (cfg - kNumBase) % kNumNt : cfg; }
 
 bool ws_fits(int i, int K) {
   const int kb = K / 64;
@@ -827,7 +889,7 @@ int gemm_nt_num_cfg() { return kNumCfg; }
 // The BatchNorm-prologue form of configuration cfg: its LDS (ring + scale / shift table) fits, and a
 // K-loop tile spans at most two workers (BM <= rows per worker)
 bool gemm_nt_pro_ok(int cfg, int K, int64_t prg, int groups) {
-  if (cfg < 0 || cfg >= kNumCfg || prg <= 0 || prg >= (int64_t{1} << 31)) return false;
+  if (cfg < 0 || cfg >= kNumBase || prg <= 0 || prg >= (int64_t{1} << 31)) return false;
   if (cfg < kNumNt) return kCfgBM[cfg] <= prg && static_cast<int64_t>(4) * K * 4 <= 32 * 1024;
   const int i = cfg - kNumNt;
   const int64_t tab = static_cast<int64_t>(2) * groups * K * 4;   // dynamic LDS: <= 64 KB without an attribute
@@ -836,21 +898,27 @@ bool gemm_nt_pro_ok(int cfg, int K, int64_t prg, int groups) {
 
 bool gemm_nt_valid(int cfg, int N, int K) {
   if (cfg < 0 || cfg >= kNumCfg || K % 64 || K <= 0) return false;
+  if (cfg >= kNumBase) return K % (64 * split_of(cfg)) == 0 && N % kCfgBN[base_of(cfg)] == 0 && N % 8 == 0;
   if (cfg < kNumNt) return N % kCfgBN[cfg] == 0;
   return N % kWsBN[cfg - kNumNt] == 0 && ws_fits(cfg - kNumNt, K);
 }
 
+int gemm_nt_splits(int cfg) { return cfg >= 0 && cfg < kNumCfg ? split_of(cfg) : 1; }
+
 int gemm_nt_tile_m(int cfg) {
+  if (cfg >= kNumBase && cfg < kNumCfg) return kCfgBM[base_of(cfg)];
   if (cfg >= 0 && cfg < kNumNt) return kCfgBM[cfg];
   if (cfg >= kNumNt && cfg < kNumCfg) return (4 / (kWsBN[cfg - kNumNt] / 64)) * kWsRW[cfg - kNumNt];
   return 0;
 }
 int gemm_nt_tile_n(int cfg) {
+  if (cfg >= kNumBase && cfg < kNumCfg) return kCfgBN[base_of(cfg)];
   if (cfg >= 0 && cfg < kNumNt) return kCfgBN[cfg];
   if (cfg >= kNumNt && cfg < kNumCfg) return kWsBN[cfg - kNumNt];
   return 0;
 }
 int gemm_nt_stats_rows(int cfg) {
+  if (cfg >= kNumBase) return 1 << 30;   // split-K forms have no statistics epilogue
   if (cfg >= 0 && cfg < kNumNt) return kCfgSR[cfg];
   if (cfg >= kNumNt && cfg < kNumCfg) return ws_bm(kWsBN[cfg - kNumNt], kWsRW[cfg - kNumNt]);
   return 0;
@@ -902,8 +970,23 @@ int gemm_nt_pick(int64_t M, int N, int K, int64_t rg_limit) {
 
 void gemm_nt(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
              float* stats, int64_t rg, int cfg, hipStream_t stream, const float* pro_scale, const float* pro_shift,
-             int64_t pro_rg, int pro_groups) {
+             int64_t pro_rg, int pro_groups, float* split_ws) {
   if (M <= 0) return;
+  if (cfg >= kNumBase) {   // split-K (no statistics, no prologue; the caller provides the fp32 slabs)
+    const int S = split_of(cfg);
+    switch (base_of(cfg)) {
+      case 0: launch_split<4, 4, 2, 2, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+      case 6: launch_split<4, 4, 2, 2, 3>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+      case 7: launch_split<2, 2, 2, 2, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+      case 8: launch_split<2, 4, 1, 4, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+      case 1: launch_split<4, 4, 4, 1, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+      case 2: launch_split<2, 4, 2, 2, 3>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+      case 3: launch_split<4, 4, 1, 4, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+      case 4: launch_split<2, 2, 2, 2, 4>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+      default: launch_split<4, 8, 2, 2, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+    }
+    return;
+  }
   GemmPro pro{};
   if (pro_scale) {
     pro.sc = pro_scale;

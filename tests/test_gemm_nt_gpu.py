@@ -21,8 +21,8 @@ def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
     b = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
     add = torch.randn(M, N, device=cuda).to(torch.bfloat16)
     ref = a.float() @ b.float().t()
-    ran = 0
-    for cfg in range(native.gemm_nt_num_cfg()):
+    ran = splits = 0
+    for cfg in range(native.gemm_nt_num_cfg()):   # split-K forms included (fp32 slabs + one summing pass)
         if not native.gemm_nt_valid(cfg, N, K):
             continue
         c = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
@@ -32,7 +32,9 @@ def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
         native.gpu_gemm_nt(a, b, c2, c2, None, 0, cfg)        # in place: c = a·bᵀ + c
         assert rel(c2, ref + add.float()) < 5e-3, cfg
         ran += 1
+        splits += native.gemm_nt_splits(cfg) > 1
     assert ran >= 2
+    assert splits > 0 or K % 128 != 0
     c = torch.empty((M, N), device=cuda, dtype=torch.bfloat16)
     native.gpu_gemm_nt(a, b, c)                                 # automatic configuration
     assert rel(c, ref) < 5e-3
