@@ -625,7 +625,8 @@ void g_sc_expand(const std::vector<at::Tensor>& ws, const std::vector<int64_t>& 
                     w.size(2) == 3 && w.size(3) == 3 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "gpu_sc_expand: weights must be channels_last bf16 [Cout, Cin, 3, 3] on one device");
     const int64_t co = w.size(0), ci = w.size(1), P = H * W;
-    TORCH_CHECK(H >= 1 && H <= 2 && W >= 1 && W <= 2 && ci % 8 == 0, "gpu_sc_expand: H, W in {1, 2}, Cin % 8 == 0");
+    TORCH_CHECK(H >= 1 && H <= 2 && W >= 1 && W <= 2 && ci % 8 == 0 && co % 8 == 0,
+                "gpu_sc_expand: H, W in {1, 2}, Cin % 8 == 0, Cout % 8 == 0");
     for (const auto* t : {&bigs[k], &bigTs[k]})
       TORCH_CHECK(t->device() == w.device() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() &&
                       t->numel() == P * co * P * ci,

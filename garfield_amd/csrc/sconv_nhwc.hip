@@ -23,31 +23,47 @@ namespace gpu {
 using namespace dev;
 namespace {
 
-// one thread per 8 consecutive ci of a Wbig row (16-byte load / store); its 8 Wbigᵀ elements are
-// scattered 2-byte stores (the matrices are 0.25-2 MB: the launch is latency-bound either way)
+// one thread per 8 consecutive elements of a Wbig row (8 ci: one 16-byte load and store) or of a
+// Wbigᵀ row (8 co: 8 strided 2-byte loads of the L2-resident weight, one 16-byte store); the first
+// start[count] units are Wbig's, the next as many Wbigᵀ's
 __global__ __launch_bounds__(256) void k_sc_expand(ScExpandJobs jobs) {
-  const int64_t u = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t u0 = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t half = jobs.start[jobs.count];
+  if (u0 >= 2 * half) return;
+  const bool tr = u0 >= half;
+  const int64_t u = tr ? u0 - half : u0;
   int jb = 0;
   while (jb + 1 < jobs.count && u >= jobs.start[jb + 1]) ++jb;
-  if (u >= jobs.start[jobs.count]) return;
   const ScExpandJob& J = jobs.job[jb];
   const int P = J.H * J.W;
   const int64_t v = u - jobs.start[jb];
-  const int rowu = P * J.cin / 8;   // 8-element units per Wbig row
-  const int r = static_cast<int>(v / rowu), c8 = static_cast<int>(v - static_cast<int64_t>(r) * rowu);
-  const int pq = r / J.cout, co = r - pq * J.cout;
-  const int col = c8 * 8;
-  const int p = col / J.cin, ci = col - p * J.cin;
-  const int i = p / J.W - pq / J.W + 1, j = p % J.W - pq % J.W + 1;
-  uint4 val = make_uint4(0u, 0u, 0u, 0u);
-  if (i >= 0 && i < 3 && j >= 0 && j < 3)
-    val = *reinterpret_cast<const uint4*>(J.w + (static_cast<int64_t>(co) * 9 + i * 3 + j) * J.cin + ci);
-  *reinterpret_cast<uint4*>(J.big + static_cast<int64_t>(r) * P * J.cin + col) = val;
-  const uint32_t wd[4] = {val.x, val.y, val.z, val.w};
-  const int64_t ld = static_cast<int64_t>(P) * J.cout;
+  if (!tr) {
+    const int rowu = P * J.cin / 8;   // 8-element units per Wbig row
+    const int r = static_cast<int>(v / rowu), c8 = static_cast<int>(v - static_cast<int64_t>(r) * rowu);
+    const int pq = r / J.cout, co = r - pq * J.cout;
+    const int col = c8 * 8;
+    const int p = col / J.cin, ci = col - p * J.cin;
+    const int i = p / J.W - pq / J.W + 1, j = p % J.W - pq % J.W + 1;
+    uint4 val = make_uint4(0u, 0u, 0u, 0u);
+    if (i >= 0 && i < 3 && j >= 0 && j < 3)
+      val = *reinterpret_cast<const uint4*>(J.w + (static_cast<int64_t>(co) * 9 + i * 3 + j) * J.cin + ci);
+    *reinterpret_cast<uint4*>(J.big + static_cast<int64_t>(r) * P * J.cin + col) = val;
+  } else {
+    const int rowu = P * J.cout / 8;   // 8-element units per Wbigᵀ row (p, ci): columns (p', co)
+    const int r = static_cast<int>(v / rowu), c8 = static_cast<int>(v - static_cast<int64_t>(r) * rowu);
+    const int p = r / J.cin, ci = r - p * J.cin;
+    const int col = c8 * 8;
+    const int pq = col / J.cout, co = col - pq * J.cout;
+    const int i = p / J.W - pq / J.W + 1, j = p % J.W - pq % J.W + 1;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (i >= 0 && i < 3 && j >= 0 && j < 3) {
+      const uint16_t* src = J.w + (static_cast<int64_t>(co) * 9 + i * 3 + j) * J.cin + ci;
 #pragma unroll
-  for (int e = 0; e < 8; ++e)
-    J.bigT[static_cast<int64_t>(col + e) * ld + r] = static_cast<uint16_t>((wd[e >> 1] >> (16 * (e & 1))) & 0xffffu);
+      for (int e = 0; e < 8; ++e)
+        w[e >> 1] |= static_cast<uint32_t>(src[static_cast<int64_t>(e) * 9 * J.cin]) << (16 * (e & 1));
+    }
+    *reinterpret_cast<uint4*>(J.bigT + static_cast<int64_t>(r) * P * J.cout + col) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
 }
 
 // out[g][co][(i*3 + j)*Cin + ci] = Σ_s Σ_{pairs of tap (i, j)} slab[s][g][(p', co)][(p, ci)], 8 ci per thread
@@ -100,7 +116,7 @@ __global__ __launch_bounds__(256) void k_sc_fold(const float* __restrict__ slab,
 }  // namespace
 
 void sc_expand(const ScExpandJobs& jobs, hipStream_t stream) {
-  const int64_t total = jobs.start[jobs.count];
+  const int64_t total = 2 * jobs.start[jobs.count];   // Wbig units, then as many Wbigᵀ units
   if (total <= 0) return;
   hipLaunchKernelGGL(k_sc_expand, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, stream, jobs);
 }

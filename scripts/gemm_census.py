@@ -99,7 +99,7 @@ def main():
         print(f"{M:>8} {N:>6} {K:>6} {int(add):>3} {int(st):>2} {n:>6} {cfg:>4} {t_cfg:>8.1f} {best:>5} {t_best:>9.1f} "
               f"{gf:>6.2f} {gf / t_cfg * 1000.0:>8.1f}")
     print(f"total per step: {tot_cfg:.1f} us with the step's choices, {tot_best:.1f} us with the best valid ones")
-    del grouped
+    _ = grouped
 
 
 if __name__ == "__main__":
