@@ -300,6 +300,45 @@ __device__ __forceinline__ void running_update(const float* __restrict__ mean, c
   }
 }
 
+// 8 channels of one row as stored: packed bf16 (one uint4) or fp32 (two float4)
+struct F8 {
+  float4 a, b;
+};
+template <int DT>
+using Raw8 = typename std::conditional<DT == kF32, F8, uint4>::type;
+
+template <int DT>
+__device__ __forceinline__ Raw8<DT> ld_raw8(const void* p, int64_t off) {
+  if constexpr (DT == kF32) {
+    const float* f = static_cast<const float*>(p) + off;
+    return F8{*reinterpret_cast<const float4*>(f), *reinterpret_cast<const float4*>(f + 4)};
+  } else {
+    return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + off);
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void st_raw8(void* p, int64_t off, const Raw8<DT>& r) {
+  if constexpr (DT == kF32) {
+    float* f = static_cast<float*>(p) + off;
+    *reinterpret_cast<float4*>(f) = r.a;
+    *reinterpret_cast<float4*>(f + 4) = r.b;
+  } else {
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + off) = r;
+  }
+}
+
+__device__ __forceinline__ void unpack8(const uint4 u, float (&v)[8]) {
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ void unpack8(const F8& u, float (&v)[8]) {
+  v[0] = u.a.x; v[1] = u.a.y; v[2] = u.a.z; v[3] = u.a.w;
+  v[4] = u.b.x; v[5] = u.b.y; v[6] = u.b.z; v[7] = u.b.w;
+}
+
 // Elementwise passes over [R, C]: each workgroup owns kApplyIters x rp rows.
 constexpr int kApplyIters = 4;
 
@@ -330,6 +369,55 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
   const bool fixed = nv <= tch;
   int gl = -1;
   float sc[8], sf[8];
+  if (fixed && row0 + static_cast<int64_t>(kApplyIters) * rp <= R && rp * kApplyIters <= rg) {
+    // every row of the workgroup exists and it spans at most two workers: all of this thread's
+    // loads are issued before the first use (kApplyIters rows in flight, not one)
+    const int v = threadIdx.x % tch;
+    if (v >= nv) return;
+    const int c = v * 8;
+    const int g0 = static_cast<int>(row0 / rg);
+    const int64_t gb = static_cast<int64_t>(g0 + 1) * rg;   // the next worker's first row
+    Raw8<DT> xr[kApplyIters], rr[kApplyIters];
+#pragma unroll
+    for (int it = 0; it < kApplyIters; ++it) {
+      const int64_t off = (row0 + static_cast<int64_t>(it) * rp + tr) * C + c;
+      xr[it] = ld_raw8<DT>(x, off);
+      if constexpr (RES) rr[it] = ld_raw8<DT>(res, off);
+    }
+#pragma unroll
+    for (int it = 0; it < kApplyIters; ++it) {
+      const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
+      const int g = g0 + (row >= gb ? 1 : 0);
+      if (g != gl) {
+        load8f(scale + static_cast<int64_t>(g) * C + c, sc);
+        load8f(shift + static_cast<int64_t>(g) * C + c, sf);
+        gl = g;
+      }
+      const int64_t off = row * C + c;
+      float a[8], o[8];
+      unpack8(xr[it], a);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = a[i] * sc[i] + sf[i];
+      if constexpr (RES) {
+        float r[8];
+        unpack8(rr[it], r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] += r[i];
+      }
+      if constexpr (RELU) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = o[i] > 0.f ? o[i] : 0.f;
+        if (mask) {
+          uint32_t bits = 0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) bits |= (stored_pos<DT>(o[i]) ? 1u : 0u) << i;
+          mask[off >> 3] = static_cast<uint8_t>(bits);
+        }
+      }
+      store_vec<8>(y, DT, off, o);
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < kApplyIters; ++it) {
     const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
@@ -414,6 +502,57 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const void* __restrict__
   const bool fixed = nv <= tch;   // one channel group per thread: coefficients once per worker
   int gl = -1;
   float mu[8], ca[8], cb[8], cc[8], rs[8] = {}, rf[8] = {};
+  if (fixed && RM != 1 && row0 + static_cast<int64_t>(kApplyIters) * rp <= R && rp * kApplyIters <= rg) {
+    // whole rows, at most two workers: every load of the thread issued before the first use
+    const int v = threadIdx.x % tch;
+    if (v >= nv) return;
+    const int c = v * 8;
+    const int g0 = static_cast<int>(row0 / rg);
+    const int64_t gb = static_cast<int64_t>(g0 + 1) * rg;
+    Raw8<DT> xr[kApplyIters], dr[kApplyIters];
+    uint32_t mb[kApplyIters];
+#pragma unroll
+    for (int it = 0; it < kApplyIters; ++it) {
+      const int64_t off = (row0 + static_cast<int64_t>(it) * rp + tr) * C + c;
+      xr[it] = ld_raw8<DT>(x, off);
+      dr[it] = ld_raw8<DT>(dy, off);
+      if constexpr (RM == 2) mb[it] = mask[off >> 3];
+    }
+#pragma unroll
+    for (int it = 0; it < kApplyIters; ++it) {
+      const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
+      const int g = g0 + (row >= gb ? 1 : 0);
+      if (g != gl) {
+        const float* cg = coef + static_cast<int64_t>(g) * 3 * C;
+        load8f(mean + static_cast<int64_t>(g) * C + c, mu);
+        load8f(cg + c, ca);
+        load8f(cg + C + c, cb);
+        load8f(cg + 2 * C + c, cc);
+        if constexpr (RM == 3) {
+          load8f(rsc + static_cast<int64_t>(g) * C + c, rs);
+          load8f(rsh + static_cast<int64_t>(g) * C + c, rf);
+        }
+        gl = g;
+      }
+      const int64_t off = row * C + c;
+      float a[8], d[8];
+      unpack8(xr[it], a);
+      unpack8(dr[it], d);
+      if constexpr (RM == 2) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = (mb[it] >> i) & 1u ? d[i] : 0.f;
+      } else if constexpr (RM == 3) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = stored_pos<DT>(fmaxf(fmaf(a[i], rs[i], rf[i]), 0.f)) ? d[i] : 0.f;
+      }
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = ca[i] * (d[i] - cb[i] - (a[i] - mu[i]) * cc[i]);
+      store_vec<8>(dx, DT, off, o);
+      if constexpr (RES_OUT) store_vec<8>(dres, DT, off, d);
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < kApplyIters; ++it) {
     const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
@@ -502,45 +641,6 @@ __device__ __forceinline__ void small_reduce(float (&red)[2][SmallGeo<CH>::Lanes
   __syncthreads();
 }
 
-
-// 8 channels of one row as stored: packed bf16 (one uint4) or fp32 (two float4)
-struct F8 {
-  float4 a, b;
-};
-template <int DT>
-using Raw8 = typename std::conditional<DT == kF32, F8, uint4>::type;
-
-template <int DT>
-__device__ __forceinline__ Raw8<DT> ld_raw8(const void* p, int64_t off) {
-  if constexpr (DT == kF32) {
-    const float* f = static_cast<const float*>(p) + off;
-    return F8{*reinterpret_cast<const float4*>(f), *reinterpret_cast<const float4*>(f + 4)};
-  } else {
-    return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + off);
-  }
-}
-
-template <int DT>
-__device__ __forceinline__ void st_raw8(void* p, int64_t off, const Raw8<DT>& r) {
-  if constexpr (DT == kF32) {
-    float* f = static_cast<float*>(p) + off;
-    *reinterpret_cast<float4*>(f) = r.a;
-    *reinterpret_cast<float4*>(f + 4) = r.b;
-  } else {
-    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + off) = r;
-  }
-}
-
-__device__ __forceinline__ void unpack8(const uint4 u, float (&v)[8]) {
-  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
-  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
-  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
-  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
-}
-__device__ __forceinline__ void unpack8(const F8& u, float (&v)[8]) {
-  v[0] = u.a.x; v[1] = u.a.y; v[2] = u.a.z; v[3] = u.a.w;
-  v[4] = u.b.x; v[5] = u.b.y; v[6] = u.b.z; v[7] = u.b.w;
-}
 
 // dz = dy where the forward output y > 0 (RM 1) / its mask bit is set (RM 2), else 0
 __device__ __forceinline__ uint4 keep_pos(uint4 d, const uint4 yy) {
