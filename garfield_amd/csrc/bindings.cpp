@@ -818,7 +818,7 @@ int64_t g_conv3x3_pick(int64_t n, int64_t h, int64_t w, int64_t c, int64_t cout)
 void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, const c10::optional<at::Tensor>& add,
                const c10::optional<at::Tensor>& stats, int64_t rg, int64_t cfg,
                const c10::optional<at::Tensor>& pro_scale, const c10::optional<at::Tensor>& pro_shift,
-               int64_t pro_groups) {
+               int64_t pro_groups, const c10::optional<at::Tensor>& add_mask) {
   const auto dev = a.device();
   auto chk = [&](const at::Tensor& t, const char* what) {
     TORCH_CHECK(t.is_cuda() && t.device() == dev && t.scalar_type() == at::kBFloat16 && t.dim() == 2 &&
@@ -874,6 +874,14 @@ void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, co
                 "gpu_gemm_nt: configuration ", cfg, " has no BatchNorm-prologue form for K = ", K, ", ", prg,
                 " rows per worker");
   }
+  const uint8_t* mp = nullptr;
+  if (add_mask.has_value() && add_mask->defined()) {
+    TORCH_CHECK(ap != nullptr, "gpu_gemm_nt: add_mask needs add");
+    TORCH_CHECK(add_mask->is_cuda() && add_mask->device() == dev && add_mask->scalar_type() == at::kByte &&
+                    add_mask->is_contiguous() && add_mask->numel() * 8 == M * N,
+                "gpu_gemm_nt: add_mask must be a contiguous uint8 bit mask of M * N / 8 bytes on a's device");
+    mp = add_mask->data_ptr<uint8_t>();
+  }
   const int S = garfield::gpu::gemm_nt_splits(static_cast<int>(cfg));
   at::Tensor slabs;
   if (S > 1) {   // split-K: fp32 slabs from the caching allocator (graph-capture safe), summed into c
@@ -883,7 +891,7 @@ void g_gemm_nt(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c, co
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::gemm_nt(u16(a), u16(b), static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), u16_mut(c),
                          ap, sp, rg, static_cast<int>(cfg), stream_of(dev), psc, psh, prg,
-                         static_cast<int>(pro_groups), S > 1 ? slabs.data_ptr<float>() : nullptr);
+                         static_cast<int>(pro_groups), S > 1 ? slabs.data_ptr<float>() : nullptr, mp);
 }
 
 // Transposes of many bf16 matrices in one launch: dsts[i] = srcs[i]ᵀ (2-D, contiguous, 16-B aligned,
@@ -1986,10 +1994,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "rg=0, cfg=-1); stats: fp32 per-worker BatchNorm statistics of c, laid out as gemm_nt_stats_geometry "
         "says (gpu_bn_forward's tile_stats / tile_m / tile_e); pro_scale / pro_shift [pro_groups, K] fp32: a is a "
         "pre-BatchNorm activation used as bf16(max(a * scale + shift, 0)) of its row's worker (the BatchNorm + ReLU "
-        "fused into the staging of a)",
+        "fused into the staging of a); add_mask [M * N / 8] uint8: add counts only where its bit is set (a "
+        "BatchNorm's ReLU bits: add = dy gives the residual gradient without materialising it)",
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("add") = py::none(), py::arg("stats") = py::none(),
         py::arg("rg") = 0, py::arg("cfg") = -1, py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none(),
-        py::arg("pro_groups") = 0);
+        py::arg("pro_groups") = 0, py::arg("add_mask") = py::none());
   m.def("gemm_nt_pro_ok", [](int64_t cfg, int64_t K, int64_t prg, int64_t groups) {
     return garfield::gpu::gemm_nt_pro_ok(static_cast<int>(cfg), static_cast<int>(K), prg, static_cast<int>(groups));
   }, py::arg("cfg"), py::arg("K"), py::arg("rows_per_worker"), py::arg("groups"),

@@ -86,7 +86,8 @@ void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, 
 // bf16(max(a * scale + shift, 0)) (gemm_nt_pro_ok(cfg, ...) must hold)
 void gemm_nt(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
              float* stats, int64_t rg, int cfg, hipStream_t stream, const float* pro_scale = nullptr,
-             const float* pro_shift = nullptr, int64_t pro_rg = 0, int pro_groups = 0, float* split_ws = nullptr);
+             const float* pro_shift = nullptr, int64_t pro_rg = 0, int pro_groups = 0, float* split_ws = nullptr,
+             const uint8_t* add_mask = nullptr);
 bool gemm_nt_pro_ok(int cfg, int K, int64_t prg, int groups);
 // split-K factor of a configuration (1: none); a split configuration needs split_ws = S x M x N floats
 int gemm_nt_splits(int cfg);

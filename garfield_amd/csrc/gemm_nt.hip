@@ -53,6 +53,7 @@ struct GemmPro {         // BatchNorm prologue of A (see pro_chunk); sc == nullp
   const float* sh;       // [G][K] shift
   FastDiv frg;           // rows per worker
   int G;
+  const uint8_t* amask;  // EPI_ADD: add is masked by this 1-bit-per-element mask (BatchNorm ReLU bits); nullptr: not
 };  // 128 zero bytes: source of padded rows
 
 constexpr int EPI_PLAIN = 0, EPI_ADD = 1, EPI_STATS = 2;
@@ -84,6 +85,47 @@ __device__ __forceinline__ void pro_chunk(char* p, const float* sc, const float*
   *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]),
                                             pack_bf16x2(y[4], y[5]), pack_bf16x2(y[6], y[7]));
 }
+
+// v[0..3] += add[e .. e + 4), term i kept where bit i of keep is set
+__device__ __forceinline__ void add_bf16x4(float (&v)[4], const uint16_t* __restrict__ add, uint32_t keep, int64_t e) {
+  const uint2 a = *reinterpret_cast<const uint2*>(add + e);
+  v[0] += (keep & 1u) ? bf16_to_f(a.x & 0xffffu) : 0.f;
+  v[1] += (keep & 2u) ? bf16_to_f(a.x >> 16) : 0.f;
+  v[2] += (keep & 4u) ? bf16_to_f(a.y & 0xffffu) : 0.f;
+  v[3] += (keep & 8u) ? bf16_to_f(a.y >> 16) : 0.f;
+}
+
+// EPI_ADD with amask (the residual gradient dres = dy · [y > 0] of a BatchNorm + ReLU, read from dy and
+// the forward's ReLU bits instead of a materialised dres): the mask bits of a lane's row over the
+// wave's 16 * NG channels from element e (a multiple of 16 * NG) in ONE load of 2 * NG bytes; all ones
+// without a mask
+template <int NG>
+struct RowMask {
+  uint32_t w[NG / 2];
+  __device__ __forceinline__ void load(const uint8_t* __restrict__ amask, int64_t e) {
+    static_assert(NG == 2 || NG == 4 || NG == 8, "2, 4 or 8 channel groups of 16");
+    if (!amask) {
+#pragma unroll
+      for (int i = 0; i < NG / 2; ++i) w[i] = 0xffffffffu;
+      return;
+    }
+    const uint8_t* p = amask + (e >> 3);
+    if constexpr (NG == 2) {
+      w[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if constexpr (NG == 4) {
+      const uint2 u = *reinterpret_cast<const uint2*>(p);
+      w[0] = u.x; w[1] = u.y;
+    } else {
+      const uint4 u = *reinterpret_cast<const uint4*>(p);
+      w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+    }
+  }
+  // bits of channel group c's 4 channels at 4 * fq (byte 2c + fq / 2, nibble fq % 2)
+  __device__ __forceinline__ uint32_t nib(int c, int fq) const {
+    const int b = 2 * c + (fq >> 1);
+    return (w[b >> 2] >> ((b & 3) * 8 + (fq & 1) * 4)) & 0xfu;
+  }
+};
 
 // ---------------------------------------------------------------------------------------------
 // K-loop kernel
@@ -261,17 +303,14 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
 #pragma unroll
     for (int r = 0; r < WPM; ++r) {
       const int m = m0 + mwl + r * 16 + fr;
+      RowMask<WPN> rm;
+      if constexpr (EPI == EPI_ADD)
+        if (m < M) rm.load(pro.amask, static_cast<int64_t>(m) * N + n0 + wn * 16 * WPN);
 #pragma unroll
       for (int c = 0; c < WPN; ++c) {
         float v[4] = {acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]};
         if constexpr (EPI == EPI_ADD) {                 // one rounding: the sum is formed in fp32
-          if (m < M) {
-            const uint2 a = *reinterpret_cast<const uint2*>(add + static_cast<int64_t>(m) * N + n0 + nwl + c * 16);
-            v[0] += bf16_to_f(a.x & 0xffffu);
-            v[1] += bf16_to_f(a.x >> 16);
-            v[2] += bf16_to_f(a.y & 0xffffu);
-            v[3] += bf16_to_f(a.y >> 16);
-          }
+          if (m < M) add_bf16x4(v, add, rm.nib(c, fq), static_cast<int64_t>(m) * N + n0 + nwl + c * 16);
         }
         uint2 o;
         o.x = static_cast<uint32_t>(f_to_bf16(v[0])) | (static_cast<uint32_t>(f_to_bf16(v[1])) << 16);
@@ -503,17 +542,14 @@ __global__ __launch_bounds__(256) void k_gemm_ws(const uint16_t* __restrict__ A,
     for (int r = 0; r < WPM; ++r) {
       const int rr = r * 16 + fr;
       const int m = r0 + rr;
+      RowMask<4> rm;
+      if constexpr (EPI == EPI_ADD)
+        if (m < M) rm.load(pro.amask, static_cast<int64_t>(m) * N + nc);
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         float v[4] = {acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]};
         if constexpr (EPI == EPI_ADD) {
-          if (m < M) {
-            const uint2 a = *reinterpret_cast<const uint2*>(add + static_cast<int64_t>(m) * N + nc + c * 16 + 4 * fq);
-            v[0] += bf16_to_f(a.x & 0xffffu);
-            v[1] += bf16_to_f(a.x >> 16);
-            v[2] += bf16_to_f(a.y & 0xffffu);
-            v[3] += bf16_to_f(a.y >> 16);
-          }
+          if (m < M) add_bf16x4(v, add, rm.nib(c, fq), static_cast<int64_t>(m) * N + nc + c * 16 + 4 * fq);
         }
         pk[r][c][0] = pack_bf16x2(v[0], v[1]);
         pk[r][c][1] = pack_bf16x2(v[2], v[3]);
@@ -656,10 +692,11 @@ __global__ __launch_bounds__(kMergeCh * kMergeLanes) void k_finalize_tiles(
   shift[gc] = (beta ? beta[c] : 0.f) - MU * sc;
 }
 
-// C[i] = bf16(Σ_s ws[s][i] (+ add[i])), 8 elements per thread
+// C[i] = bf16(Σ_s ws[s][i] (+ add[i], masked by amask when given)), 8 elements per thread
 template <bool ADD>
 __global__ __launch_bounds__(256) void k_split_sum(const float* __restrict__ ws, int S, int64_t n8,
-                                                   uint16_t* __restrict__ C, const uint16_t* __restrict__ add) {
+                                                   uint16_t* __restrict__ C, const uint16_t* __restrict__ add,
+                                                   const uint8_t* __restrict__ amask) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= n8) return;
   float v[8];
@@ -673,8 +710,10 @@ __global__ __launch_bounds__(256) void k_split_sum(const float* __restrict__ ws,
   if constexpr (ADD) {
     const uint4 u = reinterpret_cast<const uint4*>(add)[i];
     const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+    const uint32_t keep = amask ? static_cast<uint32_t>(amask[i]) : 0xffu;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += bf16_to_f((e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xffffu));
+    for (int e = 0; e < 8; ++e)
+      v[e] += ((keep >> e) & 1u) ? bf16_to_f((e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xffffu)) : 0.f;
   }
   reinterpret_cast<uint4*>(C)[i] = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
                                               pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
@@ -682,15 +721,15 @@ __global__ __launch_bounds__(256) void k_split_sum(const float* __restrict__ ws,
 
 template <int WPM, int WPN, int WM, int WN, int NS>
 void launch_split(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
-                  float* ws, int S, hipStream_t stream) {
+                  const uint8_t* amask, float* ws, int S, hipStream_t stream) {
   constexpr int BM = 16 * WPM * WM, BN = 16 * WPN * WN;
   const dim3 grid(((M + BM - 1) / BM) * (N / BN), S);
   hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_SPLIT, false>), grid, dim3(256), 0, stream, A, B, M, N, K,
                      reinterpret_cast<uint16_t*>(ws), nullptr, nullptr, int64_t{0}, GemmPro{});
   const int64_t n8 = static_cast<int64_t>(M) * N / 8;
   const dim3 g2(static_cast<unsigned>((n8 + 255) / 256));
-  if (add) hipLaunchKernelGGL((k_split_sum<true>), g2, dim3(256), 0, stream, ws, S, n8, C, add);
-  else hipLaunchKernelGGL((k_split_sum<false>), g2, dim3(256), 0, stream, ws, S, n8, C, add);
+  if (add) hipLaunchKernelGGL((k_split_sum<true>), g2, dim3(256), 0, stream, ws, S, n8, C, add, amask);
+  else hipLaunchKernelGGL((k_split_sum<false>), g2, dim3(256), 0, stream, ws, S, n8, C, add, amask);
 }
 
 template <int WPM, int WPN, int WM, int WN, int NS>
@@ -970,24 +1009,25 @@ int gemm_nt_pick(int64_t M, int N, int K, int64_t rg_limit) {
 
 void gemm_nt(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
              float* stats, int64_t rg, int cfg, hipStream_t stream, const float* pro_scale, const float* pro_shift,
-             int64_t pro_rg, int pro_groups, float* split_ws) {
+             int64_t pro_rg, int pro_groups, float* split_ws, const uint8_t* add_mask) {
   if (M <= 0) return;
   if (cfg >= kNumBase) {   // split-K (no statistics, no prologue; the caller provides the fp32 slabs)
     const int S = split_of(cfg);
     switch (base_of(cfg)) {
-      case 0: launch_split<4, 4, 2, 2, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
-      case 6: launch_split<4, 4, 2, 2, 3>(A, B, M, N, K, C, add, split_ws, S, stream); break;
-      case 7: launch_split<2, 2, 2, 2, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
-      case 8: launch_split<2, 4, 1, 4, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
-      case 1: launch_split<4, 4, 4, 1, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
-      case 2: launch_split<2, 4, 2, 2, 3>(A, B, M, N, K, C, add, split_ws, S, stream); break;
-      case 3: launch_split<4, 4, 1, 4, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
-      case 4: launch_split<2, 2, 2, 2, 4>(A, B, M, N, K, C, add, split_ws, S, stream); break;
-      default: launch_split<4, 8, 2, 2, 2>(A, B, M, N, K, C, add, split_ws, S, stream); break;
+      case 0: launch_split<4, 4, 2, 2, 2>(A, B, M, N, K, C, add, add_mask, split_ws, S, stream); break;
+      case 6: launch_split<4, 4, 2, 2, 3>(A, B, M, N, K, C, add, add_mask, split_ws, S, stream); break;
+      case 7: launch_split<2, 2, 2, 2, 2>(A, B, M, N, K, C, add, add_mask, split_ws, S, stream); break;
+      case 8: launch_split<2, 4, 1, 4, 2>(A, B, M, N, K, C, add, add_mask, split_ws, S, stream); break;
+      case 1: launch_split<4, 4, 4, 1, 2>(A, B, M, N, K, C, add, add_mask, split_ws, S, stream); break;
+      case 2: launch_split<2, 4, 2, 2, 3>(A, B, M, N, K, C, add, add_mask, split_ws, S, stream); break;
+      case 3: launch_split<4, 4, 1, 4, 2>(A, B, M, N, K, C, add, add_mask, split_ws, S, stream); break;
+      case 4: launch_split<2, 2, 2, 2, 4>(A, B, M, N, K, C, add, add_mask, split_ws, S, stream); break;
+      default: launch_split<4, 8, 2, 2, 2>(A, B, M, N, K, C, add, add_mask, split_ws, S, stream); break;
     }
     return;
   }
   GemmPro pro{};
+  pro.amask = add ? add_mask : nullptr;
   if (pro_scale) {
     pro.sc = pro_scale;
     pro.sh = pro_shift;

@@ -87,6 +87,10 @@ S2_FORCE = False        # tests: take the parity-class kernel wherever it fits, 
 # dense GEMMs over [N, P * C] rows with the per-step expanded weight (sconv_nhwc.hip): no out-of-image
 # taps computed (2.25x / 9x of the useful MFMA work on the implicit-GEMM / im2col paths).
 SMALL_CONV = os.environ.get("GARFIELD_SMALL_CONV", "1") == "1"
+# An identity block's residual gradient (dres = dy masked by the last BatchNorm's ReLU) is not written by
+# that BatchNorm's backward when the block's conv1 is a 1x1 GEMM: conv1's data-gradient epilogue adds
+# dy where the forward's ReLU bit is set (gpu_gemm_nt add_mask), saving dres's write and re-read (MaskedGrad).
+LAZY_RES = os.environ.get("GARFIELD_LAZY_RES", "1") == "1"
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -215,10 +219,11 @@ class GradJoin:
     its own output (``addmm_`` for a 1x1 GEMM dgrad, an accumulating col2im for a
     k x k one) and returns the sum. A fresh join is made per forward."""
 
-    __slots__ = ("pending",)
+    __slots__ = ("pending", "lazy")
 
     def __init__(self):
         self.pending = None
+        self.lazy = False     # the other branch folds a MaskedGrad into its GEMM epilogue (set by its forward)
 
     def take(self):
         prev, self.pending = self.pending, None
@@ -228,6 +233,23 @@ class GradJoin:
         if self.pending is not None:
             raise RuntimeError("GradJoin: both branches parked a gradient")
         self.pending = g
+
+
+class MaskedGrad:
+    """dres = dy where the forward ReLU bit is set, else 0, not materialised: dy [N, C, H, W]
+    channels_last and the BatchNorm's bit mask (one byte per 8 elements in dy's memory order)."""
+
+    __slots__ = ("dy", "mask")
+
+    def __init__(self, dy: torch.Tensor, mask: torch.Tensor):
+        self.dy, self.mask = dy, mask
+
+    def materialize(self) -> torch.Tensor:
+        bits = (self.mask.unsqueeze(1) >> torch.arange(8, dtype=torch.uint8, device=self.mask.device)) & 1
+        d2 = rows2d(self.dy)
+        out = torch.where(bits.view(d2.shape).bool(), d2, torch.zeros((), dtype=d2.dtype, device=d2.device))
+        n, _, h, w = self.dy.shape
+        return from_rows(out, n, h, w)
 
 
 # --------------------------------------------------------------------------- #
@@ -392,9 +414,14 @@ class _GroupedBN(torch.autograd.Function):
         dy = _cl(dy)
         x2, dy2 = rows2d(x), rows2d(dy)
         y2 = (y if y.dim() == 1 else rows2d(y)) if y is not None else None
+        lazy = None
         if x.is_cuda:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+            if (ctx.has_res and LAZY_RES and ctx.join is not None and ctx.join.lazy and y2 is not None
+                    and y2.dim() == 1):
+                lazy = MaskedGrad(dy, y2)        # the consumer's GEMM applies the ReLU bits itself
+            dres = torch.empty_like(x, memory_format=torch.channels_last) if (ctx.has_res and lazy is None) \
+                else None
             rg = x2.shape[0] // st.groups
             C_ = _native.native()
             part = ws.get("bn_part", C_.bn_part_floats(rg, st.groups, C), x.device)
@@ -411,7 +438,9 @@ class _GroupedBN(torch.autograd.Function):
             dx2, dr2 = _bn_bwd_ref(x2, dy2, y2, st, ctx.has_res)
             dx = from_rows(dx2, n, h, w)
             dres = from_rows(dr2, n, h, w) if dr2 is not None else None
-        if dres is not None and ctx.join is not None:
+        if lazy is not None:
+            ctx.join.park(lazy)
+        elif dres is not None and ctx.join is not None:
             ctx.join.park(dres)
             dres = None
         return dx, None, None, dres, None, None, None
@@ -625,18 +654,26 @@ def _halo_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", add: torch.
     return _iconv(dy, spec.wd, (3, 3, 1, 1, 1, 1, 1, 1), (dy.shape[2], dy.shape[3]), add)
 
 
-def _gemm_nt_dgrad(dy2: torch.Tensor, w2: torch.Tensor, add: torch.Tensor | None, spec: "ConvSpec | None" = None):
+def _gemm_nt_dgrad(dy2: torch.Tensor, w2: torch.Tensor, add: torch.Tensor | None, spec: "ConvSpec | None" = None,
+                   add_mask: torch.Tensor | None = None):
     """dx = dy2 · w2 (+ add, in place of add) on gemm_nt.hip with the transposed weight (the step's
-    ``spec.wt`` when refreshed, else transposed here); None: use hipBLASLt."""
+    ``spec.wt`` when refreshed, else transposed here); None: use hipBLASLt. ``add_mask``: add is a
+    MaskedGrad's dy, counted where its bit is set, and dx is a new tensor."""
     if not (GEMM_NT and GEMM_NT_DGRAD and dy2.is_cuda and w2.shape[1] % 64 == 0):
         return None
     wt = spec.wt if (spec is not None and spec.wt is not None) else w2.t().contiguous()
     if not _gemm_nt_ok(dy2, wt) or (add is not None and not add.is_contiguous()):
         return None
+    if add_mask is not None and (add is None or add.shape != (dy2.shape[0], wt.shape[0])):
+        return None
     C_ = _native.native()
     cfg = _gemm_cfg(dy2, wt, 0, add)
     if cfg < 0:
         return None
+    if add_mask is not None:
+        out = torch.empty_like(add)
+        C_.gpu_gemm_nt(dy2, wt, out, add, None, 0, cfg, add_mask=add_mask)
+        return out
     out = add if add is not None else torch.empty((dy2.shape[0], wt.shape[0]), dtype=dy2.dtype, device=dy2.device)
     C_.gpu_gemm_nt(dy2, wt, out, add, None, 0, cfg)
     return out
@@ -1187,6 +1224,8 @@ class _GroupedConv(torch.autograd.Function):
         if spec.gemm:
             ctx.mode = "rows"
             ctx.save_for_backward(x, w)
+            if join is not None and x.is_cuda:
+                join.lazy = True                 # the backward's GEMM takes the other branch's MaskedGrad
             y2 = _gemm_nt_forward(rows2d(x), w.reshape(w.shape[0], -1), spec)
             if y2 is None:
                 y2 = torch.mm(rows2d(x), w.reshape(w.shape[0], -1).t())
@@ -1235,6 +1274,8 @@ class _GroupedConv(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         prev = ctx.join.take() if (need_dx and ctx.join is not None) else None
         first = need_dx and ctx.join is not None and prev is None   # park dx for the other branch
+        if isinstance(prev, MaskedGrad) and mode != "rows":
+            prev = prev.materialize()
         if mode == "f32":                        # a = x
             if need_dx:
                 if _stem_shape(w, spec) or _gathered(w):   # a first layer: dx of the input, never wanted in training
@@ -1247,7 +1288,13 @@ class _GroupedConv(torch.autograd.Function):
         elif mode == "rows":                     # a = x
             if need_dx:
                 w2 = w.reshape(cout, -1)
-                if prev is not None:             # the other branch's gradient, folded into the GEMM
+                if isinstance(prev, MaskedGrad):   # dres from dy + the ReLU bits, inside the GEMM epilogue
+                    d2 = _gemm_nt_dgrad(dy2, w2, rows2d(prev.dy), spec, prev.mask)
+                    if d2 is None:
+                        d2 = rows2d(prev.materialize()).addmm_(dy2, w2)
+                    dx = from_rows(d2, n, h, wd)
+                    prev = None
+                elif prev is not None:           # the other branch's gradient, folded into the GEMM
                     p2 = rows2d(_cl(prev))
                     d2 = _gemm_nt_dgrad(dy2, w2, p2, spec)
                     dx = from_rows(d2 if d2 is not None else p2.addmm_(dy2, w2), n, h, wd)

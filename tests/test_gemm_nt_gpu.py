@@ -21,6 +21,9 @@ def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
     b = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
     add = torch.randn(M, N, device=cuda).to(torch.bfloat16)
     ref = a.float() @ b.float().t()
+    mask = torch.randint(0, 256, (M * N // 8,), device=cuda, dtype=torch.uint8)
+    bits = ((mask.unsqueeze(1) >> torch.arange(8, device=cuda, dtype=torch.uint8)) & 1).view(M, N).bool()
+    masked = torch.where(bits, add, torch.zeros((), device=cuda, dtype=torch.bfloat16))
     ran = splits = 0
     for cfg in range(native.gemm_nt_num_cfg()):   # split-K forms included (fp32 slabs + one summing pass)
         if not native.gemm_nt_valid(cfg, N, K):
@@ -31,6 +34,13 @@ def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
         c2 = add.clone()
         native.gpu_gemm_nt(a, b, c2, c2, None, 0, cfg)        # in place: c = a·bᵀ + c
         assert rel(c2, ref + add.float()) < 5e-3, cfg
+        # add_mask: add counts only where its bit is set (the lazily applied ReLU of a residual
+        # gradient): bitwise the GEMM over the materialised masked add
+        c3 = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+        native.gpu_gemm_nt(a, b, c3, add, None, 0, cfg, add_mask=mask)
+        c4 = masked.clone()
+        native.gpu_gemm_nt(a, b, c4, c4, None, 0, cfg)
+        assert torch.equal(c3, c4), cfg
         ran += 1
         splits += native.gemm_nt_splits(cfg) > 1
     assert ran >= 2

@@ -100,3 +100,18 @@ def test_wgrad3x3_split_choice():
         S = _wgrad3x3_splits(rows, (c // 64) * (co // 64) * G)
         assert S == want, (rows, c, co, S)
         assert S <= -(-rows // 128)
+
+
+def test_masked_grad_materialize_applies_bits_in_memory_order():
+    """MaskedGrad (the lazily masked residual gradient): bit i of byte j keeps element 8j + i of dy's
+    channels_last memory order, as the BatchNorm forward writes its ReLU bits."""
+    from garfield_amd.ops.grouped import MaskedGrad, rows2d
+
+    torch.manual_seed(0)
+    dy = torch.randn(2, 16, 3, 5).contiguous(memory_format=torch.channels_last)
+    flat = rows2d(dy).reshape(-1)
+    keep = torch.rand(flat.numel()) > 0.5
+    w = (keep.view(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    out = MaskedGrad(dy, w).materialize()
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(rows2d(out).reshape(-1), torch.where(keep, flat, torch.zeros(())))

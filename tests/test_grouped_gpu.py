@@ -484,6 +484,30 @@ def test_implicit_1x1_weight_gradients_match_gemm_path(cuda, monkeypatch):
         assert rel(b[j], a[j]) < 1e-2, (j, rel(b[j], a[j]))
 
 
+def test_lazy_residual_gradient_is_bitwise_the_materialised_one(cuda, monkeypatch):
+    """LAZY_RES: an identity block's last BatchNorm parks dy + its ReLU bits (MaskedGrad) instead of
+    writing dres, and conv1's data-gradient GEMM applies the bits in its epilogue: the exchange rows
+    equal the materialised-dres step's bit for bit (same fp32 sums, one rounding)."""
+    import garfield_amd.ops.grouped as grouped
+
+    parked = []
+    orig = grouped.MaskedGrad.__init__
+
+    def rec(self, dy, mask):
+        parked.append(1)
+        orig(self, dy, mask)
+
+    monkeypatch.setattr(grouped.MaskedGrad, "__init__", rec)
+    monkeypatch.setattr(grouped, "LAZY_RES", False)
+    _grouped_rows(cuda, "resnet50", 4, 16)          # fills the per-shape tuner caches
+    a = _grouped_rows(cuda, "resnet50", 4, 16)
+    assert not parked
+    monkeypatch.setattr(grouped, "LAZY_RES", True)
+    b = _grouped_rows(cuda, "resnet50", 4, 16)
+    assert len(parked) == 12                         # ResNet-50: 16 blocks, 4 with a projection shortcut
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("flag", ["SMALL_CONV", "S2_DGRAD"])
 def test_dense_small_image_and_stride2_paths_match_implicit_path(cuda, monkeypatch, flag):
     """SMALL_CONV (2x2 / 1x1-image 3x3 layers as dense GEMMs + folded weight gradients) and S2_DGRAD
