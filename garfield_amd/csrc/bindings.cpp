@@ -1999,6 +1999,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("add") = py::none(), py::arg("stats") = py::none(),
         py::arg("rg") = 0, py::arg("cfg") = -1, py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none(),
         py::arg("pro_groups") = 0, py::arg("add_mask") = py::none());
+  m.def("bn_small_ch", &garfield::gpu::bn_small_ch,
+        "Forced channels per workgroup of the single-kernel small-layer BatchNorm (GARFIELD_BN_SMALL_CH: 8, 16, 32; 0 automatic)");
+  m.def("set_bn_small_ch", &garfield::gpu::set_bn_small_ch, py::arg("ch"),
+        "Force the small-layer BatchNorm's channels per workgroup (8, 16 or 32; 0 automatic) for later launches");
   m.def("gemm_nt_pro_ok", [](int64_t cfg, int64_t K, int64_t prg, int64_t groups) {
     return garfield::gpu::gemm_nt_pro_ok(static_cast<int>(cfg), static_cast<int>(K), prg, static_cast<int>(groups));
   }, py::arg("cfg"), py::arg("K"), py::arg("rows_per_worker"), py::arg("groups"),

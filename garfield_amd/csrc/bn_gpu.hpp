@@ -36,6 +36,11 @@ struct RunJobs {
 void bn_running_update(const RunJobs& jobs, hipStream_t stream);
 // True when a layer of rg rows per worker takes the single-kernel small-layer path.
 bool bn_small(int64_t rg);
+// channels per workgroup of the single-kernel small-layer BatchNorm: 8, 16 or 32 forced
+// (GARFIELD_BN_SMALL_CH), 0 automatic (small_ch_for)
+int bn_small_ch();
+void set_bn_small_ch(int ch);
+int small_ch_for(int C, int groups);
 
 // defer_running (small-layer path, and any layer with y null): skip the running-statistics replay; the
 // caller batches it with bn_running_update. y null: statistics and scale / shift only, no apply pass (the

@@ -606,24 +606,39 @@ dim3 apply_grid(int64_t R, int rp) {
 // (L2-resident) rows. No inter-workgroup hand-off; the running statistics are
 // replayed by k_running (one tiny launch, or batched for many layers by the caller).
 constexpr int kSmallRows = 1024;
-constexpr int kSmallThreads = 1024;             // 16 waves per workgroup to hide the load latency
-// Channels per workgroup CH (32): a layer of C channels and k workers runs C / CH x k workgroups,
-// e.g. 64 for CIFAR layer3 (C = 256).
-template <int CH>
+constexpr int kSmallThreads = 1024;             // CH = 32: 16 waves per workgroup to hide the load latency
+// Channels per workgroup CH with T threads: a layer of C channels and k workers runs C / CH x k
+// workgroups. One CU streams only ~24 GB/s (10 B/cycle), so the 64 workgroups of CH = 32 on a 256-channel
+// layer leave three quarters of the chip idle; CH = 8 (T = 256) runs four times as many, each a quarter
+// of the bytes (bn_small_ch(), GARFIELD_BN_SMALL_CH).
+template <int CH, int T>
 struct SmallGeo {
   static constexpr int Vec = CH / 8;                       // 16-byte vectors per row
-  static constexpr int Lanes = kSmallThreads / Vec;        // row lanes
-  static constexpr int Split = kSmallThreads / CH;         // first-stage reduction splits per channel
+  static constexpr int Lanes = T / Vec;                    // row lanes
+  static constexpr int Split = T / CH;                     // first-stage reduction splits per channel
   static constexpr int It = kSmallRows / Lanes;            // rows per thread, held in registers
   static_assert(kSmallRows % Lanes == 0 && Lanes % Split == 0, "small-layer rows must tile the row lanes");
 };
-
-// Sums red[k][lane][c] over the kSmallLanes lanes for both k; result in red[k][0][c].
 template <int CH>
-__device__ __forceinline__ void small_reduce(float (&red)[2][SmallGeo<CH>::Lanes][CH]) {
-  constexpr int kSmallCh = CH, kSmallSplit = SmallGeo<CH>::Split;
+constexpr int small_threads() { return CH == 8 ? 256 : (CH == 16 ? 512 : kSmallThreads); }
+
+// (channel group, worker) of this workgroup: the workgroups that share a 128-byte row segment (8 / CH
+// consecutive channel groups of one worker) get consecutive ids within one XCD's share of the grid
+// (blocks are dealt to the 8 XCDs round-robin), so each segment is fetched into one L2 only
+__device__ __forceinline__ void small_block(int& cg, int& g) {
+  const int ncg = gridDim.x, total = gridDim.x * gridDim.y;
+  const int b = blockIdx.x + blockIdx.y * ncg;
+  const int w = (total % 8 == 0) ? (b % 8) * (total / 8) + b / 8 : b;
+  g = w / ncg;
+  cg = w - g * ncg;
+}
+
+// Sums red[k][lane][c] over the row lanes for both k; result in red[k][0][c].
+template <int CH, int T, int L>
+__device__ __forceinline__ void small_reduce(float (&red)[2][L][CH]) {
+  constexpr int kSmallCh = CH, kSmallSplit = SmallGeo<CH, T>::Split;
   const int c = threadIdx.x % kSmallCh, part = threadIdx.x / kSmallCh;
-  constexpr int per = SmallGeo<CH>::Lanes / kSmallSplit;
+  constexpr int per = SmallGeo<CH, T>::Lanes / kSmallSplit;
   float a = 0.f, b = 0.f;
 #pragma unroll 8
   for (int t = 0; t < per; ++t) { a += red[0][part * per + t][c]; b += red[1][part * per + t][c]; }
@@ -698,25 +713,34 @@ __device__ __forceinline__ Raw8<DT> keep_affine(Raw8<DT> d, const Raw8<DT>& xr, 
 
 // Each thread keeps its (<= kSmallIt) rows of 8 channels in registers as stored (packed
 // bf16 or fp32), so the apply pass does not re-read x (or dy) from memory.
-template <int CH, bool RES, bool RELU, int DT>
-__global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const void* __restrict__ x,
+template <int CH, bool RES, bool RELU, int DT, int T = small_threads<CH>()>
+__global__ __launch_bounds__(T) void k_bn_fwd_small(const void* __restrict__ x,
                                                           const void* __restrict__ res, int64_t rg, int C,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps,
                                                           float* __restrict__ mean, float* __restrict__ istd,
                                                           float* __restrict__ scale, float* __restrict__ shift,
                                                           void* __restrict__ y, uint8_t* __restrict__ mask) {
-  constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH>::Vec, kSmallLanes = SmallGeo<CH>::Lanes,
-                kSmallIt = SmallGeo<CH>::It;
+  constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH, T>::Vec, kSmallLanes = SmallGeo<CH, T>::Lanes,
+                kSmallIt = SmallGeo<CH, T>::It;
   __shared__ float red[2][kSmallLanes][kSmallCh];
   __shared__ float lsc[kSmallCh], lsh[kSmallCh];
   const int tc = threadIdx.x % kSmallVec, tr = threadIdx.x / kSmallVec;
-  const int g = blockIdx.y;
-  const int c0 = blockIdx.x * kSmallCh + tc * 8;
+  int cg, g;
+  small_block(cg, g);
+  const int c0 = cg * kSmallCh + tc * 8;
   const bool act = c0 < C;
   const int64_t base = static_cast<int64_t>(g) * rg;
   float s[8], q[8], sh[8];
   Raw8<DT> xr[kSmallIt];
+  // the finalize thread's operands, loaded now instead of after the reduction (off its critical path)
+  float fg = 1.f, fb = 0.f, fx0 = 0.f;
+  if (threadIdx.x < kSmallCh && cg * kSmallCh + static_cast<int>(threadIdx.x) < C) {
+    const int c = cg * kSmallCh + threadIdx.x;
+    fg = gamma ? gamma[c] : 1.f;
+    fb = beta ? beta[c] : 0.f;
+    fx0 = load_one<DT>(x, base * C + c);
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) { s[i] = 0.f; q[i] = 0.f; sh[i] = 0.f; }
   if (act) {
@@ -739,9 +763,9 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const void* __re
 #pragma unroll
   for (int i = 0; i < 8; ++i) { red[0][tr][tc * 8 + i] = s[i]; red[1][tr][tc * 8 + i] = q[i]; }
   __syncthreads();
-  small_reduce<CH>(red);
+  small_reduce<CH, T, kSmallLanes>(red);
   if (threadIdx.x < kSmallCh) {
-    const int c = blockIdx.x * kSmallCh + threadIdx.x;
+    const int c = cg * kSmallCh + threadIdx.x;
     const float S = red[0][0][threadIdx.x], Q = red[1][0][threadIdx.x];
     float sc = 0.f, sf = 0.f;
     if (c < C) {
@@ -749,13 +773,13 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const void* __re
       const float m1 = S / M;
       float var = Q / M - m1 * m1;
       var = var > 0.f ? var : 0.f;
-      const float mu = load_one<DT>(x, base * C + c) + m1;
+      const float mu = fx0 + m1;
       const float is = rsqrtf(var + eps);
       const int64_t gc = static_cast<int64_t>(g) * C + c;
       mean[gc] = mu;
       istd[gc] = is;
-      sc = (gamma ? gamma[c] : 1.f) * is;
-      sf = (beta ? beta[c] : 0.f) - mu * sc;
+      sc = fg * is;
+      sf = fb - mu * sc;
       scale[gc] = sc;
       shift[gc] = sf;
     }
@@ -796,25 +820,32 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_fwd_small(const void* __re
   }
 }
 
-template <int CH, int RM, bool RES_OUT, int DT>
-__global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
+template <int CH, int RM, bool RES_OUT, int DT, int T = small_threads<CH>()>
+__global__ __launch_bounds__(T) void k_bn_bwd_small(
     const void* __restrict__ x, const void* __restrict__ dy, const void* __restrict__ y,
     const uint8_t* __restrict__ mask, int64_t rg, int C, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ istd, void* __restrict__ dx,
     void* __restrict__ dres, void* grow, int grow_dt, int64_t row_stride, int64_t off_gamma, int64_t off_beta,
     const float* __restrict__ rsc, const float* __restrict__ rsh) {
-  constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH>::Vec, kSmallLanes = SmallGeo<CH>::Lanes,
-                kSmallIt = SmallGeo<CH>::It;
+  constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH, T>::Vec, kSmallLanes = SmallGeo<CH, T>::Lanes,
+                kSmallIt = SmallGeo<CH, T>::It;
   __shared__ float red[2][kSmallLanes][kSmallCh];
   __shared__ float la[kSmallCh], lb[kSmallCh], lc[kSmallCh];
   const int tc = threadIdx.x % kSmallVec, tr = threadIdx.x / kSmallVec;
-  const int g = blockIdx.y;
-  const int c0 = blockIdx.x * kSmallCh + tc * 8;
+  int cg, g;
+  small_block(cg, g);
+  const int c0 = cg * kSmallCh + tc * 8;
   const bool act = c0 < C;
   const int64_t base = static_cast<int64_t>(g) * rg;
   // dz = dy masked by the forward ReLU, kept as stored in registers with x
   Raw8<DT> xr[kSmallIt], dr[kSmallIt];
   float A[8], B[8], mu[8], rs[8] = {}, rf[8] = {};
+  float fis = 0.f, fg = 1.f;   // the finalize thread's operands, loaded before the reduction
+  if (threadIdx.x < kSmallCh && cg * kSmallCh + static_cast<int>(threadIdx.x) < C) {
+    const int c = cg * kSmallCh + threadIdx.x;
+    fis = istd[static_cast<int64_t>(g) * C + c];
+    fg = gamma ? gamma[c] : 1.f;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) { A[i] = 0.f; B[i] = 0.f; mu[i] = 0.f; }
   if (act) {
@@ -850,20 +881,20 @@ __global__ __launch_bounds__(kSmallThreads) void k_bn_bwd_small(
 #pragma unroll
   for (int i = 0; i < 8; ++i) { red[0][tr][tc * 8 + i] = A[i]; red[1][tr][tc * 8 + i] = B[i]; }
   __syncthreads();
-  small_reduce<CH>(red);
+  small_reduce<CH, T, kSmallLanes>(red);
   if (threadIdx.x < kSmallCh) {
-    const int c = blockIdx.x * kSmallCh + threadIdx.x;
+    const int c = cg * kSmallCh + threadIdx.x;
     const float SA = red[0][0][threadIdx.x], SB = red[1][0][threadIdx.x];
     float ca = 0.f, cb = 0.f, cc = 0.f;
     if (c < C) {
       const float M = static_cast<float>(rg);
-      const float is = istd[static_cast<int64_t>(g) * C + c];
+      const float is = fis;
       const float dgamma = SB * is, dbeta = SA;
       if (grow) {
         if (off_gamma >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_gamma + c, dgamma);
         if (off_beta >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + off_beta + c, dbeta);
       }
-      ca = (gamma ? gamma[c] : 1.f) * is;
+      ca = fg * is;
       cb = dbeta / M;
       cc = dgamma / M * is;
     }
@@ -916,11 +947,11 @@ void launch_fwd_small(const void* x, const void* res, int64_t rg, int groups, in
                       bool relu, uint8_t* mask, hipStream_t stream) {
   const dim3 sgrid((C + CH - 1) / CH, groups);
   if (res) {
-    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, true, true, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
-    else hipLaunchKernelGGL((k_bn_fwd_small<CH, true, false, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, true, true, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
+    else hipLaunchKernelGGL((k_bn_fwd_small<CH, true, false, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
   } else {
-    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, false, true, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
-    else hipLaunchKernelGGL((k_bn_fwd_small<CH, false, false, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, false, true, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
+    else hipLaunchKernelGGL((k_bn_fwd_small<CH, false, false, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
   }
 }
 
@@ -931,7 +962,7 @@ void launch_bwd_small(const void* x, const void* dy, const void* y, const uint8_
                       int rm, hipStream_t stream, const float* rsc, const float* rsh) {
   const dim3 sgrid((C + CH - 1) / CH, groups);
 #define GARFIELD_BWD_SMALL(RMV, RESV)                                                                           \
-  hipLaunchKernelGGL((k_bn_bwd_small<CH, RMV, RESV, DT>), sgrid, dim3(kSmallThreads), 0, stream, x, dy, y, mask, rg, C, \
+  hipLaunchKernelGGL((k_bn_bwd_small<CH, RMV, RESV, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, dy, y, mask, rg, C, \
                      gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rsc, rsh)
   if (rm == 3) { if (dres) GARFIELD_BWD_SMALL(3, true); else GARFIELD_BWD_SMALL(3, false); }
   else if (rm == 2) { if (dres) GARFIELD_BWD_SMALL(2, true); else GARFIELD_BWD_SMALL(2, false); }
@@ -946,8 +977,11 @@ void forward_dt(const void* x, const void* res, int64_t rg, int groups, int C, c
                 float* mean, float* istd, float* scale, float* shift, void* y, bool relu, uint8_t* mask,
                 bool defer_running, hipStream_t stream, const float* tile_stats, int64_t tile_m, int tile_e) {
   if (rg <= kSmallRows && tile_stats == nullptr) {
-    // 32 channels per workgroup (16 / 64 measured slower: profiles/r2/bn_small_ch_sweep.log)
-    launch_fwd_small<32, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream);
+    switch (small_ch_for(C, groups)) {
+      case 8: launch_fwd_small<8, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream); break;
+      case 16: launch_fwd_small<16, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream); break;
+      default: launch_fwd_small<32, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream); break;
+    }
     if (run_mean && !defer_running) {
       RunJobs jobs{};
       jobs.j[0] = RunJob{mean, istd, run_mean, run_var, rg, C, groups, eps, momentum};
@@ -997,8 +1031,11 @@ void backward_dt(const void* x, const void* dy, const void* y, const uint8_t* ma
                  hipStream_t stream, const float* rsc, const float* rsh) {
   const int rm = mask ? 2 : (y ? 1 : (rsc ? 3 : 0));
   if (rg <= kSmallRows) {
-    launch_bwd_small<32, DT>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride,
-                             off_gamma, off_beta, rm, stream, rsc, rsh);
+    switch (small_ch_for(C, groups)) {
+      case 8: launch_bwd_small<8, DT>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream, rsc, rsh); break;
+      case 16: launch_bwd_small<16, DT>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream, rsc, rsh); break;
+      default: launch_bwd_small<32, DT>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, dx, dres, grow, grow_dt, row_stride, off_gamma, off_beta, rm, stream, rsc, rsh); break;
+    }
     return;
   }
   const Geo g = geometry(rg, groups, C);
@@ -1067,6 +1104,29 @@ void bn_running_update(const RunJobs& jobs, hipStream_t stream) {
 }
 
 bool bn_small(int64_t rg) { return rg <= kSmallRows; }
+
+namespace {
+int g_small_ch = -1;
+}
+int bn_small_ch() {
+  if (g_small_ch < 0) {
+    const char* e = std::getenv("GARFIELD_BN_SMALL_CH");
+    const int v = e ? std::atoi(e) : 0;
+    g_small_ch = (v == 8 || v == 16 || v == 32) ? v : 0;
+  }
+  return g_small_ch;
+}
+void set_bn_small_ch(int ch) { g_small_ch = (ch == 8 || ch == 16 || ch == 32) ? ch : 0; }
+// 0 (automatic): the widest CH whose grid has >= 256 workgroups (one per CU), else 8. ResNet-50 CIFAR,
+// 8 workers: 256-channel layers run CH = 8 (9.8 -> 7.2 µs forward), 1024 / 2048-channel ones CH = 32
+// (18.4 vs 21.4 µs with CH = 8) (profiles/r5/bn_small_ch/)
+int small_ch_for(int C, int groups) {
+  const int forced = bn_small_ch();
+  if (forced) return forced;
+  for (int ch : {32, 16})
+    if (static_cast<int64_t>((C + ch - 1) / ch) * groups >= 256) return ch;
+  return 8;
+}
 
 }  // namespace gpu
 }  // namespace garfield

@@ -35,9 +35,20 @@ def _bn_ref_group(xg, gamma, beta, eps, rg, relu):
                                               (4, 32, 8, 64, True, True), (2, 20, 10, 192, True, False),
                                               (3, 17, 9, 520, True, True)])
 @pytest.mark.parametrize("defer", [False, True])
-def test_bn_kernels_match_fp32_reference(cuda, G, B, H, C, relu, res, defer):
+@pytest.mark.parametrize("small_ch", [8, 16, 32])
+def test_bn_kernels_match_fp32_reference(cuda, native, G, B, H, C, relu, res, defer, small_ch):
     """Grouped BatchNorm forward + backward against an fp32 autograd reference per worker, on the
-    single-kernel small path (<= 1024 rows per worker) and the large path."""
+    single-kernel small path (<= 1024 rows per worker; 8, 16 or 32 channels per workgroup) and the
+    large path."""
+    prev = native.bn_small_ch()
+    native.set_bn_small_ch(small_ch)
+    try:
+        _bn_kernels_case(cuda, G, B, H, C, relu, res, defer)
+    finally:
+        native.set_bn_small_ch(prev)
+
+
+def _bn_kernels_case(cuda, G, B, H, C, relu, res, defer):
     torch.manual_seed(C + G)
     N = G * B
     x = (torch.randn(N, C, H, H, device=cuda) * 2 + 0.5).to(torch.bfloat16)
