@@ -108,6 +108,45 @@ __device__ __forceinline__ void relu_mask8(float (&d)[8], const float (&a)[8], c
   }
 }
 
+// 8 channels of one row as stored: packed bf16 (one uint4) or fp32 (two float4)
+struct F8 {
+  float4 a, b;
+};
+template <int DT>
+using Raw8 = typename std::conditional<DT == kF32, F8, uint4>::type;
+
+template <int DT>
+__device__ __forceinline__ Raw8<DT> ld_raw8(const void* p, int64_t off) {
+  if constexpr (DT == kF32) {
+    const float* f = static_cast<const float*>(p) + off;
+    return F8{*reinterpret_cast<const float4*>(f), *reinterpret_cast<const float4*>(f + 4)};
+  } else {
+    return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + off);
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void st_raw8(void* p, int64_t off, const Raw8<DT>& r) {
+  if constexpr (DT == kF32) {
+    float* f = static_cast<float*>(p) + off;
+    *reinterpret_cast<float4*>(f) = r.a;
+    *reinterpret_cast<float4*>(f + 4) = r.b;
+  } else {
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + off) = r;
+  }
+}
+
+__device__ __forceinline__ void unpack8(const uint4 u, float (&v)[8]) {
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ void unpack8(const F8& u, float (&v)[8]) {
+  v[0] = u.a.x; v[1] = u.a.y; v[2] = u.a.z; v[3] = u.a.w;
+  v[4] = u.b.x; v[5] = u.b.y; v[6] = u.b.z; v[7] = u.b.w;
+}
+
 // Partial per-(group, channel) sums over one row chunk.
 //   forward : s = Σ (x - shift), q = Σ (x - shift)^2  with shift = x[first row of the group]
 //             (shifted sums: no catastrophic cancellation when |mean| >> std)
@@ -145,29 +184,59 @@ __global__ __launch_bounds__(kThreads) void k_partial(const void* __restrict__ x
       load8f(rsh + static_cast<int64_t>(g) * C + c0, rf);
     }
     int64_t r = r0 + tr;
-    // two rows in flight per lane
-    for (; r + geo.rp < r1; r += 2 * geo.rp) {
-      const int64_t o0 = (base + r) * C + c0, o1 = o0 + static_cast<int64_t>(geo.rp) * C;
-      float a0[8], a1[8];
-      load8<DT>(x, o0, a0);
-      load8<DT>(x, o1, a1);
-      if constexpr (BWD) {
-        float d0[8], d1[8];
-        load8<DT>(dy, o0, d0);
-        load8<DT>(dy, o1, d1);
-        relu_mask8<RM, DT>(d0, a0, y, mask, o0, rs, rf);
-        relu_mask8<RM, DT>(d1, a1, y, mask, o1, rs, rf);
+    if constexpr (!BWD || RM != 0) {
+      // two rows in flight per lane, unpacked as loaded (for these forms hipcc keeps this loop's loads
+      // in one batch but serialises a four-row raw batch, checked in the ISA)
+      for (; r + geo.rp < r1; r += 2 * geo.rp) {
+        const int64_t o0 = (base + r) * C + c0, o1 = o0 + static_cast<int64_t>(geo.rp) * C;
+        float a0[8], a1[8];
+        load8<DT>(x, o0, a0);
+        load8<DT>(x, o1, a1);
+        if constexpr (BWD) {
+          float d0[8], d1[8];
+          load8<DT>(dy, o0, d0);
+          load8<DT>(dy, o1, d1);
+          relu_mask8<RM, DT>(d0, a0, y, mask, o0, rs, rf);
+          relu_mask8<RM, DT>(d1, a1, y, mask, o1, rs, rf);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          s[i] += d0[i] + d1[i];
-          q[i] += d0[i] * (a0[i] - sh[i]) + d1[i] * (a1[i] - sh[i]);
+          for (int i = 0; i < 8; ++i) {
+            s[i] += d0[i] + d1[i];
+            q[i] += d0[i] * (a0[i] - sh[i]) + d1[i] * (a1[i] - sh[i]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float e0 = a0[i] - sh[i], e1 = a1[i] - sh[i];
+            s[i] += e0 + e1;
+            q[i] += e0 * e0 + e1 * e1;
+          }
         }
-      } else {
+      }
+    } else {   // the backward without a ReLU mask
+      // four rows in flight per lane: every load of the batch issued before the first use
+      constexpr int RB = 4;
+      static_assert(BWD, "the forward keeps the two-row loop");
+      for (; r + (RB - 1) * geo.rp < r1; r += RB * geo.rp) {
+        Raw8<DT> xa[RB], da[RB];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float e0 = a0[i] - sh[i], e1 = a1[i] - sh[i];
-          s[i] += e0 + e1;
-          q[i] += e0 * e0 + e1 * e1;
+        for (int k = 0; k < RB; ++k) {
+          const int64_t o = (base + r + static_cast<int64_t>(k) * geo.rp) * C + c0;
+          xa[k] = ld_raw8<DT>(x, o);
+          if constexpr (BWD) da[k] = ld_raw8<DT>(dy, o);
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+          float a0[8];
+          unpack8(xa[k], a0);
+          if constexpr (BWD) {
+            float d0[8];
+            unpack8(da[k], d0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { s[i] += d0[i]; q[i] += d0[i] * (a0[i] - sh[i]); }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { const float e = a0[i] - sh[i]; s[i] += e; q[i] += e * e; }
+          }
         }
       }
     }
@@ -197,11 +266,26 @@ __global__ __launch_bounds__(kThreads) void k_partial(const void* __restrict__ x
     *reinterpret_cast<float4*>(p1 + 4) = make_float4(q[4], q[5], q[6], q[7]);
   }
   __syncthreads();
+  // row lanes summed by all threads: nparts = 256 / cb threads per channel (cb < 256), each over
+  // every nparts-th lane row, then the parts (in the free tail of red) by one thread per channel
+  const int nparts = geo.cb < kThreads ? kThreads / geo.cb : 1;
+  if (nparts > 1) {
+    const int c = threadIdx.x % geo.cb, pt = threadIdx.x / geo.cb;
+    float a = 0.f, b = 0.f;
+    for (int t = pt; t < geo.rp; t += nparts) { a += red[0][t * geo.cb + c]; b += red[1][t * geo.cb + c]; }
+    __syncthreads();
+    if (pt < nparts) {   // (256 % cb threads left over when cb does not divide 256)
+      red[0][pt * geo.cb + c] = a;
+      red[1][pt * geo.cb + c] = b;
+    }
+    __syncthreads();
+  }
+  const int rows = nparts > 1 ? nparts : geo.rp;
   for (int c = threadIdx.x; c < geo.cb; c += kThreads) {
     const int cc = cbk * geo.cb + c;
     if (cc >= C) continue;
     float a = 0.f, b = 0.f;
-    for (int t = 0; t < geo.rp; ++t) { a += red[0][t * geo.cb + c]; b += red[1][t * geo.cb + c]; }
+    for (int t = 0; t < rows; ++t) { a += red[0][t * geo.cb + c]; b += red[1][t * geo.cb + c]; }
     const int64_t o = (static_cast<int64_t>(g) * geo.chunks + chunk) * 2 * C;
     part[o + cc] = a;
     part[o + C + cc] = b;
@@ -298,45 +382,6 @@ __device__ __forceinline__ void running_update(const float* __restrict__ mean, c
     run_mean[c] = rm;
     run_var[c] = rv;
   }
-}
-
-// 8 channels of one row as stored: packed bf16 (one uint4) or fp32 (two float4)
-struct F8 {
-  float4 a, b;
-};
-template <int DT>
-using Raw8 = typename std::conditional<DT == kF32, F8, uint4>::type;
-
-template <int DT>
-__device__ __forceinline__ Raw8<DT> ld_raw8(const void* p, int64_t off) {
-  if constexpr (DT == kF32) {
-    const float* f = static_cast<const float*>(p) + off;
-    return F8{*reinterpret_cast<const float4*>(f), *reinterpret_cast<const float4*>(f + 4)};
-  } else {
-    return *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(p) + off);
-  }
-}
-
-template <int DT>
-__device__ __forceinline__ void st_raw8(void* p, int64_t off, const Raw8<DT>& r) {
-  if constexpr (DT == kF32) {
-    float* f = static_cast<float*>(p) + off;
-    *reinterpret_cast<float4*>(f) = r.a;
-    *reinterpret_cast<float4*>(f + 4) = r.b;
-  } else {
-    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(p) + off) = r;
-  }
-}
-
-__device__ __forceinline__ void unpack8(const uint4 u, float (&v)[8]) {
-  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
-  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
-  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
-  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
-}
-__device__ __forceinline__ void unpack8(const F8& u, float (&v)[8]) {
-  v[0] = u.a.x; v[1] = u.a.y; v[2] = u.a.z; v[3] = u.a.w;
-  v[4] = u.b.x; v[5] = u.b.y; v[6] = u.b.z; v[7] = u.b.w;
 }
 
 // Elementwise passes over [R, C]: each workgroup owns kApplyIters x rp rows.

@@ -250,7 +250,8 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
 #pragma unroll
   for (int u = 0; u < WI; ++u) {
     const int row = (wave * WI + u) * 8 + lrow;
-    if constexpr (TW) wsrc[u] = w + static_cast<int64_t>(row) * KF + co0 + lchunk * 8;
+    // TW: the transposed fragment reads' bank swizzle (tr_g): row r's 16-byte chunks XOR 2 tr_g(r)
+    if constexpr (TW) wsrc[u] = w + static_cast<int64_t>(row) * KF + co0 + (lchunk ^ (2 * tr_g(row))) * 8;
     else wsrc[u] = w + static_cast<int64_t>(co0 + row) * K + (lchunk ^ (row & 7)) * 8;
   }
   const uint16_t* zsrc = reinterpret_cast<const uint16_t*>(g_iconv_zero) + lchunk * 8;
@@ -317,31 +318,36 @@ __global__ __launch_bounds__(256) void k_iconv_lds(const uint16_t* __restrict__ 
     s16x4 tr[TW ? 16 : 1];
     if constexpr (TW) {
       // A fragments of both 32-deep halves: lane (group grp, 4q+p) reads W-tile row
-      // 32*ks + 8*grp + 4h + q, columns 16c + 4p .. +3 (inline asm: see k_iwgrad)
-      const uint32_t ab = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)base)) + XB +
-                          (8 * (lane >> 4) + ((lane & 15) >> 2)) * 128 + 8 * (lane & 3);
+      // 32*ks + 8*grp + 4h + q, columns 16c + 4p .. +3 (inline asm: see k_iwgrad); column block c
+      // of that row is stored at block c ^ tr_g(8*grp + q) (the staging's swizzle: no 4-way conflicts
+      // between rows 0, 2, 8, 10 of a half-wave)
+      const int tq = 8 * (lane >> 4) + ((lane & 15) >> 2), tg = tr_g(tq);
+      const uint32_t ab = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr)base)) + XB + tq * 128 +
+                          8 * (lane & 3);
+      const uint32_t a0 = ab + 32 * (0 ^ tg), a1 = ab + 32 * (1 ^ tg), a2 = ab + 32 * (2 ^ tg),
+                     a3 = ab + 32 * (3 ^ tg);
       asm volatile(
             "ds_read_b64_tr_b16 %0, %16 offset:0\n\t"
             "ds_read_b64_tr_b16 %1, %16 offset:512\n\t"
-            "ds_read_b64_tr_b16 %2, %16 offset:32\n\t"
-            "ds_read_b64_tr_b16 %3, %16 offset:544\n\t"
-            "ds_read_b64_tr_b16 %4, %16 offset:64\n\t"
-            "ds_read_b64_tr_b16 %5, %16 offset:576\n\t"
-            "ds_read_b64_tr_b16 %6, %16 offset:96\n\t"
-            "ds_read_b64_tr_b16 %7, %16 offset:608\n\t"
+            "ds_read_b64_tr_b16 %2, %17 offset:0\n\t"
+            "ds_read_b64_tr_b16 %3, %17 offset:512\n\t"
+            "ds_read_b64_tr_b16 %4, %18 offset:0\n\t"
+            "ds_read_b64_tr_b16 %5, %18 offset:512\n\t"
+            "ds_read_b64_tr_b16 %6, %19 offset:0\n\t"
+            "ds_read_b64_tr_b16 %7, %19 offset:512\n\t"
             "ds_read_b64_tr_b16 %8, %16 offset:4096\n\t"
             "ds_read_b64_tr_b16 %9, %16 offset:4608\n\t"
-            "ds_read_b64_tr_b16 %10, %16 offset:4128\n\t"
-            "ds_read_b64_tr_b16 %11, %16 offset:4640\n\t"
-            "ds_read_b64_tr_b16 %12, %16 offset:4160\n\t"
-            "ds_read_b64_tr_b16 %13, %16 offset:4672\n\t"
-            "ds_read_b64_tr_b16 %14, %16 offset:4192\n\t"
-            "ds_read_b64_tr_b16 %15, %16 offset:4704\n\t"
+            "ds_read_b64_tr_b16 %10, %17 offset:4096\n\t"
+            "ds_read_b64_tr_b16 %11, %17 offset:4608\n\t"
+            "ds_read_b64_tr_b16 %12, %18 offset:4096\n\t"
+            "ds_read_b64_tr_b16 %13, %18 offset:4608\n\t"
+            "ds_read_b64_tr_b16 %14, %19 offset:4096\n\t"
+            "ds_read_b64_tr_b16 %15, %19 offset:4608\n\t"
             "s_waitcnt lgkmcnt(0)"
           : "=&v"(tr[0]), "=&v"(tr[1]), "=&v"(tr[2]), "=&v"(tr[3]), "=&v"(tr[4]), "=&v"(tr[5]), "=&v"(tr[6]),
             "=&v"(tr[7]), "=&v"(tr[8]), "=&v"(tr[9]), "=&v"(tr[10]), "=&v"(tr[11]), "=&v"(tr[12]), "=&v"(tr[13]),
             "=&v"(tr[14]), "=&v"(tr[15])
-          : "v"(ab)
+          : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
           : "memory");
     }
 #pragma unroll
