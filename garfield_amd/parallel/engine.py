@@ -24,6 +24,7 @@ Byzantine workers are simulated per global slot (``byzantine={slot: attack}``).
 from __future__ import annotations
 
 import contextlib
+import gc
 import math
 import os
 from dataclasses import dataclass, field
@@ -74,6 +75,22 @@ FP32_GROUPED = os.environ.get("GARFIELD_FP32_GROUPED", "1")
 # sharded steps with a comm stream: the grouped step captured as stages cut at the bucket boundaries,
 # so the next forward's early layers run beside the late buckets' updates / all-gathers ("0": one graph)
 STAGE_FORWARD = os.environ.get("GARFIELD_STAGE_FORWARD", "1") != "0"
+
+
+@contextlib.contextmanager
+def _capture_guard():
+    """No cyclic garbage collection while HIP graphs are captured: a dead cycle holding a previous
+    engine's graphs or events (freed by the collector at an arbitrary allocation) would destroy them
+    in the middle of this capture (torch 2.10's torch.cuda.graph no longer collects first). Dead
+    cycles are collected once before the capture instead."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 @dataclass
@@ -943,17 +960,18 @@ class RobustDataParallel:
                 # forward: the next step's early layers need not wait for the late buckets' updates
                 graphs, pool, stages = [], None, self._gexec.run_stages(self._gx, self._gy, self._gloss)
                 done = False
-                while not done:
-                    g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode=mode):
-                        done = next(stages, None) is None
-                    graphs.append(g)
-                    pool = g.pool()
+                with _capture_guard():
+                    while not done:
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode=mode):
+                            done = next(stages, None) is None
+                        graphs.append(g)
+                        pool = g.pool()
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 self._ggraph = graphs
             else:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
+                with _capture_guard(), torch.cuda.graph(g, stream=s, capture_error_mode=mode):
                     self._gexec.run(self._gx, self._gy, self._gloss)
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 self._ggraph = g
@@ -1015,7 +1033,7 @@ class RobustDataParallel:
             for j in self.local_slots:
                 g = torch.cuda.CUDAGraph()
                 mode = "thread_local" if self.world > 1 else "global"  # RCCL watchdog thread
-                with torch.cuda.graph(g, stream=s, pool=pool, capture_error_mode=mode):
+                with _capture_guard(), torch.cuda.graph(g, stream=s, pool=pool, capture_error_mode=mode):
                     x, y = self._static[j]
                     self._worker_body(j, x, y, self._static_loss[j])
                 if pool is None and shared:
