@@ -429,7 +429,7 @@ void g_xent_forward(const at::Tensor& logits, const at::Tensor& labels, int64_t 
   TORCH_CHECK(xent_dtype(dlogits, "dlogits") == dt && dlogits.sizes() == logits.sizes(), "gpu_xent: dlogits shape/dtype");
   const int64_t N = logits.size(0), nc = logits.size(1);
   TORCH_CHECK(groups > 0 && N % groups == 0, "gpu_xent: rows not divisible into groups");
-  TORCH_CHECK(nc >= 1 && nc <= garfield::gpu::kXentMaxClasses, "gpu_xent: 1..", garfield::gpu::kXentMaxClasses, " classes");
+  TORCH_CHECK(nc >= 1, "gpu_xent: at least one class");
   TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == N,
               "gpu_xent: labels must be a contiguous int64 GPU tensor of N entries");
   TORCH_CHECK(loss.is_cuda() && loss.scalar_type() == at::kFloat && loss.is_contiguous() && loss.numel() == groups,
@@ -437,8 +437,20 @@ void g_xent_forward(const at::Tensor& logits, const at::Tensor& labels, int64_t 
   const auto dev = logits.device();
   TORCH_CHECK(labels.device() == dev && loss.device() == dev && dlogits.device() == dev, "gpu_xent: one device");
   c10::hip::HIPGuard guard(dev.index());
+  at::Tensor rowloss;   // wide heads: per-row losses (caching allocator: graph-capture safe)
+  if (nc > garfield::gpu::kXentMaxClasses) rowloss = at::empty({N}, logits.options().dtype(at::kFloat));
   garfield::gpu::xent_forward(logits.data_ptr(), dt, labels.data_ptr<int64_t>(), N / groups, static_cast<int>(groups),
-                              static_cast<int>(nc), loss.data_ptr<float>(), dlogits.data_ptr(), stream_of(dev));
+                              static_cast<int>(nc), loss.data_ptr<float>(), dlogits.data_ptr(), stream_of(dev),
+                              rowloss.defined() ? rowloss.data_ptr<float>() : nullptr);
+}
+
+at::Tensor g_mean_f32(const at::Tensor& x) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous() && x.numel() >= 1,
+              "gpu_mean_f32: a non-empty contiguous fp32 GPU tensor");
+  c10::hip::HIPGuard guard(x.device().index());
+  at::Tensor out = at::empty({}, x.options());
+  garfield::gpu::mean_f32(x.data_ptr<float>(), x.numel(), out.data_ptr<float>(), stream_of(x.device()));
+  return out;
 }
 
 void g_xent_backward(const at::Tensor& dlogits, const at::Tensor& grad_loss, int64_t groups, const at::Tensor& dx) {
@@ -1919,8 +1931,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_bn_running_update", &g_bn_running_update,
         "Replay the per-worker running-statistics updates of several layers in one launch; args (jobs) with "
         "jobs = [(mean, istd, running_mean, running_var, rows_per_worker, eps, momentum), ...]");
+  m.def("gpu_mean_f32", &g_mean_f32, py::arg("x"),
+        "0-d fp32 mean of a contiguous fp32 GPU tensor (one workgroup, fixed summation order)");
   m.def("gpu_xent_forward", &g_xent_forward,
-        "Per-worker mean cross-entropy of [groups*rows, nc] logits (nc <= 64) and d(loss_g)/d(logits); args "
+        "Per-worker mean cross-entropy of [groups*rows, nc] logits (nc <= 64: one thread per row; wider: one wave "
+        "per row) and d(loss_g)/d(logits); args "
         "(logits, labels, groups, loss[groups] fp32, dlogits like logits)");
   m.def("gpu_xent_backward", &g_xent_backward,
         "dx = dlogits scaled row-wise by the upstream per-worker loss gradient; args (dlogits, grad_loss, groups, dx)");
@@ -2190,6 +2205,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                      rows.data_ptr(), dtype_code(rows), row_stride, off_w, off_b, stream_of(dev));
   }, py::arg("x"), py::arg("dl"), py::arg("groups"), py::arg("rows"), py::arg("row_stride"), py::arg("off_w"),
      py::arg("off_b"), "Per-worker bf16 classifier dW / db (fp32 sums, one rounding) written into the exchange rows");
+  m.def("gpu_linear_bias_grad", [](const at::Tensor& dl, int64_t groups, const at::Tensor& rows, int64_t row_stride,
+                                    int64_t off_b) {
+    const auto dev = dl.device();
+    TORCH_CHECK(dl.is_cuda() && dl.dim() == 2 && dl.is_contiguous() &&
+                    (dl.scalar_type() == at::kBFloat16 || dl.scalar_type() == at::kFloat),
+                "gpu_linear_bias_grad: dl must be a contiguous 2-D bf16 / fp32 GPU tensor");
+    const int64_t R = dl.size(0), O = dl.size(1);
+    TORCH_CHECK(groups >= 1 && R % groups == 0, "gpu_linear_bias_grad: rows do not split into groups");
+    TORCH_CHECK(rows.is_cuda() && rows.device() == dev && rows.is_contiguous() &&
+                    (rows.scalar_type() == at::kFloat || rows.scalar_type() == at::kBFloat16 ||
+                     rows.scalar_type() == at::kHalf),
+                "gpu_linear_bias_grad: rows must be a contiguous fp32 / bf16 / fp16 exchange buffer");
+    TORCH_CHECK(off_b >= 0 && row_stride >= 0 && (groups - 1) * row_stride + off_b + O <= rows.numel(),
+                "gpu_linear_bias_grad: row offsets out of bounds");
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::linear_bias_grad(dl.data_ptr(), dl.scalar_type() == at::kFloat, static_cast<int>(groups),
+                                    static_cast<int>(R / groups), static_cast<int>(O), rows.data_ptr(),
+                                    dtype_code(rows), row_stride, off_b, stream_of(dev));
+  }, py::arg("dl"), py::arg("groups"), py::arg("rows"), py::arg("row_stride"), py::arg("off_b"),
+     "Per-worker classifier bias gradient db_g[o] = sum of worker g's dl rows (fp32 sums), written into the exchange rows");
   m.def("gpu_avgpool_f32", [](const at::Tensor& x, const at::Tensor& y, bool backward) {
     // forward: x [N, C, H, W] channels_last -> y [N, C]; backward: x = dy [N, C] -> y = dx [N, C, H, W]
     const at::Tensor& big = backward ? y : x;

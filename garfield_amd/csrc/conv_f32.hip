@@ -939,6 +939,19 @@ __global__ __launch_bounds__(256) void k_linear_wgrad(const T* __restrict__ x, c
     store_one(out, odt, og + off_b + threadIdx.x, s);
   }
 }
+// db_g[o] for a wide head (the ImageNet classifier's 1000 outputs): one thread per output, the rows of
+// the worker read coalesced across the threads
+template <typename T>
+__global__ __launch_bounds__(256) void k_linear_bias_grad(const T* __restrict__ dl, int rg, int O, void* __restrict__ out,
+                                                          int odt, int64_t row_stride, int64_t off_b) {
+  const int g = blockIdx.y;
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= O) return;
+  const T* dg = dl + static_cast<int64_t>(g) * rg * O;
+  float s = 0.f;
+  for (int r = 0; r < rg; ++r) s += lin_ld(dg, static_cast<int64_t>(r) * O + o);
+  store_one(out, odt, static_cast<int64_t>(g) * row_stride + off_b + o, s);
+}
 // ---- bf16 classifier with 16-byte operand loads (F % 8 == 0, O <= kLinV) ------------------------
 // The step's classifier is [2000 x 2048] x [2048 x 10]: ~0.1 GFLOP and 8 MB of activations, so it is
 // an HBM stream, not a GEMM: each lane holds 8 consecutive features of a row (one 16-byte load), the
@@ -1333,6 +1346,17 @@ void linear_bf16_dgrad(const uint16_t* dl, const uint16_t* w, int R, int F, int 
     return;
   }
   hipLaunchKernelGGL(k_linear_dgrad<uint16_t>, dim3(blocks_for(items)), dim3(256), 0, stream, dl, w, R, F, O, dx);
+}
+
+void linear_bias_grad(const void* dl, bool dl_f32, int groups, int rg, int O, void* out, int odt, int64_t row_stride,
+                      int64_t off_b, hipStream_t stream) {
+  const dim3 grid((O + 255) / 256, groups);
+  if (dl_f32)
+    hipLaunchKernelGGL(k_linear_bias_grad<float>, grid, dim3(256), 0, stream, static_cast<const float*>(dl), rg, O, out,
+                       odt, row_stride, off_b);
+  else
+    hipLaunchKernelGGL(k_linear_bias_grad<uint16_t>, grid, dim3(256), 0, stream, static_cast<const uint16_t*>(dl), rg,
+                       O, out, odt, row_stride, off_b);
 }
 
 void linear_bf16_wgrad(const uint16_t* x, const uint16_t* dl, int groups, int rg, int F, int O, void* out, int odt,

@@ -57,6 +57,9 @@ void linear_f32_wgrad(const float* x, const float* dl, int groups, int rg, int F
 void linear_bf16_fwd(const uint16_t* x, const uint16_t* w, const uint16_t* b, int R, int F, int O, uint16_t* y,
                      hipStream_t stream);
 void linear_bf16_dgrad(const uint16_t* dl, const uint16_t* w, int R, int F, int O, uint16_t* dx, hipStream_t stream);
+// db_g[o] = Σ_{r in worker g} dl[r][o] (dl bf16 or fp32), into worker g's exchange row at off_b
+void linear_bias_grad(const void* dl, bool dl_f32, int groups, int rg, int O, void* out, int odt, int64_t row_stride,
+                      int64_t off_b, hipStream_t stream);
 void linear_bf16_wgrad(const uint16_t* x, const uint16_t* dl, int groups, int rg, int F, int O, void* out, int odt,
                        int64_t row_stride, int64_t off_w, int64_t off_b, hipStream_t stream);
 void avgpool_bf16_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t stream);

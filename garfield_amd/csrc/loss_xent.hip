@@ -94,10 +94,91 @@ __global__ __launch_bounds__(kXentThreads) void k_xent_bwd(const void* __restric
   }
 }
 
+// nc > kXentMaxClasses (an ImageNet head): one wave per row, the lanes over the classes in three
+// passes over the row's (L1 / L2-resident) logits: max, Σ exp, then d(loss)/d(logits); the row's loss
+// goes to rowloss and k_xent_rowsum reduces each worker's rows in a fixed order (deterministic)
+template <int DT>
+__global__ __launch_bounds__(kXentThreads) void k_xent_rows_wide(const void* __restrict__ logits,
+                                                                 const int64_t* __restrict__ labels, int64_t total,
+                                                                 int64_t rows, int nc, float* __restrict__ rowloss,
+                                                                 void* __restrict__ dl) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * (kXentThreads / 64) + (threadIdx.x >> 6);
+  if (r >= total) return;
+  const int64_t o = r * nc;
+  const int64_t lab = labels[r];
+  const bool ok = lab >= 0 && lab < nc;
+  const float inv = 1.f / static_cast<float>(rows);
+  float m = -INFINITY;
+  for (int c = lane; c < nc; c += 64) m = fmaxf(m, ld<DT>(logits, o + c));
+#pragma unroll
+  for (int sft = 32; sft >= 1; sft >>= 1) m = fmaxf(m, __shfl_xor(m, sft));
+  float sum = 0.f;
+  for (int c = lane; c < nc; c += 64) sum += __expf(ld<DT>(logits, o + c) - m);
+  sum = wave_sum(sum);
+  const float is = 1.f / sum;
+  for (int c = lane; c < nc; c += 64) {
+    const float pr = __expf(ld<DT>(logits, o + c) - m) * is;
+    st<DT>(dl, o + c, (pr - ((ok && c == lab) ? 1.f : 0.f)) * inv);
+  }
+  if (lane == 0) rowloss[r] = ok ? (m + __logf(sum) - ld<DT>(logits, o + lab)) : __int_as_float(0x7fc00000);
+}
+
+// loss[g] = mean of worker g's row losses (one workgroup per worker)
+__global__ __launch_bounds__(kXentThreads) void k_xent_rowsum(const float* __restrict__ rowloss, int64_t rows,
+                                                              float* __restrict__ loss) {
+  __shared__ float wsum[kXentThreads / 64];
+  const int g = blockIdx.x;
+  float acc = 0.f;
+  for (int64_t t = threadIdx.x; t < rows; t += kXentThreads) acc += rowloss[static_cast<int64_t>(g) * rows + t];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kXentThreads / 64; ++w) t += wsum[w];
+    loss[g] = t / static_cast<float>(rows);
+  }
+}
+
+// out[0] = mean of n fp32 values (the step's reported loss over the workers), fixed order
+__global__ __launch_bounds__(kXentThreads) void k_mean_f32(const float* __restrict__ x, int64_t n,
+                                                           float* __restrict__ out) {
+  __shared__ float wsum[kXentThreads / 64];
+  float acc = 0.f;
+  for (int64_t t = threadIdx.x; t < n; t += kXentThreads) acc += x[t];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kXentThreads / 64; ++w) t += wsum[w];
+    out[0] = t / static_cast<float>(n);
+  }
+}
+
 }  // namespace
 
+void mean_f32(const float* x, int64_t n, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(k_mean_f32, dim3(1), dim3(kXentThreads), 0, stream, x, n, out);
+}
+
 void xent_forward(const void* logits, int dt, const int64_t* labels, int64_t rows, int groups, int nc,
-                  float* loss, void* dlogits, hipStream_t stream) {
+                  float* loss, void* dlogits, hipStream_t stream, float* rowloss) {
+  if (nc > kXentMaxClasses) {
+    const int64_t total = rows * groups;
+    const dim3 grid(static_cast<unsigned>((total + kXentThreads / 64 - 1) / (kXentThreads / 64)));
+    if (dt == kF32)
+      hipLaunchKernelGGL(k_xent_rows_wide<kF32>, grid, dim3(kXentThreads), 0, stream, logits, labels, total, rows, nc,
+                         rowloss, dlogits);
+    else
+      hipLaunchKernelGGL(k_xent_rows_wide<kBF16>, grid, dim3(kXentThreads), 0, stream, logits, labels, total, rows, nc,
+                         rowloss, dlogits);
+    hipLaunchKernelGGL(k_xent_rowsum, dim3(groups), dim3(kXentThreads), 0, stream, rowloss, rows, loss);
+    return;
+  }
   if (dt == kF32)
     hipLaunchKernelGGL(k_xent_fwd<kF32>, dim3(groups), dim3(kXentThreads), 0, stream, logits, labels, rows, nc, loss,
                        dlogits);

@@ -1611,11 +1611,18 @@ class _GroupedLinear(torch.autograd.Function):
             else:
                 spec.sink.put_groups(spec.lin.weight, torch.bmm(dy3.transpose(1, 2), x3))
             if spec.lin.bias is not None:
-                bv = spec.sink.rows_view(spec.lin.bias, (out,), dy.dtype)
-                if bv is not None:       # reduced in fp32, written in the exchange dtype
-                    torch.sum(dy3, 1, out=bv)
+                sink = spec.sink
+                if (dy.is_cuda and dy.dtype in (torch.bfloat16, torch.float32) and sink.flat.is_cuda
+                        and sink.flat.dtype in (torch.float32, torch.bfloat16, torch.float16)):
+                    # fp32 sums straight into the exchange rows (no ATen reduction)
+                    _native.native().gpu_linear_bias_grad(dy, G, sink.flat, sink.row_stride,
+                                                          sink.base + sink.offset(spec.lin.bias))
                 else:
-                    spec.sink.put_groups(spec.lin.bias, _acc(dy3).sum(1))
+                    bv = sink.rows_view(spec.lin.bias, (out,), dy.dtype)
+                    if bv is not None:       # reduced in fp32, written in the exchange dtype
+                        torch.sum(dy3, 1, out=bv)
+                    else:
+                        sink.put_groups(spec.lin.bias, _acc(dy3).sum(1))
         return dx, None, None, None
 
 
@@ -1724,8 +1731,9 @@ class _GroupedXent(torch.autograd.Function):
 
 def grouped_cross_entropy(logits: torch.Tensor, labels: torch.Tensor, groups: int) -> torch.Tensor:
     """[groups] per-worker mean cross-entropy of ``logits`` [groups*rows, classes];
-    the fused kernel on GPU (bf16/fp32 logits, <= 64 classes, int64 labels), else ATen."""
-    if (XENT and logits.is_cuda and logits.dim() == 2 and logits.shape[1] <= 64
+    the fused kernels on GPU (bf16/fp32 logits, int64 labels: one thread per row up to 64 classes,
+    one wave per row beyond), else ATen."""
+    if (XENT and logits.is_cuda and logits.dim() == 2
             and logits.dtype in (torch.bfloat16, torch.float32) and labels.dtype == torch.int64):
         return _GroupedXent.apply(logits.contiguous(), labels.contiguous(), groups)
     lg = logits if logits.dtype == torch.float64 else logits.float()

@@ -598,9 +598,11 @@ def test_grouped_engine_graph_matches_eager_and_excludes_attacker(cuda):
 
 
 @pytest.mark.parametrize("G,B,nc,dt", [(8, 250, 10, torch.bfloat16), (3, 7, 64, torch.float32),
-                                      (1, 300, 2, torch.bfloat16)])
+                                      (1, 300, 2, torch.bfloat16), (8, 250, 1000, torch.bfloat16),
+                                      (3, 17, 65, torch.float32), (2, 5, 200, torch.bfloat16)])
 def test_grouped_cross_entropy_matches_fp32_reference(cuda, native, G, B, nc, dt):
-    """loss_xent.hip: per-worker mean loss and its logits gradient vs fp32 ATen."""
+    """loss_xent.hip: per-worker mean loss and its logits gradient vs fp32 ATen (up to 64 classes one
+    thread per row; wider heads one wave per row plus a fixed-order per-worker sum)."""
     torch.manual_seed(nc)
     z = (torch.randn(G * B, nc, device=cuda) * 4).to(dt)
     y = torch.randint(0, nc, (G * B,), device=cuda)
@@ -614,6 +616,27 @@ def test_grouped_cross_entropy_matches_fp32_reference(cuda, native, G, B, nc, dt
     assert rel(loss, ref) < 1e-5
     assert zi.grad.dtype == dt
     assert rel(zi.grad, zr.grad) < (1e-2 if dt == torch.bfloat16 else 1e-5)
+
+
+def test_mean_f32_and_linear_bias_grad(cuda, native):
+    """gpu_mean_f32 (the step's reported loss) and gpu_linear_bias_grad (a wide head's per-worker db
+    written into strided exchange rows, any exchange dtype) against fp32 torch."""
+    torch.manual_seed(3)
+    for n in (1, 8, 300, 5000):
+        x = torch.randn(n, device=cuda)
+        m = native.gpu_mean_f32(x)
+        assert m.dim() == 0 and abs(m.item() - x.double().mean().item()) < 1e-5 * (1 + x.abs().mean().item())
+    G, rg, O = 4, 37, 1000
+    for dt in (torch.bfloat16, torch.float32):
+        dl = torch.randn(G * rg, O, device=cuda).to(dt)
+        ref = dl.float().view(G, rg, O).sum(1)
+        for odt in (torch.float32, torch.bfloat16):
+            stride, off = O + 24, 8
+            rows = torch.zeros(G * stride + 16, device=cuda, dtype=odt)
+            native.gpu_linear_bias_grad(dl, G, rows, stride, off)
+            got = torch.stack([rows[g * stride + off:g * stride + off + O] for g in range(G)]).float()
+            assert rel(got, ref) < (1e-2 if odt == torch.bfloat16 else 1e-5)
+            assert rows[:off].abs().max() == 0   # nothing written before the first row's offset
 
 
 def _train(cuda, grouped: bool, steps: int, seed: int = 0):
