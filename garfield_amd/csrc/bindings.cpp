@@ -736,9 +736,10 @@ void g_dgrad_s2(const at::Tensor& dy, const at::Tensor& w, int64_t kh, int64_t k
 
 // Implicit-GEMM convolution: y = conv(x, w) (+ add); x/y/add channels_last bf16, w the
 // [Cout, KH, KW, C]-ordered weight (a channels_last 4-D weight or its [Cout, K] matrix).
-void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
+bool g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t ph,
              int64_t pw, int64_t dh, int64_t dw, const at::Tensor& y, const c10::optional<at::Tensor>& add,
-             int64_t pm, bool transpose_w, const c10::optional<at::Tensor>& stats, int64_t rg) {
+             int64_t pm, bool transpose_w, const c10::optional<at::Tensor>& stats, int64_t rg,
+             const c10::optional<at::Tensor>& add_mask) {
   auto g = conv_geometry(x, kh, kw, sh, sw, ph, pw, dh, dw);
   TORCH_CHECK(g.C % 32 == 0, "gpu_iconv: input channels must be a multiple of 32 (got ", g.C, ")");
   TORCH_CHECK(y.is_cuda() && y.device() == x.device() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 &&
@@ -796,27 +797,44 @@ void g_iconv(const at::Tensor& x, const at::Tensor& w, int64_t kh, int64_t kw, i
     TORCH_CHECK(garfield::gpu::conv3x3_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), nullptr,
                                             pm == 0 ? 0 : static_cast<int>(pm - 20), stream_of(x.device()), sp, rg),
                 "gpu_iconv: the halo-staged kernel refused the statistics launch");
-    return;
+    return true;
   }
-  // pm 0 (auto): the halo-staged 3x3 kernel whenever it fits (GARFIELD_CONV3X3=0 disables it);
-  // pm 22 / 24: force it with 2 / 4 pixel fragments per wave; 1..14: the implicit-GEMM kernel
   static const bool c3 = [] {
     const char* e = std::getenv("GARFIELD_CONV3X3");
     return !(e && e[0] == '0');
   }();
+  if (add_mask.has_value() && add_mask->defined()) {
+    // add masked by a 1-bit-per-element mask (a BatchNorm's ReLU bits): the halo-staged kernel only;
+    // false (nothing launched) when it does not take this launch, the caller then materialises
+    const auto& mk = *add_mask;
+    TORCH_CHECK(ap != nullptr, "gpu_iconv: add_mask needs add");
+    TORCH_CHECK(mk.is_cuda() && mk.device() == x.device() && mk.scalar_type() == at::kByte && mk.is_contiguous() &&
+                    mk.numel() * 8 == y.numel(),
+                "gpu_iconv: add_mask must be a contiguous uint8 bit mask of y.numel() / 8 bytes");
+    TORCH_CHECK(y.data_ptr() != ap, "gpu_iconv: with add_mask, y must not alias add");
+    if (transpose_w || !(pm == 0 || pm == 22 || pm == 24) || !c3 ||
+        garfield::gpu::conv3x3_pick(g, static_cast<int>(cout)) == 0)
+      return false;
+    return garfield::gpu::conv3x3_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap,
+                                       pm == 0 ? 0 : static_cast<int>(pm - 20), stream_of(x.device()), nullptr, 0,
+                                       mk.data_ptr<uint8_t>());
+  }
+  // pm 0 (auto): the halo-staged 3x3 kernel whenever it fits (GARFIELD_CONV3X3=0 disables it);
+  // pm 22 / 24: force it with 2 / 4 pixel fragments per wave; 1..14: the implicit-GEMM kernel
   if (!transpose_w && (pm == 22 || pm == 24)) {
     TORCH_CHECK(garfield::gpu::conv3x3_pick(g, static_cast<int>(cout)) != 0 &&
                     garfield::gpu::conv3x3_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap,
                                                 static_cast<int>(pm - 20), stream_of(x.device())),
                 "gpu_iconv: pm ", pm, " (halo-staged 3x3 kernel) does not fit this shape");
-    return;
+    return true;
   }
   if (!transpose_w && pm == 0 && c3 &&
       garfield::gpu::conv3x3_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap, 0,
                                   stream_of(x.device())))
-    return;
+    return true;
   garfield::gpu::iconv_nhwc(u16(x), u16(w), g, static_cast<int>(cout), u16_mut(y), ap, static_cast<int>(pm),
                             transpose_w, stream_of(x.device()));
+  return true;
 }
 
 int64_t g_conv3x3_pick(int64_t n, int64_t h, int64_t w, int64_t c, int64_t cout) {
@@ -2050,10 +2068,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_iconv", &g_iconv, "Implicit-GEMM NHWC convolution on MFMA: y = conv(x, w) (+ add); args (x, w, kh, kw, "
         "sh, sw, ph, pw, dh, dw, y, add=None, pm=0, transpose_w=False); x/y/add channels_last bf16, C % 32 == 0, "
         "Cout % 64 == 0; transpose_w: w is the forward weight [C, Cout, KH, KW] whose flipped transpose is applied "
-        "(the data gradient of that convolution)",
+        "(the data gradient of that convolution); add_mask [y.numel() / 8] uint8: add counts where its bit is set "
+        "(halo-staged 3x3 kernel only, y a separate tensor). Returns False when nothing was launched (add_mask on a "
+        "shape the halo kernel does not take)",
         py::arg("x"), py::arg("w"), py::arg("kh"), py::arg("kw"), py::arg("sh"), py::arg("sw"), py::arg("ph"),
         py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("y"), py::arg("add") = py::none(), py::arg("pm") = 0,
-        py::arg("transpose_w") = false, py::arg("stats") = py::none(), py::arg("rg") = 0);
+        py::arg("transpose_w") = false, py::arg("stats") = py::none(), py::arg("rg") = 0,
+        py::arg("add_mask") = py::none());
   m.def("conv3x3_stats_rows", [](int64_t n, int64_t h, int64_t w, int64_t c, int64_t cout) -> int64_t {
           return 16 * g_conv3x3_pick(n, h, w, c, cout);
         }, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("c"), py::arg("cout"),

@@ -179,7 +179,8 @@ void dgrad_s2_nhwc(const uint16_t* dy, const uint16_t* w, const Im2col& g, int C
 // stats (nullable, no add): per-worker (rg pixels) BatchNorm statistics of y for bn_finalize_tiles, one
 // statistics tile of 16 * pmf pixels per wave (H = 16 * pmf, E = 1: ceil(M / H) * 6 * Cout floats).
 bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
-                  int pmf, hipStream_t stream, float* stats = nullptr, int64_t rg = 0);
+                  int pmf, hipStream_t stream, float* stats = nullptr, int64_t rg = 0,
+                  const uint8_t* add_mask = nullptr);   // add_mask: add counts where its bit is set (1 bit / element)
 // Halo-staged per-worker weight gradient of the same 3x3 convolutions (conv3x3_nhwc.hip), same
 // contract as iwgrad_nhwc; splits cut each worker's 128-pixel tiles into contiguous ranges (an empty
 // range writes a zero slab). wgrad3x3_fits: the shape fits (rg whole images); otherwise

@@ -87,6 +87,47 @@ __device__ __forceinline__ void wave_stats(const float (&v)[WPM][WPN][4], int64_
   }
 }
 
+// v[0..3] += add[e .. e + 4), term i kept where bit i of keep is set
+__device__ __forceinline__ void add_bf16x4(float (&v)[4], const uint16_t* __restrict__ add, uint32_t keep, int64_t e) {
+  const uint2 a = *reinterpret_cast<const uint2*>(add + e);
+  v[0] += (keep & 1u) ? bf16_to_f(a.x & 0xffffu) : 0.f;
+  v[1] += (keep & 2u) ? bf16_to_f(a.x >> 16) : 0.f;
+  v[2] += (keep & 4u) ? bf16_to_f(a.y & 0xffffu) : 0.f;
+  v[3] += (keep & 8u) ? bf16_to_f(a.y >> 16) : 0.f;
+}
+
+// EPI_ADD with amask (the residual gradient dres = dy · [y > 0] of a BatchNorm + ReLU, read from dy and
+// the forward's ReLU bits instead of a materialised dres): the mask bits of a lane's row over the
+// wave's 16 * NG channels from element e (a multiple of 16 * NG) in ONE load of 2 * NG bytes; all ones
+// without a mask
+template <int NG>
+struct RowMask {
+  uint32_t w[NG / 2];
+  __device__ __forceinline__ void load(const uint8_t* __restrict__ amask, int64_t e) {
+    static_assert(NG == 2 || NG == 4 || NG == 8, "2, 4 or 8 channel groups of 16");
+    if (!amask) {
+#pragma unroll
+      for (int i = 0; i < NG / 2; ++i) w[i] = 0xffffffffu;
+      return;
+    }
+    const uint8_t* p = amask + (e >> 3);
+    if constexpr (NG == 2) {
+      w[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if constexpr (NG == 4) {
+      const uint2 u = *reinterpret_cast<const uint2*>(p);
+      w[0] = u.x; w[1] = u.y;
+    } else {
+      const uint4 u = *reinterpret_cast<const uint4*>(p);
+      w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+    }
+  }
+  // bits of channel group c's 4 channels at 4 * fq (byte 2c + fq / 2, nibble fq % 2)
+  __device__ __forceinline__ uint32_t nib(int c, int fq) const {
+    const int b = 2 * c + (fq >> 1);
+    return (w[b >> 2] >> ((b & 3) * 8 + (fq & 1) * 4)) & 0xfu;
+  }
+};
+
 }  // namespace dev
 }  // namespace gpu
 }  // namespace garfield

@@ -61,25 +61,23 @@ constexpr int EPI_PLAIN = 0, EPI_ADD = 1, EPI_STATS = 2;
 // other gradient branch), EPI_STATS writes the wave's per-worker statistics tile (bn_stats.hpp).
 template <int PMF, int EPI>
 __device__ __forceinline__ void conv_epilogue(const f32x4 (&acc)[PMF][4], int mw, int M, int Cout, int co0, uint16_t* y,
-                                              const uint16_t* add, float* __restrict__ stats, int64_t rg) {
+                                              const uint16_t* add, float* __restrict__ stats, int64_t rg,
+                                              const uint8_t* __restrict__ amask) {
   const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
   float vs[PMF][4][4];   // the stored (bf16-rounded) values, for the statistics
 #pragma unroll
   for (int r = 0; r < PMF; ++r) {
     const int m = mw + r * 16 + fr;
     const int64_t rowoff = static_cast<int64_t>(m < M ? m : 0) * Cout;
+    RowMask<4> rm;   // amask: add counts only where the (BatchNorm ReLU) bit is set
+    if constexpr (EPI == EPI_ADD)
+      if (m < M) rm.load(amask, rowoff + co0);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int64_t off = rowoff + co0 + c * 16 + fq * 4;
       float v[4] = {acc[r][c][0], acc[r][c][1], acc[r][c][2], acc[r][c][3]};
       if constexpr (EPI == EPI_ADD) {
-        if (m < M) {
-          const uint2 a = *reinterpret_cast<const uint2*>(add + off);
-          v[0] += bf16_to_f(static_cast<uint16_t>(a.x & 0xffffu));
-          v[1] += bf16_to_f(static_cast<uint16_t>(a.x >> 16));
-          v[2] += bf16_to_f(static_cast<uint16_t>(a.y & 0xffffu));
-          v[3] += bf16_to_f(static_cast<uint16_t>(a.y >> 16));
-        }
+        if (m < M) add_bf16x4(v, add, rm.nib(c, fq), off);
       }
       uint2 o;
       o.x = static_cast<uint32_t>(f_to_bf16(v[0])) | (static_cast<uint32_t>(f_to_bf16(v[1])) << 16);
@@ -102,7 +100,7 @@ __device__ __forceinline__ void conv_epilogue(const f32x4 (&acc)[PMF][4], int mw
 template <int PMF, int NU, int EPI>
 __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                  Im2col g, Halo hp, int Cout, uint16_t* y, const uint16_t* add,
-                                                 float* __restrict__ stats, int64_t rg) {
+                                                 float* __restrict__ stats, int64_t rg, const uint8_t* amask) {
   constexpr int NSW = 3;               // weight ring stages
   constexpr int BM = 64 * PMF;         // output pixels per workgroup
   constexpr int XB = NU * 4096;        // halo bytes (NU glds rounds of 4 waves x 8 pixels)
@@ -236,7 +234,7 @@ __global__ __launch_bounds__(256) void k_conv3x3(const uint16_t* __restrict__ x,
     }
   }
 
-  conv_epilogue<PMF, EPI>(acc, m0 + wave * PMF * 16, mlim, Cout, co0, y, add, stats, rg);
+  conv_epilogue<PMF, EPI>(acc, m0 + wave * PMF * 16, mlim, Cout, co0, y, add, stats, rg, amask);
 }
 
 // 64 input channels (one halo block per tile: ResNet layer1-type layers). The one-shot kernel above
@@ -250,7 +248,8 @@ constexpr int kNuRes = 11;   // 256-pixel tiles of 32- or 16-wide images: 340 / 
 template <int EPI>
 __global__ __launch_bounds__(256) void k_conv3x3_res(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                                                      Im2col g, Halo hp, int Cout, int tiles, uint16_t* y,
-                                                     const uint16_t* add, float* __restrict__ stats, int64_t rg) {
+                                                     const uint16_t* add, float* __restrict__ stats, int64_t rg,
+                                                     const uint8_t* amask) {
   constexpr int PMF = 4, BM = 256, NU = kNuRes;
   constexpr int XB = NU * 4096;
   constexpr int WB = 9 * 64 * 128;
@@ -360,7 +359,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_res(const uint16_t* __restrict_
     }
     const int mt = tile * hp.TP;
     conv_epilogue<PMF, EPI>(acc, mt + wave * PMF * 16, mt + hp.TP < M ? mt + hp.TP : M, Cout, co0, y, add, stats,
-                            rg);
+                            rg, amask);
     // the next halo has landed and every wave is done with this one before it is refilled. The
     // epilogue's 16 output stores (PMF x 4 global_store_dwordx2, issued after the halo loads) may stay
     // in flight: waiting for them too exposed the store latency once per tile. A ragged tile (the
@@ -403,18 +402,18 @@ bool plan(const Im2col& g, int pmf, int nu_max, Halo& hp) {
 
 template <int PMF, int NU>
 void launch(const uint16_t* x, const uint16_t* w, const Im2col& g, const Halo& hp, int Cout, uint16_t* y,
-            const uint16_t* add, float* stats, int64_t rg, hipStream_t stream) {
+            const uint16_t* add, float* stats, int64_t rg, hipStream_t stream, const uint8_t* amask) {
   const int tiles = (g.N * g.Ho + hp.TR - 1) / hp.TR;
   const dim3 grid(tiles, Cout / 64);
   if (add)
     hipLaunchKernelGGL((k_conv3x3<PMF, NU, EPI_ADD>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add, stats,
-                       rg);
+                       rg, amask);
   else if (stats)
     hipLaunchKernelGGL((k_conv3x3<PMF, NU, EPI_STATS>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add, stats,
-                       rg);
+                       rg, nullptr);
   else
     hipLaunchKernelGGL((k_conv3x3<PMF, NU, EPI_PLAIN>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, y, add, stats,
-                       rg);
+                       rg, nullptr);
 }
 
 constexpr int kNuBig = 14;    // PMF 4: 14 x 4 KB halo + 3 x 8 KB ring = 80 KB (two workgroups per CU)
@@ -648,8 +647,9 @@ int cu_count() {
 }  // namespace
 
 bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cout, uint16_t* y, const uint16_t* add,
-                  int pmf, hipStream_t stream, float* stats, int64_t rg) {
+                  int pmf, hipStream_t stream, float* stats, int64_t rg, const uint8_t* add_mask) {
   if (pmf <= 0) pmf = conv3x3_pick(g, Cout);
+  if (!add) add_mask = nullptr;
   if (stats && (add || rg < 16 * pmf)) return false;
   Halo hp;
   // the statistics epilogue indexes its tiles by 16 * PMF-pixel wave ranges: whole tiles only
@@ -661,23 +661,23 @@ bool conv3x3_nhwc(const uint16_t* x, const uint16_t* w, const Im2col& g, int Cou
     const dim3 grid(gx, Cout / 64);
     if (add)
       hipLaunchKernelGGL((k_conv3x3_res<EPI_ADD>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, tiles, y, add, stats,
-                         rg);
+                         rg, add_mask);
     else if (stats)
       hipLaunchKernelGGL((k_conv3x3_res<EPI_STATS>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, tiles, y, add,
-                         stats, rg);
+                         stats, rg, nullptr);
     else
       hipLaunchKernelGGL((k_conv3x3_res<EPI_PLAIN>), grid, dim3(256), 0, stream, x, w, g, hp, Cout, tiles, y, add,
-                         stats, rg);
+                         stats, rg, nullptr);
     return true;
   }
   const int pick = conv3x3_pick(g, Cout);
   const bool s1 = g.sh == 1;
   if (pmf == 4 && pick && s1 && plan(g, 4, kNuBig, hp)) {
-    launch<4, kNuBig>(x, w, g, hp, Cout, y, add, stats, rg, stream);
+    launch<4, kNuBig>(x, w, g, hp, Cout, y, add, stats, rg, stream, add_mask);
     return true;
   }
   if (pmf == 2 && pick && s1 && plan(g, 2, kNuSmall, hp)) {
-    launch<2, kNuSmall>(x, w, g, hp, Cout, y, add, stats, rg, stream);
+    launch<2, kNuSmall>(x, w, g, hp, Cout, y, add, stats, rg, stream, add_mask);
     return true;
   }
   return false;

@@ -647,11 +647,12 @@ def _halo_dgrad_ok(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> bool:
             and _native.native().conv3x3_pick(dy.shape[0], dy.shape[2], dy.shape[3], w.shape[0], w.shape[1]) > 0)
 
 
-def _halo_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", add: torch.Tensor | None) -> torch.Tensor:
+def _halo_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", add: torch.Tensor | None,
+                add_mask: torch.Tensor | None = None) -> torch.Tensor | None:
     if not spec.flip or spec.wd is None:       # first use (eager): make the flipped weight now
         spec.flip = True
         _native.native().gpu_transpose_multi([w.detach()], [_flip_weight_buf(spec)])
-    return _iconv(dy, spec.wd, (3, 3, 1, 1, 1, 1, 1, 1), (dy.shape[2], dy.shape[3]), add)
+    return _iconv(dy, spec.wd, (3, 3, 1, 1, 1, 1, 1, 1), (dy.shape[2], dy.shape[3]), add, add_mask=add_mask)
 
 
 def _gemm_nt_dgrad(dy2: torch.Tensor, w2: torch.Tensor, add: torch.Tensor | None, spec: "ConvSpec | None" = None,
@@ -898,15 +899,19 @@ _ICONV_MINWG = 400   # workgroups (profiles/bench_iconv_r1.log)
 
 
 def _iconv(x: torch.Tensor, w: torch.Tensor, geom, out_hw, add: torch.Tensor | None = None,
-           transpose_w: bool = False) -> torch.Tensor:
+           transpose_w: bool = False, add_mask: torch.Tensor | None = None) -> torch.Tensor | None:
     """y = conv(x, w) (+ add, written in place of add when given) on the MFMA kernel;
-    ``transpose_w``: w is a forward weight and its flipped transpose is applied (dgrad)."""
+    ``transpose_w``: w is a forward weight and its flipped transpose is applied (dgrad). ``add_mask``
+    (a MaskedGrad's ReLU bits): add counts where its bit is set and y is a new tensor; None when the
+    halo-staged kernel (the only one with the masked epilogue) does not take the shape."""
     n = x.shape[0]
     cout = w.shape[1] if transpose_w else w.shape[0]
-    if add is not None:
+    if add is not None and add_mask is None:
         y = add
     else:
         y = torch.empty((n, cout, *out_hw), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    if add_mask is not None:
+        return y if _native.native().gpu_iconv(x, w, *geom, y, add, 0, transpose_w, add_mask=add_mask) else None
     _native.native().gpu_iconv(x, w, *geom, y, add, 0, transpose_w)
     return y
 
@@ -1248,7 +1253,10 @@ class _GroupedConv(torch.autograd.Function):
         if _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
             ctx.mode = "iconv"
             ctx.save_for_backward(x, w)
-            return _iconv(x, w, _geom(spec), _out_hw(spec, h, wd))
+            y = _iconv(x, w, _geom(spec), _out_hw(spec, h, wd))
+            if join is not None and _halo_dgrad_ok(y, w, spec):
+                join.lazy = True                 # the halo-staged dgrad takes the other branch's MaskedGrad
+            return y
         if x.is_cuda and _channels_last_weight(w):
             ctx.mode = "col"
             col = _im2col(x, spec)
@@ -1274,7 +1282,7 @@ class _GroupedConv(torch.autograd.Function):
         need_dx = ctx.needs_input_grad[0]
         prev = ctx.join.take() if (need_dx and ctx.join is not None) else None
         first = need_dx and ctx.join is not None and prev is None   # park dx for the other branch
-        if isinstance(prev, MaskedGrad) and mode != "rows":
+        if isinstance(prev, MaskedGrad) and mode not in ("rows", "iconv"):
             prev = prev.materialize()
         if mode == "f32":                        # a = x
             if need_dx:
@@ -1318,7 +1326,16 @@ class _GroupedConv(torch.autograd.Function):
             col = None if use_iw else _im2col(a, spec)
             kp = col.shape[1] if col is not None else K
             if need_dx:
-                if _halo_dgrad_ok(dy, w, spec):
+                if isinstance(prev, MaskedGrad):   # dres from dy + the ReLU bits, in the halo kernel's epilogue
+                    if _halo_dgrad_ok(dy, w, spec):
+                        dx = _halo_dgrad(dy, w, spec, prev.dy, prev.mask)
+                    if dx is None:
+                        prev = prev.materialize()
+                    else:
+                        prev = None
+                if dx is not None:
+                    pass
+                elif _halo_dgrad_ok(dy, w, spec):
                     dx = _halo_dgrad(dy, w, spec, _cl(prev) if prev is not None else None)
                 elif ((sh, sw, dh, dw) == (1, 1, 1, 1) and ph <= kh - 1 and pw <= kw - 1
                         and _iconv_ok(dy, _dgrad_weight_shape(w), dy2.shape[0])):
