@@ -184,59 +184,32 @@ __global__ __launch_bounds__(kThreads) void k_partial(const void* __restrict__ x
       load8f(rsh + static_cast<int64_t>(g) * C + c0, rf);
     }
     int64_t r = r0 + tr;
-    if constexpr (!BWD || RM != 0) {
-      // two rows in flight per lane, unpacked as loaded (for these forms hipcc keeps this loop's loads
-      // in one batch but serialises a four-row raw batch, checked in the ISA)
-      for (; r + geo.rp < r1; r += 2 * geo.rp) {
-        const int64_t o0 = (base + r) * C + c0, o1 = o0 + static_cast<int64_t>(geo.rp) * C;
-        float a0[8], a1[8];
-        load8<DT>(x, o0, a0);
-        load8<DT>(x, o1, a1);
-        if constexpr (BWD) {
-          float d0[8], d1[8];
-          load8<DT>(dy, o0, d0);
-          load8<DT>(dy, o1, d1);
-          relu_mask8<RM, DT>(d0, a0, y, mask, o0, rs, rf);
-          relu_mask8<RM, DT>(d1, a1, y, mask, o1, rs, rf);
+    // two rows in flight per lane, unpacked as loaded (hipcc keeps this loop's loads in one batch but
+    // serialises a four-row raw batch, checked in the ISA). One loop for every form: the sums of a
+    // shortcut BatchNorm fed dy + ReLU bits (RM 2) and of one fed the written dres (RM 0) agree bit for bit
+    // (the ResLink path, tests/test_grouped_gpu.py::test_lazy_residual_*)
+    for (; r + geo.rp < r1; r += 2 * geo.rp) {
+      const int64_t o0 = (base + r) * C + c0, o1 = o0 + static_cast<int64_t>(geo.rp) * C;
+      float a0[8], a1[8];
+      load8<DT>(x, o0, a0);
+      load8<DT>(x, o1, a1);
+      if constexpr (BWD) {
+        float d0[8], d1[8];
+        load8<DT>(dy, o0, d0);
+        load8<DT>(dy, o1, d1);
+        relu_mask8<RM, DT>(d0, a0, y, mask, o0, rs, rf);
+        relu_mask8<RM, DT>(d1, a1, y, mask, o1, rs, rf);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            s[i] += d0[i] + d1[i];
-            q[i] += d0[i] * (a0[i] - sh[i]) + d1[i] * (a1[i] - sh[i]);
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float e0 = a0[i] - sh[i], e1 = a1[i] - sh[i];
-            s[i] += e0 + e1;
-            q[i] += e0 * e0 + e1 * e1;
-          }
+        for (int i = 0; i < 8; ++i) {
+          s[i] += d0[i] + d1[i];
+          q[i] += d0[i] * (a0[i] - sh[i]) + d1[i] * (a1[i] - sh[i]);
         }
-      }
-    } else {   // the backward without a ReLU mask
-      // four rows in flight per lane: every load of the batch issued before the first use
-      constexpr int RB = 4;
-      static_assert(BWD, "the forward keeps the two-row loop");
-      for (; r + (RB - 1) * geo.rp < r1; r += RB * geo.rp) {
-        Raw8<DT> xa[RB], da[RB];
+      } else {
 #pragma unroll
-        for (int k = 0; k < RB; ++k) {
-          const int64_t o = (base + r + static_cast<int64_t>(k) * geo.rp) * C + c0;
-          xa[k] = ld_raw8<DT>(x, o);
-          if constexpr (BWD) da[k] = ld_raw8<DT>(dy, o);
-        }
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-          float a0[8];
-          unpack8(xa[k], a0);
-          if constexpr (BWD) {
-            float d0[8];
-            unpack8(da[k], d0);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) { s[i] += d0[i]; q[i] += d0[i] * (a0[i] - sh[i]); }
-          } else {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) { const float e = a0[i] - sh[i]; s[i] += e; q[i] += e * e; }
-          }
+        for (int i = 0; i < 8; ++i) {
+          const float e0 = a0[i] - sh[i], e1 = a1[i] - sh[i];
+          s[i] += e0 + e1;
+          q[i] += e0 * e0 + e1 * e1;
         }
       }
     }

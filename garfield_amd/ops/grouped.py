@@ -252,6 +252,19 @@ class MaskedGrad:
         return from_rows(out, n, h, w)
 
 
+class ResLink:
+    """A projection-shortcut block's residual gradient, handed from the block's last BatchNorm (whose
+    residual input is the shortcut BatchNorm's output) to the shortcut BatchNorm's backward as dy + the
+    ReLU bits (MaskedGrad) instead of a written dres: autograd passes None along that edge, and the
+    shortcut BatchNorm (no ReLU of its own) applies the bits as its ReLU mask."""
+
+    __slots__ = ("pending", "ok")
+
+    def __init__(self):
+        self.pending = None
+        self.ok = False          # set by the shortcut BatchNorm's forward: it can take a MaskedGrad
+
+
 # --------------------------------------------------------------------------- #
 # Grouped BatchNorm (+ residual) (+ ReLU)
 
@@ -373,7 +386,8 @@ def _bn_bwd_ref(x2, dy2, y2, st: BNState, need_res: bool):
 
 class _GroupedBN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, st: BNState, ws: Workspace, join: GradJoin | None = None):
+    def forward(ctx, x, gamma, beta, res, st: BNState, ws: Workspace, join: GradJoin | None = None,
+                res_link: ResLink | None = None, out_link: ResLink | None = None):
         n, C, h, w = x.shape
         x2 = rows2d(x)
         r2 = rows2d(res) if res is not None else None
@@ -403,6 +417,10 @@ class _GroupedBN(torch.autograd.Function):
             y = from_rows(_bn_fwd_ref(x2, r2, st), n, h, w)
             relu_state = y if st.relu else None
         ctx.st, ctx.ws, ctx.has_res, ctx.join = st, ws, res is not None, join
+        ctx.res_link, ctx.out_link = res_link, out_link
+        if out_link is not None and x.is_cuda and not st.relu and LAZY_RES:
+            ctx.set_materialize_grads(False)     # the output's gradient may arrive through out_link only
+            out_link.ok = True
         ctx.save_for_backward(x, relu_state)
         return y
 
@@ -411,15 +429,20 @@ class _GroupedBN(torch.autograd.Function):
         x, y = ctx.saved_tensors                # y: the ReLU state (bit mask on the GPU, y on the CPU) or None
         st, ws = ctx.st, ctx.ws
         n, C, h, w = x.shape
+        y2 = (y if y.dim() == 1 else rows2d(y)) if y is not None else None
+        if dy is None:                          # a shortcut BatchNorm: dy + ReLU bits through out_link
+            m, ctx.out_link.pending = ctx.out_link.pending, None
+            if m is None:
+                return (None,) * 9
+            dy, y2 = m.dy, m.mask               # no ReLU of its own: the bits are its only mask
         dy = _cl(dy)
         x2, dy2 = rows2d(x), rows2d(dy)
-        y2 = (y if y.dim() == 1 else rows2d(y)) if y is not None else None
         lazy = None
         if x.is_cuda:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            if (ctx.has_res and LAZY_RES and ctx.join is not None and ctx.join.lazy and y2 is not None
-                    and y2.dim() == 1):
-                lazy = MaskedGrad(dy, y2)        # the consumer's GEMM applies the ReLU bits itself
+            if (ctx.has_res and LAZY_RES and y2 is not None and y2.dim() == 1 and
+                    ((ctx.join is not None and ctx.join.lazy) or (ctx.res_link is not None and ctx.res_link.ok))):
+                lazy = MaskedGrad(dy, y2)        # the consumer applies the ReLU bits itself
             dres = torch.empty_like(x, memory_format=torch.channels_last) if (ctx.has_res and lazy is None) \
                 else None
             rg = x2.shape[0] // st.groups
@@ -439,18 +462,23 @@ class _GroupedBN(torch.autograd.Function):
             dx = from_rows(dx2, n, h, w)
             dres = from_rows(dr2, n, h, w) if dr2 is not None else None
         if lazy is not None:
-            ctx.join.park(lazy)
+            if ctx.join is not None:
+                ctx.join.park(lazy)
+            else:
+                ctx.res_link.pending = lazy     # autograd passes None to the shortcut BatchNorm
         elif dres is not None and ctx.join is not None:
             ctx.join.park(dres)
             dres = None
-        return dx, None, None, dres, None, None, None
+        return dx, None, None, dres, None, None, None, None, None
 
 
-def grouped_bn(x, st: BNState, ws: Workspace, res=None, res_join: GradJoin | None = None):
+def grouped_bn(x, st: BNState, ws: Workspace, res=None, res_join: GradJoin | None = None,
+               res_link: ResLink | None = None, out_link: ResLink | None = None):
     """y = [relu](BN_per_worker(x) [+ res]); x/res channels_last. With ``res_join``
-    the residual's gradient is handed to the join instead of autograd."""
+    the residual's gradient is handed to the join instead of autograd; ``res_link`` / ``out_link``:
+    the block's last BatchNorm / its shortcut BatchNorm of one ResLink (see there)."""
     return _GroupedBN.apply(_cl(x), st.bn.weight, st.bn.bias, _cl(res) if res is not None else None, st, ws,
-                            res_join)
+                            res_join, res_link, out_link)
 
 
 # --------------------------------------------------------------------------- #

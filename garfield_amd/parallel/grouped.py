@@ -21,8 +21,8 @@ import torch.nn.functional as F
 
 from garfield_amd.models.resnet import BasicBlock, Bottleneck, ResNet
 from garfield_amd.parallel.signals import DeviceSignal
-from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, Workspace, bn_conv_ok,
-                                      global_avgpool, grouped_bn, grouped_bn_conv, grouped_conv,
+from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, LinearSpec, ResLink, Workspace,
+                                      bn_conv_ok, global_avgpool, grouped_bn, grouped_bn_conv, grouped_conv,
                                       grouped_cross_entropy, grouped_linear, grouped_maxpool, refresh_dgrad_weights,
                                       refresh_f32_weights, refresh_sc_weights)
 
@@ -111,13 +111,14 @@ class GroupedResNet:
             st = self.bn[bn] = BNState(bn, relu, self.sink, self.groups)
         return st
 
-    def _bn(self, x, bn: nn.BatchNorm2d, relu: bool, res=None, res_join=None):
-        return grouped_bn(x, self._state(bn, relu), self.ws, res, res_join)
+    def _bn(self, x, bn: nn.BatchNorm2d, relu: bool, res=None, res_join=None, res_link=None, out_link=None):
+        return grouped_bn(x, self._state(bn, relu), self.ws, res, res_join, res_link, out_link)
 
     def _conv(self, x, conv: nn.Conv2d, join=None):
         return grouped_conv(x, self.conv[conv], join)
 
-    def _conv_bn(self, x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, join=None, res=None, res_join=None):
+    def _conv_bn(self, x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, join=None, res=None, res_join=None,
+                 res_link=None, out_link=None):
         """conv -> BatchNorm; the convolution may hand the BatchNorm its statistics (gemm_nt.hip)."""
         st = self._state(bn, relu)
         spec = self.conv[conv]
@@ -126,7 +127,7 @@ class GroupedResNet:
             y = grouped_conv(x, spec, join)
         finally:
             spec.bn_next = None
-        return grouped_bn(y, st, self.ws, res, res_join)
+        return grouped_bn(y, st, self.ws, res, res_join, res_link, out_link)
 
     def _block(self, blk, x):
         # x's two gradient branches (conv1 and the shortcut) are summed inside the
@@ -152,16 +153,19 @@ class GroupedResNet:
                     spec3.bn_next = None
                 if blk.downsample is None:
                     return grouped_bn(y3, st3, self.ws, x, join)
-                sc = self._conv_bn(x, blk.downsample[0], blk.downsample[1], False, join)
-                return grouped_bn(y3, st3, self.ws, sc)
+                link = ResLink()
+                sc = self._conv_bn(x, blk.downsample[0], blk.downsample[1], False, join, out_link=link)
+                return grouped_bn(y3, st3, self.ws, sc, res_link=link)
             out = grouped_bn(x2, st2, self.ws)
             last_conv, last_bn = blk.conv3, blk.bn3
         else:
             last_conv, last_bn = blk.conv2, blk.bn2
         if blk.downsample is None:
             return self._conv_bn(out, last_conv, last_bn, True, res=x, res_join=join)
-        sc = self._conv_bn(x, blk.downsample[0], blk.downsample[1], False, join)
-        return self._conv_bn(out, last_conv, last_bn, True, res=sc)
+        # the shortcut BatchNorm receives the residual gradient as dy + the last BatchNorm's ReLU bits
+        link = ResLink()
+        sc = self._conv_bn(x, blk.downsample[0], blk.downsample[1], False, join, out_link=link)
+        return self._conv_bn(out, last_conv, last_bn, True, res=sc, res_link=link)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         out = []

@@ -495,12 +495,13 @@ def test_implicit_1x1_weight_gradients_match_gemm_path(cuda, monkeypatch):
         assert rel(b[j], a[j]) < 1e-2, (j, rel(b[j], a[j]))
 
 
-@pytest.mark.parametrize("name,parks", [("resnet50", 12), ("resnet18", None)])
+@pytest.mark.parametrize("name,parks", [("resnet50", 16), ("resnet18", None)])
 def test_lazy_residual_gradient_is_bitwise_the_materialised_one(cuda, monkeypatch, name, parks):
     """LAZY_RES: an identity block's last BatchNorm parks dy + its ReLU bits (MaskedGrad) instead of
     writing dres, and conv1's data-gradient kernel (the 1x1 GEMM, or the halo-staged 3x3 of a basic
-    block) applies the bits in its epilogue: the exchange rows equal the materialised-dres step's bit
-    for bit (same fp32 sums, one rounding)."""
+    block) applies the bits in its epilogue; a projection block's shortcut BatchNorm takes them as its
+    ReLU mask (ResLink). The exchange rows equal the materialised-dres step's bit for bit (same fp32
+    sums, one rounding)."""
     import garfield_amd.ops.grouped as grouped
 
     parked = []
@@ -518,9 +519,9 @@ def test_lazy_residual_gradient_is_bitwise_the_materialised_one(cuda, monkeypatc
     monkeypatch.setattr(grouped, "LAZY_RES", True)
     b = _grouped_rows(cuda, name, 4, 16)
     if parks is not None:
-        assert len(parked) == parks                 # ResNet-50: 16 blocks, 4 with a projection shortcut
+        assert len(parked) == parks                 # ResNet-50: 12 identity blocks + 4 projection shortcuts
     else:
-        assert 0 < len(parked) <= 5                 # ResNet-18: 5 identity blocks (halo-staged shapes)
+        assert 3 < len(parked) <= 8                 # ResNet-18: 3 shortcuts + up to 5 identity blocks
     assert torch.equal(a, b)
 
 
