@@ -368,7 +368,8 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
                   const at::Tensor& istd, const at::Tensor& scale, const at::Tensor& shift,
                   const c10::optional<at::Tensor>& y, bool relu, const c10::optional<at::Tensor>& mask,
                   bool defer_running,
-                  const c10::optional<at::Tensor>& tile_stats, int64_t tile_m, int64_t tile_e) {
+                  const c10::optional<at::Tensor>& tile_stats, int64_t tile_m, int64_t tile_e,
+                  const c10::optional<at::Tensor>& res_scale, const c10::optional<at::Tensor>& res_shift) {
   const auto dev = x.device();
   const int dt = check_act_rows(x, dev, "x");
   void* yp = nullptr;
@@ -410,10 +411,16 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
     const int64_t tiles = (x.size(0) + tile_m - 1) / tile_m;
     ts = ws_vec(*tile_stats, tiles * tile_e * 6 * C, dev, "tile_stats");
   }
+  const float* rsc = opt_vec(res_scale, groups * C, dev, "res_scale");
+  const float* rsh = opt_vec(res_shift, groups * C, dev, "res_shift");
+  TORCH_CHECK((rsc == nullptr) == (rsh == nullptr), "garfield bn: pass both res_scale and res_shift or neither");
+  TORCH_CHECK(rsc == nullptr || (r != nullptr && yp != nullptr), "garfield bn: res_scale needs res and y");
+  TORCH_CHECK(rsc == nullptr || (reinterpret_cast<uintptr_t>(rsc) % 16 == 0 && reinterpret_cast<uintptr_t>(rsh) % 16 == 0),
+              "garfield bn: res_scale / res_shift must be 16-byte aligned");
   c10::hip::HIPGuard guard(dev.index());
   garfield::gpu::bn_forward(x.data_ptr(), r, rg, G, static_cast<int>(C), g, b, static_cast<float>(eps),
                             static_cast<float>(momentum), rm, rv, pw, m, is, sc, sh, yp, relu, mp,
-                            defer_running, stream_of(dev), ts, tile_m, static_cast<int>(tile_e), dt);
+                            defer_running, stream_of(dev), ts, tile_m, static_cast<int>(tile_e), dt, rsc, rsh);
 }
 
 int xent_dtype(const at::Tensor& t, const char* what) {
@@ -1937,12 +1944,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_bn_forward", &g_bn_forward,
         "Per-worker BatchNorm(+residual)(+ReLU) forward on [k*Rg, C] bf16 rows; args (x, res|None, groups, gamma, "
         "beta, eps, momentum, running_mean|None, running_var|None, part, mean, istd, scale, shift, y, relu, "
-        "mask=None); mask: uint8 [numel/8] ReLU bit mask written for the backward",
+        "mask=None); mask: uint8 [numel/8] ReLU bit mask written for the backward; res_scale / res_shift "
+        "([groups, C] fp32): res is a pre-BatchNorm activation added as res * res_scale + res_shift (a projection "
+        "shortcut's BatchNorm folded into this apply pass)",
         py::arg("x"), py::arg("res"), py::arg("groups"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
         py::arg("momentum"), py::arg("running_mean"), py::arg("running_var"), py::arg("part"), py::arg("mean"),
         py::arg("istd"), py::arg("scale"), py::arg("shift"), py::arg("y"), py::arg("relu"),
         py::arg("mask") = py::none(), py::arg("defer_running") = false, py::arg("tile_stats") = py::none(),
-        py::arg("tile_m") = 0, py::arg("tile_e") = 1);
+        py::arg("tile_m") = 0, py::arg("tile_e") = 1, py::arg("res_scale") = py::none(),
+        py::arg("res_shift") = py::none());
   m.def("bn_small", [](int64_t rg) { return garfield::gpu::bn_small(rg); },
         "True when rg rows per worker take the single-kernel BatchNorm path (whose running statistics "
         "can be deferred to gpu_bn_running_update)");

@@ -50,7 +50,9 @@ void bn_forward(const void* x, const void* res, int64_t rg, int groups, int C, c
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
                 float* mean, float* istd, float* scale, float* shift, void* y, bool relu, uint8_t* mask,
                 bool defer_running, hipStream_t stream, const float* tile_stats = nullptr, int64_t tile_m = 0,
-                int tile_e = 1, int dt = 1);
+                int tile_e = 1, int dt = 1, const float* res_scale = nullptr, const float* res_shift = nullptr);
+// res_scale / res_shift ([groups][C] fp32): res is a PRE-BatchNorm activation, added as res * res_scale + res_shift
+// (its own BatchNorm, a projection shortcut's, folded into this one's apply pass)
 
 // Fresh batches (data_aug.hip): out[r] (bf16 channels_last [R, C, H, W]) = normalise(random crop
 // (pad) + random horizontal flip of uint8 NHWC image src[idx[r]]); the crop/flip of row r is a hash

@@ -368,6 +368,10 @@ struct RunStats {
   float eps;
   float momentum;
   int groups;
+  // RES: the residual is a PRE-BatchNorm activation whose own per-worker scale / shift ([groups][C])
+  // is applied here (a projection shortcut's BatchNorm folded into this apply pass); nullptr: plain add
+  const float* res_sc;
+  const float* res_sh;
 };
 
 template <bool RES, bool RELU, int DT>
@@ -386,7 +390,8 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
   // instead of once per row (they were 4x the row's own bytes in load instructions)
   const bool fixed = nv <= tch;
   int gl = -1;
-  float sc[8], sf[8];
+  float sc[8], sf[8], rsc[8], rsf[8];
+  const bool raff = RES && rs.res_sc != nullptr;
   if (fixed && row0 + static_cast<int64_t>(kApplyIters) * rp <= R && rp * kApplyIters <= rg) {
     // every row of the workgroup exists and it spans at most two workers: all of this thread's
     // loads are issued before the first use (kApplyIters rows in flight, not one)
@@ -409,6 +414,10 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
       if (g != gl) {
         load8f(scale + static_cast<int64_t>(g) * C + c, sc);
         load8f(shift + static_cast<int64_t>(g) * C + c, sf);
+        if (raff) {
+          load8f(rs.res_sc + static_cast<int64_t>(g) * C + c, rsc);
+          load8f(rs.res_sh + static_cast<int64_t>(g) * C + c, rsf);
+        }
         gl = g;
       }
       const int64_t off = row * C + c;
@@ -419,6 +428,10 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
       if constexpr (RES) {
         float r[8];
         unpack8(rr[it], r);
+        if (raff) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) r[i] = r[i] * rsc[i] + rsf[i];
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] += r[i];
       }
@@ -449,6 +462,10 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
       if (!fixed || g != gl) {
         load8f(scale + static_cast<int64_t>(g) * C + c, sc);
         load8f(shift + static_cast<int64_t>(g) * C + c, sf);
+        if (raff) {
+          load8f(rs.res_sc + static_cast<int64_t>(g) * C + c, rsc);
+          load8f(rs.res_sh + static_cast<int64_t>(g) * C + c, rsf);
+        }
         gl = g;
       }
       float o[8];
@@ -457,6 +474,10 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
       if constexpr (RES) {
         float r[8];
         load8<DT>(res, off, r);
+        if (raff) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) r[i] = r[i] * rsc[i] + rsf[i];
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] += r[i];
       }
@@ -738,7 +759,9 @@ __global__ __launch_bounds__(T) void k_bn_fwd_small(const void* __restrict__ x,
                                                           const float* __restrict__ beta, float eps,
                                                           float* __restrict__ mean, float* __restrict__ istd,
                                                           float* __restrict__ scale, float* __restrict__ shift,
-                                                          void* __restrict__ y, uint8_t* __restrict__ mask) {
+                                                          void* __restrict__ y, uint8_t* __restrict__ mask,
+                                                          const float* __restrict__ res_sc,
+                                                          const float* __restrict__ res_sh) {
   constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH, T>::Vec, kSmallLanes = SmallGeo<CH, T>::Lanes,
                 kSmallIt = SmallGeo<CH, T>::It;
   __shared__ float red[2][kSmallLanes][kSmallCh];
@@ -821,6 +844,13 @@ __global__ __launch_bounds__(T) void k_bn_fwd_small(const void* __restrict__ x,
     if constexpr (RES) {
       float rr[8];
       load8<DT>(res, off, rr);
+      if (res_sc) {   // a pre-BatchNorm residual: its BatchNorm's scale / shift applied here
+        float ra[8], rb[8];
+        load8f(res_sc + static_cast<int64_t>(g) * C + c0, ra);
+        load8f(res_sh + static_cast<int64_t>(g) * C + c0, rb);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rr[i] = rr[i] * ra[i] + rb[i];
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] += rr[i];
     }
@@ -962,14 +992,14 @@ __global__ __launch_bounds__(kThreads) void k_running(RunJobs jobs) {
 template <int CH, int DT>
 void launch_fwd_small(const void* x, const void* res, int64_t rg, int groups, int C, const float* gamma,
                       const float* beta, float eps, float* mean, float* istd, float* scale, float* shift, void* y,
-                      bool relu, uint8_t* mask, hipStream_t stream) {
+                      bool relu, uint8_t* mask, hipStream_t stream, const float* res_sc, const float* res_sh) {
   const dim3 sgrid((C + CH - 1) / CH, groups);
   if (res) {
-    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, true, true, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
-    else hipLaunchKernelGGL((k_bn_fwd_small<CH, true, false, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, true, true, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask, res_sc, res_sh);
+    else hipLaunchKernelGGL((k_bn_fwd_small<CH, true, false, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr, res_sc, res_sh);
   } else {
-    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, false, true, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask);
-    else hipLaunchKernelGGL((k_bn_fwd_small<CH, false, false, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr);
+    if (relu) hipLaunchKernelGGL((k_bn_fwd_small<CH, false, true, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, mask, res_sc, res_sh);
+    else hipLaunchKernelGGL((k_bn_fwd_small<CH, false, false, DT>), sgrid, dim3(small_threads<CH>()), 0, stream, x, res, rg, C, gamma, beta, eps, mean, istd, scale, shift, y, nullptr, res_sc, res_sh);
   }
 }
 
@@ -993,12 +1023,13 @@ template <int DT>
 void forward_dt(const void* x, const void* res, int64_t rg, int groups, int C, const float* gamma,
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
                 float* mean, float* istd, float* scale, float* shift, void* y, bool relu, uint8_t* mask,
-                bool defer_running, hipStream_t stream, const float* tile_stats, int64_t tile_m, int tile_e) {
+                bool defer_running, hipStream_t stream, const float* tile_stats, int64_t tile_m, int tile_e,
+                const float* res_sc, const float* res_sh) {
   if (rg <= kSmallRows && tile_stats == nullptr) {
     switch (small_ch_for(C, groups)) {
-      case 8: launch_fwd_small<8, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream); break;
-      case 16: launch_fwd_small<16, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream); break;
-      default: launch_fwd_small<32, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream); break;
+      case 8: launch_fwd_small<8, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream, res_sc, res_sh); break;
+      case 16: launch_fwd_small<16, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream, res_sc, res_sh); break;
+      default: launch_fwd_small<32, DT>(x, res, rg, groups, C, gamma, beta, eps, mean, istd, scale, shift, y, relu, mask, stream, res_sc, res_sh); break;
     }
     if (run_mean && !defer_running) {
       RunJobs jobs{};
@@ -1028,7 +1059,7 @@ void forward_dt(const void* x, const void* res, int64_t rg, int groups, int C, c
     }
     return;
   }
-  const RunStats rs{mean, istd, run_mean, run_var, eps, momentum, groups};
+  const RunStats rs{mean, istd, run_mean, run_var, eps, momentum, groups, res_sc, res_sh};
   int tch, rp;
   apply_geometry(C, &tch, &rp);
   const int64_t R = rg * groups;
@@ -1092,13 +1123,15 @@ void bn_forward(const void* x, const void* res, int64_t rg, int groups, int C, c
                 const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* part,
                 float* mean, float* istd, float* scale, float* shift, void* y, bool relu, uint8_t* mask,
                 bool defer_running, hipStream_t stream, const float* tile_stats, int64_t tile_m,
-                int tile_e, int dt) {
+                int tile_e, int dt, const float* res_sc, const float* res_sh) {
   if (dt == kF32)
     forward_dt<kF32>(x, res, rg, groups, C, gamma, beta, eps, momentum, run_mean, run_var, part, mean, istd, scale,
-                     shift, y, relu, mask, defer_running, stream, tile_stats, tile_m, tile_e);
+                     shift, y, relu, mask, defer_running, stream, tile_stats, tile_m, tile_e, res_sc,
+                     res_sh);
   else
     forward_dt<kBF16>(x, res, rg, groups, C, gamma, beta, eps, momentum, run_mean, run_var, part, mean, istd, scale,
-                      shift, y, relu, mask, defer_running, stream, tile_stats, tile_m, tile_e);
+                      shift, y, relu, mask, defer_running, stream, tile_stats, tile_m, tile_e, res_sc,
+                     res_sh);
 }
 
 void bn_backward(const void* x, const void* dy, const void* y, const uint8_t* mask, int64_t rg, int groups,

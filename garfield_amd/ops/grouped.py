@@ -91,6 +91,10 @@ SMALL_CONV = os.environ.get("GARFIELD_SMALL_CONV", "1") == "1"
 # that BatchNorm's backward when the block's conv1 is a 1x1 GEMM: conv1's data-gradient epilogue adds
 # dy where the forward's ReLU bit is set (gpu_gemm_nt add_mask), saving dres's write and re-read (MaskedGrad).
 LAZY_RES = os.environ.get("GARFIELD_LAZY_RES", "1") == "1"
+# A projection block's shortcut BatchNorm folded into the block's last BatchNorm (statistics pass only,
+# its scale / shift applied to the pre-BatchNorm shortcut inside the last BatchNorm's apply pass, its
+# backward run there too): the shortcut's normalised activation is never written (_GroupedBN res_st).
+FOLD_SHORTCUT_BN = os.environ.get("GARFIELD_FOLD_SHORTCUT_BN", "1") == "1"
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -384,10 +388,34 @@ def _bn_bwd_ref(x2, dy2, y2, st: BNState, need_res: bool):
     return dx.reshape(-1, st.C).to(x2.dtype), dres
 
 
+def _bn_forward_gpu(x2: torch.Tensor, r2, st: BNState, ws: Workspace, y2, relu_state, res_st: "BNState | None" = None):
+    """One grouped BatchNorm forward on the HIP kernels; y2 None: statistics only (scale / shift for a
+    consumer that applies them itself); ``res_st``: r2 is the pre-BatchNorm input of that (shortcut)
+    BatchNorm, whose scale / shift the apply pass applies to it."""
+    bn = st.bn
+    C = x2.shape[1]
+    rg = x2.shape[0] // st.groups
+    C_ = _native.native()
+    part = ws.get("bn_part", C_.bn_part_floats(rg, st.groups, C), x2.device)
+    track = bn.track_running_stats and bn.running_mean is not None
+    tile, st.tile = st.tile, None
+    defer = bool(track and ws.defer_running and C_.bn_small(rg) and tile is None)
+    C_.gpu_bn_forward(x2, r2, st.groups, bn.weight, bn.bias, float(bn.eps), float(bn.momentum),
+                      bn.running_mean if track else None, bn.running_var if track else None,
+                      part, st.mean, st.istd, st.scale, st.shift, y2, st.relu and y2 is not None, relu_state, defer,
+                      tile_stats=tile[0] if tile is not None else None,
+                      tile_m=tile[1] if tile is not None else 0, tile_e=tile[2] if tile is not None else 1,
+                      res_scale=res_st.scale if res_st is not None else None,
+                      res_shift=res_st.shift if res_st is not None else None)
+    if defer:
+        ws.running_jobs.append((st.mean, st.istd, bn.running_mean, bn.running_var, rg, float(bn.eps),
+                                float(bn.momentum)))
+
+
 class _GroupedBN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, res, st: BNState, ws: Workspace, join: GradJoin | None = None,
-                res_link: ResLink | None = None, out_link: ResLink | None = None):
+                res_link: ResLink | None = None, out_link: ResLink | None = None, res_st: BNState | None = None):
         n, C, h, w = x.shape
         x2 = rows2d(x)
         r2 = rows2d(res) if res is not None else None
@@ -396,44 +424,37 @@ class _GroupedBN(torch.autograd.Function):
             if x.dtype not in (torch.bfloat16, torch.float32):
                 raise TypeError("grouped BatchNorm on the GPU takes bf16 or fp32 activations")
             y = torch.empty_like(x, memory_format=torch.channels_last)
-            bn = st.bn
-            rg = x2.shape[0] // st.groups
-            C_ = _native.native()
-            part = ws.get("bn_part", C_.bn_part_floats(rg, st.groups, C), x.device)
-            track = bn.track_running_stats and bn.running_mean is not None
             # the backward's ReLU test reads one bit per element instead of y
             relu_state = torch.empty((x2.numel() // 8,), dtype=torch.uint8, device=x.device) if st.relu else None
-            tile, st.tile = st.tile, None
-            defer = bool(track and ws.defer_running and C_.bn_small(rg) and tile is None)
-            C_.gpu_bn_forward(x2, r2, st.groups, bn.weight, bn.bias, float(bn.eps), float(bn.momentum),
-                              bn.running_mean if track else None, bn.running_var if track else None,
-                              part, st.mean, st.istd, st.scale, st.shift, rows2d(y), st.relu, relu_state, defer,
-                              tile_stats=tile[0] if tile is not None else None,
-                              tile_m=tile[1] if tile is not None else 0, tile_e=tile[2] if tile is not None else 1)
-            if defer:
-                ws.running_jobs.append((st.mean, st.istd, bn.running_mean, bn.running_var, rg, float(bn.eps),
-                                        float(bn.momentum)))
+            if res_st is not None:   # the shortcut BatchNorm: statistics only, applied inside this apply pass
+                if res is None or res_st.relu:
+                    raise ValueError("res_st: a pre-BatchNorm residual without a ReLU of its own")
+                res_st.ensure(x.device, torch.float32)
+                _bn_forward_gpu(r2, None, res_st, ws, None, None)
+            _bn_forward_gpu(x2, r2, st, ws, rows2d(y), relu_state, res_st)
         else:
+            if res_st is not None:
+                raise ValueError("res_st (a folded shortcut BatchNorm) is a GPU path")
             y = from_rows(_bn_fwd_ref(x2, r2, st), n, h, w)
             relu_state = y if st.relu else None
         ctx.st, ctx.ws, ctx.has_res, ctx.join = st, ws, res is not None, join
-        ctx.res_link, ctx.out_link = res_link, out_link
+        ctx.res_link, ctx.out_link, ctx.res_st = res_link, out_link, res_st
         if out_link is not None and x.is_cuda and not st.relu and LAZY_RES:
             ctx.set_materialize_grads(False)     # the output's gradient may arrive through out_link only
             out_link.ok = True
-        ctx.save_for_backward(x, relu_state)
+        ctx.save_for_backward(x, relu_state, res if res_st is not None else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y = ctx.saved_tensors                # y: the ReLU state (bit mask on the GPU, y on the CPU) or None
+        x, y, xs = ctx.saved_tensors            # y: the ReLU state (bit mask on the GPU, y on the CPU) or None
         st, ws = ctx.st, ctx.ws
         n, C, h, w = x.shape
         y2 = (y if y.dim() == 1 else rows2d(y)) if y is not None else None
         if dy is None:                          # a shortcut BatchNorm: dy + ReLU bits through out_link
             m, ctx.out_link.pending = ctx.out_link.pending, None
             if m is None:
-                return (None,) * 9
+                return (None,) * 10
             dy, y2 = m.dy, m.mask               # no ReLU of its own: the bits are its only mask
         dy = _cl(dy)
         x2, dy2 = rows2d(x), rows2d(dy)
@@ -443,8 +464,8 @@ class _GroupedBN(torch.autograd.Function):
             if (ctx.has_res and LAZY_RES and y2 is not None and y2.dim() == 1 and
                     ((ctx.join is not None and ctx.join.lazy) or (ctx.res_link is not None and ctx.res_link.ok))):
                 lazy = MaskedGrad(dy, y2)        # the consumer applies the ReLU bits itself
-            dres = torch.empty_like(x, memory_format=torch.channels_last) if (ctx.has_res and lazy is None) \
-                else None
+            dres = torch.empty_like(x, memory_format=torch.channels_last) \
+                if (ctx.has_res and lazy is None and ctx.res_st is None) else None
             rg = x2.shape[0] // st.groups
             C_ = _native.native()
             part = ws.get("bn_part", C_.bn_part_floats(rg, st.groups, C), x.device)
@@ -457,6 +478,15 @@ class _GroupedBN(torch.autograd.Function):
                 ob = sink.base + sink.offset(bn.bias) if bn.bias is not None else -1
             C_.gpu_bn_backward(x2, dy2, y2, st.groups, bn.weight, st.mean, st.istd, part, coef, rows2d(dx),
                                rows2d(dres) if dres is not None else None, grow, stride, og, ob)
+            if ctx.res_st is not None:           # the folded shortcut BatchNorm: dy + this one's ReLU bits
+                rs_, rbn = ctx.res_st, ctx.res_st.bn
+                dres = torch.empty_like(xs, memory_format=torch.channels_last)
+                ogs = sink.base + sink.offset(rbn.weight) if (sink is not None and rbn.weight is not None) else -1
+                obs = sink.base + sink.offset(rbn.bias) if (sink is not None and rbn.bias is not None) else -1
+                xs2 = rows2d(xs)
+                part = ws.get("bn_part", C_.bn_part_floats(rg, rs_.groups, C), x.device)
+                C_.gpu_bn_backward(xs2, dy2, y2, rs_.groups, rbn.weight, rs_.mean, rs_.istd, part, coef,
+                                   rows2d(dres), None, grow, stride, ogs, obs)
         else:
             dx2, dr2 = _bn_bwd_ref(x2, dy2, y2, st, ctx.has_res)
             dx = from_rows(dx2, n, h, w)
@@ -469,16 +499,19 @@ class _GroupedBN(torch.autograd.Function):
         elif dres is not None and ctx.join is not None:
             ctx.join.park(dres)
             dres = None
-        return dx, None, None, dres, None, None, None, None, None
+        return dx, None, None, dres, None, None, None, None, None, None
 
 
 def grouped_bn(x, st: BNState, ws: Workspace, res=None, res_join: GradJoin | None = None,
-               res_link: ResLink | None = None, out_link: ResLink | None = None):
+               res_link: ResLink | None = None, out_link: ResLink | None = None, res_st: BNState | None = None):
     """y = [relu](BN_per_worker(x) [+ res]); x/res channels_last. With ``res_join``
     the residual's gradient is handed to the join instead of autograd; ``res_link`` / ``out_link``:
-    the block's last BatchNorm / its shortcut BatchNorm of one ResLink (see there)."""
+    the block's last BatchNorm / its shortcut BatchNorm of one ResLink (see there). ``res_st`` (GPU):
+    res is the shortcut convolution's output BEFORE its BatchNorm, which this call folds in (statistics
+    pass, then res * scale + shift inside this apply pass; its backward here too): the shortcut's
+    normalised activation is never written."""
     return _GroupedBN.apply(_cl(x), st.bn.weight, st.bn.bias, _cl(res) if res is not None else None, st, ws,
-                            res_join, res_link, out_link)
+                            res_join, res_link, out_link, res_st)
 
 
 # --------------------------------------------------------------------------- #

@@ -25,6 +25,7 @@ from garfield_amd.ops.grouped import (BNState, ConvSpec, GradJoin, GradSink, Lin
                                       bn_conv_ok, global_avgpool, grouped_bn, grouped_bn_conv, grouped_conv,
                                       grouped_cross_entropy, grouped_linear, grouped_maxpool, refresh_dgrad_weights,
                                       refresh_f32_weights, refresh_sc_weights)
+import garfield_amd.ops.grouped as _gops
 
 
 def supports(model: nn.Module) -> bool:
@@ -118,16 +119,30 @@ class GroupedResNet:
         return grouped_conv(x, self.conv[conv], join)
 
     def _conv_bn(self, x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, join=None, res=None, res_join=None,
-                 res_link=None, out_link=None):
+                 res_link=None, out_link=None, res_st=None):
         """conv -> BatchNorm; the convolution may hand the BatchNorm its statistics (gemm_nt.hip)."""
         st = self._state(bn, relu)
+        y = self._conv_stats(x, conv, st, join)
+        return grouped_bn(y, st, self.ws, res, res_join, res_link, out_link, res_st)
+
+    def _conv_stats(self, x, conv: nn.Conv2d, st, join=None):
+        """The convolution, handing the BatchNorm ``st`` its statistics when its kernel can."""
         spec = self.conv[conv]
         spec.bn_next = st
         try:
-            y = grouped_conv(x, spec, join)
+            return grouped_conv(x, spec, join)
         finally:
             spec.bn_next = None
-        return grouped_bn(y, st, self.ws, res, res_join, res_link, out_link)
+
+    def _shortcut(self, blk, x, join):
+        """A projection block's shortcut: (pre-BatchNorm output, its BatchNorm state) when that BatchNorm
+        is folded into the block's last one (GPU), else (its normalised output, None) and the ResLink."""
+        conv, bn = blk.downsample[0], blk.downsample[1]
+        if _gops.FOLD_SHORTCUT_BN and x.is_cuda and isinstance(bn, nn.BatchNorm2d):
+            st = self._state(bn, False)
+            return self._conv_stats(x, conv, st, join), st, None
+        link = ResLink()   # the shortcut BatchNorm receives the residual gradient as dy + ReLU bits
+        return self._conv_bn(x, conv, bn, False, join, out_link=link), None, link
 
     def _block(self, blk, x):
         # x's two gradient branches (conv1 and the shortcut) are summed inside the
@@ -153,19 +168,16 @@ class GroupedResNet:
                     spec3.bn_next = None
                 if blk.downsample is None:
                     return grouped_bn(y3, st3, self.ws, x, join)
-                link = ResLink()
-                sc = self._conv_bn(x, blk.downsample[0], blk.downsample[1], False, join, out_link=link)
-                return grouped_bn(y3, st3, self.ws, sc, res_link=link)
+                sc, sst, link = self._shortcut(blk, x, join)
+                return grouped_bn(y3, st3, self.ws, sc, res_link=link, res_st=sst)
             out = grouped_bn(x2, st2, self.ws)
             last_conv, last_bn = blk.conv3, blk.bn3
         else:
             last_conv, last_bn = blk.conv2, blk.bn2
         if blk.downsample is None:
             return self._conv_bn(out, last_conv, last_bn, True, res=x, res_join=join)
-        # the shortcut BatchNorm receives the residual gradient as dy + the last BatchNorm's ReLU bits
-        link = ResLink()
-        sc = self._conv_bn(x, blk.downsample[0], blk.downsample[1], False, join, out_link=link)
-        return self._conv_bn(out, last_conv, last_bn, True, res=sc, res_link=link)
+        sc, sst, link = self._shortcut(blk, x, join)
+        return self._conv_bn(out, last_conv, last_bn, True, res=sc, res_link=link, res_st=sst)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         out = []

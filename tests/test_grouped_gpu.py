@@ -512,6 +512,7 @@ def test_lazy_residual_gradient_is_bitwise_the_materialised_one(cuda, monkeypatc
         orig(self, dy, mask)
 
     monkeypatch.setattr(grouped.MaskedGrad, "__init__", rec)
+    monkeypatch.setattr(grouped, "FOLD_SHORTCUT_BN", False)   # the shortcuts through ResLink here
     monkeypatch.setattr(grouped, "LAZY_RES", False)
     _grouped_rows(cuda, name, 4, 16)                # fills the per-shape tuner caches
     a = _grouped_rows(cuda, name, 4, 16)
@@ -523,6 +524,61 @@ def test_lazy_residual_gradient_is_bitwise_the_materialised_one(cuda, monkeypatc
     else:
         assert 3 < len(parked) <= 8                 # ResNet-18: 3 shortcuts + up to 5 identity blocks
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("G,B,H,C,dt", [(8, 16, 4, 64, torch.bfloat16), (4, 8, 2, 256, torch.float32),
+                                        (2, 64, 8, 128, torch.bfloat16), (3, 20, 10, 64, torch.float32)])
+def test_bn_folded_shortcut_matches_fp32_reference(cuda, G, B, H, C, dt):
+    """A projection block's last BatchNorm with the shortcut BatchNorm folded in (res_st): y =
+    relu(BN3(x) + BN_ds(r)) with only BN_ds's statistics pass of its own; forward, both inputs'
+    gradients and both BatchNorms' dgamma / dbeta against fp32 autograd (small and large paths)."""
+    torch.manual_seed(C + G)
+    N = G * B
+    x = (torch.randn(N, C, H, H, device=cuda) * 2 + 0.5).to(dt).contiguous(memory_format=torch.channels_last)
+    r = (torch.randn(N, C, H, H, device=cuda) * 3 - 1).to(dt).contiguous(memory_format=torch.channels_last)
+    bns = [nn.BatchNorm2d(C).to(cuda) for _ in range(2)]
+    for bn in bns:
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+    ld = 8 * C + 64
+    X = torch.zeros(G, ld, device=cuda)
+    offs = {id(bns[0].weight): 0, id(bns[0].bias): 2 * C, id(bns[1].weight): 4 * C, id(bns[1].bias): 6 * C}
+    sink = GradSink(X.view(-1), ld, 0, offs, G)
+    st3, sts = BNState(bns[0], True, sink, G), BNState(bns[1], False, sink, G)
+    ws = Workspace()
+    xin, rin = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    y = grouped_bn(xin, st3, ws, rin, res_st=sts)
+    dy = torch.randn_like(x).contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    x2, r2, dy2 = rows2d(x).float(), rows2d(r).float(), rows2d(dy).float()
+    rows = x2.shape[0] // G
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+    for g in range(G):
+        sl = slice(g * rows, (g + 1) * rows)
+        xg, rg_ = x2[sl].clone().requires_grad_(True), r2[sl].clone().requires_grad_(True)
+        p = [t.detach().clone().requires_grad_(True) for t in (bns[0].weight, bns[0].bias, bns[1].weight, bns[1].bias)]
+        sc = _bn_ref_group(rg_, p[2], p[3], bns[1].eps, None, False)
+        yg = _bn_ref_group(xg, p[0], p[1], bns[0].eps, sc, True)
+        yg.backward(dy2[sl])
+        assert rel(rows2d(y)[sl], yg.detach()) < tol
+        assert rel(rows2d(xin.grad)[sl], xg.grad) < 2 * tol
+        assert rel(rows2d(rin.grad)[sl], rg_.grad) < 2 * tol
+        for k, grad in zip((0, 2, 4, 6), (p[0].grad, p[1].grad, p[2].grad, p[3].grad)):
+            assert rel(X[g, k * C:k * C + C], grad) < 2 * tol, (g, k)
+
+
+def test_folded_shortcut_step_as_accurate_as_separate(cuda, monkeypatch):
+    """FOLD_SHORTCUT_BN: a ResNet-50 step's exchange rows are as close to fp32 autograd as with the
+    shortcut BatchNorm run on its own (the fold skips one bf16 rounding of the shortcut)."""
+    import garfield_amd.ops.grouped as grouped
+
+    monkeypatch.setattr(grouped, "FOLD_SHORTCUT_BN", False)
+    err_off = _rows_vs_fp32(cuda, "resnet50", 4, 16, True)
+    monkeypatch.setattr(grouped, "FOLD_SHORTCUT_BN", True)
+    err_on = _rows_vs_fp32(cuda, "resnet50", 4, 16, True)
+    for j in range(4):
+        assert err_on[j] < 1.1 * err_off[j] + 0.01, (j, err_on, err_off)
 
 
 @pytest.mark.parametrize("flag", ["SMALL_CONV", "S2_DGRAD"])
