@@ -423,6 +423,58 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
                             defer_running, stream_of(dev), ts, tile_m, static_cast<int>(tile_e), dt, rsc, rsh);
 }
 
+// Backward of a projection block's last BatchNorm (a) and its folded shortcut BatchNorm (b) sharing dz;
+// False when the shapes take the single-kernel small path (the caller then runs two gpu_bn_backward).
+bool g_bn_backward_dual(const at::Tensor& xa, const at::Tensor& xb, const at::Tensor& dy,
+                        const c10::optional<at::Tensor>& mask, int64_t groups, const c10::optional<at::Tensor>& gamma_a,
+                        const c10::optional<at::Tensor>& gamma_b, const at::Tensor& mean_a, const at::Tensor& istd_a,
+                        const at::Tensor& mean_b, const at::Tensor& istd_b, const at::Tensor& part_a,
+                        const at::Tensor& part_b, const at::Tensor& coef_a, const at::Tensor& coef_b,
+                        const at::Tensor& dxa, const at::Tensor& dxb, const c10::optional<at::Tensor>& grow,
+                        int64_t row_stride, int64_t og_a, int64_t ob_a, int64_t og_b, int64_t ob_b) {
+  const auto dev = xa.device();
+  const int dt = check_act_rows(xa, dev, "xa");
+  for (const at::Tensor* t : {&xb, &dy, &dxa, &dxb}) {
+    check_act_rows(*t, dev, "dual operand", dt);
+    TORCH_CHECK(t->sizes() == xa.sizes(), "garfield bn dual: operands must have xa's shape");
+  }
+  const int64_t rg = bn_groups(xa, groups);
+  const int64_t C = xa.size(1);
+  if (!garfield::gpu::bn_small(rg)) {
+    const uint8_t* mp = nullptr;
+    if (mask.has_value() && mask->defined()) {
+      check_relu_mask(*mask, xa);
+      mp = static_cast<const uint8_t*>(mask->data_ptr());
+    }
+    const int G = static_cast<int>(groups);
+    const int64_t pn = garfield::gpu::bn_part_floats(rg, G, static_cast<int>(C));
+    float* pa = ws_vec(part_a, pn, dev, "part_a");
+    float* pb = ws_vec(part_b, pn, dev, "part_b");
+    float* ca = ws_vec(coef_a, 3 * groups * C, dev, "coef_a");
+    float* cb = ws_vec(coef_b, 3 * groups * C, dev, "coef_b");
+    void* gp = nullptr;
+    int gdt = garfield::kF32;
+    if (grow.has_value() && grow->defined()) {
+      TORCH_CHECK(grow->device() == dev && grow->is_contiguous(), "garfield bn dual: grow must be contiguous");
+      gdt = dtype_code(*grow);
+      TORCH_CHECK(gdt != garfield::kF64, "garfield bn dual: grow must be fp32, bf16 or fp16");
+      for (int64_t off : {og_a, ob_a, og_b, ob_b})
+        if (off >= 0)
+          TORCH_CHECK(row_stride >= 0 && (groups - 1) * row_stride + off + C <= grow->numel(),
+                      "garfield bn dual: grow offset ", off, " out of bounds");
+      gp = grow->data_ptr();
+    }
+    c10::hip::HIPGuard guard(dev.index());
+    return garfield::gpu::bn_backward_dual(
+        xa.data_ptr(), xb.data_ptr(), dy.data_ptr(), mp, rg, G, static_cast<int>(C), opt_vec(gamma_a, C, dev, "gamma_a"),
+        opt_vec(gamma_b, C, dev, "gamma_b"), ws_vec(mean_a, groups * C, dev, "mean_a"),
+        ws_vec(istd_a, groups * C, dev, "istd_a"), ws_vec(mean_b, groups * C, dev, "mean_b"),
+        ws_vec(istd_b, groups * C, dev, "istd_b"), pa, pb, ca, cb, dxa.data_ptr(), dxb.data_ptr(), gp, gdt, row_stride,
+        og_a, ob_a, og_b, ob_b, stream_of(dev), dt);
+  }
+  return false;
+}
+
 int xent_dtype(const at::Tensor& t, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 2, "gpu_xent: ", what, " must be a contiguous 2-D GPU tensor");
   if (t.scalar_type() == at::kFloat) return garfield::kF32;
@@ -1953,6 +2005,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mask") = py::none(), py::arg("defer_running") = false, py::arg("tile_stats") = py::none(),
         py::arg("tile_m") = 0, py::arg("tile_e") = 1, py::arg("res_scale") = py::none(),
         py::arg("res_shift") = py::none());
+  m.def("gpu_bn_backward_dual", &g_bn_backward_dual,
+        "Backward of a BatchNorm (a) and a folded shortcut BatchNorm (b) sharing dz = dy under mask: one statistics "
+        "pass and one apply pass read dy and the mask once; False (nothing launched) on the small path",
+        py::arg("xa"), py::arg("xb"), py::arg("dy"), py::arg("mask"), py::arg("groups"), py::arg("gamma_a"),
+        py::arg("gamma_b"), py::arg("mean_a"), py::arg("istd_a"), py::arg("mean_b"), py::arg("istd_b"),
+        py::arg("part_a"), py::arg("part_b"), py::arg("coef_a"), py::arg("coef_b"), py::arg("dxa"), py::arg("dxb"),
+        py::arg("grow"), py::arg("row_stride"), py::arg("og_a"), py::arg("ob_a"), py::arg("og_b"), py::arg("ob_b"));
   m.def("bn_small", [](int64_t rg) { return garfield::gpu::bn_small(rg); },
         "True when rg rows per worker take the single-kernel BatchNorm path (whose running statistics "
         "can be deferred to gpu_bn_running_update)");

@@ -33,6 +33,14 @@ struct RunJobs {
   RunJob j[kRunJobs];
   int n;
 };
+// Backward of a projection block's last BatchNorm (a) and its folded shortcut BatchNorm (b), which share
+// dz = dy · [mask bit] (mask nullptr: dz = dy): one statistics pass and one apply pass read dy / mask once.
+// false (nothing launched) on the single-kernel small path (rg <= 1024 rows per worker).
+bool bn_backward_dual(const void* xa, const void* xb, const void* dy, const uint8_t* mask, int64_t rg, int groups,
+                      int C, const float* gamma_a, const float* gamma_b, const float* mean_a, const float* istd_a,
+                      const float* mean_b, const float* istd_b, float* part_a, float* part_b, float* coef_a,
+                      float* coef_b, void* dxa, void* dxb, void* grow, int grow_dt, int64_t row_stride,
+                      int64_t og_a, int64_t ob_a, int64_t og_b, int64_t ob_b, hipStream_t stream, int dt);
 void bn_running_update(const RunJobs& jobs, hipStream_t stream);
 // True when a layer of rg rows per worker takes the single-kernel small-layer path.
 bool bn_small(int64_t rg);

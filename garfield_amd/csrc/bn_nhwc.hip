@@ -625,6 +625,140 @@ __global__ __launch_bounds__(kThreads) void k_bwd_apply(const void* __restrict__
   }
 }
 
+// Dual backward of a projection block's last BatchNorm and its folded shortcut BatchNorm: both see
+// the same dz = dy · [ReLU bit] (RM 2, or RM 0 without a ReLU), so one pass reads dy and the mask once
+// for the two statistics (Σdz is shared: part_a and part_b get the same s, q_a = Σdz(x_a - μ_a),
+// q_b = Σdz(x_b - μ_b)), and one apply pass writes both data gradients.
+template <int RM, int DT>
+__global__ __launch_bounds__(kThreads) void k_partial_dual(const void* __restrict__ xa, const void* __restrict__ xb,
+                                                          const void* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                          const float* __restrict__ mean_a,
+                                                          const float* __restrict__ mean_b, Geo geo,
+                                                          float* __restrict__ part_a, float* __restrict__ part_b) {
+  static_assert(RM == 0 || RM == 2, "dz is dy or dy under the bit mask");
+  __shared__ __attribute__((aligned(16))) float red[3][kThreads * 8];
+  const int C = geo.C;
+  const int tc = threadIdx.x % geo.tch;
+  const int tr = threadIdx.x / geo.tch;
+  const int chunk = blockIdx.x, cbk = blockIdx.y, g = blockIdx.z;
+  const int c0 = cbk * geo.cb + tc * 8;
+  const bool lane_ok = tr < geo.rp;
+  const bool active = lane_ok && (c0 < C);
+  const int64_t base = static_cast<int64_t>(g) * geo.rg;
+  const int64_t r0 = static_cast<int64_t>(chunk) * geo.rows_per_chunk;
+  int64_t r1 = r0 + geo.rows_per_chunk;
+  if (r1 > geo.rg) r1 = geo.rg;
+  float s[8], qa[8], qb[8], ma[8], mb[8], dum[8] = {};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s[i] = 0.f; qa[i] = 0.f; qb[i] = 0.f; ma[i] = 0.f; mb[i] = 0.f; }
+  if (active) {
+    load8f(mean_a + static_cast<int64_t>(g) * C + c0, ma);
+    load8f(mean_b + static_cast<int64_t>(g) * C + c0, mb);
+    int64_t r = r0 + tr;
+    for (; r + geo.rp < r1; r += 2 * geo.rp) {
+      const int64_t o0 = (base + r) * C + c0, o1 = o0 + static_cast<int64_t>(geo.rp) * C;
+      float a0[8], a1[8], b0[8], b1[8], d0[8], d1[8];
+      load8<DT>(xa, o0, a0);
+      load8<DT>(xa, o1, a1);
+      load8<DT>(xb, o0, b0);
+      load8<DT>(xb, o1, b1);
+      load8<DT>(dy, o0, d0);
+      load8<DT>(dy, o1, d1);
+      relu_mask8<RM, DT>(d0, a0, nullptr, mask, o0, dum, dum);
+      relu_mask8<RM, DT>(d1, a1, nullptr, mask, o1, dum, dum);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        s[i] += d0[i] + d1[i];
+        qa[i] += d0[i] * (a0[i] - ma[i]) + d1[i] * (a1[i] - ma[i]);
+        qb[i] += d0[i] * (b0[i] - mb[i]) + d1[i] * (b1[i] - mb[i]);
+      }
+    }
+    for (; r < r1; r += geo.rp) {
+      const int64_t o0 = (base + r) * C + c0;
+      float a0[8], b0[8], d0[8];
+      load8<DT>(xa, o0, a0);
+      load8<DT>(xb, o0, b0);
+      load8<DT>(dy, o0, d0);
+      relu_mask8<RM, DT>(d0, a0, nullptr, mask, o0, dum, dum);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { s[i] += d0[i]; qa[i] += d0[i] * (a0[i] - ma[i]); qb[i] += d0[i] * (b0[i] - mb[i]); }
+    }
+  }
+  if (lane_ok) {
+    float* p0 = &red[0][tr * geo.cb + tc * 8];
+    float* p1 = &red[1][tr * geo.cb + tc * 8];
+    float* p2 = &red[2][tr * geo.cb + tc * 8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { p0[i] = s[i]; p1[i] = qa[i]; p2[i] = qb[i]; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < geo.cb; c += kThreads) {
+    const int cc = cbk * geo.cb + c;
+    if (cc >= C) continue;
+    float a = 0.f, b = 0.f, e = 0.f;
+    for (int t = 0; t < geo.rp; ++t) { a += red[0][t * geo.cb + c]; b += red[1][t * geo.cb + c]; e += red[2][t * geo.cb + c]; }
+    const int64_t o = (static_cast<int64_t>(g) * geo.chunks + chunk) * 2 * C;
+    part_a[o + cc] = a;
+    part_a[o + C + cc] = b;
+    part_b[o + cc] = a;
+    part_b[o + C + cc] = e;
+  }
+}
+
+template <int RM, int DT>
+__global__ __launch_bounds__(kThreads) void k_bwd_apply_dual(const void* __restrict__ xa, const void* __restrict__ xb,
+                                                            const void* __restrict__ dy,
+                                                            const uint8_t* __restrict__ mask,
+                                                            const float* __restrict__ mean_a,
+                                                            const float* __restrict__ mean_b,
+                                                            const float* __restrict__ coef_a,
+                                                            const float* __restrict__ coef_b, int64_t rg, int64_t R,
+                                                            int C, int tch, int rp, void* __restrict__ dxa,
+                                                            void* __restrict__ dxb) {
+  const int tr = threadIdx.x / tch;
+  if (tr >= rp) return;
+  const int nv = C / 8;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * rp * kApplyIters;
+  const bool fixed = nv <= tch;   // one channel group per thread: its coefficients once per worker
+  int gl = -1;
+  float dum[8] = {}, mua[8], mub[8], caa[8], cba[8], cca[8], cab[8], cbb[8], ccb[8];
+  for (int it = 0; it < kApplyIters; ++it) {
+    const int64_t row = row0 + static_cast<int64_t>(it) * rp + tr;
+    if (row >= R) break;
+    const int g = static_cast<int>(row / rg);
+    const float* ga = coef_a + static_cast<int64_t>(g) * 3 * C;
+    const float* gb = coef_b + static_cast<int64_t>(g) * 3 * C;
+    for (int v = threadIdx.x % tch; v < nv; v += tch) {
+      const int c = v * 8;
+      const int64_t off = row * C + c;
+      float a[8], b[8], d[8];
+      load8<DT>(xa, off, a);
+      load8<DT>(xb, off, b);
+      load8<DT>(dy, off, d);
+      if (!fixed || g != gl) {
+        load8f(mean_a + static_cast<int64_t>(g) * C + c, mua);
+        load8f(mean_b + static_cast<int64_t>(g) * C + c, mub);
+        load8f(ga + c, caa);
+        load8f(ga + C + c, cba);
+        load8f(ga + 2 * C + c, cca);
+        load8f(gb + c, cab);
+        load8f(gb + C + c, cbb);
+        load8f(gb + 2 * C + c, ccb);
+        gl = g;
+      }
+      relu_mask8<RM, DT>(d, a, nullptr, mask, off, dum, dum);
+      float oa[8], ob[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        oa[i] = caa[i] * (d[i] - cba[i] - (a[i] - mua[i]) * cca[i]);
+        ob[i] = cab[i] * (d[i] - cbb[i] - (b[i] - mub[i]) * ccb[i]);
+      }
+      store_vec<8>(dxa, DT, off, oa);
+      store_vec<8>(dxb, DT, off, ob);
+    }
+  }
+}
+
 void apply_geometry(int C, int* tch, int* rp) {
   int t = C / 8;
   if (t > kThreads) t = kThreads;
@@ -1112,6 +1246,38 @@ void backward_dt(const void* x, const void* dy, const void* y, const uint8_t* ma
 #undef GARFIELD_BWD_APPLY
 }
 
+template <int DT>
+void backward_dual_dt(const void* xa, const void* xb, const void* dy, const uint8_t* mask, int64_t rg, int groups,
+                      int C, const float* gamma_a, const float* gamma_b, const float* mean_a, const float* istd_a,
+                      const float* mean_b, const float* istd_b, float* part_a, float* part_b, float* coef_a,
+                      float* coef_b, void* dxa, void* dxb, void* grow, int grow_dt, int64_t row_stride,
+                      int64_t og_a, int64_t ob_a, int64_t og_b, int64_t ob_b, hipStream_t stream) {
+  const Geo g = geometry(rg, groups, C);
+  const int ncb = (C + g.cb - 1) / g.cb;
+  const dim3 pgrid(g.chunks, ncb, groups);
+  if (mask)
+    hipLaunchKernelGGL((k_partial_dual<2, DT>), pgrid, dim3(kThreads), 0, stream, xa, xb, dy, mask, mean_a, mean_b, g,
+                       part_a, part_b);
+  else
+    hipLaunchKernelGGL((k_partial_dual<0, DT>), pgrid, dim3(kThreads), 0, stream, xa, xb, dy, mask, mean_a, mean_b, g,
+                       part_a, part_b);
+  const dim3 fgrid((C + kFin - 1) / kFin, groups);
+  hipLaunchKernelGGL(k_bwd_finalize<kFin>, fgrid, dim3(kThreads), 0, stream, part_a, g, gamma_a, istd_a, coef_a, grow,
+                     grow_dt, row_stride, og_a, ob_a);
+  hipLaunchKernelGGL(k_bwd_finalize<kFin>, fgrid, dim3(kThreads), 0, stream, part_b, g, gamma_b, istd_b, coef_b, grow,
+                     grow_dt, row_stride, og_b, ob_b);
+  int tch, rp;
+  apply_geometry(C, &tch, &rp);
+  const int64_t R = rg * groups;
+  const dim3 grid = apply_grid(R, rp);
+  if (mask)
+    hipLaunchKernelGGL((k_bwd_apply_dual<2, DT>), grid, dim3(kThreads), 0, stream, xa, xb, dy, mask, mean_a, mean_b,
+                       coef_a, coef_b, rg, R, C, tch, rp, dxa, dxb);
+  else
+    hipLaunchKernelGGL((k_bwd_apply_dual<0, DT>), grid, dim3(kThreads), 0, stream, xa, xb, dy, mask, mean_a, mean_b,
+                       coef_a, coef_b, rg, R, C, tch, rp, dxa, dxb);
+}
+
 }  // namespace
 
 int64_t bn_part_floats(int64_t rg, int groups, int C) {
@@ -1144,6 +1310,22 @@ void bn_backward(const void* x, const void* dy, const void* y, const uint8_t* ma
   else
     backward_dt<kBF16>(x, dy, y, mask, rg, groups, C, gamma, mean, istd, part, coef, dx, dres, grow, grow_dt,
                        row_stride, off_gamma, off_beta, stream, rsc, rsh);
+}
+
+bool bn_backward_dual(const void* xa, const void* xb, const void* dy, const uint8_t* mask, int64_t rg, int groups,
+                      int C, const float* gamma_a, const float* gamma_b, const float* mean_a, const float* istd_a,
+                      const float* mean_b, const float* istd_b, float* part_a, float* part_b, float* coef_a,
+                      float* coef_b, void* dxa, void* dxb, void* grow, int grow_dt, int64_t row_stride,
+                      int64_t og_a, int64_t ob_a, int64_t og_b, int64_t ob_b, hipStream_t stream, int dt) {
+  if (rg <= kSmallRows) return false;   // the single-kernel small path runs the two backwards separately
+  if (dt == kF32)
+    backward_dual_dt<kF32>(xa, xb, dy, mask, rg, groups, C, gamma_a, gamma_b, mean_a, istd_a, mean_b, istd_b, part_a,
+                           part_b, coef_a, coef_b, dxa, dxb, grow, grow_dt, row_stride, og_a, ob_a, og_b, ob_b, stream);
+  else
+    backward_dual_dt<kBF16>(xa, xb, dy, mask, rg, groups, C, gamma_a, gamma_b, mean_a, istd_a, mean_b, istd_b, part_a,
+                            part_b, coef_a, coef_b, dxa, dxb, grow, grow_dt, row_stride, og_a, ob_a, og_b, ob_b,
+                            stream);
+  return true;
 }
 
 void bn_running_update(const RunJobs& jobs, hipStream_t stream) {

@@ -95,6 +95,8 @@ LAZY_RES = os.environ.get("GARFIELD_LAZY_RES", "1") == "1"
 # its scale / shift applied to the pre-BatchNorm shortcut inside the last BatchNorm's apply pass, its
 # backward run there too): the shortcut's normalised activation is never written (_GroupedBN res_st).
 FOLD_SHORTCUT_BN = os.environ.get("GARFIELD_FOLD_SHORTCUT_BN", "1") == "1"
+# ... and its backward shares one statistics pass and one apply pass with the last BatchNorm's (large layers)
+BN_DUAL = os.environ.get("GARFIELD_BN_DUAL", "1") == "1"
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -476,17 +478,26 @@ class _GroupedBN(torch.autograd.Function):
                 grow, stride = sink.flat, sink.row_stride
                 og = sink.base + sink.offset(bn.weight) if bn.weight is not None else -1
                 ob = sink.base + sink.offset(bn.bias) if bn.bias is not None else -1
-            C_.gpu_bn_backward(x2, dy2, y2, st.groups, bn.weight, st.mean, st.istd, part, coef, rows2d(dx),
-                               rows2d(dres) if dres is not None else None, grow, stride, og, ob)
+            done = False
             if ctx.res_st is not None:           # the folded shortcut BatchNorm: dy + this one's ReLU bits
                 rs_, rbn = ctx.res_st, ctx.res_st.bn
                 dres = torch.empty_like(xs, memory_format=torch.channels_last)
                 ogs = sink.base + sink.offset(rbn.weight) if (sink is not None and rbn.weight is not None) else -1
                 obs = sink.base + sink.offset(rbn.bias) if (sink is not None and rbn.bias is not None) else -1
                 xs2 = rows2d(xs)
-                part = ws.get("bn_part", C_.bn_part_floats(rg, rs_.groups, C), x.device)
-                C_.gpu_bn_backward(xs2, dy2, y2, rs_.groups, rbn.weight, rs_.mean, rs_.istd, part, coef,
-                                   rows2d(dres), None, grow, stride, ogs, obs)
+                if BN_DUAL and (y2 is None or y2.dim() == 1):  # one statistics / apply pass for both
+                    part_b = ws.get("bn_part2", C_.bn_part_floats(rg, st.groups, C), x.device)
+                    coef_b = ws.get("bn_coef2", 3 * st.groups * C, x.device)
+                    done = C_.gpu_bn_backward_dual(x2, xs2, dy2, y2, st.groups, bn.weight, rbn.weight, st.mean,
+                                                   st.istd, rs_.mean, rs_.istd, part, part_b, coef, coef_b,
+                                                   rows2d(dx), rows2d(dres), grow, stride, og, ob, ogs, obs)
+            if not done:
+                C_.gpu_bn_backward(x2, dy2, y2, st.groups, bn.weight, st.mean, st.istd, part, coef, rows2d(dx),
+                                   rows2d(dres) if (dres is not None and ctx.res_st is None) else None, grow, stride,
+                                   og, ob)
+                if ctx.res_st is not None:
+                    C_.gpu_bn_backward(xs2, dy2, y2, rs_.groups, rbn.weight, rs_.mean, rs_.istd, part, coef,
+                                       rows2d(dres), None, grow, stride, ogs, obs)
         else:
             dx2, dr2 = _bn_bwd_ref(x2, dy2, y2, st, ctx.has_res)
             dx = from_rows(dx2, n, h, w)
