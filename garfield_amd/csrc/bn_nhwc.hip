@@ -499,12 +499,11 @@ __global__ __launch_bounds__(kThreads) void k_fwd_apply(const void* __restrict__
 // Backward finalize of one (group, 64-channel block): dγ, dβ -> exchange rows;
 // apply coefficients.
 template <int FC>
-__global__ __launch_bounds__(kThreads) void k_bwd_finalize(const float* __restrict__ part, Geo geo,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ istd,
-                                                          float* __restrict__ coef, void* grow, int grow_dt,
-                                                          int64_t row_stride, int64_t off_gamma, int64_t off_beta) {
-  __shared__ float sred[kThreads], qred[kThreads];
+__device__ __forceinline__ void bwd_finalize_body(const float* __restrict__ part, const Geo& geo,
+                                                  const float* __restrict__ gamma, const float* __restrict__ istd,
+                                                  float* __restrict__ coef, void* grow, int grow_dt,
+                                                  int64_t row_stride, int64_t off_gamma, int64_t off_beta,
+                                                  float* sred, float* qred) {
   const int C = geo.C;
   const int g = blockIdx.y;
   const int c = blockIdx.x * FC + threadIdx.x % FC;
@@ -524,6 +523,33 @@ __global__ __launch_bounds__(kThreads) void k_bwd_finalize(const float* __restri
   coef[o3 + c] = (gamma ? gamma[c] : 1.f) * is;  // a
   coef[o3 + C + c] = dbeta / M;                 // b
   coef[o3 + 2 * C + c] = dgamma / M * is;       // c  (x̂·dγ/M = (x-μ)·c)
+}
+
+template <int FC>
+__global__ __launch_bounds__(kThreads) void k_bwd_finalize(const float* __restrict__ part, Geo geo,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ istd,
+                                                          float* __restrict__ coef, void* grow, int grow_dt,
+                                                          int64_t row_stride, int64_t off_gamma, int64_t off_beta) {
+  __shared__ float sred[kThreads], qred[kThreads];
+  bwd_finalize_body<FC>(part, geo, gamma, istd, coef, grow, grow_dt, row_stride, off_gamma, off_beta, sred, qred);
+}
+
+// the two BatchNorms of a dual backward in one launch (blockIdx.z: 0 = a, 1 = b)
+struct FinJob {
+  const float* part;
+  const float* gamma;
+  const float* istd;
+  float* coef;
+  int64_t off_gamma, off_beta;
+};
+template <int FC>
+__global__ __launch_bounds__(kThreads) void k_bwd_finalize_dual(FinJob ja, FinJob jb, Geo geo, void* grow, int grow_dt,
+                                                               int64_t row_stride) {
+  __shared__ float sred[kThreads], qred[kThreads];
+  const FinJob& j = blockIdx.z ? jb : ja;
+  bwd_finalize_body<FC>(j.part, geo, j.gamma, j.istd, j.coef, grow, grow_dt, row_stride, j.off_gamma, j.off_beta,
+                        sred, qred);
 }
 
 template <int RM, bool RES_OUT, int DT>
@@ -1261,11 +1287,10 @@ void backward_dual_dt(const void* xa, const void* xb, const void* dy, const uint
   else
     hipLaunchKernelGGL((k_partial_dual<0, DT>), pgrid, dim3(kThreads), 0, stream, xa, xb, dy, mask, mean_a, mean_b, g,
                        part_a, part_b);
-  const dim3 fgrid((C + kFin - 1) / kFin, groups);
-  hipLaunchKernelGGL(k_bwd_finalize<kFin>, fgrid, dim3(kThreads), 0, stream, part_a, g, gamma_a, istd_a, coef_a, grow,
-                     grow_dt, row_stride, og_a, ob_a);
-  hipLaunchKernelGGL(k_bwd_finalize<kFin>, fgrid, dim3(kThreads), 0, stream, part_b, g, gamma_b, istd_b, coef_b, grow,
-                     grow_dt, row_stride, og_b, ob_b);
+  const dim3 fgrid((C + kFin - 1) / kFin, groups, 2);
+  hipLaunchKernelGGL(k_bwd_finalize_dual<kFin>, fgrid, dim3(kThreads), 0, stream,
+                     FinJob{part_a, gamma_a, istd_a, coef_a, og_a, ob_a}, FinJob{part_b, gamma_b, istd_b, coef_b, og_b, ob_b},
+                     g, grow, grow_dt, row_stride);
   int tch, rp;
   apply_geometry(C, &tch, &rp);
   const int64_t R = rg * groups;
