@@ -440,7 +440,7 @@ bool g_bn_backward_dual(const at::Tensor& xa, const at::Tensor& xb, const at::Te
   }
   const int64_t rg = bn_groups(xa, groups);
   const int64_t C = xa.size(1);
-  if (!garfield::gpu::bn_small(rg)) {
+  {
     const uint8_t* mp = nullptr;
     if (mask.has_value() && mask->defined()) {
       check_relu_mask(*mask, xa);
@@ -472,7 +472,6 @@ bool g_bn_backward_dual(const at::Tensor& xa, const at::Tensor& xb, const at::Te
         ws_vec(istd_b, groups * C, dev, "istd_b"), pa, pb, ca, cb, dxa.data_ptr(), dxb.data_ptr(), gp, gdt, row_stride,
         og_a, ob_a, og_b, ob_b, stream_of(dev), dt);
   }
-  return false;
 }
 
 int xent_dtype(const at::Tensor& t, const char* what) {
@@ -2007,7 +2006,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res_shift") = py::none());
   m.def("gpu_bn_backward_dual", &g_bn_backward_dual,
         "Backward of a BatchNorm (a) and a folded shortcut BatchNorm (b) sharing dz = dy under mask: one statistics "
-        "pass and one apply pass read dy and the mask once; False (nothing launched) on the small path",
+        "pass and one apply pass (or one single-kernel workgroup per channel group on small layers) read dy and the "
+        "mask once; returns True",
         py::arg("xa"), py::arg("xb"), py::arg("dy"), py::arg("mask"), py::arg("groups"), py::arg("gamma_a"),
         py::arg("gamma_b"), py::arg("mean_a"), py::arg("istd_a"), py::arg("mean_b"), py::arg("istd_b"),
         py::arg("part_a"), py::arg("part_b"), py::arg("coef_a"), py::arg("coef_b"), py::arg("dxa"), py::arg("dxb"),

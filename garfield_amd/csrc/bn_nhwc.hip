@@ -1130,6 +1130,130 @@ __global__ __launch_bounds__(T) void k_bn_bwd_small(
   }
 }
 
+// Dual form of the above for a projection block's last BatchNorm (a) and its folded shortcut BatchNorm
+// (b), which share dz: x_a, x_b and dz rows held in registers, Σdz shared, both finalizes in the same
+// workgroup, both data gradients from one read of dy and the mask.
+template <int CH, int RM, int DT, int T = small_threads<CH>()>
+__global__ __launch_bounds__(T) void k_bn_bwd_small_dual(
+    const void* __restrict__ xa, const void* __restrict__ xb, const void* __restrict__ dy,
+    const uint8_t* __restrict__ mask, int64_t rg, int C, const float* __restrict__ gamma_a,
+    const float* __restrict__ mean_a, const float* __restrict__ istd_a, const float* __restrict__ gamma_b,
+    const float* __restrict__ mean_b, const float* __restrict__ istd_b, void* __restrict__ dxa,
+    void* __restrict__ dxb, void* grow, int grow_dt, int64_t row_stride, int64_t oga, int64_t oba, int64_t ogb,
+    int64_t obb) {
+  static_assert(RM == 0 || RM == 2, "dz is dy or dy under the bit mask");
+  constexpr int kSmallCh = CH, kSmallVec = SmallGeo<CH, T>::Vec, kSmallLanes = SmallGeo<CH, T>::Lanes,
+                kSmallIt = SmallGeo<CH, T>::It;
+  __shared__ float red[2][kSmallLanes][kSmallCh];
+  __shared__ float sA[kSmallCh], la[2][kSmallCh], lb[2][kSmallCh], lc[2][kSmallCh];
+  const int tc = threadIdx.x % kSmallVec, tr = threadIdx.x / kSmallVec;
+  int cg, g;
+  small_block(cg, g);
+  const int c0 = cg * kSmallCh + tc * 8;
+  const bool act = c0 < C;
+  const int64_t base = static_cast<int64_t>(g) * rg;
+  Raw8<DT> xra[kSmallIt], xrb[kSmallIt], dr[kSmallIt];
+  float A[8], Ba[8], Bb[8], mua[8], mub[8];
+  float fis[2] = {0.f, 0.f}, fg[2] = {1.f, 1.f};   // the finalize thread's operands, loaded up front
+  if (threadIdx.x < kSmallCh && cg * kSmallCh + static_cast<int>(threadIdx.x) < C) {
+    const int c = cg * kSmallCh + threadIdx.x;
+    fis[0] = istd_a[static_cast<int64_t>(g) * C + c];
+    fis[1] = istd_b[static_cast<int64_t>(g) * C + c];
+    fg[0] = gamma_a ? gamma_a[c] : 1.f;
+    fg[1] = gamma_b ? gamma_b[c] : 1.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { A[i] = 0.f; Ba[i] = 0.f; Bb[i] = 0.f; mua[i] = 0.f; mub[i] = 0.f; }
+  if (act) {
+    load8f(mean_a + static_cast<int64_t>(g) * C + c0, mua);
+    load8f(mean_b + static_cast<int64_t>(g) * C + c0, mub);
+#pragma unroll
+    for (int it = 0; it < kSmallIt; ++it) {
+      const int64_t r = tr + it * kSmallLanes;
+      if (r < rg) {
+        const int64_t off = (base + r) * C + c0;
+        xra[it] = ld_raw8<DT>(xa, off);
+        xrb[it] = ld_raw8<DT>(xb, off);
+        Raw8<DT> d = ld_raw8<DT>(dy, off);
+        if constexpr (RM == 2) d = keep_bits(d, mask[off >> 3]);
+        dr[it] = d;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < kSmallIt; ++it) {
+      if (tr + it * kSmallLanes < rg) {
+        float a[8], b[8], d[8];
+        unpack8(xra[it], a);
+        unpack8(xrb[it], b);
+        unpack8(dr[it], d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { A[i] += d[i]; Ba[i] += d[i] * (a[i] - mua[i]); Bb[i] += d[i] * (b[i] - mub[i]); }
+      }
+    }
+  }
+  // Σdz and Σdz(x_a - μ_a), then Σdz(x_b - μ_b) (in red[1] again)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[0][tr][tc * 8 + i] = A[i]; red[1][tr][tc * 8 + i] = Ba[i]; }
+  __syncthreads();
+  small_reduce<CH, T, kSmallLanes>(red);
+  float SA = 0.f, SBa = 0.f;
+  if (threadIdx.x < kSmallCh) { SA = red[0][0][threadIdx.x]; SBa = red[1][0][threadIdx.x]; }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { red[0][tr][tc * 8 + i] = 0.f; red[1][tr][tc * 8 + i] = Bb[i]; }
+  __syncthreads();
+  small_reduce<CH, T, kSmallLanes>(red);
+  if (threadIdx.x < kSmallCh) {
+    const int c = cg * kSmallCh + threadIdx.x;
+    const float SBb = red[1][0][threadIdx.x];
+    const float M = static_cast<float>(rg);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float ca = 0.f, cb = 0.f, cc = 0.f;
+      if (c < C) {
+        const float is = fis[k];
+        const float dgamma = (k == 0 ? SBa : SBb) * is, dbeta = SA;
+        const int64_t og = k == 0 ? oga : ogb, ob = k == 0 ? oba : obb;
+        if (grow) {
+          if (og >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + og + c, dgamma);
+          if (ob >= 0) store_one(grow, grow_dt, static_cast<int64_t>(g) * row_stride + ob + c, dbeta);
+        }
+        ca = fg[k] * is;
+        cb = dbeta / M;
+        cc = dgamma / M * is;
+      }
+      la[k][threadIdx.x] = ca;
+      lb[k][threadIdx.x] = cb;
+      lc[k][threadIdx.x] = cc;
+    }
+  }
+  __syncthreads();
+  if (!act) return;
+  float caa[8], cba[8], cca[8], cab[8], cbb[8], ccb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    caa[i] = la[0][tc * 8 + i]; cba[i] = lb[0][tc * 8 + i]; cca[i] = lc[0][tc * 8 + i];
+    cab[i] = la[1][tc * 8 + i]; cbb[i] = lb[1][tc * 8 + i]; ccb[i] = lc[1][tc * 8 + i];
+  }
+#pragma unroll
+  for (int it = 0; it < kSmallIt; ++it) {
+    const int64_t r = tr + it * kSmallLanes;
+    if (r >= rg) break;
+    const int64_t off = (base + r) * C + c0;
+    float a[8], b[8], d[8], oa[8], ob[8];
+    unpack8(xra[it], a);
+    unpack8(xrb[it], b);
+    unpack8(dr[it], d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      oa[i] = caa[i] * (d[i] - cba[i] - (a[i] - mua[i]) * cca[i]);
+      ob[i] = cab[i] * (d[i] - cbb[i] - (b[i] - mub[i]) * ccb[i]);
+    }
+    store_vec<8>(dxa, DT, off, oa);
+    store_vec<8>(dxb, DT, off, ob);
+  }
+}
+
 // Running statistics of up to kRunJobs layers in one launch (blockIdx.y = layer).
 __global__ __launch_bounds__(kThreads) void k_running(RunJobs jobs) {
   const RunJob& j = jobs.j[blockIdx.y];
@@ -1342,7 +1466,28 @@ bool bn_backward_dual(const void* xa, const void* xb, const void* dy, const uint
                       const float* mean_b, const float* istd_b, float* part_a, float* part_b, float* coef_a,
                       float* coef_b, void* dxa, void* dxb, void* grow, int grow_dt, int64_t row_stride,
                       int64_t og_a, int64_t ob_a, int64_t og_b, int64_t ob_b, hipStream_t stream, int dt) {
-  if (rg <= kSmallRows) return false;   // the single-kernel small path runs the two backwards separately
+  if (rg <= kSmallRows) {   // the single-kernel small path, both BatchNorms in one workgroup
+    const int ch = small_ch_for(C, groups);
+    const int rm = mask ? 2 : 0;
+#define GARFIELD_DUAL_SMALL(CHV, RMV, DTV)                                                                          \
+  hipLaunchKernelGGL((k_bn_bwd_small_dual<CHV, RMV, DTV>), dim3((C + CHV - 1) / CHV, groups),                       \
+                     dim3(small_threads<CHV>()), 0, stream, xa, xb, dy, mask, rg, C, gamma_a, mean_a, istd_a, gamma_b, \
+                     mean_b, istd_b, dxa, dxb, grow, grow_dt, row_stride, og_a, ob_a, og_b, ob_b)
+#define GARFIELD_DUAL_SMALL_RM(CHV, DTV) \
+  if (rm == 2) GARFIELD_DUAL_SMALL(CHV, 2, DTV); else GARFIELD_DUAL_SMALL(CHV, 0, DTV)
+    if (dt == kF32) {
+      if (ch == 8) { GARFIELD_DUAL_SMALL_RM(8, kF32); }
+      else if (ch == 16) { GARFIELD_DUAL_SMALL_RM(16, kF32); }
+      else { GARFIELD_DUAL_SMALL_RM(32, kF32); }
+    } else {
+      if (ch == 8) { GARFIELD_DUAL_SMALL_RM(8, kBF16); }
+      else if (ch == 16) { GARFIELD_DUAL_SMALL_RM(16, kBF16); }
+      else { GARFIELD_DUAL_SMALL_RM(32, kBF16); }
+    }
+#undef GARFIELD_DUAL_SMALL_RM
+#undef GARFIELD_DUAL_SMALL
+    return true;
+  }
   if (dt == kF32)
     backward_dual_dt<kF32>(xa, xb, dy, mask, rg, groups, C, gamma_a, gamma_b, mean_a, istd_a, mean_b, istd_b, part_a,
                            part_b, coef_a, coef_b, dxa, dxb, grow, grow_dt, row_stride, og_a, ob_a, og_b, ob_b, stream);
