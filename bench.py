@@ -158,6 +158,17 @@ def timed_steps(eng, batches, steps, warmup, ctx, trend=None):
     return elapsed, float(loss)
 
 
+def worker_loss(eng, ctx, loss):
+    """Mean of ``loss`` over the ranks that compute gradients (collective): in the Byzantine-server
+    mode a pure server rank computes none and reports nothing (its 0.0 is not a loss)."""
+    computes = getattr(eng, "computes", True)
+    if not ctx.is_distributed:
+        return loss if computes else None
+    t = torch.tensor([loss if computes else 0.0, 1.0 if computes else 0.0], dtype=torch.float64, device=ctx.device)
+    dist.all_reduce(t)
+    return float(t[0] / t[1]) if float(t[1]) > 0 else None
+
+
 def build_job(a, ctx, model, shape, num_classes, fp32: bool):
     """The engine of the benchmarked job and its batch source; fp32: the reference's precision
     (no autocast, fp32 exchange rows and weights: the grouped NHWC executor on the fp32 kernels)."""
@@ -223,6 +234,8 @@ def main():
         load_engine(a.resume, eng)
     trend = []
     elapsed, loss = timed_steps(eng, batches, a.steps, a.warmup, ctx, trend)
+    loss = worker_loss(eng, ctx, loss)
+    first = worker_loss(eng, ctx, trend[0] if trend else 0.0) if trend else None
     if a.checkpoint:
         from garfield_amd.utils.checkpoint import save_engine
 
@@ -325,8 +338,9 @@ def main():
                 "lp_weights": eng._shadow is not None,
                 "optimizer": f"SGD lr={a.lr} momentum=0.9 wd=5e-4 (fused into the GAR combine kernel)",
             },
-            "final_loss": round(loss, 4),
-            "first_loss": round(trend[0], 4) if trend else None,   # loss of the first (warm-up) step
+            # mean over the gradient-computing ranks (Byzantine-server mode: servers without workers excluded)
+            "final_loss": round(loss, 4) if loss is not None else None,
+            "first_loss": round(first, 4) if first is not None else None,   # loss of the first (warm-up) step
             **extra,
         }
         print(json.dumps(out), flush=True)

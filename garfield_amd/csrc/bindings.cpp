@@ -423,9 +423,9 @@ void g_bn_forward(const at::Tensor& x, const c10::optional<at::Tensor>& res, int
                             defer_running, stream_of(dev), ts, tile_m, static_cast<int>(tile_e), dt, rsc, rsh);
 }
 
-// Backward of a projection block's last BatchNorm (a) and its folded shortcut BatchNorm (b) sharing dz;
-// False when the shapes take the single-kernel small path (the caller then runs two gpu_bn_backward).
-bool g_bn_backward_dual(const at::Tensor& xa, const at::Tensor& xb, const at::Tensor& dy,
+// Backward of a projection block's last BatchNorm (a) and its folded shortcut BatchNorm (b) sharing dz
+// (every shape: the small layers on the single-kernel dual path, the others on one statistics + one apply pass).
+void g_bn_backward_dual(const at::Tensor& xa, const at::Tensor& xb, const at::Tensor& dy,
                         const c10::optional<at::Tensor>& mask, int64_t groups, const c10::optional<at::Tensor>& gamma_a,
                         const c10::optional<at::Tensor>& gamma_b, const at::Tensor& mean_a, const at::Tensor& istd_a,
                         const at::Tensor& mean_b, const at::Tensor& istd_b, const at::Tensor& part_a,
@@ -465,7 +465,7 @@ bool g_bn_backward_dual(const at::Tensor& xa, const at::Tensor& xb, const at::Te
       gp = grow->data_ptr();
     }
     c10::hip::HIPGuard guard(dev.index());
-    return garfield::gpu::bn_backward_dual(
+    garfield::gpu::bn_backward_dual(
         xa.data_ptr(), xb.data_ptr(), dy.data_ptr(), mp, rg, G, static_cast<int>(C), opt_vec(gamma_a, C, dev, "gamma_a"),
         opt_vec(gamma_b, C, dev, "gamma_b"), ws_vec(mean_a, groups * C, dev, "mean_a"),
         ws_vec(istd_a, groups * C, dev, "istd_a"), ws_vec(mean_b, groups * C, dev, "mean_b"),
@@ -2007,7 +2007,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_bn_backward_dual", &g_bn_backward_dual,
         "Backward of a BatchNorm (a) and a folded shortcut BatchNorm (b) sharing dz = dy under mask: one statistics "
         "pass and one apply pass (or one single-kernel workgroup per channel group on small layers) read dy and the "
-        "mask once; returns True",
+        "mask once",
         py::arg("xa"), py::arg("xb"), py::arg("dy"), py::arg("mask"), py::arg("groups"), py::arg("gamma_a"),
         py::arg("gamma_b"), py::arg("mean_a"), py::arg("istd_a"), py::arg("mean_b"), py::arg("istd_b"),
         py::arg("part_a"), py::arg("part_b"), py::arg("coef_a"), py::arg("coef_b"), py::arg("dxa"), py::arg("dxb"),

@@ -35,8 +35,8 @@ struct RunJobs {
 };
 // Backward of a projection block's last BatchNorm (a) and its folded shortcut BatchNorm (b), which share
 // dz = dy · [mask bit] (mask nullptr: dz = dy): one statistics pass and one apply pass read dy / mask once.
-// (the single-kernel small path: one workgroup per (worker, channel group) for both). Always true.
-bool bn_backward_dual(const void* xa, const void* xb, const void* dy, const uint8_t* mask, int64_t rg, int groups,
+// (the single-kernel small path: one workgroup per (worker, channel group) for both).
+void bn_backward_dual(const void* xa, const void* xb, const void* dy, const uint8_t* mask, int64_t rg, int groups,
                       int C, const float* gamma_a, const float* gamma_b, const float* mean_a, const float* istd_a,
                       const float* mean_b, const float* istd_b, float* part_a, float* part_b, float* coef_a,
                       float* coef_b, void* dxa, void* dxb, void* grow, int grow_dt, int64_t row_stride,

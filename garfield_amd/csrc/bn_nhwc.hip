@@ -1461,7 +1461,7 @@ void bn_backward(const void* x, const void* dy, const void* y, const uint8_t* ma
                        row_stride, off_gamma, off_beta, stream, rsc, rsh);
 }
 
-bool bn_backward_dual(const void* xa, const void* xb, const void* dy, const uint8_t* mask, int64_t rg, int groups,
+void bn_backward_dual(const void* xa, const void* xb, const void* dy, const uint8_t* mask, int64_t rg, int groups,
                       int C, const float* gamma_a, const float* gamma_b, const float* mean_a, const float* istd_a,
                       const float* mean_b, const float* istd_b, float* part_a, float* part_b, float* coef_a,
                       float* coef_b, void* dxa, void* dxb, void* grow, int grow_dt, int64_t row_stride,
@@ -1486,7 +1486,7 @@ bool bn_backward_dual(const void* xa, const void* xb, const void* dy, const uint
     }
 #undef GARFIELD_DUAL_SMALL_RM
 #undef GARFIELD_DUAL_SMALL
-    return true;
+    return;
   }
   if (dt == kF32)
     backward_dual_dt<kF32>(xa, xb, dy, mask, rg, groups, C, gamma_a, gamma_b, mean_a, istd_a, mean_b, istd_b, part_a,
@@ -1495,7 +1495,6 @@ bool bn_backward_dual(const void* xa, const void* xb, const void* dy, const uint
     backward_dual_dt<kBF16>(xa, xb, dy, mask, rg, groups, C, gamma_a, gamma_b, mean_a, istd_a, mean_b, istd_b, part_a,
                             part_b, coef_a, coef_b, dxa, dxb, grow, grow_dt, row_stride, og_a, ob_a, og_b, ob_b,
                             stream);
-  return true;
 }
 
 void bn_running_update(const RunJobs& jobs, hipStream_t stream) {

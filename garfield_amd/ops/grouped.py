@@ -45,6 +45,7 @@ import torch
 import torch.nn.functional as F
 
 from garfield_amd import _native
+from garfield_amd.ops import tuning
 from garfield_amd.utils.flat import is_dense
 
 # Kernel choices of the grouped step. Each was measured against the path it replaced (the
@@ -81,7 +82,7 @@ BN_PROLOGUE = os.environ.get("GARFIELD_BN_PROLOGUE", "0") == "1"
 # measured it faster (ResNet-18 CIFAR: 15.20 -> 14.93 ms/step; ResNet-50 CIFAR / ImageNet layers keep the
 # GEMM: profiles/r5/s2_dgrad/).
 S2_DGRAD = os.environ.get("GARFIELD_S2_DGRAD", "1") == "1"
-_S2_CHOICE: dict = {}   # (dy shape, w shape, dx shape, kernel, padding) -> use the parity-class kernel
+_S2_CHOICE: dict = tuning.register("s2", {})   # (dy shape, w shape, dx shape, kernel, padding) -> use the parity-class kernel
 S2_FORCE = False        # tests: take the parity-class kernel wherever it fits, unmeasured
 # 3x3 / stride-1 / pad-1 convolutions on images of at most 2x2 pixels (ResNet-50 CIFAR layer3 / layer4) as
 # dense GEMMs over [N, P * C] rows with the per-step expanded weight (sconv_nhwc.hip): no out-of-image
@@ -95,8 +96,9 @@ LAZY_RES = os.environ.get("GARFIELD_LAZY_RES", "1") == "1"
 # its scale / shift applied to the pre-BatchNorm shortcut inside the last BatchNorm's apply pass, its
 # backward run there too): the shortcut's normalised activation is never written (_GroupedBN res_st).
 FOLD_SHORTCUT_BN = os.environ.get("GARFIELD_FOLD_SHORTCUT_BN", "1") == "1"
-# ... and its backward shares one statistics pass and one apply pass with the last BatchNorm's (large layers)
-BN_DUAL = os.environ.get("GARFIELD_BN_DUAL", "1") == "1"
+# ... and its backward shares one statistics pass and one apply pass with the last BatchNorm's (a ReLU-bit
+# mask or none; tests set False to run the two-call form, which a saved ReLU output still takes)
+BN_DUAL = True
 
 
 def rows2d(t: torch.Tensor) -> torch.Tensor:
@@ -478,7 +480,7 @@ class _GroupedBN(torch.autograd.Function):
                 grow, stride = sink.flat, sink.row_stride
                 og = sink.base + sink.offset(bn.weight) if bn.weight is not None else -1
                 ob = sink.base + sink.offset(bn.bias) if bn.bias is not None else -1
-            done = False
+            dual = False
             if ctx.res_st is not None:           # the folded shortcut BatchNorm: dy + this one's ReLU bits
                 rs_, rbn = ctx.res_st, ctx.res_st.bn
                 dres = torch.empty_like(xs, memory_format=torch.channels_last)
@@ -488,10 +490,11 @@ class _GroupedBN(torch.autograd.Function):
                 if BN_DUAL and (y2 is None or y2.dim() == 1):  # one statistics / apply pass for both
                     part_b = ws.get("bn_part2", C_.bn_part_floats(rg, st.groups, C), x.device)
                     coef_b = ws.get("bn_coef2", 3 * st.groups * C, x.device)
-                    done = C_.gpu_bn_backward_dual(x2, xs2, dy2, y2, st.groups, bn.weight, rbn.weight, st.mean,
+                    dual = True
+                    C_.gpu_bn_backward_dual(x2, xs2, dy2, y2, st.groups, bn.weight, rbn.weight, st.mean,
                                                    st.istd, rs_.mean, rs_.istd, part, part_b, coef, coef_b,
                                                    rows2d(dx), rows2d(dres), grow, stride, og, ob, ogs, obs)
-            if not done:
+            if not dual:   # (the two backward calls run in stream order on the same workspaces)
                 C_.gpu_bn_backward(x2, dy2, y2, st.groups, bn.weight, st.mean, st.istd, part, coef, rows2d(dx),
                                    rows2d(dres) if (dres is not None and ctx.res_st is None) else None, grow, stride,
                                    og, ob)
@@ -569,7 +572,7 @@ def _gemm_nt_ok(a2: torch.Tensor, b2: torch.Tensor) -> bool:
 # step's first (eager) run times every valid tile configuration on the real operands (scratch
 # outputs, 3 calls each after a warm call) and keeps the fastest; graph captures and replays
 # reuse it (during a capture the static choice of gemm_nt_pick stands in).
-_GEMM_CFG: dict = {}
+_GEMM_CFG: dict = tuning.register("gemm", {})   # (ops/tuning.py: agreed over ranks, checkpointed)
 
 
 def _gemm_cfg(a2: torch.Tensor, b2: torch.Tensor, rg: int, add: torch.Tensor | None, pro=None) -> int:
@@ -592,6 +595,9 @@ def _gemm_cfg(a2: torch.Tensor, b2: torch.Tensor, rg: int, add: torch.Tensor | N
     if cfg >= 0 and not pro_ok(cfg):
         cfg = cands[0] if cands else -1
     if cfg < 0 or torch.cuda.is_current_stream_capturing():
+        return cfg
+    if not tuning.measuring():   # GARFIELD_TUNING=fixed: the static pick, identical everywhere
+        _GEMM_CFG[key] = cfg
         return cfg
     out = torch.empty((M, N), dtype=a2.dtype, device=a2.device)
     addc = add.clone() if add is not None else None
@@ -789,7 +795,7 @@ def _s2_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", xshape, add: 
     if use is None:
         probe = torch.empty(xshape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
         use = bool(C_.dgrad_s2_ok(dy, probe, *spec.kernel, *spec.padding))
-        if use and not S2_FORCE and not torch.cuda.is_current_stream_capturing():
+        if use and not S2_FORCE and not torch.cuda.is_current_stream_capturing() and tuning.measuring():
             dflag = spec.dcol
             t_s2 = _timed(lambda: C_.gpu_dgrad_s2(dy, w, *spec.kernel, *spec.padding, probe))
             t_col = _timed(lambda: _dcol_dx(rows2d(dy), w, kp, spec, xshape, None))
@@ -851,7 +857,7 @@ def _sc_gemm(a2: torch.Tensor, b2: torch.Tensor, add: torch.Tensor | None) -> to
     return out
 
 
-_SC_WG_CHOICE: dict = {}   # (x shape, dy shape, G) -> the dense form (else the implicit 3x3 kernel)
+_SC_WG_CHOICE: dict = tuning.register("scwg", {})   # (x shape, dy shape, G) -> the dense form (else the implicit 3x3 kernel)
 SC_DENSE_WGRAD = None      # tests: True / False force the dense / implicit form (None: measured)
 
 
@@ -864,7 +870,7 @@ def _sc_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> No
     dense = _SC_WG_CHOICE.get(key) if SC_DENSE_WGRAD is None else SC_DENSE_WGRAD
     if dense is None:
         dense = True
-        if not torch.cuda.is_current_stream_capturing() and _iwgrad_ok(x, dy):
+        if not torch.cuda.is_current_stream_capturing() and tuning.measuring() and _iwgrad_ok(x, dy):
             sink = spec.sink
             spec.sink = _NullSink(sink, G)
             try:

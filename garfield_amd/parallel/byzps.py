@@ -33,7 +33,7 @@ import torch
 import torch.nn as nn
 
 from garfield_amd.ops import gar
-from garfield_amd.parallel.comm import DistContext, all_gather_rows
+from garfield_amd.parallel.comm import DistContext, all_gather_rows, collectives_on
 from garfield_amd.parallel.engine import COORD_RULES, WEIGHTED_RULES, EngineConfig, RobustDataParallel
 from garfield_amd.runtime.attacks import SERVER_ATTACKS
 
@@ -100,13 +100,14 @@ class ByzantinePSDataParallel(RobustDataParallel):
         return torch.stack(losses).float().mean()
 
     def step(self, batches) -> torch.Tensor:
+        self._agree_tuning()
         cfg = self.cfg
         # 1-2: gradients (worker ranks) + exchange (everyone)
         if self.computes:
             loss = self._compute(batches)
         else:
             works = [all_gather_rows(self.X[j], self.rank, async_op=True) for j in range(self.k)] \
-                if self.world > 1 else []
+                if collectives_on(self.world) else []
             for w in works:
                 w.wait()
             loss = torch.zeros((), device=self.device)
@@ -125,14 +126,14 @@ class ByzantinePSDataParallel(RobustDataParallel):
         import torch.distributed as dist
 
         if self.num_ps == 1:   # the rule over one model is that model
-            if self.world > 1:
+            if collectives_on(self.world):
                 dist.broadcast(self.flat.data, src=0)
                 if not self.is_ps:
                     self.sync_shadow()
             return
         if self.is_ps:
             self.M[self.rank].copy_(self.flat.data)
-        if self.world > 1:
+        if collectives_on(self.world):
             works = [dist.broadcast(self.M[p], src=p, async_op=True) for p in range(self.num_ps)]
             for w in works:
                 w.wait()

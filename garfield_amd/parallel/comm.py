@@ -36,7 +36,9 @@ class DistContext:
 
     @property
     def is_distributed(self) -> bool:
-        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+        """Whether the engines issue their collectives: several ranks, or the one-rank RCCL
+        rehearsal of the multi-rank step (``world1_collectives``)."""
+        return collectives_on(self.world_size)
 
     def barrier(self) -> None:
         if self.is_distributed:
@@ -75,17 +77,44 @@ def init_distributed(backend: str | None = None, device: str | None = None, time
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
         ctx.initialized_here = True
-    elif world == 1 and use_cuda and os.environ.get("GARFIELD_DIRECT_RCCL_WORLD1") == "1" and not dist.is_initialized():
-        # a one-rank RCCL communicator for the direct path's world-1 run (parallel/sharded.py)
+    elif world == 1 and world1_requested() and not dist.is_initialized():
+        # a one-rank communicator (RCCL on a GPU) on which the world-1 run issues every
+        # collective of the multi-rank step (world1_collectives)
         import socket
 
         s = socket.socket()
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
         s.close()
-        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+        kw = {"device_id": dev} if use_cuda else {}
+        dist.init_process_group("nccl" if use_cuda else "gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1, **kw)
+        ctx.backend = "nccl" if use_cuda else "gloo"
         ctx.initialized_here = True
     return ctx
+
+
+def world1_requested() -> bool:
+    """``GARFIELD_COLL_WORLD1=1``: a one-rank job runs the multi-rank code path with real
+    collectives on a one-rank process group instead of taking its world-1 shortcuts: the
+    sharded step's packed all-to-all per bucket from the comm stream, partial-Gram all-gather,
+    in-place weight all-gathers and BatchNorm-affine all-reduce; the unsharded slot
+    all-gathers; the Byzantine-server broadcasts; the quorum engine's per-root groups. On
+    one GPU this exercises every RCCL call pattern of the 8-GPU job (tests, traces)."""
+    return os.environ.get("GARFIELD_COLL_WORLD1", "0") == "1"
+
+
+def world1_collectives() -> bool:
+    """``world1_requested()`` and a process group is initialised (of one rank)."""
+    return world1_requested() and dist.is_available() and dist.is_initialized()
+
+
+def collectives_on(world: int) -> bool:
+    """Whether a job of ``world`` ranks issues its collectives (every multi-rank job; a
+    one-rank job under ``GARFIELD_COLL_WORLD1=1`` with a one-rank process group)."""
+    if world > 1:
+        return dist.is_available() and dist.is_initialized()
+    return world1_collectives()
 
 
 def shutdown(ctx: DistContext) -> None:
@@ -139,7 +168,7 @@ class RoleGroups:
 
 def make_role_groups(num_ps: int, world_size: int) -> RoleGroups:
     rg = RoleGroups(num_ps, world_size)
-    if dist.is_initialized() and world_size > 1:
+    if collectives_on(world_size):
         rg.all = dist.group.WORLD
         rg.ps = dist.new_group(rg.ps_ranks) if num_ps > 0 else None
         rg.workers = dist.new_group(rg.worker_ranks) if world_size > num_ps else None

@@ -27,6 +27,7 @@ import contextlib
 import gc
 import math
 import os
+import weakref
 from dataclasses import dataclass, field
 
 import torch
@@ -35,7 +36,7 @@ import torch.nn as nn
 
 from garfield_amd import _native
 from garfield_amd.ops import gar
-from garfield_amd.parallel.comm import DistContext, all_gather_rows
+from garfield_amd.parallel.comm import DistContext, all_gather_rows, collectives_on
 from garfield_amd.runtime.attacks import NEEDS_ESTIMATES, apply_attack
 from garfield_amd.utils.flat import FlatParams
 from garfield_amd.utils.profiling import PhaseTimer
@@ -209,7 +210,8 @@ class RobustDataParallel:
         if ctx.is_distributed:
             dist.broadcast(self.flat.data, src=0)
         self.d, self.ld = self.flat.d, self.flat.ld
-        self.flat.before_read = self.synchronize    # readers of the weights join a staged step first
+        # readers of the weights join a staged step first (weak: no engine <-> FlatParams cycle)
+        self.flat.before_read = weakref.WeakMethod(self.synchronize)
         self.work_params = list(self.flat.params)   # what forward/backward sees (see _install_shadow)
         self._shadow = None
         self._install_shadow()
@@ -242,6 +244,7 @@ class RobustDataParallel:
         self.timer = PhaseTimer(self.device, cfg.profile_phases)
         self._graph = None
         self._graph_failed = False
+        self._tuning_agreed = False
         self._static = None
         self._static_loss = None
         self._gexec = None
@@ -282,7 +285,7 @@ class RobustDataParallel:
 
         sg = self.cfg.shard_gar
         if sg is None:   # default: on for multi-rank jobs
-            sg = self.ctx.world_size > 1 and self.ctx.is_distributed
+            sg = self.ctx.is_distributed   # (or the one-rank run of the multi-rank collectives)
         if not (sg and self._supports_sharding):
             return False
         if self.ctx.world_size > 1 and not self.ctx.is_distributed:
@@ -292,12 +295,16 @@ class RobustDataParallel:
         if (self.cfg.layerwise and self.cfg.gar in LAYERWISE_RULES and self.device.type == "cuda"
                 and not layerwise_device_ok(self.cfg.gar, self.cfg.workers_per_rank * self.ctx.world_size,
                                             self.cfg.f)):
+            if self.cfg.shard_gar:   # asked for explicitly: say why it cannot be honoured
+                raise ValueError(f"shard_gar=True: the sharded layer-wise {self.cfg.gar!r} kernels do not take n="
+                                 f"{self.cfg.workers_per_rank * self.ctx.world_size}, f={self.cfg.f} (leave shard_gar "
+                                 f"unset to run the unsharded per-segment loop)")
             return False   # beyond the segmented device kernels: the unsharded per-segment loop
         return True
 
     def _gather_slot(self, j: int):
         """Start the all-gather of local worker j's slot (unsharded form only)."""
-        if self.world == 1 or self._sharded:
+        if self._sharded or not collectives_on(self.world):
             return None
         return all_gather_rows(self.X[j], self.rank, async_op=True)
 
@@ -748,6 +755,7 @@ class RobustDataParallel:
 
         With worker batching (``_grouped_step``) the k local workers are one
         batched forward/backward instead, captured as ONE graph."""
+        self._agree_tuning()
         if self._gexec is not None and self._groupable(batches):
             return self._grouped_step(batches)
         if not self.graph_capturable() or self.step_count == 0:
@@ -779,6 +787,16 @@ class RobustDataParallel:
 
     # ------------------------------------------------------------------ #
     # Worker batching: the k local workers as one grouped batch
+
+    def _agree_tuning(self) -> None:
+        """Once, at the start of the second step (before any capture): every rank adopts rank 0's
+        measured kernel choices (``ops/tuning.py``), so all ranks replay the same kernels."""
+        if self.step_count >= 1 and not self._tuning_agreed:
+            self._tuning_agreed = True
+            if self.device.type == "cuda" and collectives_on(self.world):
+                from garfield_amd.ops import tuning
+
+                tuning.agree()
 
     def _groupable(self, batches) -> bool:
         if len(batches) != self.k:
@@ -957,7 +975,7 @@ class RobustDataParallel:
             with torch.cuda.stream(s):  # warm-up on the capture stream (per-stream library state)
                 self._gexec.run(self._gx, self._gy, self._gloss)
             s.synchronize()
-            mode = "thread_local" if self.world > 1 else "global"
+            mode = "thread_local" if collectives_on(self.world) else "global"
             if self._staging():
                 # one graph per stage (shared memory pool), cut at the bucket boundaries of the
                 # forward: the next step's early layers need not wait for the late buckets' updates
@@ -1035,7 +1053,7 @@ class RobustDataParallel:
             s.synchronize()
             for j in self.local_slots:
                 g = torch.cuda.CUDAGraph()
-                mode = "thread_local" if self.world > 1 else "global"  # RCCL watchdog thread
+                mode = "thread_local" if collectives_on(self.world) else "global"  # RCCL watchdog thread
                 with _capture_guard(), torch.cuda.graph(g, stream=s, pool=pool, capture_error_mode=mode):
                     x, y = self._static[j]
                     self._worker_body(j, x, y, self._static_loss[j])

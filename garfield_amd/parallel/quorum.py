@@ -102,6 +102,7 @@ class QuorumDataParallel(RobustDataParallel):
         return torch.stack(self.compute_local(batches)).float().mean()
 
     def step(self, batches) -> torch.Tensor:
+        self._agree_tuning()
         cfg, W, r0 = self.cfg, self.world, self.rank
         par = self.step_count % 2
         buf, dec = self._buf[par], self._dec[par]

@@ -57,7 +57,7 @@ import torch.distributed as dist
 from garfield_amd import _native
 from garfield_amd.ops import gar
 from garfield_amd.ops import reference as ref
-from garfield_amd.parallel.comm import gloo_backend
+from garfield_amd.parallel.comm import collectives_on, gloo_backend, world1_collectives
 from garfield_amd.parallel.rccl import direct_backend
 from garfield_amd.parallel.signals import Handoff
 
@@ -90,11 +90,12 @@ def overlap_enabled(world: int = 1) -> bool:
     """Whether each bucket's exchange starts INSIDE the step's backward: the grouped
     executor's captured graph carries a device-side counter signal per bucket mark
     (``parallel/signals.py``) and the comm stream waits for it on the device. On by
-    default when there is something to overlap (world > 1); ``GARFIELD_OVERLAP=1``
-    forces it (e.g. the world-1 loopback exchange), ``0`` disables it."""
+    default when there is something to overlap (world > 1, or the one-rank run of the
+    multi-rank collectives, ``comm.world1_collectives``); ``GARFIELD_OVERLAP=1`` forces it
+    (e.g. the world-1 loopback exchange), ``0`` disables it."""
     v = os.environ.get("GARFIELD_OVERLAP", "")
     if v == "":
-        return world > 1
+        return collectives_on(world)
     return v != "0"
 
 
@@ -105,12 +106,12 @@ class _Bucket:
     the whole bucket leaves in ONE ``all_to_all_single``), ``recv[src, j]`` = shard ``rank`` of source
     rank src's local worker j (the row of global slot j * world + src)."""
 
-    def __init__(self, lo: int, hi: int, world: int, rank: int, k: int, dev, dt, pack: bool):
+    def __init__(self, lo: int, hi: int, world: int, rank: int, k: int, dev, dt, coll: bool, pack: bool):
         self.lo, self.hi = lo, hi
         self.S = (hi - lo) // world
         self.own = slice(lo + rank * self.S, lo + (rank + 1) * self.S)
-        self.send = torch.empty((world, k, self.S), dtype=dt, device=dev) if world > 1 and pack else None
-        self.recv = torch.empty((world, k, self.S), dtype=dt, device=dev) if world > 1 else None
+        self.send = torch.empty((world, k, self.S), dtype=dt, device=dev) if coll and pack else None
+        self.recv = torch.empty((world, k, self.S), dtype=dt, device=dev) if coll else None
         self.p2p = None        # the direct exchange's (sends, to, recvs, from) lists
         self.moff = 0          # offset of this bucket's shard in the momentum buffer
         self.works: list = []
@@ -139,19 +140,20 @@ class ShardedAggregator:
         # (world 1 without the loopback exchange: nothing to overlap, and a second active
         # queue alone costs the main stream's graph ~4-5 % (profiles/r3/probe_cross_stream.log):
         # everything stays on the main stream)
-        forced = dev.type == "cuda" and self.world == 1 and direct_world1()
+        # the one-rank run of the multi-rank collectives (GARFIELD_COLL_WORLD1=1 on a one-rank
+        # process group, tests and traces: real RCCL calls, no shortcut taken for world 1)
+        forced = self.world == 1 and world1_collectives()
         side = dev.type == "cuda" and (self.world > 1 or loopback_enabled() or overlap_enabled(self.world) or forced)
         self._comm_stream = torch.cuda.Stream(dev) if side else None
         self._handoff = Handoff(dev) if side else None
-        # RCCL kernels straight onto the comm stream (rccl.py); None: torch.distributed
-        self._rccl = direct_backend(self.world, self.rank, side, forced)
-        # whether the step issues its collectives: several ranks, or the one-rank run of the
-        # direct RCCL path (GARFIELD_DIRECT_RCCL_WORLD1=1, tests and traces: real RCCL calls on a
-        # one-rank communicator beside the staged graphs, no shortcut taken for world 1)
-        self._coll = self.world > 1 or self._rccl is not None
+        # RCCL kernels straight onto the comm stream (rccl.py, GARFIELD_DIRECT_RCCL=1); None:
+        # torch.distributed
+        self._rccl = direct_backend(self.world, self.rank, side, forced and dev.type == "cuda")
+        # whether the step issues its collectives (several ranks, or the forced one-rank run)
+        self._coll = self.world > 1 or forced
         # ready order of the backward: highest coordinates (last layers) first
-        self.buckets = [_Bucket(edges[i], edges[i + 1], self.world, self.rank, self.k, dev, dt, self._rccl is None)
-                        for i in reversed(range(len(edges) - 1))]
+        self.buckets = [_Bucket(edges[i], edges[i + 1], self.world, self.rank, self.k, dev, dt, self._coll,
+                                self._rccl is None) for i in reversed(range(len(edges) - 1))]
         off = 0
         for b in sorted(self.buckets, key=lambda b: b.lo):
             b.moff = off
@@ -180,7 +182,7 @@ class ShardedAggregator:
         direct exchange this rank's own workers' rows are read in place from the exchange
         rows (the own shard never moves); the packed all_to_all receives them in recv[rank]."""
         e = self.e
-        if self.world == 1:
+        if not self._coll:
             return [e.X[j, 0, b.lo:b.hi] for j in range(self.k)]
         rows = []
         for s in range(self.n):
@@ -277,7 +279,7 @@ class ShardedAggregator:
                 b.works = []
                 if self._coll and self._rccl is not None:   # straight from the exchange rows
                     self._rccl.exchange(*b.p2p, self._comm_stream)
-                elif self.world > 1:
+                elif self._coll:
                     local = e.X[:, 0, b.lo:b.hi].view(self.k, self.world, b.S).transpose(0, 1)   # [dst, j, S]
                     b.send.copy_(local)
                     b.works.append(dist.all_to_all_single(b.recv.view(-1), b.send.view(-1), async_op=True))
@@ -400,7 +402,7 @@ class ShardedAggregator:
     def staging_ok(self) -> bool:
         """Whether the updates can run beside the next forward: a comm stream, and every
         collective stream-ordered on it (the direct RCCL path, or nothing to exchange)."""
-        return self._comm_stream is not None and (self.world == 1 or self._rccl is not None)
+        return self._comm_stream is not None and (not self._coll or self._rccl is not None)
 
     def _update_buckets(self, fn) -> None:
         """``fn(b)`` issues bucket b's update; buckets in update order (low coordinates first).
@@ -460,7 +462,7 @@ class ShardedAggregator:
         """Collective: refresh the fp32 master outside this rank's shards (checkpoints,
         the reference-layout flat vector). Every rank must call it."""
         self.quiesce()
-        if not self.master_stale or self.world == 1:
+        if not self.master_stale or not self._coll:
             self.master_stale = False
             return
         data = self.e.flat.data
@@ -569,7 +571,7 @@ class ShardedAggregator:
     def _matrix(self, b: _Bucket) -> torch.Tensor:
         """Bucket b's received shards as ONE [n, S] matrix (row src * k + j: the receive
         buffer as it lands, no copy); ``self._perm[s]`` is the matrix row of global slot s."""
-        if self.world == 1:
+        if not self._coll:
             return torch.stack(b.rows)
         if self._rccl is not None:   # the own shard was read in place: bring it into the matrix
             b.recv[self.rank].copy_(self.e.X[:, 0, b.own])
@@ -936,7 +938,7 @@ class ShardedAggregator:
         out = torch.zeros(e.ld, dtype=e.mom.dtype, device=e.mom.device)
         for b in sorted(self.buckets, key=lambda b: b.lo):
             mine = e.mom[b.moff:b.moff + b.S].clone()
-            if self.world == 1:
+            if not self._coll:
                 out[b.lo:b.hi] = mine
             else:
                 dist.all_gather_into_tensor(out[b.lo:b.hi], mine)
@@ -960,14 +962,6 @@ class _nullctx:
 # GARFIELD_EXCHANGE_TIMING=1: the per-bucket "exchange issued" events are timing events
 # (scripts/overlap_timing.py reads them against the step's start and its backward's end)
 _TIMING = os.environ.get("GARFIELD_EXCHANGE_TIMING", "0") == "1"
-
-
-def direct_world1() -> bool:
-    """GARFIELD_DIRECT_RCCL_WORLD1=1 (with GARFIELD_DIRECT_RCCL=1, on a one-rank NCCL process
-    group): the sharded step at world 1 issues every collective of the multi-rank step through
-    the direct RCCL path on the comm stream, instead of taking the world-1 shortcuts (tests,
-    traces)."""
-    return os.environ.get("GARFIELD_DIRECT_RCCL_WORLD1", "0") == "1"
 
 
 def loopback_enabled() -> bool:

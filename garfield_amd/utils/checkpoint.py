@@ -10,7 +10,9 @@ in registration order (``server.py:196-200,289-297``). A checkpoint here holds:
 * ``momentum``: the engine's momentum in the same reference layout as ``flat``
   (so a channels_last / grouped GPU checkpoint resumes correctly on an NCHW
   engine, and vice versa), when present;
-* ``step`` and free-form ``meta``.
+* ``step`` and free-form ``meta``;
+* ``tuning`` (engine checkpoints): the measured kernel choices of the grouped step
+  (``ops/tuning.py``), restored on load so the resumed run replays the same kernels.
 
 Files are written atomically (temp file + rename) with ``torch.save`` and read back
 with ``torch.load(weights_only=True)`` — plain tensors and primitives only.
@@ -35,9 +37,11 @@ def model_state(model: nn.Module, flat: torch.Tensor | None = None) -> dict:
 
 
 def save(path: str, model: nn.Module, step: int = 0, momentum: torch.Tensor | None = None,
-         meta: dict | None = None, flat: torch.Tensor | None = None) -> str:
+         meta: dict | None = None, flat: torch.Tensor | None = None, tuning: dict | None = None) -> str:
     state = model_state(model, flat)
     state["step"] = int(step)
+    if tuning:
+        state["tuning"] = tuning
     if momentum is not None:
         state["momentum"] = momentum.detach().cpu()
         state["momentum_layout"] = "reference"   # checkpoints without the key hold the same layout
@@ -80,11 +84,18 @@ def save_engine(path: str, engine, meta: dict | None = None, write: bool = True)
     mom_ref = engine.flat.to_reference(mom)
     if not write:
         return path
-    return save(path, engine.model, engine.step_count, mom_ref, meta, flat=engine.flat.reference_vector())
+    from garfield_amd.ops import tuning
+
+    return save(path, engine.model, engine.step_count, mom_ref, meta, flat=engine.flat.reference_vector(),
+                tuning=tuning.export())
 
 
 def load_engine(path: str, engine) -> dict:
     state = load(path)
+    if state.get("tuning"):   # the writer's kernel choices (ops/tuning.py), before any re-capture
+        from garfield_amd.ops import tuning
+
+        tuning.load(state["tuning"])
     shard = getattr(engine, "_shard", None)
     if shard is not None and hasattr(shard, "quiesce"):
         shard.quiesce()   # a previous step's updates may still run on the exchange stream

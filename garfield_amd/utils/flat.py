@@ -14,6 +14,7 @@ multiple of 64 elements (16-byte aligned rows for every dtype).
 """
 from __future__ import annotations
 
+import weakref
 from typing import Iterable
 
 import torch
@@ -123,12 +124,17 @@ class FlatParams:
             self.grad = torch.zeros(self.ld, dtype=dtype, device=device)
             self.attach_grads(self.grad)
         # called before the readers below: an engine whose updates may still be in flight on a
-        # side stream (a staged sharded step) installs its ``synchronize`` here
+        # side stream (a staged sharded step) installs its ``synchronize`` here, as a
+        # ``weakref.WeakMethod`` (a bound method would tie the engine, its HIP graphs and pools
+        # into a reference cycle with these parameters, freed only by the cyclic collector)
         self.before_read = None
 
     def _sync(self) -> None:
-        if self.before_read is not None:
-            self.before_read()
+        fn = self.before_read
+        if fn is not None and isinstance(fn, weakref.WeakMethod):
+            fn = fn()
+        if fn is not None:
+            fn()
 
     def views(self, flat: torch.Tensor):
         """Per-parameter views (parameter strides) of a flat buffer laid out like ``data``;

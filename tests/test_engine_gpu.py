@@ -1,4 +1,6 @@
 """Single-GPU robust training engine (native HIP path) — one process, n logical workers."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -465,3 +467,71 @@ def test_fused_collude_kernel_matches_attack_functions(cuda, native, P, T, d, dt
             got, w = X[P + t].float(), want[t].float()
             err = ((got - w).abs() / (w.abs() + 1e-3)).max().item()
             assert err < 1e-2, (empire, t, err)
+
+
+def test_resume_in_new_process_replays_kernel_choices(cuda, tmp_path):
+    """The grouped step times some kernel choices in its first eager step (gemm_nt tiles, stride-2
+    dgrad form, small-image wgrad form: ops/tuning.py), and the candidates round bf16 differently.
+    A checkpoint carries the table: a NEW process whose tables were pre-seeded with other choices
+    restores the checkpoint and continues bit for bit like the writer."""
+    import json
+    import subprocess
+    import sys
+
+    from garfield_amd.ops import tuning
+    from garfield_amd.utils.checkpoint import save_engine
+
+    torch.manual_seed(0)
+    eng = RobustDataParallel(build_model("resnet50"), F.cross_entropy, DistContext(device=cuda),
+                             EngineConfig(gar="krum", f=1, workers_per_rank=4, lr=0.02, cuda_graph=True))
+    batches = synthetic_batches(4, 8, (3, 32, 32), 10, cuda)
+    for _ in range(2):
+        eng.step(batches)
+    ck = str(tmp_path / "ck.pt")
+    save_engine(ck, eng)
+    for _ in range(2):
+        eng.step(batches)
+    torch.cuda.synchronize()
+    want = eng.flat_model().cpu()
+    table = tuning.export()
+    assert table["gemm"] and table["scwg"], "the measured paths must have run (ResNet-50 CIFAR)"
+    tp = tmp_path / "table.json"
+    tp.write_text(json.dumps(table))
+    out = str(tmp_path / "child.pt")
+    child = os.path.join(os.path.dirname(__file__), "_resume_child.py")
+    r = subprocess.run([sys.executable, child, ck, str(tp), out], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = torch.load(out, weights_only=True)
+    assert got["table"] == table
+    assert torch.equal(got["flat"], want)
+
+
+def test_capture_after_dropping_engine_in_reference_cycle(cuda):
+    """Regression (round 5 suite abort): a dead engine held only by a reference cycle, with its HIP
+    graphs, must not be collected in the middle of the next engine's graph capture (_capture_guard).
+    The collector runs at nearly every allocation here; the new engine captures and steps normally."""
+    import gc
+
+    def make():
+        torch.manual_seed(0)
+        return RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda),
+                                  EngineConfig(gar="krum", f=1, workers_per_rank=4, lr=0.02, cuda_graph=True))
+
+    batches = synthetic_batches(4, 8, (3, 32, 32), 10, cuda)
+    old = make()
+    for _ in range(3):
+        old.step(batches)
+    assert old._ggraph is not None
+    old.cycle = {"engine": old}     # only the cyclic collector can free it now
+    del old
+    thresholds = gc.get_threshold()
+    gc.set_threshold(1, 1, 1)
+    try:
+        new = make()
+        for _ in range(3):
+            new.step(batches)
+        torch.cuda.synchronize()
+    finally:
+        gc.set_threshold(*thresholds)
+    assert new._ggraph is not None
+    assert torch.isfinite(new.flat_model()).all()

@@ -526,12 +526,18 @@ def test_lazy_residual_gradient_is_bitwise_the_materialised_one(cuda, monkeypatc
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dual", [True, False])
 @pytest.mark.parametrize("G,B,H,C,dt", [(8, 16, 4, 64, torch.bfloat16), (4, 8, 2, 256, torch.float32),
                                         (2, 64, 8, 128, torch.bfloat16), (3, 20, 10, 64, torch.float32)])
-def test_bn_folded_shortcut_matches_fp32_reference(cuda, G, B, H, C, dt):
+def test_bn_folded_shortcut_matches_fp32_reference(cuda, G, B, H, C, dt, dual, monkeypatch):
     """A projection block's last BatchNorm with the shortcut BatchNorm folded in (res_st): y =
     relu(BN3(x) + BN_ds(r)) with only BN_ds's statistics pass of its own; forward, both inputs'
-    gradients and both BatchNorms' dgamma / dbeta against fp32 autograd (small and large paths)."""
+    gradients and both BatchNorms' dgamma / dbeta against fp32 autograd (small and large paths).
+    ``dual``: the shared backward (one statistics + one apply pass, or the single-kernel small form);
+    False: the two sequential backward calls on the same workspaces and ReLU bits."""
+    import garfield_amd.ops.grouped as grouped_mod
+
+    monkeypatch.setattr(grouped_mod, "BN_DUAL", dual)
     torch.manual_seed(C + G)
     N = G * B
     x = (torch.randn(N, C, H, H, device=cuda) * 2 + 0.5).to(dt).contiguous(memory_format=torch.channels_last)

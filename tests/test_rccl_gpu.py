@@ -66,34 +66,146 @@ def test_direct_rccl_calls_on_one_rank(one_rank_nccl, monkeypatch):
     assert torch.equal(out, blk)
 
 
-def test_sharded_step_on_direct_rccl_one_rank_equals_loopback(one_rank_nccl, monkeypatch):
-    """The full sharded grouped step with its collectives issued through the direct RCCL path on
-    a one-rank communicator (GARFIELD_DIRECT_RCCL_WORLD1=1): the partial-Gram all-gather, the
-    in-place bf16 weight all-gathers and the BatchNorm-affine all-reduce run as real RCCL calls on
-    the comm stream, beside the next step's staged three-graph forward, with the in-graph bucket
-    signals on. Ten steps with fresh inputs must be bitwise equal to the same step without the
-    collectives (the world-1 loopback run of the same machinery)."""
+class _Calls:
+    """Counts the torch.distributed collectives the engines issue (wrapping the module functions)."""
+
+    NAMES = ("all_to_all_single", "all_gather_into_tensor", "all_reduce", "broadcast", "broadcast_object_list")
+
+    def __init__(self, monkeypatch):
+        self.n = dict.fromkeys(self.NAMES, 0)
+        for name in self.NAMES:
+            fn = getattr(dist, name)
+
+            def wrap(*a, _fn=fn, _name=name, **kw):
+                self.n[_name] += 1
+                return _fn(*a, **kw)
+            monkeypatch.setattr(dist, name, wrap)
+
+
+def _resnet_engine(dev, cls=None, cfg=None, **kw):
     import torch.nn.functional as F
 
     from garfield_amd.models import build_model
     from garfield_amd.parallel.comm import DistContext
-    from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel, synthetic_batches
+    from garfield_amd.parallel.engine import EngineConfig, RobustDataParallel
+
+    torch.manual_seed(0)
+    cfg = cfg or EngineConfig(gar="krum", f=2, workers_per_rank=8, lr=0.01, cuda_graph=True, **kw)
+    return (cls or RobustDataParallel)(build_model("resnet18"), F.cross_entropy,
+                                       DistContext(device=dev, backend="nccl"), cfg)
+
+
+def _run(eng, dev, steps=10):
+    from garfield_amd.parallel.engine import synthetic_batches
+
+    for it in range(steps):
+        eng.step(synthetic_batches(8, 8, (3, 32, 32), 10, dev, seed=300 + it))
+    eng.synchronize()
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("path", ["torch.distributed", "direct"])
+def test_sharded_step_on_one_rank_rccl_equals_loopback(one_rank_nccl, monkeypatch, path):
+    """The default multi-rank sharded step (``torch.distributed``: per bucket a ``[dst, worker,
+    shard]`` pack and one ``all_to_all_single`` issued from the comm stream after the device-side
+    hand-off, the partial-Gram all-gather, the in-place ``all_gather_into_tensor`` of the bf16
+    working weights, the BatchNorm-affine all-reduce, ``sync_master`` and ``momentum_vector``;
+    the grouped step captured with ``capture_error_mode="thread_local"`` beside RCCL's watchdog)
+    and the opt-in direct RCCL path (point-to-point from the exchange rows, staged three-graph
+    forward), both as REAL RCCL calls on a one-rank communicator (``GARFIELD_COLL_WORLD1=1``).
+    Ten HIP-graph steps with fresh inputs must be bitwise equal to the same step without any
+    collective (the world-1 loopback run of the same machinery)."""
+    dev = one_rank_nccl
+    outs = []
+    for coll in ("0", "1"):
+        monkeypatch.setenv("GARFIELD_COLL_WORLD1", coll)
+        monkeypatch.setenv("GARFIELD_LOOPBACK_EXCHANGE", "1" if coll == "0" else "0")
+        monkeypatch.setenv("GARFIELD_OVERLAP", "1")
+        monkeypatch.setenv("GARFIELD_DIRECT_RCCL", "1" if (coll == "1" and path == "direct") else "0")
+        calls = _Calls(monkeypatch) if coll == "1" else None
+        eng = _resnet_engine(dev, shard_gar=True)
+        sh = eng._shard
+        assert sh._coll == (coll == "1")
+        assert (sh._rccl is not None) == (coll == "1" and path == "direct")
+        _run(eng, dev)
+        if coll == "1" and path == "torch.distributed":
+            nb = len(sh.buckets)
+            assert nb == 3
+            assert calls.n["all_to_all_single"] == 10 * nb            # one packed exchange per bucket and step
+            assert calls.n["all_gather_into_tensor"] >= 10 * (nb + 1)  # weights per bucket + the partial Grams
+            assert calls.n["all_reduce"] >= 10                         # BatchNorm affine (fp32 read directly)
+            assert calls.n["broadcast_object_list"] == 1               # the kernel-choice agreement (ops/tuning)
+            assert not isinstance(eng._ggraph, list) and eng._ggraph is not None   # one graph (not staged)
+        else:
+            assert isinstance(eng._ggraph, list) and len(eng._ggraph) == 3 and sh.staged
+        eng.sync_master()
+        outs.append((eng.flat.reference_vector().clone(), eng.momentum_vector().clone()))
+        del eng, sh
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_unsharded_slot_allgather_on_one_rank_rccl(one_rank_nccl, monkeypatch):
+    """The unsharded engine's in-place slot all-gathers (``comm.all_gather_rows``: NCCL's in-place
+    ``all_gather_into_tensor``, input = this rank's row of the output) on a real one-rank RCCL
+    communicator: bitwise equal to the run without collectives."""
+    dev = one_rank_nccl
+    outs = []
+    for coll in ("0", "1"):
+        monkeypatch.setenv("GARFIELD_COLL_WORLD1", coll)
+        calls = _Calls(monkeypatch)
+        eng = _resnet_engine(dev, shard_gar=False)
+        assert eng._shard is None
+        _run(eng, dev, steps=5)
+        assert calls.n["all_gather_into_tensor"] == (5 * 8 if coll == "1" else 0)
+        outs.append(eng.flat.reference_vector().clone())
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_byzps_on_one_rank_rccl(one_rank_nccl, monkeypatch):
+    """Byzantine-server mode (one server replica hosting its 8 workers, MAR over one model) with its
+    slot all-gathers and model broadcast on a real one-rank RCCL communicator: equal to the run
+    without collectives."""
+    from dataclasses import asdict
+
+    from garfield_amd.parallel.byzps import ByzantinePSDataParallel, ByzPSConfig
+    from garfield_amd.parallel.engine import EngineConfig
 
     dev = one_rank_nccl
-    monkeypatch.setenv("GARFIELD_LOOPBACK_EXCHANGE", "1")
-    monkeypatch.setenv("GARFIELD_OVERLAP", "1")
     outs = []
-    for direct in ("0", "1"):
-        monkeypatch.setenv("GARFIELD_DIRECT_RCCL", direct)
-        monkeypatch.setenv("GARFIELD_DIRECT_RCCL_WORLD1", direct)
-        torch.manual_seed(0)
-        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, shard_gar=True, lr=0.01, cuda_graph=True)
-        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=dev), cfg)
-        assert (eng._shard._rccl is not None) == (direct == "1")
-        for it in range(10):
-            eng.step(synthetic_batches(8, 8, (3, 32, 32), 10, dev, seed=300 + it))
-        eng.synchronize()
-        torch.cuda.synchronize()
-        assert isinstance(eng._ggraph, list) and len(eng._ggraph) == 3 and eng._shard.staged
-        outs.append((eng.flat.reference_vector().clone(), eng.momentum_vector().clone()))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for coll in ("0", "1"):
+        monkeypatch.setenv("GARFIELD_COLL_WORLD1", coll)
+        calls = _Calls(monkeypatch)
+        base = EngineConfig(gar="krum", f=2, workers_per_rank=8, lr=0.01, cuda_graph=True, byzantine={6: "reverse"})
+        cfg = ByzPSConfig(**asdict(base), num_ps=1, fps=0, mar="median", ps_workers=True)
+        eng = _resnet_engine(dev, cls=ByzantinePSDataParallel, cfg=cfg)
+        _run(eng, dev, steps=4)
+        assert calls.n["broadcast"] == (1 + 4 if coll == "1" else 0)   # initial weights + one model per step
+        assert calls.n["all_gather_into_tensor"] == (4 * 8 if coll == "1" else 0)
+        outs.append(eng.flat.reference_vector().clone())
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_quorum_engine_on_one_rank_rccl(one_rank_nccl, monkeypatch):
+    """The asynchronous-quorum engine's per-root broadcast groups and decision group (``new_group``
+    subgroups of a real RCCL communicator, one rank: quorum 1 = this rank): the update equals the
+    synchronous engine's on the same rows."""
+    from dataclasses import asdict
+
+    from garfield_amd.parallel.engine import EngineConfig
+    from garfield_amd.parallel.quorum import QuorumConfig, QuorumDataParallel
+
+    dev = one_rank_nccl
+    outs = []
+    for quorum in (False, True):
+        monkeypatch.setenv("GARFIELD_COLL_WORLD1", "1" if quorum else "0")
+        base = EngineConfig(gar="krum", f=2, workers_per_rank=8, lr=0.01, cuda_graph=True, shard_gar=False)
+        if quorum:
+            eng = _resnet_engine(dev, cls=QuorumDataParallel, cfg=QuorumConfig(**asdict(base)))
+        else:
+            eng = _resnet_engine(dev, cfg=base)
+        _run(eng, dev, steps=4)
+        if quorum:
+            eng.finish()
+            assert eng.last_quorum == [0] and eng.skipped == 0
+        outs.append(eng.flat.reference_vector().clone())
+    assert torch.equal(outs[0], outs[1])

@@ -289,3 +289,40 @@ def test_byzantine_server_config5_attacked_server_is_rejected():
         hit = [torch.load(os.path.join(d, f"reverse_{r}.pt"), weights_only=True)["flat"] for r in range(world)]
     assert all(torch.equal(c, clean[0]) for c in clean)
     assert all(torch.equal(h, clean[0]) for h in hit)
+
+
+def _world1_worker(port, outdir):
+    """One rank, gloo: the sharded step with its collectives (GARFIELD_COLL_WORLD1=1) vs without."""
+    import torch.distributed as dist
+
+    from garfield_amd.parallel.comm import DistContext
+
+    outs = []
+    for coll in ("0", "1"):
+        os.environ["GARFIELD_COLL_WORLD1"] = coll
+        if coll == "1":
+            dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        torch.manual_seed(0)
+        eng = RobustDataParallel(build_model("convnet"), F.nll_loss, DistContext(backend="gloo" if coll == "1" else "none"),
+                                 EngineConfig(gar="krum", f=1, workers_per_rank=5, shard_gar=True, lr=0.05))
+        assert eng._shard._coll == (coll == "1")
+        for it in range(3):
+            eng.step(synthetic_batches(5, 4, (1, 28, 28), 10, torch.device("cpu"), seed=it))
+        eng.sync_master()
+        outs.append((eng.flat.reference_vector().clone(), eng.momentum_vector().clone()))
+    dist.destroy_process_group()
+    torch.save(outs, os.path.join(outdir, "w1.pt"))
+
+
+def test_world1_collectives_equal_shortcuts():
+    """GARFIELD_COLL_WORLD1=1 on a one-rank gloo group: the multi-rank sharded call sequence
+    (packed all_to_all per bucket, partial-Gram all-gather, weight all-gathers, sync_master,
+    momentum_vector) equals the world-1 shortcuts bit for bit (the GPU twin runs on a one-rank
+    RCCL communicator: tests/test_rccl_gpu.py)."""
+    with tempfile.TemporaryDirectory() as d:
+        p = mp.get_context("spawn").Process(target=_world1_worker, args=(free_port(), d))
+        p.start()
+        p.join(300)
+        assert p.exitcode == 0
+        (a, ma), (b, mb) = torch.load(os.path.join(d, "w1.pt"), weights_only=True)
+        assert torch.equal(a, b) and torch.equal(ma, mb)
