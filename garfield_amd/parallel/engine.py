@@ -245,6 +245,7 @@ class RobustDataParallel:
         self._graph = None
         self._graph_failed = False
         self._tuning_agreed = False
+        self._routed: set = set()     # (rows, sample shape) of grouped steps routed to the per-worker path
         self._static = None
         self._static_loss = None
         self._gexec = None
@@ -802,7 +803,27 @@ class RobustDataParallel:
         if len(batches) != self.k:
             return False
         x0, y0 = batches[0]
-        return x0.dim() == 4 and all(x.shape == x0.shape and y.shape == y0.shape for x, y in batches)
+        if not (x0.dim() == 4 and all(x.shape == x0.shape and y.shape == y0.shape for x, y in batches)):
+            return False
+        return self._grouped_fits(x0.shape[0], tuple(x0.shape[1:]))
+
+    def _grouped_fits(self, batch: int, sample_shape: tuple) -> bool:
+        """Capacity routing, decided before anything runs or is captured: a grouped step whose largest
+        tensor would pass the kernels' 32-bit indexing (e.g. 16 ImageNet workers x 250 images on one GPU:
+        a 3.2e9-element stem activation) runs its workers one at a time instead (warned once)."""
+        from garfield_amd.parallel import grouped
+        from garfield_amd.utils.logging import warning
+
+        rows = self.k * int(batch)
+        if grouped.fits(self.model, rows, sample_shape):
+            return True
+        key = (rows, sample_shape)
+        if key not in self._routed:
+            self._routed.add(key)
+            warning(f"grouped step of {self.k} workers x {batch} images {sample_shape}: its largest tensor has "
+                    f"{grouped.largest_index(self.model, rows, sample_shape)} elements (> {grouped.INDEX_LIMIT}, the "
+                    f"kernels' 32-bit indexing); running the workers one at a time")
+        return False
 
     def _ensure_gbuf(self, B: int, sample_shape: tuple, label_shape: tuple = (), label_dtype=torch.int64) -> None:
         shape = (self.k * B, *sample_shape)
@@ -818,7 +839,7 @@ class RobustDataParallel:
         """The grouped step's static input buffers ([k*batch, *sample_shape] channels_last, bf16 or
         fp32 by the step's precision, and the labels) for a producer that writes each step's batch in place
         (``data.fresh.DeviceBatches.attach``): no staging copy. None when the step is not grouped."""
-        if self._gexec is None:
+        if self._gexec is None or not self._grouped_fits(int(batch), tuple(sample_shape)):
             return None
         self._ensure_gbuf(int(batch), tuple(sample_shape), (), label_dtype)
         return self._gx, self._gy

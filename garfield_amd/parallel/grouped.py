@@ -46,6 +46,48 @@ def supports(model: nn.Module) -> bool:
     return isinstance(model.maxpool, (nn.MaxPool2d, nn.Identity))
 
 
+INDEX_LIMIT = 2 ** 31 - 1   # the grouped kernels index activations with 32-bit element offsets
+_CAPACITY: dict = {}
+
+
+def largest_index(model: ResNet, rows: int, sample_shape) -> int:
+    """The largest element count a grouped step of ``rows`` images of ``sample_shape`` must index:
+    every convolution's input and output, every BatchNorm / pooling / ReLU output, the logits, and
+    the column matrix (pixels x taps x Cin) of the strided k x k convolutions whose data gradient can
+    take the dcol GEMM + col2im form (the stem runs on its own implicit kernels). Shapes come from a
+    forward on meta tensors (no memory, no kernel); cached per (model, rows, shape)."""
+    key = (id(model), int(rows), tuple(sample_shape))
+    hit = _CAPACITY.get(key)
+    if hit is not None:
+        return hit
+    sizes = [int(rows) * int(torch.Size(sample_shape).numel())]
+
+    def hook(mod, inp, out):
+        sizes.append(out.numel())
+        if isinstance(mod, nn.Conv2d):
+            sizes.append(inp[0].numel())
+            kh, kw = mod.kernel_size
+            if mod is not model.conv1 and kh * kw > 1 and tuple(mod.stride) != (1, 1):
+                sizes.append(out.numel() // mod.out_channels * mod.in_channels * kh * kw)
+
+    hooks = [m.register_forward_hook(hook) for m in model.modules()
+             if isinstance(m, (nn.Conv2d, nn.BatchNorm2d, nn.MaxPool2d, nn.ReLU, nn.Linear, nn.AdaptiveAvgPool2d))]
+    state = {n: torch.empty_like(t, device="meta") for n, t in [*model.named_parameters(), *model.named_buffers()]}
+    try:
+        with torch.no_grad():
+            torch.func.functional_call(model, state, (torch.empty((rows, *sample_shape), device="meta"),))
+    finally:
+        for h in hooks:
+            h.remove()
+    _CAPACITY[key] = out = max(sizes)
+    return out
+
+
+def fits(model: ResNet, rows: int, sample_shape) -> bool:
+    """Whether a grouped step of ``rows`` images stays within the kernels' 32-bit indexing."""
+    return largest_index(model, rows, sample_shape) <= INDEX_LIMIT
+
+
 class GroupedResNet:
     """Forward + backward of ``groups`` workers' micro-batches in one pass.
 

@@ -88,7 +88,7 @@ def main():
         for c in range(C.gemm_nt_num_cfg()):
             if c == cfg or not C.gemm_nt_valid(c, N, K) or (rg and C.gemm_nt_stats_rows(c) > rg):
                 continue
-            if kw and not C.gemm_nt_pro_ok(c, K, M // kw["pro_groups"], kw["pro_groups"]):
+            if kw.get("pro_groups") and not C.gemm_nt_pro_ok(c, K, M // kw["pro_groups"], kw["pro_groups"]):
                 continue
             t = timed(run(c))
             if t < t_best:

@@ -8,7 +8,7 @@ mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_rccl_gpu.py \
   "tests/test_engine_gpu.py::test_resume_in_new_process_replays_kernel_choices" \
   "tests/test_engine_gpu.py::test_capture_after_dropping_engine_in_reference_cycle" \
-  -k "not nothing" tests/test_grouped_gpu.py::test_bn_folded_shortcut_matches_fp32_reference > $O/pytest.log 2>&1 &&
+  tests/test_grouped_gpu.py::test_bn_folded_shortcut_matches_fp32_reference > $O/pytest.log 2>&1 &&
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-fp32 > $O/bench_plain.json.log 2>&1 &&
 GARFIELD_COLL_WORLD1=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-fp32 --shard-gar > $O/bench_coll1_shard.json.log 2>&1 &&
 GARFIELD_LOOPBACK_EXCHANGE=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-fp32 --shard-gar > $O/bench_loopback_shard.json.log 2>&1 &&

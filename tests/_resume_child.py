@@ -37,9 +37,9 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     eng = RobustDataParallel(build_model("resnet50"), F.cross_entropy, DistContext(device=dev),
-                             EngineConfig(gar="krum", f=1, workers_per_rank=4, lr=0.02, cuda_graph=True))
+                             EngineConfig(gar="krum", f=1, workers_per_rank=5, lr=0.02, cuda_graph=True))
     load_engine(ck, eng)
-    batches = synthetic_batches(4, 8, (3, 32, 32), 10, dev)
+    batches = synthetic_batches(5, 8, (3, 32, 32), 10, dev)
     for _ in range(2):
         eng.step(batches)
     torch.cuda.synchronize()

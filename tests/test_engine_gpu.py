@@ -483,8 +483,8 @@ def test_resume_in_new_process_replays_kernel_choices(cuda, tmp_path):
 
     torch.manual_seed(0)
     eng = RobustDataParallel(build_model("resnet50"), F.cross_entropy, DistContext(device=cuda),
-                             EngineConfig(gar="krum", f=1, workers_per_rank=4, lr=0.02, cuda_graph=True))
-    batches = synthetic_batches(4, 8, (3, 32, 32), 10, cuda)
+                             EngineConfig(gar="krum", f=1, workers_per_rank=5, lr=0.02, cuda_graph=True))
+    batches = synthetic_batches(5, 8, (3, 32, 32), 10, cuda)
     for _ in range(2):
         eng.step(batches)
     ck = str(tmp_path / "ck.pt")
@@ -515,9 +515,9 @@ def test_capture_after_dropping_engine_in_reference_cycle(cuda):
     def make():
         torch.manual_seed(0)
         return RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda),
-                                  EngineConfig(gar="krum", f=1, workers_per_rank=4, lr=0.02, cuda_graph=True))
+                                  EngineConfig(gar="krum", f=1, workers_per_rank=5, lr=0.02, cuda_graph=True))
 
-    batches = synthetic_batches(4, 8, (3, 32, 32), 10, cuda)
+    batches = synthetic_batches(5, 8, (3, 32, 32), 10, cuda)
     old = make()
     for _ in range(3):
         old.step(batches)

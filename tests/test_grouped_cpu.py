@@ -115,3 +115,38 @@ def test_masked_grad_materialize_applies_bits_in_memory_order():
     out = MaskedGrad(dy, w).materialize()
     assert out.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(rows2d(out).reshape(-1), torch.where(keep, flat, torch.zeros(())))
+
+
+def test_largest_index_counts_activations_and_strided_columns():
+    """Capacity accounting of the grouped step (meta-tensor forward): ResNet-50 ImageNet shape, the
+    layer1 output (rows x 256 x 56 x 56) or layer2's stride-2 3x3 column matrix, whichever is larger."""
+    from garfield_amd.parallel import grouped
+
+    m = build_model("resnet50", 1000)
+    for rows in (8, 4000):
+        want = max(rows * 256 * 56 * 56, rows * 28 * 28 * 9 * 128)
+        assert grouped.largest_index(m, rows, (3, 224, 224)) == want
+    assert grouped.fits(m, 2000, (3, 224, 224)) and not grouped.fits(m, 4000, (3, 224, 224))
+
+
+def test_oversized_grouped_step_routes_to_per_worker_path(monkeypatch):
+    """A grouped step past the kernels' 32-bit indexing runs its workers one at a time (decided before
+    any kernel runs, not a mid-step error): with the limit lowered below the job's size the engine
+    steps like the per-worker engine (same math; its model is channels_last, so not bit for bit)."""
+    from garfield_amd.parallel import grouped
+
+    batches = synthetic_batches(5, 4, (3, 32, 32), 10, torch.device("cpu"))
+    outs = []
+    for wb in (True, False):
+        torch.manual_seed(0)
+        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(),
+                                 EngineConfig(gar="krum", f=1, workers_per_rank=5, lr=0.05, worker_batching=wb,
+                                              exchange_dtype=torch.float32, autocast_dtype=None))
+        if wb:
+            assert eng._gexec is not None
+            monkeypatch.setattr(grouped, "INDEX_LIMIT", grouped.largest_index(eng.model, 20, (3, 32, 32)) - 1)
+            assert not eng._groupable(batches) and eng.grouped_inputs(4, (3, 32, 32)) is None
+        for _ in range(2):
+            eng.step(batches)
+        outs.append(eng.flat.reference_vector().clone())
+    assert ((outs[0] - outs[1]).norm() / outs[1].norm()).item() < 1e-3   # as test_engine_worker_batching_matches_per_worker
