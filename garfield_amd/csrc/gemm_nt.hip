@@ -89,21 +89,33 @@ __device__ __forceinline__ void pro_chunk(char* p, const float* sc, const float*
 // ---------------------------------------------------------------------------------------------
 // K-loop kernel
 
-template <int WPM, int WPN, int WM, int WN, int NS, int EPI, bool PRO>
-__global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
-                                                 int M, int N, int K, uint16_t* __restrict__ C,
-                                                 const uint16_t* __restrict__ add, float* __restrict__ stats,
-                                                 int64_t rg, GemmPro pro) {
+// KG > 1 (in-workgroup split-K): KG groups of 4 waves (256 * KG threads) walk consecutive quarters
+// (halves) of the K range over their own LDS rings, so each SIMD holds KG waves to hide the ring's
+// latency with, and each group makes 1 / KG of the serial k-steps. The groups' fp32 accumulators
+// are summed in group order through LDS (deterministic) and group 0 runs the epilogue. For the
+// latency-bound small-M problems (ResNet-50 CIFAR layer3 / layer4: ~250 workgroups, 16-32 k-steps
+// each at one wave per SIMD), without the split-K slabs' second launch and fp32 HBM round trip.
+// The ring then lives in dynamic LDS (> 64 KB).
+template <int WPM, int WPN, int WM, int WN, int NS, int EPI, bool PRO, int KG = 1>
+__global__ __launch_bounds__(256 * KG) void k_gemm_nt(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                      int M, int N, int K, uint16_t* __restrict__ C,
+                                                      const uint16_t* __restrict__ add, float* __restrict__ stats,
+                                                      int64_t rg, GemmPro pro) {
   static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(KG == 1 || (!PRO && EPI != EPI_SPLIT), "in-workgroup split-K: plain / add / statistics epilogues");
   constexpr int BM = 16 * WPM * WM, BN = 16 * WPN * WN;
   constexpr int AB = BM * 128, BB = BN * 128, SB = AB + BB;
   constexpr int AI = BM / 32, BI = BN / 32;     // glds instructions per wave per stage
   constexpr int PER = AI + BI;
   static_assert(BM % 32 == 0 && BN % 32 == 0, "tiles are whole 8-row glds blocks per wave");
-  __shared__ __attribute__((aligned(16))) char lds[NS * SB];
+  static_assert(KG == 1 || (KG - 1) * 4 * WPM * WPN * 1024 <= KG * NS * SB, "the group sums fit the rings");
+  __shared__ __attribute__((aligned(16))) char lds_s[KG == 1 ? NS * SB : 16];
+  extern __shared__ __attribute__((aligned(16))) char lds_d[];
+  char* const lds = KG == 1 ? lds_s : lds_d;
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = (threadIdx.x >> 6) & 3;
+  const int kg = KG == 1 ? 0 : static_cast<int>(threadIdx.x >> 8);   // K group
   const int tiles_n = N / BN;
   const int nt = gridDim.x;
   const int b = blockIdx.x;
@@ -132,7 +144,9 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
     bsrc[u] = B + static_cast<int64_t>(n0 + row) * K + kbase + (lchunk ^ lrow) * 8;
   }
   const uint64_t az = reinterpret_cast<uint64_t>(reinterpret_cast<const uint16_t*>(g_gemm_zero) + lchunk * 8);
-  const int steps = KS / 64;
+  const int steps = KS / 64 / KG;                // (K / 64) % KG == 0: every group makes the same k-steps
+  const int kstep0 = kg * steps;                 // this group's first k-step
+  char* const ring = lds + kg * NS * SB;
 
   // PRO: the [2][K] scale and shift of the tile's (at most two) workers: rows of worker g0 use entry 0
   extern __shared__ __attribute__((aligned(16))) float ptab[];
@@ -150,8 +164,8 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
   }
 
   auto issue = [&](int s, int slot) {
-    char* base = lds + slot * SB;
-    const int k0 = s * 64;
+    char* base = ring + slot * SB;
+    const int k0 = (kstep0 + s) * 64;
 #pragma unroll
     for (int u = 0; u < AI; ++u) {
       const uint64_t a = reinterpret_cast<uint64_t>(asrc[u] + k0);
@@ -208,7 +222,7 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
     else wait_landed(s, issued);
     __builtin_amdgcn_s_barrier();
     if (s + NS - 1 < steps) issue(s + NS - 1, (s + NS - 1) % NS);
-    const char* base = lds + (s % NS) * SB;
+    const char* base = ring + (s % NS) * SB;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = (ks * 4 + fq) ^ (fr & 7);
@@ -252,10 +266,36 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
   // lines per 8 lanes). Statistics come from the registers (wave_stats).
   constexpr int TP = BN * 2 + 16;                       // LDS row pitch (bytes)
   constexpr int CPR = BN / 8;                           // 16-byte chunks per tile row
-  constexpr int RL = 256 / CPR;                         // tile rows per pass of the workgroup
+  constexpr int RL = 256 * KG / CPR;                    // tile rows per pass of the workgroup
   static_assert(BM * TP <= NS * SB, "epilogue tile fits the ring");
   __syncthreads();                                      // every wave's last ring reads are done
-  {
+  if constexpr (KG > 1) {   // the groups' accumulators, summed in group order into group 0's
+    constexpr int WB = WPM * WPN * 1024;                // bytes of one wave's accumulators
+    if (kg > 0) {
+#pragma unroll
+      for (int r = 0; r < WPM; ++r)
+#pragma unroll
+        for (int c = 0; c < WPN; ++c)
+          *reinterpret_cast<f32x4*>(lds + ((kg - 1) * 4 + wave) * WB + ((r * WPN + c) * 64 + lane) * 16) = acc[r][c];
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+      for (int q = 1; q < KG; ++q)
+#pragma unroll
+        for (int r = 0; r < WPM; ++r)
+#pragma unroll
+          for (int c = 0; c < WPN; ++c) {
+            const f32x4 o = *reinterpret_cast<const f32x4*>(lds + ((q - 1) * 4 + wave) * WB + ((r * WPN + c) * 64 + lane) * 16);
+            acc[r][c][0] += o[0];
+            acc[r][c][1] += o[1];
+            acc[r][c][2] += o[2];
+            acc[r][c][3] += o[3];
+          }
+    }
+    __syncthreads();                                    // the sums are read before the tile reuses the LDS
+  }
+  if (kg == 0) {
     const int mwl = wm * 16 * WPM;                      // first tile row of this wave
     const int nwl = wn * 16 * WPN + 4 * fq;             // first tile channel of this lane (c = 0)
     float vs[WPM][WPN][4];
@@ -287,7 +327,7 @@ __global__ __launch_bounds__(256) void k_gemm_nt(const uint16_t* __restrict__ A,
       if (m0 + mwl < M) wave_stats<WPM, WPN>(vs, m0 + mwl, M, rg, N, n0 + wn * 16 * WPN, stats);
   }
   __syncthreads();
-  const int ck = threadIdx.x % CPR, rl = threadIdx.x / CPR;
+  const int ck = static_cast<int>(threadIdx.x) % CPR, rl = static_cast<int>(threadIdx.x) / CPR;
   const int rows = M - m0 < BM ? M - m0 : BM;
   for (int rr = rl; rr < rows; rr += RL) {
     const uint4 v = *reinterpret_cast<const uint4*>(lds + rr * TP + ck * 16);
@@ -691,11 +731,33 @@ void launch_split(const uint16_t* A, const uint16_t* B, int M, int N, int K, uin
   else hipLaunchKernelGGL((k_split_sum<false>), g2, dim3(256), 0, stream, ws, S, n8, C, add, amask);
 }
 
-template <int WPM, int WPN, int WM, int WN, int NS>
+template <int WPM, int WPN, int WM, int WN, int NS, int KG = 1>
 void launch_cfg(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t* C, const uint16_t* add,
                 float* stats, int64_t rg, hipStream_t stream, const GemmPro& pro) {
   constexpr int BM = 16 * WPM * WM, BN = 16 * WPN * WN;
   const dim3 grid(((M + BM - 1) / BM) * (N / BN));
+  if constexpr (KG > 1) {   // in-workgroup split-K: 256 * KG threads, the KG rings in dynamic LDS
+    constexpr int lds = KG * NS * (BM + BN) * 128;
+    static_assert(lds <= 160 * 1024, "LDS");
+    static bool once = (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_STATS, false, KG>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds),
+                        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_ADD, false, KG>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds),
+                        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_PLAIN, false, KG>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds),
+                        true);
+    (void)once;
+    if (stats)
+      hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_STATS, false, KG>), grid, dim3(256 * KG), lds, stream, A, B,
+                         M, N, K, C, add, stats, rg, pro);
+    else if (add)
+      hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_ADD, false, KG>), grid, dim3(256 * KG), lds, stream, A, B,
+                         M, N, K, C, add, stats, rg, pro);
+    else
+      hipLaunchKernelGGL((k_gemm_nt<WPM, WPN, WM, WN, NS, EPI_PLAIN, false, KG>), grid, dim3(256 * KG), lds, stream, A, B,
+                         M, N, K, C, add, stats, rg, pro);
+    return;
+  }
   if (pro.sc) {   // forward of a 1x1 convolution over a pre-BatchNorm input (plain or statistics epilogue)
     const size_t tab = static_cast<size_t>(4) * K * sizeof(float);
     if (stats)
@@ -793,10 +855,18 @@ constexpr int kWsBN[] = {256, 256, 128, 128, 64, 64};
 constexpr int kWsRW[] = {32, 64, 16, 32, 16, 32};
 constexpr int kNumBase = kNumNt + 6;
 constexpr int kSplits[] = {2, 4};                       // split-K variants of the K-loop configurations
-constexpr int kNumCfg = kNumBase + 2 * kNumNt;
-// configuration -> (K-loop configuration, splits); splits 1 for the base configurations
-inline int split_of(int cfg) { return cfg >= kNumBase ? kSplits[(cfg - kNumBase) / kNumNt] : 1; }
-inline int base_of(int cfg) { return cfg >= kNumBase ? (cfg - kNumBase) % kNumNt : cfg; }
+constexpr int kNumSplit = kNumBase + 2 * kNumNt;        // first in-workgroup split-K configuration
+// in-workgroup split-K variants (k_gemm_nt KG): {K-loop configuration, K groups}
+constexpr int kKgBase[] = {7, 7, 4, 2, 8};
+constexpr int kKgK[] = {2, 4, 2, 2, 2};
+constexpr int kNumCfg = kNumSplit + 5;
+// configuration -> (K-loop configuration, splits, K groups); 1 / 1 for the base configurations
+inline int split_of(int cfg) { return cfg >= kNumBase && cfg < kNumSplit ? kSplits[(cfg - kNumBase) / kNumNt] : 1; }
+inline int kg_of(int cfg) { return cfg >= kNumSplit && cfg < kNumCfg ? kKgK[cfg - kNumSplit] : 1; }
+inline int base_of(int cfg) {
+  if (cfg >= kNumSplit) return kKgBase[cfg - kNumSplit];
+  return cfg >= kNumBase ? (cfg - kNumBase) % kNumNt : cfg;
+}
 
 bool ws_fits(int i, int K) {
   const int kb = K / 64;
@@ -896,6 +966,7 @@ bool gemm_nt_pro_ok(int cfg, int K, int64_t prg, int groups) {
 
 bool gemm_nt_valid(int cfg, int N, int K) {
   if (cfg < 0 || cfg >= kNumCfg || K % 64 || K <= 0) return false;
+  if (cfg >= kNumSplit) return K % (64 * kg_of(cfg)) == 0 && N % kCfgBN[base_of(cfg)] == 0;
   if (cfg >= kNumBase) return K % (64 * split_of(cfg)) == 0 && N % kCfgBN[base_of(cfg)] == 0 && N % 8 == 0;
   if (cfg < kNumNt) return N % kCfgBN[cfg] == 0;
   return N % kWsBN[cfg - kNumNt] == 0 && ws_fits(cfg - kNumNt, K);
@@ -916,6 +987,7 @@ int gemm_nt_tile_n(int cfg) {
   return 0;
 }
 int gemm_nt_stats_rows(int cfg) {
+  if (cfg >= kNumSplit && cfg < kNumCfg) return kCfgSR[base_of(cfg)];   // in-workgroup split-K: as its base
   if (cfg >= kNumBase) return 1 << 30;   // split-K forms have no statistics epilogue
   if (cfg >= 0 && cfg < kNumNt) return kCfgSR[cfg];
   if (cfg >= kNumNt && cfg < kNumCfg) return ws_bm(kWsBN[cfg - kNumNt], kWsRW[cfg - kNumNt]);
@@ -923,8 +995,8 @@ int gemm_nt_stats_rows(int cfg) {
 }
 
 void gemm_nt_stats_geometry(int cfg, int64_t M, int N, int K, int64_t rg, int64_t* H, int* E) {
-  if (cfg >= 0 && cfg < kNumNt) {
-    *H = kCfgSR[cfg];
+  if ((cfg >= 0 && cfg < kNumNt) || (cfg >= kNumSplit && cfg < kNumCfg)) {
+    *H = kCfgSR[base_of(cfg)];
     *E = 1;
     return;
   }
@@ -970,6 +1042,18 @@ void gemm_nt(const uint16_t* A, const uint16_t* B, int M, int N, int K, uint16_t
              float* stats, int64_t rg, int cfg, hipStream_t stream, const float* pro_scale, const float* pro_shift,
              int64_t pro_rg, int pro_groups, float* split_ws, const uint8_t* add_mask) {
   if (M <= 0) return;
+  if (cfg >= kNumSplit) {   // in-workgroup split-K (no prologue)
+    GemmPro pk{};
+    pk.amask = add ? add_mask : nullptr;
+    switch (cfg - kNumSplit) {
+      case 0: launch_cfg<2, 2, 2, 2, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream, pk); break;
+      case 1: launch_cfg<2, 2, 2, 2, 2, 4>(A, B, M, N, K, C, add, stats, rg, stream, pk); break;
+      case 2: launch_cfg<2, 2, 2, 2, 4, 2>(A, B, M, N, K, C, add, stats, rg, stream, pk); break;
+      case 3: launch_cfg<2, 4, 2, 2, 3, 2>(A, B, M, N, K, C, add, stats, rg, stream, pk); break;
+      default: launch_cfg<2, 4, 1, 4, 2, 2>(A, B, M, N, K, C, add, stats, rg, stream, pk); break;
+    }
+    return;
+  }
   if (cfg >= kNumBase) {   // split-K (no statistics, no prologue; the caller provides the fp32 slabs)
     const int S = split_of(cfg);
     switch (base_of(cfg)) {

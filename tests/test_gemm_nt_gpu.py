@@ -14,7 +14,7 @@ def rel(a, b):
 
 @pytest.mark.parametrize("M,K,N", [(128000, 64, 256), (4000, 256, 64), (2000, 512, 2048), (1000, 1024, 256),
                                    (333, 128, 128), (77, 64, 64), (128000, 256, 128), (32000, 128, 512),
-                                   (8000, 256, 1024), (5000, 192, 64)])
+                                   (8000, 256, 1024), (5000, 192, 64), (8000, 1024, 256), (2000, 2048, 512)])
 def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
     torch.manual_seed(M + K + N)
     a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
@@ -25,7 +25,9 @@ def test_gemm_nt_every_config_matches_fp32(cuda, native, M, K, N):
     bits = ((mask.unsqueeze(1) >> torch.arange(8, device=cuda, dtype=torch.uint8)) & 1).view(M, N).bool()
     masked = torch.where(bits, add, torch.zeros((), device=cuda, dtype=torch.bfloat16))
     ran = splits = 0
-    for cfg in range(native.gemm_nt_num_cfg()):   # split-K forms included (fp32 slabs + one summing pass)
+    # split-K forms included (fp32 slabs + one summing pass), and the in-workgroup split-K ones (KG groups of
+    # 4 waves summed through LDS)
+    for cfg in range(native.gemm_nt_num_cfg()):
         if not native.gemm_nt_valid(cfg, N, K):
             continue
         c = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
