@@ -39,7 +39,6 @@ test suite); on the GPU the native extension is mandatory.
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 import torch.nn.functional as F
@@ -76,26 +75,27 @@ GEMM_NT_DGRAD = True
 CONV3X3 = True
 # A bottleneck's bn2 + ReLU applied inside its 1x1 conv3 (GEMM prologue, weight-gradient prologue, ReLU test
 # recomputed in the BatchNorm backward): the normalised activation is never written (_GroupedBNConv).
-BN_PROLOGUE = os.environ.get("GARFIELD_BN_PROLOGUE", "0") == "1"
+# Measured slower on the CIFAR and ImageNet steps (profiles/r5/bn_prologue/): off; tests exercise it.
+BN_PROLOGUE = False
 # Data gradients of the stride-2 convolutions (3x3 downsampling, 1x1 projection shortcut) on the parity-class
 # MFMA kernel (iconv_nhwc.hip S2) instead of a dcol GEMM + col2im, per layer where the first (eager) step
 # measured it faster (ResNet-18 CIFAR: 15.20 -> 14.93 ms/step; ResNet-50 CIFAR / ImageNet layers keep the
 # GEMM: profiles/r5/s2_dgrad/).
-S2_DGRAD = os.environ.get("GARFIELD_S2_DGRAD", "1") == "1"
+S2_DGRAD = True
 _S2_CHOICE: dict = tuning.register("s2", {})   # (dy shape, w shape, dx shape, kernel, padding) -> use the parity-class kernel
 S2_FORCE = False        # tests: take the parity-class kernel wherever it fits, unmeasured
 # 3x3 / stride-1 / pad-1 convolutions on images of at most 2x2 pixels (ResNet-50 CIFAR layer3 / layer4) as
 # dense GEMMs over [N, P * C] rows with the per-step expanded weight (sconv_nhwc.hip): no out-of-image
 # taps computed (2.25x / 9x of the useful MFMA work on the implicit-GEMM / im2col paths).
-SMALL_CONV = os.environ.get("GARFIELD_SMALL_CONV", "1") == "1"
+SMALL_CONV = True
 # An identity block's residual gradient (dres = dy masked by the last BatchNorm's ReLU) is not written by
 # that BatchNorm's backward when the block's conv1 is a 1x1 GEMM: conv1's data-gradient epilogue adds
 # dy where the forward's ReLU bit is set (gpu_gemm_nt add_mask), saving dres's write and re-read (MaskedGrad).
-LAZY_RES = os.environ.get("GARFIELD_LAZY_RES", "1") == "1"
+LAZY_RES = True
 # A projection block's shortcut BatchNorm folded into the block's last BatchNorm (statistics pass only,
 # its scale / shift applied to the pre-BatchNorm shortcut inside the last BatchNorm's apply pass, its
 # backward run there too): the shortcut's normalised activation is never written (_GroupedBN res_st).
-FOLD_SHORTCUT_BN = os.environ.get("GARFIELD_FOLD_SHORTCUT_BN", "1") == "1"
+FOLD_SHORTCUT_BN = True
 # ... and its backward shares one statistics pass and one apply pass with the last BatchNorm's (a ReLU-bit
 # mask or none; tests set False to run the two-call form, which a saved ReLU output still takes)
 BN_DUAL = True

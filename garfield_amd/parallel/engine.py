@@ -1059,18 +1059,15 @@ class RobustDataParallel:
         torch.cuda.synchronize()
         graphs = [None] * self.k
         pool = None
-        shared = os.environ.get("GARFIELD_GRAPH_SHARED_POOL", "1") == "1"
-        warm = int(os.environ.get("GARFIELD_GRAPH_WARMUP", "1"))
         try:
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             # warm-up ON THE CAPTURE STREAM (lazy per-stream library state: BLAS / MIOpen
             # workspaces, algorithm caches) before any capture
             with torch.cuda.stream(s):
-                for _ in range(warm):
-                    for j in self.local_slots:
-                        x, y = self._static[j]
-                        self._worker_body(j, x, y, self._static_loss[j])
+                for j in self.local_slots:
+                    x, y = self._static[j]
+                    self._worker_body(j, x, y, self._static_loss[j])
             s.synchronize()
             for j in self.local_slots:
                 g = torch.cuda.CUDAGraph()
@@ -1078,7 +1075,7 @@ class RobustDataParallel:
                 with _capture_guard(), torch.cuda.graph(g, stream=s, pool=pool, capture_error_mode=mode):
                     x, y = self._static[j]
                     self._worker_body(j, x, y, self._static_loss[j])
-                if pool is None and shared:
+                if pool is None:
                     pool = g.pool()
                 graphs[j] = g
             torch.cuda.current_stream(self.device).wait_stream(s)

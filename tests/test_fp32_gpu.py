@@ -266,7 +266,8 @@ def _cpu_grads(model, x, y) -> torch.Tensor:
 
 def _fp32_rows_vs_references(cuda, name, k, B, bn_bias=None, shape=(3, 32, 32)):
     """Per worker: (ours vs float64 CPU autograd, PyTorch fp32 CPU autograd vs float64, ours vs fp32
-    CPU autograd, ours vs fp32 GPU autograd, fp32 GPU autograd vs float64). bn_bias: every
+    CPU autograd, ours vs fp32 GPU autograd, fp32 GPU autograd vs float64, ours vs float64 on the
+    classifier's weight + bias alone, PyTorch fp32 CPU vs float64 on the classifier). bn_bias: every
     BatchNorm shift set to this value first."""
     torch.manual_seed(0)
     ref = build_model(name, 10).to(cuda)
@@ -298,7 +299,9 @@ def _fp32_rows_vs_references(cuda, name, k, B, bn_bias=None, shape=(3, 32, 32)):
         xc, yc = x.float().cpu(), y.cpu()
         g64 = _cpu_grads(m64, xc.double(), yc)
         g32 = _cpu_grads(m32, xc, yc)
-        out.append((rel(g_eng, g64), rel(g32, g64), rel(g_eng, g32), rel(g_eng, g_gpu32), rel(g_gpu32, g64)))
+        nfc = sum(p.numel() for p in ref.fc.parameters())   # registered last
+        out.append((rel(g_eng, g64), rel(g32, g64), rel(g_eng, g32), rel(g_eng, g_gpu32), rel(g_gpu32, g64),
+                    rel(g_eng[-nfc:], g64[-nfc:]), rel(g32[-nfc:], g64[-nfc:])))
     return out
 
 
@@ -313,7 +316,7 @@ def test_fp32_grouped_rows_match_fp32_autograd(cuda, name):
     res = _fp32_rows_vs_references(cuda, name, 4, 8, bn_bias=6.0)
     print(name, "(ours-fp64, torch32cpu-fp64, ours-torch32cpu, ours-torch32gpu, torch32gpu-fp64):",
           [tuple(f"{v:.2e}" for v in r) for r in res])
-    for ours64, cpu64, ours32, _, _ in res:
+    for ours64, cpu64, ours32, *_ in res:
         assert ours64 < 1e-4 and ours32 < 1e-4, res
         assert ours64 < 3 * cpu64 + 1e-6, res     # as close to float64 as PyTorch's fp32
 
@@ -326,11 +329,16 @@ def test_fp32_grouped_rows_at_init_within_the_kink_floor(cuda, name, floor):
     (ResNet-50). PyTorch's own fp32 CPU autograd -- the reference's precision -- differs from
     float64 by that much on such workers, and a 1e-7 relative weight perturbation moves the float64
     gradient as far (scripts/diag_fp32_rows.py). So here: every worker within that floor of float64
-    (no gross error anywhere); the per-worker errors are printed next to PyTorch fp32's."""
+    (no gross error anywhere), and -- the tight part -- the classifier's gradient (no backward ReLU
+    between it and the loss: a smooth function of the forward, whose kinks move activations by only
+    a rounding) within 1e-5 of float64, like PyTorch's fp32, on every worker; the per-worker errors
+    are printed next to PyTorch fp32's."""
     res = _fp32_rows_vs_references(cuda, name, 4, 8)
-    print(name, "(ours-fp64, torch32cpu-fp64, ours-torch32cpu, ours-torch32gpu, torch32gpu-fp64):",
-          [tuple(f"{v:.2e}" for v in r) for r in res])
+    print(name, "(ours-fp64, torch32cpu-fp64, ours-torch32cpu, ours-torch32gpu, torch32gpu-fp64, fc ours-fp64, "
+          "fc torch32cpu-fp64):", [tuple(f"{v:.2e}" for v in r) for r in res])
     assert max(r[0] for r in res) < floor, res
+    for r in res:
+        assert r[5] < 1e-5 or r[5] < 3 * r[6], res   # the classifier: as close to float64 as PyTorch's fp32
 
 
 def test_fp32_grouped_graph_step_matches_eager(cuda):
