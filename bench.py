@@ -227,7 +227,7 @@ def main():
     model = build_model(a.model, num_classes=num_classes)
     d = num_parameters(model)
     fp32 = a.precision == "fp32"
-    eng, batches, xdt, amp = build_job(a, ctx, model, shape, num_classes, fp32)
+    eng, batches, _, _ = build_job(a, ctx, model, shape, num_classes, fp32)
     if a.resume:
         from garfield_amd.utils.checkpoint import load_engine
 
@@ -260,13 +260,12 @@ def main():
             eng.step(batches() if callable(batches) else batches)
         extra["phase_ms"] = {k: round(v, 3) for k, v in eng.phase_times().items()}
     if a.overhead:
-        cfg_avg = EngineConfig(gar="average", f=a.f, workers_per_rank=a.workers_per_gpu, lr=a.lr, momentum=0.9,
-                               weight_decay=5e-4, exchange_dtype=xdt, channels_last=a.channels_last,
-                               cuda_graph=not a.no_graph, lp_weights=not a.no_lp_weights,
-                               worker_batching=False if a.no_worker_batching else None, **amp)
+        # the same job (precision, exchange, executor, data) with the average GAR
+        a_avg = argparse.Namespace(**{**vars(a), "gar": "average", "attack": "", "layerwise": False})
         torch.manual_seed(1234)
-        eng_avg = RobustDataParallel(build_model(a.model, num_classes=num_classes), F.cross_entropy, ctx, cfg_avg)
-        e_avg, _ = timed_steps(eng_avg, batches, a.steps, a.warmup, ctx)
+        eng_avg, b_avg, _, _ = build_job(a_avg, ctx, build_model(a.model, num_classes=num_classes), shape,
+                                         num_classes, fp32)
+        e_avg, _ = timed_steps(eng_avg, b_avg, a.steps, a.warmup, ctx)
         ms_avg = 1000.0 * e_avg / a.steps
         extra.update({"avg_ms_per_step": round(ms_avg, 3),
                       "gar_overhead_pct_vs_average": round(100.0 * (ms - ms_avg) / ms_avg, 3)})

@@ -474,6 +474,24 @@ void g_bn_backward_dual(const at::Tensor& xa, const at::Tensor& xb, const at::Te
   }
 }
 
+}  // namespace
+
+namespace garfield {
+namespace gpu {
+// Experiment switches of kernel forms under measurement (A/B runs set them; 0 is the default form).
+static std::map<std::string, int>& variant_table() {
+  static std::map<std::string, int> m;
+  return m;
+}
+int kernel_variant(const char* name) {
+  const auto& m = variant_table();
+  const auto it = m.find(name);
+  return it == m.end() ? 0 : it->second;
+}
+}  // namespace gpu
+}  // namespace garfield
+
+namespace {
 int xent_dtype(const at::Tensor& t, const char* what) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.dim() == 2, "gpu_xent: ", what, " must be a contiguous 2-D GPU tensor");
   if (t.scalar_type() == at::kFloat) return garfield::kF32;
@@ -2119,6 +2137,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gpu_transpose_multi", &g_transpose_multi,
         "dsts[i] = srcs[i]ᵀ for 2-D bf16 matrices (dims multiples of 8), one launch per 40 matrices",
         py::arg("srcs"), py::arg("dsts"));
+  m.def("_set_kernel_variant", [](const std::string& name, int64_t v) {
+    garfield::gpu::variant_table()[name] = static_cast<int>(v);
+  }, py::arg("name"), py::arg("value"), "Experiment switch of a kernel form under measurement (0: default)");
   m.def("gemm_nt_num_cfg", &garfield::gpu::gemm_nt_num_cfg, "Number of gpu_gemm_nt tile configurations");
   m.def("gemm_nt_splits", &garfield::gpu::gemm_nt_splits, py::arg("cfg"),
         "Split-K factor of a gpu_gemm_nt configuration (1: none)");

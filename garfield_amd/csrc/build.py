@@ -32,7 +32,7 @@ HIP_SOURCES = [
     "gar_coord_m0.hip", "gar_coord_m1.hip", "gar_coord_m2.hip",
     "gar_coord_m3.hip", "gar_coord_m4.hip", "gar_coord_m5.hip",
     "bn_nhwc.hip", "im2col_nhwc.hip", "iconv_nhwc.hip", "gemm_nt.hip", "data_aug.hip", "gar_large.hip", "loss_xent.hip", "stream_signal.hip", "stem_nhwc.hip",
-    "gar_layerwise.hip", "conv3x3_nhwc.hip", "conv_f32.hip", "sconv_nhwc.hip",
+    "gar_layerwise.hip", "conv3x3_nhwc.hip", "conv_f32.hip", "sconv_nhwc.hip", "gar_tail_f32.hip",
 ]
 TORCH_SOURCES = ["bindings.cpp", "mailbox.cpp", "rccl_direct.cpp"]   # need torch + HIP headers
 PLAIN_SOURCES = ["threadpool.cpp", "gar_cpu.cpp"]  # plain C++17

@@ -578,6 +578,11 @@ bool launch_bulyan_tail_mfma(const RowTable& rows, int n, int64_t d, int beta, c
   return true;
 }
 
+// fp32, n <= 64, t <= 64, e = t - beta <= 16: the register kernel of gar_tail_f32.hip; otherwise false
+// (generic kernels)
+bool launch_bulyan_tail_f32(const RowTable& rows, int n, int64_t d, int beta, const float* W, int t, void* out,
+                            int out_dt, hipStream_t s);
+
 }  // namespace coord
 }  // namespace gpu
 }  // namespace garfield

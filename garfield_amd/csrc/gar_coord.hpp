@@ -314,6 +314,9 @@ void launch_coord(const RowTable& rows, int n, int64_t d, int f, int beta, const
         launch_bulyan_tail_mfma<DT>(rows, n, d, beta, W, t, out, out_dt, s))
       return;
   }
+  if constexpr (MODE == kBulyanTail && DT == kF32) {
+    if (n <= 64 && coord16_enabled() && launch_bulyan_tail_f32(rows, n, d, beta, W, t, out, out_dt, s)) return;
+  }
   if constexpr ((MODE == kBulyanTail || MODE == kAveragedMedian) && NP <= 64) {
     const int tt = MODE == kBulyanTail ? t : n;
     if (n <= 64 && tt - beta <= kTailMaxExcluded && coord16_enabled()) {

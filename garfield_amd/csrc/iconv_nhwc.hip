@@ -1005,12 +1005,15 @@ __global__ __launch_bounds__(256) void k_iwgrad_1x1(const uint16_t* __restrict__
 // transposed; 3-deep ring (96 KB: one workgroup per CU).
 constexpr int kW1Stage = 4 * 64 * 128;   // bytes per stage: dy0 | dy1 | x0 | x1
 
-template <bool OUT_BF16, bool PRO>
+// NS: ring depth (3: 96 KB, one workgroup per CU; 2: 64 KB, two, for splits of at most four 64-pixel
+// stages, where a workgroup's whole K loop is shorter than the load latency the third stage hides:
+// ResNet-50 CIFAR layer4, 10.9-21.8 vs 13.6-26.3 us per call, profiles/r6/iwgrad_wide/). (A 16-byte
+// LDS-staged epilogue measured no faster than the 2-byte stores, which merge in L2.)
+template <bool OUT_BF16, bool PRO, int NS = 3>
 __global__ __launch_bounds__(256) void k_iwgrad_1x1_wide(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                          Im2col g, int Cout, int64_t rg, int64_t per_split, void* out,
                                                          int64_t split_stride, int64_t group_stride,
                                                          const float* __restrict__ psc, const float* __restrict__ psh) {
-  constexpr int NS = 3;
   constexpr int SUB = 64 * 128;          // one [64 px][64 ch] sub-tile
   extern __shared__ __attribute__((aligned(16))) char wlds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1175,11 +1178,22 @@ void iwgrad_launch(const uint16_t* x, const uint16_t* dy, const Im2col& g, int C
                                             hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kW1Stage),
                         hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iwgrad_1x1_wide<false, PRO>),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, 3 * kW1Stage),
+                        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iwgrad_1x1_wide<true, PRO, 2>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kW1Stage),
+                        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_iwgrad_1x1_wide<false, PRO, 2>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kW1Stage),
                         true);
     (void)once;
     const dim3 grid((g.C / 128) * (Cout / 128), groups, splits);
-    if (out_bf16)
+    const bool ns2 = (per_split + 63) / 64 <= 4;
+    if (out_bf16 && ns2)
+      hipLaunchKernelGGL((k_iwgrad_1x1_wide<true, PRO, 2>), grid, dim3(256), 2 * kW1Stage, stream, x, dy, g, Cout, rg,
+                         per_split, out, split_stride, group_stride, psc, psh);
+    else if (out_bf16)
       hipLaunchKernelGGL((k_iwgrad_1x1_wide<true, PRO>), grid, dim3(256), 3 * kW1Stage, stream, x, dy, g, Cout, rg,
+                         per_split, out, split_stride, group_stride, psc, psh);
+    else if (ns2)
+      hipLaunchKernelGGL((k_iwgrad_1x1_wide<false, PRO, 2>), grid, dim3(256), 2 * kW1Stage, stream, x, dy, g, Cout, rg,
                          per_split, out, split_stride, group_stride, psc, psh);
     else
       hipLaunchKernelGGL((k_iwgrad_1x1_wide<false, PRO>), grid, dim3(256), 3 * kW1Stage, stream, x, dy, g, Cout, rg,

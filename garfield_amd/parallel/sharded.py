@@ -102,16 +102,20 @@ def overlap_enabled(world: int = 1) -> bool:
 class _Bucket:
     """One layer bucket [lo, hi) of the flat vector, cut into ``world`` shards of S.
 
-    ``send[dst, j]`` = local worker j's shard ``dst`` (torch.distributed path only: packed so
-    the whole bucket leaves in ONE ``all_to_all_single``), ``recv[src, j]`` = shard ``rank`` of source
-    rank src's local worker j (the row of global slot j * world + src)."""
+    This rank's own shard never moves (its rows are read in place from the exchange rows).
+    ``send[i, j]`` = local worker j's shard for the i-th OTHER rank in rank order (torch.distributed
+    path only: packed so the whole bucket leaves in ONE ``all_to_all_single`` with an empty chunk for
+    this rank), ``recv[pos[src], j]`` = shard ``rank`` of source rank src's local worker j (the row of
+    global slot j * world + src), pos[src] = src below this rank, src - 1 above it; with ``slots`` =
+    world the last slot holds this rank's own rows for the one-matrix (more than MAX_ROWS rows) path."""
 
-    def __init__(self, lo: int, hi: int, world: int, rank: int, k: int, dev, dt, coll: bool, pack: bool):
+    def __init__(self, lo: int, hi: int, world: int, rank: int, k: int, dev, dt, coll: bool, pack: bool,
+                 slots: int):
         self.lo, self.hi = lo, hi
         self.S = (hi - lo) // world
         self.own = slice(lo + rank * self.S, lo + (rank + 1) * self.S)
-        self.send = torch.empty((world, k, self.S), dtype=dt, device=dev) if coll and pack else None
-        self.recv = torch.empty((world, k, self.S), dtype=dt, device=dev) if coll else None
+        self.send = torch.empty((world - 1, k, self.S), dtype=dt, device=dev) if coll and pack else None
+        self.recv = torch.empty((slots, k, self.S), dtype=dt, device=dev) if coll else None
         self.p2p = None        # the direct exchange's (sends, to, recvs, from) lists
         self.moff = 0          # offset of this bucket's shard in the momentum buffer
         self.works: list = []
@@ -152,8 +156,12 @@ class ShardedAggregator:
         # whether the step issues its collectives (several ranks, or the forced one-rank run)
         self._coll = self.world > 1 or forced
         # ready order of the backward: highest coordinates (last layers) first
+        # receive slot of each source rank (this rank's own rows: the last slot, one-matrix path only)
+        self._pos = [src if src < self.rank else src - 1 for src in range(self.world)]
+        self._pos[self.rank] = self.world - 1
+        slots = self.world if self.n > gar.MAX_ROWS else self.world - 1
         self.buckets = [_Bucket(edges[i], edges[i + 1], self.world, self.rank, self.k, dev, dt, self._coll,
-                                self._rccl is None) for i in reversed(range(len(edges) - 1))]
+                                self._rccl is None, slots) for i in reversed(range(len(edges) - 1))]
         off = 0
         for b in sorted(self.buckets, key=lambda b: b.lo):
             b.moff = off
@@ -178,22 +186,21 @@ class ShardedAggregator:
     # layout
 
     def _rows_of(self, b: _Bucket) -> list:
-        """Row (global slot j * world + src) -> its shard of bucket b, in slot order. On the
-        direct exchange this rank's own workers' rows are read in place from the exchange
-        rows (the own shard never moves); the packed all_to_all receives them in recv[rank]."""
+        """Row (global slot j * world + src) -> its shard of bucket b, in slot order. This rank's
+        own workers' rows are read in place from the exchange rows (the own shard never moves)."""
         e = self.e
         if not self._coll:
             return [e.X[j, 0, b.lo:b.hi] for j in range(self.k)]
         rows = []
         for s in range(self.n):
             src, j = s % self.world, s // self.world
-            rows.append(e.X[j, 0, b.own] if src == self.rank and self._rccl is not None else b.recv[src, j])
+            rows.append(e.X[j, 0, b.own] if src == self.rank else b.recv[self._pos[src], j])
         return rows
 
     def _p2p_of(self, b: _Bucket):
         """The direct exchange of bucket b as point-to-point transfers with no packing copy:
         local worker j's shard dst (contiguous in its exchange row) goes to rank dst, and
-        source rank src's worker j lands in recv[src, j]; pairs match in issue order."""
+        source rank src's worker j lands in recv[pos[src], j]; pairs match in issue order."""
         e, W = self.e, self.world
         sends, to, recvs, frm = [], [], [], []
         for d in range(1, W):
@@ -202,7 +209,7 @@ class ShardedAggregator:
             for j in range(self.k):
                 sends.append(e.X[j, 0, b.lo + dst * b.S:b.lo + (dst + 1) * b.S])
                 to.append(dst)
-                recvs.append(b.recv[src, j])
+                recvs.append(b.recv[self._pos[src], j])
                 frm.append(src)
         return sends, to, recvs, frm
 
@@ -281,8 +288,14 @@ class ShardedAggregator:
                     self._rccl.exchange(*b.p2p, self._comm_stream)
                 elif self._coll:
                     local = e.X[:, 0, b.lo:b.hi].view(self.k, self.world, b.S).transpose(0, 1)   # [dst, j, S]
-                    b.send.copy_(local)
-                    b.works.append(dist.all_to_all_single(b.recv.view(-1), b.send.view(-1), async_op=True))
+                    r, W = self.rank, self.world
+                    if r > 0:
+                        b.send[:r].copy_(local[:r])
+                    if r < W - 1:
+                        b.send[r:].copy_(local[r + 1:])
+                    split = [0 if q == r else self.k * b.S for q in range(W)]   # nothing to or from itself
+                    b.works.append(dist.all_to_all_single(b.recv[:W - 1].view(-1), b.send.view(-1), split, split,
+                                                          async_op=True))
                 if side:
                     b.done = torch.cuda.Event(enable_timing=_TIMING)
                     b.done.record(s)
@@ -569,12 +582,11 @@ class ShardedAggregator:
         self._update_buckets(update)
 
     def _matrix(self, b: _Bucket) -> torch.Tensor:
-        """Bucket b's received shards as ONE [n, S] matrix (row src * k + j: the receive
-        buffer as it lands, no copy); ``self._perm[s]`` is the matrix row of global slot s."""
+        """Bucket b's received shards as ONE [n, S] matrix (row pos[src] * k + j: the receive
+        buffer as it lands, this rank's own rows copied into the last slot)."""
         if not self._coll:
             return torch.stack(b.rows)
-        if self._rccl is not None:   # the own shard was read in place: bring it into the matrix
-            b.recv[self.rank].copy_(self.e.X[:, 0, b.own])
+        b.recv[self.world - 1].copy_(self.e.X[:, 0, b.own])
         return b.recv.view(self.n, b.S)
 
     def _gpu_large(self, cfg, first: bool) -> None:
@@ -586,7 +598,7 @@ class ShardedAggregator:
         rule, f, kw = cfg.gar, cfg.f, dict(cfg.gar_kwargs)
         n, k, world = self.n, self.k, self.world
         args = (cfg.lr, cfg.momentum, cfg.dampening, cfg.weight_decay, cfg.nesterov, first)
-        perm = torch.tensor([(s % world) * k + s // world for s in range(n)], device=e.device)
+        perm = torch.tensor([self._pos[s % world] * k + s // world for s in range(n)], device=e.device)
         mats = {}
         for b in self.buckets:
             self._wait(b)

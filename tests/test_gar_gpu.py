@@ -65,12 +65,13 @@ def test_bulyan(cuda, n, f, dtype):
     assert close(gar.bulyan(X, f), ref.bulyan(X, f), dtype)
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("n,f", [(26, 2), (40, 1), (64, 3)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n,f", [(26, 2), (40, 1), (64, 3), (16, 3)])
 def test_bulyan_tail_nonfinite_rows_take_exact_pass(cuda, n, f, dtype):
     """inf / NaN in a row that Krum never selects: the MFMA set sums of those
     64-coordinate groups turn NaN (0 * inf), so the groups go through the exact
-    per-set pass; the result must equal set means taken by indexing (fp64 oracle)."""
+    per-set pass (fp32: the register kernel's weighted sums likewise, per lane); the result
+    must equal set means taken by indexing (fp64 oracle)."""
     d = 64 * 40 + 37
     X = separated(n, d, torch.float32, "cpu", seed=n)
     cols = torch.arange(3, d, 97)

@@ -169,9 +169,10 @@ def test_iconv_matches_conv2d(cuda, native, N, C, Co, H, k, s, p, pm):
                                                      (2, 9, 64, 192, 3, 3, 1, 1, 3), (2, 5, 128, 256, 6, 1, 1, 0, 3),
                                                      (3, 4, 512, 64, 4, 1, 1, 0, 1), (2, 3, 64, 128, 5, 1, 1, 0, 2),
                                                      # 1x1 with C, Cout % 128: the 128 x 128-tile kernel (ragged
-                                                     # 64-pixel stages, stride 2, empty splits)
+                                                     # 64-pixel stages, stride 2, empty splits; splits of <= 4
+                                                     # stages on the depth-2 ring, the last case on depth 3)
                                                      (4, 5, 256, 512, 6, 1, 1, 0, 1), (3, 7, 128, 256, 8, 1, 2, 0, 4),
-                                                     (2, 2, 512, 128, 3, 1, 1, 0, 8)])
+                                                     (2, 2, 512, 128, 3, 1, 1, 0, 8), (2, 20, 128, 256, 8, 1, 1, 0, 1)])
 def test_iwgrad_matches_per_worker_conv_weight_grad(cuda, native, G, B, C, Co, H, k, s, p, splits):
     """Implicit per-worker weight gradient vs fp32 conv2d_weight of each worker's slice
     (ragged pixel splits, strides, padding, the fp32-slab and bf16 strided-view outputs)."""
