@@ -432,7 +432,10 @@ constexpr int kNuSmall = 10;  // PMF 2: 40 + 24 = 64 KB
 // Both operands are reduced over pixels, so fragments are read transposed (ds_read_b64_tr_b16:
 // lane 4q+p of a 16-lane group addresses pixel row 8*grp + 4h + q, channels 16f + 4p .. +3). The
 // staged 128-byte rows carry their 16-byte chunks XOR-swizzled by bits 1 and 3 of the row, which makes
-// those reads conflict-free on consecutive rows. Wave tile: 2 co fragments x 2 ci fragments x 9 taps.
+// those reads conflict-free on consecutive rows. Wave tile (WL 1, the default): all 4 co fragments x one
+// ci fragment x 9 taps, so each transposed read of the halo feeds four MFMAs instead of two (26 instead
+// of 40 fragment reads per 36 MFMAs: the kernel is bound by its LDS reads, not its MFMAs); WL 0 (2 co x
+// 2 ci) was 15-20 % slower per call on every ResNet-18 layer, bit-identical (profiles/r6/wgrad3x3/).
 __device__ __forceinline__ int tr_swz(int row) { return (((row >> 3) & 1) << 2) | (((row >> 1) & 1) << 1); }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -444,7 +447,7 @@ __device__ __forceinline__ s16x4 tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)((lds_ptr)p));
 }
 
-template <int NU, bool OUT_BF16>
+template <int NU, bool OUT_BF16, int WL = 1>
 __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                   Im2col g, Halo hp, int Cout, int64_t rg, int tiles_per_split,
                                                   void* out, int64_t split_stride, int64_t group_stride) {
@@ -485,15 +488,16 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
 
   // transposed-read addresses: lane (grp, q, p) of pixel rows 8*grp + 4h + q of each 32-pixel step
   const int grp = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
-  const int cf0 = 2 * (wave >> 1), kf0 = 2 * (wave & 1);
+  constexpr int NCF = WL == 0 ? 2 : 4, NKF = WL == 0 ? 2 : 1;   // co x ci fragments per wave
+  const int cf0 = WL == 0 ? 2 * (wave >> 1) : 0, kf0 = WL == 0 ? 2 * (wave & 1) : wave;
 
-  f32x4 acc[9][2][2];
+  f32x4 acc[9][NCF][NKF];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < NCF; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc[t][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < NKF; ++b) acc[t][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int tile = t0; tile < t1; ++tile) {
     const int64_t P0 = pbeg + static_cast<int64_t>(tile) * hp.TP;   // first pixel of the tile
@@ -536,26 +540,26 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
         // a pixel past TP has a zero dy row; it reads halo pixel 0 (finite) so 0 x stale LDS cannot be NaN
         hp0[h] = m < hp.TP ? seg * hp.SEGP + (static_cast<int>(t) - seg * hp.TRI) * hp.SW + static_cast<int>(col) : 0;
       }
-      // A = dyᵀ fragments of co fragments cf0, cf0 + 1: dy rows 32c + 8grp + 4h + q
-      s16x4 ra[4];
+      // A = dyᵀ fragments of co fragments cf0 .. cf0 + NCF - 1: dy rows 32c + 8grp + 4h + q
+      s16x4 ra[2 * NCF];
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < NCF; ++u)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int m = 32 * c + 8 * grp + 4 * h + q;
           const int ch = 2 * (cf0 + u) + (pp >> 1);
           ra[2 * u + h] = tr_read(lds + m * 128 + ((ch ^ tr_swz(m)) * 16) + (pp & 1) * 8);
         }
-      bf16x8 a[2];
+      bf16x8 a[NCF];
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < NCF; ++u)
         a[u] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(ra[2 * u], ra[2 * u + 1], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int toff = (tap / 3) * hp.SW + (tap % 3);
-        s16x4 rb[4];
+        s16x4 rb[2 * NKF];
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
+        for (int v = 0; v < NKF; ++v)
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int s = hp0[h] + toff;
@@ -563,11 +567,11 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
             rb[2 * v + h] = tr_read(lds + DB + s * 128 + ((ch ^ tr_swz(s)) * 16) + (pp & 1) * 8);
           }
 #pragma unroll
-        for (int v = 0; v < 2; ++v) {
+        for (int v = 0; v < NKF; ++v) {
           const bf16x8 b = __builtin_bit_cast(bf16x8,
                                               __builtin_shufflevector(rb[2 * v], rb[2 * v + 1], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
-          for (int u = 0; u < 2; ++u)
+          for (int u = 0; u < NCF; ++u)
             acc[tap][u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], b, acc[tap][u][v], 0, 0, 0);
         }
       }
@@ -579,9 +583,9 @@ __global__ __launch_bounds__(256, 2) void k_wgrad3x3(const uint16_t* __restrict_
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < NCF; ++u)
 #pragma unroll
-      for (int v = 0; v < 2; ++v)
+      for (int v = 0; v < NKF; ++v)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int co = co0 + (cf0 + u) * 16 + 4 * grp + e;
