@@ -535,3 +535,25 @@ def test_capture_after_dropping_engine_in_reference_cycle(cuda):
         gc.set_threshold(*thresholds)
     assert new._ggraph is not None
     assert torch.isfinite(new.flat_model()).all()
+
+
+def test_capacity_routing_at_the_boundary(cuda, monkeypatch):
+    """Capacity routing decided before capture: with the indexing limit at exactly the job's largest tensor
+    the step is grouped (one HIP graph); one element lower it runs the workers one at a time, and both
+    train (finite, changed parameters). The limit is lowered instead of allocating 2^31-element tensors."""
+    from garfield_amd.parallel import grouped
+
+    batches = synthetic_batches(5, 8, (3, 32, 32), 10, cuda)
+    for delta, want_grouped in ((0, True), (-1, False)):
+        torch.manual_seed(0)
+        eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda),
+                                 EngineConfig(gar="krum", f=1, workers_per_rank=5, lr=0.02, cuda_graph=True))
+        limit = grouped.largest_index(eng.model, 5 * 8, (3, 32, 32)) + delta
+        monkeypatch.setattr(grouped, "INDEX_LIMIT", limit)
+        before = eng.flat_model().clone()
+        for _ in range(3):
+            loss = eng.step(batches)
+        torch.cuda.synchronize()
+        assert (eng._ggraph is not None) == want_grouped
+        assert (eng._graph is not None) == (not want_grouped)   # the per-worker graphs
+        assert torch.isfinite(loss).item() and not torch.equal(before, eng.flat_model())
