@@ -294,8 +294,12 @@ class ShardedAggregator:
                     if r < W - 1:
                         b.send[r:].copy_(local[r + 1:])
                     split = [0 if q == r else self.k * b.S for q in range(W)]   # nothing to or from itself
-                    b.works.append(dist.all_to_all_single(b.recv[:W - 1].view(-1), b.send.view(-1), split, split,
-                                                          async_op=True))
+                    w = dist.all_to_all_single(b.recv[:W - 1].view(-1), b.send.view(-1), split, split,
+                                               async_op=True)
+                    if side:     # the COMM stream waits for RCCL's internal stream (the main stream only
+                        w.wait()  # ever waits on the comm stream's events: the cheap direction, signals.py)
+                    else:
+                        b.works.append(w)
                 if side:
                     b.done = torch.cuda.Event(enable_timing=_TIMING)
                     b.done.record(s)
@@ -330,6 +334,9 @@ class ShardedAggregator:
                 work = None
             else:
                 work = dist.all_gather_into_tensor(out.view(-1), src, async_op=True)
+                if self._comm_stream is not None:   # the comm stream waits, then the main stream on it
+                    work.wait()
+                    work = None
         self._back_to_main(work)
         return out
 
@@ -375,13 +382,20 @@ class ShardedAggregator:
             else:
                 if gloo_backend():
                     mine = mine.clone()  # gloo rejects an input aliasing the output
-                self._gathers.append(dist.all_gather_into_tensor(full, mine, async_op=True))
+                w = dist.all_gather_into_tensor(full, mine, async_op=True)
+                if self._comm_stream is not None:
+                    w.wait()    # stream-ordered on the comm stream, as the direct path
+                else:
+                    self._gathers.append(w)
             if b.np is not None:
                 idx, own_pos, own_idx, nb = b.np
                 nb.zero_()
                 nb[own_pos] = e.flat.data[own_idx]
                 if self._rccl is not None:   # stream-ordered: scattered back on the comm stream
                     self._rccl.all_reduce_sum(nb, self._comm_stream)
+                    e.flat.data[idx] = nb
+                elif self._comm_stream is not None:
+                    dist.all_reduce(nb, async_op=True).wait()
                     e.flat.data[idx] = nb
                 else:
                     self._gathers.append(dist.all_reduce(nb, async_op=True))
@@ -414,8 +428,9 @@ class ShardedAggregator:
 
     def staging_ok(self) -> bool:
         """Whether the updates can run beside the next forward: a comm stream, and every
-        collective stream-ordered on it (the direct RCCL path, or nothing to exchange)."""
-        return self._comm_stream is not None and (not self._coll or self._rccl is not None)
+        collective stream-ordered on it (the direct RCCL path; torch.distributed's works waited on
+        by the comm stream; or nothing to exchange)."""
+        return self._comm_stream is not None
 
     def _update_buckets(self, fn) -> None:
         """``fn(b)`` issues bucket b's update; buckets in update order (low coordinates first).

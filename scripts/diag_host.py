@@ -25,7 +25,7 @@ def main():
     eng = RobustDataParallel(build_model("resnet50", num_classes=10), F.cross_entropy, ctx,
                              EngineConfig(gar="krum", f=2, workers_per_rank=8, lr=0.01, momentum=0.9,
                                           weight_decay=5e-4, exchange_dtype=torch.bfloat16, cuda_graph=True,
-                                          lp_weights=True))
+                                          lp_weights=True, shard_gar=True if "--shard-gar" in sys.argv else None))
     batches = synthetic_batches(8, 250, (3, 32, 32), 10, ctx.device, seed=1)
     acc = {}
 
@@ -46,8 +46,11 @@ def main():
     wrap(eng, "aggregate_and_update")
     wrap(eng, "_stage_grouped")
     g = eng._ggraph
-    if g is not None:
-        wrap(g, "replay")
+    for gg in (g if isinstance(g, list) else [g] if g is not None else []):
+        wrap(gg, "replay")
+    if eng._shard is not None:   # the sharded exchange's host calls (python bench: --shard-gar)
+        for name in ("start_exchange", "_gather_bucket", "_gather_ranks", "_wait", "_finish_gathers"):
+            wrap(eng._shard, name)
     steps = 20
     per = []
     t0 = time.perf_counter()

@@ -110,7 +110,8 @@ def test_sharded_step_on_one_rank_rccl_equals_loopback(one_rank_nccl, monkeypatc
     shard]`` pack and one ``all_to_all_single`` issued from the comm stream after the device-side
     hand-off, the partial-Gram all-gather, the in-place ``all_gather_into_tensor`` of the bf16
     working weights, the BatchNorm-affine all-reduce, ``sync_master`` and ``momentum_vector``;
-    the grouped step captured with ``capture_error_mode="thread_local"`` beside RCCL's watchdog)
+    the grouped step captured with ``capture_error_mode="thread_local"`` beside RCCL's watchdog, as the
+    staged three-graph forward: every torch.distributed work is waited on by the comm stream)
     and the opt-in direct RCCL path (point-to-point from the exchange rows, staged three-graph
     forward), both as REAL RCCL calls on a one-rank communicator (``GARFIELD_COLL_WORLD1=1``).
     Ten HIP-graph steps with fresh inputs must be bitwise equal to the same step without any
@@ -135,9 +136,8 @@ def test_sharded_step_on_one_rank_rccl_equals_loopback(one_rank_nccl, monkeypatc
             assert calls.n["all_gather_into_tensor"] >= 10 * (nb + 1)  # weights per bucket + the partial Grams
             assert calls.n["all_reduce"] >= 10                         # BatchNorm affine (fp32 read directly)
             assert calls.n["broadcast_object_list"] == 1               # the kernel-choice agreement (ops/tuning)
-            assert not isinstance(eng._ggraph, list) and eng._ggraph is not None   # one graph (not staged)
-        else:
-            assert isinstance(eng._ggraph, list) and len(eng._ggraph) == 3 and sh.staged
+        # every path stream-ordered on the comm stream: the next forward staged at the bucket boundaries
+        assert isinstance(eng._ggraph, list) and len(eng._ggraph) == 3 and sh.staged
         eng.sync_master()
         outs.append((eng.flat.reference_vector().clone(), eng.momentum_vector().clone()))
         del eng, sh
