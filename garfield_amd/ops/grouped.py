@@ -602,19 +602,21 @@ def _gemm_cfg(a2: torch.Tensor, b2: torch.Tensor, rg: int, add: torch.Tensor | N
     out = torch.empty((M, N), dtype=a2.dtype, device=a2.device)
     addc = add.clone() if add is not None else None
     pkw = {} if pro is None else {"pro_scale": pro[0], "pro_shift": pro[1], "pro_groups": pro[2]}
-    best, best_t = cfg, float("inf")
-    for c in cands:
-        st = torch.empty(C_.gemm_nt_stats_geometry(c, M, N, K, rg)[2], device=a2.device) if rg else None
-        C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c, **pkw)   # warm
-        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0.record()
-        for _ in range(3):
-            C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c, **pkw)
-        t1.record()
-        t1.synchronize()
-        t = t0.elapsed_time(t1)
-        if t < best_t:
-            best, best_t = c, t
+    # two rounds over the candidates, each candidate's best of its rounds (5 calls after a warm one):
+    # a single short sample let clock / cache noise flip near-tied choices from run to run
+    times = {}
+    for _ in range(2):
+        for c in cands:
+            st = torch.empty(C_.gemm_nt_stats_geometry(c, M, N, K, rg)[2], device=a2.device) if rg else None
+            C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c, **pkw)   # warm
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0.record()
+            for _ in range(5):
+                C_.gpu_gemm_nt(a2, b2, addc if addc is not None else out, addc, st, rg, c, **pkw)
+            t1.record()
+            t1.synchronize()
+            times[c] = min(times.get(c, float("inf")), t0.elapsed_time(t1))
+    best = min(cands, key=lambda c: (times[c], c)) if cands else cfg
     _GEMM_CFG[key] = best
     return best
 
@@ -769,15 +771,19 @@ def _dcol_dx(dy2: torch.Tensor, w: torch.Tensor, kp: int, spec: "ConvSpec", xsha
     return dx
 
 
-def _timed(fn, reps: int = 3) -> float:
+def _timed(fn, reps: int = 5, rounds: int = 2) -> float:
+    """Best of ``rounds`` timings of ``reps`` calls (after a warm call)."""
     fn()
-    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0.record()
-    for _ in range(reps):
-        fn()
-    t1.record()
-    t1.synchronize()
-    return t0.elapsed_time(t1)
+    best = float("inf")
+    for _ in range(rounds):
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(reps):
+            fn()
+        t1.record()
+        t1.synchronize()
+        best = min(best, t0.elapsed_time(t1))
+    return best
 
 
 def _s2_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", xshape, add: torch.Tensor | None, kp: int):
@@ -1228,6 +1234,38 @@ def refresh_f32_weights(specs) -> None:
         _native.native().gpu_wsplit_multi(jobs)
 
 
+# Kernel form of each fp32 convolution (forward or data gradient), measured once like the gemm_nt tiles:
+# key (dgrad, src shape, out shape, geometry, add) -> (pm, ksplit) of gpu_conv_f32 (pm 11..15: pixel
+# fragments per wave 1 / 2 / 2 / 4 / 4 with a 3 / 3 / 2 / 2 / 3-deep ring; ksplit > 1: split-K slabs
+# summed by a second pass). The static choice (pm 0: 2 fragments, 2-deep ring, split-K below 400 tiles)
+# is one of the candidates, so measuring never picks a slower form than it, up to the timing noise.
+_F32_CONV_CFG: dict = tuning.register("f32conv", {})
+_F32_CONV_CANDS = [(pm, 1) for pm in (11, 12, 13, 14, 15)] + [(pm, S) for S in (2, 4, 8) for pm in (13, 14, 15)]
+
+
+def _f32_conv_cfg(src: torch.Tensor, w3: torch.Tensor, spec: "ConvSpec", dgrad: bool, out: torch.Tensor,
+                  add: torch.Tensor | None) -> tuple:
+    key = (bool(dgrad), tuple(src.shape), tuple(out.shape), _geom(spec), add is not None)
+    cfg = _F32_CONV_CFG.get(key)
+    if cfg is not None:
+        return tuple(cfg)
+    if torch.cuda.is_current_stream_capturing():
+        return (0, 0)
+    if not tuning.measuring():
+        _F32_CONV_CFG[key] = (0, 0)
+        return (0, 0)
+    C_ = _native.native()
+    scratch = torch.empty_like(out)
+    addc = add.clone() if add is not None else None
+    best, best_t = (0, 0), _timed(lambda: C_.gpu_conv_f32(src, w3, *_geom(spec), dgrad, scratch, addc))
+    for pm, S in _F32_CONV_CANDS:
+        t = _timed(lambda: C_.gpu_conv_f32(src, w3, *_geom(spec), dgrad, scratch, addc, pm, S))
+        if t < best_t:
+            best, best_t = (pm, S), t
+    _F32_CONV_CFG[key] = best
+    return best
+
+
 def _f32_forward(x: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> torch.Tensor:
     if spec.w3 is None:
         refresh_f32_weights([spec])
@@ -1237,7 +1275,8 @@ def _f32_forward(x: torch.Tensor, w: torch.Tensor, spec: "ConvSpec") -> torch.Te
     if _stem_shape(w, spec):
         _native.native().gpu_stem_fwd(x, spec.w3, y)
     else:
-        _native.native().gpu_conv_f32(x, spec.w3, *_geom(spec), False, y)
+        pm, S = _f32_conv_cfg(x, spec.w3, spec, False, y, None)
+        _native.native().gpu_conv_f32(x, spec.w3, *_geom(spec), False, y, None, pm, S)
     return y
 
 
@@ -1245,7 +1284,8 @@ def _f32_dgrad(dy: torch.Tensor, w: torch.Tensor, spec: "ConvSpec", xshape, add:
     """dx (+ add, written in place of add) of an fp32 convolution, any stride."""
     dx = add if add is not None else torch.empty(xshape, dtype=dy.dtype, device=dy.device,
                                                  memory_format=torch.channels_last)
-    _native.native().gpu_conv_f32(dy, spec.wt3, *_geom(spec), True, dx, add)
+    pm, S = _f32_conv_cfg(dy, spec.wt3, spec, True, dx, add)
+    _native.native().gpu_conv_f32(dy, spec.wt3, *_geom(spec), True, dx, add, pm, S)
     return dx
 
 

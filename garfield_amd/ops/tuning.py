@@ -52,9 +52,17 @@ def _lst(x):
     return [_lst(v) for v in x] if isinstance(x, (list, tuple)) else x
 
 
+def _val(v):
+    if isinstance(v, bool):
+        return v
+    if isinstance(v, (list, tuple)):
+        return tuple(_val(x) for x in v)
+    return int(v)
+
+
 def export() -> dict:
     """The whole table as plain lists / ints / bools (JSON and ``weights_only`` safe)."""
-    return {kind: [[_lst(k), v] for k, v in sorted(t.items(), key=repr)] for kind, t in _TABLES.items()}
+    return {kind: [[_lst(k), _lst(v)] for k, v in sorted(t.items(), key=repr)] for kind, t in _TABLES.items()}
 
 
 def load(table: dict | None, replace: bool = False) -> None:
@@ -62,7 +70,7 @@ def load(table: dict | None, replace: bool = False) -> None:
     if not table:
         return
     for kind, items in table.items():
-        entries = {_tup(k): (bool(v) if isinstance(v, bool) else int(v)) for k, v in items}
+        entries = {_tup(k): _val(v) for k, v in items}
         t = _TABLES.get(kind)
         if t is None:
             _PENDING.setdefault(kind, {}).update(entries)
