@@ -1296,6 +1296,53 @@ _F32_WGRAD_WG = 1024
 _F32_WGRAD_MINPIX = 250
 
 
+# (pixel splits, kernel form) of each fp32 weight gradient, measured once (ops/tuning.py): key (x shape, dy
+# shape, geometry, groups) -> (S, variant: 2 the 128 x 128 tile, 3 the 64 x 64 one). A split's cost counts
+# its share of the deferred slab sum (S slabs read, one row written, at the split-K sum's ~4.5 TB/s);
+# the static choice (up to ~1024 workgroups, >= 250 pixels per split) is a candidate.
+_F32_WGRAD_CFG: dict = tuning.register("f32wgrad", {})
+
+
+def _f32_wgrad_static(x: torch.Tensor, dy: torch.Tensor, G: int, cout: int, K: int) -> int:
+    rows = dy.shape[0] * dy.shape[2] * dy.shape[3] // G
+    tile = 128 if (x.shape[1] % 128 == 0 and cout % 128 == 0) else 64   # conv_f32.hip: the wide form
+    tiles = -(-K // tile) * (cout // tile) * G
+    S = 1
+    while S < 16 and tiles * S < _F32_WGRAD_WG and rows // (2 * S) >= _F32_WGRAD_MINPIX:
+        S *= 2
+    return S
+
+
+def _f32_wgrad_cfg(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int, cout: int, K: int) -> tuple:
+    key = (tuple(x.shape), tuple(dy.shape), _geom(spec), G)
+    cfg = _F32_WGRAD_CFG.get(key)
+    if cfg is not None:
+        return tuple(cfg)
+    static = (_f32_wgrad_static(x, dy, G, cout, K), 0)
+    if torch.cuda.is_current_stream_capturing():
+        return static
+    if not tuning.measuring():
+        _F32_WGRAD_CFG[key] = static
+        return static
+    C_ = _native.native()
+    rows = dy.shape[0] * dy.shape[2] * dy.shape[3] // G
+    wide = x.shape[1] % 128 == 0 and cout % 128 == 0
+    variants = (2, 3) if wide else (3,)
+    cands = [(S, v) for S in (1, 2, 4, 8, 16) if S == 1 or rows // S >= 64 for v in variants]
+    slab = G * cout * K * 4
+    best, best_t = None, float("inf")
+    for S, v in cands:
+        part = torch.empty((S, G, cout, K), dtype=torch.float32, device=dy.device)
+        t = _timed(lambda: C_.gpu_wgrad_f32(x, dy, *_geom(spec), G, part, S, v)) / 5.0
+        if S > 1:
+            t += (S + 1) * slab / 4.5e9   # ms: the deferred sum of the S slabs into the row
+        if t < best_t:
+            best, best_t = (S, v), t
+        del part
+    _F32_WGRAD_CFG[key] = best
+    return best
+
+
 def _f32_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> None:
     """Per-worker fp32 weight gradients straight into the (fp32) exchange rows, or as split
     slabs summed there by the deferred split-K reduction."""
@@ -1306,18 +1353,13 @@ def _f32_wgrad(x: torch.Tensor, dy: torch.Tensor, spec: "ConvSpec", G: int) -> N
         return
     cout = dy.shape[1]
     K = w.numel() // cout
-    rows = dy.shape[0] * dy.shape[2] * dy.shape[3] // G
-    tile = 128 if (x.shape[1] % 128 == 0 and cout % 128 == 0) else 64   # conv_f32.hip: the wide form
-    tiles = -(-K // tile) * (cout // tile) * G
-    S = 1
-    while S < 16 and tiles * S < _F32_WGRAD_WG and rows // (2 * S) >= _F32_WGRAD_MINPIX:
-        S *= 2
+    S, var = _f32_wgrad_cfg(x, dy, spec, G, cout, K)
     out = spec.sink.rows_view(w, (cout, K), torch.float32) if S == 1 else None
     if out is not None:
-        C_.gpu_wgrad_f32(x, dy, *_geom(spec), G, out, 1)
+        C_.gpu_wgrad_f32(x, dy, *_geom(spec), G, out, 1, var)
         return
     part = torch.empty((S, G, cout, K), dtype=torch.float32, device=dy.device)
-    C_.gpu_wgrad_f32(x, dy, *_geom(spec), G, part, S)
+    C_.gpu_wgrad_f32(x, dy, *_geom(spec), G, part, S, var)
     rows_v = spec.sink.rows_view(w, (cout, K), spec.sink.flat.dtype)
     if rows_v is not None:
         spec.sink.queue_split(part, rows_v)
