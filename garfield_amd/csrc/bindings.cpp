@@ -2282,6 +2282,41 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                                    stream_of(dev));
   }, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"),
      "bf16 classifier forward y = x wᵀ + b (fp32 accumulation, one rounding)");
+  m.def("gpu_head_weights", [check_bf16_mat](const at::Tensor& w, const at::Tensor& wp, const at::Tensor& wpt) {
+    const auto dev = w.device();
+    TORCH_CHECK(w.dim() == 2 && wp.dim() == 2, "gpu_head_weights: 2-D weights");
+    const int64_t O = w.size(0), F = w.size(1), Op = wp.size(0);
+    TORCH_CHECK(F % 64 == 0 && Op % 64 == 0 && Op >= O && O > 0, "gpu_head_weights: F and Op multiples of 64, Op >= O");
+    check_bf16_mat(w, dev, O, F, "w");
+    check_bf16_mat(wp, dev, Op, F, "wp");
+    check_bf16_mat(wpt, dev, F, Op, "wpt");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0, "gpu_head_weights: w must be 16-byte aligned");
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::head_weights_bf16(reinterpret_cast<const uint16_t*>(w.data_ptr()), static_cast<int>(O),
+                                     static_cast<int>(F), static_cast<int>(Op), reinterpret_cast<uint16_t*>(wp.data_ptr()),
+                                     reinterpret_cast<uint16_t*>(wpt.data_ptr()), stream_of(dev));
+  }, py::arg("w"), py::arg("wp"), py::arg("wpt"),
+     "Padded copies of a wide head's weight: wp [Op, F] (zero rows) and wpt [F, Op] (zero columns)");
+  m.def("gpu_repitch", [check_bf16_mat](const at::Tensor& src, const at::Tensor& dst, const c10::optional<at::Tensor>& b) {
+    const auto dev = src.device();
+    TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && src.size(0) == dst.size(0), "gpu_repitch: [R, a] -> [R, b]");
+    const int64_t R = src.size(0), a = src.size(1), bb = dst.size(1);
+    TORCH_CHECK(a % 8 == 0 && bb % 8 == 0, "gpu_repitch: row lengths must be multiples of 8");
+    check_bf16_mat(src, dev, R, a, "src");
+    check_bf16_mat(dst, dev, R, bb, "dst");
+    const uint16_t* bp = nullptr;
+    if (b.has_value() && b->defined()) {
+      check_bf16_mat(*b, dev, 1, std::min(a, bb), "b");
+      bp = reinterpret_cast<const uint16_t*>(b->data_ptr());
+      TORCH_CHECK(reinterpret_cast<uintptr_t>(bp) % 16 == 0, "gpu_repitch: b must be 16-byte aligned");
+    }
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
+                "gpu_repitch: src and dst must be 16-byte aligned");
+    c10::hip::HIPGuard guard(dev.index());
+    garfield::gpu::repitch_bf16(reinterpret_cast<const uint16_t*>(src.data_ptr()), static_cast<int>(a),
+                                reinterpret_cast<uint16_t*>(dst.data_ptr()), static_cast<int>(bb), R, bp, stream_of(dev));
+  }, py::arg("src"), py::arg("dst"), py::arg("b"),
+     "bf16 rows [R, a] -> [R, b]: cropped or zero-padded, + b on the copied columns");
   m.def("gpu_linear_bf16_dgrad", [check_bf16_mat](const at::Tensor& dl, const at::Tensor& w, const at::Tensor& dx) {
     const auto dev = dl.device();
     const int64_t R = dl.size(0), O = dl.size(1), F = w.size(1);

@@ -1293,6 +1293,85 @@ void wsplit_multi(const WSplitJob* jobs, int count, hipStream_t stream) {
   }
 }
 
+namespace {
+// Wide bf16 classifier heads (O > kLinV outputs, e.g. ImageNet's 1000 classes) are GEMMs: they run on
+// gemm_nt.hip (and the 1x1 weight-gradient kernel) with the output dimension padded to Op, a multiple
+// of 64. Once per step one launch writes wp [Op][F] (rows >= O zero: the forward's B operand) and
+// wpt [F][Op] (columns >= O zero: the data gradient's B operand) from w [O][F], through a 64 x 64 LDS
+// tile (row pitch 72: the column reads of the transpose spread over the banks).
+constexpr int kHT = 64;
+
+__device__ __forceinline__ uint4 pack8_u16(const uint16_t (&e)[8]) {
+  return make_uint4(e[0] | (static_cast<uint32_t>(e[1]) << 16), e[2] | (static_cast<uint32_t>(e[3]) << 16),
+                    e[4] | (static_cast<uint32_t>(e[5]) << 16), e[6] | (static_cast<uint32_t>(e[7]) << 16));
+}
+
+__global__ __launch_bounds__(256) void k_head_weights(const uint16_t* __restrict__ w, int O, int F, int Op,
+                                                      uint16_t* __restrict__ wp, uint16_t* __restrict__ wpt) {
+  __shared__ __attribute__((aligned(16))) uint16_t t[kHT][kHT + 8];
+  const int f0 = blockIdx.x * kHT, o0 = blockIdx.y * kHT;
+  for (int i = threadIdx.x; i < kHT * 8; i += 256) {
+    const int r = i / 8, cv = (i % 8) * 8;
+    const int o = o0 + r;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (o < O) v = *reinterpret_cast<const uint4*>(w + static_cast<int64_t>(o) * F + f0 + cv);
+    *reinterpret_cast<uint4*>(wp + static_cast<int64_t>(o) * F + f0 + cv) = v;
+    *reinterpret_cast<uint4*>(&t[r][cv]) = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHT * 8; i += 256) {
+    const int fr = i / 8, ov = (i % 8) * 8;
+    uint16_t e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = t[ov + k][fr];
+    *reinterpret_cast<uint4*>(wpt + static_cast<int64_t>(f0 + fr) * Op + o0 + ov) = pack8_u16(e);
+  }
+}
+
+// bf16 rows re-pitched: dst[r][c] = src[r][c] (+ bias[c], added in fp32, one rounding) for c < min(a, b),
+// 0 for a <= c < b (the padded head's logits cropped, its logit gradient padded)
+__global__ __launch_bounds__(256) void k_repitch(const uint16_t* __restrict__ src, int a, uint16_t* __restrict__ dst,
+                                                 int b, int64_t R, const uint16_t* __restrict__ bias) {
+  const int nv = b / 8, ncp = a < b ? a : b;
+  const int64_t items = R * nv;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < items;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t r = i / nv;
+    const int c = static_cast<int>(i - r * nv) * 8;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (c < ncp) {
+      v = *reinterpret_cast<const uint4*>(src + r * a + c);
+      if (bias) {
+        const uint4 bv = *reinterpret_cast<const uint4*>(bias + c);
+        const uint32_t xs[4] = {v.x, v.y, v.z, v.w}, bs[4] = {bv.x, bv.y, bv.z, bv.w};
+        uint16_t e[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          e[2 * k] = f_to_bf16(__uint_as_float(xs[k] << 16) + __uint_as_float(bs[k] << 16));
+          e[2 * k + 1] = f_to_bf16(__uint_as_float(xs[k] & 0xffff0000u) + __uint_as_float(bs[k] & 0xffff0000u));
+        }
+        v = pack8_u16(e);
+      }
+    }
+    *reinterpret_cast<uint4*>(dst + r * b + c) = v;
+  }
+}
+}  // namespace
+
+void head_weights_bf16(const uint16_t* w, int O, int F, int Op, uint16_t* wp, uint16_t* wpt, hipStream_t stream) {
+  if (O <= 0 || F <= 0) return;
+  hipLaunchKernelGGL(k_head_weights, dim3(F / kHT, Op / kHT), dim3(256), 0, stream, w, O, F, Op, wp, wpt);
+}
+
+void repitch_bf16(const uint16_t* src, int a, uint16_t* dst, int b, int64_t R, const uint16_t* bias,
+                  hipStream_t stream) {
+  const int64_t items = R * (b / 8);
+  if (items <= 0) return;
+  int64_t blocks = (items + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_repitch, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, src, a, dst, b, R, bias);
+}
+
 void linear_f32_fwd(const float* x, const float* w, const float* b, int R, int F, int O, float* y, hipStream_t stream) {
   if (R <= 0) return;
   hipLaunchKernelGGL(k_linear_fwd<float>, dim3((R + 3) / 4), dim3(256), 0, stream, x, w, b, R, F, O, y);

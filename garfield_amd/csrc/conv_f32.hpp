@@ -62,6 +62,11 @@ void linear_bias_grad(const void* dl, bool dl_f32, int groups, int rg, int O, vo
                       int64_t off_b, hipStream_t stream);
 void linear_bf16_wgrad(const uint16_t* x, const uint16_t* dl, int groups, int rg, int F, int O, void* out, int odt,
                        int64_t row_stride, int64_t off_w, int64_t off_b, hipStream_t stream);
+// wide bf16 heads on gemm_nt (output dimension padded to Op, a multiple of 64; F % 64 == 0): wp [Op][F]
+// and wpt [F][Op] from w [O][F], zero-padded; and bf16 rows re-pitched [R][a] -> [R][b] (cropped, or
+// zero-padded; + bias on the copied columns; a, b multiples of 8)
+void head_weights_bf16(const uint16_t* w, int O, int F, int Op, uint16_t* wp, uint16_t* wpt, hipStream_t stream);
+void repitch_bf16(const uint16_t* src, int a, uint16_t* dst, int b, int64_t R, const uint16_t* bias, hipStream_t stream);
 void avgpool_bf16_fwd(const uint16_t* x, int N, int HW, int C, uint16_t* y, hipStream_t stream);
 void avgpool_bf16_bwd(const uint16_t* dy, int N, int HW, int C, uint16_t* dx, hipStream_t stream);
 void avgpool_f32_fwd(const float* x, int N, int HW, int C, float* y, hipStream_t stream);

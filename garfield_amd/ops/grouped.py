@@ -1732,11 +1732,14 @@ class LinearSpec:
         self.lin = lin
         self.sink = sink
         self.groups = groups
+        self.wp = None    # wide bf16 head: the step's zero-padded weight [Op, F] and its transpose [F, Op]
+        self.wpt = None
 
 
 # outputs up to which the bf16 classifier runs on its own streaming kernels (conv_f32.hip: the CIFAR
-# 10-class head is an 8 MB HBM stream, not a GEMM); a 1000-class ImageNet head is a real GEMM
-# (8 GFLOP) and stays on hipBLASLt
+# 10-class head is an 8 MB HBM stream, not a GEMM); a wider head (ImageNet's 1000 classes: 8 GFLOP
+# per pass) is a GEMM and runs on gemm_nt.hip / the 1x1 weight-gradient kernel with its outputs
+# padded to a multiple of 64 (``_wide_head_*``)
 _LINEAR_BF16_MAX_O = 16
 
 
@@ -1748,7 +1751,9 @@ def _native_linear(x: torch.Tensor, w: torch.Tensor) -> str | None:
     if x.dtype == torch.float32 and w.dtype == torch.float32:
         return "f32"
     if x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
-        return "bf16" if w.shape[0] <= _LINEAR_BF16_MAX_O and x.shape[1] % 8 == 0 else None
+        if w.shape[0] <= _LINEAR_BF16_MAX_O:
+            return "bf16" if x.shape[1] % 8 == 0 else None
+        return "wide" if x.shape[1] % 64 == 0 and w.shape[0] % 8 == 0 else None
     raise TypeError(f"grouped linear on the GPU: fp32 or bf16 operands, got {x.dtype} x {w.dtype}")
 
 
@@ -1758,6 +1763,8 @@ class _GroupedLinear(torch.autograd.Function):
         ctx.spec = spec
         ctx.save_for_backward(x, w)
         kind = _native_linear(x, w)
+        if kind == "wide":
+            return _wide_head_forward(x, w, b, spec)
         if kind is not None:   # no library GEMM: the classifier's own kernel
             y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
             bb = b.detach().to(x.dtype).contiguous() if b is not None else None
@@ -1777,6 +1784,8 @@ class _GroupedLinear(torch.autograd.Function):
             return _linear_f32_backward(ctx, x, w, dy, spec, G)
         if kind == "bf16":
             return _linear_bf16_backward(ctx, x, w, dy.to(torch.bfloat16), spec, G)
+        if kind == "wide":
+            return _wide_head_backward(ctx, x, w, dy.to(torch.bfloat16), spec, G)
         dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
         if spec.sink is not None:
             out, fin = dy.shape[1], x.shape[1]
@@ -1801,6 +1810,68 @@ class _GroupedLinear(torch.autograd.Function):
                     else:
                         sink.put_groups(spec.lin.bias, _acc(dy3).sum(1))
         return dx, None, None, None
+
+
+def _wide_head_forward(x: torch.Tensor, w: torch.Tensor, b, spec: LinearSpec) -> torch.Tensor:
+    """y = x·wᵀ + b for a wide bf16 head: the step's padded weights (one launch, refreshed here since the
+    weights change once per step), the GEMM on gemm_nt.hip into [R, Op] rows, then one pass that crops
+    them to [R, O] adding the bias (fp32 add, so the logits are rounded twice: GEMM, bias)."""
+    C_ = _native.native()
+    O, F = w.shape
+    Op = -(-O // 64) * 64
+    if spec.wp is None or spec.wp.shape != (Op, F) or spec.wp.device != w.device:
+        spec.wp = torch.empty((Op, F), dtype=w.dtype, device=w.device)
+        spec.wpt = torch.empty((F, Op), dtype=w.dtype, device=w.device)
+    C_.gpu_head_weights(w.detach().contiguous(), spec.wp, spec.wpt)
+    x = x.contiguous()
+    yp = torch.empty((x.shape[0], Op), dtype=x.dtype, device=x.device)
+    cfg = _gemm_cfg(x, spec.wp, 0, None)
+    if cfg < 0:
+        raise RuntimeError(f"wide head: no gemm_nt configuration for [{x.shape[0]}, {F}] x [{Op}, {F}]")
+    C_.gpu_gemm_nt(x, spec.wp, yp, None, None, 0, cfg)
+    y = torch.empty((x.shape[0], O), dtype=x.dtype, device=x.device)
+    bb = b.detach().to(x.dtype).contiguous() if b is not None else None
+    C_.gpu_repitch(yp, y, bb)
+    return y
+
+
+def _wide_head_backward(ctx, x, w, dy, spec: LinearSpec, G: int):
+    """Wide bf16 head backward without a library GEMM: dy padded to [R, Op] (zero columns), dx = dyp·wpᵀᵀ
+    on gemm_nt.hip with the step's wpt, every worker's dW on the 1x1 weight-gradient kernel as fp32 split
+    slabs of [Op, F] whose first O rows are summed into the exchange rows (deferred, batched with the
+    convolutions' slabs), db from dy straight into the rows."""
+    C_ = _native.native()
+    O, F = w.shape
+    R = x.shape[0]
+    Op = spec.wpt.shape[1]
+    dyp = torch.empty((R, Op), dtype=dy.dtype, device=dy.device)
+    C_.gpu_repitch(dy, dyp, None)
+    dx = None
+    if ctx.needs_input_grad[0]:
+        dx = torch.empty((R, F), dtype=x.dtype, device=x.device)
+        cfg = _gemm_cfg(dyp, spec.wpt, 0, None)
+        if cfg < 0:
+            raise RuntimeError(f"wide head: no gemm_nt configuration for [{R}, {Op}] x [{F}, {Op}]")
+        C_.gpu_gemm_nt(dyp, spec.wpt, dx, None, None, 0, cfg)
+    sink = spec.sink
+    if sink is not None:
+        lin = spec.lin
+        x4 = x.contiguous().view(R, F, 1, 1)     # a 1x1 convolution over R one-pixel images
+        dy4 = dyp.view(R, Op, 1, 1)
+        S = _iwgrad_splits(R // G, (F // 64) * (Op // 64) * G // C_.iwgrad_taps_per_block(1, 1, F, Op))
+        part = torch.empty((S, G, Op, F), dtype=torch.float32, device=x.device)
+        C_.gpu_iwgrad(x4, dy4, 1, 1, 1, 1, 0, 0, 1, 1, G, part, S)
+        rows = sink.rows_view(lin.weight, (O, F), sink.flat.dtype)
+        if rows is not None:
+            sink.queue_split(part[:, :, :O], rows)
+        else:
+            sink.put_groups(lin.weight, part.sum(0)[:, :O])
+        if lin.bias is not None:
+            if sink.flat.is_cuda and sink.flat.dtype in (torch.float32, torch.bfloat16, torch.float16):
+                C_.gpu_linear_bias_grad(dy, G, sink.flat, sink.row_stride, sink.base + sink.offset(lin.bias))
+            else:
+                sink.put_groups(lin.bias, dy.view(G, -1, O).float().sum(1))
+    return dx, None, None, None
 
 
 def _linear_f32_backward(ctx, x, w, dy, spec: LinearSpec, G: int):

@@ -749,13 +749,25 @@ def test_headline_path_trains_like_fp32(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("G,B,F_,O,xdt", [(8, 250, 2048, 10, torch.bfloat16), (3, 7, 512, 16, torch.float32),
-                                          (2, 5, 96, 10, torch.bfloat16), (3, 7, 512, 37, torch.float32)])
-def test_grouped_linear_bf16_matches_fp32_reference(cuda, native, G, B, F_, O, xdt):
-    """The bf16 classifier on its own kernels (no hipBLASLt / ATen): forward, data gradient and every
+                                          (2, 5, 96, 10, torch.bfloat16), (3, 7, 512, 37, torch.float32),
+                                          (8, 250, 2048, 1000, torch.bfloat16), (2, 5, 128, 1000, torch.float32),
+                                          (3, 7, 256, 72, torch.bfloat16)])
+def test_grouped_linear_bf16_matches_fp32_reference(cuda, native, G, B, F_, O, xdt, monkeypatch):
+    """The bf16 classifier on its own kernels (no hipBLASLt / ATen GEMM): forward, data gradient and every
     worker's dW / db written into its exchange row (bf16 or fp32 rows), against an fp32 PyTorch
-    reference of the same op on the same bf16 operands (fp32 accumulation, one rounding)."""
+    reference of the same op on the same bf16 operands (fp32 accumulation). Heads wider than 16
+    outputs (the 1000-class ImageNet head) run on gemm_nt.hip / the 1x1 weight-gradient kernel with the
+    outputs padded to a multiple of 64: nothing past the head's own slots is written."""
+    from garfield_amd.ops import grouped as gmod
     from garfield_amd.ops.grouped import LinearSpec, grouped_linear
 
+    def _no_library_gemm(*a, **k):
+        raise AssertionError("library GEMM called by the grouped classifier")
+
+    if O <= 16 or (O % 8 == 0 and F_ % 64 == 0):   # (else the library GEMM path, e.g. 37 outputs)
+        monkeypatch.setattr(gmod.torch, "mm", _no_library_gemm)
+        monkeypatch.setattr(gmod.torch, "bmm", _no_library_gemm)
+        monkeypatch.setattr(gmod.F, "linear", _no_library_gemm)
     torch.manual_seed(0)
     lin = nn.Linear(F_, O).to(cuda).to(torch.bfloat16)
     R = G * B
@@ -777,6 +789,7 @@ def test_grouped_linear_bf16_matches_fp32_reference(cuda, native, G, B, F_, O, x
         db = dyf[sl].sum(0)
         assert rel(flat[g, :O * F_].float().view(O, F_), dw) < 1e-2
         assert rel(flat[g, O * F_:O * F_ + O].float(), db) < 1e-2
+        assert not flat[g, d:].any()
 
 
 @pytest.mark.gpu
