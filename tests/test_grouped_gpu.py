@@ -33,7 +33,7 @@ def _bn_ref_group(xg, gamma, beta, eps, rg, relu):
                                               (4, 8, 2, 256, True, True), (2, 9, 1, 2048, True, True),
                                               (8, 2, 8, 520, True, False), (1, 64, 8, 128, False, True),
                                               (4, 32, 8, 64, True, True), (2, 20, 10, 192, True, False),
-                                              (3, 17, 9, 520, True, True)])
+                                              (3, 17, 9, 520, True, True), (2, 80, 8, 64, True, True)])
 @pytest.mark.parametrize("defer", [False, True])
 @pytest.mark.parametrize("small_ch", [8, 16, 32])
 def test_bn_kernels_match_fp32_reference(cuda, native, G, B, H, C, relu, res, defer, small_ch):
@@ -529,7 +529,8 @@ def test_lazy_residual_gradient_is_bitwise_the_materialised_one(cuda, monkeypatc
 
 @pytest.mark.parametrize("dual", [True, False])
 @pytest.mark.parametrize("G,B,H,C,dt", [(8, 16, 4, 64, torch.bfloat16), (4, 8, 2, 256, torch.float32),
-                                        (2, 64, 8, 128, torch.bfloat16), (3, 20, 10, 64, torch.float32)])
+                                        (2, 64, 8, 128, torch.bfloat16), (3, 20, 10, 64, torch.float32),
+                                        (2, 80, 8, 64, torch.bfloat16)])
 def test_bn_folded_shortcut_matches_fp32_reference(cuda, G, B, H, C, dt, dual, monkeypatch):
     """A projection block's last BatchNorm with the shortcut BatchNorm folded in (res_st): y =
     relu(BN3(x) + BN_ds(r)) with only BN_ds's statistics pass of its own; forward, both inputs'
