@@ -270,8 +270,11 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
 
 // Weight gradient: workgroup (slice s, worker g) sums over images [i0, i1) of worker g, each in
 // bands of g.band output rows. Pixels are processed 32 at a time (one MFMA reduction step): the
-// dy tile [32][64] is written transposed into LDS ([64][32 + pad]); each of the 4 waves owns 16
-// output channels and all 10 k-blocks of 16 (160 padded taps): acc[10] f32x4.
+// dy tile [32][64] is written transposed into LDS ([64][32 + pad]). The 7x7 stem (10 k-blocks of 16
+// taps): each of the 4 waves owns every output channel (4 dyT fragments) and the k-blocks
+// wave, wave + 4, wave + 8, so each patch column is gathered from LDS once per tile, not once per
+// wave (the gathers were 80 scalar LDS reads per lane per tile, 4x redundant); the 3x3 stem (2
+// k-blocks): each wave owns 16 output channels and both k-blocks.
 constexpr int kDyPitch = 40;   // bf16 per transposed dy row (32 + 8: 16-byte aligned, conflict-spread)
 
 template <class SH, bool SPLIT>
@@ -292,13 +295,22 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
   if (i1 > (grp + 1) * imgs_per_worker) i1 = (grp + 1) * imgs_per_worker;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  // this lane's 10 taps (k = 16 kb + fr), as staged-row offsets
-  int toff[SH::KP / 16];
+  constexpr int NKB = SH::KP / 16;
+  constexpr bool KSPLIT = NKB >= 8;                  // k-blocks dealt to the waves (the 7x7 stem)
+  constexpr int KBW = KSPLIT ? (NKB + 3) / 4 : NKB;  // k-blocks per wave
+  constexpr int CF = KSPLIT ? 4 : 1;                 // 16-channel dyT fragments per wave
+  // this lane's taps (k = 16 kb + fr of its k-blocks), as staged-row offsets
+  int toff[KBW];
 #pragma unroll
-  for (int kb = 0; kb < SH::KP / 16; ++kb) toff[kb] = tap_offset<SH>(kb * 16 + fr, g.pw, zero);
-  f32x4 acc[SH::KP / 16];
+  for (int i = 0; i < KBW; ++i) {
+    const int kb = KSPLIT ? wave + 4 * i : i;
+    toff[i] = kb < NKB ? tap_offset<SH>(kb * 16 + fr, g.pw, zero) : zero;
+  }
+  f32x4 acc[CF][KBW];
 #pragma unroll
-  for (int kb = 0; kb < SH::KP / 16; ++kb) acc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < CF; ++c)
+#pragma unroll
+    for (int i = 0; i < KBW; ++i) acc[c][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int npix = g.Ho * g.Wo;
   const int pq = threadIdx.x >> 3, cv = threadIdx.x & 7;   // this thread's 8 channels of one dy pixel
   for (int n = i0; n < i1; ++n) {
@@ -334,11 +346,14 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
         }
         if (q0 + 32 < q_hi) load_dy(q0 + 32, vnext);
         __syncthreads();
-        // A = dyᵀ: lane holds channel (16 wave + fr), pixels q0 + 8 fq .. +7
-        bf16x8 a[NP];
+        // A = dyᵀ: lane holds channel (16 c + fr; c = wave without KSPLIT), pixels q0 + 8 fq .. +7
+        bf16x8 a[CF][NP];
 #pragma unroll
-        for (int pc = 0; pc < NP; ++pc)
-          a[pc] = *reinterpret_cast<const bf16x8*>(dyt + pc * kCout * kDyPitch + (wave * 16 + fr) * kDyPitch + fq * 8);
+        for (int c = 0; c < CF; ++c)
+#pragma unroll
+          for (int pc = 0; pc < NP; ++pc)
+            a[c][pc] = *reinterpret_cast<const bf16x8*>(dyt + pc * kCout * kDyPitch +
+                                                        ((KSPLIT ? c : wave) * 16 + fr) * kDyPitch + fq * 8);
         // B: pixels q0 + 8 fq + j (rows of the reduction), tap k = 16 kb + fr (column)
         // (the 8 pixels are consecutive: one division, then column steps with a row wrap)
         int pb[8];
@@ -355,30 +370,37 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
           }
         }
 #pragma unroll
-        for (int kb = 0; kb < SH::KP / 16; ++kb) {
+        for (int i = 0; i < KBW; ++i) {
+          if (KSPLIT && wave + 4 * i >= NKB) continue;   // wave-uniform: waves 2, 3 own two k-blocks
           bf16x8 b[NP];
 #pragma unroll
           for (int pc = 0; pc < NP; ++pc) {
             uint16_t vh[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-              vh[j] = patch[pc * pstride + ((pb[j] < 0 || toff[kb] == zero) ? zero : pb[j] + toff[kb])];
+              vh[j] = patch[pc * pstride + ((pb[j] < 0 || toff[i] == zero) ? zero : pb[j] + toff[i])];
             b[pc] = u8_to_bf16x8(vh);
           }
-          if constexpr (SPLIT) acc[kb] = mma6(a, b, acc[kb]);
-          else acc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc[kb], 0, 0, 0);
+#pragma unroll
+          for (int c = 0; c < CF; ++c) {
+            if constexpr (SPLIT) acc[c][i] = mma6(a[c], b, acc[c][i]);
+            else acc[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c][0], b[0], acc[c][i], 0, 0, 0);
+          }
         }
       }
     }
   }
-  // D[co][k]: col = k = 16 kb + fr, rows co = 16 wave + 4 fq + r; slab [slices][G][64][K]
+  // D[co][k]: col = k = 16 kb + fr, rows co = 16 c + 4 fq + r (c = wave without KSPLIT); slab [slices][G][64][K]
   float* o = part + (static_cast<int64_t>(s) * gridDim.y + grp) * kCout * SH::K;
 #pragma unroll
-  for (int kb = 0; kb < SH::KP / 16; ++kb) {
+  for (int i = 0; i < KBW; ++i) {
+    const int kb = KSPLIT ? wave + 4 * i : i;
     const int k = kb * 16 + fr;
-    if (k >= SH::K) continue;
+    if (kb >= NKB || k >= SH::K) continue;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) o[(wave * 16 + fq * 4 + r) * SH::K + k] = acc[kb][r];
+    for (int c = 0; c < CF; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[(((KSPLIT ? c : wave) * 16) + fq * 4 + r) * SH::K + k] = acc[c][i][r];
   }
 }
 

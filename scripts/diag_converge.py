@@ -30,9 +30,11 @@ def run(grouped, lr, steps, model="resnet18", batch=32, wd=5e-4, momentum=0.9):
 
 if __name__ == "__main__":
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 150
-    for lr in (0.002, 0.005, 0.01, 0.02):
+    model = sys.argv[2] if len(sys.argv) > 2 else "resnet18"
+    lrs = [float(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else (0.002, 0.005, 0.01, 0.02)
+    for lr in lrs:
         for grouped in (True, False):
-            ls = run(grouped, lr, steps)
-            print(json.dumps({"lr": lr, "grouped_bf16": grouped, "first": round(ls[0], 4),
+            ls = run(grouped, lr, steps, model=model)
+            print(json.dumps({"model": model, "lr": lr, "grouped_bf16": grouped, "first": round(ls[0], 4),
                               "curve": [round(sum(ls[i:i + 10]) / 10, 3) for i in range(0, steps, 10)],
                               "last10": round(sum(ls[-10:]) / 10, 4)}), flush=True)
