@@ -2436,9 +2436,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                 "gpu_stem_fwd: y must be a channels_last [N, 64, Ho, Wo] tensor of x's dtype");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(wm.data_ptr()) % 16 == 0, "gpu_stem_fwd: w must be 16-byte aligned");
     c10::hip::HIPGuard guard(x.device().index());
+    // the channel-padded weight of the bf16 7x7 form: scratch from the caching allocator (graph-pool safe)
+    const int sc = split ? 0 : garfield::gpu::stem_fwd_scratch(kd);
+    at::Tensor scratch = sc > 0 ? at::empty({sc}, wm.options()) : at::Tensor();
     garfield::gpu::stem_fwd(x.data_ptr(), reinterpret_cast<const uint16_t*>(wm.data_ptr()), split,
                             static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), y.data_ptr(),
-                            stream_of(x.device()), raw ? K : KP, kd);
+                            stream_of(x.device()), raw ? K : KP, kd,
+                            sc > 0 ? reinterpret_cast<uint16_t*>(scratch.data_ptr()) : nullptr);
   }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("kind") = 0,
      "Implicit-GEMM ResNet stem forward (3 -> 64; kind 0: 7x7/2 pad 3, 1: 3x3/1 pad 1); fp32 x: split-bf16 MFMA on "
      "the weight's pieces");

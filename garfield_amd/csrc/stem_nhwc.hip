@@ -26,6 +26,8 @@
 // is split into three bf16 pieces (LDS holds all three), the weight comes as its three pieces, and
 // each product is the six piece products of order <= 2 on the bf16 MFMA with fp32 accumulation
 // (see conv_f32.hip).
+#include <type_traits>
+
 #include "bn_gpu.hpp"
 #include "gar_device.hpp"
 
@@ -268,6 +270,116 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd(const void* __restrict__ 
   }
 }
 
+// bf16 7x7 stem forward on a channel-padded staging: input rows as [rows][pw][4] (channel 3 = 0) and the
+// weight as [64][7 ky][8 kx][4 ci] (kx 7 and ci 3 zero; written once per call by k_stem_wprep), so k-step
+// s is kernel row ky and a lane's 8 consecutive reduction elements (taps kx = 2 fq, 2 fq + 1, 4 channels
+// each) of one pixel are ONE aligned ds_read_b128 (even staged row width) instead of k_stem_fwd's 8
+// scalar LDS gathers: 7 k-steps of 32 instead of 5 (40% more MFMA work on zeros). The output tile leaves
+// through LDS rows of 72 elements (a 64-element pitch put the 16 pixels of a fragment in one bank).
+constexpr int kKP4 = 7 * 32;
+constexpr int kTileP = kCout + 8;
+
+__global__ __launch_bounds__(kThreads) void k_stem_wprep(const uint16_t* __restrict__ w, int wpitch,
+                                                         uint16_t* __restrict__ wp4) {
+  const int e = blockIdx.x * kThreads + threadIdx.x;
+  if (e >= kCout * kKP4) return;
+  const int co = e / kKP4, k4 = e - co * kKP4;
+  const int ky = k4 >> 5, kx = (k4 >> 2) & 7, ci = k4 & 3;
+  wp4[e] = (kx < 7 && ci < 3) ? w[co * wpitch + (ky * 7 + kx) * 3 + ci] : static_cast<uint16_t>(0);
+}
+
+__device__ __forceinline__ void stage_rows4(const uint16_t* __restrict__ x, const StemGeo& g, int n, int iy0, int rows,
+                                            uint16_t* patch) {
+  const int total = rows * g.pw;   // staged pixels
+  const int64_t img = static_cast<int64_t>(n) * g.H * g.W;
+  for (int e0 = threadIdx.x; e0 < total; e0 += kThreads * kStageBatch) {
+    uint32_t lo[kStageBatch], hi[kStageBatch];
+#pragma unroll
+    for (int b = 0; b < kStageBatch; ++b) {
+      const int e = e0 + b * kThreads;
+      const int r = e / g.pw, c = e - r * g.pw - Stem7::P;   // staged pixel -> image column
+      const int iy = iy0 + r;
+      lo[b] = 0u;
+      hi[b] = 0u;
+      if (e < total && iy >= 0 && iy < g.H && c >= 0 && c < g.W) {
+        const uint16_t* px = x + (img + static_cast<int64_t>(iy) * g.W + c) * kC;
+        lo[b] = static_cast<uint32_t>(px[0]) | (static_cast<uint32_t>(px[1]) << 16);
+        hi[b] = px[2];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < kStageBatch; ++b) {
+      const int e = e0 + b * kThreads;
+      if (e < total) *reinterpret_cast<uint2*>(patch + static_cast<int64_t>(e) * 4) = make_uint2(lo[b], hi[b]);
+    }
+  }
+}
+
+template <int F>
+__global__ __launch_bounds__(kThreads) void k_stem_fwd4(const uint16_t* __restrict__ x, const uint16_t* __restrict__ wp4,
+                                                        StemGeo g, uint16_t* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* wl = lds;                         // [64][224]
+  uint16_t* patch = lds + kCout * kKP4;       // [rows][pw][4]
+  constexpr int kTile = 64 * F;
+  const int tiles = (g.Ho * g.Wo + kTile - 1) / kTile;
+  const int n = blockIdx.x / tiles;
+  const int p0 = (blockIdx.x - n * tiles) * kTile;
+  const int npix = g.Ho * g.Wo - p0 < kTile ? g.Ho * g.Wo - p0 : kTile;
+  const int oy0 = p0 / g.Wo, oy1 = (p0 + npix - 1) / g.Wo;
+  const int iy0 = oy0 * Stem7::S - Stem7::P;
+  const int rows = (oy1 - oy0) * Stem7::S + Stem7::KH;
+  for (int e = threadIdx.x; e < kCout * kKP4 / 8; e += kThreads)
+    reinterpret_cast<uint4*>(wl)[e] = reinterpret_cast<const uint4*>(wp4)[e];
+  stage_rows4(x, g, n, iy0, rows, patch);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  int pbase[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    int p = p0 + wave * 16 * F + f * 16 + fr;
+    if (p > p0 + npix - 1) p = p0 + npix - 1;   // clamp: computed, never stored
+    const int oy = p / g.Wo, ox = p - oy * g.Wo;
+    pbase[f] = ((oy * Stem7::S - Stem7::P - iy0) * g.pw + ox * Stem7::S + 2 * fq) * 4;
+  }
+  f32x4 acc[F][4];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[f][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    bf16x8 bx[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) bx[f] = *reinterpret_cast<const bf16x8*>(patch + pbase[f] + s * g.pw * 4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8 aw = *reinterpret_cast<const bf16x8*>(wl + (c * 16 + fr) * kKP4 + s * 32 + fq * 8);
+#pragma unroll
+      for (int f = 0; f < F; ++f) acc[f][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx[f], acc[f][c], 0, 0, 0);
+    }
+  }
+  __syncthreads();   // every wave's weight and patch reads are done: reuse the area
+  uint16_t* tile = lds;
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    const int pl = wave * 16 * F + f * 16 + fr;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint2 o;
+      o.x = pack_bf16x2(acc[f][c][0], acc[f][c][1]);
+      o.y = pack_bf16x2(acc[f][c][2], acc[f][c][3]);
+      *reinterpret_cast<uint2*>(tile + pl * kTileP + c * 16 + fq * 4) = o;
+    }
+  }
+  __syncthreads();
+  uint16_t* out = y + (static_cast<int64_t>(n) * g.Ho * g.Wo + p0) * kCout;
+  for (int e = threadIdx.x; e < npix * (kCout / 8); e += kThreads)
+    *reinterpret_cast<uint4*>(out + e * 8) = *reinterpret_cast<const uint4*>(tile + (e >> 3) * kTileP + (e & 7) * 8);
+}
+
 // Weight gradient: workgroup (slice s, worker g) sums over images [i0, i1) of worker g, each in
 // bands of g.band output rows. Pixels are processed 32 at a time (one MFMA reduction step): the
 // dy tile [32][64] is written transposed into LDS ([64][32 + pad]). The 7x7 stem (10 k-blocks of 16
@@ -304,7 +416,8 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
 #pragma unroll
   for (int i = 0; i < KBW; ++i) {
     const int kb = KSPLIT ? wave + 4 * i : i;
-    toff[i] = kb < NKB ? tap_offset<SH>(kb * 16 + fr, g.pw, zero) : zero;
+    // padded taps (k >= K) read any staged value: their D columns are never stored
+    toff[i] = kb < NKB && kb * 16 + fr < SH::K ? tap_offset<SH>(kb * 16 + fr, g.pw, zero) : 0;
   }
   f32x4 acc[CF][KBW];
 #pragma unroll
@@ -322,29 +435,38 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
       if (threadIdx.x < NP) patch[threadIdx.x * pstride + zero] = 0;
       const int64_t dyi = static_cast<int64_t>(n) * npix * kCout;
       // the next tile's load is issued before the current tile's MFMAs (one latency per band, not per tile)
-      auto load_dy = [&](int q0, float (&v)[8]) {
+      // (bf16: the raw 16-byte vector, written to LDS as loaded)
+      auto load_dy = [&](int q0, float (&v)[8], uint4& raw) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = 0.f;
+        raw = make_uint4(0u, 0u, 0u, 0u);
         if (q0 + pq < q_hi) {
           if constexpr (SPLIT) load_vec<kF32, 8>(dy, dyi + static_cast<int64_t>(q0 + pq) * kCout + cv * 8, v);
-          else load_vec<kBF16, 8>(dy, dyi + static_cast<int64_t>(q0 + pq) * kCout + cv * 8, v);
+          else raw = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(dy) + dyi +
+                                                    static_cast<int64_t>(q0 + pq) * kCout + cv * 8);
         }
       };
       float vnext[8];
-      load_dy(q_lo, vnext);
+      uint4 rnext;
+      load_dy(q_lo, vnext, rnext);
       for (int q0 = q_lo; q0 < q_hi; q0 += 32) {
         __syncthreads();   // previous dy tile consumed (and, first time, the band staged)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          float r = vnext[i];
+          if constexpr (SPLIT) {
+            float r = vnext[i];
 #pragma unroll
-          for (int pc = 0; pc < NP; ++pc) {
-            const uint16_t h = f_to_bf16(r);
-            dyt[pc * kCout * kDyPitch + (cv * 8 + i) * kDyPitch + pq] = h;
-            r -= bf16_to_f(h);
+            for (int pc = 0; pc < NP; ++pc) {
+              const uint16_t h = f_to_bf16(r);
+              dyt[pc * kCout * kDyPitch + (cv * 8 + i) * kDyPitch + pq] = h;
+              r -= bf16_to_f(h);
+            }
+          } else {
+            const uint32_t wd = i < 2 ? rnext.x : (i < 4 ? rnext.y : (i < 6 ? rnext.z : rnext.w));
+            dyt[(cv * 8 + i) * kDyPitch + pq] = static_cast<uint16_t>((i & 1) ? (wd >> 16) : (wd & 0xffffu));
           }
         }
-        if (q0 + 32 < q_hi) load_dy(q0 + 32, vnext);
+        if (q0 + 32 < q_hi) load_dy(q0 + 32, vnext, rnext);
         __syncthreads();
         // A = dyᵀ: lane holds channel (16 c + fr; c = wave without KSPLIT), pixels q0 + 8 fq .. +7
         bf16x8 a[CF][NP];
@@ -362,7 +484,8 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
           int oy = p / g.Wo, ox = p - oy * g.Wo;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            pb[j] = p + j < q_hi ? ((oy - ob0) * SH::S * g.pw + ox * SH::S) * kC : -1;   // band staged from row ob0*S - P
+            // band staged from row ob0*S - P; pixels past the band (dy zero-filled) read the first staged value
+            pb[j] = p + j < q_hi ? ((oy - ob0) * SH::S * g.pw + ox * SH::S) * kC : 0;
             if (++ox == g.Wo) {
               ox = 0;
               ++oy;
@@ -378,7 +501,7 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
             uint16_t vh[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-              vh[j] = patch[pc * pstride + ((pb[j] < 0 || toff[i] == zero) ? zero : pb[j] + toff[i])];
+              vh[j] = patch[pc * pstride + pb[j] + toff[i]];
             b[pc] = u8_to_bf16x8(vh);
           }
 #pragma unroll
@@ -439,7 +562,8 @@ bool supported_t(int H, int W) {
 }
 
 template <class SH>
-void fwd_t(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream, int wpitch) {
+void fwd_t(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream, int wpitch,
+           uint16_t* scratch) {
   const StemGeo g = geo<SH>(N, H, W, split);
   const int T = 64 * (split ? kFwdFragSplit : kFwdFragBf16);
   const int tiles = (g.Ho * g.Wo + T - 1) / T;
@@ -452,6 +576,16 @@ void fwd_t(const void* x, const uint16_t* w, bool split, int N, int H, int W, vo
     allow_lds(k_stem_fwd<SH, true, kFwdFragSplit>, lds);
     hipLaunchKernelGGL((k_stem_fwd<SH, true, kFwdFragSplit>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y,
                        SH::KP);
+  } else if (std::is_same<SH, Stem7>::value && g.pw % 2 == 0 && scratch != nullptr) {   // channel-padded form
+    const int wp = wpitch == SH::K ? SH::K : SH::KP;
+    hipLaunchKernelGGL(k_stem_wprep, dim3((kCout * kKP4 + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, w, wp,
+                       scratch);
+    size_t lds4 = (static_cast<size_t>(kCout) * kKP4 + static_cast<size_t>(fwd_rows<SH>(g, T)) * g.pw * 4) * 2;
+    const size_t tile4 = static_cast<size_t>(T) * kTileP * 2;
+    if (lds4 < tile4) lds4 = tile4;
+    allow_lds(k_stem_fwd4<kFwdFragBf16>, lds4);
+    hipLaunchKernelGGL((k_stem_fwd4<kFwdFragBf16>), dim3(N * tiles), dim3(kThreads), lds4, stream,
+                       static_cast<const uint16_t*>(x), scratch, g, static_cast<uint16_t*>(y));
   } else {
     allow_lds(k_stem_fwd<SH, false, kFwdFragBf16>, lds);
     hipLaunchKernelGGL((k_stem_fwd<SH, false, kFwdFragBf16>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y,
@@ -486,10 +620,12 @@ bool stem_supported(int H, int W, int kind) {
   return kind == kStem3x3 ? supported_t<Stem3>(H, W) : supported_t<Stem7>(H, W);
 }
 
+int stem_fwd_scratch(int kind) { return kind == kStem3x3 ? 0 : kCout * kKP4; }
+
 void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream,
-              int wpitch, int kind) {
-  if (kind == kStem3x3) fwd_t<Stem3>(x, w, split, N, H, W, y, stream, wpitch);
-  else fwd_t<Stem7>(x, w, split, N, H, W, y, stream, wpitch);
+              int wpitch, int kind, uint16_t* scratch) {
+  if (kind == kStem3x3) fwd_t<Stem3>(x, w, split, N, H, W, y, stream, wpitch, nullptr);
+  else fwd_t<Stem7>(x, w, split, N, H, W, y, stream, wpitch, scratch);
 }
 
 void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,

@@ -197,19 +197,22 @@ def test_iwgrad_matches_per_worker_conv_weight_grad(cuda, native, G, B, C, Co, H
         assert torch.count_nonzero(flat[:40]) == 0
 
 
-@pytest.mark.parametrize("G,B,H,W,splits", [(2, 3, 32, 32, 1), (3, 2, 32, 32, 4), (2, 2, 33, 20, 2),
-                                            (1, 2, 64, 64, 3), (4, 1, 17, 9, 1)])
-def test_stem_kernels_match_fp32_conv(cuda, native, G, B, H, W, splits):
+@pytest.mark.parametrize("G,B,H,W,splits,raw", [(2, 3, 32, 32, 1, False), (3, 2, 32, 32, 4, True),
+                                                (2, 2, 33, 20, 2, False), (1, 2, 64, 64, 3, True),
+                                                (4, 1, 17, 9, 1, False), (2, 1, 224, 224, 1, True)])
+def test_stem_kernels_match_fp32_conv(cuda, native, G, B, H, W, splits, raw):
     """stem_nhwc.hip (7x7/2/pad 3, 3 -> 64, no patch matrix): forward vs fp32 conv2d of the same
-    bf16 operands (ragged last pixel tile, odd/non-square sizes), and the per-worker weight
-    gradient vs fp32 conv2d_weight of each worker's images (image slices, empty slices)."""
+    bf16 operands (ragged last pixel tile, odd/non-square sizes; even widths take the channel-padded
+    staging, odd ones the gathering kernel; the padded [64, 160] or the raw channels_last weight), and
+    the per-worker weight gradient vs fp32 conv2d_weight of each worker's images (image slices, empty
+    slices)."""
     from garfield_amd.ops.grouped import _wmat
     assert native.stem_supported(H, W)
     x = torch.randn(G * B, 3, H, W, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(64, 3, 7, 7, device=cuda) / 12).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     ref = F.conv2d(x.float(), w.float(), None, 2, 3)
     y = torch.empty(ref.shape, dtype=torch.bfloat16, device=cuda, memory_format=torch.channels_last)
-    native.gpu_stem_fwd(x, _wmat(w, 160).contiguous(), y)
+    native.gpu_stem_fwd(x, w if raw else _wmat(w, 160).contiguous(), y)
     assert rel(y.float(), ref) < 1e-2
     dy = torch.randn(ref.shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     part = torch.full((splits, G, 64, 147), float("nan"), device=cuda)
