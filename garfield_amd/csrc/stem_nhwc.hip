@@ -387,7 +387,10 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd4(const uint16_t* __restri
 // wave, wave + 4, wave + 8, so each patch column is gathered from LDS once per tile, not once per
 // wave (the gathers were 80 scalar LDS reads per lane per tile, 4x redundant); the 3x3 stem (2
 // k-blocks): each wave owns 16 output channels and both k-blocks.
-constexpr int kDyPitch = 40;   // bf16 per transposed dy row (32 + 8: 16-byte aligned, conflict-spread)
+// bf16 per transposed dy row: 34 (17 dwords), so the 8 rows a wave's transposing 2-byte stores hit at once
+// (channels 8 cv + i, cv = 0..7) fall in 8 different bank groups; the A fragments are then read as four
+// dwords (rows are 4-byte, not 16-byte, aligned). A 40-element pitch put them 4 / 8 to a bank.
+constexpr int kDyPitch = 34;
 
 template <class SH, bool SPLIT>
 __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict__ x, const void* __restrict__ dy,
@@ -474,8 +477,11 @@ __global__ __launch_bounds__(kThreads) void k_stem_wgrad(const void* __restrict_
         for (int c = 0; c < CF; ++c)
 #pragma unroll
           for (int pc = 0; pc < NP; ++pc)
-            a[c][pc] = *reinterpret_cast<const bf16x8*>(dyt + pc * kCout * kDyPitch +
-                                                        ((KSPLIT ? c : wave) * 16 + fr) * kDyPitch + fq * 8);
+          {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(dyt + pc * kCout * kDyPitch +
+                                                                    ((KSPLIT ? c : wave) * 16 + fr) * kDyPitch + fq * 8);
+            a[c][pc] = __builtin_bit_cast(bf16x8, make_uint4(src[0], src[1], src[2], src[3]));
+          }
         // B: pixels q0 + 8 fq + j (rows of the reduction), tap k = 16 kb + fr (column)
         // (the 8 pixels are consecutive: one division, then column steps with a row wrap)
         int pb[8];
