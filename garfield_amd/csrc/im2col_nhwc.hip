@@ -190,6 +190,8 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_fwd(const void* __restrict
   const int cv = g.C / 8;
   const int64_t total = static_cast<int64_t>(g.N) * g.Ho * g.Wo * cv;
   const bool narrow = total <= 0x7fffffff;   // 32-bit index math (the 64-bit divisions dominated)
+  const bool pool3s2 = g.KH == 3 && g.KW == 3 && g.sh == 2 && g.sw == 2 && g.ph == 1 && g.pw == 1 && g.dh == 1 &&
+                       g.dw == 1;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
        t += static_cast<int64_t>(gridDim.x) * kThreads) {
     const int v = narrow ? static_cast<int>(t) % cv : static_cast<int>(t % cv);
@@ -201,6 +203,28 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_fwd(const void* __restrict
     int arg[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { best[e] = -__builtin_inff(); arg[e] = 0; }
+    if (pool3s2) {
+      // the ResNet stem pool (3x3, stride 2, pad 1): all nine window loads issued before the first
+      // comparison (rows / columns outside the image read a clamped neighbour and are skipped)
+      float a[9][8];
+      bool ok[9];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int hi = 2 * ho - 1 + i, wi = 2 * wo - 1 + j;
+          ok[i * 3 + j] = hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+          const int hc = hi < 0 ? 0 : (hi >= g.H ? g.H - 1 : hi), wc = wi < 0 ? 0 : (wi >= g.W ? g.W - 1 : wi);
+          load_vec<DT, 8>(x, ((static_cast<int64_t>(n) * g.H + hc) * g.W + wc) * g.C + v * 8, a[i * 3 + j]);
+        }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        if (!ok[tap]) continue;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (a[tap][e] > best[e] || (a[tap][e] != a[tap][e] && best[e] == best[e])) { best[e] = a[tap][e]; arg[e] = tap; }
+      }
+    } else
     for (int i = 0; i < g.KH; ++i) {
       const int hi = ho * g.sh - g.ph + i * g.dh;
       if (hi < 0 || hi >= g.H) continue;
@@ -234,6 +258,7 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_bwd(const void* __restrict
   // undilated windows: only the output rows / columns whose window covers (hi, wi) are visited
   // (1-4 of the 9 taps of a 3x3 / 2 pool), in the generic loop's (i, j) order
   const bool unit = g.dh == 1 && g.dw == 1;
+  const bool pool3s2 = unit && g.KH == 3 && g.KW == 3 && g.sh == 2 && g.sw == 2 && g.ph == 1 && g.pw == 1;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
        t += static_cast<int64_t>(gridDim.x) * kThreads) {
     const int v = narrow ? static_cast<int>(t) % cv : static_cast<int>(t % cv);
@@ -253,7 +278,39 @@ __global__ __launch_bounds__(kThreads) void k_maxpool_bwd(const void* __restrict
         if (static_cast<int>((word >> (8 * (e & 3))) & 0xffu) == tap) acc[e] += d[e];
       }
     };
-    if (unit) {
+    if (pool3s2) {
+      // 3x3 / 2 / pad 1: at most two covering rows and columns; their four (idx, dy) loads issued before
+      // the sums, which run in the general loop's order (ho, then wo, descending)
+      const int ah = hi + 1, aw = wi + 1;
+      const int ho1 = ah / 2 < g.Ho - 1 ? ah / 2 : g.Ho - 1, wo1 = aw / 2 < g.Wo - 1 ? aw / 2 : g.Wo - 1;
+      const int ho0 = ah - 2 <= 0 ? 0 : (ah - 1) / 2, wo0 = aw - 2 <= 0 ? 0 : (aw - 1) / 2;
+      uint2 pk[4];
+      float d[4][8];
+      int tp[4];
+      bool ok[4];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int ho = ho1 - a, wo = wo1 - b;
+          const int q = a * 2 + b;
+          ok[q] = ho >= ho0 && wo >= wo0;
+          const int hc = ok[q] ? ho : ho1, wcl = ok[q] ? wo : wo1;
+          const int64_t o = (static_cast<int64_t>((n * g.Ho + hc) * g.Wo + wcl)) * g.C + v * 8;
+          pk[q] = *reinterpret_cast<const uint2*>(idx + o);
+          load_vec<DT, 8>(dy, o, d[q]);
+          tp[q] = (ah - ho * 2) * 3 + (aw - wo * 2);
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!ok[q]) continue;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t word = e < 4 ? pk[q].x : pk[q].y;
+          if (static_cast<int>((word >> (8 * (e & 3))) & 0xffu) == tp[q]) acc[e] += d[q][e];
+        }
+      }
+    } else if (unit) {
       // window (ho, wo) covers hi iff i = hi + ph - ho*sh lies in [0, KH)
       const int ah = hi + g.ph, aw = wi + g.pw;
       int ho1 = ah / g.sh, wo1 = aw / g.sw;
