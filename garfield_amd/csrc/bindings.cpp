@@ -2405,13 +2405,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       garfield::gpu::avgpool_f32_fwd(x.data_ptr<float>(), static_cast<int>(N), static_cast<int>(HW),
                                      static_cast<int>(C), y.data_ptr<float>(), stream_of(dev));
   }, py::arg("x"), py::arg("y"), py::arg("backward"), "fp32 / bf16 NHWC global average pool (forward / backward)");
+  m.def("stem_fwd_stat_tiles", [](int64_t n, int64_t h, int64_t w, int64_t kind) {
+    return garfield::gpu::stem_fwd_stat_tiles(static_cast<int>(n), static_cast<int>(h), static_cast<int>(w),
+                                              static_cast<int>(kind));
+  }, py::arg("n"), py::arg("h"), py::arg("w"), py::arg("kind") = 0,
+        "Statistics tiles (256 output pixels each) the bf16 stem forward writes for its BatchNorm (0: none)");
   m.def("stem_supported", [](int64_t h, int64_t w, int64_t kind) {
           return garfield::gpu::stem_supported(static_cast<int>(h), static_cast<int>(w), static_cast<int>(kind));
         }, py::arg("h"), py::arg("w"), py::arg("kind") = 0,
         "True when the implicit stem kernels (3 -> 64 channels; kind 0: 7x7/2 pad 3, 1: 3x3/1 pad 1) handle H x W images");
   m.def("stem_k", &garfield::gpu::stem_k, py::arg("kind") = 0, "taps x channels of the stem kind (147 / 27)");
   m.def("stem_kp", &garfield::gpu::stem_kp, py::arg("kind") = 0, "K padded to whole 32-wide k-steps (160 / 32)");
-  m.def("gpu_stem_fwd", [](const at::Tensor& x, const at::Tensor& wm, const at::Tensor& y, int64_t kind) {
+  m.def("gpu_stem_fwd", [](const at::Tensor& x, const at::Tensor& wm, const at::Tensor& y, int64_t kind,
+                            const c10::optional<at::Tensor>& stats) {
     const bool split = x.scalar_type() == at::kFloat;
     const int kd = static_cast<int>(kind);
     const int K = garfield::gpu::stem_k(kd), KP = garfield::gpu::stem_kp(kd);
@@ -2439,11 +2445,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     // the channel-padded weight of the bf16 7x7 form: scratch from the caching allocator (graph-pool safe)
     const int sc = split ? 0 : garfield::gpu::stem_fwd_scratch(kd);
     at::Tensor scratch = sc > 0 ? at::empty({sc}, wm.options()) : at::Tensor();
+    float* sp = nullptr;
+    if (stats.has_value() && stats->defined()) {
+      const int64_t tiles = garfield::gpu::stem_fwd_stat_tiles(static_cast<int>(N), static_cast<int>(H),
+                                                               static_cast<int>(W), kd);
+      TORCH_CHECK(!split && tiles > 0, "gpu_stem_fwd: no statistics tiles for this geometry / dtype");
+      TORCH_CHECK(stats->is_cuda() && stats->device() == x.device() && stats->scalar_type() == at::kFloat &&
+                      stats->is_contiguous() && stats->numel() >= tiles * 2 * 3 * 64,
+                  "gpu_stem_fwd: stats must be a contiguous fp32 tensor of >= ", tiles * 2 * 3 * 64, " elements");
+      sp = stats->data_ptr<float>();
+    }
     garfield::gpu::stem_fwd(x.data_ptr(), reinterpret_cast<const uint16_t*>(wm.data_ptr()), split,
                             static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), y.data_ptr(),
                             stream_of(x.device()), raw ? K : KP, kd,
-                            sc > 0 ? reinterpret_cast<uint16_t*>(scratch.data_ptr()) : nullptr);
-  }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("kind") = 0,
+                            sc > 0 ? reinterpret_cast<uint16_t*>(scratch.data_ptr()) : nullptr, sp);
+  }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("kind") = 0, py::arg("stats") = py::none(),
      "Implicit-GEMM ResNet stem forward (3 -> 64; kind 0: 7x7/2 pad 3, 1: 3x3/1 pad 1); fp32 x: split-bf16 MFMA on "
      "the weight's pieces");
   m.def("gpu_stem_wgrad", [](const at::Tensor& x, const at::Tensor& dy, int64_t groups, const at::Tensor& part,

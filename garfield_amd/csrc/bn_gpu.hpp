@@ -85,9 +85,12 @@ bool stem_supported(int H, int W, int kind = kStem7x7);
 // w: the zero-padded [64][KP] matrix (split: its three pieces), or (wpitch = K, bf16 only) the
 // channels_last [64][KH][KW][3] weight itself
 void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream,
-              int wpitch = 160, int kind = kStem7x7, uint16_t* scratch = nullptr);
+              int wpitch = 160, int kind = kStem7x7, uint16_t* scratch = nullptr, float* stats = nullptr);
 // bf16 elements of the scratch stem_fwd takes for its channel-padded weight (0: none used)
 int stem_fwd_scratch(int kind);
+// statistics tiles (of 256 output pixels, gemm_nt.hip's layout, E = 1) the bf16 stem forward writes for
+// the consuming BatchNorm, 0 when the geometry has none (tiles must hold whole images' pixels)
+int64_t stem_fwd_stat_tiles(int N, int H, int W, int kind);
 // per-worker weight gradients: part fp32 [slices][groups][64][K] (sum over slices = dW of the worker);
 // split: x / dy fp32
 void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,

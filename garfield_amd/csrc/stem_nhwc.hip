@@ -315,9 +315,12 @@ __device__ __forceinline__ void stage_rows4(const uint16_t* __restrict__ x, cons
   }
 }
 
+// stats (optional): the consuming BatchNorm's statistics of this tile's stored bf16 values, in
+// gemm_nt.hip's tile layout ([tile][entry 1][slot 2][n, Σy, Σ(y - ȳ)²][64], slot 0 only: a tile lies in
+// one image, so in one worker), merged by bn_finalize_tiles: the BatchNorm forward then has no partial pass
 template <int F>
 __global__ __launch_bounds__(kThreads) void k_stem_fwd4(const uint16_t* __restrict__ x, const uint16_t* __restrict__ wp4,
-                                                        StemGeo g, uint16_t* __restrict__ y) {
+                                                        StemGeo g, uint16_t* __restrict__ y, float* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* wl = lds;                         // [64][224]
   uint16_t* patch = lds + kCout * kKP4;       // [rows][pw][4]
@@ -378,6 +381,31 @@ __global__ __launch_bounds__(kThreads) void k_stem_fwd4(const uint16_t* __restri
   uint16_t* out = y + (static_cast<int64_t>(n) * g.Ho * g.Wo + p0) * kCout;
   for (int e = threadIdx.x; e < npix * (kCout / 8); e += kThreads)
     *reinterpret_cast<uint4*>(out + e * 8) = *reinterpret_cast<const uint4*>(tile + (e >> 3) * kTileP + (e & 7) * 8);
+  if (stats == nullptr) return;
+  // channel c = thread % 64 over every 4th pixel from part = thread / 64, shifted by the tile's first
+  // stored value (no cancellation whatever |mean| / std), the 4 parts summed in order through LDS
+  const int c = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const float sh = bf16_to_f(tile[c]);
+  float sd = 0.f, sq = 0.f;
+  for (int p = part; p < npix; p += 4) {
+    const float d = bf16_to_f(tile[p * kTileP + c]) - sh;
+    sd += d;
+    sq = fmaf(d, d, sq);
+  }
+  __syncthreads();   // the tile reads are done: reuse its first bytes for the parts
+  float* red = reinterpret_cast<float*>(lds);
+  red[part * 64 + c] = sd;
+  red[256 + part * 64 + c] = sq;
+  __syncthreads();
+  if (part == 0) {
+    const float D = red[c] + red[64 + c] + red[128 + c] + red[192 + c];
+    const float Q = red[256 + c] + red[320 + c] + red[384 + c] + red[448 + c];
+    const float nn = static_cast<float>(npix);
+    float* ps = stats + static_cast<int64_t>(blockIdx.x) * 2 * 3 * kCout;   // tile = blockIdx.x, slot 0
+    ps[c] = nn;
+    ps[kCout + c] = D + nn * sh;
+    ps[2 * kCout + c] = fmaxf(Q - D * D / nn, 0.f);
+  }
 }
 
 // Weight gradient: workgroup (slice s, worker g) sums over images [i0, i1) of worker g, each in
@@ -569,7 +597,7 @@ bool supported_t(int H, int W) {
 
 template <class SH>
 void fwd_t(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream, int wpitch,
-           uint16_t* scratch) {
+           uint16_t* scratch, float* stats) {
   const StemGeo g = geo<SH>(N, H, W, split);
   const int T = 64 * (split ? kFwdFragSplit : kFwdFragBf16);
   const int tiles = (g.Ho * g.Wo + T - 1) / T;
@@ -591,7 +619,7 @@ void fwd_t(const void* x, const uint16_t* w, bool split, int N, int H, int W, vo
     if (lds4 < tile4) lds4 = tile4;
     allow_lds(k_stem_fwd4<kFwdFragBf16>, lds4);
     hipLaunchKernelGGL((k_stem_fwd4<kFwdFragBf16>), dim3(N * tiles), dim3(kThreads), lds4, stream,
-                       static_cast<const uint16_t*>(x), scratch, g, static_cast<uint16_t*>(y));
+                       static_cast<const uint16_t*>(x), scratch, g, static_cast<uint16_t*>(y), stats);
   } else {
     allow_lds(k_stem_fwd<SH, false, kFwdFragBf16>, lds);
     hipLaunchKernelGGL((k_stem_fwd<SH, false, kFwdFragBf16>), dim3(N * tiles), dim3(kThreads), lds, stream, x, w, g, y,
@@ -628,10 +656,18 @@ bool stem_supported(int H, int W, int kind) {
 
 int stem_fwd_scratch(int kind) { return kind == kStem3x3 ? 0 : kCout * kKP4; }
 
+int64_t stem_fwd_stat_tiles(int N, int H, int W, int kind) {
+  if (kind == kStem3x3) return 0;
+  const StemGeo g = geo<Stem7>(N, H, W);
+  const int T = 64 * kFwdFragBf16;
+  if (g.pw % 2 != 0 || (g.Ho * g.Wo) % T != 0) return 0;   // the channel-padded form, tiles of whole images
+  return static_cast<int64_t>(N) * (g.Ho * g.Wo / T);
+}
+
 void stem_fwd(const void* x, const uint16_t* w, bool split, int N, int H, int W, void* y, hipStream_t stream,
-              int wpitch, int kind, uint16_t* scratch) {
-  if (kind == kStem3x3) fwd_t<Stem3>(x, w, split, N, H, W, y, stream, wpitch, nullptr);
-  else fwd_t<Stem7>(x, w, split, N, H, W, y, stream, wpitch, scratch);
+              int wpitch, int kind, uint16_t* scratch, float* stats) {
+  if (kind == kStem3x3) fwd_t<Stem3>(x, w, split, N, H, W, y, stream, wpitch, nullptr, nullptr);
+  else fwd_t<Stem7>(x, w, split, N, H, W, y, stream, wpitch, scratch, split ? nullptr : stats);
 }
 
 void stem_wgrad(const void* x, const void* dy, int N, int H, int W, int groups, int slices, float* part, bool split,

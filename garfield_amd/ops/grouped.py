@@ -1408,7 +1408,17 @@ class _GroupedConv(torch.autograd.Function):
             ctx.save_for_backward(x, w)
             ho, wo = _out_hw(spec, h, wd)
             y = torch.empty((n, 64, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-            _native.native().gpu_stem_fwd(x, w, y, _stem_kind(w, spec))   # the weight is padded while staged
+            C_ = _native.native()
+            kind = _stem_kind(w, spec)
+            # the consuming BatchNorm's statistics from the kernel's epilogue (whole-image tiles): no partial pass
+            st, stats = spec.bn_next, None
+            if st is not None and kind == 0 and n % spec.groups == 0 and not C_.bn_small(n // spec.groups * ho * wo):
+                tiles = C_.stem_fwd_stat_tiles(n, h, wd, 0)
+                if tiles:
+                    stats = torch.empty(tiles * 2 * 3 * 64, dtype=torch.float32, device=x.device)
+            C_.gpu_stem_fwd(x, w, y, kind, stats)   # the weight is padded while staged
+            if stats is not None:
+                st.tile = (stats, 256, 1)
             return y
         if _channels_last_weight(w) and _iconv_ok(x, w, n * math.prod(_out_hw(spec, h, wd))):
             ctx.mode = "iconv"

@@ -223,6 +223,26 @@ def test_stem_kernels_match_fp32_conv(cuda, native, G, B, H, W, splits, raw):
         assert rel(part[:, gi].sum(0), dw.permute(0, 2, 3, 1).reshape(64, 147)) < 1e-2
 
 
+@pytest.mark.parametrize("G,B,H", [(2, 2, 32), (1, 3, 64), (2, 1, 224)])
+def test_stem_forward_tile_statistics(cuda, native, G, B, H):
+    """The bf16 7x7 stem forward's statistics epilogue (whole-image 256-pixel tiles, gemm_nt.hip's layout,
+    slot 0): count, sum and centred sum of squares of each tile's STORED bf16 outputs, per channel."""
+    x = torch.randn(G * B, 3, H, H, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, device=cuda) / 12).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ho = (H + 6 - 7) // 2 + 1
+    tiles = native.stem_fwd_stat_tiles(G * B, H, H, 0)
+    assert tiles == G * B * ho * ho // 256
+    y = torch.empty(G * B, 64, ho, ho, dtype=torch.bfloat16, device=cuda).contiguous(memory_format=torch.channels_last)
+    stats = torch.full((tiles * 2 * 3 * 64,), float("nan"), device=cuda)
+    native.gpu_stem_fwd(x, w, y, 0, stats)
+    assert rel(y.float(), F.conv2d(x.float(), w.float(), None, 2, 3)) < 1e-2
+    rows = rows2d(y).double().view(tiles, 256, 64)
+    st = stats.view(tiles, 2, 3, 64)[:, 0].double()
+    assert torch.equal(st[:, 0], torch.full_like(st[:, 0], 256.0))
+    assert rel(st[:, 1], rows.sum(1)) < 1e-5
+    assert rel(st[:, 2], ((rows - rows.mean(1, keepdim=True)) ** 2).sum(1)) < 1e-4
+
+
 @pytest.mark.parametrize("G,B,H,W,splits,raw", [(2, 3, 32, 32, 1, True), (3, 2, 32, 32, 4, False),
                                                 (2, 2, 33, 20, 2, True), (4, 1, 17, 9, 1, False)])
 def test_stem3x3_kernels_match_fp32_conv(cuda, native, G, B, H, W, splits, raw):
