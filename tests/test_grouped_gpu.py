@@ -732,17 +732,17 @@ def test_mean_f32_and_linear_bias_grad(cuda, native):
             assert rows[:off].abs().max() == 0   # nothing written before the first row's offset
 
 
-def _train(cuda, grouped: bool, steps: int, seed: int = 0):
-    """ResNet-18, 8 logical workers (one `reverse` Byzantine), Krum f=2, fresh learnable
+def _train(cuda, grouped: bool, steps: int, seed: int = 0, model: str = "resnet18", lr: float = 0.01):
+    """ResNet-18 (or ``model``), 8 logical workers (one `reverse` Byzantine), Krum f=2, fresh learnable
     synthetic batches every step (labels: argmax of a fixed random projection)."""
     torch.manual_seed(seed)
     if grouped:   # the bench's path: grouped NHWC bf16, HIP graph
-        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, byzantine={7: "reverse"}, lr=0.01, cuda_graph=True)
+        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, byzantine={7: "reverse"}, lr=lr, cuda_graph=True)
     else:         # fp32 reference: per-worker eager fp32 forward/backward, fp32 exchange
-        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, byzantine={7: "reverse"}, lr=0.01,
+        cfg = EngineConfig(gar="krum", f=2, workers_per_rank=8, byzantine={7: "reverse"}, lr=lr,
                            autocast_dtype=None, exchange_dtype=torch.float32, worker_batching=False,
                            lp_weights=False)
-    eng = RobustDataParallel(build_model("resnet18"), F.cross_entropy, DistContext(device=cuda), cfg)
+    eng = RobustDataParallel(build_model(model), F.cross_entropy, DistContext(device=cuda), cfg)
     assert (eng._gexec is not None) == grouped
     pool = [synthetic_batches(8, 32, (3, 32, 32), 10, cuda, seed=1000 + i) for i in range(8)]
     losses = []
@@ -769,6 +769,24 @@ def test_headline_path_trains_like_fp32(cuda):
     print(f"last-10 mean loss: grouped bf16 {lb:.4f}, fp32 {lf:.4f}; first {bf[0]:.4f} / {fp[0]:.4f}")
     assert lb < 0.6 * math.log(10), (lb, bf[::10])
     assert abs(lb - lf) <= 0.05 + 0.05 * lf, (lb, lf)
+
+
+def test_headline_model_trains_like_fp32(cuda):
+    """The headline model itself (ResNet-50, CIFAR shape, 8 workers, Krum f=2, one reverse attacker) on the
+    grouped bf16 HIP-graph path against the per-worker fp32 engine on the same data, 150 steps at lr 0.002:
+    both learn (last-10 mean below 0.8 ln 10) and agree to 0.1 + 0.05 L_fp32. Measured
+    (scripts/diag_converge.py 150 resnet50 0.002, profiles/r6/converge/): 1.715 vs 1.674, and 1.650 vs 1.636
+    in the test's own run (pytest_converge.log); at lr 0.005 / 0.01 both paths are unstable alike on this
+    task (converge_r50_lr005_01.jsonl)."""
+    import math
+
+    steps = 150
+    bf = _train(cuda, True, steps, model="resnet50", lr=0.002)
+    fp = _train(cuda, False, steps, model="resnet50", lr=0.002)
+    lb, lf = sum(bf[-10:]) / 10, sum(fp[-10:]) / 10
+    print(f"last-10 mean loss: grouped bf16 {lb:.4f}, fp32 {lf:.4f}")
+    assert lb < 0.8 * math.log(10), (lb, bf[::10])
+    assert abs(lb - lf) <= 0.1 + 0.05 * lf, (lb, lf)
 
 
 @pytest.mark.gpu
